@@ -1,0 +1,143 @@
+/*
+ * qvq.h -- C ABI of the MI355X LBG vector-quantization engine (libqvq.so).
+ *
+ * This is the drop-in boundary for coodie/quant's hot path.  The reference has no FFI;
+ * its plugin interface is C++:
+ *
+ *   AbstractQuantizer::quantize(const std::vector<Vector>& trainingSet, size_t n, VectorType eps)
+ *       -> tuple<codebook, assignedCodeVector, distortion>        include/Quantizer.hpp:10-16
+ *   getQuantizer(Quantizers)                                       include/Quantizer.hpp:20,
+ *                                                                  src/Quantizer.cpp:146-155
+ *   CompressedImage::compress(image, quantizer, colorSpace, w, h, eps, N)
+ *       (times getBlocksAsVectorsFromImage + quantize)             src/Compressor.cpp:107-123
+ *
+ * The C++ layer in include/quant_amd/ (libquant_amd.so) re-exposes exactly that
+ * interface on top of these entry points; INTEGRATION.md shows the binding.  Everything
+ * here is plain C: pointers, sizes, status codes; no exceptions cross this boundary.
+ *
+ * Results: code-vector indices are bit-identical to the reference's kd-tree assignment
+ * (src/Quantizer.cpp:24-32), centroids equal the exact sum of the members rounded once
+ * and multiplied by fl(1/count) (the reference's Kahan sum agrees to <= 1 ulp,
+ * src/Quantizer.cpp:59-87).
+ */
+#ifndef QVQ_H
+#define QVQ_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define QVQ_API __attribute__((visibility("default")))
+
+typedef struct qvq_ctx qvq_ctx;
+
+typedef enum {
+    QVQ_OK = 0,
+    QVQ_EINVAL = 1,       /* bad argument (sizes, null pointers, bits out of range) */
+    QVQ_ENOMEM = 2,       /* device or host allocation failed */
+    QVQ_EDEVICE = 3,      /* HIP runtime error, or no HIP device */
+    QVQ_ECOMM = 4,        /* RCCL error */
+    QVQ_EUNSUPPORTED = 5, /* training set the engine cannot sum exactly (see qvq_set_vectors) */
+    QVQ_ESTATE = 6        /* call order violated (e.g. qvq_lbg before a training set) */
+} qvq_status;
+
+/* Colour spaces, numbered as the reference's enum class ColorSpaces
+ * (include/ColorSpace.hpp:6).  Only NORMAL and SCALED map bytes to values the engine
+ * can sum exactly; CIE1931 is rejected with QVQ_EUNSUPPORTED. */
+enum { QVQ_CS_NORMAL = 0, QVQ_CS_SCALED = 1, QVQ_CS_CIE1931 = 2 };
+
+/* Per-level / per-call timings filled by qvq_get_timings (device ms from HIP events). */
+typedef struct {
+    int levels;                 /* split levels run by the last qvq_lbg */
+    double total_ms;            /* whole qvq_lbg, host wall */
+    double assign_ms[32];       /* device time of the assignment kernel per level */
+    double update_ms[32];       /* device time of the centroid-sum kernel per level */
+    double other_ms[32];        /* recheck + finalize + host tie resolution per level */
+    uint64_t flagged[32];       /* rows re-checked in fp64 per level */
+    uint64_t host_ties[32];     /* rows resolved by the host kd-tree per level */
+} qvq_timings;
+
+/* Context: one per GPU per host thread.  Owns device memory and one HIP stream. */
+QVQ_API qvq_status qvq_create(int hip_device, qvq_ctx **out);
+QVQ_API void qvq_destroy(qvq_ctx *ctx);
+QVQ_API const char *qvq_last_error(const qvq_ctx *ctx);
+QVQ_API const char *qvq_version(void);
+
+/*
+ * Training set, way 1: raw P6 rasters (host pointer, n_images x xSize x ySize x 3 bytes,
+ * image-major), tiled on the device exactly as getBlocksAsVectorsFromImage
+ * (src/Compressor.cpp:31-62): the raster is read as xSize rows of ySize pixels, columns
+ * past ySize wrap into the next row, components past the end of the buffer are 0.
+ * Blocks of image i follow all blocks of image i-1.
+ */
+QVQ_API qvq_status qvq_set_images(qvq_ctx *ctx, const uint8_t *rgb, uint32_t n_images, uint32_t xSize,
+                                  uint32_t ySize, uint32_t bw, uint32_t bh, int colorspace);
+/* Same, but the rasters are already in device memory (e.g. a torch tensor). */
+QVQ_API qvq_status qvq_set_images_device(qvq_ctx *ctx, const void *d_rgb, uint32_t n_images, uint32_t xSize,
+                                         uint32_t ySize, uint32_t bw, uint32_t bh, int colorspace);
+/* Same, with the rasters generated on the device by the synthetic generator of
+ * SURVEY.md 8(d) (image i uses seed0 + i); for benchmarks and scale tests. */
+QVQ_API qvq_status qvq_set_synthetic(qvq_ctx *ctx, uint32_t S, uint64_t seed0, uint32_t n_images, uint32_t bw,
+                                     uint32_t bh, int colorspace);
+/*
+ * Training set, way 2: flat fp64 N x dim (the AbstractQuantizer path).  Every value must
+ * be one the NORMAL or SCALED colour space produces from a byte (or 0.0); other data
+ * returns QVQ_EUNSUPPORTED.
+ */
+QVQ_API qvq_status qvq_set_vectors(qvq_ctx *ctx, const double *X, uint64_t n, uint32_t dim);
+
+QVQ_API uint64_t qvq_num_vectors(const qvq_ctx *ctx);
+QVQ_API uint32_t qvq_dim(const qvq_ctx *ctx);
+
+/*
+ * Full split-LBG (LBGQuantizer::quantize, src/Quantizer.cpp:122-143) over the training
+ * set: n = bits levels, K = 2^bits code vectors.  eps is accepted for signature parity;
+ * it cannot change the outputs (one Lloyd step per level).
+ * Outputs (caller-owned host memory, any may be NULL):
+ *   codebook   : K x dim fp64
+ *   assign     : n u32 (this rank's rows)
+ *   distortion : mean squared error of the final codebook, as updateDistortion
+ * With a communicator (qvq_comm_init) every rank runs this on its own rows and all ranks
+ * get the same codebook.
+ */
+QVQ_API qvq_status qvq_lbg(qvq_ctx *ctx, uint32_t bits, double eps, double *codebook, uint32_t *assign,
+                           double *distortion);
+/* Device pointer to the last qvq_lbg's assignment (u32, qvq_num_vectors entries). */
+QVQ_API const uint32_t *qvq_assign_device(const qvq_ctx *ctx);
+
+/* Single steps over the current training set, for tests and benchmarks.
+ * qvq_assign: nearest code vector of every row for codebook C (K x dim fp64, host),
+ *   with the same fp32 search + fp64 recheck + host kd-tree tie resolution as qvq_lbg.
+ * qvq_update: centroids of the rows under assignment A (host, n u32) into C_out
+ *   (K x dim fp64) and counts (K u64), the engine's exact-sum rule. */
+QVQ_API qvq_status qvq_assign(qvq_ctx *ctx, const double *C, uint32_t K, uint32_t *assign);
+QVQ_API qvq_status qvq_update(qvq_ctx *ctx, const uint32_t *assign, uint32_t K, double *C_out, uint64_t *counts);
+
+/* Multi-GPU: join an RCCL communicator (unique_id from qvq_comm_unique_id on rank 0,
+ * shipped to the other ranks by the caller).  Each level then all-reduces the
+ * per-code-vector sums and counts over xGMI. */
+QVQ_API qvq_status qvq_comm_unique_id(uint8_t id[128]);
+QVQ_API qvq_status qvq_comm_init(qvq_ctx *ctx, int nranks, int rank, const uint8_t id[128]);
+
+QVQ_API qvq_status qvq_get_timings(const qvq_ctx *ctx, qvq_timings *out);
+
+/* Host-only helpers (no GPU needed), exported for tests of the host logic. */
+/* The reference kd-tree's answer for nq queries (nanoflann semantics, see kdtree.hpp). */
+QVQ_API qvq_status qvq_host_kdtree_nn(const double *C, uint32_t K, uint32_t dim, const double *Q, uint64_t nq,
+                                      uint32_t *out);
+/* Exact centroid finalisation from reduced sums, as the device does it:
+ * C[k][d] = round(R*hi + lo - bias*cnt) * 2^-scale * fl(1/cnt).  For tests. */
+QVQ_API qvq_status qvq_host_finalize(const uint64_t *hi, const uint64_t *lo, const uint64_t *cnt, uint32_t K,
+                                     uint32_t dim, int colorspace, double *C_out);
+/* Per-block exact contributions of one row of codes, as the device sums them: hi/lo
+ * (dim entries each) -- for the host-side sharding tests. */
+QVQ_API qvq_status qvq_host_row_terms(const uint8_t *codes, uint32_t dim, int colorspace, uint64_t *hi,
+                                      uint64_t *lo);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* QVQ_H */

@@ -1,0 +1,208 @@
+// See kdtree.hpp.  Build: nanoflann.hpp:863-871 (buildIndex), :1014-1036 (bounding box),
+// :1046-1094 (divideTree), :1108-1147 (middleSplit_), :1159-1186 (planeSplit).
+// Search: :906-920 (findNeighbors), :1188-1205 (initial distances), :1212-1270
+// (searchLevel) with KNNResultSet capacity 1 (:77-138): strict '<' everywhere, so among
+// equal distances the first point visited wins.
+#include "kdtree.hpp"
+
+#include <algorithm>
+#include <limits>
+
+namespace qvq {
+
+double ref_l2(const double *a, const double *b, int dim) {
+    double r = 0;
+    int d = 0;
+    for (; d + 3 < dim; d += 4) {
+        const double e0 = a[d] - b[d], e1 = a[d + 1] - b[d + 1];
+        const double e2 = a[d + 2] - b[d + 2], e3 = a[d + 3] - b[d + 3];
+        r += (e1 * e1 + e2 * e2) + (e0 * e0 + e3 * e3);
+    }
+    for (; d < dim; d++) {
+        const double e = a[d] - b[d];
+        r += e * e;
+    }
+    return r;
+}
+
+RefKDTree::RefKDTree(const double *pts, size_t K, int dim) : pts_(pts), K_(K), dim_(dim) {
+    vind_.resize(K);
+    for (size_t i = 0; i < K; i++) vind_[i] = i;
+    root_bbox_.resize(dim);
+    for (int d = 0; d < dim; d++) root_bbox_[d].low = root_bbox_[d].high = pt(0, d);
+    for (size_t k = 1; k < K; k++)
+        for (int d = 0; d < dim; d++) {
+            const double v = pt(k, d);
+            if (v < root_bbox_[d].low) root_bbox_[d].low = v;
+            if (v > root_bbox_[d].high) root_bbox_[d].high = v;
+        }
+    nodes_.reserve(2 * (K / 5 + 1));
+    divide(0, K, root_bbox_);
+}
+
+void RefKDTree::min_max(const size_t *ind, size_t count, int e, double &mn, double &mx) const {
+    mn = mx = pt(ind[0], e);
+    for (size_t i = 1; i < count; i++) {
+        const double v = pt(ind[i], e);
+        if (v < mn) mn = v;
+        if (v > mx) mx = v;
+    }
+}
+
+void RefKDTree::plane_split(size_t *ind, size_t count, int cutfeat, double cutval, size_t &lim1,
+                            size_t &lim2) {
+    // Two Hoare-style passes: [< cutval | == cutval | > cutval].  'right' is unsigned, so
+    // the reference stops when it reaches 0 as well.
+    size_t left = 0, right = count - 1;
+    for (;;) {
+        while (left <= right && pt(ind[left], cutfeat) < cutval) ++left;
+        while (right && left <= right && pt(ind[right], cutfeat) >= cutval) --right;
+        if (left > right || !right) break;
+        std::swap(ind[left], ind[right]);
+        ++left;
+        --right;
+    }
+    lim1 = left;
+    right = count - 1;
+    for (;;) {
+        while (left <= right && pt(ind[left], cutfeat) <= cutval) ++left;
+        while (right && left <= right && pt(ind[right], cutfeat) > cutval) --right;
+        if (left > right || !right) break;
+        std::swap(ind[left], ind[right]);
+        ++left;
+        --right;
+    }
+    lim2 = left;
+}
+
+void RefKDTree::middle_split(size_t *ind, size_t count, size_t &index, int &cutfeat, double &cutval,
+                             const std::vector<Box> &bbox) {
+    const double EPS = 0.00001;
+    double max_span = bbox[0].high - bbox[0].low;
+    for (int i = 1; i < dim_; i++) max_span = std::max(max_span, bbox[i].high - bbox[i].low);
+    double max_spread = -1;
+    cutfeat = 0;
+    for (int i = 0; i < dim_; i++) {
+        const double span = bbox[i].high - bbox[i].low;
+        if (span > (1 - EPS) * max_span) {
+            double mn, mx;
+            min_max(ind, count, i, mn, mx);
+            if (mx - mn > max_spread) {
+                cutfeat = i;
+                max_spread = mx - mn;
+            }
+        }
+    }
+    const double split_val = (bbox[cutfeat].low + bbox[cutfeat].high) / 2;
+    double mn, mx;
+    min_max(ind, count, cutfeat, mn, mx);
+    cutval = split_val < mn ? mn : (split_val > mx ? mx : split_val);
+    size_t lim1, lim2;
+    plane_split(ind, count, cutfeat, cutval, lim1, lim2);
+    if (lim1 > count / 2) index = lim1;
+    else if (lim2 < count / 2) index = lim2;
+    else index = count / 2;
+}
+
+// bbox is in/out: the caller's cell box on entry, the node's actual point box on exit.
+int RefKDTree::divide(size_t left, size_t right, std::vector<Box> &bbox) {
+    const int me = (int)nodes_.size();
+    nodes_.push_back(Node());
+    if (right - left <= 10) {   // leaf_max_size (KDTreeVectorOfVectorsAdaptor.hpp:59)
+        Node &n = nodes_[me];
+        n.leaf = true;
+        n.left = left;
+        n.right = right;
+        n.child1 = n.child2 = -1;
+        for (int d = 0; d < dim_; d++) bbox[d].low = bbox[d].high = pt(vind_[left], d);
+        for (size_t k = left + 1; k < right; k++)
+            for (int d = 0; d < dim_; d++) {
+                const double v = pt(vind_[k], d);
+                if (bbox[d].low > v) bbox[d].low = v;
+                if (bbox[d].high < v) bbox[d].high = v;
+            }
+        return me;
+    }
+    size_t idx;
+    int cutfeat;
+    double cutval;
+    middle_split(vind_.data() + left, right - left, idx, cutfeat, cutval, bbox);
+    std::vector<Box> lb(bbox), rb;
+    lb[cutfeat].high = cutval;
+    const int c1 = divide(left, left + idx, lb);
+    rb = bbox;
+    rb[cutfeat].low = cutval;
+    const int c2 = divide(left + idx, right, rb);
+    Node &n = nodes_[me];
+    n.leaf = false;
+    n.divfeat = cutfeat;
+    n.child1 = c1;
+    n.child2 = c2;
+    n.divlow = lb[cutfeat].high;
+    n.divhigh = rb[cutfeat].low;
+    for (int d = 0; d < dim_; d++) {
+        bbox[d].low = std::min(lb[d].low, rb[d].low);
+        bbox[d].high = std::max(lb[d].high, rb[d].high);
+    }
+    return me;
+}
+
+void RefKDTree::search(const double *q, int node, double mindistsq, std::vector<double> &dists, double &best,
+                       size_t &best_idx, bool &have) const {
+    const Node &n = nodes_[node];
+    if (n.leaf) {
+        const double worst = best;   // captured once per leaf, as the reference does
+        for (size_t i = n.left; i < n.right; i++) {
+            const size_t index = vind_[i];
+            const double dist = ref_l2(q, pts_ + index * (size_t)dim_, dim_);
+            if (dist < worst && (!have || best > dist)) {
+                best = dist;
+                best_idx = index;
+                have = true;
+            }
+        }
+        return;
+    }
+    const int f = n.divfeat;
+    const double val = q[f];
+    const double diff1 = val - n.divlow, diff2 = val - n.divhigh;
+    int first, other;
+    double cut_dist;
+    if ((diff1 + diff2) < 0) {
+        first = n.child1;
+        other = n.child2;
+        cut_dist = (val - n.divhigh) * (val - n.divhigh);
+    } else {
+        first = n.child2;
+        other = n.child1;
+        cut_dist = (val - n.divlow) * (val - n.divlow);
+    }
+    search(q, first, mindistsq, dists, best, best_idx, have);
+    const double dst = dists[f];
+    mindistsq = (mindistsq - dst) + cut_dist;   // the reference build's association
+    dists[f] = cut_dist;
+    if (mindistsq * 1.0f <= best) search(q, other, mindistsq, dists, best, best_idx, have);
+    dists[f] = dst;
+}
+
+uint32_t RefKDTree::nearest(const double *q) const {
+    std::vector<double> dists(dim_, 0.0);
+    double distsq = 0;
+    for (int d = 0; d < dim_; d++) {
+        if (q[d] < root_bbox_[d].low) {
+            dists[d] = (q[d] - root_bbox_[d].low) * (q[d] - root_bbox_[d].low);
+            distsq += dists[d];
+        }
+        if (q[d] > root_bbox_[d].high) {
+            dists[d] = (q[d] - root_bbox_[d].high) * (q[d] - root_bbox_[d].high);
+            distsq += dists[d];
+        }
+    }
+    double best = std::numeric_limits<double>::max();
+    size_t best_idx = 0;
+    bool have = false;
+    search(q, 0, distsq, dists, best, best_idx, have);
+    return (uint32_t)best_idx;
+}
+
+}  // namespace qvq
