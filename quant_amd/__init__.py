@@ -1,0 +1,242 @@
+"""quant_amd -- MI355X LBG vector-quantization engine (Python mirror of the C ABI).
+
+The product is libqvq.so (quant_amd/lib), a C-ABI library of hand-written HIP kernels
+for gfx950 (include/qvq.h).  This module binds it with ctypes and mirrors the
+reference's quantizer plugin interface (include/Quantizer.hpp:8-20):
+
+    getQuantizer(Quantizers.LBG).quantize(trainingSet, n, eps) -> (codebook, assigned, distortion)
+
+There is no CPU fallback: every compute call goes to the GPU through libqvq.so and raises
+QVQError when the library or the device is missing.
+"""
+import ctypes
+import enum
+import os
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "lib", "libqvq.so")
+
+NORMAL, SCALED, CIE1931 = 0, 1, 2   # enum class ColorSpaces (include/ColorSpace.hpp:6)
+
+
+class QVQError(RuntimeError):
+    def __init__(self, status, msg):
+        super().__init__("qvq status %d: %s" % (status, msg))
+        self.status = status
+
+
+class _Timings(ctypes.Structure):
+    _fields_ = [("levels", ctypes.c_int), ("total_ms", ctypes.c_double),
+                ("assign_ms", ctypes.c_double * 32), ("update_ms", ctypes.c_double * 32),
+                ("other_ms", ctypes.c_double * 32), ("flagged", ctypes.c_uint64 * 32),
+                ("host_ties", ctypes.c_uint64 * 32)]
+
+
+_lib = None
+EXPORTED = ["qvq_create", "qvq_destroy", "qvq_last_error", "qvq_version", "qvq_set_images",
+            "qvq_set_images_device", "qvq_set_synthetic", "qvq_set_vectors", "qvq_num_vectors",
+            "qvq_dim", "qvq_lbg", "qvq_assign_device", "qvq_assign", "qvq_update",
+            "qvq_comm_unique_id", "qvq_comm_init", "qvq_get_timings", "qvq_host_kdtree_nn",
+            "qvq_host_finalize", "qvq_host_row_terms"]
+
+
+def lib():
+    """Load libqvq.so (built in-tree by __graft_entry__.build() / make -C quant_amd/csrc)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise QVQError(-1, "libqvq.so not built (%s); run __graft_entry__.build()" % LIB_PATH)
+        L = ctypes.CDLL(LIB_PATH)
+        P, u32, u64, i = ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_int
+        sig = {
+            "qvq_create": ([i, ctypes.POINTER(P)], i),
+            "qvq_destroy": ([P], None),
+            "qvq_last_error": ([P], ctypes.c_char_p),
+            "qvq_version": ([], ctypes.c_char_p),
+            "qvq_set_images": ([P, P, u32, u32, u32, u32, u32, i], i),
+            "qvq_set_images_device": ([P, P, u32, u32, u32, u32, u32, i], i),
+            "qvq_set_synthetic": ([P, u32, u64, u32, u32, u32, i], i),
+            "qvq_set_vectors": ([P, P, u64, u32], i),
+            "qvq_num_vectors": ([P], u64),
+            "qvq_dim": ([P], u32),
+            "qvq_lbg": ([P, u32, ctypes.c_double, P, P, P], i),
+            "qvq_assign_device": ([P], P),
+            "qvq_assign": ([P, P, u32, P], i),
+            "qvq_update": ([P, P, u32, P, P], i),
+            "qvq_comm_unique_id": ([P], i),
+            "qvq_comm_init": ([P, i, i, P], i),
+            "qvq_get_timings": ([P, ctypes.POINTER(_Timings)], i),
+            "qvq_host_kdtree_nn": ([P, u32, u32, P, u64, P], i),
+            "qvq_host_finalize": ([P, P, P, u32, u32, i, P], i),
+            "qvq_host_row_terms": ([P, u32, i, P, P], i),
+        }
+        for name, (args, res) in sig.items():
+            fn = getattr(L, name)
+            fn.argtypes = args
+            fn.restype = res
+        _lib = L
+    return _lib
+
+
+def _p(a):
+    return a.ctypes.data_as(ctypes.c_void_p)
+
+
+def _check(st, ctx=None):
+    if st != 0:
+        msg = lib().qvq_last_error(ctx)
+        raise QVQError(st, msg.decode() if msg else "")
+
+
+class Engine:
+    """One qvq context: one GPU, one HIP stream, one resident training set."""
+
+    def __init__(self, device=0):
+        h = ctypes.c_void_p()
+        _check(lib().qvq_create(device, ctypes.byref(h)))
+        self._h = h
+
+    def close(self):
+        if getattr(self, "_h", None):
+            lib().qvq_destroy(self._h)
+            self._h = None
+
+    __del__ = close
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    # -- training sets -------------------------------------------------------------------
+    def set_images(self, rgb, n_images, xSize, ySize, bw, bh, colorspace=SCALED):
+        rgb = np.ascontiguousarray(rgb, np.uint8)
+        assert rgb.size == n_images * xSize * ySize * 3
+        _check(lib().qvq_set_images(self._h, _p(rgb), n_images, xSize, ySize, bw, bh, colorspace), self._h)
+
+    def set_images_device(self, ptr, n_images, xSize, ySize, bw, bh, colorspace=SCALED):
+        _check(lib().qvq_set_images_device(self._h, ctypes.c_void_p(ptr), n_images, xSize, ySize, bw, bh,
+                                           colorspace), self._h)
+
+    def set_synthetic(self, S, seed0=0x5EED, n_images=1, bw=2, bh=2, colorspace=SCALED):
+        _check(lib().qvq_set_synthetic(self._h, S, seed0, n_images, bw, bh, colorspace), self._h)
+
+    def set_vectors(self, X):
+        X = np.ascontiguousarray(X, np.float64)
+        _check(lib().qvq_set_vectors(self._h, _p(X), X.shape[0], X.shape[1]), self._h)
+
+    @property
+    def n(self):
+        return int(lib().qvq_num_vectors(self._h))
+
+    @property
+    def dim(self):
+        return int(lib().qvq_dim(self._h))
+
+    # -- hot path ------------------------------------------------------------------------
+    def lbg(self, bits, eps=1e-6, want_assign=True):
+        K = 1 << bits
+        C = np.empty((K, self.dim), np.float64)
+        A = np.empty(self.n, np.uint32) if want_assign else None
+        d = np.zeros(1, np.float64)
+        _check(lib().qvq_lbg(self._h, bits, eps, _p(C), _p(A) if want_assign else None, _p(d)), self._h)
+        return C, A, float(d[0])
+
+    def assign(self, C):
+        C = np.ascontiguousarray(C, np.float64)
+        A = np.empty(self.n, np.uint32)
+        _check(lib().qvq_assign(self._h, _p(C), C.shape[0], _p(A)), self._h)
+        return A
+
+    def update(self, A, K):
+        A = np.ascontiguousarray(A, np.uint32)
+        C = np.empty((K, self.dim), np.float64)
+        cnt = np.empty(K, np.uint64)
+        _check(lib().qvq_update(self._h, _p(A), K, _p(C), _p(cnt)), self._h)
+        return C, cnt
+
+    def assign_device_ptr(self):
+        return lib().qvq_assign_device(self._h)
+
+    def timings(self):
+        t = _Timings()
+        _check(lib().qvq_get_timings(self._h, ctypes.byref(t)), self._h)
+        L = t.levels
+        return {"levels": L, "total_ms": t.total_ms,
+                "assign_ms": list(t.assign_ms[:max(L, 1)]), "update_ms": list(t.update_ms[:max(L, 1)]),
+                "flagged": list(t.flagged[:max(L, 1)]), "host_ties": list(t.host_ties[:max(L, 1)])}
+
+    # -- multi-GPU -----------------------------------------------------------------------
+    @staticmethod
+    def comm_unique_id():
+        buf = (ctypes.c_uint8 * 128)()
+        _check(lib().qvq_comm_unique_id(buf))
+        return bytes(buf)
+
+    def comm_init(self, nranks, rank, uid):
+        buf = (ctypes.c_uint8 * 128).from_buffer_copy(uid)
+        _check(lib().qvq_comm_init(self._h, nranks, rank, buf), self._h)
+
+
+# -- host-only helpers (no GPU) ------------------------------------------------------------
+def host_kdtree_nn(C, Q):
+    C = np.ascontiguousarray(C, np.float64)
+    Q = np.ascontiguousarray(Q, np.float64)
+    out = np.empty(Q.shape[0], np.uint32)
+    _check(lib().qvq_host_kdtree_nn(_p(C), C.shape[0], C.shape[1], _p(Q), Q.shape[0], _p(out)))
+    return out
+
+
+def host_finalize(hi, lo, cnt, colorspace=SCALED):
+    hi = np.ascontiguousarray(hi, np.uint64)
+    lo = np.ascontiguousarray(lo, np.uint64)
+    cnt = np.ascontiguousarray(cnt, np.uint64)
+    K, D = hi.shape
+    C = np.empty((K, D), np.float64)
+    _check(lib().qvq_host_finalize(_p(hi), _p(lo), _p(cnt), K, D, colorspace, _p(C)))
+    return C
+
+
+def host_row_terms(codes, colorspace=SCALED):
+    """(hi, lo) exact-sum terms of each byte code, shape like codes (uint64)."""
+    codes = np.ascontiguousarray(codes, np.uint8)
+    flat = codes.reshape(-1)
+    hi = np.empty(flat.size, np.uint64)
+    lo = np.empty(flat.size, np.uint64)
+    _check(lib().qvq_host_row_terms(_p(flat), flat.size, colorspace, _p(hi), _p(lo)))
+    return hi.reshape(codes.shape), lo.reshape(codes.shape)
+
+
+# -- the reference's plugin interface (include/Quantizer.hpp:8-20) ---------------------------
+class Quantizers(enum.IntEnum):
+    LBG = 0
+    MEDIAN_CUT = 1
+    LBG_MEDIAN_CUT = 2
+    ABC = 3
+
+
+class AbstractQuantizer:
+    def quantize(self, trainingSet, n, eps):
+        raise NotImplementedError
+
+
+class LBGQuantizer(AbstractQuantizer):
+    """LBGQuantizer (src/Quantizer.cpp:119-144) on the MI355X engine."""
+
+    def __init__(self, device=0):
+        self._device = device
+        self._engine = None
+
+    def quantize(self, trainingSet, n, eps):
+        if self._engine is None:
+            self._engine = Engine(self._device)
+        self._engine.set_vectors(np.asarray(trainingSet, np.float64))
+        return self._engine.lbg(int(n), eps)
+
+
+def getQuantizer(q):
+    """src/Quantizer.cpp:146-155: only LBG exists; other enumerators give None."""
+    return LBGQuantizer() if Quantizers(q) == Quantizers.LBG else None

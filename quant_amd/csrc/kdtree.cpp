@@ -25,7 +25,7 @@ double ref_l2(const double *a, const double *b, int dim) {
     return r;
 }
 
-RefKDTree::RefKDTree(const double *pts, size_t K, int dim) : pts_(pts), K_(K), dim_(dim) {
+RefKDTree::RefKDTree(const double *pts, size_t K, int dim) : pts_(pts), dim_(dim) {
     vind_.resize(K);
     for (size_t i = 0; i < K; i++) vind_[i] = i;
     root_bbox_.resize(dim);

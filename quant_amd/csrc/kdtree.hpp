@@ -45,7 +45,6 @@ private:
                 size_t &best_idx, bool &have) const;
 
     const double *pts_;
-    size_t K_;
     int dim_;
     std::vector<size_t> vind_;
     std::vector<Node> nodes_;

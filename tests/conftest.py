@@ -1,0 +1,30 @@
+import os
+import sys
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+GOLDEN = os.path.join(ROOT, "tests", "golden")
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs an MI355X (runs through libqvq.so)")
+    config.addinivalue_line("markers", "slow: long CPU oracle runs")
+
+
+def load_png_rgb(name):
+    """Reference image fixture -> (raster bytes, xSize, ySize) as RGBImage reads a P6 file."""
+    from PIL import Image
+    im = Image.open(os.path.join(GOLDEN, name)).convert("RGB")
+    w, h = im.size
+    return np.frombuffer(im.tobytes(), np.uint8).copy(), w, h
+
+
+@pytest.fixture(scope="session")
+def engine():
+    import quant_amd
+    eng = quant_amd.Engine(0)
+    yield eng
+    eng.close()

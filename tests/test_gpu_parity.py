@@ -1,0 +1,121 @@
+"""GPU parity: the HIP engine against the oracle (lbg_oracle.c) on the same inputs.
+
+Bar: code-vector indices bit-exact; codebooks bit-exact against the oracle's exact-sum
+mode (the engine's documented centroid rule) and within 1e-12 relative of the oracle's
+Kahan mode (the reference's own rule; north-star tolerance is 1e-5)."""
+import numpy as np
+import pytest
+
+from conftest import load_png_rgb
+from oracle import oracle
+
+pytestmark = pytest.mark.gpu
+
+KAHAN_RTOL = 1e-12
+
+
+def _check_against_oracle(engine, rgb, xs, ys, bw, bh, bits, cs=oracle.SCALED):
+    import quant_amd
+    X, _ = oracle.tile(rgb, xs, ys, bw, bh, cs=cs, pad_code=128 if cs == oracle.SCALED else 0)
+    C_k, A_k, d_k = oracle.lbg(X, bits, sum_mode=0)
+    C_x, A_x, d_x = oracle.lbg(X, bits, sum_mode=1)
+    engine.set_images(rgb, 1, xs, ys, bw, bh, cs)
+    C, A, d = engine.lbg(bits)
+    assert A.shape == A_k.shape
+    np.testing.assert_array_equal(A, A_k)          # reference rule
+    np.testing.assert_array_equal(A, A_x)
+    np.testing.assert_array_equal(C, C_x)          # engine rule, bit-exact
+    scale = np.maximum(np.abs(C_k), 1e-300)
+    assert np.max(np.abs(C - C_k) / scale) <= KAHAN_RTOL
+    assert abs(d - d_k) <= 1e-9 * abs(d_k)
+    return C, A, d
+
+
+def test_beans_n8(engine):
+    rgb, xs, ys = load_png_rgb("beans.png")
+    _check_against_oracle(engine, rgb, xs, ys, 2, 2, 8)
+
+
+def test_kodim01_n10(engine):
+    rgb, xs, ys = load_png_rgb("kodim01.png")
+    _check_against_oracle(engine, rgb, xs, ys, 2, 2, 10)
+
+
+def test_t_wrap_pad_n4(engine):
+    # 510 x 383: odd height exercises the column wrap and the end-of-buffer zero pad.
+    rgb, xs, ys = load_png_rgb("t.png")
+    _check_against_oracle(engine, rgb, xs, ys, 2, 2, 4)
+
+
+def test_s512_n10(engine):
+    _check_against_oracle(engine, oracle.gen_image(512), 512, 512, 2, 2, 10)
+
+
+@pytest.mark.parametrize("bw,bh,bits", [(1, 1, 5), (1, 3, 6), (2, 4, 6), (4, 4, 8), (3, 3, 7)])
+def test_block_shapes(engine, bw, bh, bits):
+    _check_against_oracle(engine, oracle.gen_image(96), 96, 96, bw, bh, bits)
+
+
+def test_normal_colorspace(engine):
+    _check_against_oracle(engine, oracle.gen_image(64), 64, 64, 2, 2, 6, cs=oracle.NORMAL)
+
+
+def test_synthetic_generator_matches(engine):
+    rgb = oracle.gen_image(256, 0x5EED + 3)
+    engine.set_images(rgb, 1, 256, 256, 2, 2)
+    C1, A1, d1 = engine.lbg(7)
+    engine.set_synthetic(256, 0x5EED + 3, 1, 2, 2)
+    C2, A2, d2 = engine.lbg(7)
+    np.testing.assert_array_equal(A1, A2)
+    np.testing.assert_array_equal(C1, C2)
+
+
+def test_multi_image_batch(engine):
+    # image-major concatenation (SURVEY.md 8(d) C5 definition) on a small batch
+    imgs = [oracle.gen_image(64, 0x5EED + b) for b in range(3)]
+    X = np.concatenate([oracle.tile(im, 64, 64, 2, 2)[0] for im in imgs])
+    C_x, A_x, _ = oracle.lbg(X, 6, sum_mode=1)
+    engine.set_synthetic(64, 0x5EED, 3, 2, 2)
+    C, A, _ = engine.lbg(6)
+    np.testing.assert_array_equal(A, A_x)
+    np.testing.assert_array_equal(C, C_x)
+
+
+def test_set_vectors_path(engine):
+    X, _ = oracle.tile(oracle.gen_image(64), 64, 64, 2, 2)
+    C_x, A_x, _ = oracle.lbg(X, 5, sum_mode=1)
+    engine.set_vectors(X)
+    C, A, _ = engine.lbg(5)
+    np.testing.assert_array_equal(A, A_x)
+    np.testing.assert_array_equal(C, C_x)
+
+
+def test_set_vectors_rejects_general_data(engine):
+    import quant_amd
+    with pytest.raises(quant_amd.QVQError):
+        engine.set_vectors(np.random.rand(100, 12))
+
+
+def test_assign_ties_and_duplicates(engine):
+    """Duplicated code vectors and split pairs (the structural tie sources) are resolved
+    exactly as the reference kd-tree resolves them."""
+    rng = np.random.default_rng(7)
+    X, _ = oracle.tile(oracle.gen_image(128), 128, 128, 2, 2)
+    engine.set_vectors(X)
+    base = X[rng.choice(len(X), 40, replace=False)]
+    C = np.concatenate([base * (1 + 0.2), base * (1 - 0.2), np.zeros((8, 12)), base[:4], base[:4]])
+    A = engine.assign(C)
+    np.testing.assert_array_equal(A, oracle.kdtree_nn(C, X))
+    t = engine.timings()
+    assert t["host_ties"][0] > 0      # rows equal to base[:4] tie between the two copies
+
+
+def test_update_exact(engine):
+    X, codes = oracle.tile(oracle.gen_image(128), 128, 128, 2, 2)
+    engine.set_vectors(X)
+    rng = np.random.default_rng(3)
+    K = 300
+    A = rng.integers(0, K - 20, len(X)).astype(np.uint32)   # some empty cells
+    C, cnt = engine.update(A, K)
+    np.testing.assert_array_equal(C, oracle.centroids(X, A, K, sum_mode=1))
+    np.testing.assert_array_equal(cnt, np.bincount(A, minlength=K))
