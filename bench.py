@@ -1,0 +1,174 @@
+"""bench.py -- LBG vector-quantization hot path on MI355X (BASELINE.json metric).
+
+One step = one full LBGQuantizer::quantize (src/Quantizer.cpp:122-143): mean init plus
+`bits` split levels, each one assign + one centroid update (+ the RCCL all-reduce of the
+per-code-vector sums when N > 1), over a training set already resident in HBM.
+
+Workload per rank: one 4096x4096 synthetic RGB image (seed 0x5EED+rank),
+2x2 blocks (D = 12), 1024 code vectors -- BASELINE.json configs[2]/C3, the configuration
+the reference CPU baseline (8.53 s) is quoted on.  N ranks train ONE joint codebook over
+N images (weak scaling: per-GPU work fixed, one all-reduce per level).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    torchrun --nproc-per-node N bench.py --gpus N ...
+
+Rank 0 prints one JSON line.  value = Mblocks/s = (blocks on all ranks) x levels x steps
+/ max-over-ranks wall time / 1e6 (BASELINE.md section 2 definition).
+"""
+import argparse
+import json
+import os
+import subprocess
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+PEAK_FP32_TFLOPS = 157.3     # MI355X_MICROARCH.md: FP32 vector = FP32 matrix peak
+PEAK_HBM_GBS = 8000.0
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--size", type=int, default=4096)
+    ap.add_argument("--block", type=int, default=2)
+    ap.add_argument("--bits", type=int, default=10)
+    ap.add_argument("--images-per-rank", type=int, default=1)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, host cores)")
+    return ap.parse_args()
+
+
+def cpu_baseline(args):
+    """The oracle port (lbg_oracle.c, OpenMP on the same loops as the reference) on the
+    same workload, on this host's cores: one full quantize of one image."""
+    from oracle import oracle  # noqa: F401  (builds liboracle if missing)
+    cli = os.path.join(ROOT, "oracle", "build", "oracle_cli")
+    if not os.path.exists(cli):
+        subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "oracle")], check=True)
+    threads = args.cpu_threads or min(16, os.cpu_count() or 1)
+    out = subprocess.run([cli, "gen", str(args.size), str(0x5EED), str(args.block), str(args.block),
+                          str(args.bits), str(threads), "1"], check=True, capture_output=True, text=True,
+                         timeout=600).stdout
+    rec = json.loads(out.strip().splitlines()[-1])
+    n = rec["N"]
+    mbps = n * args.bits / rec["quantize_s"] / 1e6
+    return {"value": round(mbps, 4), "unit": "Mblocks/s", "cores": threads, "kind": "port",
+            "sample": "one full quantize (tiling excluded) of the rank-0 workload: %dx%d synthetic, %dx%d "
+                      "blocks, %d levels; quantize %.3f s, tiling %.3f s"
+                      % (args.size, args.size, args.block, args.block, args.bits, rec["quantize_s"],
+                         rec["tile_s"])}
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    import torch
+    import torch.distributed as dist
+    import quant_amd
+
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("gloo", rank=rank, world_size=world)   # control plane only
+    torch.cuda.set_device(local)
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+
+    eng = quant_amd.Engine(local)
+    if world > 1:
+        uid = [quant_amd.Engine.comm_unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(uid, src=0)
+        eng.comm_init(world, rank, uid[0])   # RCCL over xGMI for the per-level sums
+    ipr = args.images_per_rank
+    eng.set_synthetic(args.size, 0x5EED + rank * ipr, ipr, args.block, args.block, quant_amd.SCALED)
+    n_local = eng.n
+    D = eng.dim
+
+    for _ in range(args.warmup):
+        eng.lbg(args.bits, want_assign=False)
+    barrier()
+    torch.cuda.synchronize()
+    assign_ms, update_ms, flagged = [], [], []
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        eng.lbg(args.bits, want_assign=False)
+        tm = eng.timings()
+        assign_ms.append(tm["assign_ms"])
+        update_ms.append(tm["update_ms"])
+        flagged.append(tm["flagged"])
+    torch.cuda.synchronize()
+    barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t[0])
+        n = torch.tensor([n_local], dtype=torch.int64)
+        dist.all_reduce(n)
+        n_total = int(n[0])
+    else:
+        n_total = n_local
+
+    levels = args.bits
+    value = n_total * levels * args.steps / elapsed / 1e6
+    ms_per_step = elapsed * 1e3 / args.steps
+
+    # Roofline of the dominant kernel (assign), from HIP events on the engine's stream:
+    # algorithmic work per launch = 3*K_l*D flop per block x n_local blocks.
+    launches = [(1 << (l + 1), ms) for step in assign_ms for l, ms in enumerate(step)]
+    flops = sum(3.0 * K * D * n_local for K, _ in launches)
+    secs = sum(ms for _, ms in launches) * 1e-3
+    achieved = flops / len(launches) / (secs / len(launches)) / 1e12
+    upd_secs = sum(sum(s) for s in update_ms) * 1e-3
+    upd_bytes = len(update_ms) * levels * n_local * (((D + 3) & ~3) + 4)
+    result = {
+        "metric": "Mblocks/s (assign+update)",
+        "value": round(value, 3),
+        "unit": "Mblocks/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(ms_per_step, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32 search + f64 recheck/centroids",
+        "data": "synthetic (SURVEY.md 8(d) generator, seed 0x5EED+image), resident in HBM",
+        "config": {"workload": "C3: %dx%d synthetic RGB per image, %dx%d blocks (D=%d), %d code vectors, "
+                               "%d image(s) per rank, joint codebook" % (args.size, args.size, args.block,
+                                                                         args.block, D, 1 << args.bits, ipr),
+                   "blocks_per_rank": n_local, "levels": levels, "parallelism": "dp%d" % world},
+        "lbg_iters_per_s": round(levels * args.steps / elapsed, 3),
+        "roofline": {"bound": "mfma", "kernel": "assign_kernel<12> (fp32 VALU; vector roof = matrix roof)",
+                     "achieved": round(achieved, 3), "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
+                     "frac": round(achieved / PEAK_FP32_TFLOPS, 4), "traffic": None,
+                     "avg_launch_ms": round(secs * 1e3 / len(launches), 5)},
+        "update_kernel": {"avg_launch_ms": round(upd_secs * 1e3 / max(1, len(update_ms) * levels), 5),
+                          "achieved_GBps": round(upd_bytes / upd_secs / 1e9, 1) if upd_secs else None,
+                          "peak_GBps": PEAK_HBM_GBS},
+        "flagged_rows_per_step": sum(flagged[-1]),
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        try:
+            cb = cpu_baseline(args)
+            result["cpu_baseline"] = cb
+            result["speedup_vs_cpu"] = round(value / cb["value"], 1)
+        except Exception as e:   # the GPU number stands on its own
+            result["cpu_baseline"] = {"error": str(e)}
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    eng.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,62 @@
+"""Host-side logic of the product (no GPU): C-ABI exports, the host kd-tree resolver,
+the exact-sum finaliser, and the fail-loudly behaviour without a device."""
+import os
+import re
+
+import numpy as np
+import pytest
+
+from conftest import ROOT
+from oracle import oracle
+
+
+def test_library_exports_every_declared_symbol():
+    import quant_amd
+    L = quant_amd.lib()
+    hdr = open(os.path.join(ROOT, "include", "qvq.h")).read()
+    names = re.findall(r"QVQ_API\s+[\w\s\*]+?\b(qvq_\w+)\s*\(", hdr)
+    assert len(names) >= 18
+    for n in names:
+        assert hasattr(L, n), n
+    assert set(names) == set(quant_amd.EXPORTED)
+
+
+def test_no_device_fails_loudly():
+    import torch
+    import quant_amd
+    if torch.cuda.is_available():
+        pytest.skip("a GPU is present")
+    with pytest.raises(quant_amd.QVQError):
+        quant_amd.Engine(0)
+
+
+def test_host_kdtree_matches_oracle():
+    import quant_amd
+    rng = np.random.default_rng(5)
+    X, _ = oracle.tile(oracle.gen_image(96), 96, 96, 2, 2)
+    for K in (1, 2, 11, 100, 513):
+        base = X[rng.choice(len(X), K, replace=False)]
+        C = np.concatenate([base * (1 + 0.2), base * (1 - 0.2), np.zeros((2, 12))])
+        np.testing.assert_array_equal(quant_amd.host_kdtree_nn(C, X), oracle.kdtree_nn(C, X))
+    # 4x4 blocks (D = 48) and 1x1 (D = 3: leftover-component path of the distance)
+    for bw in (1, 4):
+        X, _ = oracle.tile(oracle.gen_image(64), 64, 64, bw, bw)
+        C = np.concatenate([X[:50] * 1.2, X[:50] * 0.8, X[:5]])
+        np.testing.assert_array_equal(quant_amd.host_kdtree_nn(C, X), oracle.kdtree_nn(C, X))
+
+
+@pytest.mark.parametrize("cs", [oracle.SCALED, oracle.NORMAL])
+def test_exact_sum_finaliser(cs):
+    import quant_amd
+    X, codes = oracle.tile(oracle.gen_image(128), 128, 128, 2, 2, cs=cs, pad_code=128 if cs else 0)
+    rng = np.random.default_rng(1)
+    K = 64
+    A = rng.integers(0, K - 4, len(X)).astype(np.uint32)
+    hi, lo = quant_amd.host_row_terms(codes, cs)
+    H = np.zeros((K, 12), np.uint64)
+    Lo = np.zeros((K, 12), np.uint64)
+    np.add.at(H, A, hi)
+    np.add.at(Lo, A, lo)
+    cnt = np.bincount(A, minlength=K).astype(np.uint64)
+    C = quant_amd.host_finalize(H, Lo, cnt, cs)
+    np.testing.assert_array_equal(C, oracle.centroids(X, A, K, sum_mode=1))

@@ -1,0 +1,100 @@
+"""The oracle (lbg_oracle.c) against the reference's own fingerprints and unit test."""
+import hashlib
+import json
+import os
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN, load_png_rgb
+from oracle import oracle
+
+FP = json.load(open(os.path.join(GOLDEN, "fingerprints.json")))
+
+
+def sha(a):
+    return hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()[:16]
+
+
+def test_beans_ppm_fixture():
+    rgb, xs, ys = load_png_rgb("beans.png")
+    ppm = b"P6\n%d %d\n255\n" % (xs, ys) + rgb.tobytes()
+    assert hashlib.sha256(ppm).hexdigest()[:16] == FP["beans_ppm"]
+
+
+def test_generator_pixels():
+    assert sha(oracle.gen_image(512)) == FP["pixels_s512"]
+
+
+CASES = [("beans_2x2_n8", "beans.png", 2, 8), ("s512_2x2_n10", 512, 2, 10), ("kodim01_2x2_n10", "kodim01.png", 2, 10),
+         ("s4096_2x2_n10", 4096, 2, 10), ("s4096_4x4_n12", 4096, 4, 12)]
+
+
+@pytest.mark.parametrize("key,src,bw,bits", CASES)
+def test_reference_fingerprints(key, src, bw, bits):
+    if isinstance(src, str):
+        rgb, xs, ys = load_png_rgb(src)
+    else:
+        rgb, xs, ys = oracle.gen_image(src), src, src
+        if src == 4096:
+            assert sha(rgb) == FP["pixels_s4096"]
+    X, _ = oracle.tile(rgb, xs, ys, bw, bw)
+    assert sha(X) == FP[key]["X"]
+    C, A, d = oracle.lbg(X, bits, threads=8)
+    assert sha(A.astype("<u4")) == FP[key]["A"]
+    assert sha(C) == FP[key]["C"]
+    # the engine's centroid rule (exact sums) changes no index and no centroid by > 1 ulp
+    C1, A1, _ = oracle.lbg(X, bits, sum_mode=1, threads=8)
+    np.testing.assert_array_equal(A1, A)
+    assert np.max(np.abs(C1 - C)) <= 4.5e-16
+
+
+@pytest.mark.parametrize("w,h", [(1, 1), (2, 2), (1, 3), (2, 4)])
+def test_reference_unit_test_tiling_roundtrip(w, h):
+    """src/test.cpp:5-62: blocks -> NORMAL bytes -> image is the identity on a 4x4 image
+    of rows 'abc','def','ghi','jkl'."""
+    row = np.frombuffer(b"abcdefghijkl", np.uint8)
+    img = np.tile(row, 4)
+    X, _ = oracle.tile(img, 4, 4, w, h, cs=oracle.NORMAL, pad_code=0)
+    blocks = oracle.codebook_bytes(X, cs=oracle.NORMAL)
+    np.testing.assert_array_equal(oracle.untile(blocks, 4, 4, w, h), img)
+
+
+def test_tiling_wrap_and_pad():
+    """Compressor.cpp:49-57: columns past ySize wrap into the next raster row; bytes past
+    the end of the buffer are 0.  5 x 3 image, 2x2 blocks."""
+    img = np.arange(5 * 3 * 3, dtype=np.uint8) + 1
+    _, codes = oracle.tile(img, 5, 3, 2, 2, cs=oracle.NORMAL, pad_code=0)
+    # block (i=0, j=1): x in {0,1}, y in {2,3}: imgIndex 2, 3 (wraps to row 1), 5, 6
+    np.testing.assert_array_equal(codes[1], np.concatenate([img[6:9], img[9:12], img[15:18], img[18:21]]))
+    # last block (i=2, j=1): x in {4,5}: imgIndex 14, 15 (past end -> 0), 17, 18 (past end)
+    np.testing.assert_array_equal(codes[5], np.concatenate([img[42:45], np.zeros(9, np.uint8)]))
+
+
+def test_scaled_colour_quirks():
+    """Signed char: byte 128 -> 0.0, byte 127 -> 1.0; inverse wraps (ColorSpace.cpp:16-28)."""
+    lut = oracle.lut(oracle.SCALED)
+    assert lut[128] == 0.0 and lut[127] == 1.0 and lut[0] == 128 * (1.0 / 255)
+    back = oracle.codebook_bytes(lut[None, :], cs=oracle.SCALED)[0]
+    np.testing.assert_array_equal(back, np.arange(256, dtype=np.uint8))
+
+
+REF_SO = os.path.join(os.path.dirname(oracle.HERE), "oracle", "_ref", "libref_nn.so")
+
+
+@pytest.mark.skipif(not os.path.exists(REF_SO), reason="oracle/_ref not built (reference not mounted)")
+def test_kdtree_restatement_vs_compiled_reference():
+    """The restated kd-tree against the reference's own nanoflann compiled with its flags,
+    on tie-heavy codebooks (duplicates, zero vectors, split pairs)."""
+    import ctypes
+    R = ctypes.CDLL(REF_SO)
+    R.ref_kdtree_nn.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_void_p, ctypes.c_size_t,
+                                ctypes.c_void_p]
+    rng = np.random.default_rng(11)
+    X, _ = oracle.tile(oracle.gen_image(128), 128, 128, 2, 2)
+    for K in (2, 7, 64, 300):
+        base = X[rng.choice(len(X), K, replace=False)]
+        C = np.concatenate([base * (1 + 0.2), base * (1 - 0.2), np.zeros((3, 12)), base[: K // 3]])
+        ref = np.empty(len(X), np.uint32)
+        R.ref_kdtree_nn(oracle._p(C), len(C), 12, oracle._p(X), len(X), oracle._p(ref))
+        np.testing.assert_array_equal(oracle.kdtree_nn(C, X), ref)
