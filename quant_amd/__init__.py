@@ -167,6 +167,7 @@ class Engine:
         L = t.levels
         return {"levels": L, "total_ms": t.total_ms,
                 "assign_ms": list(t.assign_ms[:max(L, 1)]), "update_ms": list(t.update_ms[:max(L, 1)]),
+                "other_ms": list(t.other_ms[:max(L, 1)]),
                 "flagged": list(t.flagged[:max(L, 1)]), "host_ties": list(t.host_ties[:max(L, 1)])}
 
     # -- multi-GPU -----------------------------------------------------------------------

@@ -1,0 +1,142 @@
+// common.hpp -- shared numerics and kernel launch interface of the qvq engine.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdint>
+
+namespace qvq {
+
+// ---------------------------------------------------------------------------------------
+// Exact-sum decomposition of a colour space's byte -> value map.
+// Every value v[b] is an integer multiple of 2^-scale: q[b] = v[b] * 2^scale.  We write
+// q[b] = R * hi[b] + (lo[b] - bias) with hi[b] <= 255 and 0 <= lo[b] <= 2*bias small, so one
+// u64 LDS atomic of (hi << 32 | lo) per component accumulates both parts without carries
+// for up to 2^24 rows per workgroup; the finaliser rebuilds the exact 128-bit sum.
+//
+// For the MFMA search every value is also an exact small integer in centred form:
+// v[b] - mu = w[b] * sx with |w[b]| <= 255 (f16-exact), up to fl() rounding of v.
+// ---------------------------------------------------------------------------------------
+struct Terms {
+    double v64[256];
+    float v32[256];
+    uint32_t hi[256];
+    uint32_t lo[256];
+    float w[256];       // centred integer value of each byte
+    int64_t R;
+    int64_t bias;
+    int scale;
+    uint8_t pad_code;   // byte whose value is exactly 0.0 (padding past the raster end)
+    double vmax;        // max |v|
+    double mu, sx;      // v ~= mu + w * sx
+};
+
+bool make_terms(int cs, Terms &t);
+
+// Correctly rounded (nearest-even) conversion of a signed 128-bit integer to double.
+__host__ __device__ inline double i128_to_double(__int128 v) {
+    const bool neg = v < 0;
+    unsigned __int128 m = neg ? (unsigned __int128)0 - (unsigned __int128)v : (unsigned __int128)v;
+    const uint64_t hi = (uint64_t)(m >> 64), lo = (uint64_t)m;
+    if (hi == 0 && (lo >> 53) == 0) {
+        const double d = (double)lo;   // exact
+        return neg ? -d : d;
+    }
+#ifdef __HIP_DEVICE_COMPILE__
+    const int lz = hi ? __clzll((long long)hi) : 64 + __clzll((long long)lo);
+#else
+    const int lz = hi ? __builtin_clzll(hi) : 64 + __builtin_clzll(lo);
+#endif
+    const int sh = (128 - lz) - 53;
+    uint64_t top = (uint64_t)(m >> sh);
+    const unsigned __int128 rem = m & (((unsigned __int128)1 << sh) - 1);
+    const unsigned __int128 half = (unsigned __int128)1 << (sh - 1);
+    if (rem > half || (rem == half && (top & 1))) top++;
+    const double d = ldexp((double)top, sh);
+    return neg ? -d : d;
+}
+
+// Centroid component from reduced sums: round(R*hi + lo - bias*cnt) * 2^-scale * fl(1/cnt).
+// Empty cell -> zero vector (src/Quantizer.cpp:81-85).  The reciprocal multiply is the
+// reference's operator/= under -freciprocal-math (include/VectorOperations.hpp:96-98).
+__host__ __device__ inline double centroid_value(uint64_t hi, uint64_t lo, uint64_t cnt, int64_t R, int64_t bias,
+                                                 int scale) {
+    if (cnt == 0) return 0.0;
+    const __int128 S = (__int128)R * (__int128)hi + (__int128)lo - (__int128)bias * (__int128)cnt;
+    return ldexp(i128_to_double(S), -scale) * (1.0 / (double)cnt);
+}
+
+// The reference build's nanoflann distance (kdtree.hpp, ref_l2): bit-identical.
+__device__ inline double ref_l2_dev(const double *a, const double *b, int dim) {
+    double r = 0;
+    int d = 0;
+    for (; d + 3 < dim; d += 4) {
+        const double e0 = a[d] - b[d], e1 = a[d + 1] - b[d + 1];
+        const double e2 = a[d + 2] - b[d + 2], e3 = a[d + 3] - b[d + 3];
+        r += (e1 * e1 + e2 * e2) + (e0 * e0 + e3 * e3);
+    }
+    for (; d < dim; d++) {
+        const double e = a[d] - b[d];
+        r += e * e;
+    }
+    return r;
+}
+
+// MFMA search layout (D = 12): per code vector one 56-byte row of 28 f16
+// [hi0..11, lo0..11, nhi, nlo, 0, 0], where hi+lo ~= -2*sx*(c-mu)*2^t and
+// nhi+nlo ~= 2^t*||c-mu||^2, so that score = 2^t*(||x-c||^2 - ||x-mu||^2).
+constexpr int MF_D = 12;
+constexpr int MF_ROW_F16 = 28;
+constexpr int MF_ROW_BYTES = 2 * MF_ROW_F16;
+constexpr float MF_PAD_SCORE = 65504.0f;   // nhi = nlo = f16 max for padding code vectors
+
+// ---------------------------------------------------------------------------------------
+// Launch wrappers (each defined next to its kernel).  All take the stream last-but-args.
+// ---------------------------------------------------------------------------------------
+hipError_t launch_gen(hipStream_t s, uint8_t *rgb, uint32_t S, uint64_t seed0, uint64_t npix);
+hipError_t launch_tile(hipStream_t s, const uint8_t *rgb, uint8_t *codes, uint32_t n_images, uint32_t xSize,
+                       uint32_t ySize, uint32_t bw, uint32_t bh, uint32_t D, uint32_t Dp, uint8_t pad);
+// VALU fp32 search for any Dp (multiple of 4, <= 64); codebook C32 [K][Dp].
+hipError_t launch_assign_valu(hipStream_t s, int num_cu, uint32_t Dp, const uint8_t *codes, uint64_t N,
+                              const float *C32, uint32_t K, const float *lut32, float alpha, float beta, float gamma,
+                              uint32_t *A, uint32_t *flags, unsigned *flag_cnt);
+// MFMA f16 search for D = 12, optionally with the centroid sums fused (K <= mf_fuse_max_k()).
+// Flag rule (distances, unscaled): second - best <= mfma + 2*(alpha*sqrt(second) + beta*second)
+// + gamma, where `mfma` bounds the error of one MFMA score and the rest the fp32 direct-form
+// recompute ("near-tie flags").
+struct MfThresholds {
+    float mfma, alpha, beta, gamma;
+    float inv_scale;   // 2^-t
+    float mu, sx;      // x = mu + w * sx
+};
+uint32_t mf_fuse_max_k();
+bool mf_can_search(uint32_t K);
+hipError_t launch_assign_mfma(hipStream_t s, int grid, bool fuse, const uint8_t *codes, uint64_t N,
+                              const _Float16 *cb_rows, uint32_t K, const float *C32, const uint64_t *plut,
+                              const MfThresholds &th, uint32_t *A, uint32_t *flags, unsigned *flag_cnt,
+                              uint64_t *part, uint32_t *part_cnt);
+// fp64 recheck of flagged rows; with sums != nullptr also adds the resolved rows' terms.
+hipError_t launch_recheck(hipStream_t s, int num_cu, const uint8_t *codes, uint32_t Dp, uint32_t D,
+                          const uint32_t *flags, const unsigned *flag_cnt, const double *C64, uint32_t K,
+                          const double *lut64, double tie_rel, uint32_t *A, uint32_t *ties, unsigned *tie_cnt,
+                          uint64_t *sums, const uint64_t *plut);
+hipError_t launch_update(hipStream_t s, uint32_t Dp, uint32_t G, const uint8_t *codes, uint64_t N, const uint32_t *A,
+                         uint32_t K, uint32_t D, const uint64_t *plut, uint64_t *part, uint32_t *part_cnt);
+hipError_t launch_reduce(hipStream_t s, const uint64_t *part, const uint32_t *part_cnt, uint32_t G, uint32_t K,
+                         uint32_t D, uint64_t *sums);
+hipError_t launch_mean_sums(hipStream_t s, uint32_t Dp, const uint8_t *codes, uint64_t N, uint32_t D,
+                            const uint64_t *plut, uint64_t *sums);
+hipError_t launch_finalize(hipStream_t s, const uint64_t *sums, uint32_t K, uint32_t D, int64_t R, int64_t bias,
+                           int scale, double *C_cent, bool split, double *C64n);
+// f16 MFMA tables (D = 12) and fp32 VALU table from an fp64 codebook of K code vectors.
+hipError_t launch_prep(hipStream_t s, const double *C64, uint32_t K, uint32_t Kpad, uint32_t D, uint32_t Dp,
+                       double mu, double sx, int t, float *C32, _Float16 *cb_rows);
+hipError_t launch_gather_codes(hipStream_t s, const uint8_t *codes, uint32_t Dp, const uint32_t *rows, uint32_t n,
+                               uint8_t *out);
+hipError_t launch_scatter(hipStream_t s, uint32_t *A, const uint32_t *rows, const uint32_t *vals, uint32_t n,
+                          const uint8_t *codes, uint32_t Dp, uint32_t D, uint32_t K, uint64_t *sums,
+                          const uint64_t *plut);
+hipError_t launch_distortion(hipStream_t s, const uint8_t *codes, uint64_t N, uint32_t D, uint32_t Dp,
+                             const uint32_t *A, const double *C, const double *lut64, double *partial, int grid);
+
+}  // namespace qvq

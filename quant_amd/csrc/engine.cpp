@@ -1,0 +1,720 @@
+// engine.cpp -- host side of the qvq engine: context, per-level schedule, host tie
+// resolution, RCCL exchange and the C ABI of include/qvq.h.  No kernels here; the HIP
+// kernels and their launch wrappers live in k_assign.hip and k_misc.hip.
+//
+// Per split level (LBGIterate, src/Quantizer.cpp:98-108, one effective Lloyd step):
+//   D == 12, K <= mf_fuse_max_k():  assign_mfma<fused sums> -> reduce -> recheck(+sums)
+//                                   -> [host kd-tree + scatter(+sums)] -> [all-reduce]
+//                                   -> finalize+split -> prep (next level's tables)
+//   otherwise:                      assign (MFMA or VALU) -> recheck -> [host] -> update
+//                                   -> reduce -> [all-reduce] -> finalize+split -> prep
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "common.hpp"
+#include "kdtree.hpp"
+#include "qvq.h"
+
+namespace qvq {
+
+// src/ColorSpace.cpp:4-6 (NORMAL) and :16-21 (SCALED, reciprocal multiply under fast-math)
+static double cs_value(int cs, int b) {
+    const double s = (double)(signed char)(unsigned char)b;
+    return cs == QVQ_CS_NORMAL ? s : (s + 128.0) * (1.0 / 255);
+}
+
+bool make_terms(int cs, Terms &t) {
+    if (cs != QVQ_CS_NORMAL && cs != QVQ_CS_SCALED) return false;
+    const bool scaled = cs == QVQ_CS_SCALED;
+    t.scale = scaled ? 60 : 0;
+    t.vmax = 0;
+    // u = (int8)b + 128 orders the bytes by value: SCALED v = fl(u * fl(1/255)),
+    // NORMAL v = u - 128.  q = R*u + E with |E| <= 64 (SCALED) or E = -128 (NORMAL).
+    t.R = scaled ? (int64_t)std::ldexp(1.0 / 255, 60) : 1;
+    t.mu = scaled ? 0.5 : -0.5;
+    t.sx = scaled ? (1.0 / 255) / 2 : 0.5;
+    int64_t E[256], emax = 0;
+    for (int b = 0; b < 256; b++) {
+        t.v64[b] = cs_value(cs, b);
+        t.v32[b] = (float)t.v64[b];
+        t.vmax = std::max(t.vmax, std::fabs(t.v64[b]));
+        const double qd = std::ldexp(t.v64[b], t.scale);
+        if (qd != std::floor(qd)) return false;
+        const int64_t u = (int64_t)(signed char)(unsigned char)b + 128;
+        E[b] = (int64_t)qd - t.R * u;
+        emax = std::max<int64_t>(emax, E[b] < 0 ? -E[b] : E[b]);
+        t.hi[b] = (uint32_t)u;
+        t.w[b] = (float)(2 * u - 255);   // v - mu = w * sx (exactly, up to fl() of v)
+    }
+    t.bias = emax;
+    for (int b = 0; b < 256; b++) t.lo[b] = (uint32_t)(E[b] + t.bias);
+    t.pad_code = scaled ? 0x80 : 0x00;
+    return t.v64[t.pad_code] == 0.0;
+}
+
+}  // namespace qvq
+
+using namespace qvq;
+
+struct qvq_ctx {
+    int dev = 0;
+    int num_cu = 256;
+    hipStream_t stream = nullptr;
+    std::string err;
+
+    // training set
+    uint64_t N = 0;
+    uint32_t D = 0, Dp = 0;
+    int cs = -1;
+    Terms terms;
+    int mf_t = 0;            // MFMA score scale exponent
+    MfThresholds mf_th{};
+    uint8_t *d_codes = nullptr;
+    float *d_lut32 = nullptr, *d_w = nullptr;
+    double *d_lut64 = nullptr;
+    uint64_t *d_plut = nullptr;
+    uint32_t *d_A = nullptr, *d_flags = nullptr, *d_ties = nullptr;
+    unsigned *d_counters = nullptr;   // [0] flags, [1] ties
+
+    // level buffers
+    uint32_t Kcap = 0;
+    uint32_t G = 0;   // workgroup slabs
+    double *d_C64_cent = nullptr, *d_C64_split = nullptr;
+    float *d_C32 = nullptr;
+    _Float16 *d_rows = nullptr;   // MFMA code-vector rows
+    uint64_t *d_part = nullptr, *d_sums = nullptr;
+    uint32_t *d_part_cnt = nullptr;
+    double *d_dist_part = nullptr;
+    uint32_t *d_scatter = nullptr;
+    uint64_t scatter_bytes = 0;
+
+    // multi-GPU
+    ncclComm_t comm = nullptr;
+    int nranks = 1, rank = 0;
+
+    qvq_timings tm;
+    hipEvent_t ev[32][4];
+    bool ev_ready = false;
+};
+
+namespace {
+
+thread_local std::string g_static_err;
+
+qvq_status fail(qvq_ctx *c, qvq_status st, const std::string &msg) {
+    if (c) c->err = msg;
+    else g_static_err = msg;
+    return st;
+}
+
+#define HIPCHK(expr)                                                                                  \
+    do {                                                                                              \
+        hipError_t e_ = (expr);                                                                       \
+        if (e_ != hipSuccess)                                                                         \
+            return fail(ctx, QVQ_EDEVICE, std::string(#expr) + ": " + hipGetErrorString(e_));         \
+    } while (0)
+
+#define NCCLCHK(expr)                                                                                 \
+    do {                                                                                              \
+        ncclResult_t r_ = (expr);                                                                     \
+        if (r_ != ncclSuccess)                                                                        \
+            return fail(ctx, QVQ_ECOMM, std::string(#expr) + ": " + ncclGetErrorString(r_));          \
+    } while (0)
+
+template <typename T>
+void dfree(T *&p) {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+}
+
+uint32_t pad32(uint32_t K) { return (K + 31) & ~31u; }   // MFMA tile pairs
+// QVQ_SEARCH=valu|mfma and QVQ_FUSE=0 select paths for ablation benchmarks.
+bool env_is(const char *name, const char *val) {
+    const char *v = std::getenv(name);
+    return v && std::strcmp(v, val) == 0;
+}
+bool use_mfma(const qvq_ctx *ctx, uint32_t K) {
+    return ctx->D == MF_D && mf_can_search(K) && !env_is("QVQ_SEARCH", "valu");
+}
+bool use_fused(const qvq_ctx *ctx, uint32_t K) {
+    return use_mfma(ctx, K) && K <= mf_fuse_max_k() && !env_is("QVQ_FUSE", "0");
+}
+
+void free_training(qvq_ctx *ctx) {
+    dfree(ctx->d_codes);
+    dfree(ctx->d_A);
+    dfree(ctx->d_flags);
+    dfree(ctx->d_ties);
+    ctx->N = 0;
+    ctx->D = ctx->Dp = 0;
+}
+
+void free_levels(qvq_ctx *ctx) {
+    dfree(ctx->d_C64_cent);
+    dfree(ctx->d_C64_split);
+    dfree(ctx->d_C32);
+    dfree(ctx->d_rows);
+    dfree(ctx->d_part);
+    dfree(ctx->d_part_cnt);
+    dfree(ctx->d_sums);
+    ctx->Kcap = 0;
+}
+
+// MFMA score scale and error bounds for the near-tie flag ("near-tie flags").
+void mfma_setup(qvq_ctx *ctx) {
+    const Terms &t = ctx->terms;
+    const double D = ctx->D;
+    // centroids are means of data values, the split scales them by 1.2 or 0.8
+    double vmin = 1e300, vmax = -1e300, wmax = 0;
+    for (int b = 0; b < 256; b++) {
+        vmin = std::min(vmin, t.v64[b]);
+        vmax = std::max(vmax, t.v64[b]);
+        wmax = std::max(wmax, (double)std::fabs(t.w[b]));
+    }
+    const double cmin = std::min(1.2 * vmin, 0.8 * vmin), cmax = std::max(1.2 * vmax, 0.8 * vmax);
+    const double cp = std::max(std::fabs(cmin - t.mu), std::fabs(cmax - t.mu));   // max |c - mu|
+    const double n_max = D * cp * cp;
+    const double c2_max = 2 * t.sx * cp;
+    const double s_bound = n_max + D * wmax * c2_max;    // sum of |terms| of one score, unscaled
+    int tt = 0;
+    while (std::ldexp(n_max, tt + 1) <= 60000.0 && std::ldexp(s_bound, tt + 1) <= 120000.0) tt++;
+    while (std::ldexp(n_max, tt) > 60000.0 || std::ldexp(s_bound, tt) > 120000.0) tt--;
+    ctx->mf_t = tt;
+    const double u = std::ldexp(1.0, -24);
+    // one MFMA score: <= 33 sequential fp32 roundings over the terms, the f16 hi/lo split
+    // (2^-22 relative + 2^-25 absolute per operand, scaled back), the fp32 scale/shift of
+    // the score and of ||x - mu||^2, x ~ mu + w*sx (2^-53)
+    const double e_acc = 33.0 * u * s_bound;
+    const double e_rep = D * wmax * (c2_max * std::ldexp(1.0, -22) + std::ldexp(1.0, -25 - tt)) +
+                         n_max * std::ldexp(1.0, -22) + std::ldexp(1.0, -25 - tt);
+    const double e_conv = 4 * u * (s_bound + D * cp * cp) + 1e-12 * s_bound;
+    ctx->mf_th.mfma = (float)(1.25 * (e_acc + e_rep + e_conv));
+    // direct-form fp32 recompute (same bound as the VALU search)
+    const double L = std::sqrt(D) * (std::max(std::fabs(vmin), std::fabs(vmax)) + std::max(std::fabs(cmin), std::fabs(cmax))) * 1.001;
+    ctx->mf_th.alpha = (float)(3.0 * 4.01 * u * L);   // x in fp32 is mu + w*sx: <= 2u relative
+    ctx->mf_th.beta = (float)(2.0 * ((ctx->Dp + 4) * u * 1.01 + 4e-15));
+    ctx->mf_th.gamma = (float)(2.0 * 4.01 * u * u * L * L + 1e-30);
+    ctx->mf_th.inv_scale = (float)std::ldexp(1.0, -tt);
+    ctx->mf_th.mu = (float)t.mu;
+    ctx->mf_th.sx = (float)t.sx;
+}
+
+// Allocate the per-row buffers and upload the colour-space tables.
+qvq_status alloc_training(qvq_ctx *ctx, uint64_t N, uint32_t D, int cs) {
+    free_training(ctx);
+    free_levels(ctx);
+    if (!make_terms(cs, ctx->terms)) return fail(ctx, QVQ_EUNSUPPORTED, "colour space has no exact byte sums");
+    if (N == 0 || D == 0) return fail(ctx, QVQ_EINVAL, "empty training set");
+    if (N >= (1ull << 32)) return fail(ctx, QVQ_EINVAL, "more than 2^32-1 rows per rank");
+    const uint32_t Dp = (D + 3) & ~3u;
+    if (Dp > 64) return fail(ctx, QVQ_EINVAL, "block dimension above 64 (3*w*h) is not supported");
+    ctx->N = N;
+    ctx->D = D;
+    ctx->Dp = Dp;
+    ctx->cs = cs;
+    mfma_setup(ctx);
+    HIPCHK(hipMalloc(&ctx->d_codes, N * Dp));
+    HIPCHK(hipMalloc(&ctx->d_A, N * 4));
+    HIPCHK(hipMalloc(&ctx->d_flags, N * 4));
+    HIPCHK(hipMalloc(&ctx->d_ties, N * 4));
+    uint64_t plut[256];
+    for (int b = 0; b < 256; b++) plut[b] = ((uint64_t)ctx->terms.hi[b] << 32) | ctx->terms.lo[b];
+    HIPCHK(hipMemcpy(ctx->d_lut32, ctx->terms.v32, sizeof(ctx->terms.v32), hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(ctx->d_w, ctx->terms.w, sizeof(ctx->terms.w), hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(ctx->d_lut64, ctx->terms.v64, sizeof(ctx->terms.v64), hipMemcpyHostToDevice));
+    HIPCHK(hipMemcpy(ctx->d_plut, plut, sizeof(plut), hipMemcpyHostToDevice));
+    return QVQ_OK;
+}
+
+qvq_status ensure_levels(qvq_ctx *ctx, uint32_t Kmax) {
+    if (ctx->Kcap >= Kmax) return QVQ_OK;
+    free_levels(ctx);
+    const uint64_t KD = (uint64_t)Kmax * ctx->D;
+    const uint64_t Kp = pad32(Kmax);
+    HIPCHK(hipMalloc(&ctx->d_C64_cent, KD * 8));
+    HIPCHK(hipMalloc(&ctx->d_C64_split, KD * 8));
+    HIPCHK(hipMalloc(&ctx->d_C32, Kp * ctx->Dp * 4));
+    HIPCHK(hipMalloc(&ctx->d_rows, Kp * MF_ROW_BYTES));
+    HIPCHK(hipMalloc(&ctx->d_part, (uint64_t)ctx->G * KD * 8));
+    HIPCHK(hipMalloc(&ctx->d_part_cnt, (uint64_t)ctx->G * Kmax * 4));
+    HIPCHK(hipMalloc(&ctx->d_sums, (2 * KD + Kmax) * 8));
+    ctx->Kcap = Kmax;
+    return QVQ_OK;
+}
+
+// Search tables for the K code vectors in d_C64_split.
+qvq_status run_prep(qvq_ctx *ctx, uint32_t K) {
+    HIPCHK(launch_prep(ctx->stream, ctx->d_C64_split, K, pad32(K), ctx->D, ctx->Dp, ctx->terms.mu, ctx->terms.sx,
+                       ctx->mf_t, ctx->d_C32, ctx->d_rows));
+    return QVQ_OK;
+}
+
+// fp32 error-bound coefficients for the VALU search flag ("near-tie flags").
+void valu_coeffs(const qvq_ctx *ctx, float &alpha, float &beta, float &gamma) {
+    const double u = std::ldexp(1.0, -24);
+    const double vmax = ctx->terms.vmax;
+    const double L = std::sqrt((double)ctx->D) * (vmax + 1.2 * vmax) * 1.001;   // >= || |x| + |c| ||
+    alpha = (float)(2.0 * 4.01 * u * L);
+    beta = (float)(2.0 * ((ctx->Dp + 4) * u * 1.01 + 4e-15));
+    gamma = (float)(2.0 * 4.01 * u * u * L * L + 1e-30);
+}
+
+qvq_status all_reduce_sums(qvq_ctx *ctx, uint32_t K) {
+    if (ctx->comm)
+        NCCLCHK(ncclAllReduce(ctx->d_sums, ctx->d_sums, 2 * (uint64_t)K * ctx->D + K, ncclUint64, ncclSum, ctx->comm,
+                              ctx->stream));
+    return QVQ_OK;
+}
+
+qvq_status run_update(qvq_ctx *ctx, const uint32_t *d_A, uint32_t K) {
+    HIPCHK(launch_update(ctx->stream, ctx->Dp, ctx->G, ctx->d_codes, ctx->N, d_A, K, ctx->D, ctx->d_plut, ctx->d_part,
+                         ctx->d_part_cnt));
+    HIPCHK(launch_reduce(ctx->stream, ctx->d_part, ctx->d_part_cnt, ctx->G, K, ctx->D, ctx->d_sums));
+    return QVQ_OK;
+}
+
+// Rows whose fp64 minimum is (nearly) shared: ask the reference kd-tree (kdtree.cpp).
+qvq_status resolve_host_ties(qvq_ctx *ctx, uint32_t K, uint32_t nt, bool accumulate) {
+    const uint32_t D = ctx->D, Dp = ctx->Dp;
+    std::vector<uint32_t> rows(nt);
+    std::vector<double> C((uint64_t)K * D);
+    HIPCHK(hipMemcpyAsync(rows.data(), ctx->d_ties, nt * 4, hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(hipMemcpyAsync(C.data(), ctx->d_C64_split, C.size() * 8, hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+    std::sort(rows.begin(), rows.end());
+    const uint64_t need = (uint64_t)nt * (8 + Dp);   // rows | resolved indices | gathered codes
+    if (ctx->scatter_bytes < need) {
+        dfree(ctx->d_scatter);
+        HIPCHK(hipMalloc(&ctx->d_scatter, need));
+        ctx->scatter_bytes = need;
+    }
+    uint32_t *d_rows = ctx->d_scatter, *d_vals = ctx->d_scatter + nt;
+    uint8_t *d_gath = reinterpret_cast<uint8_t *>(ctx->d_scatter + 2 * (uint64_t)nt);
+    std::vector<uint8_t> code((uint64_t)nt * Dp);
+    HIPCHK(hipMemcpyAsync(d_rows, rows.data(), nt * 4, hipMemcpyHostToDevice, ctx->stream));
+    HIPCHK(launch_gather_codes(ctx->stream, ctx->d_codes, Dp, d_rows, nt, d_gath));
+    HIPCHK(hipMemcpyAsync(code.data(), d_gath, code.size(), hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+    std::vector<double> q(D);
+    std::vector<uint32_t> vals(nt);
+    RefKDTree tree(C.data(), K, (int)D);
+    for (uint32_t i = 0; i < nt; i++) {
+        for (uint32_t d = 0; d < D; d++) q[d] = ctx->terms.v64[code[(uint64_t)i * Dp + d]];
+        vals[i] = tree.nearest(q.data());
+    }
+    HIPCHK(hipMemcpyAsync(d_vals, vals.data(), nt * 4, hipMemcpyHostToDevice, ctx->stream));
+    HIPCHK(launch_scatter(ctx->stream, ctx->d_A, d_rows, d_vals, nt, ctx->d_codes, Dp, D, K,
+                          accumulate ? ctx->d_sums : nullptr, ctx->d_plut));
+    // vals/rows must outlive the async copies
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+    return QVQ_OK;
+}
+
+// One level's assignment of every row against the split codebook (d_C64_split and the
+// tables from run_prep), K code vectors.  With sums_out the exact centroid sums of the
+// final assignment are left in d_sums (fused where possible).
+qvq_status run_level(qvq_ctx *ctx, uint32_t K, int slot, bool sums_out) {
+    const bool fused = sums_out && use_fused(ctx, K);
+    HIPCHK(hipMemsetAsync(ctx->d_counters, 0, 2 * sizeof(unsigned), ctx->stream));
+    if (slot >= 0) HIPCHK(hipEventRecord(ctx->ev[slot][0], ctx->stream));
+    if (use_mfma(ctx, K)) {
+        HIPCHK(launch_assign_mfma(ctx->stream, ctx->num_cu, fused, ctx->d_codes, ctx->N, ctx->d_rows, K,
+                                  ctx->d_C32, ctx->d_plut, ctx->mf_th, ctx->d_A, ctx->d_flags,
+                                  &ctx->d_counters[0], ctx->d_part, ctx->d_part_cnt));
+    } else {
+        float alpha, beta, gamma;
+        valu_coeffs(ctx, alpha, beta, gamma);
+        HIPCHK(launch_assign_valu(ctx->stream, ctx->num_cu, ctx->Dp, ctx->d_codes, ctx->N, ctx->d_C32, K,
+                                  ctx->d_lut32, alpha, beta, gamma, ctx->d_A, ctx->d_flags, &ctx->d_counters[0]));
+    }
+    if (slot >= 0) HIPCHK(hipEventRecord(ctx->ev[slot][1], ctx->stream));
+    if (fused) HIPCHK(launch_reduce(ctx->stream, ctx->d_part, ctx->d_part_cnt, ctx->num_cu, K, ctx->D, ctx->d_sums));
+    HIPCHK(launch_recheck(ctx->stream, ctx->num_cu, ctx->d_codes, ctx->Dp, ctx->D, ctx->d_flags, &ctx->d_counters[0],
+                          ctx->d_C64_split, K, ctx->d_lut64, 1e-12, ctx->d_A, ctx->d_ties, &ctx->d_counters[1],
+                          fused ? ctx->d_sums : nullptr, ctx->d_plut));
+    unsigned counters[2];
+    HIPCHK(hipMemcpyAsync(counters, ctx->d_counters, sizeof(counters), hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+    if (slot >= 0) {
+        ctx->tm.flagged[slot] = counters[0];
+        ctx->tm.host_ties[slot] = counters[1];
+    }
+    if (counters[1]) {
+        qvq_status st = resolve_host_ties(ctx, K, counters[1], fused);
+        if (st != QVQ_OK) return st;
+    }
+    if (slot >= 0) HIPCHK(hipEventRecord(ctx->ev[slot][2], ctx->stream));
+    if (sums_out && !fused) {
+        qvq_status st = run_update(ctx, ctx->d_A, K);
+        if (st != QVQ_OK) return st;
+    }
+    if (slot >= 0) HIPCHK(hipEventRecord(ctx->ev[slot][3], ctx->stream));
+    return QVQ_OK;
+}
+
+qvq_status check_image_args(qvq_ctx *ctx, uint32_t n_images, uint32_t xSize, uint32_t ySize, uint32_t bw,
+                            uint32_t bh, uint64_t &N, uint32_t &D) {
+    if (!ctx) return QVQ_EINVAL;
+    if (n_images == 0 || xSize == 0 || ySize == 0 || bw == 0 || bh == 0)
+        return fail(ctx, QVQ_EINVAL, "image and block sizes must be positive");
+    N = (uint64_t)((xSize + bw - 1) / bw) * ((ySize + bh - 1) / bh) * n_images;
+    D = 3 * bw * bh;
+    return QVQ_OK;
+}
+
+qvq_status tile_into(qvq_ctx *ctx, const uint8_t *d_rgb, uint32_t n_images, uint32_t xSize, uint32_t ySize,
+                     uint32_t bw, uint32_t bh) {
+    HIPCHK(launch_tile(ctx->stream, d_rgb, ctx->d_codes, n_images, xSize, ySize, bw, bh, ctx->D, ctx->Dp,
+                       ctx->terms.pad_code));
+    return QVQ_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+QVQ_API const char *qvq_version(void) { return "qvq 0.2 (gfx950, f16 MFMA search)"; }
+
+QVQ_API const char *qvq_last_error(const qvq_ctx *ctx) { return ctx ? ctx->err.c_str() : g_static_err.c_str(); }
+
+QVQ_API qvq_status qvq_create(int hip_device, qvq_ctx **out) {
+    if (!out) return QVQ_EINVAL;
+    *out = nullptr;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n == 0) return fail(nullptr, QVQ_EDEVICE, "no HIP device");
+    if (hip_device < 0 || hip_device >= n) return fail(nullptr, QVQ_EINVAL, "bad device index");
+    qvq_ctx *ctx = new qvq_ctx();
+    ctx->dev = hip_device;
+    std::memset(&ctx->tm, 0, sizeof(ctx->tm));
+    auto bail = [&](hipError_t e, const char *what) {
+        g_static_err = std::string(what) + ": " + hipGetErrorString(e);
+        qvq_destroy(ctx);
+        return QVQ_EDEVICE;
+    };
+    hipError_t e;
+    if ((e = hipSetDevice(hip_device)) != hipSuccess) return bail(e, "hipSetDevice");
+    hipDeviceProp_t prop;
+    if ((e = hipGetDeviceProperties(&prop, hip_device)) != hipSuccess) return bail(e, "hipGetDeviceProperties");
+    if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0) {
+        g_static_err = std::string("libqvq is built for gfx950, device is ") + prop.gcnArchName;
+        qvq_destroy(ctx);
+        return QVQ_EDEVICE;
+    }
+    ctx->num_cu = prop.multiProcessorCount;
+    ctx->G = (uint32_t)ctx->num_cu;   // one search/update workgroup (and slab) per CU
+    if ((e = hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking)) != hipSuccess) return bail(e, "stream");
+    if ((e = hipMalloc(&ctx->d_lut32, 256 * 4)) != hipSuccess) return bail(e, "hipMalloc");
+    if ((e = hipMalloc(&ctx->d_w, 256 * 4)) != hipSuccess) return bail(e, "hipMalloc");
+    if ((e = hipMalloc(&ctx->d_lut64, 256 * 8)) != hipSuccess) return bail(e, "hipMalloc");
+    if ((e = hipMalloc(&ctx->d_plut, 256 * 8)) != hipSuccess) return bail(e, "hipMalloc");
+    if ((e = hipMalloc(&ctx->d_counters, 4 * sizeof(unsigned))) != hipSuccess) return bail(e, "hipMalloc");
+    if ((e = hipMalloc(&ctx->d_dist_part, 4096 * 8)) != hipSuccess) return bail(e, "hipMalloc");
+    for (int l = 0; l < 32; l++)
+        for (int j = 0; j < 4; j++)
+            if ((e = hipEventCreate(&ctx->ev[l][j])) != hipSuccess) return bail(e, "hipEventCreate");
+    ctx->ev_ready = true;
+    *out = ctx;
+    return QVQ_OK;
+}
+
+QVQ_API void qvq_destroy(qvq_ctx *ctx) {
+    if (!ctx) return;
+    (void)hipSetDevice(ctx->dev);
+    if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+    if (ctx->comm) ncclCommDestroy(ctx->comm);
+    free_training(ctx);
+    free_levels(ctx);
+    dfree(ctx->d_lut32);
+    dfree(ctx->d_w);
+    dfree(ctx->d_lut64);
+    dfree(ctx->d_plut);
+    dfree(ctx->d_counters);
+    dfree(ctx->d_dist_part);
+    dfree(ctx->d_scatter);
+    if (ctx->ev_ready)
+        for (int l = 0; l < 32; l++)
+            for (int j = 0; j < 4; j++) (void)hipEventDestroy(ctx->ev[l][j]);
+    if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
+    delete ctx;
+}
+
+QVQ_API uint64_t qvq_num_vectors(const qvq_ctx *ctx) { return ctx ? ctx->N : 0; }
+QVQ_API uint32_t qvq_dim(const qvq_ctx *ctx) { return ctx ? ctx->D : 0; }
+QVQ_API const uint32_t *qvq_assign_device(const qvq_ctx *ctx) { return ctx ? ctx->d_A : nullptr; }
+
+QVQ_API qvq_status qvq_set_images_device(qvq_ctx *ctx, const void *d_rgb, uint32_t n_images, uint32_t xSize,
+                                         uint32_t ySize, uint32_t bw, uint32_t bh, int colorspace) {
+    uint64_t N;
+    uint32_t D;
+    qvq_status st = check_image_args(ctx, n_images, xSize, ySize, bw, bh, N, D);
+    if (st != QVQ_OK) return st;
+    if (!d_rgb) return fail(ctx, QVQ_EINVAL, "null raster");
+    HIPCHK(hipSetDevice(ctx->dev));
+    if ((st = alloc_training(ctx, N, D, colorspace)) != QVQ_OK) return st;
+    if ((st = tile_into(ctx, (const uint8_t *)d_rgb, n_images, xSize, ySize, bw, bh)) != QVQ_OK) return st;
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+    return QVQ_OK;
+}
+
+QVQ_API qvq_status qvq_set_images(qvq_ctx *ctx, const uint8_t *rgb, uint32_t n_images, uint32_t xSize, uint32_t ySize,
+                                  uint32_t bw, uint32_t bh, int colorspace) {
+    uint64_t N;
+    uint32_t D;
+    qvq_status st = check_image_args(ctx, n_images, xSize, ySize, bw, bh, N, D);
+    if (st != QVQ_OK) return st;
+    if (!rgb) return fail(ctx, QVQ_EINVAL, "null raster");
+    HIPCHK(hipSetDevice(ctx->dev));
+    const uint64_t bytes = (uint64_t)xSize * ySize * 3 * n_images;
+    uint8_t *d_rgb = nullptr;
+    HIPCHK(hipMalloc(&d_rgb, bytes));
+    st = QVQ_OK;
+    const hipError_t e = hipMemcpy(d_rgb, rgb, bytes, hipMemcpyHostToDevice);
+    if (e != hipSuccess) st = fail(ctx, QVQ_EDEVICE, std::string("raster upload: ") + hipGetErrorString(e));
+    if (st == QVQ_OK) st = alloc_training(ctx, N, D, colorspace);
+    if (st == QVQ_OK) st = tile_into(ctx, d_rgb, n_images, xSize, ySize, bw, bh);
+    (void)hipStreamSynchronize(ctx->stream);
+    (void)hipFree(d_rgb);
+    return st;
+}
+
+QVQ_API qvq_status qvq_set_synthetic(qvq_ctx *ctx, uint32_t S, uint64_t seed0, uint32_t n_images, uint32_t bw,
+                                     uint32_t bh, int colorspace) {
+    uint64_t N;
+    uint32_t D;
+    if (!ctx) return QVQ_EINVAL;
+    if (S < 2) return fail(ctx, QVQ_EINVAL, "synthetic images need S >= 2");
+    qvq_status st = check_image_args(ctx, n_images, S, S, bw, bh, N, D);
+    if (st != QVQ_OK) return st;
+    HIPCHK(hipSetDevice(ctx->dev));
+    const uint64_t npix = (uint64_t)S * S * n_images;
+    uint8_t *d_rgb = nullptr;
+    HIPCHK(hipMalloc(&d_rgb, npix * 3));
+    st = QVQ_OK;
+    const hipError_t e = launch_gen(ctx->stream, d_rgb, S, seed0, npix);
+    if (e != hipSuccess) st = fail(ctx, QVQ_EDEVICE, std::string("gen_kernel: ") + hipGetErrorString(e));
+    if (st == QVQ_OK) st = alloc_training(ctx, N, D, colorspace);
+    if (st == QVQ_OK) st = tile_into(ctx, d_rgb, n_images, S, S, bw, bh);
+    (void)hipStreamSynchronize(ctx->stream);
+    (void)hipFree(d_rgb);
+    return st;
+}
+
+QVQ_API qvq_status qvq_set_vectors(qvq_ctx *ctx, const double *X, uint64_t n, uint32_t dim) {
+    if (!ctx) return QVQ_EINVAL;
+    if (!X || n == 0 || dim == 0) return fail(ctx, QVQ_EINVAL, "empty training set");
+    if (dim > 64) return fail(ctx, QVQ_EINVAL, "block dimension above 64 (3*w*h) is not supported");
+    // Recognise the colour space from the values: every value must be a byte's image
+    // under NORMAL or SCALED (0.0 included), so the exact sums apply.
+    int cs_found = -1;
+    std::vector<uint8_t> codes;
+    const uint32_t Dp = (dim + 3) & ~3u;
+    for (int cs : {QVQ_CS_SCALED, QVQ_CS_NORMAL}) {
+        Terms t;
+        make_terms(cs, t);
+        std::vector<std::pair<double, uint8_t>> inv;
+        for (int b = 0; b < 256; b++) inv.push_back({t.v64[b], (uint8_t)b});
+        std::sort(inv.begin(), inv.end());
+        codes.assign(n * Dp, t.pad_code);
+        bool ok = true;
+        for (uint64_t i = 0; i < n && ok; i++)
+            for (uint32_t d = 0; d < dim; d++) {
+                const double v = X[i * dim + d];
+                auto it = std::lower_bound(inv.begin(), inv.end(), std::make_pair(v, (uint8_t)0));
+                if (it == inv.end() || it->first != v || std::signbit(v)) {
+                    ok = false;
+                    break;
+                }
+                codes[i * Dp + d] = it->second;
+            }
+        if (ok) {
+            cs_found = cs;
+            break;
+        }
+    }
+    if (cs_found < 0)
+        return fail(ctx, QVQ_EUNSUPPORTED,
+                    "training values are not NORMAL/SCALED colour-space values; exact device sums need them");
+    HIPCHK(hipSetDevice(ctx->dev));
+    qvq_status st = alloc_training(ctx, n, dim, cs_found);
+    if (st != QVQ_OK) return st;
+    HIPCHK(hipMemcpy(ctx->d_codes, codes.data(), codes.size(), hipMemcpyHostToDevice));
+    return QVQ_OK;
+}
+
+QVQ_API qvq_status qvq_lbg(qvq_ctx *ctx, uint32_t bits, double eps, double *codebook, uint32_t *assign,
+                           double *distortion) {
+    (void)eps;   // cannot change the outputs: one Lloyd step per level
+    if (!ctx) return QVQ_EINVAL;
+    if (ctx->N == 0) return fail(ctx, QVQ_ESTATE, "no training set");
+    if (bits > 20) return fail(ctx, QVQ_EINVAL, "bits must be <= 20");
+    HIPCHK(hipSetDevice(ctx->dev));
+    const auto t0 = std::chrono::steady_clock::now();
+    const uint32_t Kmax = 1u << bits;
+    qvq_status st = ensure_levels(ctx, std::max<uint32_t>(Kmax, 2));
+    if (st != QVQ_OK) return st;
+    std::memset(&ctx->tm, 0, sizeof(ctx->tm));
+    ctx->tm.levels = (int)bits;
+    const Terms &T = ctx->terms;
+
+    // codeVectors[0] = trainingSetSum() / N, then the first split (src/Quantizer.cpp:129-138)
+    HIPCHK(launch_mean_sums(ctx->stream, ctx->Dp, ctx->d_codes, ctx->N, ctx->D, ctx->d_plut, ctx->d_sums));
+    if ((st = all_reduce_sums(ctx, 1)) != QVQ_OK) return st;
+    HIPCHK(launch_finalize(ctx->stream, ctx->d_sums, 1, ctx->D, T.R, T.bias, T.scale, ctx->d_C64_cent, bits > 0,
+                           ctx->d_C64_split));
+    HIPCHK(hipMemsetAsync(ctx->d_A, 0, ctx->N * 4, ctx->stream));
+
+    for (uint32_t lvl = 1; lvl <= bits; lvl++) {
+        const uint32_t K = 1u << lvl;
+        const int slot = (int)lvl - 1;
+        if ((st = run_prep(ctx, K)) != QVQ_OK) return st;
+        if ((st = run_level(ctx, K, slot, true)) != QVQ_OK) return st;
+        if ((st = all_reduce_sums(ctx, K)) != QVQ_OK) return st;
+        HIPCHK(launch_finalize(ctx->stream, ctx->d_sums, K, ctx->D, T.R, T.bias, T.scale, ctx->d_C64_cent, lvl < bits,
+                               ctx->d_C64_split));
+    }
+    // Returned distortion: updateDistortion after the last fix (src/Quantizer.cpp:9-22,103)
+    const int dgrid = (int)std::min<uint64_t>((ctx->N + 255) / 256, 4096);
+    HIPCHK(launch_distortion(ctx->stream, ctx->d_codes, ctx->N, ctx->D, ctx->Dp, ctx->d_A, ctx->d_C64_cent,
+                             ctx->d_lut64, ctx->d_dist_part, dgrid));
+    std::vector<double> dpart(dgrid);
+    HIPCHK(hipMemcpyAsync(dpart.data(), ctx->d_dist_part, dgrid * 8, hipMemcpyDeviceToHost, ctx->stream));
+    if (codebook)
+        HIPCHK(hipMemcpyAsync(codebook, ctx->d_C64_cent, (uint64_t)Kmax * ctx->D * 8, hipMemcpyDeviceToHost,
+                              ctx->stream));
+    if (assign) HIPCHK(hipMemcpyAsync(assign, ctx->d_A, ctx->N * 4, hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+    double dsum = 0;
+    for (double v : dpart) dsum += v;
+    double ntot = (double)ctx->N;
+    if (ctx->comm) {
+        double host2[2] = {dsum, ntot};
+        HIPCHK(hipMemcpy(ctx->d_dist_part, host2, 16, hipMemcpyHostToDevice));
+        NCCLCHK(ncclAllReduce(ctx->d_dist_part, ctx->d_dist_part, 2, ncclDouble, ncclSum, ctx->comm, ctx->stream));
+        HIPCHK(hipMemcpyAsync(host2, ctx->d_dist_part, 16, hipMemcpyDeviceToHost, ctx->stream));
+        HIPCHK(hipStreamSynchronize(ctx->stream));
+        dsum = host2[0];
+        ntot = host2[1];
+    }
+    if (distortion) *distortion = dsum / (ntot * (double)ctx->D);
+    for (uint32_t lvl = 1; lvl <= bits; lvl++) {
+        float a = 0, u = 0, o = 0;
+        (void)hipEventElapsedTime(&a, ctx->ev[lvl - 1][0], ctx->ev[lvl - 1][1]);
+        (void)hipEventElapsedTime(&o, ctx->ev[lvl - 1][1], ctx->ev[lvl - 1][2]);
+        (void)hipEventElapsedTime(&u, ctx->ev[lvl - 1][2], ctx->ev[lvl - 1][3]);
+        ctx->tm.assign_ms[lvl - 1] = a;
+        ctx->tm.other_ms[lvl - 1] = o;
+        ctx->tm.update_ms[lvl - 1] = u;
+    }
+    ctx->tm.total_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    return QVQ_OK;
+}
+
+QVQ_API qvq_status qvq_assign(qvq_ctx *ctx, const double *C, uint32_t K, uint32_t *assign) {
+    if (!ctx) return QVQ_EINVAL;
+    if (ctx->N == 0) return fail(ctx, QVQ_ESTATE, "no training set");
+    if (!C || K == 0) return fail(ctx, QVQ_EINVAL, "empty codebook");
+    HIPCHK(hipSetDevice(ctx->dev));
+    qvq_status st = ensure_levels(ctx, K);
+    if (st != QVQ_OK) return st;
+    std::memset(&ctx->tm, 0, sizeof(ctx->tm));
+    HIPCHK(hipMemcpy(ctx->d_C64_split, C, (uint64_t)K * ctx->D * 8, hipMemcpyHostToDevice));
+    if ((st = run_prep(ctx, K)) != QVQ_OK) return st;
+    if ((st = run_level(ctx, K, 0, false)) != QVQ_OK) return st;
+    if (assign) HIPCHK(hipMemcpy(assign, ctx->d_A, ctx->N * 4, hipMemcpyDeviceToHost));
+    return QVQ_OK;
+}
+
+QVQ_API qvq_status qvq_update(qvq_ctx *ctx, const uint32_t *assign, uint32_t K, double *C_out, uint64_t *counts) {
+    if (!ctx) return QVQ_EINVAL;
+    if (ctx->N == 0) return fail(ctx, QVQ_ESTATE, "no training set");
+    if (!assign || K == 0) return fail(ctx, QVQ_EINVAL, "empty assignment");
+    for (uint64_t i = 0; i < ctx->N; i++)
+        if (assign[i] >= K) return fail(ctx, QVQ_EINVAL, "assignment index out of range");
+    HIPCHK(hipSetDevice(ctx->dev));
+    qvq_status st = ensure_levels(ctx, K);
+    if (st != QVQ_OK) return st;
+    HIPCHK(hipMemcpy(ctx->d_A, assign, ctx->N * 4, hipMemcpyHostToDevice));
+    if ((st = run_update(ctx, ctx->d_A, K)) != QVQ_OK) return st;
+    if ((st = all_reduce_sums(ctx, K)) != QVQ_OK) return st;
+    const Terms &T = ctx->terms;
+    HIPCHK(launch_finalize(ctx->stream, ctx->d_sums, K, ctx->D, T.R, T.bias, T.scale, ctx->d_C64_cent, false, nullptr));
+    if (C_out)
+        HIPCHK(hipMemcpyAsync(C_out, ctx->d_C64_cent, (uint64_t)K * ctx->D * 8, hipMemcpyDeviceToHost, ctx->stream));
+    if (counts)
+        HIPCHK(hipMemcpyAsync(counts, ctx->d_sums + 2 * (uint64_t)K * ctx->D, (uint64_t)K * 8, hipMemcpyDeviceToHost,
+                              ctx->stream));
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+    return QVQ_OK;
+}
+
+QVQ_API qvq_status qvq_comm_unique_id(uint8_t id[128]) {
+    static_assert(sizeof(ncclUniqueId) == 128, "RCCL unique id size");
+    ncclUniqueId u;
+    const ncclResult_t r = ncclGetUniqueId(&u);
+    if (r != ncclSuccess) return fail(nullptr, QVQ_ECOMM, std::string("ncclGetUniqueId: ") + ncclGetErrorString(r));
+    std::memcpy(id, &u, 128);
+    return QVQ_OK;
+}
+
+QVQ_API qvq_status qvq_comm_init(qvq_ctx *ctx, int nranks, int rank, const uint8_t id[128]) {
+    if (!ctx || !id || nranks < 1 || rank < 0 || rank >= nranks) return QVQ_EINVAL;
+    HIPCHK(hipSetDevice(ctx->dev));
+    if (ctx->comm) {
+        ncclCommDestroy(ctx->comm);
+        ctx->comm = nullptr;
+    }
+    ctx->nranks = nranks;
+    ctx->rank = rank;
+    if (nranks == 1) return QVQ_OK;
+    ncclUniqueId u;
+    std::memcpy(&u, id, 128);
+    NCCLCHK(ncclCommInitRank(&ctx->comm, nranks, u, rank));
+    return QVQ_OK;
+}
+
+QVQ_API qvq_status qvq_get_timings(const qvq_ctx *ctx, qvq_timings *out) {
+    if (!ctx || !out) return QVQ_EINVAL;
+    *out = ctx->tm;
+    return QVQ_OK;
+}
+
+QVQ_API qvq_status qvq_host_kdtree_nn(const double *C, uint32_t K, uint32_t dim, const double *Q, uint64_t nq,
+                                      uint32_t *out) {
+    if (!C || !Q || !out || K == 0 || dim == 0) return QVQ_EINVAL;
+    RefKDTree tree(C, K, (int)dim);
+    for (uint64_t i = 0; i < nq; i++) out[i] = tree.nearest(Q + i * dim);
+    return QVQ_OK;
+}
+
+QVQ_API qvq_status qvq_host_finalize(const uint64_t *hi, const uint64_t *lo, const uint64_t *cnt, uint32_t K,
+                                     uint32_t dim, int colorspace, double *C_out) {
+    Terms t;
+    if (!hi || !lo || !cnt || !C_out) return QVQ_EINVAL;
+    if (!make_terms(colorspace, t)) return QVQ_EUNSUPPORTED;
+    for (uint64_t k = 0; k < K; k++)
+        for (uint32_t d = 0; d < dim; d++)
+            C_out[k * dim + d] = centroid_value(hi[k * dim + d], lo[k * dim + d], cnt[k], t.R, t.bias, t.scale);
+    return QVQ_OK;
+}
+
+QVQ_API qvq_status qvq_host_row_terms(const uint8_t *codes, uint32_t dim, int colorspace, uint64_t *hi,
+                                      uint64_t *lo) {
+    Terms t;
+    if (!codes || !hi || !lo) return QVQ_EINVAL;
+    if (!make_terms(colorspace, t)) return QVQ_EUNSUPPORTED;
+    for (uint32_t d = 0; d < dim; d++) {
+        hi[d] = t.hi[codes[d]];
+        lo[d] = t.lo[codes[d]];
+    }
+    return QVQ_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,595 @@
+// k_assign.hip -- nearest-code-vector search (src/Quantizer.cpp:24-32 semantics).
+//
+//  assign_mfma_kernel  D = 12.  Scores 2^t(||x-c||^2 - ||x-mu||^2) for 16 code vectors x
+//                      16 rows per v_mfma_f32_16x16x32_f16: A = code-vector tile
+//                      [f16 hi(12) | f16 lo(12) | n_hi n_lo | 0], B = data tile
+//                      [w(12) | w(12) | 1 1 | 0] with w the exact centred byte integer.
+//                      Epilogue per lane and tile: min of its 4 values, running best tile
+//                      and second-best tile minimum.  At the end each lane recomputes its
+//                      best tile's 4 scores, lanes of a row combine, and rows whose best
+//                      two scores are inside the error bound are flagged for the fp64
+//                      recheck.  Optionally the exact centroid sums of the unflagged rows
+//                      are accumulated in LDS ([d][k] layout, u64 (hi<<32|lo) terms).
+//  assign_valu_kernel  any Dp <= 64, fp32 direct form (x-c)^2 with an fp32 error bound.
+//  recheck_kernel      fp64 distances of flagged rows in the reference build's order.
+#include "common.hpp"
+
+namespace qvq {
+
+typedef _Float16 half8 __attribute__((ext_vector_type(8)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+// =======================================================================================
+// MFMA search
+// =======================================================================================
+constexpr int MF_THREADS = 1024;                 // 16 waves (4 per SIMD), one workgroup per CU
+constexpr int MF_WAVES = MF_THREADS / 64;
+constexpr int MF_TILES = 4;                      // 16-row data tiles per wave and chunk
+constexpr int MF_ROWS = 16 * MF_TILES;           // rows per wave and chunk
+constexpr int MF_LDS_MAX = 160 * 1024;
+
+struct MfLds {
+    uint32_t c32, sums, cnt, plut, total;
+};
+// LDS carve-up: code-vector rows (Kp x 56 B + 16 B pad) | [fp32 codebook Kp x 48 B] |
+// [sums K x 12 x 8 B | counts | term LUT 256 x 8 B].  Kp = K rounded up to 32 (tile pairs).
+__host__ __device__ inline MfLds mf_lds_layout(uint32_t K, bool fuse, bool staged) {
+    const uint32_t Kp = (K + 31) & ~31u;
+    MfLds L;
+    uint32_t o = Kp * MF_ROW_BYTES + 16;
+    L.c32 = o;
+    if (staged) o += Kp * MF_D * 4;
+    L.sums = o;
+    if (fuse) o += K * MF_D * 8;
+    L.cnt = o;
+    if (fuse) o += ((K + 1) & ~1u) * 4;
+    L.plut = o;
+    if (fuse) o += 256 * 8;
+    L.total = o;
+    return L;
+}
+uint32_t mf_fuse_max_k() {
+    uint32_t K = 32;
+    while (mf_lds_layout(2 * K, true, false).total <= MF_LDS_MAX) K *= 2;
+    return K;
+}
+bool mf_can_search(uint32_t K) { return mf_lds_layout(K, false, false).total <= MF_LDS_MAX; }
+
+// min/min3 without the NaN-canonicalising v_max hipcc inserts around fminf (no NaNs here).
+__device__ inline float min3f(float a, float b, float c) {
+    float r;
+    asm("v_min3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
+}
+__device__ inline float min2f(float a, float b) {
+    float r;
+    asm("v_min_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+__device__ inline float med3f(float a, float b, float c) { return __builtin_amdgcn_fmed3f(a, b, c); }
+
+// Centred integer of a byte: w = 2*((int8)b + 128) - 255 = 2*(b ^ 0x80) - 255 (both colour
+// spaces), so v(b) = mu + w*sx.  Exact in f16.
+__device__ inline float byte_w(uint32_t word, int j) {
+    return __fmaf_rn(2.f, (float)(((word ^ 0x80808080u) >> (8 * j)) & 0xFF), -255.f);
+}
+
+typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
+
+// Segmented inclusive sum over consecutive lanes with equal key (lanes hold consecutive
+// rows); returns true on the last lane of each run, which then holds the run's sums.
+__device__ inline bool wave_runs_reduce(uint32_t key, uint32_t (&v)[MF_D + 1], int lane) {
+    const uint32_t prev = __shfl_up(key, 1);
+    uint32_t seg = (lane == 0 || prev != key) ? (uint32_t)lane : 0u;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const uint32_t o = __shfl_up(seg, off);
+        seg = lane >= off ? max(seg, o) : seg;
+    }
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const bool take = lane >= off && (uint32_t)(lane - off) >= seg;
+#pragma unroll
+        for (int i = 0; i <= MF_D; i++) {
+            const uint32_t o = __shfl_up(v[i], off);
+            v[i] += take ? o : 0u;
+        }
+    }
+    const uint32_t next = __shfl_down(key, 1);
+    return lane == 63 || next != key;
+}
+
+// Epilogue of one tile pair for one data tile: minimum of the lane's 8 scores, then the
+// running best pair, best score and second-best pair minimum.
+__device__ inline void pair_update(const f32x4 &p0, const f32x4 &p1, uint32_t pair, float &b1, float &b2,
+                                   uint32_t &bp) {
+    const float m = min2f(min3f(min3f(p0[0], p0[1], p0[2]), p0[3], p1[0]), min3f(p1[1], p1[2], p1[3]));
+    b2 = med3f(b1, b2, m);
+    bp = m < b1 ? pair : bp;
+    b1 = min2f(b1, m);
+}
+
+template <bool FUSE, bool STAGED>
+__global__ __launch_bounds__(MF_THREADS) void assign_mfma_kernel(
+    const uint8_t *__restrict__ codes, uint64_t N, const _Float16 *__restrict__ g_rows, uint32_t K,
+    const float *__restrict__ g_C32, const uint64_t *__restrict__ g_plut, MfThresholds th, uint32_t *__restrict__ A,
+    uint32_t *__restrict__ flags, unsigned *__restrict__ flag_cnt, uint64_t *__restrict__ part,
+    uint32_t *__restrict__ part_cnt) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+    const uint32_t Kp = (K + 31) & ~31u;
+    const MfLds L = mf_lds_layout(K, FUSE, STAGED);
+    unsigned char *rows = lds;   // Kp x 56 B code-vector rows, then 16 B zero pad
+    float *c32s = reinterpret_cast<float *>(lds + L.c32);
+    uint64_t *sums = reinterpret_cast<uint64_t *>(lds + L.sums);   // [d][k]
+    uint32_t *cnt = reinterpret_cast<uint32_t *>(lds + L.cnt);
+    uint64_t *plut = reinterpret_cast<uint64_t *>(lds + L.plut);
+    const int tid = threadIdx.x;
+    {
+        const uint64_t *src = reinterpret_cast<const uint64_t *>(g_rows);
+        uint64_t *dst = reinterpret_cast<uint64_t *>(rows);
+        for (uint32_t i = tid; i < Kp * (MF_ROW_BYTES / 8) + 2; i += MF_THREADS)
+            dst[i] = i < Kp * (MF_ROW_BYTES / 8) ? src[i] : 0ull;
+    }
+    if (STAGED) {
+        const float4 *src = reinterpret_cast<const float4 *>(g_C32);
+        float4 *dst = reinterpret_cast<float4 *>(c32s);
+        for (uint32_t i = tid; i < Kp * (MF_D / 4); i += MF_THREADS) dst[i] = src[i];
+    }
+    if (FUSE) {
+        for (uint32_t i = tid; i < K * MF_D; i += MF_THREADS) sums[i] = 0;
+        for (uint32_t i = tid; i < K; i += MF_THREADS) cnt[i] = 0;
+        if (tid < 256) plut[tid] = g_plut[tid];
+    }
+    __syncthreads();
+    const float *C32 = STAGED ? c32s : g_C32;
+
+    const int lane = tid & 63, wave = tid >> 6;
+    const int g = lane >> 4, c = lane & 15;
+    const uint32_t npairs = Kp / 32;
+    const uint64_t nchunks = (N + MF_ROWS - 1) / MF_ROWS;
+    const f32x4 zero = {0.f, 0.f, 0.f, 0.f};
+    // k-slot words of a row for B: g=0 bytes 0-7, g=1 bytes 8-11 then 0-3, g=2 bytes 4-11
+    const int wa = g == 0 ? 0 : (g == 1 ? 2 : 1), wb = g == 0 ? 1 : (g == 1 ? 0 : 2);
+    // A fragment of tile t: 16 B of code vector t*16 + c at byte 16g of its row (g = 3
+    // reads n_hi, n_lo, 0, 0 and 8 bytes of the next row, which meet zeros in B).
+    const unsigned char *a_base = rows + (size_t)c * MF_ROW_BYTES + 16 * g;
+    auto load_a = [&](uint32_t tile) -> half8 {
+        const uint64_t *p = reinterpret_cast<const uint64_t *>(a_base + (size_t)tile * 16 * MF_ROW_BYTES);
+        const u64x2 v = {p[0], p[1]};
+        return __builtin_bit_cast(half8, v);
+    };
+    auto load_codes = [&](uint64_t chunk, uint32_t (&q)[MF_TILES][3]) {
+#pragma unroll
+        for (int t = 0; t < MF_TILES; t++) {
+            const uint64_t row = chunk * MF_ROWS + t * 16 + c;
+            if (chunk < nchunks && row < N) {
+                const uint32_t *p = reinterpret_cast<const uint32_t *>(codes + row * MF_D);
+                q[t][0] = p[0];
+                q[t][1] = p[1];
+                q[t][2] = p[2];
+            } else {
+                q[t][0] = q[t][1] = q[t][2] = 0x80808080u;
+            }
+        }
+    };
+
+    uint64_t chunk = (uint64_t)blockIdx.x * MF_WAVES + wave;
+    const uint64_t stride = (uint64_t)gridDim.x * MF_WAVES;
+    uint32_t qn[MF_TILES][3];
+    load_codes(chunk, qn);
+    for (; chunk < nchunks; chunk += stride) {
+        const uint64_t base = chunk * MF_ROWS;
+        uint32_t q[MF_TILES][3];
+#pragma unroll
+        for (int t = 0; t < MF_TILES; t++)
+#pragma unroll
+            for (int i = 0; i < 3; i++) q[t][i] = qn[t][i];
+        load_codes(chunk + stride, qn);   // prefetch the next chunk under this one's search
+        // B fragments: lane (g, c) holds k-slots 8g..8g+7 of data row c of each tile.
+        half8 b[MF_TILES];
+        uint32_t own[3] = {q[0][0], q[0][1], q[0][2]};   // this lane's own row, base + lane
+#pragma unroll
+        for (int t = 0; t < MF_TILES; t++) {
+            if (g == t) {
+                own[0] = q[t][0];
+                own[1] = q[t][1];
+                own[2] = q[t][2];
+            }
+            const uint32_t ua = wa == 0 ? q[t][0] : (wa == 1 ? q[t][1] : q[t][2]);
+            const uint32_t ub = wb == 0 ? q[t][0] : (wb == 1 ? q[t][1] : q[t][2]);
+            if (g < 3) {
+#pragma unroll
+                for (int j = 0; j < 4; j++) {
+                    b[t][j] = (_Float16)byte_w(ua, j);
+                    b[t][4 + j] = (_Float16)byte_w(ub, j);
+                }
+            } else {
+                b[t] = half8{1, 1, 0, 0, 0, 0, 0, 0};
+            }
+        }
+        float b1[MF_TILES], b2[MF_TILES];
+        uint32_t bp[MF_TILES];
+#pragma unroll
+        for (int t = 0; t < MF_TILES; t++) {
+            b1[t] = INFINITY;
+            b2[t] = INFINITY;
+            bp[t] = 0;
+        }
+        // Tile pairs, ping-pong: the MFMAs of pair i overlap the epilogue of pair i-1.
+        f32x4 pa0[MF_TILES], pa1[MF_TILES];
+        {
+            const half8 a0 = load_a(0), a1 = load_a(1);
+#pragma unroll
+            for (int t = 0; t < MF_TILES; t++) {
+                pa0[t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a0, b[t], zero, 0, 0, 0);
+                pa1[t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a1, b[t], zero, 0, 0, 0);
+            }
+        }
+        for (uint32_t pr = 1; pr < npairs; pr++) {
+            const half8 a0 = load_a(2 * pr), a1 = load_a(2 * pr + 1);
+            f32x4 qa0[MF_TILES], qa1[MF_TILES];
+#pragma unroll
+            for (int t = 0; t < MF_TILES; t++) {
+                qa0[t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a0, b[t], zero, 0, 0, 0);
+                qa1[t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a1, b[t], zero, 0, 0, 0);
+            }
+#pragma unroll
+            for (int t = 0; t < MF_TILES; t++) pair_update(pa0[t], pa1[t], pr - 1, b1[t], b2[t], bp[t]);
+#pragma unroll
+            for (int t = 0; t < MF_TILES; t++) {
+                pa0[t] = qa0[t];
+                pa1[t] = qa1[t];
+            }
+        }
+#pragma unroll
+        for (int t = 0; t < MF_TILES; t++) pair_update(pa0[t], pa1[t], npairs - 1, b1[t], b2[t], bp[t]);
+
+        // Combine the four lanes of each data row on MFMA values: winning (pair, group) and
+        // the second-best minimum among all other candidates.
+        uint32_t wsel[MF_TILES];   // 8-code-vector unit: pair*4 + g
+#pragma unroll
+        for (int t = 0; t < MF_TILES; t++) {
+            uint32_t u = bp[t] * 4 + g;
+#pragma unroll
+            for (int off = 16; off <= 32; off <<= 1) {
+                const float o1 = __shfl_xor(b1[t], off), o2 = __shfl_xor(b2[t], off);
+                const uint32_t ou = __shfl_xor(u, off);
+                if (o1 < b1[t] || (o1 == b1[t] && ou < u)) {
+                    b2[t] = min2f(o2, b1[t]);
+                    b1[t] = o1;
+                    u = ou;
+                } else {
+                    b2[t] = min2f(b2[t], o1);
+                }
+            }
+            wsel[t] = u;
+        }
+        // Lane L owns row base + L (tile L/16, row L%16): recompute the 8 code vectors of
+        // its winning unit in the direct fp32 form (x - c)^2.
+        uint32_t unit = wsel[0];
+        float sec_m = b2[0];
+#pragma unroll
+        for (int t = 1; t < MF_TILES; t++) {
+            unit = g == t ? wsel[t] : unit;
+            sec_m = g == t ? b2[t] : sec_m;
+        }
+        const uint64_t row = base + lane;
+        const bool valid = row < N;
+        uint32_t rk = 0;
+        bool flagged = false;
+        if (valid) {
+            float x[MF_D];
+            float xn = 0.f;   // ||x - mu||^2
+#pragma unroll
+            for (int d = 0; d < MF_D; d++) {
+                const float e = byte_w(own[d / 4], d % 4) * th.sx;
+                xn = __fmaf_rn(e, e, xn);
+                x[d] = e + th.mu;
+            }
+            float r1 = INFINITY, r2 = INFINITY;
+            const uint32_t pr = unit >> 2, gg = unit & 3;
+#pragma unroll
+            for (int j = 0; j < 8; j++) {
+                const uint32_t cv = (2 * pr + (j >> 2)) * 16 + 4 * gg + (j & 3);
+                const float4 *c4 = reinterpret_cast<const float4 *>(C32 + (size_t)cv * MF_D);
+                float dist = 0.f;
+#pragma unroll
+                for (int qq = 0; qq < 3; qq++) {
+                    const float4 cq = c4[qq];
+                    float e;
+                    e = x[4 * qq + 0] - cq.x; dist = __fmaf_rn(e, e, dist);
+                    e = x[4 * qq + 1] - cq.y; dist = __fmaf_rn(e, e, dist);
+                    e = x[4 * qq + 2] - cq.z; dist = __fmaf_rn(e, e, dist);
+                    e = x[4 * qq + 3] - cq.w; dist = __fmaf_rn(e, e, dist);
+                }
+                dist = cv < K ? dist : INFINITY;   // padding code vectors never win
+                r2 = med3f(r1, r2, dist);
+                rk = dist < r1 ? cv : rk;
+                r1 = min2f(r1, dist);
+            }
+            const float sec = min2f(__fmaf_rn(sec_m, th.inv_scale, xn), r2);
+            const float thr = th.mfma + 2.f * (th.alpha * sqrtf(sec) + th.beta * sec) + th.gamma;
+            A[row] = rk;
+            flagged = !(sec - r1 > thr);
+            if (flagged) flags[atomicAdd(flag_cnt, 1u)] = (uint32_t)row;
+        }
+        if (FUSE) {
+            const bool take = valid && !flagged;
+            if (K <= 64) {
+                // few code vectors: long runs of equal codes along consecutive rows; fold
+                // each run in registers first, one lane per run adds to LDS.
+                uint32_t v[MF_D + 1];
+#pragma unroll
+                for (int d = 0; d < MF_D; d++) {
+                    const uint64_t p = plut[(own[d / 4] >> (8 * (d % 4))) & 0xFF];
+                    v[d] = take ? (uint32_t)(((p >> 32) << 16) | (p & 0xFFFF)) : 0u;   // <= 64 rows: no carry
+                }
+                v[MF_D] = take ? 1u : 0u;
+                const bool tail = wave_runs_reduce(take ? rk : 0xFFFFFFFFu, v, lane);
+                if (tail && take) {
+#pragma unroll
+                    for (int d = 0; d < MF_D; d++)
+                        atomicAdd((unsigned long long *)&sums[(uint32_t)d * K + rk],
+                                  (unsigned long long)((((uint64_t)(v[d] >> 16)) << 32) | (v[d] & 0xFFFF)));
+                    atomicAdd(&cnt[rk], v[MF_D]);
+                }
+            } else if (take) {
+#pragma unroll
+                for (int d = 0; d < MF_D; d++)
+                    atomicAdd((unsigned long long *)&sums[(uint32_t)d * K + rk],
+                              (unsigned long long)plut[(own[d / 4] >> (8 * (d % 4))) & 0xFF]);
+                atomicAdd(&cnt[rk], 1u);
+            }
+        }
+    }
+    if (FUSE) {
+        __syncthreads();
+        uint64_t *pdst = part + (uint64_t)blockIdx.x * K * MF_D;   // slab layout [d][k]
+        for (uint32_t i = tid; i < K * MF_D; i += MF_THREADS) pdst[i] = sums[i];
+        uint32_t *cdst = part_cnt + (uint64_t)blockIdx.x * K;
+        for (uint32_t i = tid; i < K; i += MF_THREADS) cdst[i] = cnt[i];
+    }
+}
+
+template <bool F, bool S>
+static void launch_mfma_variant(hipStream_t s, int grid, size_t lds, const uint8_t *codes, uint64_t N,
+                                const _Float16 *cb_rows, uint32_t K, const float *C32, const uint64_t *plut,
+                                const MfThresholds &th, uint32_t *A, uint32_t *flags, unsigned *flag_cnt,
+                                uint64_t *part, uint32_t *part_cnt) {
+    auto kern = assign_mfma_kernel<F, S>;
+    hipLaunchKernelGGL(kern, dim3(grid), dim3(MF_THREADS), lds, s, codes, N, cb_rows, K, C32, plut, th, A, flags,
+                       flag_cnt, part, part_cnt);
+}
+
+hipError_t launch_assign_mfma(hipStream_t s, int grid, bool fuse, const uint8_t *codes, uint64_t N,
+                              const _Float16 *cb_rows, uint32_t K, const float *C32, const uint64_t *plut,
+                              const MfThresholds &th, uint32_t *A, uint32_t *flags, unsigned *flag_cnt,
+                              uint64_t *part, uint32_t *part_cnt) {
+    const bool staged = mf_lds_layout(K, fuse, true).total <= MF_LDS_MAX;
+    const size_t lds = mf_lds_layout(K, fuse, staged).total;
+    auto *fn = fuse ? (staged ? launch_mfma_variant<true, true> : launch_mfma_variant<true, false>)
+                    : (staged ? launch_mfma_variant<false, true> : launch_mfma_variant<false, false>);
+    fn(s, grid, lds, codes, N, cb_rows, K, C32, plut, th, A, flags, flag_cnt, part, part_cnt);
+    return hipGetLastError();
+}
+
+// =======================================================================================
+// VALU fp32 search (any Dp)
+// =======================================================================================
+constexpr int ASSIGN_THREADS = 256;
+constexpr int ASSIGN_LDS_BYTES = 64 * 1024;
+
+template <int DP>
+struct AssignCfg {
+    static constexpr int R = DP <= 16 ? 4 : (DP <= 48 ? 2 : 1);   // rows per thread
+};
+
+// Each thread keeps R rows in registers; the codebook is staged in LDS (whole when it fits,
+// else in tiles) and read by broadcast.  Per row: best and second-best fp32 distance; a gap
+// inside 2*(alpha*sqrt(d2) + beta*d2) + gamma flags the row for the fp64 recheck.
+template <int DP>
+__global__ __launch_bounds__(ASSIGN_THREADS) void assign_valu_kernel(
+    const uint8_t *__restrict__ codes, uint64_t N, const float *__restrict__ C32, uint32_t K, uint32_t KT,
+    const float *__restrict__ lut32, float alpha, float beta, float gamma, uint32_t *__restrict__ A,
+    uint32_t *__restrict__ flags, unsigned int *__restrict__ flag_cnt) {
+    constexpr int R = AssignCfg<DP>::R;
+    constexpr int D4 = DP / 4;
+    extern __shared__ __attribute__((aligned(16))) float smem[];
+    float *lut = smem;        // 256
+    float *cb = smem + 256;   // KT x DP
+    const int tid = threadIdx.x;
+    lut[tid] = lut32[tid];
+    const bool whole = K <= KT;
+    if (whole) {
+        const float4 *src = reinterpret_cast<const float4 *>(C32);
+        float4 *dst = reinterpret_cast<float4 *>(cb);
+        for (uint32_t i = tid; i < K * D4; i += ASSIGN_THREADS) dst[i] = src[i];
+    }
+    __syncthreads();
+    const uint64_t rows_per_block = (uint64_t)ASSIGN_THREADS * R;
+    const uint64_t nchunks = (N + rows_per_block - 1) / rows_per_block;
+    for (uint64_t chunk = blockIdx.x; chunk < nchunks; chunk += gridDim.x) {
+        float x[R][DP];
+        uint64_t row[R];
+#pragma unroll
+        for (int r = 0; r < R; r++) {
+            row[r] = chunk * rows_per_block + (uint64_t)r * ASSIGN_THREADS + tid;
+            if (row[r] < N) {
+                const uint32_t *w = reinterpret_cast<const uint32_t *>(codes + row[r] * DP);
+#pragma unroll
+                for (int q = 0; q < D4; q++) {
+                    const uint32_t v = w[q];
+                    x[r][4 * q + 0] = lut[v & 0xFF];
+                    x[r][4 * q + 1] = lut[(v >> 8) & 0xFF];
+                    x[r][4 * q + 2] = lut[(v >> 16) & 0xFF];
+                    x[r][4 * q + 3] = lut[v >> 24];
+                }
+            } else {
+#pragma unroll
+                for (int d = 0; d < DP; d++) x[r][d] = 0.f;
+            }
+        }
+        float b1[R], b2[R];
+        uint32_t bi[R];
+#pragma unroll
+        for (int r = 0; r < R; r++) {
+            b1[r] = INFINITY;
+            b2[r] = INFINITY;
+            bi[r] = 0;
+        }
+        for (uint32_t k0 = 0; k0 < K; k0 += KT) {
+            const uint32_t kn = min(KT, K - k0);
+            if (!whole) {
+                __syncthreads();
+                const float4 *src = reinterpret_cast<const float4 *>(C32 + (uint64_t)k0 * DP);
+                float4 *dst = reinterpret_cast<float4 *>(cb);
+                for (uint32_t i = tid; i < kn * D4; i += ASSIGN_THREADS) dst[i] = src[i];
+                __syncthreads();
+            }
+            for (uint32_t kk = 0; kk < kn; kk++) {
+                const float4 *c4 = reinterpret_cast<const float4 *>(cb + kk * DP);
+                float acc[R];
+#pragma unroll
+                for (int r = 0; r < R; r++) acc[r] = 0.f;
+#pragma unroll
+                for (int q = 0; q < D4; q++) {
+                    const float4 cq = c4[q];
+#pragma unroll
+                    for (int r = 0; r < R; r++) {
+                        float t;
+                        t = x[r][4 * q + 0] - cq.x; acc[r] = __fmaf_rn(t, t, acc[r]);
+                        t = x[r][4 * q + 1] - cq.y; acc[r] = __fmaf_rn(t, t, acc[r]);
+                        t = x[r][4 * q + 2] - cq.z; acc[r] = __fmaf_rn(t, t, acc[r]);
+                        t = x[r][4 * q + 3] - cq.w; acc[r] = __fmaf_rn(t, t, acc[r]);
+                    }
+                }
+                const uint32_t k = k0 + kk;
+#pragma unroll
+                for (int r = 0; r < R; r++) {
+                    b2[r] = med3f(b1[r], b2[r], acc[r]);
+                    bi[r] = acc[r] < b1[r] ? k : bi[r];
+                    b1[r] = fminf(b1[r], acc[r]);
+                }
+            }
+        }
+#pragma unroll
+        for (int r = 0; r < R; r++) {
+            if (row[r] < N) {
+                A[row[r]] = bi[r];
+                const float thr = 2.f * (alpha * sqrtf(b2[r]) + beta * b2[r]) + gamma;
+                if (!(b2[r] - b1[r] > thr)) flags[atomicAdd(flag_cnt, 1u)] = (uint32_t)row[r];
+            }
+        }
+    }
+}
+
+#define QVQ_FOR_EACH_DP(X) X(4) X(8) X(12) X(16) X(20) X(24) X(28) X(32) X(36) X(40) X(44) X(48) X(52) X(56) X(60) X(64)
+
+hipError_t launch_assign_valu(hipStream_t s, int num_cu, uint32_t Dp, const uint8_t *codes, uint64_t N,
+                              const float *C32, uint32_t K, const float *lut32, float alpha, float beta, float gamma,
+                              uint32_t *A, uint32_t *flags, unsigned *flag_cnt) {
+    const uint32_t KT = std::min<uint32_t>(K, (ASSIGN_LDS_BYTES - 1024) / (Dp * 4));
+    const size_t lds = 1024 + (size_t)KT * Dp * 4;
+    switch (Dp) {
+#define X(DPV)                                                                                                 \
+    case DPV: {                                                                                                \
+        const uint64_t rpb = (uint64_t)ASSIGN_THREADS * AssignCfg<DPV>::R;                                    \
+        const int grid = (int)std::min<uint64_t>((N + rpb - 1) / rpb, (uint64_t)num_cu * 8);                  \
+        hipLaunchKernelGGL(assign_valu_kernel<DPV>, dim3(grid), dim3(ASSIGN_THREADS), lds, s, codes, N, C32, K, \
+                           KT, lut32, alpha, beta, gamma, A, flags, flag_cnt);                                 \
+        return hipGetLastError();                                                                              \
+    }
+        QVQ_FOR_EACH_DP(X)
+#undef X
+    }
+    return hipErrorInvalidValue;
+}
+
+// =======================================================================================
+// fp64 recheck of flagged rows
+// =======================================================================================
+// One wave per row, lanes stride over the codebook (staged in LDS when it fits).  The row
+// gets the fp64 argmin (lowest index on exact ties); rows whose two best fp64 distances are
+// within tie_rel go to the host kd-tree.  With sums != nullptr the resolved rows' exact
+// terms are added to the global sums (the fused search skipped them).
+constexpr int RECHECK_THREADS = 512;
+constexpr int RECHECK_LDS = 150 * 1024;
+
+__global__ __launch_bounds__(RECHECK_THREADS) void recheck_kernel(
+    const uint8_t *__restrict__ codes, uint32_t Dp, uint32_t D, const uint32_t *__restrict__ flags,
+    const unsigned int *__restrict__ flag_cnt, const double *__restrict__ g_C64, uint32_t K, bool staged,
+    const double *__restrict__ lut64, double tie_rel, uint32_t *__restrict__ A, uint32_t *__restrict__ ties,
+    unsigned int *__restrict__ tie_cnt, uint64_t *__restrict__ sums, const uint64_t *__restrict__ plut) {
+    extern __shared__ __attribute__((aligned(16))) double rsm[];
+    constexpr int W = RECHECK_THREADS / 64;
+    double *xs = rsm;                      // [W][64]
+    double *cbs = rsm + W * 64;            // [K][D] when staged
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const unsigned nflag = *flag_cnt;
+    if (nflag == 0) return;
+    if (staged) {
+        for (uint32_t i = threadIdx.x; i < K * D; i += RECHECK_THREADS) cbs[i] = g_C64[i];
+        __syncthreads();
+    }
+    const double *C64 = staged ? cbs : g_C64;
+    for (unsigned base = blockIdx.x * W; base < nflag; base += gridDim.x * W) {
+        const unsigned f = base + wave;
+        const bool active = f < nflag;
+        const uint32_t row = active ? flags[f] : 0;
+        __syncthreads();
+        if (active && lane < (int)D) xs[wave * 64 + lane] = lut64[codes[(uint64_t)row * Dp + lane]];
+        __syncthreads();
+        if (!active) continue;
+        double d1 = INFINITY, d2 = INFINITY;
+        uint32_t k1 = 0xFFFFFFFFu;
+        for (uint32_t k = lane; k < K; k += 64) {
+            const double d = ref_l2_dev(xs + wave * 64, C64 + (uint64_t)k * D, D);
+            if (d < d1) {
+                d2 = d1;
+                d1 = d;
+                k1 = k;
+            } else if (d < d2) {
+                d2 = d;
+            }
+        }
+#pragma unroll
+        for (int off = 32; off >= 1; off >>= 1) {
+            const double od1 = __shfl_xor(d1, off);
+            const double od2 = __shfl_xor(d2, off);
+            const uint32_t ok1 = __shfl_xor(k1, off);
+            if (od1 < d1 || (od1 == d1 && ok1 < k1)) {
+                d2 = fmin(od2, d1);
+                d1 = od1;
+                k1 = ok1;
+            } else {
+                d2 = fmin(d2, od1);
+            }
+        }
+        const bool tie = d2 - d1 <= tie_rel * d1;
+        if (lane == 0) {
+            A[row] = k1;
+            if (tie) ties[atomicAdd(tie_cnt, 1u)] = row;
+        }
+        if (sums && !tie && lane < (int)D) {
+            const uint64_t KD = (uint64_t)K * D;
+            const uint64_t p = plut[codes[(uint64_t)row * Dp + lane]];
+            atomicAdd((unsigned long long *)&sums[(uint64_t)lane * K + k1], (unsigned long long)(p >> 32));
+            atomicAdd((unsigned long long *)&sums[KD + (uint64_t)lane * K + k1], (unsigned long long)(p & 0xFFFFFFFFull));
+            if (lane == 0) atomicAdd((unsigned long long *)&sums[2 * KD + k1], 1ull);
+        }
+    }
+}
+
+hipError_t launch_recheck(hipStream_t s, int num_cu, const uint8_t *codes, uint32_t Dp, uint32_t D,
+                          const uint32_t *flags, const unsigned *flag_cnt, const double *C64, uint32_t K,
+                          const double *lut64, double tie_rel, uint32_t *A, uint32_t *ties, unsigned *tie_cnt,
+                          uint64_t *sums, const uint64_t *plut) {
+    const size_t base = (size_t)(RECHECK_THREADS / 64) * 64 * 8;
+    const bool staged = base + (size_t)K * D * 8 <= RECHECK_LDS;
+    const size_t lds = base + (staged ? (size_t)K * D * 8 : 0);
+    hipLaunchKernelGGL(recheck_kernel, dim3(num_cu), dim3(RECHECK_THREADS), lds, s, codes, Dp, D, flags, flag_cnt,
+                       C64, K, staged, lut64, tie_rel, A, ties, tie_cnt, sums, plut);
+    return hipGetLastError();
+}
+
+}  // namespace qvq

@@ -1,0 +1,415 @@
+// k_misc.hip -- tiling, synthetic rasters, exact centroid sums, finalisation, split and
+// codebook preparation, tie scatter, distortion.
+//
+// Global sums layout (also the RCCL all-reduce buffer, u64):
+//   hi[d][k] (K*D) | lo[d][k] (K*D) | cnt[k] (K)
+// Workgroup slabs (update kernels): part[g][d][k] packed (hi << 32 | lo), part_cnt[g][k].
+#include "common.hpp"
+
+namespace qvq {
+
+__device__ inline uint64_t splitmix64(uint64_t z) {
+    z += 0x9E3779B97F4A7C15ULL;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
+    return z ^ (z >> 31);
+}
+
+// Synthetic S x S rasters; image i uses seed0 + i.  One thread per pixel.
+__global__ void gen_kernel(uint8_t *__restrict__ rgb, uint32_t S, uint64_t seed0, uint64_t npix_total) {
+    const uint64_t S2 = (uint64_t)S * S;
+    for (uint64_t g = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; g < npix_total;
+         g += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t img = g / S2, p = g - img * S2;
+        const uint64_t r = p / S, c = p - r * S;
+        const uint64_t seed = seed0 + img;
+        const int64_t sm[3] = {(int64_t)(r * 255 / (S - 1)), (int64_t)(c * 255 / (S - 1)),
+                               (int64_t)((r + c) * 255 / (2 * (uint64_t)(S - 1)))};
+#pragma unroll
+        for (int ch = 0; ch < 3; ch++) {
+            const uint64_t h = splitmix64((seed << 40) ^ (p * 3 + ch));
+            int64_t v = sm[ch] + (int64_t)(h % 33) - 16;
+            v = v < 0 ? 0 : (v > 255 ? 255 : v);
+            rgb[g * 3 + ch] = (uint8_t)v;
+        }
+    }
+}
+
+hipError_t launch_gen(hipStream_t s, uint8_t *rgb, uint32_t S, uint64_t seed0, uint64_t npix) {
+    hipLaunchKernelGGL(gen_kernel, dim3((int)std::min<uint64_t>((npix + 255) / 256, 65536)), dim3(256), 0, s, rgb, S,
+                       seed0, npix);
+    return hipGetLastError();
+}
+
+// getBlocksAsVectorsFromImage (src/Compressor.cpp:31-62) over n_images rasters, writing
+// each block's raw bytes (component order ((x-iw)*h + (y-jh))*3 + c) into codes[g][0..D),
+// padding [D, Dp) with the zero-valued byte.  One thread per block.
+__global__ void tile_kernel(const uint8_t *__restrict__ rgb, uint8_t *__restrict__ codes, uint32_t n_images,
+                            uint32_t xSize, uint32_t ySize, uint32_t bw, uint32_t bh, uint32_t D, uint32_t Dp,
+                            uint8_t pad) {
+    const uint64_t wB = (xSize + bw - 1) / bw, hB = (ySize + bh - 1) / bh, nb = wB * hB;
+    const uint64_t total = (uint64_t)xSize * ySize;
+    const uint64_t nall = nb * n_images;
+    for (uint64_t g = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; g < nall;
+         g += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t img = g / nb, b = g - img * nb;
+        const uint64_t i = b / hB, j = b - i * hB;
+        const uint8_t *src = rgb + img * total * 3;
+        uint8_t *dst = codes + g * Dp;
+        for (uint64_t x = i * bw; x < i * bw + bw; x++)
+            for (uint64_t y = j * bh; y < j * bh + bh; y++) {
+                const uint64_t imgIndex = x * ySize + y;   // wraps past ySize into the next row
+                const uint64_t vec = ((x - i * bw) * bh + (y - j * bh)) * 3;
+                for (int c = 0; c < 3; c++) dst[vec + c] = imgIndex < total ? src[imgIndex * 3 + c] : pad;
+            }
+        for (uint32_t d = D; d < Dp; d++) dst[d] = pad;
+    }
+}
+
+hipError_t launch_tile(hipStream_t s, const uint8_t *rgb, uint8_t *codes, uint32_t n_images, uint32_t xSize,
+                       uint32_t ySize, uint32_t bw, uint32_t bh, uint32_t D, uint32_t Dp, uint8_t pad) {
+    const uint64_t nb = (uint64_t)((xSize + bw - 1) / bw) * ((ySize + bh - 1) / bh) * n_images;
+    hipLaunchKernelGGL(tile_kernel, dim3((int)std::min<uint64_t>((nb + 255) / 256, 65536)), dim3(256), 0, s, rgb,
+                       codes, n_images, xSize, ySize, bw, bh, D, Dp, pad);
+    return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------------------
+// Exact centroid sums for an arbitrary assignment (the path not fused into the search).
+// Grid (G, passes): workgroup g folds its contiguous row range into LDS for code vectors
+// [k0, k0 + KR), layout [d][k], then writes its packed slab.
+// ---------------------------------------------------------------------------------------
+constexpr int UPDATE_THREADS = 1024;
+constexpr size_t UPDATE_LDS = 150 * 1024;
+
+template <int DP>
+__global__ __launch_bounds__(UPDATE_THREADS) void update_kernel(
+    const uint8_t *__restrict__ codes, uint64_t N, const uint32_t *__restrict__ A, uint32_t K, uint32_t KR,
+    uint32_t D, uint64_t rows_per_group, const uint64_t *__restrict__ plut, uint64_t *__restrict__ part,
+    uint32_t *__restrict__ part_cnt) {
+    extern __shared__ __attribute__((aligned(16))) uint64_t lsum[];   // [D][KR] | cnt u32 [KR] | lut [256]
+    const uint32_t k0 = blockIdx.y * KR;
+    const uint32_t kr = min(KR, K - k0);
+    uint32_t *lcnt = reinterpret_cast<uint32_t *>(lsum + (uint64_t)KR * D);
+    uint64_t *llut = lsum + (uint64_t)KR * D + (KR + 1) / 2;
+    const int tid = threadIdx.x;
+    for (uint32_t i = tid; i < KR * D; i += UPDATE_THREADS) lsum[i] = 0;
+    for (uint32_t i = tid; i < KR; i += UPDATE_THREADS) lcnt[i] = 0;
+    for (int i = tid; i < 256; i += UPDATE_THREADS) llut[i] = plut[i];
+    __syncthreads();
+    const uint64_t start = blockIdx.x * rows_per_group;
+    const uint64_t end = min(N, start + rows_per_group);
+    for (uint64_t row = start + tid; row < end; row += UPDATE_THREADS) {
+        const uint32_t kl = A[row] - k0;
+        if (kl < kr) {
+            const uint32_t *w = reinterpret_cast<const uint32_t *>(codes + row * DP);
+#pragma unroll
+            for (int q = 0; q < DP / 4; q++) {
+                const uint32_t v = w[q];
+#pragma unroll
+                for (int j = 0; j < 4; j++)
+                    if (4 * q + j < (int)D)
+                        atomicAdd((unsigned long long *)&lsum[(uint32_t)(4 * q + j) * KR + kl],
+                                  (unsigned long long)llut[(v >> (8 * j)) & 0xFF]);
+            }
+            atomicAdd(&lcnt[kl], 1u);
+        }
+    }
+    __syncthreads();
+    uint64_t *pdst = part + (uint64_t)blockIdx.x * K * D;
+    for (uint32_t i = tid; i < kr * D; i += UPDATE_THREADS) {
+        const uint32_t d = i / kr, k = i - d * kr;
+        pdst[(uint64_t)d * K + k0 + k] = lsum[d * KR + k];
+    }
+    uint32_t *cdst = part_cnt + (uint64_t)blockIdx.x * K + k0;
+    for (uint32_t i = tid; i < kr; i += UPDATE_THREADS) cdst[i] = lcnt[i];
+}
+
+#define QVQ_FOR_EACH_DP(X) X(4) X(8) X(12) X(16) X(20) X(24) X(28) X(32) X(36) X(40) X(44) X(48) X(52) X(56) X(60) X(64)
+
+hipError_t launch_update(hipStream_t s, uint32_t Dp, uint32_t G, const uint8_t *codes, uint64_t N, const uint32_t *A,
+                         uint32_t K, uint32_t D, const uint64_t *plut, uint64_t *part, uint32_t *part_cnt) {
+    const size_t per_k = (size_t)D * 8 + 4;
+    const uint32_t KR = (uint32_t)std::min<size_t>(K, (UPDATE_LDS - 2048 - 16) / per_k);
+    if (KR == 0) return hipErrorInvalidValue;
+    const uint32_t passes = (K + KR - 1) / KR;
+    const size_t lds = (size_t)KR * D * 8 + ((KR + 1) / 2) * 8 + 256 * 8;
+    const uint64_t rpg = (N + G - 1) / G;
+    switch (Dp) {
+#define X(DPV)                                                                                                    \
+    case DPV:                                                                                                     \
+        hipLaunchKernelGGL(update_kernel<DPV>, dim3(G, passes), dim3(UPDATE_THREADS), lds, s, codes, N, A, K, KR, \
+                           D, rpg, plut, part, part_cnt);                                                         \
+        return hipGetLastError();
+        QVQ_FOR_EACH_DP(X)
+#undef X
+    }
+    return hipErrorInvalidValue;
+}
+
+// Column reduce of G slabs into sums (layout in the file header).  A workgroup owns 64
+// columns; its 16 waves each add every 16th slab, then combine through LDS.
+constexpr int REDUCE_THREADS = 1024;
+__global__ __launch_bounds__(REDUCE_THREADS) void reduce_kernel(const uint64_t *__restrict__ part,
+                                                                const uint32_t *__restrict__ part_cnt, uint32_t G,
+                                                                uint32_t K, uint32_t D, uint64_t *__restrict__ sums) {
+    __shared__ uint64_t red_hi[16][64], red_lo[16][64];
+    const uint64_t KD = (uint64_t)K * D;
+    const uint64_t col = (uint64_t)blockIdx.x * 64 + (threadIdx.x & 63);
+    const int sg = threadIdx.x >> 6;
+    uint64_t hi = 0, lo = 0;
+    if (col < KD) {
+#pragma unroll 4
+        for (uint32_t g = sg; g < G; g += 16) {
+            const uint64_t p = part[g * KD + col];
+            hi += p >> 32;
+            lo += p & 0xFFFFFFFFull;
+        }
+    } else if (col < KD + K) {
+#pragma unroll 4
+        for (uint32_t g = sg; g < G; g += 16) hi += part_cnt[(uint64_t)g * K + (col - KD)];
+    }
+    red_hi[sg][threadIdx.x & 63] = hi;
+    red_lo[sg][threadIdx.x & 63] = lo;
+    __syncthreads();
+    if (sg == 0) {
+        for (int i = 1; i < 16; i++) {
+            hi += red_hi[i][threadIdx.x];
+            lo += red_lo[i][threadIdx.x];
+        }
+        if (col < KD) {
+            sums[col] = hi;
+            sums[KD + col] = lo;
+        } else if (col < KD + K) {
+            sums[2 * KD + (col - KD)] = hi;
+        }
+    }
+}
+
+hipError_t launch_reduce(hipStream_t s, const uint64_t *part, const uint32_t *part_cnt, uint32_t G, uint32_t K,
+                         uint32_t D, uint64_t *sums) {
+    const uint64_t cols = (uint64_t)K * D + K;
+    hipLaunchKernelGGL(reduce_kernel, dim3((int)((cols + 63) / 64)), dim3(REDUCE_THREADS), 0, s, part, part_cnt, G, K,
+                       D, sums);
+    return hipGetLastError();
+}
+
+// K = 1 (the mean initialisation, trainingSetSum, src/Quantizer.cpp:46-57): every row in
+// one cluster, so a plain register + LDS reduction; sums must be zeroed beforehand.
+constexpr int MEAN_THREADS = 256;
+template <int DP>
+__global__ __launch_bounds__(MEAN_THREADS) void mean_sums_kernel(const uint8_t *__restrict__ codes, uint64_t N,
+                                                                 uint32_t D, const uint64_t *__restrict__ plut,
+                                                                 uint64_t *__restrict__ sums) {
+    __shared__ uint64_t lut[256];
+    __shared__ uint64_t red[MEAN_THREADS / 64][DP][2];
+    lut[threadIdx.x] = plut[threadIdx.x];
+    if (blockIdx.x == 0 && threadIdx.x == 0) sums[2 * D] = N;   // cnt[0]
+    __syncthreads();
+    uint64_t acc[DP];
+#pragma unroll
+    for (int d = 0; d < DP; d++) acc[d] = 0;   // packed (hi << 32 | lo): <= 2^24 rows per thread
+    for (uint64_t row = blockIdx.x * (uint64_t)MEAN_THREADS + threadIdx.x; row < N;
+         row += (uint64_t)gridDim.x * MEAN_THREADS) {
+        const uint32_t *w = reinterpret_cast<const uint32_t *>(codes + row * DP);
+#pragma unroll
+        for (int q = 0; q < DP / 4; q++) {
+            const uint32_t v = w[q];
+#pragma unroll
+            for (int j = 0; j < 4; j++) acc[4 * q + j] += lut[(v >> (8 * j)) & 0xFF];
+        }
+    }
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+#pragma unroll
+    for (int d = 0; d < DP; d++) {
+        uint64_t h = acc[d] >> 32, l = acc[d] & 0xFFFFFFFFull;
+        for (int off = 32; off >= 1; off >>= 1) {
+            h += __shfl_xor(h, off);
+            l += __shfl_xor(l, off);
+        }
+        if (lane == 0) {
+            red[wave][d][0] = h;
+            red[wave][d][1] = l;
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x < (unsigned)D) {
+        uint64_t h = 0, l = 0;
+        for (int w = 0; w < MEAN_THREADS / 64; w++) {
+            h += red[w][threadIdx.x][0];
+            l += red[w][threadIdx.x][1];
+        }
+        atomicAdd((unsigned long long *)&sums[threadIdx.x], (unsigned long long)h);
+        atomicAdd((unsigned long long *)&sums[D + threadIdx.x], (unsigned long long)l);
+    }
+}
+
+hipError_t launch_mean_sums(hipStream_t s, uint32_t Dp, const uint8_t *codes, uint64_t N, uint32_t D,
+                            const uint64_t *plut, uint64_t *sums) {
+    const hipError_t e = hipMemsetAsync(sums, 0, (2 * (size_t)D + 1) * 8, s);
+    if (e != hipSuccess) return e;
+    const int grid = (int)std::min<uint64_t>((N + MEAN_THREADS - 1) / MEAN_THREADS, 1024);
+    switch (Dp) {
+#define X(DPV)                                                                                                    \
+    case DPV:                                                                                                     \
+        hipLaunchKernelGGL(mean_sums_kernel<DPV>, dim3(grid), dim3(MEAN_THREADS), 0, s, codes, N, D, plut, sums); \
+        return hipGetLastError();
+        QVQ_FOR_EACH_DP(X)
+#undef X
+    }
+    return hipErrorInvalidValue;
+}
+
+// Centroids from the reduced sums; optionally the next level's split codebook
+// (src/Quantizer.cpp:134-138: concat, then x(1+0.2) and x(1-0.2)) in fp64.
+__global__ void finalize_kernel(const uint64_t *__restrict__ sums, uint32_t K, uint32_t D, int64_t R, int64_t bias,
+                                int scale, double *__restrict__ C_cent, int split, double *__restrict__ C64n) {
+    const uint64_t KD = (uint64_t)K * D;
+    for (uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; t < KD; t += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t k = t / D, d = t - k * D;
+        const uint64_t c = d * K + k;
+        const double v = centroid_value(sums[c], sums[KD + c], sums[2 * KD + k], R, bias, scale);
+        C_cent[t] = v;
+        if (split) {
+            C64n[t] = v * (double)(1 + 0.2);
+            C64n[KD + t] = v * (double)(1 - 0.2);
+        }
+    }
+}
+
+hipError_t launch_finalize(hipStream_t s, const uint64_t *sums, uint32_t K, uint32_t D, int64_t R, int64_t bias,
+                           int scale, double *C_cent, bool split, double *C64n) {
+    const uint64_t n = (uint64_t)K * D;
+    hipLaunchKernelGGL(finalize_kernel, dim3((int)std::min<uint64_t>((n + 255) / 256, 4096)), dim3(256), 0, s, sums, K,
+                       D, R, bias, scale, C_cent, split ? 1 : 0, C64n);
+    return hipGetLastError();
+}
+
+// Search tables from an fp64 codebook: fp32 [Kpad][Dp] (VALU path and the MFMA recompute)
+// and, for D = 12, the f16 MFMA rows (common.hpp).  Code vectors K..Kpad-1 are padding
+// that never wins.
+__global__ void prep_kernel(const double *__restrict__ C64, uint32_t K, uint32_t Kpad, uint32_t D, uint32_t Dp,
+                            double mu, double sx, double scale_t, float *__restrict__ C32,
+                            _Float16 *__restrict__ rows) {
+    for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < Kpad; k += gridDim.x * blockDim.x) {
+        _Float16 *r = rows + (uint64_t)k * MF_ROW_F16;
+        if (k >= K) {
+            for (uint32_t d = 0; d < Dp; d++) C32[(uint64_t)k * Dp + d] = 0.f;
+            if (D == MF_D) {
+                for (int j = 0; j < MF_ROW_F16; j++) r[j] = (_Float16)0.f;
+                r[2 * MF_D] = (_Float16)MF_PAD_SCORE;
+                r[2 * MF_D + 1] = (_Float16)MF_PAD_SCORE;
+            }
+            continue;
+        }
+        const double *c = C64 + (uint64_t)k * D;
+        double n = 0;
+        for (uint32_t d = 0; d < Dp; d++) {
+            const double v = d < D ? c[d] : 0.0;
+            C32[(uint64_t)k * Dp + d] = (float)v;
+            if (D == MF_D && d < D) {
+                const double cp = v - mu;
+                n += cp * cp;
+                const double c2 = -2.0 * sx * cp * scale_t;
+                const _Float16 h = (_Float16)(float)c2;
+                r[d] = h;
+                r[MF_D + d] = (_Float16)(float)(c2 - (double)(float)h);
+            }
+        }
+        if (D == MF_D) {
+            n *= scale_t;
+            const _Float16 h = (_Float16)(float)n;
+            r[2 * MF_D] = h;
+            r[2 * MF_D + 1] = (_Float16)(float)(n - (double)(float)h);
+            r[2 * MF_D + 2] = (_Float16)0.f;
+            r[2 * MF_D + 3] = (_Float16)0.f;
+        }
+    }
+}
+
+hipError_t launch_prep(hipStream_t s, const double *C64, uint32_t K, uint32_t Kpad, uint32_t D, uint32_t Dp,
+                       double mu, double sx, int t, float *C32, _Float16 *cb_rows) {
+    hipLaunchKernelGGL(prep_kernel, dim3((Kpad + 255) / 256), dim3(256), 0, s, C64, K, Kpad, D, Dp, mu, sx,
+                       std::ldexp(1.0, t), C32, cb_rows);
+    return hipGetLastError();
+}
+
+// out[i] = codes of row rows[i] (rows the host kd-tree resolves).
+__global__ void gather_codes_kernel(const uint8_t *__restrict__ codes, uint32_t Dp, const uint32_t *__restrict__ rows,
+                                    uint32_t n, uint8_t *__restrict__ out) {
+    for (uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; t < (uint64_t)n * Dp;
+         t += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t i = t / Dp, d = t - i * Dp;
+        out[t] = codes[(uint64_t)rows[i] * Dp + d];
+    }
+}
+
+hipError_t launch_gather_codes(hipStream_t s, const uint8_t *codes, uint32_t Dp, const uint32_t *rows, uint32_t n,
+                               uint8_t *out) {
+    hipLaunchKernelGGL(gather_codes_kernel, dim3((int)std::min<uint64_t>(((uint64_t)n * Dp + 255) / 256, 4096)),
+                       dim3(256), 0, s, codes, Dp, rows, n, out);
+    return hipGetLastError();
+}
+
+// A[rows[i]] = vals[i] (host tie resolutions); with sums, also add those rows' terms.
+__global__ void scatter_kernel(uint32_t *__restrict__ A, const uint32_t *__restrict__ rows,
+                               const uint32_t *__restrict__ vals, uint32_t n, const uint8_t *__restrict__ codes,
+                               uint32_t Dp, uint32_t D, uint32_t K, uint64_t *__restrict__ sums,
+                               const uint64_t *__restrict__ plut) {
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+        const uint32_t r = rows[i], k = vals[i];
+        A[r] = k;
+        if (sums) {
+            const uint64_t KD = (uint64_t)K * D;
+            for (uint32_t d = 0; d < D; d++) {
+                const uint64_t p = plut[codes[(uint64_t)r * Dp + d]];
+                atomicAdd((unsigned long long *)&sums[(uint64_t)d * K + k], (unsigned long long)(p >> 32));
+                atomicAdd((unsigned long long *)&sums[KD + (uint64_t)d * K + k], (unsigned long long)(p & 0xFFFFFFFFull));
+            }
+            atomicAdd((unsigned long long *)&sums[2 * KD + k], 1ull);
+        }
+    }
+}
+
+hipError_t launch_scatter(hipStream_t s, uint32_t *A, const uint32_t *rows, const uint32_t *vals, uint32_t n,
+                          const uint8_t *codes, uint32_t Dp, uint32_t D, uint32_t K, uint64_t *sums,
+                          const uint64_t *plut) {
+    hipLaunchKernelGGL(scatter_kernel, dim3((n + 255) / 256), dim3(256), 0, s, A, rows, vals, n, codes, Dp, D, K, sums,
+                       plut);
+    return hipGetLastError();
+}
+
+// Sum over rows of norm(x - c_A(x)) (src/Quantizer.cpp:9-22), one partial per workgroup.
+constexpr int DIST_THREADS = 256;
+__global__ __launch_bounds__(DIST_THREADS) void distortion_kernel(
+    const uint8_t *__restrict__ codes, uint64_t N, uint32_t D, uint32_t Dp, const uint32_t *__restrict__ A,
+    const double *__restrict__ C, const double *__restrict__ lut64, double *__restrict__ partial) {
+    __shared__ double red[DIST_THREADS];
+    double s = 0;
+    for (uint64_t row = blockIdx.x * (uint64_t)DIST_THREADS + threadIdx.x; row < N;
+         row += (uint64_t)gridDim.x * DIST_THREADS) {
+        const double *c = C + (uint64_t)A[row] * D;
+        const uint8_t *x = codes + row * Dp;
+        double r = 0;
+        for (uint32_t d = 0; d < D; d++) {
+            const double e = lut64[x[d]] - c[d];
+            r += e * e;
+        }
+        s += r;
+    }
+    red[threadIdx.x] = s;
+    __syncthreads();
+    for (int w = DIST_THREADS / 2; w > 0; w >>= 1) {
+        if ((int)threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) partial[blockIdx.x] = red[0];
+}
+
+hipError_t launch_distortion(hipStream_t s, const uint8_t *codes, uint64_t N, uint32_t D, uint32_t Dp,
+                             const uint32_t *A, const double *C, const double *lut64, double *partial, int grid) {
+    hipLaunchKernelGGL(distortion_kernel, dim3(grid), dim3(DIST_THREADS), 0, s, codes, N, D, Dp, A, C, lut64, partial);
+    return hipGetLastError();
+}
+
+}  // namespace qvq

@@ -1,12 +1,23 @@
-import sys, json, time
+"""Per-level timings of qvq_lbg for a few workloads (diagnostics, not the bench)."""
+import json
+import sys
+import time
+
 sys.path.insert(0, '.')
 import quant_amd
+
+cases = [(512, 2, 10), (4096, 2, 10), (4096, 4, 12)]
+if len(sys.argv) > 1:
+    cases = [tuple(int(v) for v in c.split(',')) for c in sys.argv[1:]]
 eng = quant_amd.Engine(0)
-for (S, bw, bits) in [(512, 2, 10), (4096, 2, 10), (4096, 4, 12)]:
+for (S, bw, bits) in cases:
     eng.set_synthetic(S, 0x5EED, 1, bw, bw)
     for rep in range(3):
-        t = time.time(); C, A, d = eng.lbg(bits, want_assign=False); dt = time.time() - t
+        t = time.time()
+        C, A, d = eng.lbg(bits, want_assign=False)
+        dt = time.time() - t
     tm = eng.timings()
-    print(json.dumps({"S": S, "bw": bw, "bits": bits, "wall_s": dt, "total_ms": tm["total_ms"],
-                      "assign_ms": [round(x, 4) for x in tm["assign_ms"]], "update_ms": [round(x, 4) for x in tm["update_ms"]],
+    print(json.dumps({"S": S, "bw": bw, "bits": bits, "wall_ms": round(dt * 1e3, 3), "total_ms": round(tm["total_ms"], 3),
+                      "assign_ms": [round(x, 4) for x in tm["assign_ms"]],
+                      "update_ms": [round(x, 4) for x in tm["update_ms"]],
                       "flagged": tm["flagged"], "host_ties": tm["host_ties"]}), flush=True)
