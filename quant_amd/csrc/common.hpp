@@ -5,6 +5,8 @@
 #include <cmath>
 #include <cstdint>
 
+#include "kdtree_dev.hpp"
+
 namespace qvq {
 
 // ---------------------------------------------------------------------------------------
@@ -66,22 +68,6 @@ __host__ __device__ inline double centroid_value(uint64_t hi, uint64_t lo, uint6
     return ldexp(i128_to_double(S), -scale) * (1.0 / (double)cnt);
 }
 
-// The reference build's nanoflann distance (kdtree.hpp, ref_l2): bit-identical.
-__device__ inline double ref_l2_dev(const double *a, const double *b, int dim) {
-    double r = 0;
-    int d = 0;
-    for (; d + 3 < dim; d += 4) {
-        const double e0 = a[d] - b[d], e1 = a[d + 1] - b[d + 1];
-        const double e2 = a[d + 2] - b[d + 2], e3 = a[d + 3] - b[d + 3];
-        r += (e1 * e1 + e2 * e2) + (e0 * e0 + e3 * e3);
-    }
-    for (; d < dim; d++) {
-        const double e = a[d] - b[d];
-        r += e * e;
-    }
-    return r;
-}
-
 // MFMA search layout (D = 12): per code vector one 56-byte row of 28 f16
 // [hi0..11, lo0..11, nhi, nlo, 0, 0], where hi+lo ~= -2*sx*(c-mu)*2^t and
 // nhi+nlo ~= 2^t*||c-mu||^2, so that score = 2^t*(||x-c||^2 - ||x-mu||^2).
@@ -115,11 +101,14 @@ hipError_t launch_assign_mfma(hipStream_t s, int grid, bool fuse, const uint8_t 
                               const _Float16 *cb_rows, uint32_t K, const float *C32, const uint64_t *plut,
                               const MfThresholds &th, uint32_t *A, uint32_t *flags, unsigned *flag_cnt,
                               uint64_t *part, uint32_t *part_cnt);
-// fp64 recheck of flagged rows; with sums != nullptr also adds the resolved rows' terms.
+// Deepest kd-tree the recheck's LDS stacks can hold (deeper: host resolution).
+int recheck_max_kd_depth();
+// fp64 recheck of flagged rows; exact ties go through the device kd-tree (kd.depth > 0) or
+// are listed in ties for the host.  With sums != nullptr adds every resolved row's terms.
 hipError_t launch_recheck(hipStream_t s, int num_cu, const uint8_t *codes, uint32_t Dp, uint32_t D,
                           const uint32_t *flags, const unsigned *flag_cnt, const double *C64, uint32_t K,
-                          const double *lut64, double tie_rel, uint32_t *A, uint32_t *ties, unsigned *tie_cnt,
-                          uint64_t *sums, const uint64_t *plut);
+                          const double *lut64, double tie_rel, const KdView &kd, uint32_t *A, uint32_t *ties,
+                          unsigned *tie_cnt, uint64_t *sums, const uint64_t *plut);
 hipError_t launch_update(hipStream_t s, uint32_t Dp, uint32_t G, const uint8_t *codes, uint64_t N, const uint32_t *A,
                          uint32_t K, uint32_t D, const uint64_t *plut, uint64_t *part, uint32_t *part_cnt);
 hipError_t launch_reduce(hipStream_t s, const uint64_t *part, const uint32_t *part_cnt, uint32_t G, uint32_t K,
@@ -133,10 +122,14 @@ hipError_t launch_prep(hipStream_t s, const double *C64, uint32_t K, uint32_t Kp
                        double mu, double sx, int t, float *C32, _Float16 *cb_rows);
 hipError_t launch_gather_codes(hipStream_t s, const uint8_t *codes, uint32_t Dp, const uint32_t *rows, uint32_t n,
                                uint8_t *out);
+// A[rows[i]] = vals[i]; sums[idx[j]] += val[j] (host tie resolutions).
 hipError_t launch_scatter(hipStream_t s, uint32_t *A, const uint32_t *rows, const uint32_t *vals, uint32_t n,
-                          const uint8_t *codes, uint32_t Dp, uint32_t D, uint32_t K, uint64_t *sums,
-                          const uint64_t *plut);
-hipError_t launch_distortion(hipStream_t s, const uint8_t *codes, uint64_t N, uint32_t D, uint32_t Dp,
-                             const uint32_t *A, const double *C, const double *lut64, double *partial, int grid);
+                          uint64_t *sums, const uint64_t *idx, const uint64_t *val, uint32_t nterms);
+// 256-bin histogram of the first D bytes of every row (hist zeroed first).
+hipError_t launch_byte_hist(hipStream_t s, const uint8_t *codes, uint64_t N, uint32_t D, uint32_t Dp,
+                            uint64_t *hist);
+// out[0] = sum_k (2 c_k.S_k - n_k ||c_k||^2) from the exact sums and the centroids C [K][D].
+hipError_t launch_distortion_cf(hipStream_t s, const uint64_t *sums, uint32_t K, uint32_t D, int64_t R, int64_t bias,
+                                int scale, const double *C, double *out);
 
 }  // namespace qvq

@@ -1,13 +1,18 @@
-// engine.cpp -- host side of the qvq engine: context, per-level schedule, host tie
-// resolution, RCCL exchange and the C ABI of include/qvq.h.  No kernels here; the HIP
-// kernels and their launch wrappers live in k_assign.hip and k_misc.hip.
+// engine.cpp -- host side of the qvq engine: context, per-level schedule, kd-tree builds,
+// RCCL exchange and the C ABI of include/qvq.h.  No kernels here; the HIP kernels and
+// their launch wrappers live in k_assign.hip and k_misc.hip.
 //
-// Per split level (LBGIterate, src/Quantizer.cpp:98-108, one effective Lloyd step):
-//   D == 12, K <= mf_fuse_max_k():  assign_mfma<fused sums> -> reduce -> recheck(+sums)
-//                                   -> [host kd-tree + scatter(+sums)] -> [all-reduce]
-//                                   -> finalize+split -> prep (next level's tables)
-//   otherwise:                      assign (MFMA or VALU) -> recheck -> [host] -> update
-//                                   -> reduce -> [all-reduce] -> finalize+split -> prep
+// Per split level (LBGIterate, src/Quantizer.cpp:98-108, one effective Lloyd step), all on
+// one stream with no host round trip:
+//   D == 12, K <= mf_fuse_max_k():  prep -> assign_mfma<fused sums> -> reduce
+//                                   -> recheck(+sums, device kd-tree for exact ties)
+//                                   -> [all-reduce] -> finalize+split
+//   otherwise:                      prep -> assign (MFMA or VALU) -> recheck -> update
+//                                   -> reduce -> [all-reduce] -> finalize+split
+// While the GPU runs a level's assign, the host builds the reference kd-tree over that
+// level's codebook (downloaded on a copy stream after the previous finalize) and uploads
+// it for the recheck.  A tree deeper than the device stack falls back to a synchronous
+// host resolution of the tie rows (resolve_host_ties).
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
@@ -82,7 +87,9 @@ struct qvq_ctx {
     double *d_lut64 = nullptr;
     uint64_t *d_plut = nullptr;
     uint32_t *d_A = nullptr, *d_flags = nullptr, *d_ties = nullptr;
-    unsigned *d_counters = nullptr;   // [0] flags, [1] ties
+    unsigned *d_counters = nullptr;   // per level: [2l] flagged rows, [2l+1] kd-tree ties
+    double xsq = 0;                   // sum over rows of ||x||^2 (closed-form distortion)
+    uint64_t *d_hist = nullptr;
 
     // level buffers
     uint32_t Kcap = 0;
@@ -95,6 +102,13 @@ struct qvq_ctx {
     double *d_dist_part = nullptr;
     uint32_t *d_scatter = nullptr;
     uint64_t scatter_bytes = 0;
+    double *h_cb = nullptr;            // pinned: the level's split codebook for the tree build
+    uint8_t *h_tree = nullptr, *d_tree = nullptr;   // flattened kd-tree (pinned / device)
+    uint64_t tree_cap = 0;
+
+    // copy stream and its hand-off events
+    hipStream_t cstream = nullptr;
+    hipEvent_t ev_fin = nullptr, ev_cb = nullptr, ev_rc = nullptr, ev_tree = nullptr;
 
     // multi-GPU
     ncclComm_t comm = nullptr;
@@ -136,7 +150,7 @@ void dfree(T *&p) {
 }
 
 uint32_t pad32(uint32_t K) { return (K + 31) & ~31u; }   // MFMA tile pairs
-// QVQ_SEARCH=valu|mfma and QVQ_FUSE=0 select paths for ablation benchmarks.
+// QVQ_SEARCH=valu, QVQ_FUSE=0 and QVQ_KDTREE=host select paths for ablations and tests.
 bool env_is(const char *name, const char *val) {
     const char *v = std::getenv(name);
     return v && std::strcmp(v, val) == 0;
@@ -165,7 +179,18 @@ void free_levels(qvq_ctx *ctx) {
     dfree(ctx->d_part);
     dfree(ctx->d_part_cnt);
     dfree(ctx->d_sums);
+    dfree(ctx->d_tree);
+    if (ctx->h_cb) (void)hipHostFree(ctx->h_cb);
+    if (ctx->h_tree) (void)hipHostFree(ctx->h_tree);
+    ctx->h_cb = nullptr;
+    ctx->h_tree = nullptr;
+    ctx->tree_cap = 0;
     ctx->Kcap = 0;
+}
+
+// Flattened tree: root box lo[D], hi[D] | nodes[2K] | vind[K].
+uint64_t tree_bytes(uint32_t K, uint32_t D) {
+    return 16ull * D + (2ull * K + 1) * sizeof(KdNodeDev) + 4ull * K;
 }
 
 // MFMA score scale and error bounds for the near-tie flag ("near-tie flags").
@@ -246,6 +271,10 @@ qvq_status ensure_levels(qvq_ctx *ctx, uint32_t Kmax) {
     HIPCHK(hipMalloc(&ctx->d_part, (uint64_t)ctx->G * KD * 8));
     HIPCHK(hipMalloc(&ctx->d_part_cnt, (uint64_t)ctx->G * Kmax * 4));
     HIPCHK(hipMalloc(&ctx->d_sums, (2 * KD + Kmax) * 8));
+    HIPCHK(hipHostMalloc(&ctx->h_cb, KD * 8, hipHostMallocDefault));
+    ctx->tree_cap = tree_bytes(Kmax, ctx->D);
+    HIPCHK(hipHostMalloc(&ctx->h_tree, ctx->tree_cap, hipHostMallocDefault));
+    HIPCHK(hipMalloc(&ctx->d_tree, ctx->tree_cap));
     ctx->Kcap = Kmax;
     return QVQ_OK;
 }
@@ -281,16 +310,49 @@ qvq_status run_update(qvq_ctx *ctx, const uint32_t *d_A, uint32_t K) {
     return QVQ_OK;
 }
 
-// Rows whose fp64 minimum is (nearly) shared: ask the reference kd-tree (kdtree.cpp).
-qvq_status resolve_host_ties(qvq_ctx *ctx, uint32_t K, uint32_t nt, bool accumulate) {
+// Build the reference kd-tree over the host copy hC of the K code vectors being searched
+// and upload it for the recheck (copy stream, ordered after the previous recheck).  Returns
+// an empty view (host resolution) when the tree is deeper than the device stack.
+qvq_status upload_tree(qvq_ctx *ctx, const double *hC, uint32_t K, KdView &kd) {
+    kd = KdView{};
+    if (env_is("QVQ_KDTREE", "host")) return QVQ_OK;
+    RefKDTree tree(hC, K, (int)ctx->D);
+    if (tree.depth() > recheck_max_kd_depth()) return QVQ_OK;
+    const uint32_t D = ctx->D;
+    double *lo = reinterpret_cast<double *>(ctx->h_tree), *hi = lo + D;
+    KdNodeDev *nodes = reinterpret_cast<KdNodeDev *>(hi + D);
+    uint32_t *vind = reinterpret_cast<uint32_t *>(nodes + tree.num_nodes());
+    tree.flatten(nodes, vind, lo, hi);
+    const uint64_t bytes = 16ull * D + tree.num_nodes() * sizeof(KdNodeDev) + 4ull * K;
+    HIPCHK(hipStreamWaitEvent(ctx->cstream, ctx->ev_rc, 0));
+    HIPCHK(hipMemcpyAsync(ctx->d_tree, ctx->h_tree, bytes, hipMemcpyHostToDevice, ctx->cstream));
+    HIPCHK(hipEventRecord(ctx->ev_tree, ctx->cstream));
+    HIPCHK(hipStreamWaitEvent(ctx->stream, ctx->ev_tree, 0));
+    const double *dlo = reinterpret_cast<const double *>(ctx->d_tree);
+    kd.lo = dlo;
+    kd.hi = dlo + D;
+    kd.nodes = reinterpret_cast<const KdNodeDev *>(dlo + 2 * D);
+    kd.vind = reinterpret_cast<const uint32_t *>(kd.nodes + tree.num_nodes());
+    kd.depth = tree.depth();
+    return QVQ_OK;
+}
+
+// After the finalize that produced the next level's K code vectors in d_C64_split: copy
+// them to h_cb on the copy stream (ev_cb marks completion).
+qvq_status download_codebook(qvq_ctx *ctx, uint32_t K) {
+    HIPCHK(hipEventRecord(ctx->ev_fin, ctx->stream));
+    HIPCHK(hipStreamWaitEvent(ctx->cstream, ctx->ev_fin, 0));
+    HIPCHK(hipMemcpyAsync(ctx->h_cb, ctx->d_C64_split, (uint64_t)K * ctx->D * 8, hipMemcpyDeviceToHost,
+                          ctx->cstream));
+    HIPCHK(hipEventRecord(ctx->ev_cb, ctx->cstream));
+    return QVQ_OK;
+}
+
+// Tie rows listed by the recheck when no device tree was available: answer them with the
+// host tree over hC, write A and (accumulate) add their terms to d_sums.  Synchronous.
+qvq_status resolve_host_ties(qvq_ctx *ctx, const double *hC, uint32_t K, uint32_t nt, bool accumulate) {
     const uint32_t D = ctx->D, Dp = ctx->Dp;
-    std::vector<uint32_t> rows(nt);
-    std::vector<double> C((uint64_t)K * D);
-    HIPCHK(hipMemcpyAsync(rows.data(), ctx->d_ties, nt * 4, hipMemcpyDeviceToHost, ctx->stream));
-    HIPCHK(hipMemcpyAsync(C.data(), ctx->d_C64_split, C.size() * 8, hipMemcpyDeviceToHost, ctx->stream));
-    HIPCHK(hipStreamSynchronize(ctx->stream));
-    std::sort(rows.begin(), rows.end());
-    const uint64_t need = (uint64_t)nt * (8 + Dp);   // rows | resolved indices | gathered codes
+    const uint64_t need = (uint64_t)nt * (8 + Dp) + 8 + (uint64_t)nt * (2 * D + 1) * 16;   // + (idx, val) terms
     if (ctx->scatter_bytes < need) {
         dfree(ctx->d_scatter);
         HIPCHK(hipMalloc(&ctx->d_scatter, need));
@@ -298,65 +360,93 @@ qvq_status resolve_host_ties(qvq_ctx *ctx, uint32_t K, uint32_t nt, bool accumul
     }
     uint32_t *d_rows = ctx->d_scatter, *d_vals = ctx->d_scatter + nt;
     uint8_t *d_gath = reinterpret_cast<uint8_t *>(ctx->d_scatter + 2 * (uint64_t)nt);
+    uint64_t *d_terms = reinterpret_cast<uint64_t *>(ctx->d_scatter) + ((uint64_t)nt * (8 + Dp) + 7) / 8;
+    std::vector<uint32_t> rows(nt), vals(nt);
     std::vector<uint8_t> code((uint64_t)nt * Dp);
-    HIPCHK(hipMemcpyAsync(d_rows, rows.data(), nt * 4, hipMemcpyHostToDevice, ctx->stream));
-    HIPCHK(launch_gather_codes(ctx->stream, ctx->d_codes, Dp, d_rows, nt, d_gath));
+    HIPCHK(launch_gather_codes(ctx->stream, ctx->d_codes, Dp, ctx->d_ties, nt, d_gath));
+    HIPCHK(hipMemcpyAsync(rows.data(), ctx->d_ties, nt * 4, hipMemcpyDeviceToHost, ctx->stream));
     HIPCHK(hipMemcpyAsync(code.data(), d_gath, code.size(), hipMemcpyDeviceToHost, ctx->stream));
     HIPCHK(hipStreamSynchronize(ctx->stream));
     std::vector<double> q(D);
-    std::vector<uint32_t> vals(nt);
-    RefKDTree tree(C.data(), K, (int)D);
+    RefKDTree tree(hC, K, (int)D);
+    std::vector<uint64_t> idx, val;
+    const uint64_t KD = (uint64_t)K * D;
     for (uint32_t i = 0; i < nt; i++) {
         for (uint32_t d = 0; d < D; d++) q[d] = ctx->terms.v64[code[(uint64_t)i * Dp + d]];
         vals[i] = tree.nearest(q.data());
+        if (accumulate) {
+            for (uint32_t d = 0; d < D; d++) {
+                const uint8_t c = code[(uint64_t)i * Dp + d];
+                idx.push_back((uint64_t)d * K + vals[i]);
+                val.push_back(ctx->terms.hi[c]);
+                idx.push_back(KD + (uint64_t)d * K + vals[i]);
+                val.push_back(ctx->terms.lo[c]);
+            }
+            idx.push_back(2 * KD + vals[i]);
+            val.push_back(1);
+        }
     }
+    const uint32_t nterms = (uint32_t)idx.size();
+    HIPCHK(hipMemcpyAsync(d_rows, rows.data(), nt * 4, hipMemcpyHostToDevice, ctx->stream));
     HIPCHK(hipMemcpyAsync(d_vals, vals.data(), nt * 4, hipMemcpyHostToDevice, ctx->stream));
-    HIPCHK(launch_scatter(ctx->stream, ctx->d_A, d_rows, d_vals, nt, ctx->d_codes, Dp, D, K,
-                          accumulate ? ctx->d_sums : nullptr, ctx->d_plut));
-    // vals/rows must outlive the async copies
-    HIPCHK(hipStreamSynchronize(ctx->stream));
+    if (nterms) {
+        HIPCHK(hipMemcpyAsync(d_terms, idx.data(), nterms * 8ull, hipMemcpyHostToDevice, ctx->stream));
+        HIPCHK(hipMemcpyAsync(d_terms + nterms, val.data(), nterms * 8ull, hipMemcpyHostToDevice, ctx->stream));
+    }
+    HIPCHK(launch_scatter(ctx->stream, ctx->d_A, d_rows, d_vals, nt, ctx->d_sums, d_terms, d_terms + nterms, nterms));
+    HIPCHK(hipStreamSynchronize(ctx->stream));   // the host vectors must outlive the copies
     return QVQ_OK;
 }
 
-// One level's assignment of every row against the split codebook (d_C64_split and the
-// tables from run_prep), K code vectors.  With sums_out the exact centroid sums of the
-// final assignment are left in d_sums (fused where possible).
-qvq_status run_level(qvq_ctx *ctx, uint32_t K, int slot, bool sums_out) {
+// One level's assignment of every row against the split codebook (d_C64_split, host copy
+// hC, tables from run_prep), K code vectors.  wait_cb: hC is being downloaded (ev_cb).
+// With sums_out the exact centroid sums of the final assignment are left in d_sums.
+qvq_status run_level(qvq_ctx *ctx, uint32_t K, int slot, bool sums_out, const double *hC, bool wait_cb) {
     const bool fused = sums_out && use_fused(ctx, K);
-    HIPCHK(hipMemsetAsync(ctx->d_counters, 0, 2 * sizeof(unsigned), ctx->stream));
-    if (slot >= 0) HIPCHK(hipEventRecord(ctx->ev[slot][0], ctx->stream));
+    unsigned *cnt = ctx->d_counters + 2 * slot;
+    HIPCHK(hipEventRecord(ctx->ev[slot][0], ctx->stream));
     if (use_mfma(ctx, K)) {
         HIPCHK(launch_assign_mfma(ctx->stream, ctx->num_cu, fused, ctx->d_codes, ctx->N, ctx->d_rows, K,
-                                  ctx->d_C32, ctx->d_plut, ctx->mf_th, ctx->d_A, ctx->d_flags,
-                                  &ctx->d_counters[0], ctx->d_part, ctx->d_part_cnt));
+                                  ctx->d_C32, ctx->d_plut, ctx->mf_th, ctx->d_A, ctx->d_flags, &cnt[0],
+                                  ctx->d_part, ctx->d_part_cnt));
     } else {
         float alpha, beta, gamma;
         valu_coeffs(ctx, alpha, beta, gamma);
         HIPCHK(launch_assign_valu(ctx->stream, ctx->num_cu, ctx->Dp, ctx->d_codes, ctx->N, ctx->d_C32, K,
-                                  ctx->d_lut32, alpha, beta, gamma, ctx->d_A, ctx->d_flags, &ctx->d_counters[0]));
+                                  ctx->d_lut32, alpha, beta, gamma, ctx->d_A, ctx->d_flags, &cnt[0]));
     }
-    if (slot >= 0) HIPCHK(hipEventRecord(ctx->ev[slot][1], ctx->stream));
+    HIPCHK(hipEventRecord(ctx->ev[slot][1], ctx->stream));
     if (fused) HIPCHK(launch_reduce(ctx->stream, ctx->d_part, ctx->d_part_cnt, ctx->num_cu, K, ctx->D, ctx->d_sums));
-    HIPCHK(launch_recheck(ctx->stream, ctx->num_cu, ctx->d_codes, ctx->Dp, ctx->D, ctx->d_flags, &ctx->d_counters[0],
-                          ctx->d_C64_split, K, ctx->d_lut64, 1e-12, ctx->d_A, ctx->d_ties, &ctx->d_counters[1],
+    // the tree build overlaps the search just enqueued
+    if (wait_cb) HIPCHK(hipEventSynchronize(ctx->ev_cb));
+    KdView kd;
+    qvq_status st = upload_tree(ctx, hC, K, kd);
+    if (st != QVQ_OK) return st;
+    HIPCHK(launch_recheck(ctx->stream, ctx->num_cu, ctx->d_codes, ctx->Dp, ctx->D, ctx->d_flags, &cnt[0],
+                          ctx->d_C64_split, K, ctx->d_lut64, 1e-12, kd, ctx->d_A, ctx->d_ties, &cnt[1],
                           fused ? ctx->d_sums : nullptr, ctx->d_plut));
-    unsigned counters[2];
-    HIPCHK(hipMemcpyAsync(counters, ctx->d_counters, sizeof(counters), hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(hipEventRecord(ctx->ev_rc, ctx->stream));
+    if (kd.depth == 0) {   // ties listed for the host
+        unsigned nt = 0;
+        HIPCHK(hipMemcpyAsync(&nt, &cnt[1], sizeof(nt), hipMemcpyDeviceToHost, ctx->stream));
+        HIPCHK(hipStreamSynchronize(ctx->stream));
+        if (nt && (st = resolve_host_ties(ctx, hC, K, nt, fused)) != QVQ_OK) return st;
+    }
+    HIPCHK(hipEventRecord(ctx->ev[slot][2], ctx->stream));
+    if (sums_out && !fused && (st = run_update(ctx, ctx->d_A, K)) != QVQ_OK) return st;
+    HIPCHK(hipEventRecord(ctx->ev[slot][3], ctx->stream));
+    return QVQ_OK;
+}
+
+// sum ||x||^2 over the resident rows, exactly from the byte histogram.
+qvq_status compute_xsq(qvq_ctx *ctx) {
+    uint64_t hist[256];
+    HIPCHK(launch_byte_hist(ctx->stream, ctx->d_codes, ctx->N, ctx->D, ctx->Dp, ctx->d_hist));
+    HIPCHK(hipMemcpyAsync(hist, ctx->d_hist, sizeof(hist), hipMemcpyDeviceToHost, ctx->stream));
     HIPCHK(hipStreamSynchronize(ctx->stream));
-    if (slot >= 0) {
-        ctx->tm.flagged[slot] = counters[0];
-        ctx->tm.host_ties[slot] = counters[1];
-    }
-    if (counters[1]) {
-        qvq_status st = resolve_host_ties(ctx, K, counters[1], fused);
-        if (st != QVQ_OK) return st;
-    }
-    if (slot >= 0) HIPCHK(hipEventRecord(ctx->ev[slot][2], ctx->stream));
-    if (sums_out && !fused) {
-        qvq_status st = run_update(ctx, ctx->d_A, K);
-        if (st != QVQ_OK) return st;
-    }
-    if (slot >= 0) HIPCHK(hipEventRecord(ctx->ev[slot][3], ctx->stream));
+    long double x = 0;
+    for (int b = 0; b < 256; b++) x += (long double)hist[b] * ctx->terms.v64[b] * ctx->terms.v64[b];
+    ctx->xsq = (double)x;
     return QVQ_OK;
 }
 
@@ -415,7 +505,11 @@ QVQ_API qvq_status qvq_create(int hip_device, qvq_ctx **out) {
     if ((e = hipMalloc(&ctx->d_w, 256 * 4)) != hipSuccess) return bail(e, "hipMalloc");
     if ((e = hipMalloc(&ctx->d_lut64, 256 * 8)) != hipSuccess) return bail(e, "hipMalloc");
     if ((e = hipMalloc(&ctx->d_plut, 256 * 8)) != hipSuccess) return bail(e, "hipMalloc");
-    if ((e = hipMalloc(&ctx->d_counters, 4 * sizeof(unsigned))) != hipSuccess) return bail(e, "hipMalloc");
+    if ((e = hipStreamCreateWithFlags(&ctx->cstream, hipStreamNonBlocking)) != hipSuccess) return bail(e, "stream");
+    for (hipEvent_t *ev : {&ctx->ev_fin, &ctx->ev_cb, &ctx->ev_rc, &ctx->ev_tree})
+        if ((e = hipEventCreateWithFlags(ev, hipEventDisableTiming)) != hipSuccess) return bail(e, "hipEventCreate");
+    if ((e = hipMalloc(&ctx->d_counters, 2 * 33 * sizeof(unsigned))) != hipSuccess) return bail(e, "hipMalloc");
+    if ((e = hipMalloc(&ctx->d_hist, 256 * 8)) != hipSuccess) return bail(e, "hipMalloc");
     if ((e = hipMalloc(&ctx->d_dist_part, 4096 * 8)) != hipSuccess) return bail(e, "hipMalloc");
     for (int l = 0; l < 32; l++)
         for (int j = 0; j < 4; j++)
@@ -429,6 +523,7 @@ QVQ_API void qvq_destroy(qvq_ctx *ctx) {
     if (!ctx) return;
     (void)hipSetDevice(ctx->dev);
     if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+    if (ctx->cstream) (void)hipStreamSynchronize(ctx->cstream);
     if (ctx->comm) ncclCommDestroy(ctx->comm);
     free_training(ctx);
     free_levels(ctx);
@@ -437,6 +532,10 @@ QVQ_API void qvq_destroy(qvq_ctx *ctx) {
     dfree(ctx->d_lut64);
     dfree(ctx->d_plut);
     dfree(ctx->d_counters);
+    dfree(ctx->d_hist);
+    for (hipEvent_t ev : {ctx->ev_fin, ctx->ev_cb, ctx->ev_rc, ctx->ev_tree})
+        if (ev) (void)hipEventDestroy(ev);
+    if (ctx->cstream) (void)hipStreamDestroy(ctx->cstream);
     dfree(ctx->d_dist_part);
     dfree(ctx->d_scatter);
     if (ctx->ev_ready)
@@ -460,8 +559,7 @@ QVQ_API qvq_status qvq_set_images_device(qvq_ctx *ctx, const void *d_rgb, uint32
     HIPCHK(hipSetDevice(ctx->dev));
     if ((st = alloc_training(ctx, N, D, colorspace)) != QVQ_OK) return st;
     if ((st = tile_into(ctx, (const uint8_t *)d_rgb, n_images, xSize, ySize, bw, bh)) != QVQ_OK) return st;
-    HIPCHK(hipStreamSynchronize(ctx->stream));
-    return QVQ_OK;
+    return compute_xsq(ctx);
 }
 
 QVQ_API qvq_status qvq_set_images(qvq_ctx *ctx, const uint8_t *rgb, uint32_t n_images, uint32_t xSize, uint32_t ySize,
@@ -480,6 +578,7 @@ QVQ_API qvq_status qvq_set_images(qvq_ctx *ctx, const uint8_t *rgb, uint32_t n_i
     if (e != hipSuccess) st = fail(ctx, QVQ_EDEVICE, std::string("raster upload: ") + hipGetErrorString(e));
     if (st == QVQ_OK) st = alloc_training(ctx, N, D, colorspace);
     if (st == QVQ_OK) st = tile_into(ctx, d_rgb, n_images, xSize, ySize, bw, bh);
+    if (st == QVQ_OK) st = compute_xsq(ctx);
     (void)hipStreamSynchronize(ctx->stream);
     (void)hipFree(d_rgb);
     return st;
@@ -502,6 +601,7 @@ QVQ_API qvq_status qvq_set_synthetic(qvq_ctx *ctx, uint32_t S, uint64_t seed0, u
     if (e != hipSuccess) st = fail(ctx, QVQ_EDEVICE, std::string("gen_kernel: ") + hipGetErrorString(e));
     if (st == QVQ_OK) st = alloc_training(ctx, N, D, colorspace);
     if (st == QVQ_OK) st = tile_into(ctx, d_rgb, n_images, S, S, bw, bh);
+    if (st == QVQ_OK) st = compute_xsq(ctx);
     (void)hipStreamSynchronize(ctx->stream);
     (void)hipFree(d_rgb);
     return st;
@@ -546,7 +646,7 @@ QVQ_API qvq_status qvq_set_vectors(qvq_ctx *ctx, const double *X, uint64_t n, ui
     qvq_status st = alloc_training(ctx, n, dim, cs_found);
     if (st != QVQ_OK) return st;
     HIPCHK(hipMemcpy(ctx->d_codes, codes.data(), codes.size(), hipMemcpyHostToDevice));
-    return QVQ_OK;
+    return compute_xsq(ctx);
 }
 
 QVQ_API qvq_status qvq_lbg(qvq_ctx *ctx, uint32_t bits, double eps, double *codebook, uint32_t *assign,
@@ -563,47 +663,46 @@ QVQ_API qvq_status qvq_lbg(qvq_ctx *ctx, uint32_t bits, double eps, double *code
     std::memset(&ctx->tm, 0, sizeof(ctx->tm));
     ctx->tm.levels = (int)bits;
     const Terms &T = ctx->terms;
+    HIPCHK(hipMemsetAsync(ctx->d_counters, 0, 2 * 33 * sizeof(unsigned), ctx->stream));
+    HIPCHK(hipEventRecord(ctx->ev_rc, ctx->stream));
+    // [sum ||x||^2, rows] over all ranks, for the closed-form distortion
+    double *d_dist = ctx->d_dist_part;
+    double xn[2] = {ctx->xsq, (double)ctx->N};
+    HIPCHK(hipMemcpy(d_dist, xn, sizeof(xn), hipMemcpyHostToDevice));
+    if (ctx->comm) NCCLCHK(ncclAllReduce(d_dist, d_dist, 2, ncclDouble, ncclSum, ctx->comm, ctx->stream));
 
     // codeVectors[0] = trainingSetSum() / N, then the first split (src/Quantizer.cpp:129-138)
     HIPCHK(launch_mean_sums(ctx->stream, ctx->Dp, ctx->d_codes, ctx->N, ctx->D, ctx->d_plut, ctx->d_sums));
     if ((st = all_reduce_sums(ctx, 1)) != QVQ_OK) return st;
     HIPCHK(launch_finalize(ctx->stream, ctx->d_sums, 1, ctx->D, T.R, T.bias, T.scale, ctx->d_C64_cent, bits > 0,
                            ctx->d_C64_split));
+    if (bits > 0 && (st = download_codebook(ctx, 2)) != QVQ_OK) return st;
     HIPCHK(hipMemsetAsync(ctx->d_A, 0, ctx->N * 4, ctx->stream));
 
     for (uint32_t lvl = 1; lvl <= bits; lvl++) {
         const uint32_t K = 1u << lvl;
         const int slot = (int)lvl - 1;
         if ((st = run_prep(ctx, K)) != QVQ_OK) return st;
-        if ((st = run_level(ctx, K, slot, true)) != QVQ_OK) return st;
+        if ((st = run_level(ctx, K, slot, true, ctx->h_cb, true)) != QVQ_OK) return st;
         if ((st = all_reduce_sums(ctx, K)) != QVQ_OK) return st;
         HIPCHK(launch_finalize(ctx->stream, ctx->d_sums, K, ctx->D, T.R, T.bias, T.scale, ctx->d_C64_cent, lvl < bits,
                                ctx->d_C64_split));
+        if (lvl < bits && (st = download_codebook(ctx, 2 * K)) != QVQ_OK) return st;
     }
-    // Returned distortion: updateDistortion after the last fix (src/Quantizer.cpp:9-22,103)
-    const int dgrid = (int)std::min<uint64_t>((ctx->N + 255) / 256, 4096);
-    HIPCHK(launch_distortion(ctx->stream, ctx->d_codes, ctx->N, ctx->D, ctx->Dp, ctx->d_A, ctx->d_C64_cent,
-                             ctx->d_lut64, ctx->d_dist_part, dgrid));
-    std::vector<double> dpart(dgrid);
-    HIPCHK(hipMemcpyAsync(dpart.data(), ctx->d_dist_part, dgrid * 8, hipMemcpyDeviceToHost, ctx->stream));
+    // Returned distortion: updateDistortion after the last fix (src/Quantizer.cpp:9-22,103),
+    // from the sums of the final assignment (k_misc.hip, distortion_cf_kernel).
+    HIPCHK(launch_distortion_cf(ctx->stream, ctx->d_sums, Kmax, ctx->D, T.R, T.bias, T.scale, ctx->d_C64_cent,
+                                d_dist + 2));
+    double dres[3];
+    unsigned stats[2 * 33];
+    HIPCHK(hipMemcpyAsync(dres, d_dist, sizeof(dres), hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(hipMemcpyAsync(stats, ctx->d_counters, sizeof(stats), hipMemcpyDeviceToHost, ctx->stream));
     if (codebook)
         HIPCHK(hipMemcpyAsync(codebook, ctx->d_C64_cent, (uint64_t)Kmax * ctx->D * 8, hipMemcpyDeviceToHost,
                               ctx->stream));
     if (assign) HIPCHK(hipMemcpyAsync(assign, ctx->d_A, ctx->N * 4, hipMemcpyDeviceToHost, ctx->stream));
     HIPCHK(hipStreamSynchronize(ctx->stream));
-    double dsum = 0;
-    for (double v : dpart) dsum += v;
-    double ntot = (double)ctx->N;
-    if (ctx->comm) {
-        double host2[2] = {dsum, ntot};
-        HIPCHK(hipMemcpy(ctx->d_dist_part, host2, 16, hipMemcpyHostToDevice));
-        NCCLCHK(ncclAllReduce(ctx->d_dist_part, ctx->d_dist_part, 2, ncclDouble, ncclSum, ctx->comm, ctx->stream));
-        HIPCHK(hipMemcpyAsync(host2, ctx->d_dist_part, 16, hipMemcpyDeviceToHost, ctx->stream));
-        HIPCHK(hipStreamSynchronize(ctx->stream));
-        dsum = host2[0];
-        ntot = host2[1];
-    }
-    if (distortion) *distortion = dsum / (ntot * (double)ctx->D);
+    if (distortion) *distortion = (dres[0] - dres[2]) / (dres[1] * (double)ctx->D);
     for (uint32_t lvl = 1; lvl <= bits; lvl++) {
         float a = 0, u = 0, o = 0;
         (void)hipEventElapsedTime(&a, ctx->ev[lvl - 1][0], ctx->ev[lvl - 1][1]);
@@ -612,6 +711,8 @@ QVQ_API qvq_status qvq_lbg(qvq_ctx *ctx, uint32_t bits, double eps, double *code
         ctx->tm.assign_ms[lvl - 1] = a;
         ctx->tm.other_ms[lvl - 1] = o;
         ctx->tm.update_ms[lvl - 1] = u;
+        ctx->tm.flagged[lvl - 1] = stats[2 * (lvl - 1)];
+        ctx->tm.host_ties[lvl - 1] = stats[2 * (lvl - 1) + 1];
     }
     ctx->tm.total_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     return QVQ_OK;
@@ -626,9 +727,17 @@ QVQ_API qvq_status qvq_assign(qvq_ctx *ctx, const double *C, uint32_t K, uint32_
     if (st != QVQ_OK) return st;
     std::memset(&ctx->tm, 0, sizeof(ctx->tm));
     HIPCHK(hipMemcpy(ctx->d_C64_split, C, (uint64_t)K * ctx->D * 8, hipMemcpyHostToDevice));
+    HIPCHK(hipMemsetAsync(ctx->d_counters, 0, 2 * sizeof(unsigned), ctx->stream));
+    HIPCHK(hipEventRecord(ctx->ev_rc, ctx->stream));
     if ((st = run_prep(ctx, K)) != QVQ_OK) return st;
-    if ((st = run_level(ctx, K, 0, false)) != QVQ_OK) return st;
-    if (assign) HIPCHK(hipMemcpy(assign, ctx->d_A, ctx->N * 4, hipMemcpyDeviceToHost));
+    if ((st = run_level(ctx, K, 0, false, C, false)) != QVQ_OK) return st;
+    unsigned stats[2];
+    HIPCHK(hipMemcpyAsync(stats, ctx->d_counters, sizeof(stats), hipMemcpyDeviceToHost, ctx->stream));
+    if (assign) HIPCHK(hipMemcpyAsync(assign, ctx->d_A, ctx->N * 4, hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+    ctx->tm.levels = 1;
+    ctx->tm.flagged[0] = stats[0];
+    ctx->tm.host_ties[0] = stats[1];
     return QVQ_OK;
 }
 

@@ -513,25 +513,52 @@ hipError_t launch_assign_valu(hipStream_t s, int num_cu, uint32_t Dp, const uint
 // within tie_rel go to the host kd-tree.  With sums != nullptr the resolved rows' exact
 // terms are added to the global sums (the fused search skipped them).
 constexpr int RECHECK_THREADS = 512;
-constexpr int RECHECK_LDS = 150 * 1024;
+constexpr int RECHECK_WAVES = RECHECK_THREADS / 64;
+constexpr size_t RECHECK_LDS = 160 * 1024;
 
+// Codebook rows in LDS use an odd stride (in doubles), so the 32 lanes of a ds_read_b64
+// group, each on a different code vector, hit different banks.
+__host__ __device__ inline uint32_t recheck_stride(uint32_t D) { return D | 1u; }
+
+// LDS of the recheck without the staged codebook: row + traversal dists, kd stacks.
+size_t recheck_lds_base(int depth) {
+    return (size_t)RECHECK_WAVES * 128 * 8 + (((size_t)RECHECK_WAVES * depth * KD_FRAME_BYTES + 7) & ~(size_t)7);
+}
+
+int recheck_max_kd_depth() {
+    return (int)((RECHECK_LDS - (size_t)RECHECK_WAVES * 128 * 8) / ((size_t)RECHECK_WAVES * KD_FRAME_BYTES));
+}
+
+// fp64 recheck of flagged rows in the reference's distance order.  Rows whose best and
+// second distances are within tie_rel are exact ties for the reference: with a device tree
+// they are answered by its traversal here, otherwise listed for the host (ties).
+template <bool STAGED>
 __global__ __launch_bounds__(RECHECK_THREADS) void recheck_kernel(
     const uint8_t *__restrict__ codes, uint32_t Dp, uint32_t D, const uint32_t *__restrict__ flags,
-    const unsigned int *__restrict__ flag_cnt, const double *__restrict__ g_C64, uint32_t K, bool staged,
-    const double *__restrict__ lut64, double tie_rel, uint32_t *__restrict__ A, uint32_t *__restrict__ ties,
-    unsigned int *__restrict__ tie_cnt, uint64_t *__restrict__ sums, const uint64_t *__restrict__ plut) {
+    const unsigned int *__restrict__ flag_cnt, const double *__restrict__ g_C64, uint32_t K,
+    const double *__restrict__ lut64, double tie_rel, KdView kd, uint32_t *__restrict__ A,
+    uint32_t *__restrict__ ties, unsigned int *__restrict__ tie_cnt, uint64_t *__restrict__ sums,
+    const uint64_t *__restrict__ plut) {
     extern __shared__ __attribute__((aligned(16))) double rsm[];
-    constexpr int W = RECHECK_THREADS / 64;
-    double *xs = rsm;                      // [W][64]
-    double *cbs = rsm + W * 64;            // [K][D] when staged
+    constexpr int W = RECHECK_WAVES;
+    const int Z = kd.depth;                                         // stack frames per wave
+    double *xs = rsm;                                               // [W][64]
+    double *kdd = xs + W * 64;                                      // [W][64] traversal dists
+    double *sd = kdd + W * 64;                                      // [W][Z]
+    int32_t *sn = reinterpret_cast<int32_t *>(sd + W * Z);          // [W][Z]
+    double *cbs = rsm + W * 128 + ((size_t)W * Z * KD_FRAME_BYTES + 7) / 8;   // [K][stride] when staged
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const unsigned nflag = *flag_cnt;
     if (nflag == 0) return;
-    if (staged) {
-        for (uint32_t i = threadIdx.x; i < K * D; i += RECHECK_THREADS) cbs[i] = g_C64[i];
+    const uint32_t S = STAGED ? recheck_stride(D) : D;
+    if (STAGED) {
+        for (uint32_t i = threadIdx.x; i < K * D; i += RECHECK_THREADS) {
+            const uint32_t k = i / D, d = i - k * D;
+            cbs[k * S + d] = g_C64[i];
+        }
         __syncthreads();
     }
-    const double *C64 = staged ? cbs : g_C64;
+    const double *C64 = STAGED ? cbs : g_C64;
     for (unsigned base = blockIdx.x * W; base < nflag; base += gridDim.x * W) {
         const unsigned f = base + wave;
         const bool active = f < nflag;
@@ -543,7 +570,7 @@ __global__ __launch_bounds__(RECHECK_THREADS) void recheck_kernel(
         double d1 = INFINITY, d2 = INFINITY;
         uint32_t k1 = 0xFFFFFFFFu;
         for (uint32_t k = lane; k < K; k += 64) {
-            const double d = ref_l2_dev(xs + wave * 64, C64 + (uint64_t)k * D, D);
+            const double d = ref_l2_hd(xs + wave * 64, C64 + (uint64_t)k * S, D);
             if (d < d1) {
                 d2 = d1;
                 d1 = d;
@@ -566,11 +593,23 @@ __global__ __launch_bounds__(RECHECK_THREADS) void recheck_kernel(
             }
         }
         const bool tie = d2 - d1 <= tie_rel * d1;
-        if (lane == 0) {
-            A[row] = k1;
-            if (tie) ties[atomicAdd(tie_cnt, 1u)] = row;
+        if (tie) {
+            if (kd.depth > 0) {
+                uint32_t kk = 0;
+                if (lane == 0)
+                    kk = kd_nearest_flat(xs + wave * 64, D, kd, C64, S, sd + wave * Z, sn + wave * Z, kdd + wave * 64);
+                k1 = __shfl(kk, 0);
+                if (lane == 0) atomicAdd(tie_cnt, 1u);
+            } else {
+                if (lane == 0) {
+                    A[row] = k1;
+                    ties[atomicAdd(tie_cnt, 1u)] = row;
+                }
+                continue;   // the host adds this row (resolve_host_ties)
+            }
         }
-        if (sums && !tie && lane < (int)D) {
+        if (lane == 0) A[row] = k1;
+        if (sums && lane < (int)D) {
             const uint64_t KD = (uint64_t)K * D;
             const uint64_t p = plut[codes[(uint64_t)row * Dp + lane]];
             atomicAdd((unsigned long long *)&sums[(uint64_t)lane * K + k1], (unsigned long long)(p >> 32));
@@ -582,13 +621,19 @@ __global__ __launch_bounds__(RECHECK_THREADS) void recheck_kernel(
 
 hipError_t launch_recheck(hipStream_t s, int num_cu, const uint8_t *codes, uint32_t Dp, uint32_t D,
                           const uint32_t *flags, const unsigned *flag_cnt, const double *C64, uint32_t K,
-                          const double *lut64, double tie_rel, uint32_t *A, uint32_t *ties, unsigned *tie_cnt,
-                          uint64_t *sums, const uint64_t *plut) {
-    const size_t base = (size_t)(RECHECK_THREADS / 64) * 64 * 8;
-    const bool staged = base + (size_t)K * D * 8 <= RECHECK_LDS;
-    const size_t lds = base + (staged ? (size_t)K * D * 8 : 0);
-    hipLaunchKernelGGL(recheck_kernel, dim3(num_cu), dim3(RECHECK_THREADS), lds, s, codes, Dp, D, flags, flag_cnt,
-                       C64, K, staged, lut64, tie_rel, A, ties, tie_cnt, sums, plut);
+                          const double *lut64, double tie_rel, const KdView &kd, uint32_t *A, uint32_t *ties,
+                          unsigned *tie_cnt, uint64_t *sums, const uint64_t *plut) {
+    const size_t base = recheck_lds_base(kd.depth);
+    if (base > RECHECK_LDS) return hipErrorInvalidValue;
+    const size_t cb = (size_t)K * recheck_stride(D) * 8;
+    const bool staged = base + cb <= RECHECK_LDS;
+    const size_t lds = base + (staged ? cb : 0);
+    if (staged)
+        hipLaunchKernelGGL(recheck_kernel<true>, dim3(num_cu), dim3(RECHECK_THREADS), lds, s, codes, Dp, D, flags,
+                           flag_cnt, C64, K, lut64, tie_rel, kd, A, ties, tie_cnt, sums, plut);
+    else
+        hipLaunchKernelGGL(recheck_kernel<false>, dim3(num_cu), dim3(RECHECK_THREADS), lds, s, codes, Dp, D, flags,
+                           flag_cnt, C64, K, lut64, tie_rel, kd, A, ties, tie_cnt, sums, plut);
     return hipGetLastError();
 }
 

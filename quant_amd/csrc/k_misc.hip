@@ -351,64 +351,87 @@ hipError_t launch_gather_codes(hipStream_t s, const uint8_t *codes, uint32_t Dp,
     return hipGetLastError();
 }
 
-// A[rows[i]] = vals[i] (host tie resolutions); with sums, also add those rows' terms.
+// A[rows[i]] = vals[i] (host tie resolutions).
 __global__ void scatter_kernel(uint32_t *__restrict__ A, const uint32_t *__restrict__ rows,
-                               const uint32_t *__restrict__ vals, uint32_t n, const uint8_t *__restrict__ codes,
-                               uint32_t Dp, uint32_t D, uint32_t K, uint64_t *__restrict__ sums,
-                               const uint64_t *__restrict__ plut) {
-    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
-        const uint32_t r = rows[i], k = vals[i];
-        A[r] = k;
-        if (sums) {
-            const uint64_t KD = (uint64_t)K * D;
-            for (uint32_t d = 0; d < D; d++) {
-                const uint64_t p = plut[codes[(uint64_t)r * Dp + d]];
-                atomicAdd((unsigned long long *)&sums[(uint64_t)d * K + k], (unsigned long long)(p >> 32));
-                atomicAdd((unsigned long long *)&sums[KD + (uint64_t)d * K + k], (unsigned long long)(p & 0xFFFFFFFFull));
-            }
-            atomicAdd((unsigned long long *)&sums[2 * KD + k], 1ull);
-        }
-    }
+                               const uint32_t *__restrict__ vals, uint32_t n) {
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) A[rows[i]] = vals[i];
+}
+
+// sums[idx[i]] += val[i] (host-aggregated terms of the tie rows, one entry per touched word).
+__global__ void add_terms_kernel(uint64_t *__restrict__ sums, const uint64_t *__restrict__ idx,
+                                 const uint64_t *__restrict__ val, uint32_t n) {
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x)
+        atomicAdd((unsigned long long *)&sums[idx[i]], (unsigned long long)val[i]);
 }
 
 hipError_t launch_scatter(hipStream_t s, uint32_t *A, const uint32_t *rows, const uint32_t *vals, uint32_t n,
-                          const uint8_t *codes, uint32_t Dp, uint32_t D, uint32_t K, uint64_t *sums,
-                          const uint64_t *plut) {
-    hipLaunchKernelGGL(scatter_kernel, dim3((n + 255) / 256), dim3(256), 0, s, A, rows, vals, n, codes, Dp, D, K, sums,
-                       plut);
+                          uint64_t *sums, const uint64_t *idx, const uint64_t *val, uint32_t nterms) {
+    if (n) hipLaunchKernelGGL(scatter_kernel, dim3((n + 255) / 256), dim3(256), 0, s, A, rows, vals, n);
+    if (nterms)
+        hipLaunchKernelGGL(add_terms_kernel, dim3((nterms + 255) / 256), dim3(256), 0, s, sums, idx, val, nterms);
     return hipGetLastError();
 }
 
-// Sum over rows of norm(x - c_A(x)) (src/Quantizer.cpp:9-22), one partial per workgroup.
-constexpr int DIST_THREADS = 256;
-__global__ __launch_bounds__(DIST_THREADS) void distortion_kernel(
-    const uint8_t *__restrict__ codes, uint64_t N, uint32_t D, uint32_t Dp, const uint32_t *__restrict__ A,
-    const double *__restrict__ C, const double *__restrict__ lut64, double *__restrict__ partial) {
-    __shared__ double red[DIST_THREADS];
-    double s = 0;
-    for (uint64_t row = blockIdx.x * (uint64_t)DIST_THREADS + threadIdx.x; row < N;
-         row += (uint64_t)gridDim.x * DIST_THREADS) {
-        const double *c = C + (uint64_t)A[row] * D;
-        const uint8_t *x = codes + row * Dp;
-        double r = 0;
-        for (uint32_t d = 0; d < D; d++) {
-            const double e = lut64[x[d]] - c[d];
-            r += e * e;
-        }
-        s += r;
-    }
-    red[threadIdx.x] = s;
+// Histogram of the bytes of the first D components of every row (for sum ||x||^2).
+__global__ void byte_hist_kernel(const uint8_t *__restrict__ codes, uint64_t N, uint32_t D, uint32_t Dp,
+                                 unsigned long long *__restrict__ hist) {
+    __shared__ uint32_t h[256];
+    h[threadIdx.x] = 0;
     __syncthreads();
-    for (int w = DIST_THREADS / 2; w > 0; w >>= 1) {
+    const uint64_t total = N * Dp;
+    for (uint64_t i = (blockIdx.x * (uint64_t)blockDim.x + threadIdx.x) * 4; i < total;
+         i += (uint64_t)gridDim.x * blockDim.x * 4) {
+        const uint32_t w = *(const uint32_t *)(codes + i);   // Dp is a multiple of 4
+        const uint32_t d0 = (uint32_t)(i % Dp);
+#pragma unroll
+        for (int j = 0; j < 4; j++)
+            if (d0 + j < D) atomicAdd(&h[(w >> (8 * j)) & 0xFF], 1u);
+    }
+    __syncthreads();
+    if (h[threadIdx.x]) atomicAdd(&hist[threadIdx.x], (unsigned long long)h[threadIdx.x]);
+}
+
+hipError_t launch_byte_hist(hipStream_t s, const uint8_t *codes, uint64_t N, uint32_t D, uint32_t Dp,
+                            uint64_t *hist) {
+    hipError_t e = hipMemsetAsync(hist, 0, 256 * 8, s);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(byte_hist_kernel, dim3(1024), dim3(256), 0, s, codes, N, D, Dp, (unsigned long long *)hist);
+    return hipGetLastError();
+}
+
+// updateDistortion (src/Quantizer.cpp:9-22) in closed form from the exact sums of the final
+// assignment: sum_i ||x_i - c_A(i)||^2 = sum_i ||x_i||^2 - sum_k (2 c_k.S_k - n_k ||c_k||^2).
+// One workgroup, fixed-order tree; out[0] = the subtracted sum.
+constexpr int DCF_THREADS = 1024;
+__global__ __launch_bounds__(DCF_THREADS) void distortion_cf_kernel(const uint64_t *__restrict__ sums, uint32_t K,
+                                                                    uint32_t D, int64_t R, int64_t bias, int scale,
+                                                                    const double *__restrict__ C,
+                                                                    double *__restrict__ out) {
+    __shared__ double red[DCF_THREADS];
+    const uint64_t KD = (uint64_t)K * D;
+    double acc = 0;
+    for (uint64_t t = threadIdx.x; t < KD; t += DCF_THREADS) {
+        const uint64_t k = t / D, d = t - k * D, col = d * K + k;
+        const uint64_t n = sums[2 * KD + k];
+        if (n == 0) continue;
+        const __int128 Sq =
+            (__int128)R * (__int128)sums[col] + (__int128)sums[KD + col] - (__int128)bias * (__int128)n;
+        const double S = ldexp(i128_to_double(Sq), -scale);
+        const double c = C[t];
+        acc += 2.0 * c * S - (double)n * c * c;
+    }
+    red[threadIdx.x] = acc;
+    __syncthreads();
+    for (int w = DCF_THREADS / 2; w > 0; w >>= 1) {
         if ((int)threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
         __syncthreads();
     }
-    if (threadIdx.x == 0) partial[blockIdx.x] = red[0];
+    if (threadIdx.x == 0) out[0] = red[0];
 }
 
-hipError_t launch_distortion(hipStream_t s, const uint8_t *codes, uint64_t N, uint32_t D, uint32_t Dp,
-                             const uint32_t *A, const double *C, const double *lut64, double *partial, int grid) {
-    hipLaunchKernelGGL(distortion_kernel, dim3(grid), dim3(DIST_THREADS), 0, s, codes, N, D, Dp, A, C, lut64, partial);
+hipError_t launch_distortion_cf(hipStream_t s, const uint64_t *sums, uint32_t K, uint32_t D, int64_t R, int64_t bias,
+                                int scale, const double *C, double *out) {
+    hipLaunchKernelGGL(distortion_cf_kernel, dim3(1), dim3(DCF_THREADS), 0, s, sums, K, D, R, bias, scale, C, out);
     return hipGetLastError();
 }
 

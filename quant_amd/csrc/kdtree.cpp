@@ -1,8 +1,8 @@
 // See kdtree.hpp.  Build: nanoflann.hpp:863-871 (buildIndex), :1014-1036 (bounding box),
 // :1046-1094 (divideTree), :1108-1147 (middleSplit_), :1159-1186 (planeSplit).
-// Search: :906-920 (findNeighbors), :1188-1205 (initial distances), :1212-1270
-// (searchLevel) with KNNResultSet capacity 1 (:77-138): strict '<' everywhere, so among
-// equal distances the first point visited wins.
+// Search (kdtree_dev.hpp, kd_nearest_flat): :906-920 (findNeighbors), :1188-1205 (initial
+// distances), :1212-1270 (searchLevel) with KNNResultSet capacity 1 (:77-138): strict '<'
+// everywhere, so among equal distances the first point visited wins.
 #include "kdtree.hpp"
 
 #include <algorithm>
@@ -10,20 +10,7 @@
 
 namespace qvq {
 
-double ref_l2(const double *a, const double *b, int dim) {
-    double r = 0;
-    int d = 0;
-    for (; d + 3 < dim; d += 4) {
-        const double e0 = a[d] - b[d], e1 = a[d + 1] - b[d + 1];
-        const double e2 = a[d + 2] - b[d + 2], e3 = a[d + 3] - b[d + 3];
-        r += (e1 * e1 + e2 * e2) + (e0 * e0 + e3 * e3);
-    }
-    for (; d < dim; d++) {
-        const double e = a[d] - b[d];
-        r += e * e;
-    }
-    return r;
-}
+double ref_l2(const double *a, const double *b, int dim) { return ref_l2_hd(a, b, dim); }
 
 RefKDTree::RefKDTree(const double *pts, size_t K, int dim) : pts_(pts), dim_(dim) {
     vind_.resize(K);
@@ -37,7 +24,11 @@ RefKDTree::RefKDTree(const double *pts, size_t K, int dim) : pts_(pts), dim_(dim
             if (v > root_bbox_[d].high) root_bbox_[d].high = v;
         }
     nodes_.reserve(2 * (K / 5 + 1));
-    divide(0, K, root_bbox_);
+    divide(0, K, root_bbox_, 1);
+    flat_nodes_.resize(nodes_.size());
+    flat_vind_.resize(K);
+    flat_box_.resize(2 * (size_t)dim);
+    flatten(flat_nodes_.data(), flat_vind_.data(), flat_box_.data(), flat_box_.data() + dim);
 }
 
 void RefKDTree::min_max(const size_t *ind, size_t count, int e, double &mn, double &mx) const {
@@ -105,8 +96,9 @@ void RefKDTree::middle_split(size_t *ind, size_t count, size_t &index, int &cutf
 }
 
 // bbox is in/out: the caller's cell box on entry, the node's actual point box on exit.
-int RefKDTree::divide(size_t left, size_t right, std::vector<Box> &bbox) {
+int RefKDTree::divide(size_t left, size_t right, std::vector<Box> &bbox, int level) {
     const int me = (int)nodes_.size();
+    depth_ = std::max(depth_, level);
     nodes_.push_back(Node());
     if (right - left <= 10) {   // leaf_max_size (KDTreeVectorOfVectorsAdaptor.hpp:59)
         Node &n = nodes_[me];
@@ -129,10 +121,10 @@ int RefKDTree::divide(size_t left, size_t right, std::vector<Box> &bbox) {
     middle_split(vind_.data() + left, right - left, idx, cutfeat, cutval, bbox);
     std::vector<Box> lb(bbox), rb;
     lb[cutfeat].high = cutval;
-    const int c1 = divide(left, left + idx, lb);
+    const int c1 = divide(left, left + idx, lb, level + 1);
     rb = bbox;
     rb[cutfeat].low = cutval;
-    const int c2 = divide(left + idx, right, rb);
+    const int c2 = divide(left + idx, right, rb, level + 1);
     Node &n = nodes_[me];
     n.leaf = false;
     n.divfeat = cutfeat;
@@ -147,62 +139,42 @@ int RefKDTree::divide(size_t left, size_t right, std::vector<Box> &bbox) {
     return me;
 }
 
-void RefKDTree::search(const double *q, int node, double mindistsq, std::vector<double> &dists, double &best,
-                       size_t &best_idx, bool &have) const {
-    const Node &n = nodes_[node];
-    if (n.leaf) {
-        const double worst = best;   // captured once per leaf, as the reference does
-        for (size_t i = n.left; i < n.right; i++) {
-            const size_t index = vind_[i];
-            const double dist = ref_l2(q, pts_ + index * (size_t)dim_, dim_);
-            if (dist < worst && (!have || best > dist)) {
-                best = dist;
-                best_idx = index;
-                have = true;
-            }
+void RefKDTree::flatten(KdNodeDev *nodes, uint32_t *vind, double *lo, double *hi) const {
+    for (size_t i = 0; i < nodes_.size(); i++) {
+        const Node &n = nodes_[i];
+        KdNodeDev &o = nodes[i];
+        if (n.leaf) {
+            o.child1 = o.child2 = -1;
+            o.a = (int32_t)n.left;
+            o.b = (int32_t)n.right;
+            o.lo = o.hi = 0;
+        } else {
+            o.child1 = n.child1;
+            o.child2 = n.child2;
+            o.a = n.divfeat;
+            o.b = 0;
+            o.lo = n.divlow;
+            o.hi = n.divhigh;
         }
-        return;
     }
-    const int f = n.divfeat;
-    const double val = q[f];
-    const double diff1 = val - n.divlow, diff2 = val - n.divhigh;
-    int first, other;
-    double cut_dist;
-    if ((diff1 + diff2) < 0) {
-        first = n.child1;
-        other = n.child2;
-        cut_dist = (val - n.divhigh) * (val - n.divhigh);
-    } else {
-        first = n.child2;
-        other = n.child1;
-        cut_dist = (val - n.divlow) * (val - n.divlow);
+    for (size_t i = 0; i < vind_.size(); i++) vind[i] = (uint32_t)vind_[i];
+    for (int d = 0; d < dim_; d++) {
+        lo[d] = root_bbox_[d].low;
+        hi[d] = root_bbox_[d].high;
     }
-    search(q, first, mindistsq, dists, best, best_idx, have);
-    const double dst = dists[f];
-    mindistsq = (mindistsq - dst) + cut_dist;   // the reference build's association
-    dists[f] = cut_dist;
-    if (mindistsq * 1.0f <= best) search(q, other, mindistsq, dists, best, best_idx, have);
-    dists[f] = dst;
 }
 
+// The traversal the device runs (kdtree_dev.hpp), so host tests check the device's code.
 uint32_t RefKDTree::nearest(const double *q) const {
-    std::vector<double> dists(dim_, 0.0);
-    double distsq = 0;
-    for (int d = 0; d < dim_; d++) {
-        if (q[d] < root_bbox_[d].low) {
-            dists[d] = (q[d] - root_bbox_[d].low) * (q[d] - root_bbox_[d].low);
-            distsq += dists[d];
-        }
-        if (q[d] > root_bbox_[d].high) {
-            dists[d] = (q[d] - root_bbox_[d].high) * (q[d] - root_bbox_[d].high);
-            distsq += dists[d];
-        }
-    }
-    double best = std::numeric_limits<double>::max();
-    size_t best_idx = 0;
-    bool have = false;
-    search(q, 0, distsq, dists, best, best_idx, have);
-    return (uint32_t)best_idx;
+    KdView v;
+    v.nodes = flat_nodes_.data();
+    v.vind = flat_vind_.data();
+    v.lo = flat_box_.data();
+    v.hi = flat_box_.data() + dim_;
+    v.depth = depth_;
+    std::vector<double> sd((size_t)depth_ + 1), dists((size_t)dim_);
+    std::vector<int32_t> sn((size_t)depth_ + 1);
+    return kd_nearest_flat(q, (uint32_t)dim_, v, pts_, (uint32_t)dim_, sd.data(), sn.data(), dists.data());
 }
 
 }  // namespace qvq

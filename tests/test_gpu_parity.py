@@ -96,7 +96,18 @@ def test_set_vectors_rejects_general_data(engine):
         engine.set_vectors(np.random.rand(100, 12))
 
 
-def test_assign_ties_and_duplicates(engine):
+@pytest.fixture(params=["device", "host"])
+def kdmode(request, monkeypatch):
+    """Exact fp64 ties go through the device kd-tree traversal (default) or, with
+    QVQ_KDTREE=host, the synchronous host resolution; both must give the reference answer."""
+    if request.param == "host":
+        monkeypatch.setenv("QVQ_KDTREE", "host")
+    else:
+        monkeypatch.delenv("QVQ_KDTREE", raising=False)
+    return request.param
+
+
+def test_assign_ties_and_duplicates(engine, kdmode):
     """Duplicated code vectors and split pairs (the structural tie sources) are resolved
     exactly as the reference kd-tree resolves them."""
     rng = np.random.default_rng(7)
@@ -119,3 +130,21 @@ def test_update_exact(engine):
     C, cnt = engine.update(A, K)
     np.testing.assert_array_equal(C, oracle.centroids(X, A, K, sum_mode=1))
     np.testing.assert_array_equal(cnt, np.bincount(A, minlength=K))
+
+
+def test_lbg_zero_rows_and_empty_cells(engine, kdmode):
+    """Many all-zero rows (the tiling's end-of-raster padding) and more code vectors than
+    distinct rows: empty cells give zero code vectors whose split copies coincide, so
+    zero rows tie at several levels.  The result must still match the reference."""
+    rng = np.random.default_rng(11)
+    X, _ = oracle.tile(oracle.gen_image(64), 64, 64, 2, 2)
+    X = X[:300].copy()
+    X[rng.choice(300, 120, replace=False)] = 0.0
+    C_k, A_k, d_k = oracle.lbg(X, 9, sum_mode=0)
+    C_x, A_x, _ = oracle.lbg(X, 9, sum_mode=1)
+    engine.set_vectors(X)
+    C, A, d = engine.lbg(9)
+    np.testing.assert_array_equal(A, A_k)
+    np.testing.assert_array_equal(C, C_x)
+    assert abs(d - d_k) <= 1e-9 * abs(d_k)
+    assert sum(engine.timings()["host_ties"]) > 0

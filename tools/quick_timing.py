@@ -3,7 +3,7 @@ import json
 import sys
 import time
 
-sys.path.insert(0, '.')
+sys.path.insert(0, __import__('os').path.dirname(__import__('os').path.dirname(__import__('os').path.abspath(__file__))))
 import quant_amd
 
 cases = [(512, 2, 10), (4096, 2, 10), (4096, 4, 12)]
