@@ -25,8 +25,13 @@ import time
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-PEAK_FP32_TFLOPS = 157.3     # MI355X_MICROARCH.md: FP32 vector = FP32 matrix peak
+PEAK_F16_TFLOPS = 2500.0     # MI355X_MICROARCH.md: BF16/F16 MFMA ~2.5 PF dense (no sparsity)
 PEAK_HBM_GBS = 8000.0
+PMC_SUMMARY = os.path.join(ROOT, "profiles", "pmc_hbm_latest.json")   # tools/pmc_summary.py output
+
+
+def workload_key(args):
+    return "%dx%d_b%d_bits%d_ipr%d" % (args.size, args.size, args.block, args.bits, args.images_per_rank)
 
 
 def parse():
@@ -121,12 +126,26 @@ def main():
     value = n_total * levels * args.steps / elapsed / 1e6
     ms_per_step = elapsed * 1e3 / args.steps
 
-    # Roofline of the dominant kernel (assign), from HIP events on the engine's stream:
-    # algorithmic work per launch = 3*K_l*D flop per block x n_local blocks.
+    # Roofline of the dominant kernel, the search (assign_mfma_kernel: f16 MFMA 16x16x32 with
+    # the centroid sums fused), from HIP events recorded around each launch on the engine's
+    # stream.  Algorithmic work per launch = 3*K_l*D flop per block x blocks.
     launches = [(1 << (l + 1), ms) for step in assign_ms for l, ms in enumerate(step)]
     flops = sum(3.0 * K * D * n_local for K, _ in launches)
     secs = sum(ms for _, ms in launches) * 1e-3
-    achieved = flops / len(launches) / (secs / len(launches)) / 1e12
+    achieved = flops / secs / 1e12
+    avg_launch_s = secs / len(launches)
+    # its HBM view: codes in (Dp bytes per block) + index out (4 bytes per block)
+    assign_bytes = n_local * (((D + 3) & ~3) + 4)
+    traffic, traffic_src = None, None
+    try:
+        pmc = json.load(open(PMC_SUMMARY))
+        ks = [v for k, v in pmc["kernels"].items() if k.startswith("assign_mfma_kernel")]
+        if ks and pmc.get("workload") == workload_key(args):
+            tot = sum(v["hbm_bytes"] * v["launches"] for v in ks)
+            traffic = round(tot / sum(v["launches"] for v in ks))
+            traffic_src = os.path.relpath(PMC_SUMMARY, ROOT)
+    except (OSError, ValueError, KeyError):
+        pass
     upd_secs = sum(sum(s) for s in update_ms) * 1e-3
     upd_bytes = len(update_ms) * levels * n_local * (((D + 3) & ~3) + 4)
     result = {
@@ -140,20 +159,24 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "f32 search + f64 recheck/centroids",
+        "dtype": "f16 MFMA search on exact integer byte operands + fp64 recheck, exact integer centroid sums",
         "data": "synthetic (SURVEY.md 8(d) generator, seed 0x5EED+image), resident in HBM",
         "config": {"workload": "C3: %dx%d synthetic RGB per image, %dx%d blocks (D=%d), %d code vectors, "
                                "%d image(s) per rank, joint codebook" % (args.size, args.size, args.block,
                                                                          args.block, D, 1 << args.bits, ipr),
                    "blocks_per_rank": n_local, "levels": levels, "parallelism": "dp%d" % world},
         "lbg_iters_per_s": round(levels * args.steps / elapsed, 3),
-        "roofline": {"bound": "mfma", "kernel": "assign_kernel<12> (fp32 VALU; vector roof = matrix roof)",
-                     "achieved": round(achieved, 3), "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
-                     "frac": round(achieved / PEAK_FP32_TFLOPS, 4), "traffic": None,
-                     "avg_launch_ms": round(secs * 1e3 / len(launches), 5)},
-        "update_kernel": {"avg_launch_ms": round(upd_secs * 1e3 / max(1, len(update_ms) * levels), 5),
-                          "achieved_GBps": round(upd_bytes / upd_secs / 1e9, 1) if upd_secs else None,
-                          "peak_GBps": PEAK_HBM_GBS},
+        "roofline": {"bound": "mfma", "kernel": "qvq::assign_mfma_kernel (v_mfma_f32_16x16x32_f16, fused sums)",
+                     "achieved": round(achieved, 3), "peak": PEAK_F16_TFLOPS, "unit": "TFLOP/s",
+                     "frac": round(achieved / PEAK_F16_TFLOPS, 4), "traffic": traffic,
+                     "traffic_source": traffic_src, "avg_launch_ms": round(avg_launch_s * 1e3, 5),
+                     "launches": len(launches), "flop_per_block": "3*K*D",
+                     "hbm_view": {"algorithmic_bytes_per_launch": assign_bytes,
+                                  "achieved_GBps": round(assign_bytes / avg_launch_s / 1e9, 1),
+                                  "peak_GBps": PEAK_HBM_GBS}},
+        "update_kernel": ({"avg_launch_ms": round(upd_secs * 1e3 / max(1, len(update_ms) * levels), 5),
+                           "achieved_GBps": round(upd_bytes / upd_secs / 1e9, 1), "peak_GBps": PEAK_HBM_GBS}
+                          if upd_secs else "fused into the search (LDS u64 atomics of exact integer terms)"),
         "flagged_rows_per_step": sum(flagged[-1]),
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

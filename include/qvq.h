@@ -55,7 +55,7 @@ typedef struct {
     double total_ms;            /* whole qvq_lbg, host wall */
     double assign_ms[32];       /* device time of the assignment kernel per level */
     double update_ms[32];       /* device time of the centroid-sum kernel per level */
-    double other_ms[32];        /* recheck + finalize + host tie resolution per level */
+    double other_ms[32];        /* rest of the level: recheck, kd-tree ties, reduce, finalize + tables */
     uint64_t flagged[32];       /* rows re-checked in fp64 per level */
     uint64_t host_ties[32];     /* rows resolved by the host kd-tree per level */
 } qvq_timings;

@@ -101,22 +101,36 @@ hipError_t launch_assign_mfma(hipStream_t s, int grid, bool fuse, const uint8_t 
                               const _Float16 *cb_rows, uint32_t K, const float *C32, const uint64_t *plut,
                               const MfThresholds &th, uint32_t *A, uint32_t *flags, unsigned *flag_cnt,
                               uint64_t *part, uint32_t *part_cnt);
-// Deepest kd-tree the recheck's LDS stacks can hold (deeper: host resolution).
-int recheck_max_kd_depth();
-// fp64 recheck of flagged rows; exact ties go through the device kd-tree (kd.depth > 0) or
-// are listed in ties for the host.  With sums != nullptr adds every resolved row's terms.
+// fp64 recheck of flagged rows; exact ties are listed in ties (tie_cnt) for
+// launch_kd_resolve or the host.  With sums != nullptr adds every other row's terms.
 hipError_t launch_recheck(hipStream_t s, int num_cu, const uint8_t *codes, uint32_t Dp, uint32_t D,
                           const uint32_t *flags, const unsigned *flag_cnt, const double *C64, uint32_t K,
-                          const double *lut64, double tie_rel, const KdView &kd, uint32_t *A, uint32_t *ties,
-                          unsigned *tie_cnt, uint64_t *sums, const uint64_t *plut);
+                          const double *lut64, double tie_rel, uint32_t *A, uint32_t *ties, unsigned *tie_cnt,
+                          uint64_t *sums, const uint64_t *plut);
+// Device kd-tree answers for the listed ties (tree image in mapped host memory); adds their
+// terms to sums when given.  kd_resolve_fits: the tree and stacks fit the LDS.
+bool kd_resolve_fits(const KdView &kd);
+hipError_t launch_kd_resolve(hipStream_t s, const uint8_t *codes, uint32_t Dp, uint32_t D, const uint32_t *ties,
+                             const unsigned *tie_cnt, const double *C64, uint32_t K, const double *lut64,
+                             const KdView &kd, uint32_t *A, uint64_t *sums, const uint64_t *plut);
 hipError_t launch_update(hipStream_t s, uint32_t Dp, uint32_t G, const uint8_t *codes, uint64_t N, const uint32_t *A,
                          uint32_t K, uint32_t D, const uint64_t *plut, uint64_t *part, uint32_t *part_cnt);
 hipError_t launch_reduce(hipStream_t s, const uint64_t *part, const uint32_t *part_cnt, uint32_t G, uint32_t K,
                          uint32_t D, uint64_t *sums);
 hipError_t launch_mean_sums(hipStream_t s, uint32_t Dp, const uint8_t *codes, uint64_t N, uint32_t D,
                             const uint64_t *plut, uint64_t *sums);
+// Centroids of the reduced sums (C_cent [K][D]); with split also the next level's K' = 2K
+// code vectors (C64n and, if host_cb, mapped host memory) and their search tables (see
+// launch_prep) padded to Kpad_next; without split, given dist_out, dist_out[0] =
+// sum_k (2 c_k.S_k - n_k ||c_k||^2) (closed-form distortion).  With done (a counter at 0,
+// left at 0) the last block also publishes *ready = seq in mapped host memory; dist_part
+// holds the per-block partials (<= 8000).
+hipError_t launch_finalize_prep(hipStream_t s, const uint64_t *sums, uint32_t K, uint32_t D, uint32_t Dp, int64_t R,
+                                int64_t bias, int scale, double *C_cent, bool split, double *C64n, uint32_t Kpad_next,
+                                double mu, double sx, int t, float *C32, _Float16 *cb_rows, double *host_cb,
+                                double *dist_part, unsigned *done, double *dist_out, uint64_t *ready, uint64_t seq);
 hipError_t launch_finalize(hipStream_t s, const uint64_t *sums, uint32_t K, uint32_t D, int64_t R, int64_t bias,
-                           int scale, double *C_cent, bool split, double *C64n);
+                           int scale, double *C_cent);
 // f16 MFMA tables (D = 12) and fp32 VALU table from an fp64 codebook of K code vectors.
 hipError_t launch_prep(hipStream_t s, const double *C64, uint32_t K, uint32_t Kpad, uint32_t D, uint32_t Dp,
                        double mu, double sx, int t, float *C32, _Float16 *cb_rows);
@@ -128,8 +142,4 @@ hipError_t launch_scatter(hipStream_t s, uint32_t *A, const uint32_t *rows, cons
 // 256-bin histogram of the first D bytes of every row (hist zeroed first).
 hipError_t launch_byte_hist(hipStream_t s, const uint8_t *codes, uint64_t N, uint32_t D, uint32_t Dp,
                             uint64_t *hist);
-// out[0] = sum_k (2 c_k.S_k - n_k ||c_k||^2) from the exact sums and the centroids C [K][D].
-hipError_t launch_distortion_cf(hipStream_t s, const uint64_t *sums, uint32_t K, uint32_t D, int64_t R, int64_t bias,
-                                int scale, const double *C, double *out);
-
 }  // namespace qvq

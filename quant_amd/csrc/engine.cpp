@@ -17,6 +17,7 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -102,13 +103,15 @@ struct qvq_ctx {
     double *d_dist_part = nullptr;
     uint32_t *d_scatter = nullptr;
     uint64_t scatter_bytes = 0;
-    double *h_cb = nullptr;            // pinned: the level's split codebook for the tree build
-    uint8_t *h_tree = nullptr, *d_tree = nullptr;   // flattened kd-tree (pinned / device)
+    // mapped pinned host memory (coherent): the split codebook finalize writes for the
+    // host's tree build, its ready sequence number, and two flattened kd-tree images
+    double *h_cb = nullptr, *dh_cb = nullptr;
+    uint64_t *h_ready = nullptr, *dh_ready = nullptr;
+    uint64_t seq = 0;
+    uint8_t *h_tree[2] = {nullptr, nullptr}, *dh_tree[2] = {nullptr, nullptr};
     uint64_t tree_cap = 0;
-
-    // copy stream and its hand-off events
-    hipStream_t cstream = nullptr;
-    hipEvent_t ev_fin = nullptr, ev_cb = nullptr, ev_rc = nullptr, ev_tree = nullptr;
+    bool upd[32] = {};
+    hipEvent_t ev_end = nullptr;
 
     // multi-GPU
     ncclComm_t comm = nullptr;
@@ -179,11 +182,12 @@ void free_levels(qvq_ctx *ctx) {
     dfree(ctx->d_part);
     dfree(ctx->d_part_cnt);
     dfree(ctx->d_sums);
-    dfree(ctx->d_tree);
     if (ctx->h_cb) (void)hipHostFree(ctx->h_cb);
-    if (ctx->h_tree) (void)hipHostFree(ctx->h_tree);
-    ctx->h_cb = nullptr;
-    ctx->h_tree = nullptr;
+    ctx->h_cb = ctx->dh_cb = nullptr;
+    for (int b = 0; b < 2; b++) {
+        if (ctx->h_tree[b]) (void)hipHostFree(ctx->h_tree[b]);
+        ctx->h_tree[b] = ctx->dh_tree[b] = nullptr;
+    }
     ctx->tree_cap = 0;
     ctx->Kcap = 0;
 }
@@ -271,10 +275,14 @@ qvq_status ensure_levels(qvq_ctx *ctx, uint32_t Kmax) {
     HIPCHK(hipMalloc(&ctx->d_part, (uint64_t)ctx->G * KD * 8));
     HIPCHK(hipMalloc(&ctx->d_part_cnt, (uint64_t)ctx->G * Kmax * 4));
     HIPCHK(hipMalloc(&ctx->d_sums, (2 * KD + Kmax) * 8));
-    HIPCHK(hipHostMalloc(&ctx->h_cb, KD * 8, hipHostMallocDefault));
+    const unsigned mflags = hipHostMallocMapped | hipHostMallocCoherent;
+    HIPCHK(hipHostMalloc(&ctx->h_cb, KD * 8, mflags));
+    HIPCHK(hipHostGetDevicePointer((void **)&ctx->dh_cb, ctx->h_cb, 0));
     ctx->tree_cap = tree_bytes(Kmax, ctx->D);
-    HIPCHK(hipHostMalloc(&ctx->h_tree, ctx->tree_cap, hipHostMallocDefault));
-    HIPCHK(hipMalloc(&ctx->d_tree, ctx->tree_cap));
+    for (int b = 0; b < 2; b++) {
+        HIPCHK(hipHostMalloc(&ctx->h_tree[b], ctx->tree_cap, mflags));
+        HIPCHK(hipHostGetDevicePointer((void **)&ctx->dh_tree[b], ctx->h_tree[b], 0));
+    }
     ctx->Kcap = Kmax;
     return QVQ_OK;
 }
@@ -311,40 +319,46 @@ qvq_status run_update(qvq_ctx *ctx, const uint32_t *d_A, uint32_t K) {
 }
 
 // Build the reference kd-tree over the host copy hC of the K code vectors being searched
-// and upload it for the recheck (copy stream, ordered after the previous recheck).  Returns
-// an empty view (host resolution) when the tree is deeper than the device stack.
-qvq_status upload_tree(qvq_ctx *ctx, const double *hC, uint32_t K, KdView &kd) {
+// into tree image buffer buf (mapped pinned memory, read by kd_resolve_kernel).  An empty
+// view means host resolution (tree too deep/large for the kernel's LDS, or QVQ_KDTREE=host).
+void build_tree(qvq_ctx *ctx, const double *hC, uint32_t K, int buf, KdView &kd) {
     kd = KdView{};
-    if (env_is("QVQ_KDTREE", "host")) return QVQ_OK;
+    if (env_is("QVQ_KDTREE", "host")) return;
     RefKDTree tree(hC, K, (int)ctx->D);
-    if (tree.depth() > recheck_max_kd_depth()) return QVQ_OK;
     const uint32_t D = ctx->D;
-    double *lo = reinterpret_cast<double *>(ctx->h_tree), *hi = lo + D;
+    KdView v;
+    v.depth = tree.depth();
+    v.n_nodes = (uint32_t)tree.num_nodes();
+    v.bytes = (uint32_t)(16ull * D + tree.num_nodes() * sizeof(KdNodeDev) + 4ull * K);
+    if (!kd_resolve_fits(v)) return;
+    double *lo = reinterpret_cast<double *>(ctx->h_tree[buf]), *hi = lo + D;
     KdNodeDev *nodes = reinterpret_cast<KdNodeDev *>(hi + D);
     uint32_t *vind = reinterpret_cast<uint32_t *>(nodes + tree.num_nodes());
     tree.flatten(nodes, vind, lo, hi);
-    const uint64_t bytes = 16ull * D + tree.num_nodes() * sizeof(KdNodeDev) + 4ull * K;
-    HIPCHK(hipStreamWaitEvent(ctx->cstream, ctx->ev_rc, 0));
-    HIPCHK(hipMemcpyAsync(ctx->d_tree, ctx->h_tree, bytes, hipMemcpyHostToDevice, ctx->cstream));
-    HIPCHK(hipEventRecord(ctx->ev_tree, ctx->cstream));
-    HIPCHK(hipStreamWaitEvent(ctx->stream, ctx->ev_tree, 0));
-    const double *dlo = reinterpret_cast<const double *>(ctx->d_tree);
-    kd.lo = dlo;
-    kd.hi = dlo + D;
-    kd.nodes = reinterpret_cast<const KdNodeDev *>(dlo + 2 * D);
-    kd.vind = reinterpret_cast<const uint32_t *>(kd.nodes + tree.num_nodes());
-    kd.depth = tree.depth();
-    return QVQ_OK;
+    const double *dlo = reinterpret_cast<const double *>(ctx->dh_tree[buf]);
+    v.lo = dlo;
+    v.hi = dlo + D;
+    v.nodes = reinterpret_cast<const KdNodeDev *>(dlo + 2 * D);
+    v.vind = reinterpret_cast<const uint32_t *>(v.nodes + tree.num_nodes());
+    kd = v;
 }
 
-// After the finalize that produced the next level's K code vectors in d_C64_split: copy
-// them to h_cb on the copy stream (ev_cb marks completion).
-qvq_status download_codebook(qvq_ctx *ctx, uint32_t K) {
-    HIPCHK(hipEventRecord(ctx->ev_fin, ctx->stream));
-    HIPCHK(hipStreamWaitEvent(ctx->cstream, ctx->ev_fin, 0));
-    HIPCHK(hipMemcpyAsync(ctx->h_cb, ctx->d_C64_split, (uint64_t)K * ctx->D * 8, hipMemcpyDeviceToHost,
-                          ctx->cstream));
-    HIPCHK(hipEventRecord(ctx->ev_cb, ctx->cstream));
+// Wait until finalize has published codebook seq in h_cb.  Polls the mapped flag; a stream
+// error or a drained stream without the flag ends the wait with an error (never hangs).
+qvq_status wait_codebook(qvq_ctx *ctx, uint64_t seq) {
+    volatile uint64_t *flag = ctx->h_ready;
+    for (uint64_t spin = 0;; spin++) {
+        if (*flag >= seq) break;
+        if ((spin & 255) == 255) {
+            const hipError_t q = hipStreamQuery(ctx->stream);
+            if (q == hipSuccess) {
+                if (*flag >= seq) break;
+                return fail(ctx, QVQ_EDEVICE, "finalize finished without publishing the codebook");
+            }
+            if (q != hipErrorNotReady) return fail(ctx, QVQ_EDEVICE, std::string("stream: ") + hipGetErrorString(q));
+        }
+    }
+    std::atomic_thread_fence(std::memory_order_acquire);
     return QVQ_OK;
 }
 
@@ -399,9 +413,10 @@ qvq_status resolve_host_ties(qvq_ctx *ctx, const double *hC, uint32_t K, uint32_
 }
 
 // One level's assignment of every row against the split codebook (d_C64_split, host copy
-// hC, tables from run_prep), K code vectors.  wait_cb: hC is being downloaded (ev_cb).
-// With sums_out the exact centroid sums of the final assignment are left in d_sums.
-qvq_status run_level(qvq_ctx *ctx, uint32_t K, int slot, bool sums_out, const double *hC, bool wait_cb) {
+// hC, search tables in d_C32/d_rows), K code vectors.  wait_seq != 0: hC is published by a
+// finalize still in flight.  With sums_out the exact centroid sums of the final assignment
+// are left in d_sums.
+qvq_status run_level(qvq_ctx *ctx, uint32_t K, int slot, bool sums_out, const double *hC, uint64_t wait_seq) {
     const bool fused = sums_out && use_fused(ctx, K);
     unsigned *cnt = ctx->d_counters + 2 * slot;
     HIPCHK(hipEventRecord(ctx->ev[slot][0], ctx->stream));
@@ -417,24 +432,29 @@ qvq_status run_level(qvq_ctx *ctx, uint32_t K, int slot, bool sums_out, const do
     }
     HIPCHK(hipEventRecord(ctx->ev[slot][1], ctx->stream));
     if (fused) HIPCHK(launch_reduce(ctx->stream, ctx->d_part, ctx->d_part_cnt, ctx->num_cu, K, ctx->D, ctx->d_sums));
-    // the tree build overlaps the search just enqueued
-    if (wait_cb) HIPCHK(hipEventSynchronize(ctx->ev_cb));
-    KdView kd;
-    qvq_status st = upload_tree(ctx, hC, K, kd);
-    if (st != QVQ_OK) return st;
     HIPCHK(launch_recheck(ctx->stream, ctx->num_cu, ctx->d_codes, ctx->Dp, ctx->D, ctx->d_flags, &cnt[0],
-                          ctx->d_C64_split, K, ctx->d_lut64, 1e-12, kd, ctx->d_A, ctx->d_ties, &cnt[1],
+                          ctx->d_C64_split, K, ctx->d_lut64, 1e-12, ctx->d_A, ctx->d_ties, &cnt[1],
                           fused ? ctx->d_sums : nullptr, ctx->d_plut));
-    HIPCHK(hipEventRecord(ctx->ev_rc, ctx->stream));
-    if (kd.depth == 0) {   // ties listed for the host
+    // the tree build overlaps the search just enqueued
+    qvq_status st;
+    if (wait_seq && (st = wait_codebook(ctx, wait_seq)) != QVQ_OK) return st;
+    KdView kd;
+    build_tree(ctx, hC, K, slot & 1, kd);
+    if (kd.depth > 0) {
+        HIPCHK(launch_kd_resolve(ctx->stream, ctx->d_codes, ctx->Dp, ctx->D, ctx->d_ties, &cnt[1], ctx->d_C64_split,
+                                 K, ctx->d_lut64, kd, ctx->d_A, fused ? ctx->d_sums : nullptr, ctx->d_plut));
+    } else {   // ties answered on the host
         unsigned nt = 0;
         HIPCHK(hipMemcpyAsync(&nt, &cnt[1], sizeof(nt), hipMemcpyDeviceToHost, ctx->stream));
         HIPCHK(hipStreamSynchronize(ctx->stream));
         if (nt && (st = resolve_host_ties(ctx, hC, K, nt, fused)) != QVQ_OK) return st;
     }
-    HIPCHK(hipEventRecord(ctx->ev[slot][2], ctx->stream));
-    if (sums_out && !fused && (st = run_update(ctx, ctx->d_A, K)) != QVQ_OK) return st;
-    HIPCHK(hipEventRecord(ctx->ev[slot][3], ctx->stream));
+    ctx->upd[slot] = sums_out && !fused;
+    if (ctx->upd[slot]) {
+        HIPCHK(hipEventRecord(ctx->ev[slot][2], ctx->stream));
+        if ((st = run_update(ctx, ctx->d_A, K)) != QVQ_OK) return st;
+        HIPCHK(hipEventRecord(ctx->ev[slot][3], ctx->stream));
+    }
     return QVQ_OK;
 }
 
@@ -505,15 +525,18 @@ QVQ_API qvq_status qvq_create(int hip_device, qvq_ctx **out) {
     if ((e = hipMalloc(&ctx->d_w, 256 * 4)) != hipSuccess) return bail(e, "hipMalloc");
     if ((e = hipMalloc(&ctx->d_lut64, 256 * 8)) != hipSuccess) return bail(e, "hipMalloc");
     if ((e = hipMalloc(&ctx->d_plut, 256 * 8)) != hipSuccess) return bail(e, "hipMalloc");
-    if ((e = hipStreamCreateWithFlags(&ctx->cstream, hipStreamNonBlocking)) != hipSuccess) return bail(e, "stream");
-    for (hipEvent_t *ev : {&ctx->ev_fin, &ctx->ev_cb, &ctx->ev_rc, &ctx->ev_tree})
-        if ((e = hipEventCreateWithFlags(ev, hipEventDisableTiming)) != hipSuccess) return bail(e, "hipEventCreate");
-    if ((e = hipMalloc(&ctx->d_counters, 2 * 33 * sizeof(unsigned))) != hipSuccess) return bail(e, "hipMalloc");
+    if ((e = hipHostMalloc(&ctx->h_ready, 64, hipHostMallocMapped | hipHostMallocCoherent)) != hipSuccess)
+        return bail(e, "hipHostMalloc");
+    *ctx->h_ready = 0;
+    if ((e = hipHostGetDevicePointer((void **)&ctx->dh_ready, ctx->h_ready, 0)) != hipSuccess)
+        return bail(e, "hipHostGetDevicePointer");
+    if ((e = hipMalloc(&ctx->d_counters, (2 * 33 + 1) * sizeof(unsigned))) != hipSuccess) return bail(e, "hipMalloc");
     if ((e = hipMalloc(&ctx->d_hist, 256 * 8)) != hipSuccess) return bail(e, "hipMalloc");
-    if ((e = hipMalloc(&ctx->d_dist_part, 4096 * 8)) != hipSuccess) return bail(e, "hipMalloc");
+    if ((e = hipMalloc(&ctx->d_dist_part, 8192 * 8)) != hipSuccess) return bail(e, "hipMalloc");
     for (int l = 0; l < 32; l++)
         for (int j = 0; j < 4; j++)
             if ((e = hipEventCreate(&ctx->ev[l][j])) != hipSuccess) return bail(e, "hipEventCreate");
+    if ((e = hipEventCreate(&ctx->ev_end)) != hipSuccess) return bail(e, "hipEventCreate");
     ctx->ev_ready = true;
     *out = ctx;
     return QVQ_OK;
@@ -523,7 +546,6 @@ QVQ_API void qvq_destroy(qvq_ctx *ctx) {
     if (!ctx) return;
     (void)hipSetDevice(ctx->dev);
     if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
-    if (ctx->cstream) (void)hipStreamSynchronize(ctx->cstream);
     if (ctx->comm) ncclCommDestroy(ctx->comm);
     free_training(ctx);
     free_levels(ctx);
@@ -533,14 +555,13 @@ QVQ_API void qvq_destroy(qvq_ctx *ctx) {
     dfree(ctx->d_plut);
     dfree(ctx->d_counters);
     dfree(ctx->d_hist);
-    for (hipEvent_t ev : {ctx->ev_fin, ctx->ev_cb, ctx->ev_rc, ctx->ev_tree})
-        if (ev) (void)hipEventDestroy(ev);
-    if (ctx->cstream) (void)hipStreamDestroy(ctx->cstream);
+    if (ctx->h_ready) (void)hipHostFree(ctx->h_ready);
     dfree(ctx->d_dist_part);
     dfree(ctx->d_scatter);
     if (ctx->ev_ready)
         for (int l = 0; l < 32; l++)
             for (int j = 0; j < 4; j++) (void)hipEventDestroy(ctx->ev[l][j]);
+    if (ctx->ev_end) (void)hipEventDestroy(ctx->ev_end);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
     delete ctx;
 }
@@ -663,8 +684,7 @@ QVQ_API qvq_status qvq_lbg(qvq_ctx *ctx, uint32_t bits, double eps, double *code
     std::memset(&ctx->tm, 0, sizeof(ctx->tm));
     ctx->tm.levels = (int)bits;
     const Terms &T = ctx->terms;
-    HIPCHK(hipMemsetAsync(ctx->d_counters, 0, 2 * 33 * sizeof(unsigned), ctx->stream));
-    HIPCHK(hipEventRecord(ctx->ev_rc, ctx->stream));
+    HIPCHK(hipMemsetAsync(ctx->d_counters, 0, (2 * 33 + 1) * sizeof(unsigned), ctx->stream));
     // [sum ||x||^2, rows] over all ranks, for the closed-form distortion
     double *d_dist = ctx->d_dist_part;
     double xn[2] = {ctx->xsq, (double)ctx->N};
@@ -674,25 +694,28 @@ QVQ_API qvq_status qvq_lbg(qvq_ctx *ctx, uint32_t bits, double eps, double *code
     // codeVectors[0] = trainingSetSum() / N, then the first split (src/Quantizer.cpp:129-138)
     HIPCHK(launch_mean_sums(ctx->stream, ctx->Dp, ctx->d_codes, ctx->N, ctx->D, ctx->d_plut, ctx->d_sums));
     if ((st = all_reduce_sums(ctx, 1)) != QVQ_OK) return st;
-    HIPCHK(launch_finalize(ctx->stream, ctx->d_sums, 1, ctx->D, T.R, T.bias, T.scale, ctx->d_C64_cent, bits > 0,
-                           ctx->d_C64_split));
-    if (bits > 0 && (st = download_codebook(ctx, 2)) != QVQ_OK) return st;
+    unsigned *dist_done = ctx->d_counters + 2 * 33;
+    // finalize (+ split, tables, host codebook and its ready number) / final distortion
+    auto finalize = [&](uint32_t K, bool split) {
+        if (split) ctx->seq++;
+        return launch_finalize_prep(ctx->stream, ctx->d_sums, K, ctx->D, ctx->Dp, T.R, T.bias, T.scale,
+                                    ctx->d_C64_cent, split, ctx->d_C64_split, pad32(2 * K), T.mu, T.sx, ctx->mf_t,
+                                    ctx->d_C32, ctx->d_rows, split ? ctx->dh_cb : nullptr, d_dist + 8, dist_done,
+                                    split ? nullptr : d_dist + 2, split ? ctx->dh_ready : nullptr, ctx->seq);
+    };
+    HIPCHK(finalize(1, bits > 0));
     HIPCHK(hipMemsetAsync(ctx->d_A, 0, ctx->N * 4, ctx->stream));
 
     for (uint32_t lvl = 1; lvl <= bits; lvl++) {
         const uint32_t K = 1u << lvl;
         const int slot = (int)lvl - 1;
-        if ((st = run_prep(ctx, K)) != QVQ_OK) return st;
-        if ((st = run_level(ctx, K, slot, true, ctx->h_cb, true)) != QVQ_OK) return st;
+        if ((st = run_level(ctx, K, slot, true, ctx->h_cb, ctx->seq)) != QVQ_OK) return st;
         if ((st = all_reduce_sums(ctx, K)) != QVQ_OK) return st;
-        HIPCHK(launch_finalize(ctx->stream, ctx->d_sums, K, ctx->D, T.R, T.bias, T.scale, ctx->d_C64_cent, lvl < bits,
-                               ctx->d_C64_split));
-        if (lvl < bits && (st = download_codebook(ctx, 2 * K)) != QVQ_OK) return st;
+        HIPCHK(finalize(K, lvl < bits));
     }
     // Returned distortion: updateDistortion after the last fix (src/Quantizer.cpp:9-22,103),
-    // from the sums of the final assignment (k_misc.hip, distortion_cf_kernel).
-    HIPCHK(launch_distortion_cf(ctx->stream, ctx->d_sums, Kmax, ctx->D, T.R, T.bias, T.scale, ctx->d_C64_cent,
-                                d_dist + 2));
+    // from the sums of the final assignment (finalize_prep_kernel without split).
+    HIPCHK(hipEventRecord(ctx->ev_end, ctx->stream));
     double dres[3];
     unsigned stats[2 * 33];
     HIPCHK(hipMemcpyAsync(dres, d_dist, sizeof(dres), hipMemcpyDeviceToHost, ctx->stream));
@@ -704,16 +727,19 @@ QVQ_API qvq_status qvq_lbg(qvq_ctx *ctx, uint32_t bits, double eps, double *code
     HIPCHK(hipStreamSynchronize(ctx->stream));
     if (distortion) *distortion = (dres[0] - dres[2]) / (dres[1] * (double)ctx->D);
     for (uint32_t lvl = 1; lvl <= bits; lvl++) {
-        float a = 0, u = 0, o = 0;
+        // assign: the search kernel; update: the non-fused update; other: the rest of the
+        // level up to the next level's search (recheck, kd-tree, reduce, finalize, tables)
+        float a = 0, u = 0, whole = 0;
         (void)hipEventElapsedTime(&a, ctx->ev[lvl - 1][0], ctx->ev[lvl - 1][1]);
-        (void)hipEventElapsedTime(&o, ctx->ev[lvl - 1][1], ctx->ev[lvl - 1][2]);
-        (void)hipEventElapsedTime(&u, ctx->ev[lvl - 1][2], ctx->ev[lvl - 1][3]);
+        if (ctx->upd[lvl - 1]) (void)hipEventElapsedTime(&u, ctx->ev[lvl - 1][2], ctx->ev[lvl - 1][3]);
+        (void)hipEventElapsedTime(&whole, ctx->ev[lvl - 1][0], lvl < bits ? ctx->ev[lvl][0] : ctx->ev_end);
         ctx->tm.assign_ms[lvl - 1] = a;
-        ctx->tm.other_ms[lvl - 1] = o;
+        ctx->tm.other_ms[lvl - 1] = std::max(0.f, whole - a - u);
         ctx->tm.update_ms[lvl - 1] = u;
         ctx->tm.flagged[lvl - 1] = stats[2 * (lvl - 1)];
         ctx->tm.host_ties[lvl - 1] = stats[2 * (lvl - 1) + 1];
     }
+    (void)hipGetLastError();
     ctx->tm.total_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     return QVQ_OK;
 }
@@ -728,9 +754,8 @@ QVQ_API qvq_status qvq_assign(qvq_ctx *ctx, const double *C, uint32_t K, uint32_
     std::memset(&ctx->tm, 0, sizeof(ctx->tm));
     HIPCHK(hipMemcpy(ctx->d_C64_split, C, (uint64_t)K * ctx->D * 8, hipMemcpyHostToDevice));
     HIPCHK(hipMemsetAsync(ctx->d_counters, 0, 2 * sizeof(unsigned), ctx->stream));
-    HIPCHK(hipEventRecord(ctx->ev_rc, ctx->stream));
     if ((st = run_prep(ctx, K)) != QVQ_OK) return st;
-    if ((st = run_level(ctx, K, 0, false, C, false)) != QVQ_OK) return st;
+    if ((st = run_level(ctx, K, 0, false, C, 0)) != QVQ_OK) return st;
     unsigned stats[2];
     HIPCHK(hipMemcpyAsync(stats, ctx->d_counters, sizeof(stats), hipMemcpyDeviceToHost, ctx->stream));
     if (assign) HIPCHK(hipMemcpyAsync(assign, ctx->d_A, ctx->N * 4, hipMemcpyDeviceToHost, ctx->stream));
@@ -754,7 +779,7 @@ QVQ_API qvq_status qvq_update(qvq_ctx *ctx, const uint32_t *assign, uint32_t K, 
     if ((st = run_update(ctx, ctx->d_A, K)) != QVQ_OK) return st;
     if ((st = all_reduce_sums(ctx, K)) != QVQ_OK) return st;
     const Terms &T = ctx->terms;
-    HIPCHK(launch_finalize(ctx->stream, ctx->d_sums, K, ctx->D, T.R, T.bias, T.scale, ctx->d_C64_cent, false, nullptr));
+    HIPCHK(launch_finalize(ctx->stream, ctx->d_sums, K, ctx->D, T.R, T.bias, T.scale, ctx->d_C64_cent));
     if (C_out)
         HIPCHK(hipMemcpyAsync(C_out, ctx->d_C64_cent, (uint64_t)K * ctx->D * 8, hipMemcpyDeviceToHost, ctx->stream));
     if (counts)

@@ -76,26 +76,46 @@ __device__ inline float byte_w(uint32_t word, int j) {
 
 typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
 
-// Segmented inclusive sum over consecutive lanes with equal key (lanes hold consecutive
-// rows); returns true on the last lane of each run, which then holds the run's sums.
+// Wave64 inclusive scans with DPP (row_shr within rows of 16, then row_bcast:15/31 across
+// rows): one VALU instruction per step, no LDS traffic.
+template <int CTRL, int ROW_MASK>
+__device__ inline uint32_t dpp_get(uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, ROW_MASK, 0xF, true);
+}
+__device__ inline uint32_t wave_scan_add(uint32_t v) {
+    v += dpp_get<0x111, 0xF>(v);   // row_shr:1
+    v += dpp_get<0x112, 0xF>(v);   // row_shr:2
+    v += dpp_get<0x114, 0xF>(v);   // row_shr:4
+    v += dpp_get<0x118, 0xF>(v);   // row_shr:8
+    v += dpp_get<0x142, 0xA>(v);   // row_bcast:15 into rows 1, 3
+    v += dpp_get<0x143, 0xC>(v);   // row_bcast:31 into rows 2, 3
+    return v;
+}
+__device__ inline uint32_t wave_scan_max(uint32_t v) {
+    v = max(v, dpp_get<0x111, 0xF>(v));
+    v = max(v, dpp_get<0x112, 0xF>(v));
+    v = max(v, dpp_get<0x114, 0xF>(v));
+    v = max(v, dpp_get<0x118, 0xF>(v));
+    v = max(v, dpp_get<0x142, 0xA>(v));
+    v = max(v, dpp_get<0x143, 0xC>(v));
+    return v;
+}
+
+// Per-run sums over consecutive lanes with equal key (lanes hold consecutive rows): plain
+// prefix sums, then each run's last lane takes prefix[last] - prefix[first - 1].  The
+// packed 16-bit fields of v never carry within 64 rows, so the subtraction is per field.
+// Returns true on the last lane of each run, which then holds the run's sums.
 __device__ inline bool wave_runs_reduce(uint32_t key, uint32_t (&v)[MF_D + 1], int lane) {
     const uint32_t prev = __shfl_up(key, 1);
-    uint32_t seg = (lane == 0 || prev != key) ? (uint32_t)lane : 0u;
-#pragma unroll
-    for (int off = 1; off < 64; off <<= 1) {
-        const uint32_t o = __shfl_up(seg, off);
-        seg = lane >= off ? max(seg, o) : seg;
-    }
-#pragma unroll
-    for (int off = 1; off < 64; off <<= 1) {
-        const bool take = lane >= off && (uint32_t)(lane - off) >= seg;
-#pragma unroll
-        for (int i = 0; i <= MF_D; i++) {
-            const uint32_t o = __shfl_up(v[i], off);
-            v[i] += take ? o : 0u;
-        }
-    }
     const uint32_t next = __shfl_down(key, 1);
+    const uint32_t head = wave_scan_max((lane == 0 || prev != key) ? (uint32_t)lane : 0u);
+    const int src = head == 0 ? 0 : (int)head - 1;
+#pragma unroll
+    for (int i = 0; i <= MF_D; i++) {
+        const uint32_t pre = wave_scan_add(v[i]);
+        const uint32_t before = __shfl(pre, src);
+        v[i] = pre - (head == 0 ? 0u : before);
+    }
     return lane == 63 || next != key;
 }
 
@@ -150,6 +170,10 @@ __global__ __launch_bounds__(MF_THREADS) void assign_mfma_kernel(
     const f32x4 zero = {0.f, 0.f, 0.f, 0.f};
     // k-slot words of a row for B: g=0 bytes 0-7, g=1 bytes 8-11 then 0-3, g=2 bytes 4-11
     const int wa = g == 0 ? 0 : (g == 1 ? 2 : 1), wb = g == 0 ? 1 : (g == 1 ? 0 : 2);
+    // word selects as masks: a ternary over q[t][*] becomes a lane-varying index into a
+    // private array, which the compiler keeps in scratch memory
+    const uint32_t ma0 = 0u - (wa == 0), ma1 = 0u - (wa == 1), ma2 = 0u - (wa == 2);
+    const uint32_t mb0 = 0u - (wb == 0), mb1 = 0u - (wb == 1), mb2 = 0u - (wb == 2);
     // A fragment of tile t: 16 B of code vector t*16 + c at byte 16g of its row (g = 3
     // reads n_hi, n_lo, 0, 0 and 8 bytes of the next row, which meet zeros in B).
     const unsigned char *a_base = rows + (size_t)c * MF_ROW_BYTES + 16 * g;
@@ -195,8 +219,8 @@ __global__ __launch_bounds__(MF_THREADS) void assign_mfma_kernel(
                 own[1] = q[t][1];
                 own[2] = q[t][2];
             }
-            const uint32_t ua = wa == 0 ? q[t][0] : (wa == 1 ? q[t][1] : q[t][2]);
-            const uint32_t ub = wb == 0 ? q[t][0] : (wb == 1 ? q[t][1] : q[t][2]);
+            const uint32_t ua = (q[t][0] & ma0) | (q[t][1] & ma1) | (q[t][2] & ma2);
+            const uint32_t ub = (q[t][0] & mb0) | (q[t][1] & mb1) | (q[t][2] & mb2);
             if (g < 3) {
 #pragma unroll
                 for (int j = 0; j < 4; j++) {
@@ -288,8 +312,12 @@ __global__ __launch_bounds__(MF_THREADS) void assign_mfma_kernel(
             }
             float r1 = INFINITY, r2 = INFINITY;
             const uint32_t pr = unit >> 2, gg = unit & 3;
+            // a unit is 4 code vectors of each tile of its pair; up to K = 16 the second
+            // tile is padding, and below 4 so is the rest of the first
+            const int jn = K <= 16 ? (K < 4 ? (int)K : 4) : 8;
 #pragma unroll
             for (int j = 0; j < 8; j++) {
+                if (j >= jn) continue;   // uniform: K is
                 const uint32_t cv = (2 * pr + (j >> 2)) * 16 + 4 * gg + (j & 3);
                 const float4 *c4 = reinterpret_cast<const float4 *>(C32 + (size_t)cv * MF_D);
                 float dist = 0.f;
@@ -512,7 +540,7 @@ hipError_t launch_assign_valu(hipStream_t s, int num_cu, uint32_t Dp, const uint
 // gets the fp64 argmin (lowest index on exact ties); rows whose two best fp64 distances are
 // within tie_rel go to the host kd-tree.  With sums != nullptr the resolved rows' exact
 // terms are added to the global sums (the fused search skipped them).
-constexpr int RECHECK_THREADS = 512;
+constexpr int RECHECK_THREADS = 1024;
 constexpr int RECHECK_WAVES = RECHECK_THREADS / 64;
 constexpr size_t RECHECK_LDS = 160 * 1024;
 
@@ -520,36 +548,22 @@ constexpr size_t RECHECK_LDS = 160 * 1024;
 // group, each on a different code vector, hit different banks.
 __host__ __device__ inline uint32_t recheck_stride(uint32_t D) { return D | 1u; }
 
-// LDS of the recheck without the staged codebook: row + traversal dists, kd stacks.
-size_t recheck_lds_base(int depth) {
-    return (size_t)RECHECK_WAVES * 128 * 8 + (((size_t)RECHECK_WAVES * depth * KD_FRAME_BYTES + 7) & ~(size_t)7);
-}
-
-int recheck_max_kd_depth() {
-    return (int)((RECHECK_LDS - (size_t)RECHECK_WAVES * 128 * 8) / ((size_t)RECHECK_WAVES * KD_FRAME_BYTES));
-}
-
-// fp64 recheck of flagged rows in the reference's distance order.  Rows whose best and
-// second distances are within tie_rel are exact ties for the reference: with a device tree
-// they are answered by its traversal here, otherwise listed for the host (ties).
+// fp64 recheck of flagged rows in the reference's distance order (ref_l2_hd).  Rows whose
+// best and second distances are within tie_rel are exact ties for the reference: they are
+// listed in ties (A gets the lowest index for now) and left to kd_resolve_kernel or the host.
 template <bool STAGED>
 __global__ __launch_bounds__(RECHECK_THREADS) void recheck_kernel(
     const uint8_t *__restrict__ codes, uint32_t Dp, uint32_t D, const uint32_t *__restrict__ flags,
     const unsigned int *__restrict__ flag_cnt, const double *__restrict__ g_C64, uint32_t K,
-    const double *__restrict__ lut64, double tie_rel, KdView kd, uint32_t *__restrict__ A,
-    uint32_t *__restrict__ ties, unsigned int *__restrict__ tie_cnt, uint64_t *__restrict__ sums,
-    const uint64_t *__restrict__ plut) {
+    const double *__restrict__ lut64, double tie_rel, uint32_t *__restrict__ A, uint32_t *__restrict__ ties,
+    unsigned int *__restrict__ tie_cnt, uint64_t *__restrict__ sums, const uint64_t *__restrict__ plut) {
     extern __shared__ __attribute__((aligned(16))) double rsm[];
     constexpr int W = RECHECK_WAVES;
-    const int Z = kd.depth;                                         // stack frames per wave
-    double *xs = rsm;                                               // [W][64]
-    double *kdd = xs + W * 64;                                      // [W][64] traversal dists
-    double *sd = kdd + W * 64;                                      // [W][Z]
-    int32_t *sn = reinterpret_cast<int32_t *>(sd + W * Z);          // [W][Z]
-    double *cbs = rsm + W * 128 + ((size_t)W * Z * KD_FRAME_BYTES + 7) / 8;   // [K][stride] when staged
+    double *xs = rsm;            // [W][64]
+    double *cbs = rsm + W * 64;  // [K][stride] when staged
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const unsigned nflag = *flag_cnt;
-    if (nflag == 0) return;
+    if (nflag == 0 || blockIdx.x * W >= nflag) return;
     const uint32_t S = STAGED ? recheck_stride(D) : D;
     if (STAGED) {
         for (uint32_t i = threadIdx.x; i < K * D; i += RECHECK_THREADS) {
@@ -592,23 +606,11 @@ __global__ __launch_bounds__(RECHECK_THREADS) void recheck_kernel(
                 d2 = fmin(d2, od1);
             }
         }
-        const bool tie = d2 - d1 <= tie_rel * d1;
-        if (tie) {
-            if (kd.depth > 0) {
-                uint32_t kk = 0;
-                if (lane == 0)
-                    kk = kd_nearest_flat(xs + wave * 64, D, kd, C64, S, sd + wave * Z, sn + wave * Z, kdd + wave * 64);
-                k1 = __shfl(kk, 0);
-                if (lane == 0) atomicAdd(tie_cnt, 1u);
-            } else {
-                if (lane == 0) {
-                    A[row] = k1;
-                    ties[atomicAdd(tie_cnt, 1u)] = row;
-                }
-                continue;   // the host adds this row (resolve_host_ties)
-            }
-        }
         if (lane == 0) A[row] = k1;
+        if (d2 - d1 <= tie_rel * d1) {
+            if (lane == 0) ties[atomicAdd(tie_cnt, 1u)] = row;
+            continue;
+        }
         if (sums && lane < (int)D) {
             const uint64_t KD = (uint64_t)K * D;
             const uint64_t p = plut[codes[(uint64_t)row * Dp + lane]];
@@ -621,19 +623,184 @@ __global__ __launch_bounds__(RECHECK_THREADS) void recheck_kernel(
 
 hipError_t launch_recheck(hipStream_t s, int num_cu, const uint8_t *codes, uint32_t Dp, uint32_t D,
                           const uint32_t *flags, const unsigned *flag_cnt, const double *C64, uint32_t K,
-                          const double *lut64, double tie_rel, const KdView &kd, uint32_t *A, uint32_t *ties,
-                          unsigned *tie_cnt, uint64_t *sums, const uint64_t *plut) {
-    const size_t base = recheck_lds_base(kd.depth);
-    if (base > RECHECK_LDS) return hipErrorInvalidValue;
+                          const double *lut64, double tie_rel, uint32_t *A, uint32_t *ties, unsigned *tie_cnt,
+                          uint64_t *sums, const uint64_t *plut) {
+    const size_t base = (size_t)RECHECK_WAVES * 64 * 8;
     const size_t cb = (size_t)K * recheck_stride(D) * 8;
     const bool staged = base + cb <= RECHECK_LDS;
     const size_t lds = base + (staged ? cb : 0);
     if (staged)
         hipLaunchKernelGGL(recheck_kernel<true>, dim3(num_cu), dim3(RECHECK_THREADS), lds, s, codes, Dp, D, flags,
-                           flag_cnt, C64, K, lut64, tie_rel, kd, A, ties, tie_cnt, sums, plut);
+                           flag_cnt, C64, K, lut64, tie_rel, A, ties, tie_cnt, sums, plut);
     else
         hipLaunchKernelGGL(recheck_kernel<false>, dim3(num_cu), dim3(RECHECK_THREADS), lds, s, codes, Dp, D, flags,
-                           flag_cnt, C64, K, lut64, tie_rel, kd, A, ties, tie_cnt, sums, plut);
+                           flag_cnt, C64, K, lut64, tie_rel, A, ties, tie_cnt, sums, plut);
+    return hipGetLastError();
+}
+
+// kd_nearest_flat with the leaf scan spread over the wave: every lane runs the same
+// descent (uniform values), lane i takes leaf point i, and the leaf's winner is the first
+// point in leaf order with the smallest distance below the leaf-entry worst -- what the
+// sequential strict-'<' scan picks.  Leaves hold at most 10 points (< 64 lanes).
+__device__ uint32_t kd_nearest_wave(const double *q, uint32_t D, const KdView &t, const double *pts, uint32_t S,
+                                    double *sd, int32_t *sn, double *dl, int lane) {
+    double distsq = 0;   // dl: per-dimension cell distances (LDS, uniform across lanes)
+    for (uint32_t d = 0; d < D; d++) {
+        const double x = q[d];
+        dl[d] = 0;
+        if (x < t.lo[d]) {
+            dl[d] = (x - t.lo[d]) * (x - t.lo[d]);
+            distsq += dl[d];
+        }
+        if (x > t.hi[d]) {
+            dl[d] = (x - t.hi[d]) * (x - t.hi[d]);
+            distsq += dl[d];
+        }
+    }
+    double best = 1.7976931348623157e308;
+    uint32_t best_idx = 0;
+    int sp = 0;
+    sd[0] = distsq;
+    sn[0] = 0;
+    while (sp >= 0) {
+        const int32_t node = sn[sp] >> 2, phase = sn[sp] & 3;
+        const KdNodeDev n = t.nodes[node];
+        if (n.child1 < 0) {
+            const double worst = best;
+            const int32_t cnt = n.b - n.a;
+            double dist = INFINITY;
+            int32_t pos = 0x7FFFFFFF;
+            if (lane < cnt) {
+                const double dd = ref_l2_hd(q, pts + (uint64_t)t.vind[n.a + lane] * S, (int)D);
+                if (dd < worst) {
+                    dist = dd;
+                    pos = lane;
+                }
+            }
+#pragma unroll
+            for (int off = 1; off < 64; off <<= 1) {
+                const double od = __shfl_xor(dist, off);
+                const int32_t op = __shfl_xor(pos, off);
+                if (od < dist || (od == dist && op < pos)) {
+                    dist = od;
+                    pos = op;
+                }
+            }
+            if (pos != 0x7FFFFFFF) {
+                best = dist;
+                best_idx = t.vind[n.a + pos];
+            }
+            sp--;
+            continue;
+        }
+        const int f = n.a;
+        const double val = q[f];
+        const double diff1 = val - n.lo, diff2 = val - n.hi;
+        const bool left_first = (diff1 + diff2) < 0;
+        if (phase == 0) {
+            sn[sp] = node << 2 | 1;
+            sd[sp + 1] = sd[sp];
+            sn[sp + 1] = (left_first ? n.child1 : n.child2) << 2;
+            sp++;
+            continue;
+        }
+        if (phase == 1) {
+            const double cut_dist = left_first ? (val - n.hi) * (val - n.hi) : (val - n.lo) * (val - n.lo);
+            const double dst = dl[f];
+            const double m2 = (sd[sp] - dst) + cut_dist;
+            dl[f] = cut_dist;
+            sd[sp] = dst;
+            sn[sp] = node << 2 | 2;
+            if (m2 <= best) {
+                sd[sp + 1] = m2;
+                sn[sp + 1] = (left_first ? n.child2 : n.child1) << 2;
+                sp++;
+                continue;
+            }
+        }
+        dl[f] = sd[sp];
+        sp--;
+    }
+    return best_idx;
+}
+
+// Exact ties listed by the recheck, answered by the reference kd-tree traversal
+// (kd_nearest_flat).  The tree image (kd.lo .. ) lives in mapped pinned host memory and is
+// staged into LDS by each block that has tie rows; one lane per wave walks it.
+constexpr int KDR_THREADS = 1024;
+constexpr int KDR_WAVES = KDR_THREADS / 64;
+constexpr int KDR_BLOCKS = 32;
+
+size_t kd_resolve_lds(const KdView &kd) {
+    return (size_t)KDR_WAVES * 128 * 8 + (((size_t)KDR_WAVES * kd.depth * KD_FRAME_BYTES + 7) & ~(size_t)7) +
+           (((size_t)kd.bytes + 7) & ~(size_t)7);
+}
+
+bool kd_resolve_fits(const KdView &kd) { return kd.depth > 0 && kd_resolve_lds(kd) <= RECHECK_LDS; }
+
+template <bool STAGED>
+__global__ __launch_bounds__(KDR_THREADS) void kd_resolve_kernel(
+    const uint8_t *__restrict__ codes, uint32_t Dp, uint32_t D, const uint32_t *__restrict__ ties,
+    const unsigned *__restrict__ tie_cnt, const double *__restrict__ g_C64, uint32_t K,
+    const double *__restrict__ lut64, KdView kd, uint32_t *__restrict__ A, uint64_t *__restrict__ sums,
+    const uint64_t *__restrict__ plut) {
+    extern __shared__ __attribute__((aligned(16))) double ksm[];
+    constexpr int W = KDR_WAVES;
+    const int Z = kd.depth;
+    double *xs = ksm;                                              // [W][64]
+    double *dl = xs + W * 64;                                      // [W][64]
+    double *sd = dl + W * 64;                                      // [W][Z]
+    int32_t *sn = reinterpret_cast<int32_t *>(sd + W * Z);         // [W][Z]
+    double *tr = ksm + W * 128 + ((size_t)W * Z * KD_FRAME_BYTES + 7) / 8;
+    double *cbs = tr + (kd.bytes + 7) / 8;                         // [K][stride] when STAGED
+    const unsigned nt = *tie_cnt;
+    if (blockIdx.x * W >= nt) return;
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    for (uint32_t i = threadIdx.x; i < (kd.bytes + 7) / 8; i += KDR_THREADS) tr[i] = kd.lo[i];
+    const uint32_t S = STAGED ? recheck_stride(D) : D;
+    if (STAGED)
+        for (uint32_t i = threadIdx.x; i < K * D; i += KDR_THREADS) {
+            const uint32_t k = i / D, d = i - k * D;
+            cbs[k * S + d] = g_C64[i];
+        }
+    KdView kv = kd;
+    kv.lo = tr;
+    kv.hi = tr + D;
+    kv.nodes = reinterpret_cast<const KdNodeDev *>(tr + 2 * D);
+    kv.vind = reinterpret_cast<const uint32_t *>(kv.nodes + kd.n_nodes);
+    __syncthreads();
+    const double *C64 = STAGED ? cbs : g_C64;
+    for (unsigned f = blockIdx.x * W + wave; f < nt; f += gridDim.x * W) {
+        const uint32_t row = ties[f];
+        if (lane < (int)D) xs[wave * 64 + lane] = lut64[codes[(uint64_t)row * Dp + lane]];
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        const uint32_t k = kd_nearest_wave(xs + wave * 64, D, kv, C64, S, sd + wave * Z, sn + wave * Z,
+                                           dl + wave * 64, lane);
+        if (lane == 0) A[row] = k;
+        if (sums && lane < (int)D) {
+            const uint64_t KD = (uint64_t)K * D;
+            const uint64_t p = plut[codes[(uint64_t)row * Dp + lane]];
+            atomicAdd((unsigned long long *)&sums[(uint64_t)lane * K + k], (unsigned long long)(p >> 32));
+            atomicAdd((unsigned long long *)&sums[KD + (uint64_t)lane * K + k], (unsigned long long)(p & 0xFFFFFFFFull));
+            if (lane == 0) atomicAdd((unsigned long long *)&sums[2 * KD + k], 1ull);
+        }
+        __builtin_amdgcn_wave_barrier();
+    }
+}
+
+hipError_t launch_kd_resolve(hipStream_t s, const uint8_t *codes, uint32_t Dp, uint32_t D, const uint32_t *ties,
+                             const unsigned *tie_cnt, const double *C64, uint32_t K, const double *lut64,
+                             const KdView &kd, uint32_t *A, uint64_t *sums, const uint64_t *plut) {
+    if (!kd_resolve_fits(kd)) return hipErrorInvalidValue;
+    const size_t base = kd_resolve_lds(kd), cb = (size_t)K * recheck_stride(D) * 8;
+    if (base + cb <= RECHECK_LDS)
+        hipLaunchKernelGGL(kd_resolve_kernel<true>, dim3(KDR_BLOCKS), dim3(KDR_THREADS), base + cb, s, codes, Dp, D,
+                           ties, tie_cnt, C64, K, lut64, kd, A, sums, plut);
+    else
+        hipLaunchKernelGGL(kd_resolve_kernel<false>, dim3(KDR_BLOCKS), dim3(KDR_THREADS), base, s, codes, Dp, D, ties,
+                           tie_cnt, C64, K, lut64, kd, A, sums, plut);
     return hipGetLastError();
 }
 

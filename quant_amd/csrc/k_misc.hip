@@ -260,70 +260,179 @@ hipError_t launch_mean_sums(hipStream_t s, uint32_t Dp, const uint8_t *codes, ui
     return hipErrorInvalidValue;
 }
 
-// Centroids from the reduced sums; optionally the next level's split codebook
-// (src/Quantizer.cpp:134-138: concat, then x(1+0.2) and x(1-0.2)) in fp64.
-__global__ void finalize_kernel(const uint64_t *__restrict__ sums, uint32_t K, uint32_t D, int64_t R, int64_t bias,
-                                int scale, double *__restrict__ C_cent, int split, double *__restrict__ C64n) {
+// finalize (src/Quantizer.cpp:79-94 fixCodebook + :129-138 split) fused with the next
+// level's search tables.  Block = 256/L rows x L component lanes.  With split, row j < 2K is
+// split code vector j (cluster j mod K, factor 1.2 for j < K, 0.8 above) and rows
+// 2K..Kpad_next-1 are padding; the split codebook also goes to host_cb (mapped pinned
+// memory, for the host's kd-tree build).  L = 16, 32 or 64 lanes per row (>= Dp).  Without split (last level) row k < K writes
+// centroid k and its distortion term sum_d (2 c S - n c^2).  The last block to finish sums
+// the per-block distortion terms in block order and then publishes *ready = seq (system
+// scope), which tells the host that host_cb holds the codebook.
+
+__global__ __launch_bounds__(256) void finalize_prep_kernel(
+    const uint64_t *__restrict__ sums, uint32_t K, uint32_t D, uint32_t Dp, int64_t R, int64_t bias, int scale,
+    double *__restrict__ C_cent, int split, double *__restrict__ C64n, uint32_t Kpad_next, double mu, double sx,
+    double scale_t, float *__restrict__ C32, _Float16 *__restrict__ rows, double *__restrict__ host_cb,
+    double *__restrict__ dist_part, unsigned *__restrict__ done, double *__restrict__ dist_out,
+    volatile uint64_t *ready, uint64_t seq, uint32_t L) {
     const uint64_t KD = (uint64_t)K * D;
-    for (uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; t < KD; t += (uint64_t)gridDim.x * blockDim.x) {
-        const uint64_t k = t / D, d = t - k * D;
-        const uint64_t c = d * K + k;
-        const double v = centroid_value(sums[c], sums[KD + c], sums[2 * KD + k], R, bias, scale);
-        C_cent[t] = v;
-        if (split) {
-            C64n[t] = v * (double)(1 + 0.2);
-            C64n[KD + t] = v * (double)(1 - 0.2);
+    const uint32_t d = threadIdx.x % L, r = threadIdx.x / L;
+    const uint32_t j = blockIdx.x * (256 / L) + r;
+    double term = 0;
+    if (split) {
+        if (j < 2 * K) {
+            const uint32_t k = j < K ? j : j - K;
+            double v = 0;
+            if (d < D) {
+                const uint64_t c = (uint64_t)d * K + k;
+                const double cv = centroid_value(sums[c], sums[KD + c], sums[2 * KD + k], R, bias, scale);
+                if (j < K) C_cent[(uint64_t)k * D + d] = cv;
+                v = cv * (j < K ? (double)(1 + 0.2) : (double)(1 - 0.2));
+                C64n[(uint64_t)j * D + d] = v;
+                if (host_cb) host_cb[(uint64_t)j * D + d] = v;
+            }
+            if (d < Dp) C32[(uint64_t)j * Dp + d] = (float)v;
+            if (D == MF_D) {
+                _Float16 *row = rows + (uint64_t)j * MF_ROW_F16;
+                const double cp = d < D ? v - mu : 0.0;
+                double n = cp * cp;   // L == 16 here
+#pragma unroll
+                for (int off = 8; off >= 1; off >>= 1) n += __shfl_xor(n, off, 16);
+                if (d < D) {
+                    const double c2 = -2.0 * sx * cp * scale_t;
+                    const _Float16 h = (_Float16)(float)c2;
+                    row[d] = h;
+                    row[MF_D + d] = (_Float16)(float)(c2 - (double)(float)h);
+                } else if (d == MF_D) {
+                    n *= scale_t;
+                    const _Float16 h = (_Float16)(float)n;
+                    row[2 * MF_D] = h;
+                    row[2 * MF_D + 1] = (_Float16)(float)(n - (double)(float)h);
+                    row[2 * MF_D + 2] = (_Float16)0.f;
+                    row[2 * MF_D + 3] = (_Float16)0.f;
+                }
+            }
+        } else if (j < Kpad_next) {
+            if (d < Dp) C32[(uint64_t)j * Dp + d] = 0.f;
+            if (D == MF_D) {
+                _Float16 *row = rows + (uint64_t)j * MF_ROW_F16;
+                for (uint32_t i = d; i < (uint32_t)MF_ROW_F16; i += L)
+                    row[i] = (_Float16)(i == 2 * MF_D || i == 2 * MF_D + 1 ? MF_PAD_SCORE : 0.f);
+            }
+        }
+    } else if (j < K && d < D) {
+        const uint64_t c = (uint64_t)d * K + j;
+        const uint64_t cnt = sums[2 * KD + j];
+        const double cv = centroid_value(sums[c], sums[KD + c], cnt, R, bias, scale);
+        C_cent[(uint64_t)j * D + d] = cv;
+        if (dist_out && cnt) {
+            const __int128 Sq =
+                (__int128)R * (__int128)sums[c] + (__int128)sums[KD + c] - (__int128)bias * (__int128)cnt;
+            const double S = ldexp(i128_to_double(Sq), -scale);
+            term = 2.0 * cv * S - (double)cnt * cv * cv;
+        }
+    }
+    if (!done) return;
+    __shared__ double red[256];
+    __shared__ bool last;
+    red[threadIdx.x] = term;
+    __threadfence_system();
+    __syncthreads();
+    for (int w = 128; w > 0; w >>= 1) {
+        if ((int)threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        dist_part[blockIdx.x] = red[0];
+        __threadfence();
+        last = atomicAdd(done, 1u) == gridDim.x - 1;
+    }
+    __syncthreads();
+    if (last && threadIdx.x == 0) {
+        __threadfence();
+        if (dist_out) {
+            double t = 0;
+            for (uint32_t b = 0; b < gridDim.x; b++) t += __builtin_nontemporal_load(&dist_part[b]);
+            dist_out[0] = t;
+        }
+        *done = 0;
+        if (ready) {
+            __threadfence_system();
+            *ready = seq;
         }
     }
 }
 
-hipError_t launch_finalize(hipStream_t s, const uint64_t *sums, uint32_t K, uint32_t D, int64_t R, int64_t bias,
-                           int scale, double *C_cent, bool split, double *C64n) {
-    const uint64_t n = (uint64_t)K * D;
-    hipLaunchKernelGGL(finalize_kernel, dim3((int)std::min<uint64_t>((n + 255) / 256, 4096)), dim3(256), 0, s, sums, K,
-                       D, R, bias, scale, C_cent, split ? 1 : 0, C64n);
+hipError_t launch_finalize_prep(hipStream_t s, const uint64_t *sums, uint32_t K, uint32_t D, uint32_t Dp, int64_t R,
+                                int64_t bias, int scale, double *C_cent, bool split, double *C64n, uint32_t Kpad_next,
+                                double mu, double sx, int t, float *C32, _Float16 *cb_rows, double *host_cb,
+                                double *dist_part, unsigned *done, double *dist_out, uint64_t *ready, uint64_t seq) {
+    if (D == 0 || D > 64) return hipErrorInvalidValue;
+    const uint32_t L = D <= 16 ? 16 : (D <= 32 ? 32 : 64);
+    const uint32_t n = split ? std::max(2 * K, Kpad_next) : K;
+    const uint32_t grid = (n + 256 / L - 1) / (256 / L);
+    if (done && grid > 8000) return hipErrorInvalidValue;   // dist_part capacity
+    hipLaunchKernelGGL(finalize_prep_kernel, dim3(grid), dim3(256), 0, s, sums, K, D, Dp, R, bias, scale, C_cent,
+                       split ? 1 : 0, C64n, Kpad_next, mu, sx, std::ldexp(1.0, t), C32, cb_rows, host_cb, dist_part,
+                       done, dist_out, (volatile uint64_t *)ready, seq, L);
     return hipGetLastError();
+}
+
+// finalize without the tables (qvq_update): C_cent only.
+hipError_t launch_finalize(hipStream_t s, const uint64_t *sums, uint32_t K, uint32_t D, int64_t R, int64_t bias,
+                           int scale, double *C_cent) {
+    return launch_finalize_prep(s, sums, K, D, (D + 3) & ~3u, R, bias, scale, C_cent, false, nullptr, 0, 0, 0, 0,
+                                nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, 0);
 }
 
 // Search tables from an fp64 codebook: fp32 [Kpad][Dp] (VALU path and the MFMA recompute)
 // and, for D = 12, the f16 MFMA rows (common.hpp).  Code vectors K..Kpad-1 are padding
 // that never wins.
+__device__ inline void prep_row(const double *v, uint32_t D, uint32_t Dp, double mu, double sx, double scale_t,
+                                float *__restrict__ c32, _Float16 *__restrict__ r) {
+    double n = 0;
+    for (uint32_t d = 0; d < Dp; d++) {
+        const double x = d < D ? v[d] : 0.0;
+        c32[d] = (float)x;
+        if (D == MF_D && d < D) {
+            const double cp = x - mu;
+            n += cp * cp;
+            const double c2 = -2.0 * sx * cp * scale_t;
+            const _Float16 h = (_Float16)(float)c2;
+            r[d] = h;
+            r[MF_D + d] = (_Float16)(float)(c2 - (double)(float)h);
+        }
+    }
+    if (D == MF_D) {
+        n *= scale_t;
+        const _Float16 h = (_Float16)(float)n;
+        r[2 * MF_D] = h;
+        r[2 * MF_D + 1] = (_Float16)(float)(n - (double)(float)h);
+        r[2 * MF_D + 2] = (_Float16)0.f;
+        r[2 * MF_D + 3] = (_Float16)0.f;
+    }
+}
+
+__device__ inline void prep_pad_row(uint32_t D, uint32_t Dp, float *__restrict__ c32, _Float16 *__restrict__ r) {
+    for (uint32_t d = 0; d < Dp; d++) c32[d] = 0.f;
+    if (D == MF_D) {
+        for (int j = 0; j < MF_ROW_F16; j++) r[j] = (_Float16)0.f;
+        r[2 * MF_D] = (_Float16)MF_PAD_SCORE;
+        r[2 * MF_D + 1] = (_Float16)MF_PAD_SCORE;
+    }
+}
+
 __global__ void prep_kernel(const double *__restrict__ C64, uint32_t K, uint32_t Kpad, uint32_t D, uint32_t Dp,
                             double mu, double sx, double scale_t, float *__restrict__ C32,
                             _Float16 *__restrict__ rows) {
     for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < Kpad; k += gridDim.x * blockDim.x) {
-        _Float16 *r = rows + (uint64_t)k * MF_ROW_F16;
         if (k >= K) {
-            for (uint32_t d = 0; d < Dp; d++) C32[(uint64_t)k * Dp + d] = 0.f;
-            if (D == MF_D) {
-                for (int j = 0; j < MF_ROW_F16; j++) r[j] = (_Float16)0.f;
-                r[2 * MF_D] = (_Float16)MF_PAD_SCORE;
-                r[2 * MF_D + 1] = (_Float16)MF_PAD_SCORE;
-            }
+            prep_pad_row(D, Dp, C32 + (uint64_t)k * Dp, rows + (uint64_t)k * MF_ROW_F16);
             continue;
         }
-        const double *c = C64 + (uint64_t)k * D;
-        double n = 0;
-        for (uint32_t d = 0; d < Dp; d++) {
-            const double v = d < D ? c[d] : 0.0;
-            C32[(uint64_t)k * Dp + d] = (float)v;
-            if (D == MF_D && d < D) {
-                const double cp = v - mu;
-                n += cp * cp;
-                const double c2 = -2.0 * sx * cp * scale_t;
-                const _Float16 h = (_Float16)(float)c2;
-                r[d] = h;
-                r[MF_D + d] = (_Float16)(float)(c2 - (double)(float)h);
-            }
-        }
-        if (D == MF_D) {
-            n *= scale_t;
-            const _Float16 h = (_Float16)(float)n;
-            r[2 * MF_D] = h;
-            r[2 * MF_D + 1] = (_Float16)(float)(n - (double)(float)h);
-            r[2 * MF_D + 2] = (_Float16)0.f;
-            r[2 * MF_D + 3] = (_Float16)0.f;
-        }
+        double v[64];
+        for (uint32_t d = 0; d < D; d++) v[d] = C64[(uint64_t)k * D + d];
+        prep_row(v, D, Dp, mu, sx, scale_t, C32 + (uint64_t)k * Dp, rows + (uint64_t)k * MF_ROW_F16);
     }
 }
 
@@ -396,42 +505,6 @@ hipError_t launch_byte_hist(hipStream_t s, const uint8_t *codes, uint64_t N, uin
     hipError_t e = hipMemsetAsync(hist, 0, 256 * 8, s);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(byte_hist_kernel, dim3(1024), dim3(256), 0, s, codes, N, D, Dp, (unsigned long long *)hist);
-    return hipGetLastError();
-}
-
-// updateDistortion (src/Quantizer.cpp:9-22) in closed form from the exact sums of the final
-// assignment: sum_i ||x_i - c_A(i)||^2 = sum_i ||x_i||^2 - sum_k (2 c_k.S_k - n_k ||c_k||^2).
-// One workgroup, fixed-order tree; out[0] = the subtracted sum.
-constexpr int DCF_THREADS = 1024;
-__global__ __launch_bounds__(DCF_THREADS) void distortion_cf_kernel(const uint64_t *__restrict__ sums, uint32_t K,
-                                                                    uint32_t D, int64_t R, int64_t bias, int scale,
-                                                                    const double *__restrict__ C,
-                                                                    double *__restrict__ out) {
-    __shared__ double red[DCF_THREADS];
-    const uint64_t KD = (uint64_t)K * D;
-    double acc = 0;
-    for (uint64_t t = threadIdx.x; t < KD; t += DCF_THREADS) {
-        const uint64_t k = t / D, d = t - k * D, col = d * K + k;
-        const uint64_t n = sums[2 * KD + k];
-        if (n == 0) continue;
-        const __int128 Sq =
-            (__int128)R * (__int128)sums[col] + (__int128)sums[KD + col] - (__int128)bias * (__int128)n;
-        const double S = ldexp(i128_to_double(Sq), -scale);
-        const double c = C[t];
-        acc += 2.0 * c * S - (double)n * c * c;
-    }
-    red[threadIdx.x] = acc;
-    __syncthreads();
-    for (int w = DCF_THREADS / 2; w > 0; w >>= 1) {
-        if ((int)threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
-        __syncthreads();
-    }
-    if (threadIdx.x == 0) out[0] = red[0];
-}
-
-hipError_t launch_distortion_cf(hipStream_t s, const uint64_t *sums, uint32_t K, uint32_t D, int64_t R, int64_t bias,
-                                int scale, const double *C, double *out) {
-    hipLaunchKernelGGL(distortion_cf_kernel, dim3(1), dim3(DCF_THREADS), 0, s, sums, K, D, R, bias, scale, C, out);
     return hipGetLastError();
 }
 

@@ -45,6 +45,8 @@ struct KdView {
     const uint32_t *vind = nullptr;
     const double *lo = nullptr, *hi = nullptr;   // root bounding box
     int depth = 0;                               // 0: no device tree (host resolves ties)
+    uint32_t n_nodes = 0;
+    uint32_t bytes = 0;   // contiguous image lo[D] | hi[D] | nodes | vind starting at lo
 };
 
 // Device stack frames are 12 bytes: one double (the cell bound mindistsq, replaced by the

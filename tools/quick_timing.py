@@ -20,4 +20,5 @@ for (S, bw, bits) in cases:
     print(json.dumps({"S": S, "bw": bw, "bits": bits, "wall_ms": round(dt * 1e3, 3), "total_ms": round(tm["total_ms"], 3),
                       "assign_ms": [round(x, 4) for x in tm["assign_ms"]],
                       "update_ms": [round(x, 4) for x in tm["update_ms"]],
+                      "other_ms": [round(x, 4) for x in tm["other_ms"]],
                       "flagged": tm["flagged"], "host_ties": tm["host_ties"]}), flush=True)
