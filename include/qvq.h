@@ -49,7 +49,8 @@ typedef enum {
  * can sum exactly; CIE1931 is rejected with QVQ_EUNSUPPORTED. */
 enum { QVQ_CS_NORMAL = 0, QVQ_CS_SCALED = 1, QVQ_CS_CIE1931 = 2 };
 
-/* Per-level / per-call timings filled by qvq_get_timings (device ms from HIP events). */
+/* Per-level / per-call timings filled by qvq_get_timings (device ms from HIP events
+ * recorded around each level's search kernel on the context's stream). */
 typedef struct {
     int levels;                 /* split levels run by the last qvq_lbg */
     double total_ms;            /* whole qvq_lbg, host wall */
@@ -57,7 +58,8 @@ typedef struct {
     double update_ms[32];       /* device time of the centroid-sum kernel per level */
     double other_ms[32];        /* rest of the level: recheck, kd-tree ties, reduce, finalize + tables */
     uint64_t flagged[32];       /* rows re-checked in fp64 per level */
-    uint64_t host_ties[32];     /* rows resolved by the host kd-tree per level */
+    uint64_t host_ties[32];     /* exact fp64 ties per level, answered by the reference kd-tree
+                                   traversal (device kernel; host only for trees too deep) */
 } qvq_timings;
 
 /* Context: one per GPU per host thread.  Owns device memory and one HIP stream. */
@@ -110,7 +112,7 @@ QVQ_API const uint32_t *qvq_assign_device(const qvq_ctx *ctx);
 
 /* Single steps over the current training set, for tests and benchmarks.
  * qvq_assign: nearest code vector of every row for codebook C (K x dim fp64, host),
- *   with the same fp32 search + fp64 recheck + host kd-tree tie resolution as qvq_lbg.
+ *   with the same MFMA/VALU search + fp64 recheck + kd-tree tie resolution as qvq_lbg.
  * qvq_update: centroids of the rows under assignment A (host, n u32) into C_out
  *   (K x dim fp64) and counts (K u64), the engine's exact-sum rule. */
 QVQ_API qvq_status qvq_assign(qvq_ctx *ctx, const double *C, uint32_t K, uint32_t *assign);

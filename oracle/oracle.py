@@ -153,3 +153,28 @@ def codebook_bytes(C, cs=SCALED):
     out = np.empty(C.shape, np.uint8)
     lib().orc_codebook_bytes(_p(C), C.shape[0], C.shape[1], cs, _p(out))
     return out
+
+
+def quant_file_bytes(cb_bytes, A, bits, cs, xs, ys, bw, bh):
+    """CompressedImage::saveToFile (src/Compressor.cpp:191-224) restated: ASCII header
+    'bits colorSpace count xSize ySize bw bh\\n', 2^bits x (bw*bh*3) codebook bytes, then
+    count indices of ceil(bits/8) little-endian bytes.  colorSpace is written as the real
+    enum value (the reference leaves CompressedImage::colorSpace unset)."""
+    A = np.asarray(A, np.uint64)
+    nb = (bits + 7) // 8
+    hdr = ("%d %d %d %d %d %d %d\n" % (bits, cs, len(A), xs, ys, bw, bh)).encode()
+    idx = np.stack([((A >> np.uint64(8 * b)) & np.uint64(0xFF)).astype(np.uint8) for b in range(nb)], axis=1)
+    return hdr + np.ascontiguousarray(cb_bytes, np.uint8).tobytes() + idx.tobytes()
+
+
+def decode(cb_bytes, A, xs, ys, bw, bh):
+    """CompressedImage::decompress (src/Compressor.cpp:156-165): gather + untile."""
+    blocks = np.ascontiguousarray(cb_bytes, np.uint8)[np.asarray(A, np.int64)]
+    return untile(blocks, xs, ys, bw, bh)
+
+
+def raport_distortion(rgb, dec):
+    """src/Compressor.cpp:133-144: mean squared difference of the signed bytes."""
+    a = np.asarray(rgb, np.uint8).view(np.int8).astype(np.float64)
+    b = np.asarray(dec, np.uint8).view(np.int8).astype(np.float64)
+    return float(np.mean((a - b) ** 2))

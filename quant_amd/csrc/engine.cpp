@@ -649,7 +649,7 @@ QVQ_API qvq_status qvq_set_vectors(qvq_ctx *ctx, const double *X, uint64_t n, ui
             for (uint32_t d = 0; d < dim; d++) {
                 const double v = X[i * dim + d];
                 auto it = std::lower_bound(inv.begin(), inv.end(), std::make_pair(v, (uint8_t)0));
-                if (it == inv.end() || it->first != v || std::signbit(v)) {
+                if (it == inv.end() || it->first != v || (v == 0.0 && std::signbit(v))) {   // -0.0 is no byte image
                     ok = false;
                     break;
                 }
