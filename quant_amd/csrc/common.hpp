@@ -101,15 +101,18 @@ hipError_t launch_assign_mfma(hipStream_t s, int grid, bool fuse, const uint8_t 
                               const _Float16 *cb_rows, uint32_t K, const float *C32, const uint64_t *plut,
                               const MfThresholds &th, uint32_t *A, uint32_t *flags, unsigned *flag_cnt,
                               uint64_t *part, uint32_t *part_cnt);
-// fp64 recheck of flagged rows; exact ties are listed in ties (tie_cnt) for
-// launch_kd_resolve or the host.  With sums != nullptr adds every other row's terms.
+// Recheck of flagged rows: fp32 distances to all K code vectors (C32 [Kpad][Dp]), fp64 in
+// the reference's order for those inside the fp32 error band (alpha, beta, gamma as the VALU
+// search's); exact ties are listed in ties (tie_cnt) for launch_kd_resolve or the host.
+// With sums != nullptr adds every other row's terms.
 hipError_t launch_recheck(hipStream_t s, int num_cu, const uint8_t *codes, uint32_t Dp, uint32_t D,
-                          const uint32_t *flags, const unsigned *flag_cnt, const double *C64, uint32_t K,
-                          const double *lut64, double tie_rel, uint32_t *A, uint32_t *ties, unsigned *tie_cnt,
-                          uint64_t *sums, const uint64_t *plut);
+                          const uint32_t *flags, const unsigned *flag_cnt, const double *C64, const float *C32,
+                          uint32_t K, const double *lut64, float alpha, float beta, float gamma, double tie_rel,
+                          uint32_t *A, uint32_t *ties, unsigned *tie_cnt, uint64_t *sums, const uint64_t *plut);
 // Device kd-tree answers for the listed ties (tree image in mapped host memory); adds their
-// terms to sums when given.  kd_resolve_fits: the tree and stacks fit the LDS.
-bool kd_resolve_fits(const KdView &kd);
+// terms to sums when given.  kd_resolve_fits: the tree, stacks and one wave's point
+// distances fit the LDS.
+bool kd_resolve_fits(const KdView &kd, uint32_t K);
 hipError_t launch_kd_resolve(hipStream_t s, const uint8_t *codes, uint32_t Dp, uint32_t D, const uint32_t *ties,
                              const unsigned *tie_cnt, const double *C64, uint32_t K, const double *lut64,
                              const KdView &kd, uint32_t *A, uint64_t *sums, const uint64_t *plut);

@@ -192,7 +192,7 @@ void free_levels(qvq_ctx *ctx) {
     ctx->Kcap = 0;
 }
 
-// Flattened tree: root box lo[D], hi[D] | nodes[2K] | vind[K].
+// Flattened tree: root box lo[D], hi[D] | nodes[<= 2K] | vind[K].
 uint64_t tree_bytes(uint32_t K, uint32_t D) {
     return 16ull * D + (2ull * K + 1) * sizeof(KdNodeDev) + 4ull * K;
 }
@@ -326,20 +326,23 @@ void build_tree(qvq_ctx *ctx, const double *hC, uint32_t K, int buf, KdView &kd)
     if (env_is("QVQ_KDTREE", "host")) return;
     RefKDTree tree(hC, K, (int)ctx->D);
     const uint32_t D = ctx->D;
+    const size_t nn = tree.num_nodes();
     KdView v;
     v.depth = tree.depth();
-    v.n_nodes = (uint32_t)tree.num_nodes();
-    v.bytes = (uint32_t)(16ull * D + tree.num_nodes() * sizeof(KdNodeDev) + 4ull * K);
-    if (!kd_resolve_fits(v)) return;
+    v.n_nodes = (uint32_t)nn;
+    const uint64_t bytes = 16ull * D + nn * sizeof(KdNodeDev) + 4ull * K;
+    if (bytes > ctx->tree_cap) return;
+    v.bytes = (uint32_t)bytes;
+    if (!kd_resolve_fits(v, K)) return;
     double *lo = reinterpret_cast<double *>(ctx->h_tree[buf]), *hi = lo + D;
     KdNodeDev *nodes = reinterpret_cast<KdNodeDev *>(hi + D);
-    uint32_t *vind = reinterpret_cast<uint32_t *>(nodes + tree.num_nodes());
+    uint32_t *vind = reinterpret_cast<uint32_t *>(nodes + nn);
     tree.flatten(nodes, vind, lo, hi);
     const double *dlo = reinterpret_cast<const double *>(ctx->dh_tree[buf]);
     v.lo = dlo;
     v.hi = dlo + D;
     v.nodes = reinterpret_cast<const KdNodeDev *>(dlo + 2 * D);
-    v.vind = reinterpret_cast<const uint32_t *>(v.nodes + tree.num_nodes());
+    v.vind = reinterpret_cast<const uint32_t *>(v.nodes + nn);
     kd = v;
 }
 
@@ -432,9 +435,13 @@ qvq_status run_level(qvq_ctx *ctx, uint32_t K, int slot, bool sums_out, const do
     }
     HIPCHK(hipEventRecord(ctx->ev[slot][1], ctx->stream));
     if (fused) HIPCHK(launch_reduce(ctx->stream, ctx->d_part, ctx->d_part_cnt, ctx->num_cu, K, ctx->D, ctx->d_sums));
-    HIPCHK(launch_recheck(ctx->stream, ctx->num_cu, ctx->d_codes, ctx->Dp, ctx->D, ctx->d_flags, &cnt[0],
-                          ctx->d_C64_split, K, ctx->d_lut64, 1e-12, ctx->d_A, ctx->d_ties, &cnt[1],
-                          fused ? ctx->d_sums : nullptr, ctx->d_plut));
+    {
+        float alpha, beta, gamma;
+        valu_coeffs(ctx, alpha, beta, gamma);
+        HIPCHK(launch_recheck(ctx->stream, ctx->num_cu, ctx->d_codes, ctx->Dp, ctx->D, ctx->d_flags, &cnt[0],
+                              ctx->d_C64_split, ctx->d_C32, K, ctx->d_lut64, alpha, beta, gamma, 1e-12, ctx->d_A,
+                              ctx->d_ties, &cnt[1], fused ? ctx->d_sums : nullptr, ctx->d_plut));
+    }
     // the tree build overlaps the search just enqueued
     qvq_status st;
     if (wait_seq && (st = wait_codebook(ctx, wait_seq)) != QVQ_OK) return st;

@@ -548,50 +548,106 @@ constexpr size_t RECHECK_LDS = 160 * 1024;
 // group, each on a different code vector, hit different banks.
 __host__ __device__ inline uint32_t recheck_stride(uint32_t D) { return D | 1u; }
 
-// fp64 recheck of flagged rows in the reference's distance order (ref_l2_hd).  Rows whose
-// best and second distances are within tie_rel are exact ties for the reference: they are
-// listed in ties (A gets the lowest index for now) and left to kd_resolve_kernel or the host.
-template <bool STAGED>
+// Recheck of flagged rows.  fp32 direct distances to all K code vectors (C32, staged in
+// LDS when it fits); each lane keeps its best two, the wave takes the minimum m.  Only code
+// vectors with d32 - m <= 2(alpha sqrt(d32) + beta d32) + gamma -- the search's rigorous fp32
+// error band, so every other code vector is farther in exact arithmetic by much more than
+// the tie tolerance -- get the fp64 distance in the reference's order (ref_l2_hd); a lane
+// whose second-best is inside the band rescans its code vectors.  Rows whose fp64 best and
+// second are within tie_rel are exact ties for the reference: listed in ties (A gets the
+// lowest index for now) for kd_resolve_kernel or the host.
+
+// LDS row stride in floats: Dp, or Dp + 4 so that it is 4 mod 8 dwords (16-lane b128 reads
+// of 16 consecutive rows then cover all 64 banks once).
+__host__ __device__ inline uint32_t recheck_c32_stride(uint32_t Dp) { return (Dp % 8 == 4) ? Dp : Dp + 4; }
+
+template <int DT>
+__device__ inline float d32_row(const float *__restrict__ xr, const float *__restrict__ c, uint32_t Dp) {
+    float acc = 0.f;
+    const uint32_t n4 = DT ? (uint32_t)(DT + 3) / 4 : Dp / 4;
+#pragma unroll
+    for (uint32_t q = 0; q < (DT ? (uint32_t)(DT + 3) / 4 : n4); q++) {
+        const float4 cq = reinterpret_cast<const float4 *>(c)[q];
+        const float4 xq = reinterpret_cast<const float4 *>(xr)[q];
+        float e;
+        e = xq.x - cq.x; acc = __fmaf_rn(e, e, acc);
+        e = xq.y - cq.y; acc = __fmaf_rn(e, e, acc);
+        e = xq.z - cq.z; acc = __fmaf_rn(e, e, acc);
+        e = xq.w - cq.w; acc = __fmaf_rn(e, e, acc);
+    }
+    return acc;   // padding components are 0 in both x and c
+}
+
+template <bool STAGED, int DT>
 __global__ __launch_bounds__(RECHECK_THREADS) void recheck_kernel(
     const uint8_t *__restrict__ codes, uint32_t Dp, uint32_t D, const uint32_t *__restrict__ flags,
-    const unsigned int *__restrict__ flag_cnt, const double *__restrict__ g_C64, uint32_t K,
-    const double *__restrict__ lut64, double tie_rel, uint32_t *__restrict__ A, uint32_t *__restrict__ ties,
-    unsigned int *__restrict__ tie_cnt, uint64_t *__restrict__ sums, const uint64_t *__restrict__ plut) {
+    const unsigned int *__restrict__ flag_cnt, const double *__restrict__ C64, const float *__restrict__ g_C32,
+    uint32_t K, const double *__restrict__ lut64, float alpha, float beta, float gamma, double tie_rel,
+    uint32_t *__restrict__ A, uint32_t *__restrict__ ties, unsigned int *__restrict__ tie_cnt,
+    uint64_t *__restrict__ sums, const uint64_t *__restrict__ plut) {
     extern __shared__ __attribute__((aligned(16))) double rsm[];
     constexpr int W = RECHECK_WAVES;
-    double *xs = rsm;            // [W][64]
-    double *cbs = rsm + W * 64;  // [K][stride] when staged
+    double *xs = rsm;                                              // [W][64] fp64 row
+    float *x32 = reinterpret_cast<float *>(rsm + W * 64);          // [W][64] fp32 row (zero padded)
+    float *c32s = x32 + W * 64;                                    // [K][CS] when staged
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const unsigned nflag = *flag_cnt;
     if (nflag == 0 || blockIdx.x * W >= nflag) return;
-    const uint32_t S = STAGED ? recheck_stride(D) : D;
+    const uint32_t CS = STAGED ? recheck_c32_stride(Dp) : Dp;
     if (STAGED) {
-        for (uint32_t i = threadIdx.x; i < K * D; i += RECHECK_THREADS) {
-            const uint32_t k = i / D, d = i - k * D;
-            cbs[k * S + d] = g_C64[i];
+        for (uint32_t i = threadIdx.x; i < K * (Dp / 4); i += RECHECK_THREADS) {
+            const uint32_t k = i / (Dp / 4), q = i - k * (Dp / 4);
+            reinterpret_cast<float4 *>(c32s + (size_t)k * CS)[q] = reinterpret_cast<const float4 *>(g_C32)[i];
         }
         __syncthreads();
     }
-    const double *C64 = STAGED ? cbs : g_C64;
+    const float *C32 = STAGED ? c32s : g_C32;
     for (unsigned base = blockIdx.x * W; base < nflag; base += gridDim.x * W) {
         const unsigned f = base + wave;
         const bool active = f < nflag;
         const uint32_t row = active ? flags[f] : 0;
         __syncthreads();
-        if (active && lane < (int)D) xs[wave * 64 + lane] = lut64[codes[(uint64_t)row * Dp + lane]];
+        if (active) {
+            const double v = lane < (int)D ? lut64[codes[(uint64_t)row * Dp + lane]] : 0.0;
+            xs[wave * 64 + lane] = v;
+            x32[wave * 64 + lane] = (float)v;
+        }
         __syncthreads();
         if (!active) continue;
+        const float *xr = x32 + wave * 64;
+        auto within = [&](float d, float m) { return d - m <= 2.f * (alpha * sqrtf(d) + beta * d) + gamma; };
+        float b1 = INFINITY, b2 = INFINITY;
+        uint32_t kb = 0;
+        for (uint32_t k = lane; k < K; k += 64) {
+            const float d = d32_row<DT>(xr, C32 + (size_t)k * CS, Dp);
+            if (d < b1) {
+                b2 = b1;
+                b1 = d;
+                kb = k;
+            } else if (d < b2) {
+                b2 = d;
+            }
+        }
+        float m = b1;
+#pragma unroll
+        for (int off = 32; off >= 1; off >>= 1) m = fminf(m, __shfl_xor(m, off));
         double d1 = INFINITY, d2 = INFINITY;
         uint32_t k1 = 0xFFFFFFFFu;
-        for (uint32_t k = lane; k < K; k += 64) {
-            const double d = ref_l2_hd(xs + wave * 64, C64 + (uint64_t)k * S, D);
-            if (d < d1) {
+        auto take = [&](uint32_t k) {
+            const double d = ref_l2_hd(xs + wave * 64, C64 + (uint64_t)k * D, D);
+            if (d < d1 || (d == d1 && k < k1)) {
                 d2 = d1;
                 d1 = d;
                 k1 = k;
             } else if (d < d2) {
                 d2 = d;
             }
+        };
+        if (within(b2, m)) {   // rare: more than one candidate on this lane
+            for (uint32_t k = lane; k < K; k += 64)
+                if (within(d32_row<DT>(xr, C32 + (size_t)k * CS, Dp), m)) take(k);
+        } else if (within(b1, m)) {
+            take(kb);
         }
 #pragma unroll
         for (int off = 32; off >= 1; off >>= 1) {
@@ -621,29 +677,47 @@ __global__ __launch_bounds__(RECHECK_THREADS) void recheck_kernel(
     }
 }
 
+template <bool S, int DT>
+static void launch_recheck_variant(hipStream_t s, int grid, size_t lds, const uint8_t *codes, uint32_t Dp, uint32_t D,
+                                   const uint32_t *flags, const unsigned *flag_cnt, const double *C64,
+                                   const float *C32, uint32_t K, const double *lut64, float alpha, float beta,
+                                   float gamma, double tie_rel, uint32_t *A, uint32_t *ties, unsigned *tie_cnt,
+                                   uint64_t *sums, const uint64_t *plut) {
+    hipLaunchKernelGGL((recheck_kernel<S, DT>), dim3(grid), dim3(RECHECK_THREADS), lds, s, codes, Dp, D, flags,
+                       flag_cnt, C64, C32, K, lut64, alpha, beta, gamma, tie_rel, A, ties, tie_cnt, sums, plut);
+}
+
 hipError_t launch_recheck(hipStream_t s, int num_cu, const uint8_t *codes, uint32_t Dp, uint32_t D,
-                          const uint32_t *flags, const unsigned *flag_cnt, const double *C64, uint32_t K,
-                          const double *lut64, double tie_rel, uint32_t *A, uint32_t *ties, unsigned *tie_cnt,
-                          uint64_t *sums, const uint64_t *plut) {
-    const size_t base = (size_t)RECHECK_WAVES * 64 * 8;
-    const size_t cb = (size_t)K * recheck_stride(D) * 8;
+                          const uint32_t *flags, const unsigned *flag_cnt, const double *C64, const float *C32,
+                          uint32_t K, const double *lut64, float alpha, float beta, float gamma, double tie_rel,
+                          uint32_t *A, uint32_t *ties, unsigned *tie_cnt, uint64_t *sums, const uint64_t *plut) {
+    if (Dp % 4 || Dp > 64) return hipErrorInvalidValue;
+    const size_t base = (size_t)RECHECK_WAVES * 64 * 12;
+    const size_t cb = (size_t)K * recheck_c32_stride(Dp) * 4;
     const bool staged = base + cb <= RECHECK_LDS;
     const size_t lds = base + (staged ? cb : 0);
-    if (staged)
-        hipLaunchKernelGGL(recheck_kernel<true>, dim3(num_cu), dim3(RECHECK_THREADS), lds, s, codes, Dp, D, flags,
-                           flag_cnt, C64, K, lut64, tie_rel, A, ties, tie_cnt, sums, plut);
-    else
-        hipLaunchKernelGGL(recheck_kernel<false>, dim3(num_cu), dim3(RECHECK_THREADS), lds, s, codes, Dp, D, flags,
-                           flag_cnt, C64, K, lut64, tie_rel, A, ties, tie_cnt, sums, plut);
+#define QVQ_RC(SS, DT)                                                                                             \
+    launch_recheck_variant<SS, DT>(s, num_cu, lds, codes, Dp, D, flags, flag_cnt, C64, C32, K, lut64, alpha, beta, \
+                                   gamma, tie_rel, A, ties, tie_cnt, sums, plut)
+    if (Dp == 12) {
+        if (staged) QVQ_RC(true, 12); else QVQ_RC(false, 12);
+    } else if (Dp == 48) {
+        if (staged) QVQ_RC(true, 48); else QVQ_RC(false, 48);
+    } else {
+        if (staged) QVQ_RC(true, 0); else QVQ_RC(false, 0);
+    }
+#undef QVQ_RC
     return hipGetLastError();
 }
 
 // kd_nearest_flat with the leaf scan spread over the wave: every lane runs the same
 // descent (uniform values), lane i takes leaf point i, and the leaf's winner is the first
 // point in leaf order with the smallest distance below the leaf-entry worst -- what the
-// sequential strict-'<' scan picks.  Leaves hold at most 10 points (< 64 lanes).
-__device__ uint32_t kd_nearest_wave(const double *q, uint32_t D, const KdView &t, const double *pts, uint32_t S,
-                                    double *sd, int32_t *sn, double *dl, int lane) {
+// sequential strict-'<' scan picks.  Leaves hold at most 10 points (< 64 lanes).  pv holds
+// every point's distance in vind order; subtrees none of whose points is below best are
+// skipped (same result).
+__device__ uint32_t kd_nearest_wave(const double *q, uint32_t D, const KdView &t, const double *pv, double *sd,
+                                    int32_t *sn, double *dl, int lane) {
     double distsq = 0;   // dl: per-dimension cell distances (LDS, uniform across lanes)
     for (uint32_t d = 0; d < D; d++) {
         const double x = q[d];
@@ -665,13 +739,26 @@ __device__ uint32_t kd_nearest_wave(const double *q, uint32_t D, const KdView &t
     while (sp >= 0) {
         const int32_t node = sn[sp] >> 2, phase = sn[sp] & 3;
         const KdNodeDev n = t.nodes[node];
+        // A subtree none of whose points is below best cannot change best (updates need
+        // dist < worst <= best) and its walk has no other effect: skip it.  Its points are
+        // vind[first, b), so the test is a range minimum of pv.
+        if (phase == 0 && n.child1 >= 0 && best < 1.7976931348623157e308) {
+            double m = INFINITY;
+            for (int32_t j = kd_first(n) + lane; j < n.b; j += 64) m = fmin(m, pv[j]);
+#pragma unroll
+            for (int off = 32; off >= 1; off >>= 1) m = fmin(m, __shfl_xor(m, off));
+            if (m >= best) {
+                sp--;
+                continue;
+            }
+        }
         if (n.child1 < 0) {
             const double worst = best;
             const int32_t cnt = n.b - n.a;
             double dist = INFINITY;
             int32_t pos = 0x7FFFFFFF;
             if (lane < cnt) {
-                const double dd = ref_l2_hd(q, pts + (uint64_t)t.vind[n.a + lane] * S, (int)D);
+                const double dd = pv[n.a + lane];   // ref_l2_hd(q, point vind[n.a + lane])
                 if (dd < worst) {
                     dist = dd;
                     pos = lane;
@@ -693,7 +780,7 @@ __device__ uint32_t kd_nearest_wave(const double *q, uint32_t D, const KdView &t
             sp--;
             continue;
         }
-        const int f = n.a;
+        const int f = kd_feat(n);
         const double val = q[f];
         const double diff1 = val - n.lo, diff2 = val - n.hi;
         const bool left_first = (diff1 + diff2) < 0;
@@ -727,57 +814,60 @@ __device__ uint32_t kd_nearest_wave(const double *q, uint32_t D, const KdView &t
 // Exact ties listed by the recheck, answered by the reference kd-tree traversal
 // (kd_nearest_flat).  The tree image (kd.lo .. ) lives in mapped pinned host memory and is
 // staged into LDS by each block that has tie rows; one lane per wave walks it.
-constexpr int KDR_THREADS = 1024;
-constexpr int KDR_WAVES = KDR_THREADS / 64;
-constexpr int KDR_BLOCKS = 32;
-
-size_t kd_resolve_lds(const KdView &kd) {
-    return (size_t)KDR_WAVES * 128 * 8 + (((size_t)KDR_WAVES * kd.depth * KD_FRAME_BYTES + 7) & ~(size_t)7) +
-           (((size_t)kd.bytes + 7) & ~(size_t)7);
+// LDS written by some lanes of a wave and then read by others: order the accesses.
+__device__ inline void wave_lds_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-bool kd_resolve_fits(const KdView &kd) { return kd.depth > 0 && kd_resolve_lds(kd) <= RECHECK_LDS; }
+constexpr int KDR_MAX_WAVES = 16;
+constexpr int KDR_BLOCKS = 16;
 
-template <bool STAGED>
-__global__ __launch_bounds__(KDR_THREADS) void kd_resolve_kernel(
+// LDS: per wave the row, cell distances, stack and the K point distances; plus the tree.
+static size_t kd_wave_bytes(const KdView &kd, uint32_t K) {
+    return 128 * 8 + (((size_t)kd.depth * KD_FRAME_BYTES + 7) & ~(size_t)7) + (size_t)K * 8;
+}
+static size_t kd_tree_bytes(const KdView &kd) { return ((size_t)kd.bytes + 7) & ~(size_t)7; }
+static int kd_waves(const KdView &kd, uint32_t K) {
+    const size_t wb = kd_wave_bytes(kd, K), tb = kd_tree_bytes(kd);
+    if (tb + wb > RECHECK_LDS) return 0;
+    return (int)std::min<size_t>(KDR_MAX_WAVES, (RECHECK_LDS - tb) / wb);
+}
+
+bool kd_resolve_fits(const KdView &kd, uint32_t K) { return kd.depth > 0 && kd_waves(kd, K) > 0; }
+
+__global__ __launch_bounds__(KDR_MAX_WAVES * 64) void kd_resolve_kernel(
     const uint8_t *__restrict__ codes, uint32_t Dp, uint32_t D, const uint32_t *__restrict__ ties,
-    const unsigned *__restrict__ tie_cnt, const double *__restrict__ g_C64, uint32_t K,
+    const unsigned *__restrict__ tie_cnt, const double *__restrict__ C64, uint32_t K,
     const double *__restrict__ lut64, KdView kd, uint32_t *__restrict__ A, uint64_t *__restrict__ sums,
     const uint64_t *__restrict__ plut) {
     extern __shared__ __attribute__((aligned(16))) double ksm[];
-    constexpr int W = KDR_WAVES;
+    const int W = blockDim.x / 64;
     const int Z = kd.depth;
-    double *xs = ksm;                                              // [W][64]
-    double *dl = xs + W * 64;                                      // [W][64]
-    double *sd = dl + W * 64;                                      // [W][Z]
-    int32_t *sn = reinterpret_cast<int32_t *>(sd + W * Z);         // [W][Z]
-    double *tr = ksm + W * 128 + ((size_t)W * Z * KD_FRAME_BYTES + 7) / 8;
-    double *cbs = tr + (kd.bytes + 7) / 8;                         // [K][stride] when STAGED
     const unsigned nt = *tie_cnt;
     if (blockIdx.x * W >= nt) return;
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    for (uint32_t i = threadIdx.x; i < (kd.bytes + 7) / 8; i += KDR_THREADS) tr[i] = kd.lo[i];
-    const uint32_t S = STAGED ? recheck_stride(D) : D;
-    if (STAGED)
-        for (uint32_t i = threadIdx.x; i < K * D; i += KDR_THREADS) {
-            const uint32_t k = i / D, d = i - k * D;
-            cbs[k * S + d] = g_C64[i];
-        }
+    double *tr = ksm;   // tree image
+    double *wb = ksm + ((size_t)kd.bytes + 7) / 8 + (size_t)wave * (128 + ((size_t)Z * KD_FRAME_BYTES + 7) / 8 + K);
+    double *xs = wb, *dl = wb + 64;
+    double *sd = wb + 128;
+    int32_t *sn = reinterpret_cast<int32_t *>(sd + Z);
+    double *pv = wb + 128 + ((size_t)Z * KD_FRAME_BYTES + 7) / 8;   // [K] distances in vind order
+    for (uint32_t i = threadIdx.x; i < (kd.bytes + 7) / 8; i += blockDim.x) tr[i] = kd.lo[i];
     KdView kv = kd;
     kv.lo = tr;
     kv.hi = tr + D;
     kv.nodes = reinterpret_cast<const KdNodeDev *>(tr + 2 * D);
     kv.vind = reinterpret_cast<const uint32_t *>(kv.nodes + kd.n_nodes);
     __syncthreads();
-    const double *C64 = STAGED ? cbs : g_C64;
     for (unsigned f = blockIdx.x * W + wave; f < nt; f += gridDim.x * W) {
         const uint32_t row = ties[f];
-        if (lane < (int)D) xs[wave * 64 + lane] = lut64[codes[(uint64_t)row * Dp + lane]];
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        const uint32_t k = kd_nearest_wave(xs + wave * 64, D, kv, C64, S, sd + wave * Z, sn + wave * Z,
-                                           dl + wave * 64, lane);
+        if (lane < (int)D) xs[lane] = lut64[codes[(uint64_t)row * Dp + lane]];
+        wave_lds_sync();
+        for (uint32_t j = lane; j < K; j += 64) pv[j] = ref_l2_hd(xs, C64 + (uint64_t)kv.vind[j] * D, (int)D);
+        wave_lds_sync();
+        const uint32_t k = kd_nearest_wave(xs, D, kv, pv, sd, sn, dl, lane);
         if (lane == 0) A[row] = k;
         if (sums && lane < (int)D) {
             const uint64_t KD = (uint64_t)K * D;
@@ -786,21 +876,18 @@ __global__ __launch_bounds__(KDR_THREADS) void kd_resolve_kernel(
             atomicAdd((unsigned long long *)&sums[KD + (uint64_t)lane * K + k], (unsigned long long)(p & 0xFFFFFFFFull));
             if (lane == 0) atomicAdd((unsigned long long *)&sums[2 * KD + k], 1ull);
         }
-        __builtin_amdgcn_wave_barrier();
+        wave_lds_sync();
     }
 }
 
 hipError_t launch_kd_resolve(hipStream_t s, const uint8_t *codes, uint32_t Dp, uint32_t D, const uint32_t *ties,
                              const unsigned *tie_cnt, const double *C64, uint32_t K, const double *lut64,
                              const KdView &kd, uint32_t *A, uint64_t *sums, const uint64_t *plut) {
-    if (!kd_resolve_fits(kd)) return hipErrorInvalidValue;
-    const size_t base = kd_resolve_lds(kd), cb = (size_t)K * recheck_stride(D) * 8;
-    if (base + cb <= RECHECK_LDS)
-        hipLaunchKernelGGL(kd_resolve_kernel<true>, dim3(KDR_BLOCKS), dim3(KDR_THREADS), base + cb, s, codes, Dp, D,
-                           ties, tie_cnt, C64, K, lut64, kd, A, sums, plut);
-    else
-        hipLaunchKernelGGL(kd_resolve_kernel<false>, dim3(KDR_BLOCKS), dim3(KDR_THREADS), base, s, codes, Dp, D, ties,
-                           tie_cnt, C64, K, lut64, kd, A, sums, plut);
+    const int W = kd.depth > 0 ? kd_waves(kd, K) : 0;
+    if (W == 0) return hipErrorInvalidValue;
+    const size_t lds = kd_tree_bytes(kd) + (size_t)W * kd_wave_bytes(kd, K);
+    hipLaunchKernelGGL(kd_resolve_kernel, dim3(KDR_BLOCKS), dim3(64 * W), lds, s, codes, Dp, D, ties, tie_cnt, C64,
+                       K, lut64, kd, A, sums, plut);
     return hipGetLastError();
 }
 

@@ -127,6 +127,8 @@ int RefKDTree::divide(size_t left, size_t right, std::vector<Box> &bbox, int lev
     const int c2 = divide(left + idx, right, rb, level + 1);
     Node &n = nodes_[me];
     n.leaf = false;
+    n.left = left;
+    n.right = right;
     n.divfeat = cutfeat;
     n.child1 = c1;
     n.child2 = c2;
@@ -151,8 +153,8 @@ void RefKDTree::flatten(KdNodeDev *nodes, uint32_t *vind, double *lo, double *hi
         } else {
             o.child1 = n.child1;
             o.child2 = n.child2;
-            o.a = n.divfeat;
-            o.b = 0;
+            o.a = (int32_t)((uint32_t)n.divfeat | (uint32_t)n.left << 8);
+            o.b = (int32_t)n.right;
             o.lo = n.divlow;
             o.hi = n.divhigh;
         }

@@ -35,7 +35,7 @@ private:
     struct Box { double low, high; };
     struct Node {
         bool leaf;
-        size_t left, right;      // leaf: vind[left, right)
+        size_t left, right;      // the node's points: vind[left, right)
         int divfeat;
         double divlow, divhigh;
         int child1, child2;

@@ -36,9 +36,11 @@ QVQ_HD inline double ref_l2_hd(const double *a, const double *b, int dim) {
 
 struct KdNodeDev {
     int32_t child1, child2;   // -1: leaf
-    int32_t a, b;             // leaf: vind[a, b); inner: a = divfeat
+    int32_t a, b;             // leaf: vind[a, b); inner: a = divfeat | first << 8, vind[first, b)
     double lo, hi;            // inner: divlow, divhigh
 };
+QVQ_HD inline int kd_feat(const KdNodeDev &n) { return n.a & 0xFF; }
+QVQ_HD inline int32_t kd_first(const KdNodeDev &n) { return n.child1 < 0 ? n.a : (int32_t)((uint32_t)n.a >> 8); }
 
 struct KdView {
     const KdNodeDev *nodes = nullptr;
@@ -46,7 +48,7 @@ struct KdView {
     const double *lo = nullptr, *hi = nullptr;   // root bounding box
     int depth = 0;                               // 0: no device tree (host resolves ties)
     uint32_t n_nodes = 0;
-    uint32_t bytes = 0;   // contiguous image lo[D] | hi[D] | nodes | vind starting at lo
+    uint32_t bytes = 0;   // contiguous image lo[D] | hi[D] | nodes | vind from lo
 };
 
 // Device stack frames are 12 bytes: one double (the cell bound mindistsq, replaced by the
@@ -94,7 +96,7 @@ QVQ_HD inline uint32_t kd_nearest_flat(const double *q, uint32_t D, const KdView
             sp--;
             continue;
         }
-        const int f = n.a;
+        const int f = kd_feat(n);
         const double val = q[f];
         const double diff1 = val - n.lo, diff2 = val - n.hi;
         const bool left_first = (diff1 + diff2) < 0;
