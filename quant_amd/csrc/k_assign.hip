@@ -12,6 +12,8 @@
 //                      are accumulated in LDS ([d][k] layout, u64 (hi<<32|lo) terms).
 //  assign_valu_kernel  any Dp <= 64, fp32 direct form (x-c)^2 with an fp32 error bound.
 //  recheck_kernel      fp64 distances of flagged rows in the reference build's order.
+#include <cstdlib>
+
 #include "common.hpp"
 
 namespace qvq {
@@ -129,7 +131,12 @@ __device__ inline void pair_update(const f32x4 &p0, const f32x4 &p1, uint32_t pa
     b1 = min2f(b1, m);
 }
 
-template <bool FUSE, bool STAGED>
+constexpr int MF_SMALL_K = 32;
+
+// SMALLK (K <= MF_SMALL_K): no MFMA at all -- each lane scans all K code vectors of its row
+// in the direct fp32 form (the recompute below), which is cheaper than the MFMA pass's
+// per-chunk fixed work when the codebook is this small.
+template <bool FUSE, bool STAGED, bool SMALLK>
 __global__ __launch_bounds__(MF_THREADS) void assign_mfma_kernel(
     const uint8_t *__restrict__ codes, uint64_t N, const _Float16 *__restrict__ g_rows, uint32_t K,
     const float *__restrict__ g_C32, const uint64_t *__restrict__ g_plut, MfThresholds th, uint32_t *__restrict__ A,
@@ -144,7 +151,7 @@ __global__ __launch_bounds__(MF_THREADS) void assign_mfma_kernel(
     uint32_t *cnt = reinterpret_cast<uint32_t *>(lds + L.cnt);
     uint64_t *plut = reinterpret_cast<uint64_t *>(lds + L.plut);
     const int tid = threadIdx.x;
-    {
+    if (!SMALLK) {
         const uint64_t *src = reinterpret_cast<const uint64_t *>(g_rows);
         uint64_t *dst = reinterpret_cast<uint64_t *>(rows);
         for (uint32_t i = tid; i < Kp * (MF_ROW_BYTES / 8) + 2; i += MF_THREADS)
@@ -184,8 +191,9 @@ __global__ __launch_bounds__(MF_THREADS) void assign_mfma_kernel(
     };
     auto load_codes = [&](uint64_t chunk, uint32_t (&q)[MF_TILES][3]) {
 #pragma unroll
-        for (int t = 0; t < MF_TILES; t++) {
-            const uint64_t row = chunk * MF_ROWS + t * 16 + c;
+        for (int t = 0; t < (SMALLK ? 1 : MF_TILES); t++) {
+            // SMALLK: only the lane's own row (base + lane), in q[0]
+            const uint64_t row = SMALLK ? chunk * MF_ROWS + lane : chunk * MF_ROWS + t * 16 + c;
             if (chunk < nchunks && row < N) {
                 const uint32_t *p = reinterpret_cast<const uint32_t *>(codes + row * MF_D);
                 q[t][0] = p[0];
@@ -209,9 +217,12 @@ __global__ __launch_bounds__(MF_THREADS) void assign_mfma_kernel(
 #pragma unroll
             for (int i = 0; i < 3; i++) q[t][i] = qn[t][i];
         load_codes(chunk + stride, qn);   // prefetch the next chunk under this one's search
+        uint32_t own[3] = {q[0][0], q[0][1], q[0][2]};   // this lane's own row, base + lane
+        uint32_t unit = 0;       // 8-code-vector unit (pair*4 + g) the MFMA pass picked
+        float sec_m = INFINITY;  // best MFMA score among the other units
+        if constexpr (!SMALLK) {
         // B fragments: lane (g, c) holds k-slots 8g..8g+7 of data row c of each tile.
         half8 b[MF_TILES];
-        uint32_t own[3] = {q[0][0], q[0][1], q[0][2]};   // this lane's own row, base + lane
 #pragma unroll
         for (int t = 0; t < MF_TILES; t++) {
             if (g == t) {
@@ -290,13 +301,14 @@ __global__ __launch_bounds__(MF_THREADS) void assign_mfma_kernel(
         }
         // Lane L owns row base + L (tile L/16, row L%16): recompute the 8 code vectors of
         // its winning unit in the direct fp32 form (x - c)^2.
-        uint32_t unit = wsel[0];
-        float sec_m = b2[0];
+        unit = wsel[0];
+        sec_m = b2[0];
 #pragma unroll
         for (int t = 1; t < MF_TILES; t++) {
             unit = g == t ? wsel[t] : unit;
             sec_m = g == t ? b2[t] : sec_m;
         }
+        }   // !SMALLK
         const uint64_t row = base + lane;
         const bool valid = row < N;
         uint32_t rk = 0;
@@ -314,11 +326,12 @@ __global__ __launch_bounds__(MF_THREADS) void assign_mfma_kernel(
             const uint32_t pr = unit >> 2, gg = unit & 3;
             // a unit is 4 code vectors of each tile of its pair; up to K = 16 the second
             // tile is padding, and below 4 so is the rest of the first
-            const int jn = K <= 16 ? (K < 4 ? (int)K : 4) : 8;
+            // SMALLK: the unit is the whole codebook
+            const int jn = SMALLK ? (int)K : (K <= 16 ? (K < 4 ? (int)K : 4) : 8);
 #pragma unroll
-            for (int j = 0; j < 8; j++) {
+            for (int j = 0; j < (SMALLK ? MF_SMALL_K : 8); j++) {
                 if (j >= jn) continue;   // uniform: K is
-                const uint32_t cv = (2 * pr + (j >> 2)) * 16 + 4 * gg + (j & 3);
+                const uint32_t cv = SMALLK ? (uint32_t)j : (2 * pr + (j >> 2)) * 16 + 4 * gg + (j & 3);
                 const float4 *c4 = reinterpret_cast<const float4 *>(C32 + (size_t)cv * MF_D);
                 float dist = 0.f;
 #pragma unroll
@@ -335,8 +348,8 @@ __global__ __launch_bounds__(MF_THREADS) void assign_mfma_kernel(
                 rk = dist < r1 ? cv : rk;
                 r1 = min2f(r1, dist);
             }
-            const float sec = min2f(__fmaf_rn(sec_m, th.inv_scale, xn), r2);
-            const float thr = th.mfma + 2.f * (th.alpha * sqrtf(sec) + th.beta * sec) + th.gamma;
+            const float sec = SMALLK ? r2 : min2f(__fmaf_rn(sec_m, th.inv_scale, xn), r2);
+            const float thr = (SMALLK ? 0.f : th.mfma) + 2.f * (th.alpha * sqrtf(sec) + th.beta * sec) + th.gamma;
             A[row] = rk;
             flagged = !(sec - r1 > thr);
             if (flagged) flags[atomicAdd(flag_cnt, 1u)] = (uint32_t)row;
@@ -379,14 +392,19 @@ __global__ __launch_bounds__(MF_THREADS) void assign_mfma_kernel(
     }
 }
 
-template <bool F, bool S>
+template <bool F, bool S, bool SK>
 static void launch_mfma_variant(hipStream_t s, int grid, size_t lds, const uint8_t *codes, uint64_t N,
                                 const _Float16 *cb_rows, uint32_t K, const float *C32, const uint64_t *plut,
                                 const MfThresholds &th, uint32_t *A, uint32_t *flags, unsigned *flag_cnt,
                                 uint64_t *part, uint32_t *part_cnt) {
-    auto kern = assign_mfma_kernel<F, S>;
+    auto kern = assign_mfma_kernel<F, S, SK>;
     hipLaunchKernelGGL(kern, dim3(grid), dim3(MF_THREADS), lds, s, codes, N, cb_rows, K, C32, plut, th, A, flags,
                        flag_cnt, part, part_cnt);
+}
+
+uint32_t mf_small_k() {
+    const char *e = std::getenv("QVQ_SMALLK");   // ablation: QVQ_SMALLK=0 keeps the MFMA pass
+    return e ? (uint32_t)std::min(std::atoi(e), MF_SMALL_K) : (uint32_t)MF_SMALL_K;
 }
 
 hipError_t launch_assign_mfma(hipStream_t s, int grid, bool fuse, const uint8_t *codes, uint64_t N,
@@ -394,9 +412,15 @@ hipError_t launch_assign_mfma(hipStream_t s, int grid, bool fuse, const uint8_t 
                               const MfThresholds &th, uint32_t *A, uint32_t *flags, unsigned *flag_cnt,
                               uint64_t *part, uint32_t *part_cnt) {
     const bool staged = mf_lds_layout(K, fuse, true).total <= MF_LDS_MAX;
+    const bool small = K <= mf_small_k() && staged;
     const size_t lds = mf_lds_layout(K, fuse, staged).total;
-    auto *fn = fuse ? (staged ? launch_mfma_variant<true, true> : launch_mfma_variant<true, false>)
-                    : (staged ? launch_mfma_variant<false, true> : launch_mfma_variant<false, false>);
+    using Fn = void (*)(hipStream_t, int, size_t, const uint8_t *, uint64_t, const _Float16 *, uint32_t, const float *,
+                        const uint64_t *, const MfThresholds &, uint32_t *, uint32_t *, unsigned *, uint64_t *,
+                        uint32_t *);
+    Fn fn;
+    if (small) fn = fuse ? launch_mfma_variant<true, true, true> : launch_mfma_variant<false, true, true>;
+    else if (fuse) fn = staged ? launch_mfma_variant<true, true, false> : launch_mfma_variant<true, false, false>;
+    else fn = staged ? launch_mfma_variant<false, true, false> : launch_mfma_variant<false, false, false>;
     fn(s, grid, lds, codes, N, cb_rows, K, C32, plut, th, A, flags, flag_cnt, part, part_cnt);
     return hipGetLastError();
 }
