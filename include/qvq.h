@@ -124,6 +124,10 @@ QVQ_API qvq_status qvq_update(qvq_ctx *ctx, const uint32_t *assign, uint32_t K, 
 QVQ_API qvq_status qvq_comm_unique_id(uint8_t id[128]);
 QVQ_API qvq_status qvq_comm_init(qvq_ctx *ctx, int nranks, int rank, const uint8_t id[128]);
 
+/* Which levels get HIP events around their search kernel (each event record costs a few
+ * microseconds of GPU idle): -1 every level (default), -2 none, n >= 0 level n+1 only.
+ * Unmeasured levels report 0 in qvq_get_timings. */
+QVQ_API qvq_status qvq_set_timing(qvq_ctx *ctx, int level);
 QVQ_API qvq_status qvq_get_timings(const qvq_ctx *ctx, qvq_timings *out);
 
 /* Host-only helpers (no GPU needed), exported for tests of the host logic. */

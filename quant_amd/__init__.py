@@ -38,7 +38,7 @@ _lib = None
 EXPORTED = ["qvq_create", "qvq_destroy", "qvq_last_error", "qvq_version", "qvq_set_images",
             "qvq_set_images_device", "qvq_set_synthetic", "qvq_set_vectors", "qvq_num_vectors",
             "qvq_dim", "qvq_lbg", "qvq_assign_device", "qvq_assign", "qvq_update",
-            "qvq_comm_unique_id", "qvq_comm_init", "qvq_get_timings", "qvq_host_kdtree_nn",
+            "qvq_comm_unique_id", "qvq_comm_init", "qvq_set_timing", "qvq_get_timings", "qvq_host_kdtree_nn",
             "qvq_host_finalize", "qvq_host_row_terms"]
 
 
@@ -67,6 +67,7 @@ def lib():
             "qvq_update": ([P, P, u32, P, P], i),
             "qvq_comm_unique_id": ([P], i),
             "qvq_comm_init": ([P, i, i, P], i),
+            "qvq_set_timing": ([P, i], i),
             "qvq_get_timings": ([P, ctypes.POINTER(_Timings)], i),
             "qvq_host_kdtree_nn": ([P, u32, u32, P, u64, P], i),
             "qvq_host_finalize": ([P, P, P, u32, u32, i, P], i),
@@ -160,6 +161,10 @@ class Engine:
 
     def assign_device_ptr(self):
         return lib().qvq_assign_device(self._h)
+
+    def set_timing(self, level=-1):
+        """HIP events around the search of every level (-1), none (-2) or level+1 only."""
+        _check(lib().qvq_set_timing(self._h, int(level)), self._h)
 
     def timings(self):
         t = _Timings()

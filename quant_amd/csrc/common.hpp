@@ -104,18 +104,20 @@ hipError_t launch_assign_mfma(hipStream_t s, int grid, bool fuse, const uint8_t 
 // Recheck of flagged rows: fp32 distances to all K code vectors (C32 [Kpad][Dp]), fp64 in
 // the reference's order for those inside the fp32 error band (alpha, beta, gamma as the VALU
 // search's); exact ties are listed in ties (tie_cnt) for launch_kd_resolve or the host.
-// With sums != nullptr adds every other row's terms.
+// With xslab != nullptr adds every other row's packed terms (hi << 32 | lo) to xslab [d][k]
+// and its count to xcnt [k] (the search's extra slab G).
 hipError_t launch_recheck(hipStream_t s, int num_cu, const uint8_t *codes, uint32_t Dp, uint32_t D,
                           const uint32_t *flags, const unsigned *flag_cnt, const double *C64, const float *C32,
                           uint32_t K, const double *lut64, float alpha, float beta, float gamma, double tie_rel,
-                          uint32_t *A, uint32_t *ties, unsigned *tie_cnt, uint64_t *sums, const uint64_t *plut);
+                          uint32_t *A, uint32_t *ties, unsigned *tie_cnt, uint64_t *xslab, uint32_t *xcnt,
+                          const uint64_t *plut);
 // Device kd-tree answers for the listed ties (tree image in mapped host memory); adds their
 // terms to sums when given.  kd_resolve_fits: the tree, stacks and one wave's point
 // distances fit the LDS.
 bool kd_resolve_fits(const KdView &kd, uint32_t K);
 hipError_t launch_kd_resolve(hipStream_t s, const uint8_t *codes, uint32_t Dp, uint32_t D, const uint32_t *ties,
                              const unsigned *tie_cnt, const double *C64, uint32_t K, const double *lut64,
-                             const KdView &kd, uint32_t *A, uint64_t *sums, const uint64_t *plut);
+                             const KdView &kd, uint32_t *A, uint64_t *xslab, uint32_t *xcnt, const uint64_t *plut);
 hipError_t launch_update(hipStream_t s, uint32_t Dp, uint32_t G, const uint8_t *codes, uint64_t N, const uint32_t *A,
                          uint32_t K, uint32_t D, const uint64_t *plut, uint64_t *part, uint32_t *part_cnt);
 hipError_t launch_reduce(hipStream_t s, const uint64_t *part, const uint32_t *part_cnt, uint32_t G, uint32_t K,
@@ -139,9 +141,11 @@ hipError_t launch_prep(hipStream_t s, const double *C64, uint32_t K, uint32_t Kp
                        double mu, double sx, int t, float *C32, _Float16 *cb_rows);
 hipError_t launch_gather_codes(hipStream_t s, const uint8_t *codes, uint32_t Dp, const uint32_t *rows, uint32_t n,
                                uint8_t *out);
-// A[rows[i]] = vals[i]; sums[idx[j]] += val[j] (host tie resolutions).
+// A[rows[i]] = vals[i]; host-aggregated terms of those rows into the extra slab:
+// idx < KD -> slab[idx] += val (packed hi << 32 | lo), else slab_cnt[idx - KD] += val.
 hipError_t launch_scatter(hipStream_t s, uint32_t *A, const uint32_t *rows, const uint32_t *vals, uint32_t n,
-                          uint64_t *sums, const uint64_t *idx, const uint64_t *val, uint32_t nterms);
+                          uint64_t *slab, uint32_t *slab_cnt, uint64_t KD, const uint64_t *idx, const uint64_t *val,
+                          uint32_t nterms);
 // 256-bin histogram of the first D bytes of every row (hist zeroed first).
 hipError_t launch_byte_hist(hipStream_t s, const uint8_t *codes, uint64_t N, uint32_t D, uint32_t Dp,
                             uint64_t *hist);

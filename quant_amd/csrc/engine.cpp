@@ -110,6 +110,8 @@ struct qvq_ctx {
     uint64_t seq = 0;
     uint8_t *h_tree[2] = {nullptr, nullptr}, *dh_tree[2] = {nullptr, nullptr};
     uint64_t tree_cap = 0;
+    uint32_t nslabs = 0;   // slabs holding the last run_level's sums
+    int timing_level = -1;   // qvq_set_timing: -1 all levels, -2 none, else that level only
     bool upd[32] = {};
     hipEvent_t ev_end = nullptr;
 
@@ -272,8 +274,9 @@ qvq_status ensure_levels(qvq_ctx *ctx, uint32_t Kmax) {
     HIPCHK(hipMalloc(&ctx->d_C64_split, KD * 8));
     HIPCHK(hipMalloc(&ctx->d_C32, Kp * ctx->Dp * 4));
     HIPCHK(hipMalloc(&ctx->d_rows, Kp * MF_ROW_BYTES));
-    HIPCHK(hipMalloc(&ctx->d_part, (uint64_t)ctx->G * KD * 8));
-    HIPCHK(hipMalloc(&ctx->d_part_cnt, (uint64_t)ctx->G * Kmax * 4));
+    // G per-CU slabs + one extra (rows the recheck / kd-tree resolve in the fused path)
+    HIPCHK(hipMalloc(&ctx->d_part, (uint64_t)(ctx->G + 1) * KD * 8));
+    HIPCHK(hipMalloc(&ctx->d_part_cnt, (uint64_t)(ctx->G + 1) * Kmax * 4));
     HIPCHK(hipMalloc(&ctx->d_sums, (2 * KD + Kmax) * 8));
     const unsigned mflags = hipHostMallocMapped | hipHostMallocCoherent;
     HIPCHK(hipHostMalloc(&ctx->h_cb, KD * 8, mflags));
@@ -311,9 +314,16 @@ qvq_status all_reduce_sums(qvq_ctx *ctx, uint32_t K) {
     return QVQ_OK;
 }
 
-qvq_status run_update(qvq_ctx *ctx, const uint32_t *d_A, uint32_t K) {
+// Slabs of the centroid sums under assignment d_A (no reduce).
+qvq_status run_update_slabs(qvq_ctx *ctx, const uint32_t *d_A, uint32_t K) {
     HIPCHK(launch_update(ctx->stream, ctx->Dp, ctx->G, ctx->d_codes, ctx->N, d_A, K, ctx->D, ctx->d_plut, ctx->d_part,
                          ctx->d_part_cnt));
+    return QVQ_OK;
+}
+
+qvq_status run_update(qvq_ctx *ctx, const uint32_t *d_A, uint32_t K) {
+    qvq_status st = run_update_slabs(ctx, d_A, K);
+    if (st != QVQ_OK) return st;
     HIPCHK(launch_reduce(ctx->stream, ctx->d_part, ctx->d_part_cnt, ctx->G, K, ctx->D, ctx->d_sums));
     return QVQ_OK;
 }
@@ -349,24 +359,26 @@ void build_tree(qvq_ctx *ctx, const double *hC, uint32_t K, int buf, KdView &kd)
 // Wait until finalize has published codebook seq in h_cb.  Polls the mapped flag; a stream
 // error or a drained stream without the flag ends the wait with an error (never hangs).
 qvq_status wait_codebook(qvq_ctx *ctx, uint64_t seq) {
+    // hipStreamQuery submits a marker (a few us of GPU idle), so the stream is consulted
+    // only every ~20 ms of waiting, to catch a failed or drained stream
     volatile uint64_t *flag = ctx->h_ready;
-    for (uint64_t spin = 0;; spin++) {
-        if (*flag >= seq) break;
-        if ((spin & 255) == 255) {
-            const hipError_t q = hipStreamQuery(ctx->stream);
-            if (q == hipSuccess) {
-                if (*flag >= seq) break;
-                return fail(ctx, QVQ_EDEVICE, "finalize finished without publishing the codebook");
-            }
-            if (q != hipErrorNotReady) return fail(ctx, QVQ_EDEVICE, std::string("stream: ") + hipGetErrorString(q));
+    auto next_check = std::chrono::steady_clock::now() + std::chrono::milliseconds(20);
+    while (*flag < seq) {
+        if (std::chrono::steady_clock::now() < next_check) continue;
+        const hipError_t q = hipStreamQuery(ctx->stream);
+        if (q == hipSuccess) {
+            if (*flag >= seq) break;
+            return fail(ctx, QVQ_EDEVICE, "finalize finished without publishing the codebook");
         }
+        if (q != hipErrorNotReady) return fail(ctx, QVQ_EDEVICE, std::string("stream: ") + hipGetErrorString(q));
+        next_check = std::chrono::steady_clock::now() + std::chrono::milliseconds(20);
     }
     std::atomic_thread_fence(std::memory_order_acquire);
     return QVQ_OK;
 }
 
 // Tie rows listed by the recheck when no device tree was available: answer them with the
-// host tree over hC, write A and (accumulate) add their terms to d_sums.  Synchronous.
+// host tree over hC, write A and (accumulate) add their terms to the extra slab G.  Synchronous.
 qvq_status resolve_host_ties(qvq_ctx *ctx, const double *hC, uint32_t K, uint32_t nt, bool accumulate) {
     const uint32_t D = ctx->D, Dp = ctx->Dp;
     const uint64_t need = (uint64_t)nt * (8 + Dp) + 8 + (uint64_t)nt * (2 * D + 1) * 16;   // + (idx, val) terms
@@ -391,15 +403,13 @@ qvq_status resolve_host_ties(qvq_ctx *ctx, const double *hC, uint32_t K, uint32_
     for (uint32_t i = 0; i < nt; i++) {
         for (uint32_t d = 0; d < D; d++) q[d] = ctx->terms.v64[code[(uint64_t)i * Dp + d]];
         vals[i] = tree.nearest(q.data());
-        if (accumulate) {
+        if (accumulate) {   // slab entries: packed hi << 32 | lo at d*K + k, count at KD + k
             for (uint32_t d = 0; d < D; d++) {
                 const uint8_t c = code[(uint64_t)i * Dp + d];
                 idx.push_back((uint64_t)d * K + vals[i]);
-                val.push_back(ctx->terms.hi[c]);
-                idx.push_back(KD + (uint64_t)d * K + vals[i]);
-                val.push_back(ctx->terms.lo[c]);
+                val.push_back((uint64_t)ctx->terms.hi[c] << 32 | ctx->terms.lo[c]);
             }
-            idx.push_back(2 * KD + vals[i]);
+            idx.push_back(KD + vals[i]);
             val.push_back(1);
         }
     }
@@ -410,7 +420,8 @@ qvq_status resolve_host_ties(qvq_ctx *ctx, const double *hC, uint32_t K, uint32_
         HIPCHK(hipMemcpyAsync(d_terms, idx.data(), nterms * 8ull, hipMemcpyHostToDevice, ctx->stream));
         HIPCHK(hipMemcpyAsync(d_terms + nterms, val.data(), nterms * 8ull, hipMemcpyHostToDevice, ctx->stream));
     }
-    HIPCHK(launch_scatter(ctx->stream, ctx->d_A, d_rows, d_vals, nt, ctx->d_sums, d_terms, d_terms + nterms, nterms));
+    HIPCHK(launch_scatter(ctx->stream, ctx->d_A, d_rows, d_vals, nt, ctx->d_part + (uint64_t)ctx->G * KD,
+                          ctx->d_part_cnt + (uint64_t)ctx->G * K, KD, d_terms, d_terms + nterms, nterms));
     HIPCHK(hipStreamSynchronize(ctx->stream));   // the host vectors must outlive the copies
     return QVQ_OK;
 }
@@ -418,11 +429,18 @@ qvq_status resolve_host_ties(qvq_ctx *ctx, const double *hC, uint32_t K, uint32_
 // One level's assignment of every row against the split codebook (d_C64_split, host copy
 // hC, search tables in d_C32/d_rows), K code vectors.  wait_seq != 0: hC is published by a
 // finalize still in flight.  With sums_out the exact centroid sums of the final assignment
-// are left in d_sums.
+// are left in the first ctx->nslabs slabs of d_part / d_part_cnt (fused: the search's G slabs
+// plus slab G for the rows the recheck and the kd-tree resolve; otherwise the update's G).
 qvq_status run_level(qvq_ctx *ctx, uint32_t K, int slot, bool sums_out, const double *hC, uint64_t wait_seq) {
     const bool fused = sums_out && use_fused(ctx, K);
+    uint64_t *xslab = fused ? ctx->d_part + (uint64_t)ctx->G * K * ctx->D : nullptr;
+    uint32_t *xcnt = fused ? ctx->d_part_cnt + (uint64_t)ctx->G * K : nullptr;
+    ctx->nslabs = fused ? ctx->G + 1 : ctx->G;
     unsigned *cnt = ctx->d_counters + 2 * slot;
-    HIPCHK(hipEventRecord(ctx->ev[slot][0], ctx->stream));
+    // HIP events around the search (each record costs a few us of GPU idle): every level,
+    // one level, or none (qvq_set_timing)
+    const bool timing = ctx->timing_level == -1 || ctx->timing_level == slot;
+    if (timing) HIPCHK(hipEventRecord(ctx->ev[slot][0], ctx->stream));
     if (use_mfma(ctx, K)) {
         HIPCHK(launch_assign_mfma(ctx->stream, ctx->num_cu, fused, ctx->d_codes, ctx->N, ctx->d_rows, K,
                                   ctx->d_C32, ctx->d_plut, ctx->mf_th, ctx->d_A, ctx->d_flags, &cnt[0],
@@ -433,14 +451,13 @@ qvq_status run_level(qvq_ctx *ctx, uint32_t K, int slot, bool sums_out, const do
         HIPCHK(launch_assign_valu(ctx->stream, ctx->num_cu, ctx->Dp, ctx->d_codes, ctx->N, ctx->d_C32, K,
                                   ctx->d_lut32, alpha, beta, gamma, ctx->d_A, ctx->d_flags, &cnt[0]));
     }
-    HIPCHK(hipEventRecord(ctx->ev[slot][1], ctx->stream));
-    if (fused) HIPCHK(launch_reduce(ctx->stream, ctx->d_part, ctx->d_part_cnt, ctx->num_cu, K, ctx->D, ctx->d_sums));
+    if (timing) HIPCHK(hipEventRecord(ctx->ev[slot][1], ctx->stream));
     {
         float alpha, beta, gamma;
         valu_coeffs(ctx, alpha, beta, gamma);
         HIPCHK(launch_recheck(ctx->stream, ctx->num_cu, ctx->d_codes, ctx->Dp, ctx->D, ctx->d_flags, &cnt[0],
                               ctx->d_C64_split, ctx->d_C32, K, ctx->d_lut64, alpha, beta, gamma, 1e-12, ctx->d_A,
-                              ctx->d_ties, &cnt[1], fused ? ctx->d_sums : nullptr, ctx->d_plut));
+                              ctx->d_ties, &cnt[1], xslab, xcnt, ctx->d_plut));
     }
     // the tree build overlaps the search just enqueued
     qvq_status st;
@@ -449,7 +466,7 @@ qvq_status run_level(qvq_ctx *ctx, uint32_t K, int slot, bool sums_out, const do
     build_tree(ctx, hC, K, slot & 1, kd);
     if (kd.depth > 0) {
         HIPCHK(launch_kd_resolve(ctx->stream, ctx->d_codes, ctx->Dp, ctx->D, ctx->d_ties, &cnt[1], ctx->d_C64_split,
-                                 K, ctx->d_lut64, kd, ctx->d_A, fused ? ctx->d_sums : nullptr, ctx->d_plut));
+                                 K, ctx->d_lut64, kd, ctx->d_A, xslab, xcnt, ctx->d_plut));
     } else {   // ties answered on the host
         unsigned nt = 0;
         HIPCHK(hipMemcpyAsync(&nt, &cnt[1], sizeof(nt), hipMemcpyDeviceToHost, ctx->stream));
@@ -459,7 +476,7 @@ qvq_status run_level(qvq_ctx *ctx, uint32_t K, int slot, bool sums_out, const do
     ctx->upd[slot] = sums_out && !fused;
     if (ctx->upd[slot]) {
         HIPCHK(hipEventRecord(ctx->ev[slot][2], ctx->stream));
-        if ((st = run_update(ctx, ctx->d_A, K)) != QVQ_OK) return st;
+        if ((st = run_update_slabs(ctx, ctx->d_A, K)) != QVQ_OK) return st;
         HIPCHK(hipEventRecord(ctx->ev[slot][3], ctx->stream));
     }
     return QVQ_OK;
@@ -717,8 +734,12 @@ QVQ_API qvq_status qvq_lbg(qvq_ctx *ctx, uint32_t bits, double eps, double *code
         const uint32_t K = 1u << lvl;
         const int slot = (int)lvl - 1;
         if ((st = run_level(ctx, K, slot, true, ctx->h_cb, ctx->seq)) != QVQ_OK) return st;
-        if ((st = all_reduce_sums(ctx, K)) != QVQ_OK) return st;
-        HIPCHK(finalize(K, lvl < bits));
+        const bool split = lvl < bits;
+        {
+            HIPCHK(launch_reduce(ctx->stream, ctx->d_part, ctx->d_part_cnt, ctx->nslabs, K, ctx->D, ctx->d_sums));
+            if ((st = all_reduce_sums(ctx, K)) != QVQ_OK) return st;
+            HIPCHK(finalize(K, split));
+        }
     }
     // Returned distortion: updateDistortion after the last fix (src/Quantizer.cpp:9-22,103),
     // from the sums of the final assignment (finalize_prep_kernel without split).
@@ -737,11 +758,13 @@ QVQ_API qvq_status qvq_lbg(qvq_ctx *ctx, uint32_t bits, double eps, double *code
         // assign: the search kernel; update: the non-fused update; other: the rest of the
         // level up to the next level's search (recheck, kd-tree, reduce, finalize, tables)
         float a = 0, u = 0, whole = 0;
-        (void)hipEventElapsedTime(&a, ctx->ev[lvl - 1][0], ctx->ev[lvl - 1][1]);
+        const bool timed = ctx->timing_level == -1 || ctx->timing_level == (int)lvl - 1;
+        if (timed) (void)hipEventElapsedTime(&a, ctx->ev[lvl - 1][0], ctx->ev[lvl - 1][1]);
         if (ctx->upd[lvl - 1]) (void)hipEventElapsedTime(&u, ctx->ev[lvl - 1][2], ctx->ev[lvl - 1][3]);
-        (void)hipEventElapsedTime(&whole, ctx->ev[lvl - 1][0], lvl < bits ? ctx->ev[lvl][0] : ctx->ev_end);
+        if (ctx->timing_level == -1)
+            (void)hipEventElapsedTime(&whole, ctx->ev[lvl - 1][0], lvl < bits ? ctx->ev[lvl][0] : ctx->ev_end);
         ctx->tm.assign_ms[lvl - 1] = a;
-        ctx->tm.other_ms[lvl - 1] = std::max(0.f, whole - a - u);
+        ctx->tm.other_ms[lvl - 1] = ctx->timing_level == -1 ? std::max(0.f, whole - a - u) : 0.f;
         ctx->tm.update_ms[lvl - 1] = u;
         ctx->tm.flagged[lvl - 1] = stats[2 * (lvl - 1)];
         ctx->tm.host_ties[lvl - 1] = stats[2 * (lvl - 1) + 1];
@@ -818,6 +841,12 @@ QVQ_API qvq_status qvq_comm_init(qvq_ctx *ctx, int nranks, int rank, const uint8
     ncclUniqueId u;
     std::memcpy(&u, id, 128);
     NCCLCHK(ncclCommInitRank(&ctx->comm, nranks, u, rank));
+    return QVQ_OK;
+}
+
+QVQ_API qvq_status qvq_set_timing(qvq_ctx *ctx, int level) {
+    if (!ctx || level < -2 || level > 31) return QVQ_EINVAL;
+    ctx->timing_level = level;
     return QVQ_OK;
 }
 

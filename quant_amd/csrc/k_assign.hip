@@ -133,23 +133,24 @@ __device__ inline void pair_update(const f32x4 &p0, const f32x4 &p1, uint32_t pa
 
 constexpr int MF_SMALL_K = 32;
 
-// SMALLK (K <= MF_SMALL_K): no MFMA at all -- each lane scans all K code vectors of its row
-// in the direct fp32 form (the recompute below), which is cheaper than the MFMA pass's
-// per-chunk fixed work when the codebook is this small.
-template <bool FUSE, bool STAGED, bool SMALLK>
+// SK > 0 (K <= SK <= MF_SMALL_K, SK a power of two): no MFMA at all -- each lane scans SK
+// code vectors of its row (rows K..SK-1 are zero padding and masked) in the direct fp32 form
+// (the recompute below), cheaper than the MFMA pass's per-chunk fixed work at this size.
+template <bool FUSE, bool STAGED, int SK>
 __global__ __launch_bounds__(MF_THREADS) void assign_mfma_kernel(
     const uint8_t *__restrict__ codes, uint64_t N, const _Float16 *__restrict__ g_rows, uint32_t K,
     const float *__restrict__ g_C32, const uint64_t *__restrict__ g_plut, MfThresholds th, uint32_t *__restrict__ A,
     uint32_t *__restrict__ flags, unsigned *__restrict__ flag_cnt, uint64_t *__restrict__ part,
     uint32_t *__restrict__ part_cnt) {
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+    constexpr bool SMALLK = SK > 0;
     const uint32_t Kp = (K + 31) & ~31u;
     const MfLds L = mf_lds_layout(K, FUSE, STAGED);
     unsigned char *rows = lds;   // Kp x 56 B code-vector rows, then 16 B zero pad
     float *c32s = reinterpret_cast<float *>(lds + L.c32);
     uint64_t *sums = reinterpret_cast<uint64_t *>(lds + L.sums);   // [d][k]
     uint32_t *cnt = reinterpret_cast<uint32_t *>(lds + L.cnt);
-    uint64_t *plut = reinterpret_cast<uint64_t *>(lds + L.plut);
+    uint8_t *lo8 = lds + L.plut;   // low part of each byte's exact term (high part: b ^ 0x80)
     const int tid = threadIdx.x;
     if (!SMALLK) {
         const uint64_t *src = reinterpret_cast<const uint64_t *>(g_rows);
@@ -165,7 +166,11 @@ __global__ __launch_bounds__(MF_THREADS) void assign_mfma_kernel(
     if (FUSE) {
         for (uint32_t i = tid; i < K * MF_D; i += MF_THREADS) sums[i] = 0;
         for (uint32_t i = tid; i < K; i += MF_THREADS) cnt[i] = 0;
-        if (tid < 256) plut[tid] = g_plut[tid];
+        if (tid < 256) lo8[tid] = (uint8_t)(g_plut[tid] & 0xFF);
+        if (blockIdx.x == 0) {   // the extra slab G (recheck / tie rows), after all G others
+            for (uint32_t i = tid; i < K * MF_D; i += MF_THREADS) part[(uint64_t)gridDim.x * K * MF_D + i] = 0;
+            for (uint32_t i = tid; i < K; i += MF_THREADS) part_cnt[(uint64_t)gridDim.x * K + i] = 0;
+        }
     }
     __syncthreads();
     const float *C32 = STAGED ? c32s : g_C32;
@@ -327,10 +332,10 @@ __global__ __launch_bounds__(MF_THREADS) void assign_mfma_kernel(
             // a unit is 4 code vectors of each tile of its pair; up to K = 16 the second
             // tile is padding, and below 4 so is the rest of the first
             // SMALLK: the unit is the whole codebook
-            const int jn = SMALLK ? (int)K : (K <= 16 ? (K < 4 ? (int)K : 4) : 8);
+            const int jn = SMALLK ? SK : (K <= 16 ? (K < 4 ? (int)K : 4) : 8);
 #pragma unroll
-            for (int j = 0; j < (SMALLK ? MF_SMALL_K : 8); j++) {
-                if (j >= jn) continue;   // uniform: K is
+            for (int j = 0; j < (SMALLK ? SK : 8); j++) {
+                if (!SMALLK && j >= jn) continue;   // uniform: K is
                 const uint32_t cv = SMALLK ? (uint32_t)j : (2 * pr + (j >> 2)) * 16 + 4 * gg + (j & 3);
                 const float4 *c4 = reinterpret_cast<const float4 *>(C32 + (size_t)cv * MF_D);
                 float dist = 0.f;
@@ -362,8 +367,8 @@ __global__ __launch_bounds__(MF_THREADS) void assign_mfma_kernel(
                 uint32_t v[MF_D + 1];
 #pragma unroll
                 for (int d = 0; d < MF_D; d++) {
-                    const uint64_t p = plut[(own[d / 4] >> (8 * (d % 4))) & 0xFF];
-                    v[d] = take ? (uint32_t)(((p >> 32) << 16) | (p & 0xFFFF)) : 0u;   // <= 64 rows: no carry
+                    const uint32_t b = (own[d / 4] >> (8 * (d % 4))) & 0xFF;
+                    v[d] = take ? ((b ^ 0x80u) << 16 | lo8[b]) : 0u;   // <= 64 rows: no carry
                 }
                 v[MF_D] = take ? 1u : 0u;
                 const bool tail = wave_runs_reduce(take ? rk : 0xFFFFFFFFu, v, lane);
@@ -377,8 +382,11 @@ __global__ __launch_bounds__(MF_THREADS) void assign_mfma_kernel(
             } else if (take) {
 #pragma unroll
                 for (int d = 0; d < MF_D; d++)
+                {
+                    const uint32_t b = (own[d / 4] >> (8 * (d % 4))) & 0xFF;
                     atomicAdd((unsigned long long *)&sums[(uint32_t)d * K + rk],
-                              (unsigned long long)plut[(own[d / 4] >> (8 * (d % 4))) & 0xFF]);
+                              (unsigned long long)((uint64_t)(b ^ 0x80u) << 32 | lo8[b]));
+                }
                 atomicAdd(&cnt[rk], 1u);
             }
         }
@@ -392,7 +400,163 @@ __global__ __launch_bounds__(MF_THREADS) void assign_mfma_kernel(
     }
 }
 
-template <bool F, bool S, bool SK>
+// ---------------------------------------------------------------------------------------
+// Small codebooks (K <= MF_SMALL_K): direct fp32 scan of all SK code vectors per row, rows in
+// per-lane runs.  Each wave owns a contiguous range of rows and each lane a contiguous
+// sub-range (a multiple of 4 rows, loaded 48 bytes at a time), so at small K consecutive rows
+// of a lane mostly share their code vector: their exact terms (u << 16 | lo per component,
+// no carry within 256 rows) are added in registers and go to the LDS sums only when the
+// index changes.  Flag rule and sums as in assign_mfma_kernel.
+// ---------------------------------------------------------------------------------------
+template <int SK, bool FUSE>
+__global__ __launch_bounds__(MF_THREADS) void assign_small_kernel(
+    const uint8_t *__restrict__ codes, uint64_t N, uint32_t K, const float *__restrict__ g_C32,
+    const uint64_t *__restrict__ g_plut, MfThresholds th, uint64_t rows_per_lane, uint32_t *__restrict__ A,
+    uint32_t *__restrict__ flags, unsigned *__restrict__ flag_cnt, uint64_t *__restrict__ part,
+    uint32_t *__restrict__ part_cnt) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+    const MfLds L = mf_lds_layout(K, FUSE, true);
+    float *c32s = reinterpret_cast<float *>(lds + L.c32);
+    uint64_t *sums = reinterpret_cast<uint64_t *>(lds + L.sums);   // [d][k]
+    uint32_t *cnt = reinterpret_cast<uint32_t *>(lds + L.cnt);
+    uint8_t *lo8 = lds + L.plut;   // low part of each byte's exact term (high part: b ^ 0x80)
+    const int tid = threadIdx.x;
+    for (uint32_t i = tid; i < (uint32_t)SK * (MF_D / 4); i += MF_THREADS)
+        reinterpret_cast<float4 *>(c32s)[i] = reinterpret_cast<const float4 *>(g_C32)[i];
+    if (FUSE) {
+        for (uint32_t i = tid; i < K * MF_D; i += MF_THREADS) sums[i] = 0;
+        for (uint32_t i = tid; i < K; i += MF_THREADS) cnt[i] = 0;
+        if (tid < 256) lo8[tid] = (uint8_t)(g_plut[tid] & 0xFF);
+        if (blockIdx.x == 0) {   // the extra slab G (recheck / tie rows), after all G others
+            for (uint32_t i = tid; i < K * MF_D; i += MF_THREADS) part[(uint64_t)gridDim.x * K * MF_D + i] = 0;
+            for (uint32_t i = tid; i < K; i += MF_THREADS) part_cnt[(uint64_t)gridDim.x * K + i] = 0;
+        }
+    }
+    __syncthreads();
+
+    const int lane = tid & 63, wave = tid >> 6;
+    const uint64_t first = ((uint64_t)blockIdx.x * MF_WAVES + wave) * 64 * rows_per_lane + lane * rows_per_lane;
+    const uint64_t last = min(first + rows_per_lane, N);
+    uint32_t acc[MF_D + 1];
+    uint32_t cur = 0xFFFFFFFFu;
+#pragma unroll
+    for (int i = 0; i <= MF_D; i++) acc[i] = 0;
+    auto flush = [&]() {
+        if (cur != 0xFFFFFFFFu && acc[MF_D]) {
+#pragma unroll
+            for (int d = 0; d < MF_D; d++)
+                atomicAdd((unsigned long long *)&sums[(uint32_t)d * K + cur],
+                          (unsigned long long)((((uint64_t)(acc[d] >> 16)) << 32) | (acc[d] & 0xFFFF)));
+            atomicAdd(&cnt[cur], acc[MF_D]);
+        }
+#pragma unroll
+        for (int i = 0; i <= MF_D; i++) acc[i] = 0;
+    };
+    // the next four rows' words are loaded one iteration ahead
+    auto load4 = [&](uint64_t r0, uint32_t (&w)[4][3]) {
+        if (r0 + 4 <= last) {
+            const uint4 *p = reinterpret_cast<const uint4 *>(codes + r0 * MF_D);
+            const uint4 a = p[0], b = p[1], c = p[2];
+            const uint32_t v[12] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w, c.x, c.y, c.z, c.w};
+#pragma unroll
+            for (int r = 0; r < 4; r++)
+#pragma unroll
+                for (int i = 0; i < 3; i++) w[r][i] = v[3 * r + i];
+        } else {
+#pragma unroll
+            for (int r = 0; r < 4; r++)
+#pragma unroll
+                for (int i = 0; i < 3; i++)
+                    w[r][i] = r0 + r < last ? reinterpret_cast<const uint32_t *>(codes + (r0 + r) * MF_D)[i]
+                                            : 0x80808080u;
+        }
+    };
+    uint32_t wn[4][3];
+    load4(first, wn);
+    for (uint64_t r0 = first; r0 < last; r0 += 4) {
+        uint32_t w[4][3];
+#pragma unroll
+        for (int r = 0; r < 4; r++)
+#pragma unroll
+            for (int i = 0; i < 3; i++) w[r][i] = wn[r][i];
+        if (r0 + 4 < last) load4(r0 + 4, wn);
+        // four rows at once: each code vector's 12 values are loaded once (scalar) for all
+        // four, and the four distance chains are independent
+        float x[4][MF_D];
+#pragma unroll
+        for (int r = 0; r < 4; r++)
+#pragma unroll
+            for (int d = 0; d < MF_D; d++) x[r][d] = __fmaf_rn(byte_w(w[r][d / 4], d % 4), th.sx, th.mu);
+        float r1[4], r2[4];
+        uint32_t idx[4];
+#pragma unroll
+        for (int r = 0; r < 4; r++) {
+            r1[r] = INFINITY;
+            r2[r] = INFINITY;
+            idx[r] = 0;
+        }
+#pragma unroll 2
+        for (int j = 0; j < SK; j++) {
+            // wave-uniform: scalar loads into SGPRs (VALU reads them as operands), not LDS
+            // broadcasts, which cost the full 64-lane return bandwidth
+            const float *cj = g_C32 + j * MF_D;
+            float cr[MF_D];
+#pragma unroll
+            for (int d = 0; d < MF_D; d++) cr[d] = cj[d];
+#pragma unroll
+            for (int r = 0; r < 4; r++) {
+                float dist = 0.f;
+#pragma unroll
+                for (int d = 0; d < MF_D; d++) {
+                    const float e = x[r][d] - cr[d];
+                    dist = __fmaf_rn(e, e, dist);
+                }
+                dist = (uint32_t)j < K ? dist : INFINITY;
+                r2[r] = med3f(r1[r], r2[r], dist);
+                idx[r] = dist < r1[r] ? (uint32_t)j : idx[r];
+                r1[r] = min2f(r1[r], dist);
+            }
+        }
+#pragma unroll
+        for (int r = 0; r < 4; r++) {
+            const uint64_t row = r0 + r;
+            const uint32_t rk = idx[r];
+            const float thr = 2.f * (th.alpha * sqrtf(r2[r]) + th.beta * r2[r]) + th.gamma;
+            const bool valid = row < last;
+            const bool flagged = valid && !(r2[r] - r1[r] > thr);
+            if (flagged) flags[atomicAdd(flag_cnt, 1u)] = (uint32_t)row;
+            if (FUSE && valid && !flagged) {
+                if (rk != cur || acc[MF_D] == 256) {   // 16-bit fields hold 256 rows
+                    flush();
+                    cur = rk;
+                }
+#pragma unroll
+                for (int d = 0; d < MF_D; d++) {
+                    const uint32_t b = (w[r][d / 4] >> (8 * (d % 4))) & 0xFF;
+                    acc[d] += (b ^ 0x80u) << 16 | lo8[b];
+                }
+                acc[MF_D] += 1;
+            }
+        }
+        if (r0 + 4 <= last) {
+            *reinterpret_cast<uint4 *>(A + r0) = make_uint4(idx[0], idx[1], idx[2], idx[3]);
+        } else {
+#pragma unroll
+            for (int r = 0; r < 4; r++)
+                if (r0 + r < last) A[r0 + r] = idx[r];
+        }
+    }
+    if (FUSE) {
+        flush();
+        __syncthreads();
+        uint64_t *pdst = part + (uint64_t)blockIdx.x * K * MF_D;   // slab layout [d][k]
+        for (uint32_t i = tid; i < K * MF_D; i += MF_THREADS) pdst[i] = sums[i];
+        uint32_t *cdst = part_cnt + (uint64_t)blockIdx.x * K;
+        for (uint32_t i = tid; i < K; i += MF_THREADS) cdst[i] = cnt[i];
+    }
+}
+
+template <bool F, bool S, int SK>
 static void launch_mfma_variant(hipStream_t s, int grid, size_t lds, const uint8_t *codes, uint64_t N,
                                 const _Float16 *cb_rows, uint32_t K, const float *C32, const uint64_t *plut,
                                 const MfThresholds &th, uint32_t *A, uint32_t *flags, unsigned *flag_cnt,
@@ -412,15 +576,41 @@ hipError_t launch_assign_mfma(hipStream_t s, int grid, bool fuse, const uint8_t 
                               const MfThresholds &th, uint32_t *A, uint32_t *flags, unsigned *flag_cnt,
                               uint64_t *part, uint32_t *part_cnt) {
     const bool staged = mf_lds_layout(K, fuse, true).total <= MF_LDS_MAX;
-    const bool small = K <= mf_small_k() && staged;
     const size_t lds = mf_lds_layout(K, fuse, staged).total;
     using Fn = void (*)(hipStream_t, int, size_t, const uint8_t *, uint64_t, const _Float16 *, uint32_t, const float *,
                         const uint64_t *, const MfThresholds &, uint32_t *, uint32_t *, unsigned *, uint64_t *,
                         uint32_t *);
     Fn fn;
-    if (small) fn = fuse ? launch_mfma_variant<true, true, true> : launch_mfma_variant<false, true, true>;
-    else if (fuse) fn = staged ? launch_mfma_variant<true, true, false> : launch_mfma_variant<true, false, false>;
-    else fn = staged ? launch_mfma_variant<false, true, false> : launch_mfma_variant<false, false, false>;
+    if (K <= mf_small_k() && staged) {   // C32 is padded with zero rows up to 32
+        const uint32_t sk = K <= 2 ? 2 : K <= 4 ? 4 : K <= 8 ? 8 : K <= 16 ? 16 : 32;
+        // rows per lane: a multiple of 4 covering N over grid x 16 waves x 64 lanes
+        const uint64_t lanes = (uint64_t)grid * MF_WAVES * 64;
+        const uint64_t rpl = ((N + lanes - 1) / lanes + 3) / 4 * 4;
+        const size_t slds = mf_lds_layout(K, fuse, true).total;
+#define QVQ_SMALL(V)                                                                                              \
+    do {                                                                                                          \
+        if (fuse)                                                                                                 \
+            hipLaunchKernelGGL((assign_small_kernel<V, true>), dim3(grid), dim3(MF_THREADS), slds, s, codes, N, K, \
+                               C32, plut, th, rpl, A, flags, flag_cnt, part, part_cnt);                          \
+        else                                                                                                      \
+            hipLaunchKernelGGL((assign_small_kernel<V, false>), dim3(grid), dim3(MF_THREADS), slds, s, codes, N,  \
+                               K, C32, plut, th, rpl, A, flags, flag_cnt, part, part_cnt);                        \
+    } while (0)
+        switch (sk) {
+        case 2: QVQ_SMALL(2); break;
+        case 4: QVQ_SMALL(4); break;
+        case 8: QVQ_SMALL(8); break;
+        case 16: QVQ_SMALL(16); break;
+        default: QVQ_SMALL(32); break;
+        }
+#undef QVQ_SMALL
+        return hipGetLastError();
+    }
+    if (fuse) {
+        fn = staged ? launch_mfma_variant<true, true, 0> : launch_mfma_variant<true, false, 0>;
+    } else {
+        fn = staged ? launch_mfma_variant<false, true, 0> : launch_mfma_variant<false, false, 0>;
+    }
     fn(s, grid, lds, codes, N, cb_rows, K, C32, plut, th, A, flags, flag_cnt, part, part_cnt);
     return hipGetLastError();
 }
@@ -608,7 +798,7 @@ __global__ __launch_bounds__(RECHECK_THREADS) void recheck_kernel(
     const unsigned int *__restrict__ flag_cnt, const double *__restrict__ C64, const float *__restrict__ g_C32,
     uint32_t K, const double *__restrict__ lut64, float alpha, float beta, float gamma, double tie_rel,
     uint32_t *__restrict__ A, uint32_t *__restrict__ ties, unsigned int *__restrict__ tie_cnt,
-    uint64_t *__restrict__ sums, const uint64_t *__restrict__ plut) {
+    uint64_t *__restrict__ xslab, uint32_t *__restrict__ xcnt, const uint64_t *__restrict__ plut) {
     extern __shared__ __attribute__((aligned(16))) double rsm[];
     constexpr int W = RECHECK_WAVES;
     double *xs = rsm;                                              // [W][64] fp64 row
@@ -691,12 +881,10 @@ __global__ __launch_bounds__(RECHECK_THREADS) void recheck_kernel(
             if (lane == 0) ties[atomicAdd(tie_cnt, 1u)] = row;
             continue;
         }
-        if (sums && lane < (int)D) {
-            const uint64_t KD = (uint64_t)K * D;
-            const uint64_t p = plut[codes[(uint64_t)row * Dp + lane]];
-            atomicAdd((unsigned long long *)&sums[(uint64_t)lane * K + k1], (unsigned long long)(p >> 32));
-            atomicAdd((unsigned long long *)&sums[KD + (uint64_t)lane * K + k1], (unsigned long long)(p & 0xFFFFFFFFull));
-            if (lane == 0) atomicAdd((unsigned long long *)&sums[2 * KD + k1], 1ull);
+        if (xslab && lane < (int)D) {   // the extra slab: packed hi << 32 | lo, and counts
+            atomicAdd((unsigned long long *)&xslab[(uint64_t)lane * K + k1],
+                      (unsigned long long)plut[codes[(uint64_t)row * Dp + lane]]);
+            if (lane == 0) atomicAdd(&xcnt[k1], 1u);
         }
     }
 }
@@ -706,15 +894,16 @@ static void launch_recheck_variant(hipStream_t s, int grid, size_t lds, const ui
                                    const uint32_t *flags, const unsigned *flag_cnt, const double *C64,
                                    const float *C32, uint32_t K, const double *lut64, float alpha, float beta,
                                    float gamma, double tie_rel, uint32_t *A, uint32_t *ties, unsigned *tie_cnt,
-                                   uint64_t *sums, const uint64_t *plut) {
+                                   uint64_t *xslab, uint32_t *xcnt, const uint64_t *plut) {
     hipLaunchKernelGGL((recheck_kernel<S, DT>), dim3(grid), dim3(RECHECK_THREADS), lds, s, codes, Dp, D, flags,
-                       flag_cnt, C64, C32, K, lut64, alpha, beta, gamma, tie_rel, A, ties, tie_cnt, sums, plut);
+                       flag_cnt, C64, C32, K, lut64, alpha, beta, gamma, tie_rel, A, ties, tie_cnt, xslab, xcnt, plut);
 }
 
 hipError_t launch_recheck(hipStream_t s, int num_cu, const uint8_t *codes, uint32_t Dp, uint32_t D,
                           const uint32_t *flags, const unsigned *flag_cnt, const double *C64, const float *C32,
                           uint32_t K, const double *lut64, float alpha, float beta, float gamma, double tie_rel,
-                          uint32_t *A, uint32_t *ties, unsigned *tie_cnt, uint64_t *sums, const uint64_t *plut) {
+                          uint32_t *A, uint32_t *ties, unsigned *tie_cnt, uint64_t *xslab, uint32_t *xcnt,
+                          const uint64_t *plut) {
     if (Dp % 4 || Dp > 64) return hipErrorInvalidValue;
     const size_t base = (size_t)RECHECK_WAVES * 64 * 12;
     const size_t cb = (size_t)K * recheck_c32_stride(Dp) * 4;
@@ -722,7 +911,7 @@ hipError_t launch_recheck(hipStream_t s, int num_cu, const uint8_t *codes, uint3
     const size_t lds = base + (staged ? cb : 0);
 #define QVQ_RC(SS, DT)                                                                                             \
     launch_recheck_variant<SS, DT>(s, num_cu, lds, codes, Dp, D, flags, flag_cnt, C64, C32, K, lut64, alpha, beta, \
-                                   gamma, tie_rel, A, ties, tie_cnt, sums, plut)
+                                   gamma, tie_rel, A, ties, tie_cnt, xslab, xcnt, plut)
     if (Dp == 12) {
         if (staged) QVQ_RC(true, 12); else QVQ_RC(false, 12);
     } else if (Dp == 48) {
@@ -864,8 +1053,8 @@ bool kd_resolve_fits(const KdView &kd, uint32_t K) { return kd.depth > 0 && kd_w
 __global__ __launch_bounds__(KDR_MAX_WAVES * 64) void kd_resolve_kernel(
     const uint8_t *__restrict__ codes, uint32_t Dp, uint32_t D, const uint32_t *__restrict__ ties,
     const unsigned *__restrict__ tie_cnt, const double *__restrict__ C64, uint32_t K,
-    const double *__restrict__ lut64, KdView kd, uint32_t *__restrict__ A, uint64_t *__restrict__ sums,
-    const uint64_t *__restrict__ plut) {
+    const double *__restrict__ lut64, KdView kd, uint32_t *__restrict__ A, uint64_t *__restrict__ xslab,
+    uint32_t *__restrict__ xcnt, const uint64_t *__restrict__ plut) {
     extern __shared__ __attribute__((aligned(16))) double ksm[];
     const int W = blockDim.x / 64;
     const int Z = kd.depth;
@@ -893,12 +1082,10 @@ __global__ __launch_bounds__(KDR_MAX_WAVES * 64) void kd_resolve_kernel(
         wave_lds_sync();
         const uint32_t k = kd_nearest_wave(xs, D, kv, pv, sd, sn, dl, lane);
         if (lane == 0) A[row] = k;
-        if (sums && lane < (int)D) {
-            const uint64_t KD = (uint64_t)K * D;
-            const uint64_t p = plut[codes[(uint64_t)row * Dp + lane]];
-            atomicAdd((unsigned long long *)&sums[(uint64_t)lane * K + k], (unsigned long long)(p >> 32));
-            atomicAdd((unsigned long long *)&sums[KD + (uint64_t)lane * K + k], (unsigned long long)(p & 0xFFFFFFFFull));
-            if (lane == 0) atomicAdd((unsigned long long *)&sums[2 * KD + k], 1ull);
+        if (xslab && lane < (int)D) {
+            atomicAdd((unsigned long long *)&xslab[(uint64_t)lane * K + k],
+                      (unsigned long long)plut[codes[(uint64_t)row * Dp + lane]]);
+            if (lane == 0) atomicAdd(&xcnt[k], 1u);
         }
         wave_lds_sync();
     }
@@ -906,12 +1093,12 @@ __global__ __launch_bounds__(KDR_MAX_WAVES * 64) void kd_resolve_kernel(
 
 hipError_t launch_kd_resolve(hipStream_t s, const uint8_t *codes, uint32_t Dp, uint32_t D, const uint32_t *ties,
                              const unsigned *tie_cnt, const double *C64, uint32_t K, const double *lut64,
-                             const KdView &kd, uint32_t *A, uint64_t *sums, const uint64_t *plut) {
+                             const KdView &kd, uint32_t *A, uint64_t *xslab, uint32_t *xcnt, const uint64_t *plut) {
     const int W = kd.depth > 0 ? kd_waves(kd, K) : 0;
     if (W == 0) return hipErrorInvalidValue;
     const size_t lds = kd_tree_bytes(kd) + (size_t)W * kd_wave_bytes(kd, K);
     hipLaunchKernelGGL(kd_resolve_kernel, dim3(KDR_BLOCKS), dim3(64 * W), lds, s, codes, Dp, D, ties, tie_cnt, C64,
-                       K, lut64, kd, A, sums, plut);
+                       K, lut64, kd, A, xslab, xcnt, plut);
     return hipGetLastError();
 }
 

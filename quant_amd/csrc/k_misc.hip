@@ -127,8 +127,168 @@ __global__ __launch_bounds__(UPDATE_THREADS) void update_kernel(
 
 #define QVQ_FOR_EACH_DP(X) X(4) X(8) X(12) X(16) X(20) X(24) X(28) X(32) X(36) X(40) X(44) X(48) X(52) X(56) X(60) X(64)
 
+// Centroid sums of a final assignment, HBM-bound.  A wave takes 256 consecutive rows per
+// round, lane L rows 4L..4L+3 (coalesced: 4*DP code bytes and 16 index bytes per lane).  A
+// lane adds the exact terms of its rows with equal index in registers (u << 16 | lo per
+// component, no carry below 256 rows) and flushes a run to the LDS sums [d][k] when the index
+// changes and at the end of the round -- except when all 256 rows of the round share one
+// index (common at small K), then the wave folds its registers with DPP and one lane adds.
+// At small K many lanes flush to the same few addresses at once, which the LDS serialises:
+// the sums are replicated C times (lane L adds into copy L mod C) and the copies are summed
+// when the workgroup writes its slab [g][d][k] for reduce_kernel.
+constexpr int URUN_THREADS = 1024;
+constexpr size_t URUN_LDS = 160 * 1024;
+
+static size_t urun_bytes(uint32_t K, uint32_t D, uint32_t C) {
+    return (size_t)C * K * D * 8 + (size_t)C * ((K + 1) & ~1u) * 4 + 256;
+}
+static uint32_t urun_copies(uint32_t K, uint32_t D) {
+    for (uint32_t C : {16u, 8u, 4u, 2u})
+        if (urun_bytes(K, D, C) <= URUN_LDS / 2) return C;   // replicas only while they are cheap
+    return 1;
+}
+bool update_runs_fits(uint32_t K, uint32_t D) { return urun_bytes(K, D, 1) <= URUN_LDS; }
+
+template <int CTRL, int ROW_MASK>
+__device__ inline uint32_t urun_dpp(uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, ROW_MASK, 0xF, true);
+}
+__device__ inline uint32_t urun_wave_sum(uint32_t v) {   // total in lane 63
+    v += urun_dpp<0x111, 0xF>(v);
+    v += urun_dpp<0x112, 0xF>(v);
+    v += urun_dpp<0x114, 0xF>(v);
+    v += urun_dpp<0x118, 0xF>(v);
+    v += urun_dpp<0x142, 0xA>(v);
+    v += urun_dpp<0x143, 0xC>(v);
+    return v;
+}
+
+template <int DP>
+__global__ __launch_bounds__(URUN_THREADS) void update_runs_kernel(const uint8_t *__restrict__ codes, uint64_t N,
+                                                                   const uint32_t *__restrict__ A, uint32_t K,
+                                                                   uint32_t D, uint32_t C, const uint64_t *__restrict__ plut,
+                                                                   uint64_t *__restrict__ part,
+                                                                   uint32_t *__restrict__ part_cnt) {
+    extern __shared__ __attribute__((aligned(16))) uint64_t usm[];
+    const uint32_t K2 = (K + 1) & ~1u;
+    uint64_t *sums_all = usm;                                                         // [C][D][K]
+    uint32_t *cnt_all = reinterpret_cast<uint32_t *>(usm + (size_t)C * K * D);       // [C][K2]
+    uint8_t *lo8 = reinterpret_cast<uint8_t *>(cnt_all + (size_t)C * K2);            // [256]
+    const int tid = threadIdx.x, lane = tid & 63;
+    for (uint32_t i = tid; i < C * K * D; i += URUN_THREADS) sums_all[i] = 0;
+    for (uint32_t i = tid; i < C * K2; i += URUN_THREADS) cnt_all[i] = 0;
+    uint64_t *sums = sums_all + (size_t)(lane % C) * K * D;   // this lane's copy
+    uint32_t *cnt = cnt_all + (size_t)(lane % C) * K2;
+    if (tid < 256) lo8[tid] = (uint8_t)(plut[tid] & 0xFF);
+    __syncthreads();
+    constexpr int W4 = DP / 4;   // code words per row
+    uint32_t acc[DP + 1];
+    uint32_t cur = 0xFFFFFFFFu;
+#pragma unroll
+    for (int i = 0; i <= DP; i++) acc[i] = 0;
+    auto flush = [&]() {
+        if (acc[DP]) {
+#pragma unroll
+            for (int d = 0; d < DP; d++)
+                if ((uint32_t)d < D)
+                    atomicAdd((unsigned long long *)&sums[(uint32_t)d * K + cur],
+                              (unsigned long long)((((uint64_t)(acc[d] >> 16)) << 32) | (acc[d] & 0xFFFF)));
+            atomicAdd(&cnt[cur], acc[DP]);
+        }
+#pragma unroll
+        for (int i = 0; i <= DP; i++) acc[i] = 0;
+    };
+    auto add_row = [&](const uint32_t *w, uint32_t k) {
+        if (k != cur) {
+            flush();
+            cur = k;
+        }
+#pragma unroll
+        for (int d = 0; d < DP; d++) {
+            const uint32_t b = (w[d / 4] >> (8 * (d % 4))) & 0xFF;
+            acc[d] += (b ^ 0x80u) << 16 | lo8[b];
+        }
+        acc[DP] += 1;
+    };
+    const uint64_t wave_g = ((uint64_t)blockIdx.x * URUN_THREADS + tid) >> 6;
+    const uint64_t n_waves = ((uint64_t)gridDim.x * URUN_THREADS) >> 6;
+    for (uint64_t r0 = wave_g * 256; r0 < N; r0 += n_waves * 256) {
+        const uint64_t row = r0 + 4 * (uint64_t)lane;
+        bool uniform = false;
+        if (r0 + 256 <= N) {
+            uint32_t w[4 * W4];
+            const uint4 *p = reinterpret_cast<const uint4 *>(codes + row * DP);
+#pragma unroll
+            for (int i = 0; i < W4; i++) {
+                const uint4 v = p[i];
+                w[4 * i] = v.x;
+                w[4 * i + 1] = v.y;
+                w[4 * i + 2] = v.z;
+                w[4 * i + 3] = v.w;
+            }
+            const uint4 a = *reinterpret_cast<const uint4 *>(A + row);
+            add_row(w, a.x);
+            add_row(w + W4, a.y);
+            add_row(w + 2 * W4, a.z);
+            add_row(w + 3 * W4, a.w);
+            // one index for the whole round (and no earlier run left in a lane)?
+            const uint32_t k0 = __shfl(a.x, 0);
+            uniform = __all(a.x == k0 && a.w == k0 && acc[DP] == 4);
+        } else {
+            for (uint64_t r = row; r < row + 4 && r < N; r++) {
+                uint32_t w[W4];
+#pragma unroll
+                for (int i = 0; i < W4; i++) w[i] = reinterpret_cast<const uint32_t *>(codes + r * DP)[i];
+                add_row(w, A[r]);
+            }
+        }
+        if (uniform) {
+#pragma unroll
+            for (int d = 0; d < DP; d++) {
+                const uint32_t t = urun_wave_sum(acc[d]);   // 256 rows: still no carry
+                if (lane == 63 && (uint32_t)d < D)
+                    atomicAdd((unsigned long long *)&sums[(uint32_t)d * K + cur],
+                              (unsigned long long)((((uint64_t)(t >> 16)) << 32) | (t & 0xFFFF)));
+            }
+            if (lane == 63) atomicAdd(&cnt[cur], 256u);
+#pragma unroll
+            for (int i = 0; i <= DP; i++) acc[i] = 0;
+        } else {
+            flush();
+        }
+        cur = 0xFFFFFFFFu;
+    }
+    __syncthreads();
+    uint64_t *pdst = part + (uint64_t)blockIdx.x * K * D;
+    for (uint32_t i = tid; i < K * D; i += URUN_THREADS) {
+        uint64_t t = 0;
+        for (uint32_t c = 0; c < C; c++) t += sums_all[(size_t)c * K * D + i];
+        pdst[i] = t;
+    }
+    uint32_t *cdst = part_cnt + (uint64_t)blockIdx.x * K;
+    for (uint32_t i = tid; i < K; i += URUN_THREADS) {
+        uint32_t t = 0;
+        for (uint32_t c = 0; c < C; c++) t += cnt_all[(size_t)c * K2 + i];
+        cdst[i] = t;
+    }
+}
+
 hipError_t launch_update(hipStream_t s, uint32_t Dp, uint32_t G, const uint8_t *codes, uint64_t N, const uint32_t *A,
                          uint32_t K, uint32_t D, const uint64_t *plut, uint64_t *part, uint32_t *part_cnt) {
+    if (update_runs_fits(K, D)) {
+        const uint32_t C = urun_copies(K, D);
+        const size_t lds = urun_bytes(K, D, C);
+        switch (Dp) {
+#define X(DPV)                                                                                                     \
+    case DPV:                                                                                                      \
+        hipLaunchKernelGGL(update_runs_kernel<DPV>, dim3(G), dim3(URUN_THREADS), lds, s, codes, N, A, K, D, C,    \
+                           plut, part, part_cnt);                                                                  \
+        return hipGetLastError();
+            QVQ_FOR_EACH_DP(X)
+#undef X
+        }
+        return hipErrorInvalidValue;
+    }
     const size_t per_k = (size_t)D * 8 + 4;
     const uint32_t KR = (uint32_t)std::min<size_t>(K, (UPDATE_LDS - 2048 - 16) / per_k);
     if (KR == 0) return hipErrorInvalidValue;
@@ -269,42 +429,54 @@ hipError_t launch_mean_sums(hipStream_t s, uint32_t Dp, const uint8_t *codes, ui
 // the per-block distortion terms in block order and then publishes *ready = seq (system
 // scope), which tells the host that host_cb holds the codebook.
 
-__global__ __launch_bounds__(256) void finalize_prep_kernel(
-    const uint64_t *__restrict__ sums, uint32_t K, uint32_t D, uint32_t Dp, int64_t R, int64_t bias, int scale,
-    double *__restrict__ C_cent, int split, double *__restrict__ C64n, uint32_t Kpad_next, double mu, double sx,
-    double scale_t, float *__restrict__ C32, _Float16 *__restrict__ rows, double *__restrict__ host_cb,
-    double *__restrict__ dist_part, unsigned *__restrict__ done, double *__restrict__ dist_out,
-    volatile uint64_t *ready, uint64_t seq, uint32_t L) {
+struct FinArgs {
+    const uint64_t *sums;
+    uint32_t K, D, Dp;
+    int64_t R, bias;
+    int scale;
+    double *C_cent;
+    int split;
+    double *C64n;
+    uint32_t Kpad_next;
+    double mu, sx, scale_t;
+    float *C32;
+    _Float16 *rows;
+    double *host_cb;
+    bool dist;
+};
+
+// One (row j, component lane d) item of the finalize; L lanes per row (16 when D == 12: the
+// norm of a row is a 16-lane butterfly).  Returns the item's distortion term (no split).
+__device__ inline double finalize_item(const FinArgs &a, uint32_t j, uint32_t d, uint32_t L) {
+    const uint32_t K = a.K, D = a.D, Dp = a.Dp;
     const uint64_t KD = (uint64_t)K * D;
-    const uint32_t d = threadIdx.x % L, r = threadIdx.x / L;
-    const uint32_t j = blockIdx.x * (256 / L) + r;
-    double term = 0;
-    if (split) {
+    const uint64_t *sums = a.sums;
+    if (a.split) {
         if (j < 2 * K) {
             const uint32_t k = j < K ? j : j - K;
             double v = 0;
             if (d < D) {
                 const uint64_t c = (uint64_t)d * K + k;
-                const double cv = centroid_value(sums[c], sums[KD + c], sums[2 * KD + k], R, bias, scale);
-                if (j < K) C_cent[(uint64_t)k * D + d] = cv;
+                const double cv = centroid_value(sums[c], sums[KD + c], sums[2 * KD + k], a.R, a.bias, a.scale);
+                if (j < K) a.C_cent[(uint64_t)k * D + d] = cv;
                 v = cv * (j < K ? (double)(1 + 0.2) : (double)(1 - 0.2));
-                C64n[(uint64_t)j * D + d] = v;
-                if (host_cb) host_cb[(uint64_t)j * D + d] = v;
+                a.C64n[(uint64_t)j * D + d] = v;
+                if (a.host_cb) a.host_cb[(uint64_t)j * D + d] = v;
             }
-            if (d < Dp) C32[(uint64_t)j * Dp + d] = (float)v;
+            if (d < Dp) a.C32[(uint64_t)j * Dp + d] = (float)v;
             if (D == MF_D) {
-                _Float16 *row = rows + (uint64_t)j * MF_ROW_F16;
-                const double cp = d < D ? v - mu : 0.0;
+                _Float16 *row = a.rows + (uint64_t)j * MF_ROW_F16;
+                const double cp = d < D ? v - a.mu : 0.0;
                 double n = cp * cp;   // L == 16 here
 #pragma unroll
                 for (int off = 8; off >= 1; off >>= 1) n += __shfl_xor(n, off, 16);
                 if (d < D) {
-                    const double c2 = -2.0 * sx * cp * scale_t;
+                    const double c2 = -2.0 * a.sx * cp * a.scale_t;
                     const _Float16 h = (_Float16)(float)c2;
                     row[d] = h;
                     row[MF_D + d] = (_Float16)(float)(c2 - (double)(float)h);
                 } else if (d == MF_D) {
-                    n *= scale_t;
+                    n *= a.scale_t;
                     const _Float16 h = (_Float16)(float)n;
                     row[2 * MF_D] = h;
                     row[2 * MF_D + 1] = (_Float16)(float)(n - (double)(float)h);
@@ -312,26 +484,39 @@ __global__ __launch_bounds__(256) void finalize_prep_kernel(
                     row[2 * MF_D + 3] = (_Float16)0.f;
                 }
             }
-        } else if (j < Kpad_next) {
-            if (d < Dp) C32[(uint64_t)j * Dp + d] = 0.f;
+        } else if (j < a.Kpad_next) {
+            if (d < Dp) a.C32[(uint64_t)j * Dp + d] = 0.f;
             if (D == MF_D) {
-                _Float16 *row = rows + (uint64_t)j * MF_ROW_F16;
+                _Float16 *row = a.rows + (uint64_t)j * MF_ROW_F16;
                 for (uint32_t i = d; i < (uint32_t)MF_ROW_F16; i += L)
                     row[i] = (_Float16)(i == 2 * MF_D || i == 2 * MF_D + 1 ? MF_PAD_SCORE : 0.f);
             }
         }
-    } else if (j < K && d < D) {
+        return 0.0;
+    }
+    if (j < K && d < D) {
         const uint64_t c = (uint64_t)d * K + j;
         const uint64_t cnt = sums[2 * KD + j];
-        const double cv = centroid_value(sums[c], sums[KD + c], cnt, R, bias, scale);
-        C_cent[(uint64_t)j * D + d] = cv;
-        if (dist_out && cnt) {
+        const double cv = centroid_value(sums[c], sums[KD + c], cnt, a.R, a.bias, a.scale);
+        a.C_cent[(uint64_t)j * D + d] = cv;
+        if (a.dist && cnt) {
             const __int128 Sq =
-                (__int128)R * (__int128)sums[c] + (__int128)sums[KD + c] - (__int128)bias * (__int128)cnt;
-            const double S = ldexp(i128_to_double(Sq), -scale);
-            term = 2.0 * cv * S - (double)cnt * cv * cv;
+                (__int128)a.R * (__int128)sums[c] + (__int128)sums[KD + c] - (__int128)a.bias * (__int128)cnt;
+            const double S = ldexp(i128_to_double(Sq), -a.scale);
+            return 2.0 * cv * S - (double)cnt * cv * cv;
         }
     }
+    return 0.0;
+}
+
+__device__ inline uint32_t fin_rows(const FinArgs &a) { return a.split ? max(2 * a.K, a.Kpad_next) : a.K; }
+
+__global__ __launch_bounds__(256) void finalize_prep_kernel(FinArgs a, double *__restrict__ dist_part,
+                                                            unsigned *__restrict__ done, double *__restrict__ dist_out,
+                                                            volatile uint64_t *ready, uint64_t seq, uint32_t L) {
+    const uint32_t d = threadIdx.x % L, r = threadIdx.x / L;
+    const uint32_t j = blockIdx.x * (256 / L) + r;
+    const double term = finalize_item(a, j, d, L);
     if (!done) return;
     __shared__ double red[256];
     __shared__ bool last;
@@ -363,6 +548,31 @@ __global__ __launch_bounds__(256) void finalize_prep_kernel(
     }
 }
 
+static FinArgs fin_args(const uint64_t *sums, uint32_t K, uint32_t D, uint32_t Dp, int64_t R, int64_t bias,
+                        int scale, double *C_cent, bool split, double *C64n, uint32_t Kpad_next, double mu, double sx,
+                        int t, float *C32, _Float16 *cb_rows, double *host_cb, bool dist) {
+    FinArgs a;
+    a.sums = sums;
+    a.K = K;
+    a.D = D;
+    a.Dp = Dp;
+    a.R = R;
+    a.bias = bias;
+    a.scale = scale;
+    a.C_cent = C_cent;
+    a.split = split ? 1 : 0;
+    a.C64n = C64n;
+    a.Kpad_next = Kpad_next;
+    a.mu = mu;
+    a.sx = sx;
+    a.scale_t = std::ldexp(1.0, t);
+    a.C32 = C32;
+    a.rows = cb_rows;
+    a.host_cb = host_cb;
+    a.dist = dist;
+    return a;
+}
+
 hipError_t launch_finalize_prep(hipStream_t s, const uint64_t *sums, uint32_t K, uint32_t D, uint32_t Dp, int64_t R,
                                 int64_t bias, int scale, double *C_cent, bool split, double *C64n, uint32_t Kpad_next,
                                 double mu, double sx, int t, float *C32, _Float16 *cb_rows, double *host_cb,
@@ -372,9 +582,10 @@ hipError_t launch_finalize_prep(hipStream_t s, const uint64_t *sums, uint32_t K,
     const uint32_t n = split ? std::max(2 * K, Kpad_next) : K;
     const uint32_t grid = (n + 256 / L - 1) / (256 / L);
     if (done && grid > 8000) return hipErrorInvalidValue;   // dist_part capacity
-    hipLaunchKernelGGL(finalize_prep_kernel, dim3(grid), dim3(256), 0, s, sums, K, D, Dp, R, bias, scale, C_cent,
-                       split ? 1 : 0, C64n, Kpad_next, mu, sx, std::ldexp(1.0, t), C32, cb_rows, host_cb, dist_part,
-                       done, dist_out, (volatile uint64_t *)ready, seq, L);
+    const FinArgs a = fin_args(sums, K, D, Dp, R, bias, scale, C_cent, split, C64n, Kpad_next, mu, sx, t, C32, cb_rows,
+                               host_cb, dist_out != nullptr);
+    hipLaunchKernelGGL(finalize_prep_kernel, dim3(grid), dim3(256), 0, s, a, dist_part, done, dist_out,
+                       (volatile uint64_t *)ready, seq, L);
     return hipGetLastError();
 }
 
@@ -466,18 +677,23 @@ __global__ void scatter_kernel(uint32_t *__restrict__ A, const uint32_t *__restr
     for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) A[rows[i]] = vals[i];
 }
 
-// sums[idx[i]] += val[i] (host-aggregated terms of the tie rows, one entry per touched word).
-__global__ void add_terms_kernel(uint64_t *__restrict__ sums, const uint64_t *__restrict__ idx,
-                                 const uint64_t *__restrict__ val, uint32_t n) {
-    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x)
-        atomicAdd((unsigned long long *)&sums[idx[i]], (unsigned long long)val[i]);
+// Host-aggregated terms of tie rows into the extra slab: idx < KD -> slab[idx] (packed
+// hi << 32 | lo), else cnt[idx - KD].
+__global__ void add_terms_kernel(uint64_t *__restrict__ slab, uint32_t *__restrict__ cnt, uint64_t KD,
+                                 const uint64_t *__restrict__ idx, const uint64_t *__restrict__ val, uint32_t n) {
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+        if (idx[i] < KD) atomicAdd((unsigned long long *)&slab[idx[i]], (unsigned long long)val[i]);
+        else atomicAdd(&cnt[idx[i] - KD], (uint32_t)val[i]);
+    }
 }
 
 hipError_t launch_scatter(hipStream_t s, uint32_t *A, const uint32_t *rows, const uint32_t *vals, uint32_t n,
-                          uint64_t *sums, const uint64_t *idx, const uint64_t *val, uint32_t nterms) {
+                          uint64_t *slab, uint32_t *slab_cnt, uint64_t KD, const uint64_t *idx, const uint64_t *val,
+                          uint32_t nterms) {
     if (n) hipLaunchKernelGGL(scatter_kernel, dim3((n + 255) / 256), dim3(256), 0, s, A, rows, vals, n);
     if (nterms)
-        hipLaunchKernelGGL(add_terms_kernel, dim3((nterms + 255) / 256), dim3(256), 0, s, sums, idx, val, nterms);
+        hipLaunchKernelGGL(add_terms_kernel, dim3((nterms + 255) / 256), dim3(256), 0, s, slab, slab_cnt, KD, idx, val,
+                           nterms);
     return hipGetLastError();
 }
 

@@ -15,7 +15,7 @@ for path in glob.glob(d + "/p*/**/*counter_collection.csv", recursive=True):
         names[key] = r["Kernel_Name"]
 by_pass = defaultdict(list)
 for (p, disp), v in sorted(vals.items()):
-    if "assign" in names[(p, disp)]:
+    if sys.argv[3] if len(sys.argv) > 3 else "assign" in names[(p, disp)]:
         by_pass[p].append(v)
 cols = {}
 for p, lst in by_pass.items():
