@@ -16,9 +16,11 @@ import sys
 
 def short(name):
     m = re.search(r"qvq(?:::|\d+)([A-Za-z_]+?)(?:_kernel)?(?:I|E|\(|$)", name)
-    m3 = re.search(r"assign_small_kernelILi(\d+)ELb([01])E", name)
+    m3 = re.search(r"assign_small_kernel(?:ILi(\d+)ELb([01])E|<(\d+), (true|false)>)", name)
     if m3:
-        return "assign_small_kernel<%s,%s>" % (m3.group(1), "fused" if m3.group(2) == "1" else "plain")
+        sk = m3.group(1) or m3.group(3)
+        fused = m3.group(2) == "1" or m3.group(4) == "true"
+        return "assign_small_kernel<%s,%s>" % (sk, "fused" if fused else "plain")
     m2 = re.search(r"assign_mfma_kernelILb([01])ELb([01])E", name)
     if m2:
         return "assign_mfma_kernel<%s,%s>" % ("fused" if m2.group(1) == "1" else "plain",
