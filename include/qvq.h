@@ -60,6 +60,8 @@ typedef struct {
     uint64_t flagged[32];       /* rows re-checked in fp64 per level */
     uint64_t host_ties[32];     /* exact fp64 ties per level, answered by the reference kd-tree
                                    traversal (device kernel; host only for trees too deep) */
+    double wait_ms[32];         /* host wall waiting for the level's codebook (previous finalize) */
+    double tree_ms[32];         /* host wall building the level's kd-tree image (overlaps the search) */
 } qvq_timings;
 
 /* Context: one per GPU per host thread.  Owns device memory and one HIP stream. */

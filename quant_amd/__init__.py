@@ -31,7 +31,8 @@ class _Timings(ctypes.Structure):
     _fields_ = [("levels", ctypes.c_int), ("total_ms", ctypes.c_double),
                 ("assign_ms", ctypes.c_double * 32), ("update_ms", ctypes.c_double * 32),
                 ("other_ms", ctypes.c_double * 32), ("flagged", ctypes.c_uint64 * 32),
-                ("host_ties", ctypes.c_uint64 * 32)]
+                ("host_ties", ctypes.c_uint64 * 32), ("wait_ms", ctypes.c_double * 32),
+                ("tree_ms", ctypes.c_double * 32)]
 
 
 _lib = None
@@ -173,7 +174,8 @@ class Engine:
         return {"levels": L, "total_ms": t.total_ms,
                 "assign_ms": list(t.assign_ms[:max(L, 1)]), "update_ms": list(t.update_ms[:max(L, 1)]),
                 "other_ms": list(t.other_ms[:max(L, 1)]),
-                "flagged": list(t.flagged[:max(L, 1)]), "host_ties": list(t.host_ties[:max(L, 1)])}
+                "flagged": list(t.flagged[:max(L, 1)]), "host_ties": list(t.host_ties[:max(L, 1)]),
+                "wait_ms": list(t.wait_ms[:max(L, 1)]), "tree_ms": list(t.tree_ms[:max(L, 1)])}
 
     # -- multi-GPU -----------------------------------------------------------------------
     @staticmethod

@@ -76,6 +76,16 @@ constexpr int MF_ROW_F16 = 28;
 constexpr int MF_ROW_BYTES = 2 * MF_ROW_F16;
 constexpr float MF_PAD_SCORE = 65504.0f;   // nhi = nlo = f16 max for padding code vectors
 
+// Wide MFMA layout (every D != 12, Dp <= 64): per code vector KS k-steps of 32 f16 slots,
+// [hi(DH) | lo(DH) | nhi nlo | 0 ...] with DH = Dp rounded up to 8 (hi/lo of components
+// D..DH-1 are 0), same hi/lo/n meaning as above.
+__host__ __device__ constexpr uint32_t wide_dh(uint32_t Dp) { return (Dp + 7) & ~7u; }
+__host__ __device__ constexpr uint32_t wide_ks(uint32_t Dp) { return (2 * wide_dh(Dp) + 2 + 31) / 32; }
+__host__ __device__ constexpr uint32_t wide_row_f16(uint32_t Dp) { return 32 * wide_ks(Dp); }
+// f16 slots per code-vector row and the offset of the lo half, for either layout
+__host__ __device__ inline uint32_t cb_row_f16(uint32_t D, uint32_t Dp) { return D == MF_D ? MF_ROW_F16 : wide_row_f16(Dp); }
+__host__ __device__ inline uint32_t cb_lo_off(uint32_t D, uint32_t Dp) { return D == MF_D ? MF_D : wide_dh(Dp); }
+
 // ---------------------------------------------------------------------------------------
 // Launch wrappers (each defined next to its kernel).  All take the stream last-but-args.
 // ---------------------------------------------------------------------------------------
@@ -101,6 +111,12 @@ hipError_t launch_assign_mfma(hipStream_t s, int grid, bool fuse, const uint8_t 
                               const _Float16 *cb_rows, uint32_t K, const float *C32, const uint64_t *plut,
                               const MfThresholds &th, uint32_t *A, uint32_t *flags, unsigned *flag_cnt,
                               uint64_t *part, uint32_t *part_cnt);
+// MFMA f16 search for D != 12 (wide layout), no fused sums: K >= 32, codebook staged in LDS
+// whole or in double-buffered slices.  Same flag rule as launch_assign_mfma.
+bool wide_can_search(uint32_t Dp);
+hipError_t launch_assign_wide(hipStream_t s, int num_cu, uint32_t Dp, uint32_t D, const uint8_t *codes, uint64_t N,
+                              const _Float16 *cb_rows, uint32_t K, const float *C32, const MfThresholds &th,
+                              uint32_t *A, uint32_t *flags, unsigned *flag_cnt);
 // Recheck of flagged rows: fp32 distances to all K code vectors (C32 [Kpad][Dp]), fp64 in
 // the reference's order for those inside the fp32 error band (alpha, beta, gamma as the VALU
 // search's); exact ties are listed in ties (tie_cnt) for launch_kd_resolve or the host.

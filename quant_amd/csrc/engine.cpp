@@ -109,6 +109,8 @@ struct qvq_ctx {
     uint64_t *h_ready = nullptr, *dh_ready = nullptr;
     uint64_t seq = 0;
     uint8_t *h_tree[2] = {nullptr, nullptr}, *dh_tree[2] = {nullptr, nullptr};
+    uint8_t *d_tree = nullptr;   // device copy of the level's tree image (one DMA per level)
+    std::vector<double> cb_local;   // host copy of the published codebook for the tree build
     uint64_t tree_cap = 0;
     uint32_t nslabs = 0;   // slabs holding the last run_level's sums
     int timing_level = -1;   // qvq_set_timing: -1 all levels, -2 none, else that level only
@@ -163,6 +165,14 @@ bool env_is(const char *name, const char *val) {
 bool use_mfma(const qvq_ctx *ctx, uint32_t K) {
     return ctx->D == MF_D && mf_can_search(K) && !env_is("QVQ_SEARCH", "valu");
 }
+// MFMA search for D != 12 from K = QVQ_WIDE_MIN_K (default 32) code vectors up.
+bool use_wide(const qvq_ctx *ctx, uint32_t K) {
+    static const uint32_t min_k = [] {
+        const char *e = std::getenv("QVQ_WIDE_MIN_K");
+        return e ? (uint32_t)std::max(1, std::atoi(e)) : 32u;
+    }();
+    return ctx->D != MF_D && wide_can_search(ctx->Dp) && K >= min_k && !env_is("QVQ_SEARCH", "valu");
+}
 bool use_fused(const qvq_ctx *ctx, uint32_t K) {
     return use_mfma(ctx, K) && K <= mf_fuse_max_k() && !env_is("QVQ_FUSE", "0");
 }
@@ -190,6 +200,7 @@ void free_levels(qvq_ctx *ctx) {
         if (ctx->h_tree[b]) (void)hipHostFree(ctx->h_tree[b]);
         ctx->h_tree[b] = ctx->dh_tree[b] = nullptr;
     }
+    dfree(ctx->d_tree);
     ctx->tree_cap = 0;
     ctx->Kcap = 0;
 }
@@ -220,10 +231,12 @@ void mfma_setup(qvq_ctx *ctx) {
     while (std::ldexp(n_max, tt) > 60000.0 || std::ldexp(s_bound, tt) > 120000.0) tt--;
     ctx->mf_t = tt;
     const double u = std::ldexp(1.0, -24);
-    // one MFMA score: <= 33 sequential fp32 roundings over the terms, the f16 hi/lo split
+    // one MFMA score: <= (slots + 1) sequential fp32 roundings over the terms (D = 12: 32
+    // slots in one MFMA; wide layout: KS chained MFMAs of 32 slots), the f16 hi/lo split
     // (2^-22 relative + 2^-25 absolute per operand, scaled back), the fp32 scale/shift of
     // the score and of ||x - mu||^2, x ~ mu + w*sx (2^-53)
-    const double e_acc = 33.0 * u * s_bound;
+    const double rounds = ctx->D == MF_D ? 33.0 : 32.0 * wide_ks(ctx->Dp) + 1.0;
+    const double e_acc = rounds * u * s_bound;
     const double e_rep = D * wmax * (c2_max * std::ldexp(1.0, -22) + std::ldexp(1.0, -25 - tt)) +
                          n_max * std::ldexp(1.0, -22) + std::ldexp(1.0, -25 - tt);
     const double e_conv = 4 * u * (s_bound + D * cp * cp) + 1e-12 * s_bound;
@@ -273,7 +286,7 @@ qvq_status ensure_levels(qvq_ctx *ctx, uint32_t Kmax) {
     HIPCHK(hipMalloc(&ctx->d_C64_cent, KD * 8));
     HIPCHK(hipMalloc(&ctx->d_C64_split, KD * 8));
     HIPCHK(hipMalloc(&ctx->d_C32, Kp * ctx->Dp * 4));
-    HIPCHK(hipMalloc(&ctx->d_rows, Kp * MF_ROW_BYTES));
+    HIPCHK(hipMalloc(&ctx->d_rows, Kp * 2 * cb_row_f16(ctx->D, ctx->Dp)));
     // G per-CU slabs + one extra (rows the recheck / kd-tree resolve in the fused path)
     HIPCHK(hipMalloc(&ctx->d_part, (uint64_t)(ctx->G + 1) * KD * 8));
     HIPCHK(hipMalloc(&ctx->d_part_cnt, (uint64_t)(ctx->G + 1) * Kmax * 4));
@@ -286,6 +299,7 @@ qvq_status ensure_levels(qvq_ctx *ctx, uint32_t Kmax) {
         HIPCHK(hipHostMalloc(&ctx->h_tree[b], ctx->tree_cap, mflags));
         HIPCHK(hipHostGetDevicePointer((void **)&ctx->dh_tree[b], ctx->h_tree[b], 0));
     }
+    HIPCHK(hipMalloc(&ctx->d_tree, ctx->tree_cap));
     ctx->Kcap = Kmax;
     return QVQ_OK;
 }
@@ -329,12 +343,15 @@ qvq_status run_update(qvq_ctx *ctx, const uint32_t *d_A, uint32_t K) {
 }
 
 // Build the reference kd-tree over the host copy hC of the K code vectors being searched
-// into tree image buffer buf (mapped pinned memory, read by kd_resolve_kernel).  An empty
+// into tree image buffer buf (pinned host memory, DMA-copied to d_tree for kd_resolve_kernel).  An empty
 // view means host resolution (tree too deep/large for the kernel's LDS, or QVQ_KDTREE=host).
 void build_tree(qvq_ctx *ctx, const double *hC, uint32_t K, int buf, KdView &kd) {
     kd = KdView{};
     if (env_is("QVQ_KDTREE", "host")) return;
-    RefKDTree tree(hC, K, (int)ctx->D);
+    // the build reads the codebook many times; mapped memory the GPU just wrote is read
+    // once, sequentially, into ordinary memory first
+    ctx->cb_local.assign(hC, hC + (size_t)K * ctx->D);
+    RefKDTree tree(ctx->cb_local.data(), K, (int)ctx->D);
     const uint32_t D = ctx->D;
     const size_t nn = tree.num_nodes();
     KdView v;
@@ -348,7 +365,10 @@ void build_tree(qvq_ctx *ctx, const double *hC, uint32_t K, int buf, KdView &kd)
     KdNodeDev *nodes = reinterpret_cast<KdNodeDev *>(hi + D);
     uint32_t *vind = reinterpret_cast<uint32_t *>(nodes + nn);
     tree.flatten(nodes, vind, lo, hi);
-    const double *dlo = reinterpret_cast<const double *>(ctx->dh_tree[buf]);
+    // one DMA into device memory: every kd_resolve workgroup stages the image, and reads
+    // of mapped host memory from 16 workgroups cost ~70 us per level
+    if (hipMemcpyAsync(ctx->d_tree, ctx->h_tree[buf], bytes, hipMemcpyHostToDevice, ctx->stream) != hipSuccess) return;
+    const double *dlo = reinterpret_cast<const double *>(ctx->d_tree);
     v.lo = dlo;
     v.hi = dlo + D;
     v.nodes = reinterpret_cast<const KdNodeDev *>(dlo + 2 * D);
@@ -445,6 +465,9 @@ qvq_status run_level(qvq_ctx *ctx, uint32_t K, int slot, bool sums_out, const do
         HIPCHK(launch_assign_mfma(ctx->stream, ctx->num_cu, fused, ctx->d_codes, ctx->N, ctx->d_rows, K,
                                   ctx->d_C32, ctx->d_plut, ctx->mf_th, ctx->d_A, ctx->d_flags, &cnt[0],
                                   ctx->d_part, ctx->d_part_cnt));
+    } else if (use_wide(ctx, K)) {
+        HIPCHK(launch_assign_wide(ctx->stream, ctx->num_cu, ctx->Dp, ctx->D, ctx->d_codes, ctx->N, ctx->d_rows, K,
+                                  ctx->d_C32, ctx->mf_th, ctx->d_A, ctx->d_flags, &cnt[0]));
     } else {
         float alpha, beta, gamma;
         valu_coeffs(ctx, alpha, beta, gamma);
@@ -461,9 +484,13 @@ qvq_status run_level(qvq_ctx *ctx, uint32_t K, int slot, bool sums_out, const do
     }
     // the tree build overlaps the search just enqueued
     qvq_status st;
+    const auto tw0 = std::chrono::steady_clock::now();
     if (wait_seq && (st = wait_codebook(ctx, wait_seq)) != QVQ_OK) return st;
+    const auto tw1 = std::chrono::steady_clock::now();
     KdView kd;
     build_tree(ctx, hC, K, slot & 1, kd);
+    ctx->tm.wait_ms[slot] = std::chrono::duration<double, std::milli>(tw1 - tw0).count();
+    ctx->tm.tree_ms[slot] = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tw1).count();
     if (kd.depth > 0) {
         HIPCHK(launch_kd_resolve(ctx->stream, ctx->d_codes, ctx->Dp, ctx->D, ctx->d_ties, &cnt[1], ctx->d_C64_split,
                                  K, ctx->d_lut64, kd, ctx->d_A, xslab, xcnt, ctx->d_plut));

@@ -15,11 +15,10 @@
 #include <cstdlib>
 
 #include "common.hpp"
+#include "mfma_util.hpp"
 
 namespace qvq {
 
-typedef _Float16 half8 __attribute__((ext_vector_type(8)));
-typedef float f32x4 __attribute__((ext_vector_type(4)));
 
 // =======================================================================================
 // MFMA search
@@ -57,24 +56,6 @@ uint32_t mf_fuse_max_k() {
 }
 bool mf_can_search(uint32_t K) { return mf_lds_layout(K, false, false).total <= MF_LDS_MAX; }
 
-// min/min3 without the NaN-canonicalising v_max hipcc inserts around fminf (no NaNs here).
-__device__ inline float min3f(float a, float b, float c) {
-    float r;
-    asm("v_min3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
-    return r;
-}
-__device__ inline float min2f(float a, float b) {
-    float r;
-    asm("v_min_f32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
-    return r;
-}
-__device__ inline float med3f(float a, float b, float c) { return __builtin_amdgcn_fmed3f(a, b, c); }
-
-// Centred integer of a byte: w = 2*((int8)b + 128) - 255 = 2*(b ^ 0x80) - 255 (both colour
-// spaces), so v(b) = mu + w*sx.  Exact in f16.
-__device__ inline float byte_w(uint32_t word, int j) {
-    return __fmaf_rn(2.f, (float)(((word ^ 0x80808080u) >> (8 * j)) & 0xFF), -255.f);
-}
 
 typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
 
@@ -121,15 +102,6 @@ __device__ inline bool wave_runs_reduce(uint32_t key, uint32_t (&v)[MF_D + 1], i
     return lane == 63 || next != key;
 }
 
-// Epilogue of one tile pair for one data tile: minimum of the lane's 8 scores, then the
-// running best pair, best score and second-best pair minimum.
-__device__ inline void pair_update(const f32x4 &p0, const f32x4 &p1, uint32_t pair, float &b1, float &b2,
-                                   uint32_t &bp) {
-    const float m = min2f(min3f(min3f(p0[0], p0[1], p0[2]), p0[3], p1[0]), min3f(p1[1], p1[2], p1[3]));
-    b2 = med3f(b1, b2, m);
-    bp = m < b1 ? pair : bp;
-    b1 = min2f(b1, m);
-}
 
 constexpr int MF_SMALL_K = 32;
 

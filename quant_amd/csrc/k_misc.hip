@@ -127,17 +127,17 @@ __global__ __launch_bounds__(UPDATE_THREADS) void update_kernel(
 
 #define QVQ_FOR_EACH_DP(X) X(4) X(8) X(12) X(16) X(20) X(24) X(28) X(32) X(36) X(40) X(44) X(48) X(52) X(56) X(60) X(64)
 
-// Centroid sums of a final assignment, HBM-bound.  A wave takes 256 consecutive rows per
-// round, lane L rows 4L..4L+3 (coalesced: 4*DP code bytes and 16 index bytes per lane).  A
-// lane adds the exact terms of its rows with equal index in registers (u << 16 | lo per
-// component, no carry below 256 rows) and flushes a run to the LDS sums [d][k] when the index
-// changes and at the end of the round -- except when all 256 rows of the round share one
-// index (common at small K), then the wave folds its registers with DPP and one lane adds.
-// At small K many lanes flush to the same few addresses at once, which the LDS serialises:
-// the sums are replicated C times (lane L adds into copy L mod C) and the copies are summed
-// when the workgroup writes its slab [g][d][k] for reduce_kernel.
-constexpr int URUN_THREADS = 1024;
+// Centroid sums of a final assignment, HBM-bound.  A wave takes 64*R consecutive rows per
+// round, lane L rows R*L..R*L+R-1 (coalesced), R = 4, 2 or 1 rows by width so that the codes
+// stay in registers.  A lane adds the exact terms of its rows in registers (u << 16 | lo per
+// component) while the index repeats, across rounds, and flushes the run to the LDS sums
+// [d][k] when the index changes or after 256 rows (the 16-bit fields never carry).  At small
+// K many lanes flush to the same few addresses, which the LDS serialises: the sums are
+// replicated C times (lane L adds into copy L mod C) and the copies are summed when the
+// workgroup writes its slab [g][d][k] for reduce_kernel.
 constexpr size_t URUN_LDS = 160 * 1024;
+// wide rows keep 4 + DP/4 + DP registers per lane live: fewer waves, up to 256 VGPRs
+__host__ __device__ constexpr int urun_threads(int DP) { return DP > 32 ? 512 : 1024; }
 
 static size_t urun_bytes(uint32_t K, uint32_t D, uint32_t C) {
     return (size_t)C * K * D * 8 + (size_t)C * ((K + 1) & ~1u) * 4 + 256;
@@ -149,39 +149,27 @@ static uint32_t urun_copies(uint32_t K, uint32_t D) {
 }
 bool update_runs_fits(uint32_t K, uint32_t D) { return urun_bytes(K, D, 1) <= URUN_LDS; }
 
-template <int CTRL, int ROW_MASK>
-__device__ inline uint32_t urun_dpp(uint32_t v) {
-    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, ROW_MASK, 0xF, true);
-}
-__device__ inline uint32_t urun_wave_sum(uint32_t v) {   // total in lane 63
-    v += urun_dpp<0x111, 0xF>(v);
-    v += urun_dpp<0x112, 0xF>(v);
-    v += urun_dpp<0x114, 0xF>(v);
-    v += urun_dpp<0x118, 0xF>(v);
-    v += urun_dpp<0x142, 0xA>(v);
-    v += urun_dpp<0x143, 0xC>(v);
-    return v;
-}
-
 template <int DP>
-__global__ __launch_bounds__(URUN_THREADS) void update_runs_kernel(const uint8_t *__restrict__ codes, uint64_t N,
+__global__ __launch_bounds__(urun_threads(DP)) void update_runs_kernel(const uint8_t *__restrict__ codes, uint64_t N,
                                                                    const uint32_t *__restrict__ A, uint32_t K,
                                                                    uint32_t D, uint32_t C, const uint64_t *__restrict__ plut,
                                                                    uint64_t *__restrict__ part,
                                                                    uint32_t *__restrict__ part_cnt) {
+    constexpr int T = urun_threads(DP);
+    constexpr int R = DP <= 16 ? 4 : (DP <= 32 ? 2 : 1);   // rows per lane and round
+    constexpr int W4 = DP / 4;                               // code words per row
     extern __shared__ __attribute__((aligned(16))) uint64_t usm[];
     const uint32_t K2 = (K + 1) & ~1u;
     uint64_t *sums_all = usm;                                                         // [C][D][K]
     uint32_t *cnt_all = reinterpret_cast<uint32_t *>(usm + (size_t)C * K * D);       // [C][K2]
     uint8_t *lo8 = reinterpret_cast<uint8_t *>(cnt_all + (size_t)C * K2);            // [256]
     const int tid = threadIdx.x, lane = tid & 63;
-    for (uint32_t i = tid; i < C * K * D; i += URUN_THREADS) sums_all[i] = 0;
-    for (uint32_t i = tid; i < C * K2; i += URUN_THREADS) cnt_all[i] = 0;
+    for (uint32_t i = tid; i < C * K * D; i += T) sums_all[i] = 0;
+    for (uint32_t i = tid; i < C * K2; i += T) cnt_all[i] = 0;
     uint64_t *sums = sums_all + (size_t)(lane % C) * K * D;   // this lane's copy
     uint32_t *cnt = cnt_all + (size_t)(lane % C) * K2;
     if (tid < 256) lo8[tid] = (uint8_t)(plut[tid] & 0xFF);
     __syncthreads();
-    constexpr int W4 = DP / 4;   // code words per row
     uint32_t acc[DP + 1];
     uint32_t cur = 0xFFFFFFFFu;
 #pragma unroll
@@ -199,7 +187,7 @@ __global__ __launch_bounds__(URUN_THREADS) void update_runs_kernel(const uint8_t
         for (int i = 0; i <= DP; i++) acc[i] = 0;
     };
     auto add_row = [&](const uint32_t *w, uint32_t k) {
-        if (k != cur) {
+        if (k != cur || acc[DP] == 256) {
             flush();
             cur = k;
         }
@@ -210,63 +198,39 @@ __global__ __launch_bounds__(URUN_THREADS) void update_runs_kernel(const uint8_t
         }
         acc[DP] += 1;
     };
-    const uint64_t wave_g = ((uint64_t)blockIdx.x * URUN_THREADS + tid) >> 6;
-    const uint64_t n_waves = ((uint64_t)gridDim.x * URUN_THREADS) >> 6;
-    for (uint64_t r0 = wave_g * 256; r0 < N; r0 += n_waves * 256) {
-        const uint64_t row = r0 + 4 * (uint64_t)lane;
-        bool uniform = false;
-        if (r0 + 256 <= N) {
-            uint32_t w[4 * W4];
-            const uint4 *p = reinterpret_cast<const uint4 *>(codes + row * DP);
+    const uint64_t wave_g = ((uint64_t)blockIdx.x * T + tid) >> 6;
+    const uint64_t n_waves = ((uint64_t)gridDim.x * T) >> 6;
+    for (uint64_t r0 = wave_g * 64 * R; r0 < N; r0 += n_waves * 64 * R) {
+        const uint64_t row = r0 + (uint64_t)R * lane;
+        if (r0 + 64 * R <= N) {
+            uint32_t w[R * W4];
+            const uint32_t *p = reinterpret_cast<const uint32_t *>(codes + row * DP);
 #pragma unroll
-            for (int i = 0; i < W4; i++) {
-                const uint4 v = p[i];
-                w[4 * i] = v.x;
-                w[4 * i + 1] = v.y;
-                w[4 * i + 2] = v.z;
-                w[4 * i + 3] = v.w;
-            }
-            const uint4 a = *reinterpret_cast<const uint4 *>(A + row);
-            add_row(w, a.x);
-            add_row(w + W4, a.y);
-            add_row(w + 2 * W4, a.z);
-            add_row(w + 3 * W4, a.w);
-            // one index for the whole round (and no earlier run left in a lane)?
-            const uint32_t k0 = __shfl(a.x, 0);
-            uniform = __all(a.x == k0 && a.w == k0 && acc[DP] == 4);
+            for (int i = 0; i < R * W4; i++) w[i] = p[i];
+            uint32_t a[R];
+#pragma unroll
+            for (int r = 0; r < R; r++) a[r] = A[row + r];
+#pragma unroll
+            for (int r = 0; r < R; r++) add_row(w + r * W4, a[r]);
         } else {
-            for (uint64_t r = row; r < row + 4 && r < N; r++) {
+            for (uint64_t r = row; r < row + R && r < N; r++) {
                 uint32_t w[W4];
 #pragma unroll
                 for (int i = 0; i < W4; i++) w[i] = reinterpret_cast<const uint32_t *>(codes + r * DP)[i];
                 add_row(w, A[r]);
             }
         }
-        if (uniform) {
-#pragma unroll
-            for (int d = 0; d < DP; d++) {
-                const uint32_t t = urun_wave_sum(acc[d]);   // 256 rows: still no carry
-                if (lane == 63 && (uint32_t)d < D)
-                    atomicAdd((unsigned long long *)&sums[(uint32_t)d * K + cur],
-                              (unsigned long long)((((uint64_t)(t >> 16)) << 32) | (t & 0xFFFF)));
-            }
-            if (lane == 63) atomicAdd(&cnt[cur], 256u);
-#pragma unroll
-            for (int i = 0; i <= DP; i++) acc[i] = 0;
-        } else {
-            flush();
-        }
-        cur = 0xFFFFFFFFu;
     }
+    flush();
     __syncthreads();
     uint64_t *pdst = part + (uint64_t)blockIdx.x * K * D;
-    for (uint32_t i = tid; i < K * D; i += URUN_THREADS) {
+    for (uint32_t i = tid; i < K * D; i += T) {
         uint64_t t = 0;
         for (uint32_t c = 0; c < C; c++) t += sums_all[(size_t)c * K * D + i];
         pdst[i] = t;
     }
     uint32_t *cdst = part_cnt + (uint64_t)blockIdx.x * K;
-    for (uint32_t i = tid; i < K; i += URUN_THREADS) {
+    for (uint32_t i = tid; i < K; i += T) {
         uint32_t t = 0;
         for (uint32_t c = 0; c < C; c++) t += cnt_all[(size_t)c * K2 + i];
         cdst[i] = t;
@@ -281,7 +245,7 @@ hipError_t launch_update(hipStream_t s, uint32_t Dp, uint32_t G, const uint8_t *
         switch (Dp) {
 #define X(DPV)                                                                                                     \
     case DPV:                                                                                                      \
-        hipLaunchKernelGGL(update_runs_kernel<DPV>, dim3(G), dim3(URUN_THREADS), lds, s, codes, N, A, K, D, C,    \
+        hipLaunchKernelGGL(update_runs_kernel<DPV>, dim3(G), dim3(urun_threads(DPV)), lds, s, codes, N, A, K, D, C,    \
                            plut, part, part_cnt);                                                                  \
         return hipGetLastError();
             QVQ_FOR_EACH_DP(X)
@@ -464,32 +428,34 @@ __device__ inline double finalize_item(const FinArgs &a, uint32_t j, uint32_t d,
                 if (a.host_cb) a.host_cb[(uint64_t)j * D + d] = v;
             }
             if (d < Dp) a.C32[(uint64_t)j * Dp + d] = (float)v;
-            if (D == MF_D) {
-                _Float16 *row = a.rows + (uint64_t)j * MF_ROW_F16;
+            if (a.rows) {   // MFMA row (common.hpp): hi at d, lo at LO + d, norm at 2 LO
+                const uint32_t RF = cb_row_f16(D, Dp), LO = cb_lo_off(D, Dp);
+                _Float16 *row = a.rows + (uint64_t)j * RF;
                 const double cp = d < D ? v - a.mu : 0.0;
-                double n = cp * cp;   // L == 16 here
-#pragma unroll
-                for (int off = 8; off >= 1; off >>= 1) n += __shfl_xor(n, off, 16);
+                double n = cp * cp;   // L >= LO lanes per row
+                for (uint32_t off = L / 2; off >= 1; off >>= 1) n += __shfl_xor(n, (int)off, (int)L);
                 if (d < D) {
                     const double c2 = -2.0 * a.sx * cp * a.scale_t;
                     const _Float16 h = (_Float16)(float)c2;
                     row[d] = h;
-                    row[MF_D + d] = (_Float16)(float)(c2 - (double)(float)h);
-                } else if (d == MF_D) {
-                    n *= a.scale_t;
-                    const _Float16 h = (_Float16)(float)n;
-                    row[2 * MF_D] = h;
-                    row[2 * MF_D + 1] = (_Float16)(float)(n - (double)(float)h);
-                    row[2 * MF_D + 2] = (_Float16)0.f;
-                    row[2 * MF_D + 3] = (_Float16)0.f;
+                    row[LO + d] = (_Float16)(float)(c2 - (double)(float)h);
+                } else if (d < LO) {
+                    row[d] = (_Float16)0.f;
+                    row[LO + d] = (_Float16)0.f;
                 }
+                n *= a.scale_t;
+                const _Float16 h = (_Float16)(float)n;
+                const _Float16 l = (_Float16)(float)(n - (double)(float)h);
+                for (uint32_t i = 2 * LO + d; i < RF; i += L)
+                    row[i] = i == 2 * LO ? h : (i == 2 * LO + 1 ? l : (_Float16)0.f);
             }
         } else if (j < a.Kpad_next) {
             if (d < Dp) a.C32[(uint64_t)j * Dp + d] = 0.f;
-            if (D == MF_D) {
-                _Float16 *row = a.rows + (uint64_t)j * MF_ROW_F16;
-                for (uint32_t i = d; i < (uint32_t)MF_ROW_F16; i += L)
-                    row[i] = (_Float16)(i == 2 * MF_D || i == 2 * MF_D + 1 ? MF_PAD_SCORE : 0.f);
+            if (a.rows) {
+                const uint32_t RF = cb_row_f16(D, Dp), LO = cb_lo_off(D, Dp);
+                _Float16 *row = a.rows + (uint64_t)j * RF;
+                for (uint32_t i = d; i < RF; i += L)
+                    row[i] = (_Float16)(i == 2 * LO || i == 2 * LO + 1 ? MF_PAD_SCORE : 0.f);
             }
         }
         return 0.0;
@@ -511,17 +477,20 @@ __device__ inline double finalize_item(const FinArgs &a, uint32_t j, uint32_t d,
 
 __device__ inline uint32_t fin_rows(const FinArgs &a) { return a.split ? max(2 * a.K, a.Kpad_next) : a.K; }
 
+// Grid-stride over groups of 256/L rows.  Each wave fences its mapped-host writes once, after
+// its last row (a system fence writes back the L2: per row it cost ~25 ns x rows).
 __global__ __launch_bounds__(256) void finalize_prep_kernel(FinArgs a, double *__restrict__ dist_part,
                                                             unsigned *__restrict__ done, double *__restrict__ dist_out,
                                                             volatile uint64_t *ready, uint64_t seq, uint32_t L) {
     const uint32_t d = threadIdx.x % L, r = threadIdx.x / L;
-    const uint32_t j = blockIdx.x * (256 / L) + r;
-    const double term = finalize_item(a, j, d, L);
+    const uint32_t per = 256 / L, n = fin_rows(a);
+    double term = 0.0;
+    for (uint32_t j0 = blockIdx.x * per; j0 < n; j0 += gridDim.x * per) term += finalize_item(a, j0 + r, d, L);
     if (!done) return;
     __shared__ double red[256];
     __shared__ bool last;
     red[threadIdx.x] = term;
-    __threadfence_system();
+    if (a.host_cb) __threadfence_system();
     __syncthreads();
     for (int w = 128; w > 0; w >>= 1) {
         if ((int)threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
@@ -580,8 +549,7 @@ hipError_t launch_finalize_prep(hipStream_t s, const uint64_t *sums, uint32_t K,
     if (D == 0 || D > 64) return hipErrorInvalidValue;
     const uint32_t L = D <= 16 ? 16 : (D <= 32 ? 32 : 64);
     const uint32_t n = split ? std::max(2 * K, Kpad_next) : K;
-    const uint32_t grid = (n + 256 / L - 1) / (256 / L);
-    if (done && grid > 8000) return hipErrorInvalidValue;   // dist_part capacity
+    const uint32_t grid = std::min<uint32_t>((n + 256 / L - 1) / (256 / L), 512);   // <= dist_part capacity
     const FinArgs a = fin_args(sums, K, D, Dp, R, bias, scale, C_cent, split, C64n, Kpad_next, mu, sx, t, C32, cb_rows,
                                host_cb, dist_out != nullptr);
     hipLaunchKernelGGL(finalize_prep_kernel, dim3(grid), dim3(256), 0, s, a, dist_part, done, dist_out,
@@ -597,53 +565,51 @@ hipError_t launch_finalize(hipStream_t s, const uint64_t *sums, uint32_t K, uint
 }
 
 // Search tables from an fp64 codebook: fp32 [Kpad][Dp] (VALU path and the MFMA recompute)
-// and, for D = 12, the f16 MFMA rows (common.hpp).  Code vectors K..Kpad-1 are padding
+// and the f16 MFMA rows (D = 12 or wide layout, common.hpp).  Code vectors K..Kpad-1 are padding
 // that never wins.
 __device__ inline void prep_row(const double *v, uint32_t D, uint32_t Dp, double mu, double sx, double scale_t,
                                 float *__restrict__ c32, _Float16 *__restrict__ r) {
+    const uint32_t RF = cb_row_f16(D, Dp), LO = cb_lo_off(D, Dp);
     double n = 0;
+    for (uint32_t i = 0; i < RF; i++) r[i] = (_Float16)0.f;
     for (uint32_t d = 0; d < Dp; d++) {
         const double x = d < D ? v[d] : 0.0;
         c32[d] = (float)x;
-        if (D == MF_D && d < D) {
+        if (d < D) {
             const double cp = x - mu;
             n += cp * cp;
             const double c2 = -2.0 * sx * cp * scale_t;
             const _Float16 h = (_Float16)(float)c2;
             r[d] = h;
-            r[MF_D + d] = (_Float16)(float)(c2 - (double)(float)h);
+            r[LO + d] = (_Float16)(float)(c2 - (double)(float)h);
         }
     }
-    if (D == MF_D) {
-        n *= scale_t;
-        const _Float16 h = (_Float16)(float)n;
-        r[2 * MF_D] = h;
-        r[2 * MF_D + 1] = (_Float16)(float)(n - (double)(float)h);
-        r[2 * MF_D + 2] = (_Float16)0.f;
-        r[2 * MF_D + 3] = (_Float16)0.f;
-    }
+    n *= scale_t;
+    const _Float16 h = (_Float16)(float)n;
+    r[2 * LO] = h;
+    r[2 * LO + 1] = (_Float16)(float)(n - (double)(float)h);
 }
 
 __device__ inline void prep_pad_row(uint32_t D, uint32_t Dp, float *__restrict__ c32, _Float16 *__restrict__ r) {
+    const uint32_t RF = cb_row_f16(D, Dp), LO = cb_lo_off(D, Dp);
     for (uint32_t d = 0; d < Dp; d++) c32[d] = 0.f;
-    if (D == MF_D) {
-        for (int j = 0; j < MF_ROW_F16; j++) r[j] = (_Float16)0.f;
-        r[2 * MF_D] = (_Float16)MF_PAD_SCORE;
-        r[2 * MF_D + 1] = (_Float16)MF_PAD_SCORE;
-    }
+    for (uint32_t i = 0; i < RF; i++) r[i] = (_Float16)0.f;
+    r[2 * LO] = (_Float16)MF_PAD_SCORE;
+    r[2 * LO + 1] = (_Float16)MF_PAD_SCORE;
 }
 
 __global__ void prep_kernel(const double *__restrict__ C64, uint32_t K, uint32_t Kpad, uint32_t D, uint32_t Dp,
                             double mu, double sx, double scale_t, float *__restrict__ C32,
                             _Float16 *__restrict__ rows) {
+    const uint32_t RF = cb_row_f16(D, Dp);
     for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < Kpad; k += gridDim.x * blockDim.x) {
         if (k >= K) {
-            prep_pad_row(D, Dp, C32 + (uint64_t)k * Dp, rows + (uint64_t)k * MF_ROW_F16);
+            prep_pad_row(D, Dp, C32 + (uint64_t)k * Dp, rows + (uint64_t)k * RF);
             continue;
         }
         double v[64];
         for (uint32_t d = 0; d < D; d++) v[d] = C64[(uint64_t)k * D + d];
-        prep_row(v, D, Dp, mu, sx, scale_t, C32 + (uint64_t)k * Dp, rows + (uint64_t)k * MF_ROW_F16);
+        prep_row(v, D, Dp, mu, sx, scale_t, C32 + (uint64_t)k * Dp, rows + (uint64_t)k * RF);
     }
 }
 

@@ -1,0 +1,329 @@
+// k_wide.hip -- MFMA nearest-code-vector search for every block dimension other than 12
+// (src/Quantizer.cpp:24-32 semantics; C4's 4x4 blocks are D = 48).
+//
+// Scoring as in assign_mfma_kernel (k_assign.hip): per code vector c one f16 row in the wide
+// layout (common.hpp) [c''_hi(DH) | c''_lo(DH) | n_hi n_lo | 0 ...] against the data column
+// [w(DH) | w(DH) | 1 1 | 0 ...], KS chained v_mfma_f32_16x16x32_f16 per 16 x 16 tile, so
+// score = 2^t (||x-c||^2 - ||x-mu||^2).  A wave keeps 64 rows (4 data tiles) as B fragments
+// for its whole pass over the codebook, so every A fragment read from LDS feeds 4 MFMAs.
+// The codebook sits in LDS whole when it fits; otherwise it streams in 128-code-vector slices
+// through two LDS buffers: the next slice's global loads are issued before the current
+// slice's MFMAs and written to the other buffer after them, one barrier per slice.
+// Epilogue, recompute in direct fp32 and the flag rule follow the D = 12 kernel, except that
+// with KS >= 2 (MFMA-bound, VALU to spare) the epilogue keeps the best two 8-code-vector
+// units and the third-best score: both units are recomputed, and the MFMA error bound only
+// applies against the third unit, so far fewer rows are flagged.
+#include <cstdlib>
+
+#include "common.hpp"
+#include "mfma_util.hpp"
+
+namespace qvq {
+
+constexpr int WD_THREADS = 512;   // 8 waves, 2 per SIMD: up to 256 VGPRs each
+constexpr int WD_WAVES = WD_THREADS / 64;
+constexpr int WD_TILES = 4;       // 16-row data tiles per wave
+constexpr int WD_ROWS = 16 * WD_TILES;
+constexpr uint32_t WD_SLICE = 128;   // code vectors per streamed slice
+constexpr uint32_t WD_LDS_MAX = 160 * 1024;
+
+template <int DP>
+struct WideCfg {
+    static constexpr int DH = (int)wide_dh(DP);
+    static constexpr int KS = (int)wide_ks(DP);
+    static constexpr int GROW = 64 * KS;     // global row bytes
+    static constexpr int LSTR = GROW + 16;   // LDS row stride: the 16 lanes of a k-group read
+                                             // 16 consecutive rows at 4 distinct bank quads
+    static constexpr int UPR = GROW / 16;    // 16-byte units per row
+};
+
+bool wide_can_search(uint32_t Dp) { return Dp >= 4 && Dp <= 64 && Dp % 4 == 0; }
+
+template <int DP>
+__host__ __device__ inline bool wide_resident(uint32_t K) {
+    return (uint64_t)((K + 31) & ~31u) * WideCfg<DP>::LSTR <= WD_LDS_MAX;
+}
+
+template <int DP>
+__global__ __launch_bounds__(WD_THREADS) void assign_wide_kernel(
+    const uint8_t *__restrict__ codes, uint64_t N, uint32_t D, const _Float16 *__restrict__ g_rows, uint32_t K,
+    const float *__restrict__ g_C32, MfThresholds th, uint32_t *__restrict__ A, uint32_t *__restrict__ flags,
+    unsigned *__restrict__ flag_cnt) {
+    using C = WideCfg<DP>;
+    constexpr int KS = C::KS, LSTR = C::LSTR, UPR = C::UPR, NH = C::DH / 8;
+    constexpr bool TWO = KS >= 2;   // keep two units
+    extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+    const uint32_t Kp = (K + 31) & ~31u;
+    const bool resident = wide_resident<DP>(K);
+    const uint32_t SL = resident ? Kp : WD_SLICE;
+    const uint32_t ns = (Kp + SL - 1) / SL;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int g = lane >> 4, c = lane & 15;
+    const unsigned char *gsrc = reinterpret_cast<const unsigned char *>(g_rows);
+    unsigned char *buf0 = lds, *buf1 = lds + (resident ? 0 : WD_SLICE * LSTR);
+
+    // slice s: code vectors s*WD_SLICE.. (KS 16-byte units per thread, staged in registers)
+    uint4 stage[KS];
+#define WD_STAGE_LOAD(S)                                                                                         \
+    _Pragma("unroll") for (int i = 0; i < KS; i++) {                                                            \
+        const uint32_t u = tid + i * WD_THREADS, row = (S) * WD_SLICE + u / UPR, col = u % UPR;                  \
+        stage[i] = row < Kp ? *reinterpret_cast<const uint4 *>(gsrc + (size_t)row * C::GROW + col * 16)          \
+                            : make_uint4(0, 0, 0, 0);                                                             \
+    }
+#define WD_STAGE_STORE(S, BUF)                                                                                   \
+    _Pragma("unroll") for (int i = 0; i < KS; i++) {                                                            \
+        const uint32_t u = tid + i * WD_THREADS, row = u / UPR, col = u % UPR;                                   \
+        if ((S) * WD_SLICE + row < Kp) *reinterpret_cast<uint4 *>((BUF) + row * LSTR + col * 16) = stage[i];      \
+    }
+    if (resident) {
+        for (uint32_t u = tid; u < Kp * UPR; u += WD_THREADS) {
+            const uint32_t row = u / UPR, col = u % UPR;
+            *reinterpret_cast<uint4 *>(buf0 + row * LSTR + col * 16) =
+                *reinterpret_cast<const uint4 *>(gsrc + (size_t)row * C::GROW + col * 16);
+        }
+    } else {
+        WD_STAGE_LOAD(0u)
+        WD_STAGE_STORE(0u, buf0)
+    }
+    __syncthreads();
+
+    const uint64_t nchunks = (N + WD_ROWS - 1) / WD_ROWS;
+    const uint64_t wg_stride = (uint64_t)gridDim.x * WD_WAVES;
+    const f32x4 zero = {0.f, 0.f, 0.f, 0.f};
+    uint32_t it = 0;   // slices consumed (buffer parity)
+    for (uint64_t cb = (uint64_t)blockIdx.x * WD_WAVES; cb < nchunks; cb += wg_stride) {
+        const uint64_t chunk = cb + wave;
+        const uint64_t base = chunk * WD_ROWS;
+        const bool more = cb + wg_stride < nchunks;   // uniform over the workgroup
+
+        // B fragments: lane (g, c) holds k-slots 32ks + 8g .. +7 of row c of each tile, i.e.
+        // 8-slot group G = 4ks + g: hi components 8G.., lo components 8(G-NH).., the two ones
+        // of the norm slots, or zeros.
+        half8 b[WD_TILES][KS];
+#pragma unroll
+        for (int t = 0; t < WD_TILES; t++) {
+            const uint64_t row = base + t * 16 + c;
+            const bool valid = chunk < nchunks && row < N;
+            const uint8_t *rp = codes + row * DP;
+#pragma unroll
+            for (int ks = 0; ks < KS; ks++) {
+                const int G = 4 * ks + g;
+                half8 h = {0, 0, 0, 0, 0, 0, 0, 0};
+                if (G < 2 * NH) {
+                    if (valid) {
+                        const int m = G < NH ? G : G - NH;
+                        const uint32_t w0 = *reinterpret_cast<const uint32_t *>(rp + 8 * m);
+                        const uint32_t w1 = 8 * m + 4 < DP ? *reinterpret_cast<const uint32_t *>(rp + 8 * m + 4) : 0u;
+#pragma unroll
+                        for (int j = 0; j < 4; j++) {
+                            h[j] = (_Float16)byte_w(w0, j);
+                            h[4 + j] = (_Float16)byte_w(w1, j);
+                        }
+                    }
+                } else if (G == 2 * NH) {
+                    h[0] = (_Float16)1.f;
+                    h[1] = (_Float16)1.f;
+                }
+                b[t][ks] = h;
+            }
+        }
+        float b1[WD_TILES], b2[WD_TILES], b3[WD_TILES];
+        uint32_t bp[WD_TILES], bq[WD_TILES];
+#pragma unroll
+        for (int t = 0; t < WD_TILES; t++) {
+            b1[t] = INFINITY;
+            b2[t] = INFINITY;
+            b3[t] = INFINITY;
+            bp[t] = 0;
+            bq[t] = 0;
+        }
+        for (uint32_t s = 0; s < ns; s++) {
+            const unsigned char *cur = (it & 1) ? buf1 : buf0;
+            const bool pre = !resident && (s + 1 < ns || more);
+            const uint32_t snext = s + 1 < ns ? s + 1 : 0;
+            if (pre) {
+                WD_STAGE_LOAD(snext)
+            }
+            const uint32_t r0 = resident ? 0 : s * WD_SLICE;
+            const uint32_t np = min(SL, Kp - r0) / 32;
+            const unsigned char *abase = cur + c * LSTR + 16 * g;
+#pragma unroll 2
+            for (uint32_t p = 0; p < np; p++) {
+                half8 a0[KS], a1[KS];
+#pragma unroll
+                for (int ks = 0; ks < KS; ks++) {
+                    a0[ks] = *reinterpret_cast<const half8 *>(abase + (size_t)(32 * p) * LSTR + 64 * ks);
+                    a1[ks] = *reinterpret_cast<const half8 *>(abase + (size_t)(32 * p + 16) * LSTR + 64 * ks);
+                }
+                f32x4 p0[WD_TILES], p1[WD_TILES];
+#pragma unroll
+                for (int t = 0; t < WD_TILES; t++) {
+                    p0[t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a0[0], b[t][0], zero, 0, 0, 0);
+                    p1[t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a1[0], b[t][0], zero, 0, 0, 0);
+                }
+#pragma unroll
+                for (int ks = 1; ks < KS; ks++)
+#pragma unroll
+                    for (int t = 0; t < WD_TILES; t++) {
+                        p0[t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a0[ks], b[t][ks], p0[t], 0, 0, 0);
+                        p1[t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a1[ks], b[t][ks], p1[t], 0, 0, 0);
+                    }
+#pragma unroll
+                for (int t = 0; t < WD_TILES; t++) {
+                    if (TWO)
+                        pair_update2(p0[t], p1[t], r0 / 32 + p, b1[t], b2[t], b3[t], bp[t], bq[t]);
+                    else
+                        pair_update(p0[t], p1[t], r0 / 32 + p, b1[t], b2[t], bp[t]);
+                }
+            }
+            if (!resident) {
+                if (pre) {
+                    unsigned char *nb = (it & 1) ? buf0 : buf1;
+                    WD_STAGE_STORE(snext, nb)
+                }
+                __syncthreads();
+                it++;
+            }
+        }
+
+        // Combine the four lanes of each data row.  One unit: the winning 8-code-vector unit
+        // (pair*4 + g) and the best MFMA score among all other units.  Two units: the best two
+        // units (ordered by score, then unit) and the best score among all other units.
+        uint32_t unit = 0, unit2 = 0;
+        float sec_m = INFINITY;
+#pragma unroll
+        for (int t = 0; t < WD_TILES; t++) {
+            uint32_t u = bp[t] * 4 + g, v = bq[t] * 4 + g;
+#pragma unroll
+            for (int off = 16; off <= 32; off <<= 1) {
+                const float o1 = __shfl_xor(b1[t], off), o2 = __shfl_xor(b2[t], off);
+                const uint32_t ou = __shfl_xor(u, off);
+                if (!TWO) {
+                    if (o1 < b1[t] || (o1 == b1[t] && ou < u)) {
+                        b2[t] = min2f(o2, b1[t]);
+                        b1[t] = o1;
+                        u = ou;
+                    } else {
+                        b2[t] = min2f(b2[t], o1);
+                    }
+                    continue;
+                }
+                const float o3 = __shfl_xor(b3[t], off);
+                const uint32_t ov = __shfl_xor(v, off);
+                // merge (b1,u) <= (b2,v) with (o1,ou) <= (o2,ov); thirds b3, o3
+                auto lt = [](float x, uint32_t xu, float y, uint32_t yu) { return x < y || (x == y && xu < yu); };
+                float n1, n2, n3;
+                uint32_t m1, m2;
+                if (lt(o1, ou, b1[t], u)) {   // partner's best first; then (b1,u) vs (o2,ov)
+                    n1 = o1;
+                    m1 = ou;
+                    const bool mine = lt(b1[t], u, o2, ov);
+                    n2 = mine ? b1[t] : o2;
+                    m2 = mine ? u : ov;
+                    n3 = min3f(mine ? o2 : b1[t], b2[t], min2f(b3[t], o3));
+                } else {
+                    n1 = b1[t];
+                    m1 = u;
+                    const bool mine = lt(b2[t], v, o1, ou);
+                    n2 = mine ? b2[t] : o1;
+                    m2 = mine ? v : ou;
+                    n3 = min3f(mine ? o1 : b2[t], o2, min2f(b3[t], o3));
+                }
+                b1[t] = n1;
+                b2[t] = n2;
+                b3[t] = n3;
+                u = m1;
+                v = m2;
+            }
+            unit = g == t ? u : unit;
+            unit2 = g == t ? v : unit2;
+            sec_m = g == t ? (TWO ? b3[t] : b2[t]) : sec_m;
+        }
+        // Lane L owns row base + L: direct fp32 (x - c)^2 over the 8 code vectors of its unit.
+        const uint64_t row = base + lane;
+        if (chunk < nchunks && row < N) {
+            float x[DP];
+            float xn = 0.f;   // ||x - mu||^2 over the D real components
+            const uint32_t *rw = reinterpret_cast<const uint32_t *>(codes + row * DP);
+#pragma unroll
+            for (int q = 0; q < DP / 4; q++) {
+                const uint32_t word = rw[q];
+#pragma unroll
+                for (int j = 0; j < 4; j++) {
+                    const int d = 4 * q + j;
+                    const float e = byte_w(word, j) * th.sx;
+                    const bool real = (uint32_t)d < D;
+                    xn = real ? __fmaf_rn(e, e, xn) : xn;
+                    x[d] = real ? e + th.mu : 0.f;   // C32 holds 0 in the padding components
+                }
+            }
+            float r1 = INFINITY, r2 = INFINITY;
+            uint32_t rk = 0;
+#pragma unroll 2
+            for (int j = 0; j < (TWO ? 16 : 8); j++) {
+                const uint32_t un = j < 8 ? unit : unit2, jj = j & 7;
+                const uint32_t cv = (2 * (un >> 2) + (jj >> 2)) * 16 + 4 * (un & 3) + (jj & 3);
+                const float4 *c4 = reinterpret_cast<const float4 *>(g_C32 + (size_t)cv * DP);
+                float dist = 0.f;
+#pragma unroll
+                for (int q = 0; q < DP / 4; q++) {
+                    const float4 cq = c4[q];
+                    float e;
+                    e = x[4 * q + 0] - cq.x; dist = __fmaf_rn(e, e, dist);
+                    e = x[4 * q + 1] - cq.y; dist = __fmaf_rn(e, e, dist);
+                    e = x[4 * q + 2] - cq.z; dist = __fmaf_rn(e, e, dist);
+                    e = x[4 * q + 3] - cq.w; dist = __fmaf_rn(e, e, dist);
+                }
+                dist = cv < K ? dist : INFINITY;   // padding code vectors never win
+                r2 = med3f(r1, r2, dist);
+                rk = dist < r1 ? cv : rk;
+                r1 = min2f(r1, dist);
+            }
+            const float rest = __fmaf_rn(sec_m, th.inv_scale, xn);   // best unit not recomputed
+            bool flag;
+            if (TWO) {   // recomputed runner-up (direct fp32 error), rest (plus the MFMA error)
+                const float thr2 = 2.f * (th.alpha * sqrtf(r2) + th.beta * r2) + th.gamma;
+                const float thr3 = th.mfma + 2.f * (th.alpha * sqrtf(rest) + th.beta * rest) + th.gamma;
+                flag = !(r2 - r1 > thr2) || !(rest - r1 > thr3);
+            } else {
+                const float sec = min2f(rest, r2);
+                const float thr = th.mfma + 2.f * (th.alpha * sqrtf(sec) + th.beta * sec) + th.gamma;
+                flag = !(sec - r1 > thr);
+            }
+            A[row] = rk;
+            if (flag) flags[atomicAdd(flag_cnt, 1u)] = (uint32_t)row;
+        }
+    }
+}
+
+#undef WD_STAGE_LOAD
+#undef WD_STAGE_STORE
+
+template <int DP>
+static hipError_t launch_wide_dp(hipStream_t s, int num_cu, uint32_t D, const uint8_t *codes, uint64_t N,
+                                 const _Float16 *cb_rows, uint32_t K, const float *C32, const MfThresholds &th,
+                                 uint32_t *A, uint32_t *flags, unsigned *flag_cnt) {
+    using C = WideCfg<DP>;
+    const uint32_t Kp = (K + 31) & ~31u;
+    const size_t lds = wide_resident<DP>(K) ? (size_t)Kp * C::LSTR : 2 * (size_t)WD_SLICE * C::LSTR;
+    const uint64_t nchunks = (N + WD_ROWS - 1) / WD_ROWS;
+    const int grid = (int)std::max<uint64_t>(1, std::min<uint64_t>((nchunks + WD_WAVES - 1) / WD_WAVES, num_cu));
+    hipLaunchKernelGGL(assign_wide_kernel<DP>, dim3(grid), dim3(WD_THREADS), lds, s, codes, N, D, cb_rows, K, C32, th,
+                       A, flags, flag_cnt);
+    return hipGetLastError();
+}
+
+hipError_t launch_assign_wide(hipStream_t s, int num_cu, uint32_t Dp, uint32_t D, const uint8_t *codes, uint64_t N,
+                              const _Float16 *cb_rows, uint32_t K, const float *C32, const MfThresholds &th,
+                              uint32_t *A, uint32_t *flags, unsigned *flag_cnt) {
+    if (K == 0 || !wide_can_search(Dp) || D > Dp || D + 4 <= Dp) return hipErrorInvalidValue;
+    switch (Dp) {
+#define X(DPV) \
+    case DPV: return launch_wide_dp<DPV>(s, num_cu, D, codes, N, cb_rows, K, C32, th, A, flags, flag_cnt);
+        X(4) X(8) X(12) X(16) X(20) X(24) X(28) X(32) X(36) X(40) X(44) X(48) X(52) X(56) X(60) X(64)
+#undef X
+    }
+    return hipErrorInvalidValue;
+}
+
+}  // namespace qvq

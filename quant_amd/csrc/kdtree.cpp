@@ -12,23 +12,37 @@ namespace qvq {
 
 double ref_l2(const double *a, const double *b, int dim) { return ref_l2_hd(a, b, dim); }
 
-RefKDTree::RefKDTree(const double *pts, size_t K, int dim) : pts_(pts), dim_(dim) {
+RefKDTree::RefKDTree(const double *pts, size_t K, int dim) : pts_(pts), dim_(dim), K_(K) {
+    static thread_local std::vector<double> cols;   // reused: a fresh 1.5 MB buffer per level page-faults
+    if (cols.size() < K * (size_t)dim) cols.resize(K * (size_t)dim);
+    double *const cbuf = cols.data();   // (thread_local: the helper threads must not name `cols`)
+    cols_ = cbuf;
     vind_.resize(K);
     for (size_t i = 0; i < K; i++) vind_[i] = i;
     root_bbox_.resize(dim);
-    for (int d = 0; d < dim; d++) root_bbox_[d].low = root_bbox_[d].high = pt(0, d);
-    for (size_t k = 1; k < K; k++)
+    // column-major copy and root box (threads measured slower here: ~30 us per spawn)
+    {
         for (int d = 0; d < dim; d++) {
-            const double v = pt(k, d);
-            if (v < root_bbox_[d].low) root_bbox_[d].low = v;
-            if (v > root_bbox_[d].high) root_bbox_[d].high = v;
+            double *col = cbuf + (size_t)d * K;
+            double lo = pts[d], hi = lo;
+            for (size_t k = 0; k < K; k++) {
+                const double v = pts[k * (size_t)dim + d];
+                col[k] = v;
+                if (v < lo) lo = v;
+                if (v > hi) hi = v;
+            }
+            root_bbox_[d].low = lo;
+            root_bbox_[d].high = hi;
         }
+    }
     nodes_.reserve(2 * (K / 5 + 1));
-    divide(0, K, root_bbox_, 1);
+    std::vector<Box> box(root_bbox_);
+    divide(0, K, box, 1, nodes_, depth_);
     flat_nodes_.resize(nodes_.size());
     flat_vind_.resize(K);
     flat_box_.resize(2 * (size_t)dim);
     flatten(flat_nodes_.data(), flat_vind_.data(), flat_box_.data(), flat_box_.data() + dim);
+    cols_ = nullptr;
 }
 
 void RefKDTree::min_max(const size_t *ind, size_t count, int e, double &mn, double &mx) const {
@@ -71,22 +85,27 @@ void RefKDTree::middle_split(size_t *ind, size_t count, size_t &index, int &cutf
     const double EPS = 0.00001;
     double max_span = bbox[0].high - bbox[0].low;
     for (int i = 1; i < dim_; i++) max_span = std::max(max_span, bbox[i].high - bbox[i].low);
-    double max_spread = -1;
+    // Candidate dimensions: span within EPS of the widest.  In real codebooks (empty cells at
+    // 0, saturated colours) every dimension not yet cut along the path has the root's span,
+    // so upper nodes need the point min/max of most dimensions, from the column copy.
+    int q[64], nq = 0;
+    for (int i = 0; i < dim_; i++)
+        if (bbox[i].high - bbox[i].low > (1 - EPS) * max_span) q[nq++] = i;
+    double qmn[64], qmx[64];
+    for (int j = 0; j < nq; j++) min_max(ind, count, q[j], qmn[j], qmx[j]);
+    double max_spread = -1, mn = 0, mx = 0;
     cutfeat = 0;
-    for (int i = 0; i < dim_; i++) {
-        const double span = bbox[i].high - bbox[i].low;
-        if (span > (1 - EPS) * max_span) {
-            double mn, mx;
-            min_max(ind, count, i, mn, mx);
-            if (mx - mn > max_spread) {
-                cutfeat = i;
-                max_spread = mx - mn;
-            }
+    bool have = false;
+    for (int j = 0; j < nq; j++)
+        if (qmx[j] - qmn[j] > max_spread) {
+            cutfeat = q[j];
+            max_spread = qmx[j] - qmn[j];
+            mn = qmn[j];
+            mx = qmx[j];
+            have = true;
         }
-    }
+    if (!have) min_max(ind, count, cutfeat, mn, mx);
     const double split_val = (bbox[cutfeat].low + bbox[cutfeat].high) / 2;
-    double mn, mx;
-    min_max(ind, count, cutfeat, mn, mx);
     cutval = split_val < mn ? mn : (split_val > mx ? mx : split_val);
     size_t lim1, lim2;
     plane_split(ind, count, cutfeat, cutval, lim1, lim2);
@@ -96,20 +115,21 @@ void RefKDTree::middle_split(size_t *ind, size_t count, size_t &index, int &cutf
 }
 
 // bbox is in/out: the caller's cell box on entry, the node's actual point box on exit.
-int RefKDTree::divide(size_t left, size_t right, std::vector<Box> &bbox, int level) {
-    const int me = (int)nodes_.size();
-    depth_ = std::max(depth_, level);
-    nodes_.push_back(Node());
+int RefKDTree::divide(size_t left, size_t right, std::vector<Box> &bbox, int level, std::vector<Node> &nodes,
+                      int &depth) {
+    const int me = (int)nodes.size();
+    depth = std::max(depth, level);
+    nodes.push_back(Node());
     if (right - left <= 10) {   // leaf_max_size (KDTreeVectorOfVectorsAdaptor.hpp:59)
-        Node &n = nodes_[me];
+        Node &n = nodes[me];
         n.leaf = true;
         n.left = left;
         n.right = right;
         n.child1 = n.child2 = -1;
-        for (int d = 0; d < dim_; d++) bbox[d].low = bbox[d].high = pt(vind_[left], d);
-        for (size_t k = left + 1; k < right; k++)
+        for (int d = 0; d < dim_; d++) bbox[d].low = bbox[d].high = ptr(vind_[left], d);
+        for (size_t k = left + 1; k < right; k++)   // row-major: one point's coordinates are contiguous
             for (int d = 0; d < dim_; d++) {
-                const double v = pt(vind_[k], d);
+                const double v = ptr(vind_[k], d);
                 if (bbox[d].low > v) bbox[d].low = v;
                 if (bbox[d].high < v) bbox[d].high = v;
             }
@@ -119,13 +139,12 @@ int RefKDTree::divide(size_t left, size_t right, std::vector<Box> &bbox, int lev
     int cutfeat;
     double cutval;
     middle_split(vind_.data() + left, right - left, idx, cutfeat, cutval, bbox);
-    std::vector<Box> lb(bbox), rb;
+    std::vector<Box> lb(bbox), rb(bbox);
     lb[cutfeat].high = cutval;
-    const int c1 = divide(left, left + idx, lb, level + 1);
-    rb = bbox;
     rb[cutfeat].low = cutval;
-    const int c2 = divide(left + idx, right, rb, level + 1);
-    Node &n = nodes_[me];
+    const int c1 = divide(left, left + idx, lb, level + 1, nodes, depth);
+    const int c2 = divide(left + idx, right, rb, level + 1, nodes, depth);
+    Node &n = nodes[me];
     n.leaf = false;
     n.left = left;
     n.right = right;

@@ -40,14 +40,20 @@ private:
         double divlow, divhigh;
         int child1, child2;
     };
-    double pt(size_t i, int d) const { return pts_[i * (size_t)dim_ + d]; }
-    int divide(size_t left, size_t right, std::vector<Box> &bbox, int level);
+    // the build reads one coordinate of many points at a time: a column-major copy keeps
+    // those reads in cache (row-major, every read of a 48-D codebook was a cache miss)
+    double pt(size_t i, int d) const { return cols_[(size_t)d * K_ + i]; }
+    double ptr(size_t i, int d) const { return pts_[i * (size_t)dim_ + d]; }   // row-major
+    struct Node;
+    int divide(size_t left, size_t right, std::vector<Box> &bbox, int level, std::vector<Node> &nodes, int &depth);
     void middle_split(size_t *ind, size_t count, size_t &index, int &cutfeat, double &cutval,
                       const std::vector<Box> &bbox);
     void plane_split(size_t *ind, size_t count, int cutfeat, double cutval, size_t &lim1, size_t &lim2);
     void min_max(const size_t *ind, size_t count, int e, double &mn, double &mx) const;
     const double *pts_;
     int dim_;
+    size_t K_;
+    const double *cols_ = nullptr;   // [dim][K], thread-local scratch valid during the build
     std::vector<size_t> vind_;
     std::vector<Node> nodes_;
     std::vector<Box> root_bbox_;

@@ -148,3 +148,23 @@ def test_lbg_zero_rows_and_empty_cells(engine, kdmode):
     np.testing.assert_array_equal(C, C_x)
     assert abs(d - d_k) <= 1e-9 * abs(d_k)
     assert sum(engine.timings()["host_ties"]) > 0
+
+
+@pytest.mark.parametrize("bw,bh", [(1, 1), (2, 3), (3, 3), (4, 2), (4, 4)])
+@pytest.mark.parametrize("K", [32, 100, 700])
+def test_assign_wide_mfma(engine, monkeypatch, bw, bh, K):
+    """The MFMA search for D != 12 (k_wide.hip): codebook resident in LDS or streamed in
+    slices (K=700 at D=48 streams, with a partial last slice), K not a multiple of 32
+    (padding code vectors), split pairs and duplicates.  Same answer as the reference
+    kd-tree and as the VALU search."""
+    S = 96
+    X, _ = oracle.tile(oracle.gen_image(S), S, S, bw, bh)
+    engine.set_vectors(X)
+    rng = np.random.default_rng(K + 10 * bw + bh)
+    n = (K - 8) // 2
+    base = X[rng.choice(len(X), n, replace=True)]
+    C = np.concatenate([base * (1 + 0.2), base * (1 - 0.2), np.zeros((4, X.shape[1])), base[:4]])[:K]
+    want = oracle.kdtree_nn(C, X)
+    np.testing.assert_array_equal(engine.assign(C), want)
+    monkeypatch.setenv("QVQ_SEARCH", "valu")
+    np.testing.assert_array_equal(engine.assign(C), want)

@@ -21,4 +21,6 @@ for (S, bw, bits) in cases:
                       "assign_ms": [round(x, 4) for x in tm["assign_ms"]],
                       "update_ms": [round(x, 4) for x in tm["update_ms"]],
                       "other_ms": [round(x, 4) for x in tm["other_ms"]],
-                      "flagged": tm["flagged"], "host_ties": tm["host_ties"]}), flush=True)
+                      "flagged": tm["flagged"], "host_ties": tm["host_ties"],
+                      "wait_ms": [round(x, 3) for x in tm["wait_ms"]], "tree_ms": [round(x, 3) for x in tm["tree_ms"]]}),
+          flush=True)
