@@ -365,10 +365,15 @@ void build_tree(qvq_ctx *ctx, const double *hC, uint32_t K, int buf, KdView &kd)
     KdNodeDev *nodes = reinterpret_cast<KdNodeDev *>(hi + D);
     uint32_t *vind = reinterpret_cast<uint32_t *>(nodes + nn);
     tree.flatten(nodes, vind, lo, hi);
-    // one DMA into device memory: every kd_resolve workgroup stages the image, and reads
-    // of mapped host memory from 16 workgroups cost ~70 us per level
-    if (hipMemcpyAsync(ctx->d_tree, ctx->h_tree[buf], bytes, hipMemcpyHostToDevice, ctx->stream) != hipSuccess) return;
-    const double *dlo = reinterpret_cast<const double *>(ctx->d_tree);
+    // Every kd_resolve workgroup stages the image.  Big images (C4: 150+ KB) go to device
+    // memory with one DMA first (mapped reads from 16 workgroups cost up to ~70 us); small
+    // ones are read in place (the DMA itself costs ~5 us of stream time per level).
+    const double *dlo = reinterpret_cast<const double *>(ctx->dh_tree[buf]);
+    if (bytes > 32768) {
+        if (hipMemcpyAsync(ctx->d_tree, ctx->h_tree[buf], bytes, hipMemcpyHostToDevice, ctx->stream) != hipSuccess)
+            return;
+        dlo = reinterpret_cast<const double *>(ctx->d_tree);
+    }
     v.lo = dlo;
     v.hi = dlo + D;
     v.nodes = reinterpret_cast<const KdNodeDev *>(dlo + 2 * D);

@@ -547,7 +547,8 @@ hipError_t launch_assign_mfma(hipStream_t s, int grid, bool fuse, const uint8_t 
                               const _Float16 *cb_rows, uint32_t K, const float *C32, const uint64_t *plut,
                               const MfThresholds &th, uint32_t *A, uint32_t *flags, unsigned *flag_cnt,
                               uint64_t *part, uint32_t *part_cnt) {
-    const bool staged = mf_lds_layout(K, fuse, true).total <= MF_LDS_MAX;
+    static const bool no_stage = std::getenv("QVQ_NOSTAGE") != nullptr;   // ablation
+    const bool staged = mf_lds_layout(K, fuse, true).total <= MF_LDS_MAX && (!no_stage || K <= mf_small_k());
     const size_t lds = mf_lds_layout(K, fuse, staged).total;
     using Fn = void (*)(hipStream_t, int, size_t, const uint8_t *, uint64_t, const _Float16 *, uint32_t, const float *,
                         const uint64_t *, const MfThresholds &, uint32_t *, uint32_t *, unsigned *, uint64_t *,
