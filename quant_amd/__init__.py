@@ -16,7 +16,7 @@ import os
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "lib", "libqvq.so")
+LIB_PATH = os.environ.get("QVQ_LIB") or os.path.join(_HERE, "lib", "libqvq.so")   # QVQ_LIB: A/B builds (tools/)
 
 NORMAL, SCALED, CIE1931 = 0, 1, 2   # enum class ColorSpaces (include/ColorSpace.hpp:6)
 

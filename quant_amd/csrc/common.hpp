@@ -100,10 +100,29 @@ hipError_t launch_assign_valu(hipStream_t s, int num_cu, uint32_t Dp, const uint
 // Flag rule (distances, unscaled): second - best <= mfma + 2*(alpha*sqrt(second) + beta*second)
 // + gamma, where `mfma` bounds the error of one MFMA score and the rest the fp32 direct-form
 // recompute ("near-tie flags").
+// A re-assigned row of the fused path (the search added its terms at its provisional index
+// `from`): its packed terms (hi << 32 | lo, plut) go to slab G (xslab [d][k], xcnt [k]) at
+// `to` and to slab G + 1 (xslab + K*D, xcnt + K; subtracted by the reduce) at `from`.
+// Called by the lanes of one wave (lane < D does component lane).
+__device__ inline void move_row_terms(const uint8_t *codes, uint32_t Dp, uint32_t D, uint32_t row, uint32_t from,
+                                      uint32_t to, uint32_t K, uint64_t *xslab, uint32_t *xcnt, const uint64_t *plut,
+                                      uint32_t lane) {
+    if (lane < D) {
+        const unsigned long long t = plut[codes[(uint64_t)row * Dp + lane]];
+        atomicAdd((unsigned long long *)&xslab[(uint64_t)lane * K + to], t);
+        atomicAdd((unsigned long long *)&xslab[(uint64_t)K * D + (uint64_t)lane * K + from], t);
+    }
+    if (lane == 0) {
+        atomicAdd(&xcnt[to], 1u);
+        atomicAdd(&xcnt[K + from], 1u);
+    }
+}
+
 struct MfThresholds {
     float mfma, alpha, beta, gamma;
     float inv_scale;   // 2^-t
     float mu, sx;      // x = mu + w * sx
+    uint32_t runs_max_k;   // fused sums: wave run reduction up to this K, plain LDS atomics above
 };
 uint32_t mf_fuse_max_k();
 bool mf_can_search(uint32_t K);
@@ -136,8 +155,10 @@ hipError_t launch_kd_resolve(hipStream_t s, const uint8_t *codes, uint32_t Dp, u
                              const KdView &kd, uint32_t *A, uint64_t *xslab, uint32_t *xcnt, const uint64_t *plut);
 hipError_t launch_update(hipStream_t s, uint32_t Dp, uint32_t G, const uint8_t *codes, uint64_t N, const uint32_t *A,
                          uint32_t K, uint32_t D, const uint64_t *plut, uint64_t *part, uint32_t *part_cnt);
-hipError_t launch_reduce(hipStream_t s, const uint64_t *part, const uint32_t *part_cnt, uint32_t G, uint32_t K,
-                         uint32_t D, uint64_t *sums);
+// Sums of G slabs, the last nsub of them subtracted (fused path: slab G + 1 holds the terms
+// of re-assigned rows at their provisional index).
+hipError_t launch_reduce(hipStream_t s, const uint64_t *part, const uint32_t *part_cnt, uint32_t G, uint32_t nsub,
+                         uint32_t K, uint32_t D, uint64_t *sums);
 hipError_t launch_mean_sums(hipStream_t s, uint32_t Dp, const uint8_t *codes, uint64_t N, uint32_t D,
                             const uint64_t *plut, uint64_t *sums);
 // Centroids of the reduced sums (C_cent [K][D]); with split also the next level's K' = 2K
@@ -157,11 +178,11 @@ hipError_t launch_prep(hipStream_t s, const double *C64, uint32_t K, uint32_t Kp
                        double mu, double sx, int t, float *C32, _Float16 *cb_rows);
 hipError_t launch_gather_codes(hipStream_t s, const uint8_t *codes, uint32_t Dp, const uint32_t *rows, uint32_t n,
                                uint8_t *out);
-// A[rows[i]] = vals[i]; host-aggregated terms of those rows into the extra slab:
-// idx < KD -> slab[idx] += val (packed hi << 32 | lo), else slab_cnt[idx - KD] += val.
-hipError_t launch_scatter(hipStream_t s, uint32_t *A, const uint32_t *rows, const uint32_t *vals, uint32_t n,
-                          uint64_t *slab, uint32_t *slab_cnt, uint64_t KD, const uint64_t *idx, const uint64_t *val,
-                          uint32_t nterms);
+// Host-resolved rows: A[rows[i]] = vals[i]; with xslab their terms move from the
+// provisional index (A before) to the new one (move_row_terms).
+hipError_t launch_fix_rows(hipStream_t s, const uint8_t *codes, uint32_t Dp, uint32_t D, uint32_t *A,
+                           const uint32_t *rows, const uint32_t *vals, uint32_t n, uint32_t K, uint64_t *xslab,
+                           uint32_t *xcnt, const uint64_t *plut);
 // 256-bin histogram of the first D bytes of every row (hist zeroed first).
 hipError_t launch_byte_hist(hipStream_t s, const uint8_t *codes, uint64_t N, uint32_t D, uint32_t Dp,
                             uint64_t *hist);

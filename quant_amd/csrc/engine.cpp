@@ -113,6 +113,7 @@ struct qvq_ctx {
     std::vector<double> cb_local;   // host copy of the published codebook for the tree build
     uint64_t tree_cap = 0;
     uint32_t nslabs = 0;   // slabs holding the last run_level's sums
+    uint32_t nsub = 0;     // ... of which the last nsub are subtracted
     int timing_level = -1;   // qvq_set_timing: -1 all levels, -2 none, else that level only
     bool upd[32] = {};
     hipEvent_t ev_end = nullptr;
@@ -249,6 +250,10 @@ void mfma_setup(qvq_ctx *ctx) {
     ctx->mf_th.inv_scale = (float)std::ldexp(1.0, -tt);
     ctx->mf_th.mu = (float)t.mu;
     ctx->mf_th.sx = (float)t.sx;
+    {
+        const char *e = std::getenv("QVQ_RUNS_MAXK");   // ablation
+        ctx->mf_th.runs_max_k = e ? (uint32_t)std::atoi(e) : 1u << 30;
+    }
 }
 
 // Allocate the per-row buffers and upload the colour-space tables.
@@ -287,9 +292,10 @@ qvq_status ensure_levels(qvq_ctx *ctx, uint32_t Kmax) {
     HIPCHK(hipMalloc(&ctx->d_C64_split, KD * 8));
     HIPCHK(hipMalloc(&ctx->d_C32, Kp * ctx->Dp * 4));
     HIPCHK(hipMalloc(&ctx->d_rows, Kp * 2 * cb_row_f16(ctx->D, ctx->Dp)));
-    // G per-CU slabs + one extra (rows the recheck / kd-tree resolve in the fused path)
-    HIPCHK(hipMalloc(&ctx->d_part, (uint64_t)(ctx->G + 1) * KD * 8));
-    HIPCHK(hipMalloc(&ctx->d_part_cnt, (uint64_t)(ctx->G + 1) * Kmax * 4));
+    // G per-CU slabs + two correction slabs (fused path: rows the recheck / kd-tree move, at
+    // the new index (+) and at the search's provisional one (-))
+    HIPCHK(hipMalloc(&ctx->d_part, (uint64_t)(ctx->G + 2) * KD * 8));
+    HIPCHK(hipMalloc(&ctx->d_part_cnt, (uint64_t)(ctx->G + 2) * Kmax * 4));
     HIPCHK(hipMalloc(&ctx->d_sums, (2 * KD + Kmax) * 8));
     const unsigned mflags = hipHostMallocMapped | hipHostMallocCoherent;
     HIPCHK(hipHostMalloc(&ctx->h_cb, KD * 8, mflags));
@@ -338,7 +344,7 @@ qvq_status run_update_slabs(qvq_ctx *ctx, const uint32_t *d_A, uint32_t K) {
 qvq_status run_update(qvq_ctx *ctx, const uint32_t *d_A, uint32_t K) {
     qvq_status st = run_update_slabs(ctx, d_A, K);
     if (st != QVQ_OK) return st;
-    HIPCHK(launch_reduce(ctx->stream, ctx->d_part, ctx->d_part_cnt, ctx->G, K, ctx->D, ctx->d_sums));
+    HIPCHK(launch_reduce(ctx->stream, ctx->d_part, ctx->d_part_cnt, ctx->G, 0, K, ctx->D, ctx->d_sums));
     return QVQ_OK;
 }
 
@@ -403,10 +409,11 @@ qvq_status wait_codebook(qvq_ctx *ctx, uint64_t seq) {
 }
 
 // Tie rows listed by the recheck when no device tree was available: answer them with the
-// host tree over hC, write A and (accumulate) add their terms to the extra slab G.  Synchronous.
+// host tree over hC and write A; with accumulate their terms move from the search's
+// provisional index to the answer (launch_fix_rows).  Synchronous.
 qvq_status resolve_host_ties(qvq_ctx *ctx, const double *hC, uint32_t K, uint32_t nt, bool accumulate) {
     const uint32_t D = ctx->D, Dp = ctx->Dp;
-    const uint64_t need = (uint64_t)nt * (8 + Dp) + 8 + (uint64_t)nt * (2 * D + 1) * 16;   // + (idx, val) terms
+    const uint64_t need = (uint64_t)nt * (8 + Dp);
     if (ctx->scatter_bytes < need) {
         dfree(ctx->d_scatter);
         HIPCHK(hipMalloc(&ctx->d_scatter, need));
@@ -414,7 +421,6 @@ qvq_status resolve_host_ties(qvq_ctx *ctx, const double *hC, uint32_t K, uint32_
     }
     uint32_t *d_rows = ctx->d_scatter, *d_vals = ctx->d_scatter + nt;
     uint8_t *d_gath = reinterpret_cast<uint8_t *>(ctx->d_scatter + 2 * (uint64_t)nt);
-    uint64_t *d_terms = reinterpret_cast<uint64_t *>(ctx->d_scatter) + ((uint64_t)nt * (8 + Dp) + 7) / 8;
     std::vector<uint32_t> rows(nt), vals(nt);
     std::vector<uint8_t> code((uint64_t)nt * Dp);
     HIPCHK(launch_gather_codes(ctx->stream, ctx->d_codes, Dp, ctx->d_ties, nt, d_gath));
@@ -423,30 +429,16 @@ qvq_status resolve_host_ties(qvq_ctx *ctx, const double *hC, uint32_t K, uint32_
     HIPCHK(hipStreamSynchronize(ctx->stream));
     std::vector<double> q(D);
     RefKDTree tree(hC, K, (int)D);
-    std::vector<uint64_t> idx, val;
-    const uint64_t KD = (uint64_t)K * D;
     for (uint32_t i = 0; i < nt; i++) {
         for (uint32_t d = 0; d < D; d++) q[d] = ctx->terms.v64[code[(uint64_t)i * Dp + d]];
         vals[i] = tree.nearest(q.data());
-        if (accumulate) {   // slab entries: packed hi << 32 | lo at d*K + k, count at KD + k
-            for (uint32_t d = 0; d < D; d++) {
-                const uint8_t c = code[(uint64_t)i * Dp + d];
-                idx.push_back((uint64_t)d * K + vals[i]);
-                val.push_back((uint64_t)ctx->terms.hi[c] << 32 | ctx->terms.lo[c]);
-            }
-            idx.push_back(KD + vals[i]);
-            val.push_back(1);
-        }
     }
-    const uint32_t nterms = (uint32_t)idx.size();
     HIPCHK(hipMemcpyAsync(d_rows, rows.data(), nt * 4, hipMemcpyHostToDevice, ctx->stream));
     HIPCHK(hipMemcpyAsync(d_vals, vals.data(), nt * 4, hipMemcpyHostToDevice, ctx->stream));
-    if (nterms) {
-        HIPCHK(hipMemcpyAsync(d_terms, idx.data(), nterms * 8ull, hipMemcpyHostToDevice, ctx->stream));
-        HIPCHK(hipMemcpyAsync(d_terms + nterms, val.data(), nterms * 8ull, hipMemcpyHostToDevice, ctx->stream));
-    }
-    HIPCHK(launch_scatter(ctx->stream, ctx->d_A, d_rows, d_vals, nt, ctx->d_part + (uint64_t)ctx->G * KD,
-                          ctx->d_part_cnt + (uint64_t)ctx->G * K, KD, d_terms, d_terms + nterms, nterms));
+    uint64_t *xslab = accumulate ? ctx->d_part + (uint64_t)ctx->G * K * D : nullptr;
+    uint32_t *xcnt = accumulate ? ctx->d_part_cnt + (uint64_t)ctx->G * K : nullptr;
+    HIPCHK(launch_fix_rows(ctx->stream, ctx->d_codes, Dp, D, ctx->d_A, d_rows, d_vals, nt, K, xslab, xcnt,
+                           ctx->d_plut));
     HIPCHK(hipStreamSynchronize(ctx->stream));   // the host vectors must outlive the copies
     return QVQ_OK;
 }
@@ -454,13 +446,16 @@ qvq_status resolve_host_ties(qvq_ctx *ctx, const double *hC, uint32_t K, uint32_
 // One level's assignment of every row against the split codebook (d_C64_split, host copy
 // hC, search tables in d_C32/d_rows), K code vectors.  wait_seq != 0: hC is published by a
 // finalize still in flight.  With sums_out the exact centroid sums of the final assignment
-// are left in the first ctx->nslabs slabs of d_part / d_part_cnt (fused: the search's G slabs
-// plus slab G for the rows the recheck and the kd-tree resolve; otherwise the update's G).
+// are left in the first ctx->nslabs slabs of d_part / d_part_cnt, the last ctx->nsub of them
+// to be subtracted (fused: the search's G slabs with every row at its provisional index, slab
+// G with the rows the recheck and the kd-tree move at their new index, slab G + 1 with the
+// same rows at the provisional one; otherwise the update's G).
 qvq_status run_level(qvq_ctx *ctx, uint32_t K, int slot, bool sums_out, const double *hC, uint64_t wait_seq) {
     const bool fused = sums_out && use_fused(ctx, K);
     uint64_t *xslab = fused ? ctx->d_part + (uint64_t)ctx->G * K * ctx->D : nullptr;
     uint32_t *xcnt = fused ? ctx->d_part_cnt + (uint64_t)ctx->G * K : nullptr;
-    ctx->nslabs = fused ? ctx->G + 1 : ctx->G;
+    ctx->nslabs = fused ? ctx->G + 2 : ctx->G;
+    ctx->nsub = fused ? 1 : 0;
     unsigned *cnt = ctx->d_counters + 2 * slot;
     // HIP events around the search (each record costs a few us of GPU idle): every level,
     // one level, or none (qvq_set_timing)
@@ -768,7 +763,8 @@ QVQ_API qvq_status qvq_lbg(qvq_ctx *ctx, uint32_t bits, double eps, double *code
         if ((st = run_level(ctx, K, slot, true, ctx->h_cb, ctx->seq)) != QVQ_OK) return st;
         const bool split = lvl < bits;
         {
-            HIPCHK(launch_reduce(ctx->stream, ctx->d_part, ctx->d_part_cnt, ctx->nslabs, K, ctx->D, ctx->d_sums));
+            HIPCHK(launch_reduce(ctx->stream, ctx->d_part, ctx->d_part_cnt, ctx->nslabs, ctx->nsub, K, ctx->D,
+                                 ctx->d_sums));
             if ((st = all_reduce_sums(ctx, K)) != QVQ_OK) return st;
             HIPCHK(finalize(K, split));
         }

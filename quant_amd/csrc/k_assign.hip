@@ -23,7 +23,13 @@ namespace qvq {
 // =======================================================================================
 // MFMA search
 // =======================================================================================
-constexpr int MF_THREADS = 1024;                 // 16 waves (4 per SIMD), one workgroup per CU
+#ifndef QVQ_MF_LOOP
+#define QVQ_MF_LOOP 0
+#endif
+#ifndef QVQ_MF_THREADS
+#define QVQ_MF_THREADS 1024
+#endif
+constexpr int MF_THREADS = QVQ_MF_THREADS;       // 16 waves (4 per SIMD), one workgroup per CU
 constexpr int MF_WAVES = MF_THREADS / 64;
 constexpr int MF_TILES = 4;                      // 16-row data tiles per wave and chunk
 constexpr int MF_ROWS = 16 * MF_TILES;           // rows per wave and chunk
@@ -139,9 +145,9 @@ __global__ __launch_bounds__(MF_THREADS) void assign_mfma_kernel(
         for (uint32_t i = tid; i < K * MF_D; i += MF_THREADS) sums[i] = 0;
         for (uint32_t i = tid; i < K; i += MF_THREADS) cnt[i] = 0;
         if (tid < 256) lo8[tid] = (uint8_t)(g_plut[tid] & 0xFF);
-        if (blockIdx.x == 0) {   // the extra slab G (recheck / tie rows), after all G others
-            for (uint32_t i = tid; i < K * MF_D; i += MF_THREADS) part[(uint64_t)gridDim.x * K * MF_D + i] = 0;
-            for (uint32_t i = tid; i < K; i += MF_THREADS) part_cnt[(uint64_t)gridDim.x * K + i] = 0;
+        if (blockIdx.x == 0) {   // the correction slabs G (+) and G + 1 (-), after all G others
+            for (uint32_t i = tid; i < 2 * K * MF_D; i += MF_THREADS) part[(uint64_t)gridDim.x * K * MF_D + i] = 0;
+            for (uint32_t i = tid; i < 2 * K; i += MF_THREADS) part_cnt[(uint64_t)gridDim.x * K + i] = 0;
         }
     }
     __syncthreads();
@@ -166,19 +172,18 @@ __global__ __launch_bounds__(MF_THREADS) void assign_mfma_kernel(
         const u64x2 v = {p[0], p[1]};
         return __builtin_bit_cast(half8, v);
     };
+    // Branch-free: rows past N read row N - 1 (their results are never written).  A load
+    // under a branch gets an s_waitcnt vmcnt(0) at the join, which would void the prefetch.
     auto load_codes = [&](uint64_t chunk, uint32_t (&q)[MF_TILES][3]) {
 #pragma unroll
         for (int t = 0; t < (SMALLK ? 1 : MF_TILES); t++) {
             // SMALLK: only the lane's own row (base + lane), in q[0]
-            const uint64_t row = SMALLK ? chunk * MF_ROWS + lane : chunk * MF_ROWS + t * 16 + c;
-            if (chunk < nchunks && row < N) {
-                const uint32_t *p = reinterpret_cast<const uint32_t *>(codes + row * MF_D);
-                q[t][0] = p[0];
-                q[t][1] = p[1];
-                q[t][2] = p[2];
-            } else {
-                q[t][0] = q[t][1] = q[t][2] = 0x80808080u;
-            }
+            uint64_t row = SMALLK ? chunk * MF_ROWS + lane : chunk * MF_ROWS + t * 16 + c;
+            row = row < N ? row : N - 1;
+            const uint32_t *p = reinterpret_cast<const uint32_t *>(codes + row * MF_D);
+            q[t][0] = p[0];
+            q[t][1] = p[1];
+            q[t][2] = p[2];
         }
     };
 
@@ -227,6 +232,83 @@ __global__ __launch_bounds__(MF_THREADS) void assign_mfma_kernel(
             b2[t] = INFINITY;
             bp[t] = 0;
         }
+#if QVQ_MF_LOOP == 2
+        // Tile pairs, ping-pong: the MFMAs of pair i overlap the epilogue of pair i-1, and
+        // the A fragments of pair i+1 are read from LDS under them.  Unrolled by two so the
+        // two accumulator sets alternate roles without register copies.
+        f32x4 pa0[MF_TILES], pa1[MF_TILES], qa0[MF_TILES], qa1[MF_TILES];
+        half8 a0 = load_a(0), a1 = load_a(1);
+        auto mfma_pair = [&](f32x4 (&r0)[MF_TILES], f32x4 (&r1)[MF_TILES]) {
+#pragma unroll
+            for (int t = 0; t < MF_TILES; t++) {
+                r0[t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a0, b[t], zero, 0, 0, 0);
+                r1[t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a1, b[t], zero, 0, 0, 0);
+            }
+        };
+        auto next_a = [&](uint32_t pr) {   // fragments of pair pr (clamped: the last is re-read)
+            const uint32_t p = pr < npairs ? pr : npairs - 1;
+            a0 = load_a(2 * p);
+            a1 = load_a(2 * p + 1);
+        };
+        mfma_pair(pa0, pa1);
+        next_a(1);
+        uint32_t pr = 1;
+        for (; pr + 1 < npairs; pr += 2) {
+            mfma_pair(qa0, qa1);
+            next_a(pr + 1);
+#pragma unroll
+            for (int t = 0; t < MF_TILES; t++) pair_update(pa0[t], pa1[t], pr - 1, b1[t], b2[t], bp[t]);
+            mfma_pair(pa0, pa1);
+            next_a(pr + 2);
+#pragma unroll
+            for (int t = 0; t < MF_TILES; t++) pair_update(qa0[t], qa1[t], pr, b1[t], b2[t], bp[t]);
+        }
+        if (pr < npairs) {   // npairs even: one pair left
+            mfma_pair(qa0, qa1);
+#pragma unroll
+            for (int t = 0; t < MF_TILES; t++) pair_update(pa0[t], pa1[t], pr - 1, b1[t], b2[t], bp[t]);
+#pragma unroll
+            for (int t = 0; t < MF_TILES; t++) pair_update(qa0[t], qa1[t], pr, b1[t], b2[t], bp[t]);
+        } else {
+#pragma unroll
+            for (int t = 0; t < MF_TILES; t++) pair_update(pa0[t], pa1[t], pr - 1, b1[t], b2[t], bp[t]);
+        }
+
+#elif QVQ_MF_LOOP == 1
+        // Tile pairs, ping-pong: the MFMAs of pair i overlap the epilogue of pair i-1, and
+        // the A fragments of pair i+1 are read from LDS under them.
+        f32x4 pa0[MF_TILES], pa1[MF_TILES];
+        half8 a0 = load_a(0), a1 = load_a(1);
+#pragma unroll
+        for (int t = 0; t < MF_TILES; t++) {
+            pa0[t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a0, b[t], zero, 0, 0, 0);
+            pa1[t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a1, b[t], zero, 0, 0, 0);
+        }
+        a0 = load_a(2);
+        a1 = load_a(3);
+        for (uint32_t pr = 1; pr < npairs; pr++) {
+            f32x4 qa0[MF_TILES], qa1[MF_TILES];
+#pragma unroll
+            for (int t = 0; t < MF_TILES; t++) {
+                qa0[t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a0, b[t], zero, 0, 0, 0);
+                qa1[t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a1, b[t], zero, 0, 0, 0);
+            }
+            // next pair's fragments (the last pair re-reads itself)
+            const uint32_t pn = pr + 1 < npairs ? pr + 1 : pr;
+            a0 = load_a(2 * pn);
+            a1 = load_a(2 * pn + 1);
+#pragma unroll
+            for (int t = 0; t < MF_TILES; t++) pair_update(pa0[t], pa1[t], pr - 1, b1[t], b2[t], bp[t]);
+#pragma unroll
+            for (int t = 0; t < MF_TILES; t++) {
+                pa0[t] = qa0[t];
+                pa1[t] = qa1[t];
+            }
+        }
+#pragma unroll
+        for (int t = 0; t < MF_TILES; t++) pair_update(pa0[t], pa1[t], npairs - 1, b1[t], b2[t], bp[t]);
+
+#else
         // Tile pairs, ping-pong: the MFMAs of pair i overlap the epilogue of pair i-1.
         f32x4 pa0[MF_TILES], pa1[MF_TILES];
         {
@@ -256,6 +338,7 @@ __global__ __launch_bounds__(MF_THREADS) void assign_mfma_kernel(
 #pragma unroll
         for (int t = 0; t < MF_TILES; t++) pair_update(pa0[t], pa1[t], npairs - 1, b1[t], b2[t], bp[t]);
 
+#endif
         // Combine the four lanes of each data row on MFMA values: winning (pair, group) and
         // the second-best minimum among all other candidates.
         uint32_t wsel[MF_TILES];   // 8-code-vector unit: pair*4 + g
@@ -332,10 +415,12 @@ __global__ __launch_bounds__(MF_THREADS) void assign_mfma_kernel(
             if (flagged) flags[atomicAdd(flag_cnt, 1u)] = (uint32_t)row;
         }
         if (FUSE) {
-            const bool take = valid && !flagged;
-            if (K <= 64) {
-                // few code vectors: long runs of equal codes along consecutive rows; fold
-                // each run in registers first, one lane per run adds to LDS.
+            // every row at its provisional index; the recheck / kd-tree moves re-assigned ones
+            const bool take = valid;
+            if (K <= th.runs_max_k) {
+                // runs of equal codes along consecutive rows (adjacent blocks): fold each run
+                // in registers first, one lane per run adds to LDS (fewer LDS atomics, and
+                // no same-address ones within a run).
                 uint32_t v[MF_D + 1];
 #pragma unroll
                 for (int d = 0; d < MF_D; d++) {
@@ -374,41 +459,53 @@ __global__ __launch_bounds__(MF_THREADS) void assign_mfma_kernel(
 
 // ---------------------------------------------------------------------------------------
 // Small codebooks (K <= MF_SMALL_K): direct fp32 scan of all SK code vectors per row, rows in
-// per-lane runs.  Each wave owns a contiguous range of rows and each lane a contiguous
-// sub-range (a multiple of 4 rows, loaded 48 bytes at a time), so at small K consecutive rows
-// of a lane mostly share their code vector: their exact terms (u << 16 | lo per component,
-// no carry within 256 rows) are added in registers and go to the LDS sums only when the
-// index changes.  Flag rule and sums as in assign_mfma_kernel.
+// per-lane runs.  Each wave owns a contiguous range of rows; lane L takes every 64th row of
+// it (coalesced loads and stores), four rows per iteration.  At small K a lane's consecutive
+// rows (64 blocks apart in the image) mostly share their code vector: their exact terms
+// (u << 16 | lo per component, no carry within 256 rows) are added in registers and go to the
+// LDS sums only when the index changes.  Flag rule and sums as in assign_mfma_kernel.
 // ---------------------------------------------------------------------------------------
+__host__ __device__ constexpr uint32_t small_copy_stride(uint32_t SK) { return SK * (MF_D + 1) + 1; }
+// Copies of the small kernel's sums: up to 64 (one per lane) while they fit ~112 KB of LDS.
+static uint32_t small_copies(uint32_t SK) {
+    uint32_t C = 64;
+    while (C > 1 && (size_t)C * small_copy_stride(SK) * 8 + 256 > MF_LDS_MAX / 2 + 32 * 1024) C /= 2;
+    return C;
+}
+static size_t small_lds(uint32_t SK, uint32_t C) { return (size_t)C * small_copy_stride(SK) * 8 + 256; }
+
 template <int SK, bool FUSE>
 __global__ __launch_bounds__(MF_THREADS) void assign_small_kernel(
     const uint8_t *__restrict__ codes, uint64_t N, uint32_t K, const float *__restrict__ g_C32,
-    const uint64_t *__restrict__ g_plut, MfThresholds th, uint64_t rows_per_lane, uint32_t *__restrict__ A,
-    uint32_t *__restrict__ flags, unsigned *__restrict__ flag_cnt, uint64_t *__restrict__ part,
-    uint32_t *__restrict__ part_cnt) {
+    const uint64_t *__restrict__ g_plut, MfThresholds th, uint64_t rows_per_lane, uint32_t copies,
+    uint32_t *__restrict__ A, uint32_t *__restrict__ flags, unsigned *__restrict__ flag_cnt,
+    uint64_t *__restrict__ part, uint32_t *__restrict__ part_cnt) {
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
-    const MfLds L = mf_lds_layout(K, FUSE, true);
-    float *c32s = reinterpret_cast<float *>(lds + L.c32);
-    uint64_t *sums = reinterpret_cast<uint64_t *>(lds + L.sums);   // [d][k]
-    uint32_t *cnt = reinterpret_cast<uint32_t *>(lds + L.cnt);
-    uint8_t *lo8 = lds + L.plut;   // low part of each byte's exact term (high part: b ^ 0x80)
+    // LDS: C copies of the sums, copy c = [d][k] (SK*D u64) then counts [k] (SK u64), stride
+    // S = SK*(D+1) + 1 (odd: the copies of 16 consecutive lanes sit on different banks) | lo8.
+    // SK-strided, so a flush addresses copy + d*SK + cur with immediate offsets.
+    // Lane L flushes into copy L mod C, so the flushes of a wave's lanes -- all at once at
+    // the end, mostly to the same code vector at small K -- rarely hit one address.
+    constexpr uint32_t S = small_copy_stride(SK);
+    uint64_t *cps = reinterpret_cast<uint64_t *>(lds);
+    uint8_t *lo8 = lds + (size_t)copies * S * 8;   // low part of each byte's exact term (high part: b ^ 0x80)
     const int tid = threadIdx.x;
-    for (uint32_t i = tid; i < (uint32_t)SK * (MF_D / 4); i += MF_THREADS)
-        reinterpret_cast<float4 *>(c32s)[i] = reinterpret_cast<const float4 *>(g_C32)[i];
     if (FUSE) {
-        for (uint32_t i = tid; i < K * MF_D; i += MF_THREADS) sums[i] = 0;
-        for (uint32_t i = tid; i < K; i += MF_THREADS) cnt[i] = 0;
+        for (uint32_t i = tid; i < copies * S; i += MF_THREADS) cps[i] = 0;
         if (tid < 256) lo8[tid] = (uint8_t)(g_plut[tid] & 0xFF);
-        if (blockIdx.x == 0) {   // the extra slab G (recheck / tie rows), after all G others
-            for (uint32_t i = tid; i < K * MF_D; i += MF_THREADS) part[(uint64_t)gridDim.x * K * MF_D + i] = 0;
-            for (uint32_t i = tid; i < K; i += MF_THREADS) part_cnt[(uint64_t)gridDim.x * K + i] = 0;
+        if (blockIdx.x == 0) {   // the correction slabs G (+) and G + 1 (-), after all G others
+            for (uint32_t i = tid; i < 2 * K * MF_D; i += MF_THREADS) part[(uint64_t)gridDim.x * K * MF_D + i] = 0;
+            for (uint32_t i = tid; i < 2 * K; i += MF_THREADS) part_cnt[(uint64_t)gridDim.x * K + i] = 0;
         }
     }
     __syncthreads();
+    uint64_t *mine = cps + (size_t)((tid & 63) % copies) * S;
 
     const int lane = tid & 63, wave = tid >> 6;
-    const uint64_t first = ((uint64_t)blockIdx.x * MF_WAVES + wave) * 64 * rows_per_lane + lane * rows_per_lane;
-    const uint64_t last = min(first + rows_per_lane, N);
+    // The wave owns rows [wbase, wend); lane L takes rows wbase + L + 64 t, so every load and
+    // store instruction of the wave covers 64 consecutive rows (768 contiguous bytes).
+    const uint64_t wbase = ((uint64_t)blockIdx.x * MF_WAVES + wave) * 64 * rows_per_lane;
+    const uint64_t wend = min(wbase + 64 * rows_per_lane, N);
     uint32_t acc[MF_D + 1];
     uint32_t cur = 0xFFFFFFFFu;
 #pragma unroll
@@ -417,41 +514,28 @@ __global__ __launch_bounds__(MF_THREADS) void assign_small_kernel(
         if (cur != 0xFFFFFFFFu && acc[MF_D]) {
 #pragma unroll
             for (int d = 0; d < MF_D; d++)
-                atomicAdd((unsigned long long *)&sums[(uint32_t)d * K + cur],
+                atomicAdd((unsigned long long *)&mine[d * SK + cur],
                           (unsigned long long)((((uint64_t)(acc[d] >> 16)) << 32) | (acc[d] & 0xFFFF)));
-            atomicAdd(&cnt[cur], acc[MF_D]);
+            atomicAdd((unsigned long long *)&mine[MF_D * SK + cur], (unsigned long long)acc[MF_D]);
         }
 #pragma unroll
         for (int i = 0; i <= MF_D; i++) acc[i] = 0;
     };
-    // the next four rows' words are loaded one iteration ahead
+    // four rows of this lane (base + 64 r), two iterations ahead; branch-free (rows past N
+    // read row N - 1 and are masked later), so the loads stay in flight across iterations
     auto load4 = [&](uint64_t r0, uint32_t (&w)[4][3]) {
-        if (r0 + 4 <= last) {
-            const uint4 *p = reinterpret_cast<const uint4 *>(codes + r0 * MF_D);
-            const uint4 a = p[0], b = p[1], c = p[2];
-            const uint32_t v[12] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w, c.x, c.y, c.z, c.w};
 #pragma unroll
-            for (int r = 0; r < 4; r++)
-#pragma unroll
-                for (int i = 0; i < 3; i++) w[r][i] = v[3 * r + i];
-        } else {
-#pragma unroll
-            for (int r = 0; r < 4; r++)
-#pragma unroll
-                for (int i = 0; i < 3; i++)
-                    w[r][i] = r0 + r < last ? reinterpret_cast<const uint32_t *>(codes + (r0 + r) * MF_D)[i]
-                                            : 0x80808080u;
+        for (int r = 0; r < 4; r++) {
+            uint64_t row = r0 + 64 * r;
+            row = row < N ? row : N - 1;
+            const uint32_t *p = reinterpret_cast<const uint32_t *>(codes + row * MF_D);
+            w[r][0] = p[0];
+            w[r][1] = p[1];
+            w[r][2] = p[2];
         }
     };
-    uint32_t wn[4][3];
-    load4(first, wn);
-    for (uint64_t r0 = first; r0 < last; r0 += 4) {
-        uint32_t w[4][3];
-#pragma unroll
-        for (int r = 0; r < 4; r++)
-#pragma unroll
-            for (int i = 0; i < 3; i++) w[r][i] = wn[r][i];
-        if (r0 + 4 < last) load4(r0 + 4, wn);
+    // Rows r0 + 64 r (r < 4) of this lane, their words in w.
+    auto process = [&](const uint32_t (&w)[4][3], uint64_t r0) {
         // four rows at once: each code vector's 12 values are loaded once (scalar) for all
         // four, and the four distance chains are independent
         float x[4][MF_D];
@@ -491,13 +575,13 @@ __global__ __launch_bounds__(MF_THREADS) void assign_small_kernel(
         }
 #pragma unroll
         for (int r = 0; r < 4; r++) {
-            const uint64_t row = r0 + r;
+            const uint64_t row = r0 + 64 * r;
             const uint32_t rk = idx[r];
             const float thr = 2.f * (th.alpha * sqrtf(r2[r]) + th.beta * r2[r]) + th.gamma;
-            const bool valid = row < last;
+            const bool valid = row < wend;
             const bool flagged = valid && !(r2[r] - r1[r] > thr);
             if (flagged) flags[atomicAdd(flag_cnt, 1u)] = (uint32_t)row;
-            if (FUSE && valid && !flagged) {
+            if (FUSE && valid) {   // provisional index, as in assign_mfma_kernel
                 if (rk != cur || acc[MF_D] == 256) {   // 16-bit fields hold 256 rows
                     flush();
                     cur = rk;
@@ -510,21 +594,34 @@ __global__ __launch_bounds__(MF_THREADS) void assign_small_kernel(
                 acc[MF_D] += 1;
             }
         }
-        if (r0 + 4 <= last) {
-            *reinterpret_cast<uint4 *>(A + r0) = make_uint4(idx[0], idx[1], idx[2], idx[3]);
-        } else {
 #pragma unroll
-            for (int r = 0; r < 4; r++)
-                if (r0 + r < last) A[r0 + r] = idx[r];
-        }
+        for (int r = 0; r < 4; r++)
+            if (r0 + 64 * r < wend) A[r0 + 64 * r] = idx[r];
+    };
+    // Two row groups per trip, each group's words loaded one group ahead into the other
+    // buffer (no register copies, so the loads stay in flight under the previous group).
+    // The trip count is wave-uniform; rows past wend are masked inside process.
+    uint32_t wa[4][3], wb[4][3];
+    load4(wbase + lane, wa);
+    for (uint64_t ru = wbase; ru < wend; ru += 512) {
+        load4(ru + 256 + lane, wb);
+        process(wa, ru + lane);
+        if (ru + 256 >= wend) break;
+        load4(ru + 512 + lane, wa);
+        process(wb, ru + 256 + lane);
     }
     if (FUSE) {
         flush();
         __syncthreads();
         uint64_t *pdst = part + (uint64_t)blockIdx.x * K * MF_D;   // slab layout [d][k]
-        for (uint32_t i = tid; i < K * MF_D; i += MF_THREADS) pdst[i] = sums[i];
         uint32_t *cdst = part_cnt + (uint64_t)blockIdx.x * K;
-        for (uint32_t i = tid; i < K; i += MF_THREADS) cdst[i] = cnt[i];
+        for (uint32_t i = tid; i < K * (MF_D + 1); i += MF_THREADS) {   // [d][k] of the slab
+            const uint32_t d = i / K, k = i - d * K;
+            uint64_t v = 0;
+            for (uint32_t c = 0; c < copies; c++) v += cps[(size_t)c * S + d * SK + k];
+            if (d < MF_D) pdst[i] = v;
+            else cdst[k] = (uint32_t)v;
+        }
     }
 }
 
@@ -559,15 +656,16 @@ hipError_t launch_assign_mfma(hipStream_t s, int grid, bool fuse, const uint8_t 
         // rows per lane: a multiple of 4 covering N over grid x 16 waves x 64 lanes
         const uint64_t lanes = (uint64_t)grid * MF_WAVES * 64;
         const uint64_t rpl = ((N + lanes - 1) / lanes + 3) / 4 * 4;
-        const size_t slds = mf_lds_layout(K, fuse, true).total;
+        const uint32_t copies = fuse ? small_copies(sk) : 1;
+        const size_t slds = fuse ? small_lds(sk, copies) : 256;
 #define QVQ_SMALL(V)                                                                                              \
     do {                                                                                                          \
         if (fuse)                                                                                                 \
             hipLaunchKernelGGL((assign_small_kernel<V, true>), dim3(grid), dim3(MF_THREADS), slds, s, codes, N, K, \
-                               C32, plut, th, rpl, A, flags, flag_cnt, part, part_cnt);                          \
+                               C32, plut, th, rpl, copies, A, flags, flag_cnt, part, part_cnt);                  \
         else                                                                                                      \
             hipLaunchKernelGGL((assign_small_kernel<V, false>), dim3(grid), dim3(MF_THREADS), slds, s, codes, N,  \
-                               K, C32, plut, th, rpl, A, flags, flag_cnt, part, part_cnt);                        \
+                               K, C32, plut, th, rpl, copies, A, flags, flag_cnt, part, part_cnt);                \
     } while (0)
         switch (sk) {
         case 2: QVQ_SMALL(2); break;
@@ -765,6 +863,19 @@ __device__ inline float d32_row(const float *__restrict__ xr, const float *__res
     return acc;   // padding components are 0 in both x and c
 }
 
+// LDS written by some lanes of a wave and then read by others: order the accesses.
+__device__ inline void wave_lds_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// LDS: byte LUT (256 doubles) | per wave the fp64 row and the fp32 row | staged fp32 codebook.
+constexpr size_t RECHECK_LDS_BASE = 256 * 8 + (size_t)RECHECK_WAVES * 64 * 12;
+
+// Each wave takes flagged rows f = wave id, + all waves, ...; rows are wave-private (no
+// block-wide barrier after the staging).  The flag index is fetched two rows ahead and the
+// row's bytes one row ahead, so the dependent chain flags -> codes never stalls a row.
 template <bool STAGED, int DT>
 __global__ __launch_bounds__(RECHECK_THREADS) void recheck_kernel(
     const uint8_t *__restrict__ codes, uint32_t Dp, uint32_t D, const uint32_t *__restrict__ flags,
@@ -774,46 +885,73 @@ __global__ __launch_bounds__(RECHECK_THREADS) void recheck_kernel(
     uint64_t *__restrict__ xslab, uint32_t *__restrict__ xcnt, const uint64_t *__restrict__ plut) {
     extern __shared__ __attribute__((aligned(16))) double rsm[];
     constexpr int W = RECHECK_WAVES;
-    double *xs = rsm;                                              // [W][64] fp64 row
-    float *x32 = reinterpret_cast<float *>(rsm + W * 64);          // [W][64] fp32 row (zero padded)
+    double *lut = rsm;                                             // [256] exact byte values
+    double *xs = rsm + 256;                                        // [W][64] fp64 row
+    float *x32 = reinterpret_cast<float *>(xs + W * 64);           // [W][64] fp32 row (zero padded)
     float *c32s = x32 + W * 64;                                    // [K][CS] when staged
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const unsigned nflag = *flag_cnt;
     if (nflag == 0 || blockIdx.x * W >= nflag) return;
     const uint32_t CS = STAGED ? recheck_c32_stride(Dp) : Dp;
+    const unsigned fstride = gridDim.x * W;
+    unsigned f = blockIdx.x * W + wave;
+    // two-deep prefetch: row index of f + fstride, bytes of row f
+    uint32_t row = f < nflag ? flags[f] : 0;
+    uint32_t byte = (f < nflag && lane < (int)D) ? codes[(uint64_t)row * Dp + lane] : 0;
+    uint32_t row_n = f + fstride < nflag ? flags[f + fstride] : 0;
+    for (uint32_t i = threadIdx.x; i < 256; i += RECHECK_THREADS) lut[i] = lut64[i];
     if (STAGED) {
         for (uint32_t i = threadIdx.x; i < K * (Dp / 4); i += RECHECK_THREADS) {
             const uint32_t k = i / (Dp / 4), q = i - k * (Dp / 4);
             reinterpret_cast<float4 *>(c32s + (size_t)k * CS)[q] = reinterpret_cast<const float4 *>(g_C32)[i];
         }
-        __syncthreads();
     }
+    __syncthreads();
     const float *C32 = STAGED ? c32s : g_C32;
-    for (unsigned base = blockIdx.x * W; base < nflag; base += gridDim.x * W) {
-        const unsigned f = base + wave;
-        const bool active = f < nflag;
-        const uint32_t row = active ? flags[f] : 0;
-        __syncthreads();
-        if (active) {
-            const double v = lane < (int)D ? lut64[codes[(uint64_t)row * Dp + lane]] : 0.0;
-            xs[wave * 64 + lane] = v;
-            x32[wave * 64 + lane] = (float)v;
+    double *xw = xs + wave * 64;
+    float *xr = x32 + wave * 64;
+    auto within = [&](float d, float m) { return d - m <= 2.f * (alpha * sqrtf(d) + beta * d) + gamma; };
+    for (; f < nflag; f += fstride) {
+        const uint32_t crow = row, cbyte = byte;
+        row = row_n;
+        byte = (f + fstride < nflag && lane < (int)D) ? codes[(uint64_t)row * Dp + lane] : 0;
+        row_n = f + 2 * fstride < nflag ? flags[f + 2 * fstride] : 0;
+        const double v = lane < (int)D ? lut[cbyte] : 0.0;
+        xw[lane] = v;
+        xr[lane] = (float)v;
+        wave_lds_sync();
+        // fp32 direct distance to code vector k: the row in registers for a known width
+        constexpr int NQ = DT > 0 ? (DT + 3) / 4 : 1;
+        float4 xq[NQ];
+        if constexpr (DT > 0) {
+#pragma unroll
+            for (int q = 0; q < NQ; q++) xq[q] = reinterpret_cast<const float4 *>(xr)[q];
         }
-        __syncthreads();
-        if (!active) continue;
-        const float *xr = x32 + wave * 64;
-        auto within = [&](float d, float m) { return d - m <= 2.f * (alpha * sqrtf(d) + beta * d) + gamma; };
+        auto d32 = [&](uint32_t k) -> float {
+            if constexpr (DT > 0) {
+                const float4 *c4 = reinterpret_cast<const float4 *>(C32 + (size_t)k * CS);
+                float acc = 0.f;
+#pragma unroll
+                for (int q = 0; q < NQ; q++) {
+                    const float4 cq = c4[q];
+                    float e;
+                    e = xq[q].x - cq.x; acc = __fmaf_rn(e, e, acc);
+                    e = xq[q].y - cq.y; acc = __fmaf_rn(e, e, acc);
+                    e = xq[q].z - cq.z; acc = __fmaf_rn(e, e, acc);
+                    e = xq[q].w - cq.w; acc = __fmaf_rn(e, e, acc);
+                }
+                return acc;
+            } else {
+                return d32_row<0>(xr, C32 + (size_t)k * CS, Dp);
+            }
+        };
         float b1 = INFINITY, b2 = INFINITY;
         uint32_t kb = 0;
         for (uint32_t k = lane; k < K; k += 64) {
-            const float d = d32_row<DT>(xr, C32 + (size_t)k * CS, Dp);
-            if (d < b1) {
-                b2 = b1;
-                b1 = d;
-                kb = k;
-            } else if (d < b2) {
-                b2 = d;
-            }
+            const float d = d32(k);
+            b2 = med3f(b1, b2, d);
+            kb = d < b1 ? k : kb;
+            b1 = min2f(b1, d);
         }
         float m = b1;
 #pragma unroll
@@ -821,7 +959,7 @@ __global__ __launch_bounds__(RECHECK_THREADS) void recheck_kernel(
         double d1 = INFINITY, d2 = INFINITY;
         uint32_t k1 = 0xFFFFFFFFu;
         auto take = [&](uint32_t k) {
-            const double d = ref_l2_hd(xs + wave * 64, C64 + (uint64_t)k * D, D);
+            const double d = ref_l2_hd(xw, C64 + (uint64_t)k * D, D);
             if (d < d1 || (d == d1 && k < k1)) {
                 d2 = d1;
                 d1 = d;
@@ -832,7 +970,7 @@ __global__ __launch_bounds__(RECHECK_THREADS) void recheck_kernel(
         };
         if (within(b2, m)) {   // rare: more than one candidate on this lane
             for (uint32_t k = lane; k < K; k += 64)
-                if (within(d32_row<DT>(xr, C32 + (size_t)k * CS, Dp), m)) take(k);
+                if (within(d32(k), m)) take(k);
         } else if (within(b1, m)) {
             take(kb);
         }
@@ -849,16 +987,17 @@ __global__ __launch_bounds__(RECHECK_THREADS) void recheck_kernel(
                 d2 = fmin(d2, od1);
             }
         }
-        if (lane == 0) A[row] = k1;
-        if (d2 - d1 <= tie_rel * d1) {
-            if (lane == 0) ties[atomicAdd(tie_cnt, 1u)] = row;
-            continue;
+        if (d2 - d1 <= tie_rel * d1) {   // exact tie for the reference: the kd-tree decides
+            if (lane == 0) ties[atomicAdd(tie_cnt, 1u)] = crow;   // A keeps the provisional index
+        } else {
+            // the search's index (its terms are in the slabs when fused); mostly unchanged
+            const uint32_t from = __builtin_amdgcn_readfirstlane(A[crow]);
+            if (k1 != from) {
+                if (xslab) move_row_terms(codes, Dp, D, crow, from, k1, K, xslab, xcnt, plut, lane);
+                if (lane == 0) A[crow] = k1;
+            }
         }
-        if (xslab && lane < (int)D) {   // the extra slab: packed hi << 32 | lo, and counts
-            atomicAdd((unsigned long long *)&xslab[(uint64_t)lane * K + k1],
-                      (unsigned long long)plut[codes[(uint64_t)row * Dp + lane]]);
-            if (lane == 0) atomicAdd(&xcnt[k1], 1u);
-        }
+        wave_lds_sync();   // this row's reads of xw / xr before the next row's writes
     }
 }
 
@@ -878,7 +1017,7 @@ hipError_t launch_recheck(hipStream_t s, int num_cu, const uint8_t *codes, uint3
                           uint32_t *A, uint32_t *ties, unsigned *tie_cnt, uint64_t *xslab, uint32_t *xcnt,
                           const uint64_t *plut) {
     if (Dp % 4 || Dp > 64) return hipErrorInvalidValue;
-    const size_t base = (size_t)RECHECK_WAVES * 64 * 12;
+    const size_t base = RECHECK_LDS_BASE;
     const size_t cb = (size_t)K * recheck_c32_stride(Dp) * 4;
     const bool staged = base + cb <= RECHECK_LDS;
     const size_t lds = base + (staged ? cb : 0);
@@ -1000,13 +1139,6 @@ __device__ uint32_t kd_nearest_wave(const double *q, uint32_t D, const KdView &t
 // Exact ties listed by the recheck, answered by the reference kd-tree traversal
 // (kd_nearest_flat).  The tree image (kd.lo .. ) lives in mapped pinned host memory and is
 // staged into LDS by each block that has tie rows; one lane per wave walks it.
-// LDS written by some lanes of a wave and then read by others: order the accesses.
-__device__ inline void wave_lds_sync() {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
-
 constexpr int KDR_MAX_WAVES = 16;
 constexpr int KDR_BLOCKS = 16;
 
@@ -1040,7 +1172,26 @@ __global__ __launch_bounds__(KDR_MAX_WAVES * 64) void kd_resolve_kernel(
     double *sd = wb + 128;
     int32_t *sn = reinterpret_cast<int32_t *>(sd + Z);
     double *pv = wb + 128 + ((size_t)Z * KD_FRAME_BYTES + 7) / 8;   // [K] distances in vind order
-    for (uint32_t i = threadIdx.x; i < (kd.bytes + 7) / 8; i += blockDim.x) tr[i] = kd.lo[i];
+    {   // stage the tree image: 16-byte loads, eight in flight per lane (one round trip over
+        // PCIe when the image is read in place from mapped host memory)
+        const uint4 *src = reinterpret_cast<const uint4 *>(kd.lo);
+        uint4 *dst = reinterpret_cast<uint4 *>(tr);
+        const uint32_t n16 = kd.bytes / 16;
+        constexpr int U = 8;
+        for (uint32_t i0 = threadIdx.x; i0 < n16; i0 += U * blockDim.x) {
+            uint4 v[U];
+#pragma unroll
+            for (int u = 0; u < U; u++)
+                if (i0 + u * blockDim.x < n16) v[u] = src[i0 + u * blockDim.x];
+#pragma unroll
+            for (int u = 0; u < U; u++)
+                if (i0 + u * blockDim.x < n16) dst[i0 + u * blockDim.x] = v[u];
+        }
+        const uint32_t tail = (kd.bytes & 15) / 4;   // the image is a whole number of dwords
+        if (threadIdx.x < tail)
+            reinterpret_cast<uint32_t *>(tr)[n16 * 4 + threadIdx.x] =
+                reinterpret_cast<const uint32_t *>(kd.lo)[n16 * 4 + threadIdx.x];
+    }
     KdView kv = kd;
     kv.lo = tr;
     kv.hi = tr + D;
@@ -1054,11 +1205,10 @@ __global__ __launch_bounds__(KDR_MAX_WAVES * 64) void kd_resolve_kernel(
         for (uint32_t j = lane; j < K; j += 64) pv[j] = ref_l2_hd(xs, C64 + (uint64_t)kv.vind[j] * D, (int)D);
         wave_lds_sync();
         const uint32_t k = kd_nearest_wave(xs, D, kv, pv, sd, sn, dl, lane);
-        if (lane == 0) A[row] = k;
-        if (xslab && lane < (int)D) {
-            atomicAdd((unsigned long long *)&xslab[(uint64_t)lane * K + k],
-                      (unsigned long long)plut[codes[(uint64_t)row * Dp + lane]]);
-            if (lane == 0) atomicAdd(&xcnt[k], 1u);
+        const uint32_t from = __builtin_amdgcn_readfirstlane(A[row]);   // the search's index
+        if (k != from) {
+            if (xslab) move_row_terms(codes, Dp, D, row, from, k, K, xslab, xcnt, plut, lane);
+            if (lane == 0) A[row] = k;
         }
         wave_lds_sync();
     }

@@ -272,11 +272,14 @@ hipError_t launch_update(hipStream_t s, uint32_t Dp, uint32_t G, const uint8_t *
 }
 
 // Column reduce of G slabs into sums (layout in the file header).  A workgroup owns 64
-// columns; its 16 waves each add every 16th slab, then combine through LDS.
+// columns; its 16 waves each add every 16th slab, then combine through LDS.  The last nsub
+// slabs are subtracted (hi and lo separately: the corrections of re-assigned rows, whose
+// terms the search had added at their provisional index); every total stays >= 0.
 constexpr int REDUCE_THREADS = 1024;
 __global__ __launch_bounds__(REDUCE_THREADS) void reduce_kernel(const uint64_t *__restrict__ part,
                                                                 const uint32_t *__restrict__ part_cnt, uint32_t G,
-                                                                uint32_t K, uint32_t D, uint64_t *__restrict__ sums) {
+                                                                uint32_t nsub, uint32_t K, uint32_t D,
+                                                                uint64_t *__restrict__ sums) {
     __shared__ uint64_t red_hi[16][64], red_lo[16][64];
     const uint64_t KD = (uint64_t)K * D;
     const uint64_t col = (uint64_t)blockIdx.x * 64 + (threadIdx.x & 63);
@@ -286,12 +289,16 @@ __global__ __launch_bounds__(REDUCE_THREADS) void reduce_kernel(const uint64_t *
 #pragma unroll 4
         for (uint32_t g = sg; g < G; g += 16) {
             const uint64_t p = part[g * KD + col];
-            hi += p >> 32;
-            lo += p & 0xFFFFFFFFull;
+            const uint64_t sgn = g < G - nsub ? 0 : ~0ull;   // x ^ sgn - sgn: +x or -x (mod 2^64)
+            hi += ((p >> 32) ^ sgn) - sgn;
+            lo += ((p & 0xFFFFFFFFull) ^ sgn) - sgn;
         }
     } else if (col < KD + K) {
 #pragma unroll 4
-        for (uint32_t g = sg; g < G; g += 16) hi += part_cnt[(uint64_t)g * K + (col - KD)];
+        for (uint32_t g = sg; g < G; g += 16) {
+            const uint64_t c = part_cnt[(uint64_t)g * K + (col - KD)];
+            hi += g < G - nsub ? c : 0ull - c;
+        }
     }
     red_hi[sg][threadIdx.x & 63] = hi;
     red_lo[sg][threadIdx.x & 63] = lo;
@@ -310,11 +317,12 @@ __global__ __launch_bounds__(REDUCE_THREADS) void reduce_kernel(const uint64_t *
     }
 }
 
-hipError_t launch_reduce(hipStream_t s, const uint64_t *part, const uint32_t *part_cnt, uint32_t G, uint32_t K,
-                         uint32_t D, uint64_t *sums) {
+hipError_t launch_reduce(hipStream_t s, const uint64_t *part, const uint32_t *part_cnt, uint32_t G, uint32_t nsub,
+                         uint32_t K, uint32_t D, uint64_t *sums) {
+    if (nsub > G) return hipErrorInvalidValue;
     const uint64_t cols = (uint64_t)K * D + K;
-    hipLaunchKernelGGL(reduce_kernel, dim3((int)((cols + 63) / 64)), dim3(REDUCE_THREADS), 0, s, part, part_cnt, G, K,
-                       D, sums);
+    hipLaunchKernelGGL(reduce_kernel, dim3((int)((cols + 63) / 64)), dim3(REDUCE_THREADS), 0, s, part, part_cnt, G,
+                       nsub, K, D, sums);
     return hipGetLastError();
 }
 
@@ -638,28 +646,30 @@ hipError_t launch_gather_codes(hipStream_t s, const uint8_t *codes, uint32_t Dp,
 }
 
 // A[rows[i]] = vals[i] (host tie resolutions).
-__global__ void scatter_kernel(uint32_t *__restrict__ A, const uint32_t *__restrict__ rows,
-                               const uint32_t *__restrict__ vals, uint32_t n) {
-    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) A[rows[i]] = vals[i];
-}
-
-// Host-aggregated terms of tie rows into the extra slab: idx < KD -> slab[idx] (packed
-// hi << 32 | lo), else cnt[idx - KD].
-__global__ void add_terms_kernel(uint64_t *__restrict__ slab, uint32_t *__restrict__ cnt, uint64_t KD,
-                                 const uint64_t *__restrict__ idx, const uint64_t *__restrict__ val, uint32_t n) {
-    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
-        if (idx[i] < KD) atomicAdd((unsigned long long *)&slab[idx[i]], (unsigned long long)val[i]);
-        else atomicAdd(&cnt[idx[i] - KD], (uint32_t)val[i]);
+// Host-resolved tie rows: A[rows[i]] = vals[i], and with xslab the row's terms move from its
+// provisional index (the search's, still in A) to the new one: added to slab G (xslab,
+// xcnt) at the new index and to slab G + 1 (subtracted by the reduce) at the old one.  One
+// wave per row.
+__global__ void fix_rows_kernel(const uint8_t *__restrict__ codes, uint32_t Dp, uint32_t D, uint32_t *__restrict__ A,
+                                const uint32_t *__restrict__ rows, const uint32_t *__restrict__ vals, uint32_t n,
+                                uint32_t K, uint64_t *__restrict__ xslab, uint32_t *__restrict__ xcnt,
+                                const uint64_t *__restrict__ plut) {
+    const uint32_t lane = threadIdx.x & 63;
+    for (uint32_t i = (blockIdx.x * blockDim.x + threadIdx.x) / 64; i < n; i += gridDim.x * blockDim.x / 64) {
+        const uint32_t row = rows[i], to = vals[i];
+        const uint32_t from = A[row];
+        if (from != to && xslab) move_row_terms(codes, Dp, D, row, from, to, K, xslab, xcnt, plut, lane);
+        if (lane == 0) A[row] = to;
     }
 }
 
-hipError_t launch_scatter(hipStream_t s, uint32_t *A, const uint32_t *rows, const uint32_t *vals, uint32_t n,
-                          uint64_t *slab, uint32_t *slab_cnt, uint64_t KD, const uint64_t *idx, const uint64_t *val,
-                          uint32_t nterms) {
-    if (n) hipLaunchKernelGGL(scatter_kernel, dim3((n + 255) / 256), dim3(256), 0, s, A, rows, vals, n);
-    if (nterms)
-        hipLaunchKernelGGL(add_terms_kernel, dim3((nterms + 255) / 256), dim3(256), 0, s, slab, slab_cnt, KD, idx, val,
-                           nterms);
+hipError_t launch_fix_rows(hipStream_t s, const uint8_t *codes, uint32_t Dp, uint32_t D, uint32_t *A,
+                           const uint32_t *rows, const uint32_t *vals, uint32_t n, uint32_t K, uint64_t *xslab,
+                           uint32_t *xcnt, const uint64_t *plut) {
+    if (n == 0) return hipSuccess;
+    const int blocks = (int)std::min<uint32_t>((n + 3) / 4, 1024);
+    hipLaunchKernelGGL(fix_rows_kernel, dim3(blocks), dim3(256), 0, s, codes, Dp, D, A, rows, vals, n, K, xslab, xcnt,
+                       plut);
     return hipGetLastError();
 }
 
