@@ -375,7 +375,9 @@ void build_tree(qvq_ctx *ctx, const double *hC, uint32_t K, int buf, KdView &kd)
     // memory with one DMA first (mapped reads from 16 workgroups cost up to ~70 us); small
     // ones are read in place (the DMA itself costs ~5 us of stream time per level).
     const double *dlo = reinterpret_cast<const double *>(ctx->dh_tree[buf]);
-    if (bytes > 32768) {
+    static const uint64_t dma_min = std::getenv("QVQ_TREE_DMA_MIN") ? std::atoll(std::getenv("QVQ_TREE_DMA_MIN"))
+                                                                      : 32768;   // ablation
+    if (bytes > dma_min) {
         if (hipMemcpyAsync(ctx->d_tree, ctx->h_tree[buf], bytes, hipMemcpyHostToDevice, ctx->stream) != hipSuccess)
             return;
         dlo = reinterpret_cast<const double *>(ctx->d_tree);

@@ -92,18 +92,21 @@ __device__ inline uint32_t wave_scan_max(uint32_t v) {
 
 // Per-run sums over consecutive lanes with equal key (lanes hold consecutive rows): plain
 // prefix sums, then each run's last lane takes prefix[last] - prefix[first - 1].  The
-// packed 16-bit fields of v never carry within 64 rows, so the subtraction is per field.
-// Returns true on the last lane of each run, which then holds the run's sums.
+// packed 16-bit fields of v never carry within 64 rows, so the subtraction is per field, and
+// prefix[first - 1] comes from one bpermute (a DPP max-scan form of it measured slower: the
+// search is VALU-issue bound, not LDS bound).  Returns true on the last lane of each run,
+// which then holds the run's sums.
 __device__ inline bool wave_runs_reduce(uint32_t key, uint32_t (&v)[MF_D + 1], int lane) {
-    const uint32_t prev = __shfl_up(key, 1);
-    const uint32_t next = __shfl_down(key, 1);
-    const uint32_t head = wave_scan_max((lane == 0 || prev != key) ? (uint32_t)lane : 0u);
-    const int src = head == 0 ? 0 : (int)head - 1;
+    const uint32_t prev = wave_prev_u32(key);
+    const uint32_t next = wave_next_u32(key);
+    const bool head = lane == 0 || prev != key;
+    const uint32_t h = wave_scan_max(head ? (uint32_t)lane : 0u);
+    const int src = h == 0 ? 0 : (int)h - 1;
 #pragma unroll
     for (int i = 0; i <= MF_D; i++) {
         const uint32_t pre = wave_scan_add(v[i]);
         const uint32_t before = __shfl(pre, src);
-        v[i] = pre - (head == 0 ? 0u : before);
+        v[i] = pre - (h == 0 ? 0u : before);
     }
     return lane == 63 || next != key;
 }

@@ -15,6 +15,30 @@ __device__ inline float min3f(float a, float b, float c) { return __builtin_fmin
 __device__ inline float min2f(float a, float b) { return __builtin_fminf(a, b); }
 __device__ inline float med3f(float a, float b, float c) { return __builtin_amdgcn_fmed3f(a, b, c); }
 
+// Cross-lane moves on the VALU (no LDS traffic; tools/micro/lane_ops_check.hip verifies them
+// against __shfl_*).  v_permlane16_swap exchanges the odd 16-lane rows of its first operand
+// with the even rows of its second; v_permlane32_swap the upper half of the first with the
+// lower half of the second.  With both operands x, the x of lane ^ 16 (^ 32) lands in the
+// first result on odd rows (upper half) and in the second on even rows (lower half).
+__device__ inline uint32_t xor16_u32(uint32_t x) {
+    const auto r = __builtin_amdgcn_permlane16_swap(x, x, false, false);
+    return (__lane_id() & 16) ? r[0] : r[1];
+}
+__device__ inline uint32_t xor32_u32(uint32_t x) {
+    const auto r = __builtin_amdgcn_permlane32_swap(x, x, false, false);
+    return (__lane_id() & 32) ? r[0] : r[1];
+}
+__device__ inline float xor16_f32(float x) { return __uint_as_float(xor16_u32(__float_as_uint(x))); }
+__device__ inline float xor32_f32(float x) { return __uint_as_float(xor32_u32(__float_as_uint(x))); }
+// x of lane - 1 (lane 0 keeps its own) and of lane + 1 (lane 63 keeps its own): DPP
+// wave_shr:1 / wave_shl:1.
+__device__ inline uint32_t wave_prev_u32(uint32_t x) {
+    return (uint32_t)__builtin_amdgcn_update_dpp((int)x, (int)x, 0x138, 0xF, 0xF, false);
+}
+__device__ inline uint32_t wave_next_u32(uint32_t x) {
+    return (uint32_t)__builtin_amdgcn_update_dpp((int)x, (int)x, 0x130, 0xF, 0xF, false);
+}
+
 // Centred integer of a byte: w = 2*((int8)b + 128) - 255 = 2*(b ^ 0x80) - 255 (both colour
 // spaces), so v(b) = mu + w*sx.  Exact in f16.
 __device__ inline float byte_w(uint32_t word, int j) {
