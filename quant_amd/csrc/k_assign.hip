@@ -342,35 +342,46 @@ __global__ __launch_bounds__(MF_THREADS) void assign_mfma_kernel(
         for (int t = 0; t < MF_TILES; t++) pair_update(pa0[t], pa1[t], npairs - 1, b1[t], b2[t], bp[t]);
 
 #endif
-        // Combine the four lanes of each data row on MFMA values: winning (pair, group) and
-        // the second-best minimum among all other candidates.
-        uint32_t wsel[MF_TILES];   // 8-code-vector unit: pair*4 + g
-#pragma unroll
-        for (int t = 0; t < MF_TILES; t++) {
-            uint32_t u = bp[t] * 4 + g;
-#pragma unroll
-            for (int off = 16; off <= 32; off <<= 1) {
-                const float o1 = __shfl_xor(b1[t], off), o2 = __shfl_xor(b2[t], off);
-                const uint32_t ou = __shfl_xor(u, off);
-                if (o1 < b1[t] || (o1 == b1[t] && ou < u)) {
-                    b2[t] = min2f(o2, b1[t]);
-                    b1[t] = o1;
-                    u = ou;
-                } else {
-                    b2[t] = min2f(b2[t], o1);
-                }
+        // Combine the four lanes of each data row (groups g = 0..3 of every tile) on MFMA
+        // values: winning 8-code-vector unit (pair*4 + g, lowest on equal scores) and the
+        // second-best minimum among all other candidates.  A reduce-scatter on the VALU:
+        // v_permlane32_swap merges tiles t and t + 2 across lane ^ 32, v_permlane16_swap the
+        // two survivors across lane ^ 16, and lane (g, c) is left with tile g, row c -- its
+        // own row base + lane.  The merge is order-free: (best, unit) is the lexicographic
+        // minimum and the second the second-smallest of all candidates either way.
+        auto merge = [](float &m1, float &m2, uint32_t &mu, float o1, float o2, uint32_t ou) {
+            if (o1 < m1 || (o1 == m1 && ou < mu)) {
+                m2 = min2f(o2, m1);
+                m1 = o1;
+                mu = ou;
+            } else {
+                m2 = min2f(m2, o1);
             }
-            wsel[t] = u;
+        };
+        float h1[2], h2[2];
+        uint32_t hu[2];
+#pragma unroll
+        for (int t = 0; t < 2; t++) {
+            // lanes < 32 end with tile t (g and g + 2 merged), lanes >= 32 with tile t + 2
+            const auto s1 = swap32_f32(b1[t], b1[t + 2]);
+            const auto s2 = swap32_f32(b2[t], b2[t + 2]);
+            const auto su = swap32_u32(bp[t] * 4 + g, bp[t + 2] * 4 + g);
+            h1[t] = s1.lo;
+            h2[t] = s2.lo;
+            hu[t] = su.lo;
+            merge(h1[t], h2[t], hu[t], s1.hi, s2.hi, su.hi);
+        }
+        {   // even rows keep h*[0] (tile 0 or 2), odd rows h*[1] (tile 1 or 3): tile g
+            const auto s1 = swap16_f32(h1[0], h1[1]);
+            const auto s2 = swap16_f32(h2[0], h2[1]);
+            const auto su = swap16_u32(hu[0], hu[1]);
+            float m1 = s1.lo;
+            sec_m = s2.lo;
+            unit = su.lo;
+            merge(m1, sec_m, unit, s1.hi, s2.hi, su.hi);
         }
         // Lane L owns row base + L (tile L/16, row L%16): recompute the 8 code vectors of
         // its winning unit in the direct fp32 form (x - c)^2.
-        unit = wsel[0];
-        sec_m = b2[0];
-#pragma unroll
-        for (int t = 1; t < MF_TILES; t++) {
-            unit = g == t ? wsel[t] : unit;
-            sec_m = g == t ? b2[t] : sec_m;
-        }
         }   // !SMALLK
         const uint64_t row = base + lane;
         const bool valid = row < N;

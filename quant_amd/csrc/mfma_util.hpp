@@ -28,6 +28,32 @@ __device__ inline uint32_t xor32_u32(uint32_t x) {
     const auto r = __builtin_amdgcn_permlane32_swap(x, x, false, false);
     return (__lane_id() & 32) ? r[0] : r[1];
 }
+// Both results of a swap.  swap32(x, y): lo = lanes < 32: x, lanes >= 32: y of lane - 32;
+// hi = lanes < 32: x of lane + 32, lanes >= 32: y.  swap16 the same on 16-lane rows (even
+// rows keep x in lo and take x of lane + 16 in hi; odd rows take y of lane - 16 in lo and
+// keep y in hi).
+struct LanePair {
+    uint32_t lo, hi;
+};
+struct LanePairF {
+    float lo, hi;
+};
+__device__ inline LanePair swap32_u32(uint32_t x, uint32_t y) {
+    const auto r = __builtin_amdgcn_permlane32_swap(x, y, false, false);
+    return {r[0], r[1]};
+}
+__device__ inline LanePair swap16_u32(uint32_t x, uint32_t y) {
+    const auto r = __builtin_amdgcn_permlane16_swap(x, y, false, false);
+    return {r[0], r[1]};
+}
+__device__ inline LanePairF swap32_f32(float x, float y) {
+    const LanePair p = swap32_u32(__float_as_uint(x), __float_as_uint(y));
+    return {__uint_as_float(p.lo), __uint_as_float(p.hi)};
+}
+__device__ inline LanePairF swap16_f32(float x, float y) {
+    const LanePair p = swap16_u32(__float_as_uint(x), __float_as_uint(y));
+    return {__uint_as_float(p.lo), __uint_as_float(p.hi)};
+}
 __device__ inline float xor16_f32(float x) { return __uint_as_float(xor16_u32(__float_as_uint(x))); }
 __device__ inline float xor32_f32(float x) { return __uint_as_float(xor32_u32(__float_as_uint(x))); }
 // x of lane - 1 (lane 0 keeps its own) and of lane + 1 (lane 63 keeps its own): DPP
