@@ -159,8 +159,14 @@ hipError_t launch_update(hipStream_t s, uint32_t Dp, uint32_t G, const uint8_t *
 // of re-assigned rows at their provisional index).
 hipError_t launch_reduce(hipStream_t s, const uint64_t *part, const uint32_t *part_cnt, uint32_t G, uint32_t nsub,
                          uint32_t K, uint32_t D, uint64_t *sums);
+// Up to three device ranges (sizes multiples of 4 bytes, 0 = unused) copied in one launch,
+// e.g. into mapped pinned host memory.
+hipError_t launch_copy_out(hipStream_t s, const void *src0, void *dst0, uint64_t bytes0, const void *src1, void *dst1,
+                           uint64_t bytes1, const void *src2, void *dst2, uint64_t bytes2);
+// Mean sums (K = 1) into sums[0..2D]; also clears zero[0..n_zero) and sets dist[0..1] = x0, x1.
 hipError_t launch_mean_sums(hipStream_t s, uint32_t Dp, const uint8_t *codes, uint64_t N, uint32_t D,
-                            const uint64_t *plut, uint64_t *sums);
+                            const uint64_t *plut, uint64_t *sums, unsigned *zero, uint32_t n_zero, double *dist,
+                            double x0, double x1);
 // Centroids of the reduced sums (C_cent [K][D]); with split also the next level's K' = 2K
 // code vectors (C64n and, if host_cb, mapped host memory) and their search tables (see
 // launch_prep) padded to Kpad_next; without split, given dist_out, dist_out[0] =

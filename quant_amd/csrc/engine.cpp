@@ -578,7 +578,8 @@ QVQ_API qvq_status qvq_create(int hip_device, qvq_ctx **out) {
     if ((e = hipMalloc(&ctx->d_w, 256 * 4)) != hipSuccess) return bail(e, "hipMalloc");
     if ((e = hipMalloc(&ctx->d_lut64, 256 * 8)) != hipSuccess) return bail(e, "hipMalloc");
     if ((e = hipMalloc(&ctx->d_plut, 256 * 8)) != hipSuccess) return bail(e, "hipMalloc");
-    if ((e = hipHostMalloc(&ctx->h_ready, 64, hipHostMallocMapped | hipHostMallocCoherent)) != hipSuccess)
+    // mapped: [0, 64) the codebook ready number, [64, 1024) a quantize's small results
+    if ((e = hipHostMalloc(&ctx->h_ready, 1024, hipHostMallocMapped | hipHostMallocCoherent)) != hipSuccess)
         return bail(e, "hipHostMalloc");
     *ctx->h_ready = 0;
     if ((e = hipHostGetDevicePointer((void **)&ctx->dh_ready, ctx->h_ready, 0)) != hipSuccess)
@@ -737,15 +738,13 @@ QVQ_API qvq_status qvq_lbg(qvq_ctx *ctx, uint32_t bits, double eps, double *code
     std::memset(&ctx->tm, 0, sizeof(ctx->tm));
     ctx->tm.levels = (int)bits;
     const Terms &T = ctx->terms;
-    HIPCHK(hipMemsetAsync(ctx->d_counters, 0, (2 * 33 + 1) * sizeof(unsigned), ctx->stream));
-    // [sum ||x||^2, rows] over all ranks, for the closed-form distortion
+    // codeVectors[0] = trainingSetSum() / N, then the first split (src/Quantizer.cpp:129-138).
+    // The mean kernel also clears the counters and writes [sum ||x||^2, rows] for the
+    // closed-form distortion (summed over all ranks below).
     double *d_dist = ctx->d_dist_part;
-    double xn[2] = {ctx->xsq, (double)ctx->N};
-    HIPCHK(hipMemcpy(d_dist, xn, sizeof(xn), hipMemcpyHostToDevice));
+    HIPCHK(launch_mean_sums(ctx->stream, ctx->Dp, ctx->d_codes, ctx->N, ctx->D, ctx->d_plut, ctx->d_sums,
+                            ctx->d_counters, 2 * 33 + 1, d_dist, ctx->xsq, (double)ctx->N));
     if (ctx->comm) NCCLCHK(ncclAllReduce(d_dist, d_dist, 2, ncclDouble, ncclSum, ctx->comm, ctx->stream));
-
-    // codeVectors[0] = trainingSetSum() / N, then the first split (src/Quantizer.cpp:129-138)
-    HIPCHK(launch_mean_sums(ctx->stream, ctx->Dp, ctx->d_codes, ctx->N, ctx->D, ctx->d_plut, ctx->d_sums));
     if ((st = all_reduce_sums(ctx, 1)) != QVQ_OK) return st;
     unsigned *dist_done = ctx->d_counters + 2 * 33;
     // finalize (+ split, tables, host codebook and its ready number) / final distortion
@@ -757,7 +756,8 @@ QVQ_API qvq_status qvq_lbg(qvq_ctx *ctx, uint32_t bits, double eps, double *code
                                     split ? nullptr : d_dist + 2, split ? ctx->dh_ready : nullptr, ctx->seq);
     };
     HIPCHK(finalize(1, bits > 0));
-    HIPCHK(hipMemsetAsync(ctx->d_A, 0, ctx->N * 4, ctx->stream));
+    // with bits >= 1 the first search writes every row's index
+    if (bits == 0) HIPCHK(hipMemsetAsync(ctx->d_A, 0, ctx->N * 4, ctx->stream));
 
     for (uint32_t lvl = 1; lvl <= bits; lvl++) {
         const uint32_t K = 1u << lvl;
@@ -774,15 +774,23 @@ QVQ_API qvq_status qvq_lbg(qvq_ctx *ctx, uint32_t bits, double eps, double *code
     // Returned distortion: updateDistortion after the last fix (src/Quantizer.cpp:9-22,103),
     // from the sums of the final assignment (finalize_prep_kernel without split).
     HIPCHK(hipEventRecord(ctx->ev_end, ctx->stream));
+    // distortion inputs, per-level counters and the codebook go to mapped pinned memory in one
+    // launch (the mapped split-codebook buffer is free once the last tree is built)
     double dres[3];
     unsigned stats[2 * 33];
-    HIPCHK(hipMemcpyAsync(dres, d_dist, sizeof(dres), hipMemcpyDeviceToHost, ctx->stream));
-    HIPCHK(hipMemcpyAsync(stats, ctx->d_counters, sizeof(stats), hipMemcpyDeviceToHost, ctx->stream));
-    if (codebook)
-        HIPCHK(hipMemcpyAsync(codebook, ctx->d_C64_cent, (uint64_t)Kmax * ctx->D * 8, hipMemcpyDeviceToHost,
-                              ctx->stream));
-    if (assign) HIPCHK(hipMemcpyAsync(assign, ctx->d_A, ctx->N * 4, hipMemcpyDeviceToHost, ctx->stream));
-    HIPCHK(hipStreamSynchronize(ctx->stream));
+    {
+        uint8_t *h_small = reinterpret_cast<uint8_t *>(ctx->h_ready) + 64;
+        uint8_t *dh_small = reinterpret_cast<uint8_t *>(ctx->dh_ready) + 64;
+        static_assert(sizeof(dres) + sizeof(stats) <= 1024 - 64, "small results exceed the mapped area");
+        const uint64_t cb_bytes = codebook ? (uint64_t)Kmax * ctx->D * 8 : 0;
+        HIPCHK(launch_copy_out(ctx->stream, d_dist, dh_small, sizeof(dres), ctx->d_counters, dh_small + sizeof(dres),
+                               sizeof(stats), ctx->d_C64_cent, ctx->dh_cb, cb_bytes));
+        if (assign) HIPCHK(hipMemcpyAsync(assign, ctx->d_A, ctx->N * 4, hipMemcpyDeviceToHost, ctx->stream));
+        HIPCHK(hipStreamSynchronize(ctx->stream));
+        std::memcpy(dres, h_small, sizeof(dres));
+        std::memcpy(stats, h_small + sizeof(dres), sizeof(stats));
+        if (codebook) std::memcpy(codebook, ctx->h_cb, cb_bytes);
+    }
     if (distortion) *distortion = (dres[0] - dres[2]) / (dres[1] * (double)ctx->D);
     for (uint32_t lvl = 1; lvl <= bits; lvl++) {
         // assign: the search kernel; update: the non-fused update; other: the rest of the

@@ -5,6 +5,7 @@
 //   hi[d][k] (K*D) | lo[d][k] (K*D) | cnt[k] (K)
 // Workgroup slabs (update kernels): part[g][d][k] packed (hi << 32 | lo), part_cnt[g][k].
 #include "common.hpp"
+#include "mfma_util.hpp"
 
 namespace qvq {
 
@@ -327,39 +328,87 @@ hipError_t launch_reduce(hipStream_t s, const uint64_t *part, const uint32_t *pa
 }
 
 // K = 1 (the mean initialisation, trainingSetSum, src/Quantizer.cpp:46-57): every row in
-// one cluster, so a plain register + LDS reduction; sums must be zeroed beforehand.
-constexpr int MEAN_THREADS = 256;
+// one cluster, so a register + LDS reduction; sums must be zeroed beforehand.  A thread takes
+// groups of 4 consecutive rows (4*DP bytes: DP/4 16-byte loads), two groups per trip so the
+// loads of both are in flight together, and adds each component's exact term as
+// (b ^ 0x80) << 16 | lo8[b] in u32 registers: the grid gives every thread at most 256 rows,
+// so neither 16-bit field carries.  Block 0 also writes the quantize's initial state (the
+// distortion inputs, zeroed counters), which saves two host calls per quantize.
+constexpr int MEAN_THREADS = 1024;
+constexpr uint64_t MEAN_ROWS_PER_THREAD = 256;
+struct MeanInit {
+    unsigned *zero;     // n_zero counters to clear
+    uint32_t n_zero;
+    double *dist;       // dist[0..1] = x0, x1
+    double x0, x1;
+};
 template <int DP>
 __global__ __launch_bounds__(MEAN_THREADS) void mean_sums_kernel(const uint8_t *__restrict__ codes, uint64_t N,
                                                                  uint32_t D, const uint64_t *__restrict__ plut,
-                                                                 uint64_t *__restrict__ sums) {
-    __shared__ uint64_t lut[256];
-    __shared__ uint64_t red[MEAN_THREADS / 64][DP][2];
-    lut[threadIdx.x] = plut[threadIdx.x];
-    if (blockIdx.x == 0 && threadIdx.x == 0) sums[2 * D] = N;   // cnt[0]
-    __syncthreads();
-    uint64_t acc[DP];
-#pragma unroll
-    for (int d = 0; d < DP; d++) acc[d] = 0;   // packed (hi << 32 | lo): <= 2^24 rows per thread
-    for (uint64_t row = blockIdx.x * (uint64_t)MEAN_THREADS + threadIdx.x; row < N;
-         row += (uint64_t)gridDim.x * MEAN_THREADS) {
-        const uint32_t *w = reinterpret_cast<const uint32_t *>(codes + row * DP);
-#pragma unroll
-        for (int q = 0; q < DP / 4; q++) {
-            const uint32_t v = w[q];
-#pragma unroll
-            for (int j = 0; j < 4; j++) acc[4 * q + j] += lut[(v >> (8 * j)) & 0xFF];
+                                                                 uint64_t *__restrict__ sums, MeanInit init) {
+    __shared__ uint32_t lo8[256];
+    __shared__ uint32_t red[MEAN_THREADS / 64][DP][2];
+    if (threadIdx.x < 256) lo8[threadIdx.x] = (uint32_t)(plut[threadIdx.x] & 0xFF);
+    if (blockIdx.x == 0) {
+        if (threadIdx.x == 0) {
+            sums[2 * D] = N;   // cnt[0]
+            init.dist[0] = init.x0;
+            init.dist[1] = init.x1;
         }
+        if (threadIdx.x < init.n_zero) init.zero[threadIdx.x] = 0;
+    }
+    __syncthreads();
+    uint32_t acc[DP];
+#pragma unroll
+    for (int d = 0; d < DP; d++) acc[d] = 0;
+    auto add_word = [&](uint32_t w, int d0) {
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            const uint32_t b = (w >> (8 * j)) & 0xFF;
+            acc[d0 + j] += ((b ^ 0x80u) << 16) | lo8[b];
+        }
+    };
+    constexpr int Q = DP / 4;   // 16-byte loads per group of 4 rows
+    const uint64_t groups = N / 4, stride = (uint64_t)gridDim.x * MEAN_THREADS;
+    for (uint64_t g = (uint64_t)blockIdx.x * MEAN_THREADS + threadIdx.x; g < groups; g += 2 * stride) {
+        const uint64_t g2 = g + stride < groups ? g + stride : g;
+        const uint4 *p = reinterpret_cast<const uint4 *>(codes + g * 4 * DP);
+        const uint4 *p2 = reinterpret_cast<const uint4 *>(codes + g2 * 4 * DP);
+        uint4 v[Q], v2[Q];
+#pragma unroll
+        for (int q = 0; q < Q; q++) v[q] = p[q];
+#pragma unroll
+        for (int q = 0; q < Q; q++) v2[q] = p2[q];
+        // word i of the group is component (i mod DP/4)*4.. of row i / (DP/4)
+#pragma unroll
+        for (int q = 0; q < Q; q++) {
+            add_word(v[q].x, ((4 * q + 0) % (DP / 4)) * 4);
+            add_word(v[q].y, ((4 * q + 1) % (DP / 4)) * 4);
+            add_word(v[q].z, ((4 * q + 2) % (DP / 4)) * 4);
+            add_word(v[q].w, ((4 * q + 3) % (DP / 4)) * 4);
+        }
+        if (g2 != g) {
+#pragma unroll
+            for (int q = 0; q < Q; q++) {
+                add_word(v2[q].x, ((4 * q + 0) % (DP / 4)) * 4);
+                add_word(v2[q].y, ((4 * q + 1) % (DP / 4)) * 4);
+                add_word(v2[q].z, ((4 * q + 2) % (DP / 4)) * 4);
+                add_word(v2[q].w, ((4 * q + 3) % (DP / 4)) * 4);
+            }
+        }
+    }
+    // the last N mod 4 rows, one per thread of block 0
+    if (blockIdx.x == 0 && threadIdx.x < N % 4) {
+        const uint32_t *w = reinterpret_cast<const uint32_t *>(codes + (groups * 4 + threadIdx.x) * DP);
+#pragma unroll
+        for (int q = 0; q < DP / 4; q++) add_word(w[q], 4 * q);
     }
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
 #pragma unroll
     for (int d = 0; d < DP; d++) {
-        uint64_t h = acc[d] >> 32, l = acc[d] & 0xFFFFFFFFull;
-        for (int off = 32; off >= 1; off >>= 1) {
-            h += __shfl_xor(h, off);
-            l += __shfl_xor(l, off);
-        }
-        if (lane == 0) {
+        // wave totals (< 2^22) by DPP scans on the VALU: lane 63 holds them
+        const uint32_t h = wave_scan_add(acc[d] >> 16), l = wave_scan_add(acc[d] & 0xFFFF);
+        if (lane == 63) {
             red[wave][d][0] = h;
             red[wave][d][1] = l;
         }
@@ -377,19 +426,62 @@ __global__ __launch_bounds__(MEAN_THREADS) void mean_sums_kernel(const uint8_t *
 }
 
 hipError_t launch_mean_sums(hipStream_t s, uint32_t Dp, const uint8_t *codes, uint64_t N, uint32_t D,
-                            const uint64_t *plut, uint64_t *sums) {
+                            const uint64_t *plut, uint64_t *sums, unsigned *zero, uint32_t n_zero, double *dist,
+                            double x0, double x1) {
+    if (n_zero > MEAN_THREADS) return hipErrorInvalidValue;
     const hipError_t e = hipMemsetAsync(sums, 0, (2 * (size_t)D + 1) * 8, s);
     if (e != hipSuccess) return e;
-    const int grid = (int)std::min<uint64_t>((N + MEAN_THREADS - 1) / MEAN_THREADS, 1024);
+    // one block per CU (few same-address atomics at the end), more only where a thread would
+    // otherwise take over MEAN_ROWS_PER_THREAD rows (u32 fields)
+    static const uint64_t grid_cap = std::getenv("QVQ_MEAN_GRID") ? std::atoll(std::getenv("QVQ_MEAN_GRID")) : 256;
+    const uint64_t per_block = MEAN_THREADS * MEAN_ROWS_PER_THREAD;
+    const uint64_t grid_min = (N + per_block - 1) / per_block;
+    const uint64_t grid = std::max<uint64_t>(std::max<uint64_t>(grid_min, 1),
+                                             std::min<uint64_t>((N + 4 * MEAN_THREADS - 1) / (4 * MEAN_THREADS), grid_cap));
+    if (grid > 0x7FFFFFFFull) return hipErrorInvalidValue;
+    const MeanInit init{zero, n_zero, dist, x0, x1};
     switch (Dp) {
-#define X(DPV)                                                                                                    \
-    case DPV:                                                                                                     \
-        hipLaunchKernelGGL(mean_sums_kernel<DPV>, dim3(grid), dim3(MEAN_THREADS), 0, s, codes, N, D, plut, sums); \
+#define X(DPV)                                                                                              \
+    case DPV:                                                                                               \
+        hipLaunchKernelGGL(mean_sums_kernel<DPV>, dim3((unsigned)grid), dim3(MEAN_THREADS), 0, s, codes, N, D, plut, \
+                           sums, init);                                                                     \
         return hipGetLastError();
         QVQ_FOR_EACH_DP(X)
 #undef X
     }
     return hipErrorInvalidValue;
+}
+
+// Result hand-off at the end of a quantize: up to three device ranges copied in one launch
+// straight into mapped pinned host memory (replacing three staged device-to-host copies).
+struct CopySeg {
+    const uint32_t *src;
+    uint32_t *dst;
+    uint64_t words;
+};
+struct CopySegs {
+    CopySeg seg[3];
+};
+__global__ __launch_bounds__(256) void copy_out_kernel(CopySegs a) {
+#pragma unroll
+    for (int k = 0; k < 3; k++) {
+        const CopySeg &c = a.seg[k];
+        for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < c.words; i += (uint64_t)gridDim.x * 256)
+            c.dst[i] = c.src[i];
+    }
+}
+
+hipError_t launch_copy_out(hipStream_t s, const void *src0, void *dst0, uint64_t bytes0, const void *src1, void *dst1,
+                           uint64_t bytes1, const void *src2, void *dst2, uint64_t bytes2) {
+    if ((bytes0 | bytes1 | bytes2) & 3) return hipErrorInvalidValue;
+    CopySegs a;
+    a.seg[0] = {static_cast<const uint32_t *>(src0), static_cast<uint32_t *>(dst0), bytes0 / 4};
+    a.seg[1] = {static_cast<const uint32_t *>(src1), static_cast<uint32_t *>(dst1), bytes1 / 4};
+    a.seg[2] = {static_cast<const uint32_t *>(src2), static_cast<uint32_t *>(dst2), bytes2 / 4};
+    const uint64_t words = std::max(bytes0, std::max(bytes1, bytes2)) / 4;
+    const int grid = (int)std::min<uint64_t>(std::max<uint64_t>((words + 255) / 256, 1), 256);
+    hipLaunchKernelGGL(copy_out_kernel, dim3(grid), dim3(256), 0, s, a);
+    return hipGetLastError();
 }
 
 // finalize (src/Quantizer.cpp:79-94 fixCodebook + :129-138 split) fused with the next

@@ -65,6 +65,31 @@ __device__ inline uint32_t wave_next_u32(uint32_t x) {
     return (uint32_t)__builtin_amdgcn_update_dpp((int)x, (int)x, 0x130, 0xF, 0xF, false);
 }
 
+// Wave64 inclusive scans with DPP (row_shr within rows of 16, then row_bcast:15/31 across
+// rows): one VALU instruction per step, no LDS traffic.
+template <int CTRL, int ROW_MASK>
+__device__ inline uint32_t dpp_get(uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, ROW_MASK, 0xF, true);
+}
+__device__ inline uint32_t wave_scan_add(uint32_t v) {
+    v += dpp_get<0x111, 0xF>(v);   // row_shr:1
+    v += dpp_get<0x112, 0xF>(v);   // row_shr:2
+    v += dpp_get<0x114, 0xF>(v);   // row_shr:4
+    v += dpp_get<0x118, 0xF>(v);   // row_shr:8
+    v += dpp_get<0x142, 0xA>(v);   // row_bcast:15 into rows 1, 3
+    v += dpp_get<0x143, 0xC>(v);   // row_bcast:31 into rows 2, 3
+    return v;
+}
+__device__ inline uint32_t wave_scan_max(uint32_t v) {
+    v = max(v, dpp_get<0x111, 0xF>(v));
+    v = max(v, dpp_get<0x112, 0xF>(v));
+    v = max(v, dpp_get<0x114, 0xF>(v));
+    v = max(v, dpp_get<0x118, 0xF>(v));
+    v = max(v, dpp_get<0x142, 0xA>(v));
+    v = max(v, dpp_get<0x143, 0xC>(v));
+    return v;
+}
+
 // Centred integer of a byte: w = 2*((int8)b + 128) - 255 = 2*(b ^ 0x80) - 255 (both colour
 // spaces), so v(b) = mu + w*sx.  Exact in f16.
 __device__ inline float byte_w(uint32_t word, int j) {
