@@ -69,8 +69,10 @@ __host__ __device__ inline double centroid_value(uint64_t hi, uint64_t lo, uint6
 }
 
 // MFMA search layout (D = 12): per code vector one 56-byte row of 28 f16
-// [hi0..11, lo0..11, nhi, nlo, 0, 0], where hi+lo ~= -2*sx*(c-mu)*2^t and
-// nhi+nlo ~= 2^t*||c-mu||^2, so that score = 2^t*(||x-c||^2 - ||x-mu||^2).
+// [hi0..3, lo0..3, hi4..7, lo4..7, hi8..11, lo8..11, nhi, nlo, 0, 0], where hi+lo ~=
+// -2*sx*(c-mu)*2^t and nhi+nlo ~= 2^t*||c-mu||^2, so that score = 2^t*(||x-c||^2 - ||x-mu||^2).
+// K-slot group g < 3 (slots 8g..8g+7) then meets components 4g..4g+3 twice: one word of the
+// data row per B fragment.
 constexpr int MF_D = 12;
 constexpr int MF_ROW_F16 = 28;
 constexpr int MF_ROW_BYTES = 2 * MF_ROW_F16;
@@ -85,6 +87,13 @@ __host__ __device__ constexpr uint32_t wide_row_f16(uint32_t Dp) { return 32 * w
 // f16 slots per code-vector row and the offset of the lo half, for either layout
 __host__ __device__ inline uint32_t cb_row_f16(uint32_t D, uint32_t Dp) { return D == MF_D ? MF_ROW_F16 : wide_row_f16(Dp); }
 __host__ __device__ inline uint32_t cb_lo_off(uint32_t D, uint32_t Dp) { return D == MF_D ? MF_D : wide_dh(Dp); }
+// f16 slot of component d's hi and lo part in a row of either layout (norm: slots 2*LO, +1)
+__host__ __device__ inline uint32_t cb_hi_slot(uint32_t D, uint32_t Dp, uint32_t d) {
+    return D == MF_D ? 8 * (d / 4) + d % 4 : d;
+}
+__host__ __device__ inline uint32_t cb_lo_slot(uint32_t D, uint32_t Dp, uint32_t d) {
+    return D == MF_D ? 8 * (d / 4) + 4 + d % 4 : wide_dh(Dp) + d;
+}
 
 // ---------------------------------------------------------------------------------------
 // Launch wrappers (each defined next to its kernel).  All take the stream last-but-args.

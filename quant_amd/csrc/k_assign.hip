@@ -64,6 +64,7 @@ bool mf_can_search(uint32_t K) { return mf_lds_layout(K, false, false).total <= 
 
 
 typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
 // Per-run sums over consecutive lanes with equal key (lanes hold consecutive rows): plain
 // prefix sums, then each run's last lane takes prefix[last] - prefix[first - 1].  The
@@ -136,12 +137,11 @@ __global__ __launch_bounds__(MF_THREADS) void assign_mfma_kernel(
     const uint32_t npairs = Kp / 32;
     const uint64_t nchunks = (N + MF_ROWS - 1) / MF_ROWS;
     const f32x4 zero = {0.f, 0.f, 0.f, 0.f};
-    // k-slot words of a row for B: g=0 bytes 0-7, g=1 bytes 8-11 then 0-3, g=2 bytes 4-11
-    const int wa = g == 0 ? 0 : (g == 1 ? 2 : 1), wb = g == 0 ? 1 : (g == 1 ? 0 : 2);
-    // word selects as masks: a ternary over q[t][*] becomes a lane-varying index into a
-    // private array, which the compiler keeps in scratch memory
-    const uint32_t ma0 = 0u - (wa == 0), ma1 = 0u - (wa == 1), ma2 = 0u - (wa == 2);
-    const uint32_t mb0 = 0u - (wb == 0), mb1 = 0u - (wb == 1), mb2 = 0u - (wb == 2);
+    // B fragment of a data tile (row layout, common.hpp): lane group g < 3 meets components
+    // 4g..4g+3 twice, so it needs word g of the row only; g = 3 meets [n_hi, n_lo, 0 ...] and
+    // holds [1, 1, 0 ...].  gm masks g = 3 lanes.
+    const uint32_t gm = g < 3 ? ~0u : 0u;
+    const int gw = g < 3 ? g : 2;
     // A fragment of tile t: 16 B of code vector t*16 + c at byte 16g of its row (g = 3
     // reads n_hi, n_lo, 0, 0 and 8 bytes of the next row, which meet zeros in B).
     const unsigned char *a_base = rows + (size_t)c * MF_ROW_BYTES + 16 * g;
@@ -152,55 +152,50 @@ __global__ __launch_bounds__(MF_THREADS) void assign_mfma_kernel(
     };
     // Branch-free: rows past N read row N - 1 (their results are never written).  A load
     // under a branch gets an s_waitcnt vmcnt(0) at the join, which would void the prefetch.
-    auto load_codes = [&](uint64_t chunk, uint32_t (&q)[MF_TILES][3]) {
+    // q[t] (t < MF_TILES): word gw of row t*16 + c of the chunk; q[MF_TILES..+2]: the lane's
+    // own row, base + lane.
+    constexpr int QW = MF_TILES + 3;
+    auto load_codes = [&](uint64_t chunk, uint32_t (&q)[QW]) {
+        if constexpr (!SMALLK) {
 #pragma unroll
-        for (int t = 0; t < (SMALLK ? 1 : MF_TILES); t++) {
-            // SMALLK: only the lane's own row (base + lane), in q[0]
-            uint64_t row = SMALLK ? chunk * MF_ROWS + lane : chunk * MF_ROWS + t * 16 + c;
-            row = row < N ? row : N - 1;
-            const uint32_t *p = reinterpret_cast<const uint32_t *>(codes + row * MF_D);
-            q[t][0] = p[0];
-            q[t][1] = p[1];
-            q[t][2] = p[2];
+            for (int t = 0; t < MF_TILES; t++) {
+                uint64_t row = chunk * MF_ROWS + t * 16 + c;
+                row = row < N ? row : N - 1;
+                q[t] = reinterpret_cast<const uint32_t *>(codes + row * MF_D)[gw];
+            }
         }
+        uint64_t row = chunk * MF_ROWS + lane;
+        row = row < N ? row : N - 1;
+        const uint32_t *p = reinterpret_cast<const uint32_t *>(codes + row * MF_D);
+        q[MF_TILES] = p[0];
+        q[MF_TILES + 1] = p[1];
+        q[MF_TILES + 2] = p[2];
     };
 
     uint64_t chunk = (uint64_t)blockIdx.x * MF_WAVES + wave;
     const uint64_t stride = (uint64_t)gridDim.x * MF_WAVES;
-    uint32_t qn[MF_TILES][3];
+    uint32_t qn[QW];
     load_codes(chunk, qn);
     for (; chunk < nchunks; chunk += stride) {
         const uint64_t base = chunk * MF_ROWS;
-        uint32_t q[MF_TILES][3];
+        uint32_t q[QW];
 #pragma unroll
-        for (int t = 0; t < MF_TILES; t++)
-#pragma unroll
-            for (int i = 0; i < 3; i++) q[t][i] = qn[t][i];
+        for (int i = 0; i < QW; i++) q[i] = qn[i];
         load_codes(chunk + stride, qn);   // prefetch the next chunk under this one's search
-        uint32_t own[3] = {q[0][0], q[0][1], q[0][2]};   // this lane's own row, base + lane
+        const uint32_t own[3] = {q[MF_TILES], q[MF_TILES + 1], q[MF_TILES + 2]};
         uint32_t unit = 0;       // 8-code-vector unit (pair*4 + g) the MFMA pass picked
         float sec_m = INFINITY;  // best MFMA score among the other units
         if constexpr (!SMALLK) {
-        // B fragments: lane (g, c) holds k-slots 8g..8g+7 of data row c of each tile.
+        // B fragments: lane (g, c) holds k-slots 8g..8g+7 of data row c of each tile:
+        // [w(4g..4g+3), w(4g..4g+3)] (byte_quad_w), or [1, 1, 0 ...] for g = 3, whose masked
+        // word (u = 128, w = 1) gives the two ones.
         half8 b[MF_TILES];
 #pragma unroll
         for (int t = 0; t < MF_TILES; t++) {
-            if (g == t) {
-                own[0] = q[t][0];
-                own[1] = q[t][1];
-                own[2] = q[t][2];
-            }
-            const uint32_t ua = (q[t][0] & ma0) | (q[t][1] & ma1) | (q[t][2] & ma2);
-            const uint32_t ub = (q[t][0] & mb0) | (q[t][1] & mb1) | (q[t][2] & mb2);
-            if (g < 3) {
-#pragma unroll
-                for (int j = 0; j < 4; j++) {
-                    b[t][j] = (_Float16)byte_w(ua, j);
-                    b[t][4 + j] = (_Float16)byte_w(ub, j);
-                }
-            } else {
-                b[t] = half8{1, 1, 0, 0, 0, 0, 0, 0};
-            }
+            uint32_t w01, w23;
+            byte_quad_w(q[t] & gm, w01, w23);
+            const u32x4 v = {w01, w23 & gm, w01 & gm, w23 & gm};
+            b[t] = __builtin_bit_cast(half8, v);
         }
         float b1[MF_TILES], b2[MF_TILES];
         uint32_t bp[MF_TILES];
@@ -1024,6 +1019,36 @@ hipError_t launch_recheck(hipStream_t s, int num_cu, const uint8_t *codes, uint3
     return hipGetLastError();
 }
 
+// fp64 minimum over the wave (or over lanes 0..15 with ROWS = 1) by DPP steps on the two
+// dword halves: VALU-only, no LDS round trips on the walk's serial path.  Uniform result.
+template <int CTRL, int ROW_MASK>
+__device__ inline double dpp_min_step(double v) {
+    const uint64_t b = (uint64_t)__double_as_longlong(v);
+    constexpr uint64_t inf = 0x7FF0000000000000ull;   // what lanes without a source read
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_update_dpp((int)(uint32_t)inf, (int)(uint32_t)b, CTRL, ROW_MASK,
+                                                              0xF, false);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_update_dpp((int)(uint32_t)(inf >> 32), (int)(uint32_t)(b >> 32),
+                                                              CTRL, ROW_MASK, 0xF, false);
+    return fmin(v, __longlong_as_double((long long)(((uint64_t)hi << 32) | lo)));
+}
+template <int ROWS>
+__device__ inline double wave_min_f64(double v) {
+    v = dpp_min_step<0x111, 0xF>(v);   // row_shr:1
+    v = dpp_min_step<0x112, 0xF>(v);   // row_shr:2
+    v = dpp_min_step<0x114, 0xF>(v);   // row_shr:4
+    v = dpp_min_step<0x118, 0xF>(v);   // row_shr:8: lane 15 of each row holds the row's
+    int src = 15;
+    if (ROWS > 1) {
+        v = dpp_min_step<0x142, 0xA>(v);   // row_bcast:15 into rows 1, 3
+        v = dpp_min_step<0x143, 0xC>(v);   // row_bcast:31 into rows 2, 3
+        src = 63;
+    }
+    const uint64_t b = (uint64_t)__double_as_longlong(v);
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)b, src);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(b >> 32), src);
+    return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
+}
+
 // kd_nearest_flat with the leaf scan spread over the wave: every lane runs the same
 // descent (uniform values), lane i takes leaf point i, and the leaf's winner is the first
 // point in leaf order with the smallest distance below the leaf-entry worst -- what the
@@ -1059,8 +1084,7 @@ __device__ uint32_t kd_nearest_wave(const double *q, uint32_t D, const KdView &t
         if (phase == 0 && n.child1 >= 0 && best < 1.7976931348623157e308) {
             double m = INFINITY;
             for (int32_t j = kd_first(n) + lane; j < n.b; j += 64) m = fmin(m, pv[j]);
-#pragma unroll
-            for (int off = 32; off >= 1; off >>= 1) m = fmin(m, __shfl_xor(m, off));
+            m = wave_min_f64<4>(m);
             if (m >= best) {
                 sp--;
                 continue;
@@ -1070,26 +1094,17 @@ __device__ uint32_t kd_nearest_wave(const double *q, uint32_t D, const KdView &t
             const double worst = best;
             const int32_t cnt = n.b - n.a;
             double dist = INFINITY;
-            int32_t pos = 0x7FFFFFFF;
             if (lane < cnt) {
                 const double dd = pv[n.a + lane];   // ref_l2_hd(q, point vind[n.a + lane])
-                if (dd < worst) {
-                    dist = dd;
-                    pos = lane;
-                }
+                if (dd < worst) dist = dd;
             }
-#pragma unroll
-            for (int off = 1; off < 64; off <<= 1) {
-                const double od = __shfl_xor(dist, off);
-                const int32_t op = __shfl_xor(pos, off);
-                if (od < dist || (od == dist && op < pos)) {
-                    dist = od;
-                    pos = op;
-                }
-            }
-            if (pos != 0x7FFFFFFF) {
-                best = dist;
-                best_idx = t.vind[n.a + pos];
+            // leaves hold <= 10 points: lanes 0..15 suffice; the winner is the lowest lane
+            // with the minimum
+            const double m = wave_min_f64<1>(dist);
+            if (m < worst) {
+                const uint64_t hit = __ballot(dist == m);
+                best = m;
+                best_idx = t.vind[n.a + __ffsll((unsigned long long)hit) - 1];
             }
             sp--;
             continue;

@@ -528,7 +528,7 @@ __device__ inline double finalize_item(const FinArgs &a, uint32_t j, uint32_t d,
                 if (a.host_cb) a.host_cb[(uint64_t)j * D + d] = v;
             }
             if (d < Dp) a.C32[(uint64_t)j * Dp + d] = (float)v;
-            if (a.rows) {   // MFMA row (common.hpp): hi at d, lo at LO + d, norm at 2 LO
+            if (a.rows) {   // MFMA row (common.hpp): hi / lo at their slots, norm at 2 LO
                 const uint32_t RF = cb_row_f16(D, Dp), LO = cb_lo_off(D, Dp);
                 _Float16 *row = a.rows + (uint64_t)j * RF;
                 const double cp = d < D ? v - a.mu : 0.0;
@@ -537,11 +537,11 @@ __device__ inline double finalize_item(const FinArgs &a, uint32_t j, uint32_t d,
                 if (d < D) {
                     const double c2 = -2.0 * a.sx * cp * a.scale_t;
                     const _Float16 h = (_Float16)(float)c2;
-                    row[d] = h;
-                    row[LO + d] = (_Float16)(float)(c2 - (double)(float)h);
+                    row[cb_hi_slot(D, Dp, d)] = h;
+                    row[cb_lo_slot(D, Dp, d)] = (_Float16)(float)(c2 - (double)(float)h);
                 } else if (d < LO) {
-                    row[d] = (_Float16)0.f;
-                    row[LO + d] = (_Float16)0.f;
+                    row[cb_hi_slot(D, Dp, d)] = (_Float16)0.f;
+                    row[cb_lo_slot(D, Dp, d)] = (_Float16)0.f;
                 }
                 n *= a.scale_t;
                 const _Float16 h = (_Float16)(float)n;
@@ -680,8 +680,8 @@ __device__ inline void prep_row(const double *v, uint32_t D, uint32_t Dp, double
             n += cp * cp;
             const double c2 = -2.0 * sx * cp * scale_t;
             const _Float16 h = (_Float16)(float)c2;
-            r[d] = h;
-            r[LO + d] = (_Float16)(float)(c2 - (double)(float)h);
+            r[cb_hi_slot(D, Dp, d)] = h;
+            r[cb_lo_slot(D, Dp, d)] = (_Float16)(float)(c2 - (double)(float)h);
         }
     }
     n *= scale_t;

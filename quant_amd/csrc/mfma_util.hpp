@@ -96,6 +96,20 @@ __device__ inline float byte_w(uint32_t word, int j) {
     return __fmaf_rn(2.f, (float)(((word ^ 0x80808080u) >> (8 * j)) & 0xFF), -255.f);
 }
 
+// The four centred integers w = 2*(b ^ 0x80) - 255 of a word's bytes as two f16 pairs, exact:
+// v_perm puts each u = b ^ 0x80 under an f16 exponent byte 0x64 (f16 0x64uu = 1024 + u), then
+// (h - 1024) * 2 - 255 on packed f16 (every intermediate an integer below 2^11).
+typedef _Float16 half2v __attribute__((ext_vector_type(2)));
+__device__ inline uint32_t quad_pair_w(uint32_t h) {
+    const half2v x = __builtin_bit_cast(half2v, h) + half2v{-1024, -1024};
+    return __builtin_bit_cast(uint32_t, __builtin_elementwise_fma(x, half2v{2, 2}, half2v{-255, -255}));
+}
+__device__ inline void byte_quad_w(uint32_t word, uint32_t &w01, uint32_t &w23) {
+    const uint32_t u = word ^ 0x80808080u;
+    w01 = quad_pair_w(__builtin_amdgcn_perm(0x64646464u, u, 0x04010400u));   // [u0, 64, u1, 64]
+    w23 = quad_pair_w(__builtin_amdgcn_perm(0x64646464u, u, 0x04030402u));   // [u2, 64, u3, 64]
+}
+
 // Epilogue of one tile pair for one data tile: minimum of the lane's 8 scores, then the
 // running best pair, best score and second-best pair minimum.
 __device__ inline void pair_update(const f32x4 &p0, const f32x4 &p1, uint32_t pair, float &b1, float &b2,
