@@ -24,7 +24,7 @@ namespace qvq {
 // MFMA search
 // =======================================================================================
 #ifndef QVQ_MF_LOOP
-#define QVQ_MF_LOOP 0
+#define QVQ_MF_LOOP 2
 #endif
 #ifndef QVQ_MF_THREADS
 #define QVQ_MF_THREADS 1024
@@ -368,13 +368,21 @@ __global__ __launch_bounds__(MF_THREADS) void assign_mfma_kernel(
             }
             float r1 = INFINITY, r2 = INFINITY;
             const uint32_t pr = unit >> 2, gg = unit & 3;
+#ifdef QVQ_ABL_NORECOMP   // timing ablation only (wrong results): no recompute, no flags
+            constexpr bool skip = !SMALLK;
+            rk = (2 * pr) * 16 + 4 * gg;
+            r1 = 0.f;
+            r2 = 1e30f;
+#else
+            constexpr bool skip = false;
+#endif
             // a unit is 4 code vectors of each tile of its pair; up to K = 16 the second
             // tile is padding, and below 4 so is the rest of the first
             // SMALLK: the unit is the whole codebook
             const int jn = SMALLK ? SK : (K <= 16 ? (K < 4 ? (int)K : 4) : 8);
 #pragma unroll
             for (int j = 0; j < (SMALLK ? SK : 8); j++) {
-                if (!SMALLK && j >= jn) continue;   // uniform: K is
+                if (skip || (!SMALLK && j >= jn)) continue;   // uniform: K is
                 const uint32_t cv = SMALLK ? (uint32_t)j : (2 * pr + (j >> 2)) * 16 + 4 * gg + (j & 3);
                 const float4 *c4 = reinterpret_cast<const float4 *>(C32 + (size_t)cv * MF_D);
                 float dist = 0.f;
