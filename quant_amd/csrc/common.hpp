@@ -185,7 +185,8 @@ hipError_t launch_mean_sums(hipStream_t s, uint32_t Dp, const uint8_t *codes, ui
 hipError_t launch_finalize_prep(hipStream_t s, const uint64_t *sums, uint32_t K, uint32_t D, uint32_t Dp, int64_t R,
                                 int64_t bias, int scale, double *C_cent, bool split, double *C64n, uint32_t Kpad_next,
                                 double mu, double sx, int t, float *C32, _Float16 *cb_rows, double *host_cb,
-                                double *dist_part, unsigned *done, double *dist_out, uint64_t *ready, uint64_t seq);
+                                double *dist_part, unsigned *done, double *dist_out, uint64_t *ready, uint64_t seq,
+                                bool zero_sums);
 hipError_t launch_finalize(hipStream_t s, const uint64_t *sums, uint32_t K, uint32_t D, int64_t R, int64_t bias,
                            int scale, double *C_cent);
 // f16 MFMA tables (D = 12) and fp32 VALU table from an fp64 codebook of K code vectors.

@@ -101,6 +101,7 @@ struct qvq_ctx {
     uint64_t *d_part = nullptr, *d_sums = nullptr;
     uint32_t *d_part_cnt = nullptr;
     double *d_dist_part = nullptr;
+    uint64_t *d_mean = nullptr;   // mean sums [hi D][lo D][n]: zero between quantizes (the finalize clears it)
     uint32_t *d_scatter = nullptr;
     uint64_t scatter_bytes = 0;
     // mapped pinned host memory (coherent): the split codebook finalize writes for the
@@ -327,10 +328,10 @@ void valu_coeffs(const qvq_ctx *ctx, float &alpha, float &beta, float &gamma) {
     gamma = (float)(2.0 * 4.01 * u * u * L * L + 1e-30);
 }
 
-qvq_status all_reduce_sums(qvq_ctx *ctx, uint32_t K) {
+qvq_status all_reduce_sums(qvq_ctx *ctx, uint32_t K, uint64_t *sums = nullptr) {
+    if (!sums) sums = ctx->d_sums;
     if (ctx->comm)
-        NCCLCHK(ncclAllReduce(ctx->d_sums, ctx->d_sums, 2 * (uint64_t)K * ctx->D + K, ncclUint64, ncclSum, ctx->comm,
-                              ctx->stream));
+        NCCLCHK(ncclAllReduce(sums, sums, 2 * (uint64_t)K * ctx->D + K, ncclUint64, ncclSum, ctx->comm, ctx->stream));
     return QVQ_OK;
 }
 
@@ -587,6 +588,8 @@ QVQ_API qvq_status qvq_create(int hip_device, qvq_ctx **out) {
     if ((e = hipMalloc(&ctx->d_counters, (2 * 33 + 1) * sizeof(unsigned))) != hipSuccess) return bail(e, "hipMalloc");
     if ((e = hipMalloc(&ctx->d_hist, 256 * 8)) != hipSuccess) return bail(e, "hipMalloc");
     if ((e = hipMalloc(&ctx->d_dist_part, 8192 * 8)) != hipSuccess) return bail(e, "hipMalloc");
+    if ((e = hipMalloc(&ctx->d_mean, (2 * 64 + 1) * 8)) != hipSuccess) return bail(e, "hipMalloc");
+    if ((e = hipMemset(ctx->d_mean, 0, (2 * 64 + 1) * 8)) != hipSuccess) return bail(e, "hipMemset");
     for (int l = 0; l < 32; l++)
         for (int j = 0; j < 4; j++)
             if ((e = hipEventCreate(&ctx->ev[l][j])) != hipSuccess) return bail(e, "hipEventCreate");
@@ -611,6 +614,7 @@ QVQ_API void qvq_destroy(qvq_ctx *ctx) {
     dfree(ctx->d_hist);
     if (ctx->h_ready) (void)hipHostFree(ctx->h_ready);
     dfree(ctx->d_dist_part);
+    dfree(ctx->d_mean);
     dfree(ctx->d_scatter);
     if (ctx->ev_ready)
         for (int l = 0; l < 32; l++)
@@ -742,18 +746,24 @@ QVQ_API qvq_status qvq_lbg(qvq_ctx *ctx, uint32_t bits, double eps, double *code
     // The mean kernel also clears the counters and writes [sum ||x||^2, rows] for the
     // closed-form distortion (summed over all ranks below).
     double *d_dist = ctx->d_dist_part;
-    HIPCHK(launch_mean_sums(ctx->stream, ctx->Dp, ctx->d_codes, ctx->N, ctx->D, ctx->d_plut, ctx->d_sums,
+    HIPCHK(launch_mean_sums(ctx->stream, ctx->Dp, ctx->d_codes, ctx->N, ctx->D, ctx->d_plut, ctx->d_mean,
                             ctx->d_counters, 2 * 33 + 1, d_dist, ctx->xsq, (double)ctx->N));
     if (ctx->comm) NCCLCHK(ncclAllReduce(d_dist, d_dist, 2, ncclDouble, ncclSum, ctx->comm, ctx->stream));
-    if ((st = all_reduce_sums(ctx, 1)) != QVQ_OK) return st;
+    if ((st = all_reduce_sums(ctx, 1, ctx->d_mean)) != QVQ_OK) {
+        (void)hipMemsetAsync(ctx->d_mean, 0, (2 * 64 + 1) * 8, ctx->stream);   // keep it clear for the next call
+        return st;
+    }
     unsigned *dist_done = ctx->d_counters + 2 * 33;
     // finalize (+ split, tables, host codebook and its ready number) / final distortion
+    // (K = 1 reads the mean sums and leaves them cleared for the next quantize)
     auto finalize = [&](uint32_t K, bool split) {
         if (split) ctx->seq++;
-        return launch_finalize_prep(ctx->stream, ctx->d_sums, K, ctx->D, ctx->Dp, T.R, T.bias, T.scale,
+        return launch_finalize_prep(ctx->stream, K == 1 ? ctx->d_mean : ctx->d_sums, K, ctx->D, ctx->Dp, T.R, T.bias,
+                                    T.scale,
                                     ctx->d_C64_cent, split, ctx->d_C64_split, pad32(2 * K), T.mu, T.sx, ctx->mf_t,
                                     ctx->d_C32, ctx->d_rows, split ? ctx->dh_cb : nullptr, d_dist + 8, dist_done,
-                                    split ? nullptr : d_dist + 2, split ? ctx->dh_ready : nullptr, ctx->seq);
+                                    split ? nullptr : d_dist + 2, split ? ctx->dh_ready : nullptr, ctx->seq,
+                                    K == 1);
     };
     HIPCHK(finalize(1, bits > 0));
     // with bits >= 1 the first search writes every row's index
@@ -773,7 +783,7 @@ QVQ_API qvq_status qvq_lbg(qvq_ctx *ctx, uint32_t bits, double eps, double *code
     }
     // Returned distortion: updateDistortion after the last fix (src/Quantizer.cpp:9-22,103),
     // from the sums of the final assignment (finalize_prep_kernel without split).
-    HIPCHK(hipEventRecord(ctx->ev_end, ctx->stream));
+    if (ctx->timing_level == -1) HIPCHK(hipEventRecord(ctx->ev_end, ctx->stream));   // each record idles the GPU ~6 us
     // distortion inputs, per-level counters and the codebook go to mapped pinned memory in one
     // launch (the mapped split-codebook buffer is free once the last tree is built)
     double dres[3];

@@ -328,7 +328,8 @@ hipError_t launch_reduce(hipStream_t s, const uint64_t *part, const uint32_t *pa
 }
 
 // K = 1 (the mean initialisation, trainingSetSum, src/Quantizer.cpp:46-57): every row in
-// one cluster, so a register + LDS reduction; sums must be zeroed beforehand.  A thread takes
+// one cluster, so a register + LDS reduction; sums must be zero on entry (the engine's mean
+// buffer is cleared once at creation and again by the finalize that consumes it).  A thread takes
 // groups of 4 consecutive rows (4*DP bytes: DP/4 16-byte loads), two groups per trip so the
 // loads of both are in flight together, and adds each component's exact term as
 // (b ^ 0x80) << 16 | lo8[b] in u32 registers: the grid gives every thread at most 256 rows,
@@ -429,8 +430,6 @@ hipError_t launch_mean_sums(hipStream_t s, uint32_t Dp, const uint8_t *codes, ui
                             const uint64_t *plut, uint64_t *sums, unsigned *zero, uint32_t n_zero, double *dist,
                             double x0, double x1) {
     if (n_zero > MEAN_THREADS) return hipErrorInvalidValue;
-    const hipError_t e = hipMemsetAsync(sums, 0, (2 * (size_t)D + 1) * 8, s);
-    if (e != hipSuccess) return e;
     // one block per CU (few same-address atomics at the end), more only where a thread would
     // otherwise take over MEAN_ROWS_PER_THREAD rows (u32 fields)
     static const uint64_t grid_cap = std::getenv("QVQ_MEAN_GRID") ? std::atoll(std::getenv("QVQ_MEAN_GRID")) : 256;
@@ -507,6 +506,8 @@ struct FinArgs {
     _Float16 *rows;
     double *host_cb;
     bool dist;
+    uint64_t *zero_after;   // cleared by the last block once every block has read sums (mean)
+    uint32_t n_zero;
 };
 
 // One (row j, component lane d) item of the finalize; L lanes per row (16 when D == 12: the
@@ -590,7 +591,10 @@ __global__ __launch_bounds__(256) void finalize_prep_kernel(FinArgs a, double *_
     __shared__ double red[256];
     __shared__ bool last;
     red[threadIdx.x] = term;
-    if (a.host_cb) __threadfence_system();
+    // host_cb: every wave's mapped stores complete before the barrier, and thread 0's
+    // system-scope fence below releases them with the block's count (MI355X guide's
+    // producer pattern: one fence per block, not one per thread)
+    if (a.host_cb) __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     for (int w = 128; w > 0; w >>= 1) {
         if ((int)threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
@@ -598,12 +602,14 @@ __global__ __launch_bounds__(256) void finalize_prep_kernel(FinArgs a, double *_
     }
     if (threadIdx.x == 0) {
         dist_part[blockIdx.x] = red[0];
-        __threadfence();
+        if (a.host_cb) __threadfence_system();
+        else __threadfence();
         last = atomicAdd(done, 1u) == gridDim.x - 1;
     }
     __syncthreads();
     if (last && threadIdx.x == 0) {
         __threadfence();
+        for (uint32_t i = 0; i < a.n_zero; i++) a.zero_after[i] = 0;
         if (dist_out) {
             double t = 0;
             for (uint32_t b = 0; b < gridDim.x; b++) t += __builtin_nontemporal_load(&dist_part[b]);
@@ -639,19 +645,27 @@ static FinArgs fin_args(const uint64_t *sums, uint32_t K, uint32_t D, uint32_t D
     a.rows = cb_rows;
     a.host_cb = host_cb;
     a.dist = dist;
+    a.zero_after = nullptr;
+    a.n_zero = 0;
     return a;
 }
 
 hipError_t launch_finalize_prep(hipStream_t s, const uint64_t *sums, uint32_t K, uint32_t D, uint32_t Dp, int64_t R,
                                 int64_t bias, int scale, double *C_cent, bool split, double *C64n, uint32_t Kpad_next,
                                 double mu, double sx, int t, float *C32, _Float16 *cb_rows, double *host_cb,
-                                double *dist_part, unsigned *done, double *dist_out, uint64_t *ready, uint64_t seq) {
+                                double *dist_part, unsigned *done, double *dist_out, uint64_t *ready, uint64_t seq,
+                                bool zero_sums) {
     if (D == 0 || D > 64) return hipErrorInvalidValue;
+    if (zero_sums && !done) return hipErrorInvalidValue;   // the clearing is the last block's
     const uint32_t L = D <= 16 ? 16 : (D <= 32 ? 32 : 64);
     const uint32_t n = split ? std::max(2 * K, Kpad_next) : K;
     const uint32_t grid = std::min<uint32_t>((n + 256 / L - 1) / (256 / L), 512);   // <= dist_part capacity
-    const FinArgs a = fin_args(sums, K, D, Dp, R, bias, scale, C_cent, split, C64n, Kpad_next, mu, sx, t, C32, cb_rows,
-                               host_cb, dist_out != nullptr);
+    FinArgs a = fin_args(sums, K, D, Dp, R, bias, scale, C_cent, split, C64n, Kpad_next, mu, sx, t, C32, cb_rows,
+                         host_cb, dist_out != nullptr);
+    if (zero_sums) {
+        a.zero_after = const_cast<uint64_t *>(sums);
+        a.n_zero = 2 * K * D + K;
+    }
     hipLaunchKernelGGL(finalize_prep_kernel, dim3(grid), dim3(256), 0, s, a, dist_part, done, dist_out,
                        (volatile uint64_t *)ready, seq, L);
     return hipGetLastError();
@@ -661,7 +675,7 @@ hipError_t launch_finalize_prep(hipStream_t s, const uint64_t *sums, uint32_t K,
 hipError_t launch_finalize(hipStream_t s, const uint64_t *sums, uint32_t K, uint32_t D, int64_t R, int64_t bias,
                            int scale, double *C_cent) {
     return launch_finalize_prep(s, sums, K, D, (D + 3) & ~3u, R, bias, scale, C_cent, false, nullptr, 0, 0, 0, 0,
-                                nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, 0);
+                                nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, 0, false);
 }
 
 // Search tables from an fp64 codebook: fp32 [Kpad][Dp] (VALU path and the MFMA recompute)
