@@ -139,11 +139,18 @@ class Engine:
         return int(lib().qvq_dim(self._h))
 
     # -- hot path ------------------------------------------------------------------------
-    def lbg(self, bits, eps=1e-6, want_assign=True):
+    def lbg(self, bits, eps=1e-6, want_assign=True, out=None):
+        """Split-LBG to 2**bits code vectors: (codebook, indices or None, distortion).
+        out: optional (C, d) float64 arrays of shapes (2**bits, dim) and (1,) to fill instead of
+        allocating (repeated calls, e.g. bench.py)."""
         K = 1 << bits
-        C = np.empty((K, self.dim), np.float64)
+        if out is None:
+            C, d = np.empty((K, self.dim), np.float64), np.zeros(1, np.float64)
+        else:
+            C, d = out
+            assert C.shape == (K, self.dim) and C.dtype == np.float64 and C.flags.c_contiguous
+            assert d.shape == (1,) and d.dtype == np.float64
         A = np.empty(self.n, np.uint32) if want_assign else None
-        d = np.zeros(1, np.float64)
         _check(lib().qvq_lbg(self._h, bits, eps, _p(C), _p(A) if want_assign else None, _p(d)), self._h)
         return C, A, float(d[0])
 
@@ -166,6 +173,15 @@ class Engine:
     def set_timing(self, level=-1):
         """HIP events around the search of every level (-1), none (-2) or level+1 only."""
         _check(lib().qvq_set_timing(self._h, int(level)), self._h)
+
+    def level_timing(self, level):
+        """(search ms, update ms, flagged rows over all levels) of the last lbg, without
+        building the full timings() dict (bench.py reads this once per step)."""
+        t = getattr(self, "_tm", None)
+        if t is None:
+            t = self._tm = _Timings()
+        _check(lib().qvq_get_timings(self._h, ctypes.byref(t)), self._h)
+        return t.assign_ms[level], t.update_ms[level], sum(t.flagged[:max(t.levels, 1)])
 
     def timings(self):
         t = _Timings()

@@ -169,9 +169,11 @@ hipError_t launch_update(hipStream_t s, uint32_t Dp, uint32_t G, const uint8_t *
 hipError_t launch_reduce(hipStream_t s, const uint64_t *part, const uint32_t *part_cnt, uint32_t G, uint32_t nsub,
                          uint32_t K, uint32_t D, uint64_t *sums);
 // Up to three device ranges (sizes multiples of 4 bytes, 0 = unused) copied in one launch,
-// e.g. into mapped pinned host memory.
+// e.g. into mapped pinned host memory; with flag (mapped) the copy then publishes *flag = seq
+// (done: a block counter at 0, left at 0).
 hipError_t launch_copy_out(hipStream_t s, const void *src0, void *dst0, uint64_t bytes0, const void *src1, void *dst1,
-                           uint64_t bytes1, const void *src2, void *dst2, uint64_t bytes2);
+                           uint64_t bytes1, const void *src2, void *dst2, uint64_t bytes2, uint64_t *flag = nullptr,
+                           uint64_t seq = 0, unsigned *done = nullptr);
 // Mean sums (K = 1) into sums[0..2D]; also clears zero[0..n_zero) and sets dist[0..1] = x0, x1.
 hipError_t launch_mean_sums(hipStream_t s, uint32_t Dp, const uint8_t *codes, uint64_t N, uint32_t D,
                             const uint64_t *plut, uint64_t *sums, unsigned *zero, uint32_t n_zero, double *dist,

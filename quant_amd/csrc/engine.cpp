@@ -4,15 +4,15 @@
 //
 // Per split level (LBGIterate, src/Quantizer.cpp:98-108, one effective Lloyd step), all on
 // one stream with no host round trip:
-//   D == 12, K <= mf_fuse_max_k():  prep -> assign_mfma<fused sums> -> reduce
-//                                   -> recheck(+sums, device kd-tree for exact ties)
-//                                   -> [all-reduce] -> finalize+split
-//   otherwise:                      prep -> assign (MFMA or VALU) -> recheck -> update
-//                                   -> reduce -> [all-reduce] -> finalize+split
-// While the GPU runs a level's assign, the host builds the reference kd-tree over that
-// level's codebook (downloaded on a copy stream after the previous finalize) and uploads
-// it for the recheck.  A tree deeper than the device stack falls back to a synchronous
-// host resolution of the tie rows (resolve_host_ties).
+//   D == 12, K <= mf_fuse_max_k():  search (fused exact sums) -> recheck -> kd_resolve
+//                                   -> reduce -> [all-reduce] -> finalize+split+tables
+//   otherwise:                      search (MFMA or VALU) -> recheck -> kd_resolve -> update
+//                                   -> reduce -> [all-reduce] -> finalize+split+tables
+// While the GPU runs a level's search, the host builds the reference kd-tree over that
+// level's codebook (which the previous finalize wrote to mapped memory) for kd_resolve.  A
+// tree too large for the kernel's LDS falls back to a synchronous host resolution of the tie
+// rows (resolve_host_ties).  A quantize starts with the mean kernel and ends with one
+// copy_out launch into mapped memory, whose completion flag the host polls.
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
@@ -88,7 +88,7 @@ struct qvq_ctx {
     double *d_lut64 = nullptr;
     uint64_t *d_plut = nullptr;
     uint32_t *d_A = nullptr, *d_flags = nullptr, *d_ties = nullptr;
-    unsigned *d_counters = nullptr;   // per level: [2l] flagged rows, [2l+1] kd-tree ties
+    unsigned *d_counters = nullptr;   // per level: [2l] flagged rows, [2l+1] kd-tree ties; [66], [67] block counters
     double xsq = 0;                   // sum over rows of ||x||^2 (closed-form distortion)
     uint64_t *d_hist = nullptr;
 
@@ -102,6 +102,7 @@ struct qvq_ctx {
     uint32_t *d_part_cnt = nullptr;
     double *d_dist_part = nullptr;
     uint64_t *d_mean = nullptr;   // mean sums [hi D][lo D][n]: zero between quantizes (the finalize clears it)
+    uint64_t out_seq = 0;         // quantizes whose results copy_out has published
     uint32_t *d_scatter = nullptr;
     uint64_t scatter_bytes = 0;
     // mapped pinned host memory (coherent): the split codebook finalize writes for the
@@ -390,19 +391,19 @@ void build_tree(qvq_ctx *ctx, const double *hC, uint32_t K, int buf, KdView &kd)
     kd = v;
 }
 
-// Wait until finalize has published codebook seq in h_cb.  Polls the mapped flag; a stream
-// error or a drained stream without the flag ends the wait with an error (never hangs).
-qvq_status wait_codebook(qvq_ctx *ctx, uint64_t seq) {
+// Wait until the stream has published seq in a mapped flag (the ready number of finalize's
+// codebook in h_cb, or copy_out's completion).  Polls the flag; a stream error or a drained
+// stream without the flag ends the wait with an error (never hangs).
+qvq_status wait_flag(qvq_ctx *ctx, volatile uint64_t *flag, uint64_t seq) {
     // hipStreamQuery submits a marker (a few us of GPU idle), so the stream is consulted
     // only every ~20 ms of waiting, to catch a failed or drained stream
-    volatile uint64_t *flag = ctx->h_ready;
     auto next_check = std::chrono::steady_clock::now() + std::chrono::milliseconds(20);
     while (*flag < seq) {
         if (std::chrono::steady_clock::now() < next_check) continue;
         const hipError_t q = hipStreamQuery(ctx->stream);
         if (q == hipSuccess) {
             if (*flag >= seq) break;
-            return fail(ctx, QVQ_EDEVICE, "finalize finished without publishing the codebook");
+            return fail(ctx, QVQ_EDEVICE, "the stream finished without publishing its flag");
         }
         if (q != hipErrorNotReady) return fail(ctx, QVQ_EDEVICE, std::string("stream: ") + hipGetErrorString(q));
         next_check = std::chrono::steady_clock::now() + std::chrono::milliseconds(20);
@@ -410,6 +411,7 @@ qvq_status wait_codebook(qvq_ctx *ctx, uint64_t seq) {
     std::atomic_thread_fence(std::memory_order_acquire);
     return QVQ_OK;
 }
+qvq_status wait_codebook(qvq_ctx *ctx, uint64_t seq) { return wait_flag(ctx, ctx->h_ready, seq); }
 
 // Tie rows listed by the recheck when no device tree was available: answer them with the
 // host tree over hC and write A; with accumulate their terms move from the search's
@@ -585,7 +587,7 @@ QVQ_API qvq_status qvq_create(int hip_device, qvq_ctx **out) {
     *ctx->h_ready = 0;
     if ((e = hipHostGetDevicePointer((void **)&ctx->dh_ready, ctx->h_ready, 0)) != hipSuccess)
         return bail(e, "hipHostGetDevicePointer");
-    if ((e = hipMalloc(&ctx->d_counters, (2 * 33 + 1) * sizeof(unsigned))) != hipSuccess) return bail(e, "hipMalloc");
+    if ((e = hipMalloc(&ctx->d_counters, (2 * 33 + 2) * sizeof(unsigned))) != hipSuccess) return bail(e, "hipMalloc");
     if ((e = hipMalloc(&ctx->d_hist, 256 * 8)) != hipSuccess) return bail(e, "hipMalloc");
     if ((e = hipMalloc(&ctx->d_dist_part, 8192 * 8)) != hipSuccess) return bail(e, "hipMalloc");
     if ((e = hipMalloc(&ctx->d_mean, (2 * 64 + 1) * 8)) != hipSuccess) return bail(e, "hipMalloc");
@@ -747,7 +749,7 @@ QVQ_API qvq_status qvq_lbg(qvq_ctx *ctx, uint32_t bits, double eps, double *code
     // closed-form distortion (summed over all ranks below).
     double *d_dist = ctx->d_dist_part;
     HIPCHK(launch_mean_sums(ctx->stream, ctx->Dp, ctx->d_codes, ctx->N, ctx->D, ctx->d_plut, ctx->d_mean,
-                            ctx->d_counters, 2 * 33 + 1, d_dist, ctx->xsq, (double)ctx->N));
+                            ctx->d_counters, 2 * 33 + 2, d_dist, ctx->xsq, (double)ctx->N));
     if (ctx->comm) NCCLCHK(ncclAllReduce(d_dist, d_dist, 2, ncclDouble, ncclSum, ctx->comm, ctx->stream));
     if ((st = all_reduce_sums(ctx, 1, ctx->d_mean)) != QVQ_OK) {
         (void)hipMemsetAsync(ctx->d_mean, 0, (2 * 64 + 1) * 8, ctx->stream);   // keep it clear for the next call
@@ -793,10 +795,20 @@ QVQ_API qvq_status qvq_lbg(qvq_ctx *ctx, uint32_t bits, double eps, double *code
         uint8_t *dh_small = reinterpret_cast<uint8_t *>(ctx->dh_ready) + 64;
         static_assert(sizeof(dres) + sizeof(stats) <= 1024 - 64, "small results exceed the mapped area");
         const uint64_t cb_bytes = codebook ? (uint64_t)Kmax * ctx->D * 8 : 0;
+        // without assign the copy's own flag ends the wait: polling it wakes the host at once,
+        // where a stream synchronize costs tens of us of wake-up
+        uint64_t *done = assign ? nullptr : reinterpret_cast<uint64_t *>(dh_small + (1024 - 64 - 8));
+        const uint64_t seq = ++ctx->out_seq;
         HIPCHK(launch_copy_out(ctx->stream, d_dist, dh_small, sizeof(dres), ctx->d_counters, dh_small + sizeof(dres),
-                               sizeof(stats), ctx->d_C64_cent, ctx->dh_cb, cb_bytes));
-        if (assign) HIPCHK(hipMemcpyAsync(assign, ctx->d_A, ctx->N * 4, hipMemcpyDeviceToHost, ctx->stream));
-        HIPCHK(hipStreamSynchronize(ctx->stream));
+                               sizeof(stats), ctx->d_C64_cent, ctx->dh_cb, cb_bytes, done, seq,
+                               ctx->d_counters + 2 * 33 + 1));
+        if (assign) {
+            HIPCHK(hipMemcpyAsync(assign, ctx->d_A, ctx->N * 4, hipMemcpyDeviceToHost, ctx->stream));
+            HIPCHK(hipStreamSynchronize(ctx->stream));
+        } else {
+            qvq_status ws = wait_flag(ctx, reinterpret_cast<volatile uint64_t *>(h_small + (1024 - 64 - 8)), seq);
+            if (ws != QVQ_OK) return ws;
+        }
         std::memcpy(dres, h_small, sizeof(dres));
         std::memcpy(stats, h_small + sizeof(dres), sizeof(stats));
         if (codebook) std::memcpy(codebook, ctx->h_cb, cb_bytes);
@@ -807,8 +819,15 @@ QVQ_API qvq_status qvq_lbg(qvq_ctx *ctx, uint32_t bits, double eps, double *code
         // level up to the next level's search (recheck, kd-tree, reduce, finalize, tables)
         float a = 0, u = 0, whole = 0;
         const bool timed = ctx->timing_level == -1 || ctx->timing_level == (int)lvl - 1;
-        if (timed) (void)hipEventElapsedTime(&a, ctx->ev[lvl - 1][0], ctx->ev[lvl - 1][1]);
-        if (ctx->upd[lvl - 1]) (void)hipEventElapsedTime(&u, ctx->ev[lvl - 1][2], ctx->ev[lvl - 1][3]);
+        if (timed) {
+            (void)hipEventSynchronize(ctx->ev[lvl - 1][1]);   // complete; the runtime may not know yet
+            (void)hipEventElapsedTime(&a, ctx->ev[lvl - 1][0], ctx->ev[lvl - 1][1]);
+        }
+        if (ctx->upd[lvl - 1]) {
+            (void)hipEventSynchronize(ctx->ev[lvl - 1][3]);
+            (void)hipEventElapsedTime(&u, ctx->ev[lvl - 1][2], ctx->ev[lvl - 1][3]);
+        }
+        if (ctx->timing_level == -1) (void)hipEventSynchronize(ctx->ev_end);
         if (ctx->timing_level == -1)
             (void)hipEventElapsedTime(&whole, ctx->ev[lvl - 1][0], lvl < bits ? ctx->ev[lvl][0] : ctx->ev_end);
         ctx->tm.assign_ms[lvl - 1] = a;

@@ -890,6 +890,7 @@ __global__ __launch_bounds__(RECHECK_THREADS) void recheck_kernel(
     // two-deep prefetch: row index of f + fstride, bytes of row f
     uint32_t row = f < nflag ? flags[f] : 0;
     uint32_t byte = (f < nflag && lane < (int)D) ? codes[(uint64_t)row * Dp + lane] : 0;
+    uint32_t arow = f < nflag ? A[row] : 0;   // the search's index (only this wave writes it)
     uint32_t row_n = f + fstride < nflag ? flags[f + fstride] : 0;
     for (uint32_t i = threadIdx.x; i < 256; i += RECHECK_THREADS) lut[i] = lut64[i];
     if (STAGED) {
@@ -904,9 +905,10 @@ __global__ __launch_bounds__(RECHECK_THREADS) void recheck_kernel(
     float *xr = x32 + wave * 64;
     auto within = [&](float d, float m) { return d - m <= 2.f * (alpha * sqrtf(d) + beta * d) + gamma; };
     for (; f < nflag; f += fstride) {
-        const uint32_t crow = row, cbyte = byte;
+        const uint32_t crow = row, cbyte = byte, carow = arow;
         row = row_n;
         byte = (f + fstride < nflag && lane < (int)D) ? codes[(uint64_t)row * Dp + lane] : 0;
+        arow = f + fstride < nflag ? A[row] : 0;
         row_n = f + 2 * fstride < nflag ? flags[f + 2 * fstride] : 0;
         const double v = lane < (int)D ? lut[cbyte] : 0.0;
         xw[lane] = v;
@@ -945,9 +947,8 @@ __global__ __launch_bounds__(RECHECK_THREADS) void recheck_kernel(
             kb = d < b1 ? k : kb;
             b1 = min2f(b1, d);
         }
-        float m = b1;
-#pragma unroll
-        for (int off = 32; off >= 1; off >>= 1) m = fminf(m, __shfl_xor(m, off));
+        // distances are >= 0, so their bit patterns order like the values
+        const float m = __uint_as_float(wave_min_u32(__float_as_uint(b1)));
         double d1 = INFINITY, d2 = INFINITY;
         uint32_t k1 = 0xFFFFFFFFu;
         auto take = [&](uint32_t k) {
@@ -966,24 +967,20 @@ __global__ __launch_bounds__(RECHECK_THREADS) void recheck_kernel(
         } else if (within(b1, m)) {
             take(kb);
         }
-#pragma unroll
-        for (int off = 32; off >= 1; off >>= 1) {
-            const double od1 = __shfl_xor(d1, off);
-            const double od2 = __shfl_xor(d2, off);
-            const uint32_t ok1 = __shfl_xor(k1, off);
-            if (od1 < d1 || (od1 == d1 && ok1 < k1)) {
-                d2 = fmin(od2, d1);
-                d1 = od1;
-                k1 = ok1;
-            } else {
-                d2 = fmin(d2, od1);
-            }
+        {   // wave merge on DPP: (d1, k1) the lexicographic minimum; d2 the second-smallest
+            // candidate, i.e. the winner lane's d2 or any other lane's d1
+            const double m1 = wave_min_f64<4>(d1);
+            const uint32_t mk = wave_min_u32(d1 == m1 ? k1 : 0xFFFFFFFFu);
+            const bool win = d1 == m1 && k1 == mk;
+            d2 = wave_min_f64<4>(win ? d2 : d1);
+            d1 = m1;
+            k1 = mk;
         }
         if (d2 - d1 <= tie_rel * d1) {   // exact tie for the reference: the kd-tree decides
             if (lane == 0) ties[atomicAdd(tie_cnt, 1u)] = crow;   // A keeps the provisional index
         } else {
             // the search's index (its terms are in the slabs when fused); mostly unchanged
-            const uint32_t from = __builtin_amdgcn_readfirstlane(A[crow]);
+            const uint32_t from = __builtin_amdgcn_readfirstlane(carow);
             if (k1 != from) {
                 if (xslab) move_row_terms(codes, Dp, D, crow, from, k1, K, xslab, xcnt, plut, lane);
                 if (lane == 0) A[crow] = k1;
@@ -1025,36 +1022,6 @@ hipError_t launch_recheck(hipStream_t s, int num_cu, const uint8_t *codes, uint3
     }
 #undef QVQ_RC
     return hipGetLastError();
-}
-
-// fp64 minimum over the wave (or over lanes 0..15 with ROWS = 1) by DPP steps on the two
-// dword halves: VALU-only, no LDS round trips on the walk's serial path.  Uniform result.
-template <int CTRL, int ROW_MASK>
-__device__ inline double dpp_min_step(double v) {
-    const uint64_t b = (uint64_t)__double_as_longlong(v);
-    constexpr uint64_t inf = 0x7FF0000000000000ull;   // what lanes without a source read
-    const uint32_t lo = (uint32_t)__builtin_amdgcn_update_dpp((int)(uint32_t)inf, (int)(uint32_t)b, CTRL, ROW_MASK,
-                                                              0xF, false);
-    const uint32_t hi = (uint32_t)__builtin_amdgcn_update_dpp((int)(uint32_t)(inf >> 32), (int)(uint32_t)(b >> 32),
-                                                              CTRL, ROW_MASK, 0xF, false);
-    return fmin(v, __longlong_as_double((long long)(((uint64_t)hi << 32) | lo)));
-}
-template <int ROWS>
-__device__ inline double wave_min_f64(double v) {
-    v = dpp_min_step<0x111, 0xF>(v);   // row_shr:1
-    v = dpp_min_step<0x112, 0xF>(v);   // row_shr:2
-    v = dpp_min_step<0x114, 0xF>(v);   // row_shr:4
-    v = dpp_min_step<0x118, 0xF>(v);   // row_shr:8: lane 15 of each row holds the row's
-    int src = 15;
-    if (ROWS > 1) {
-        v = dpp_min_step<0x142, 0xA>(v);   // row_bcast:15 into rows 1, 3
-        v = dpp_min_step<0x143, 0xC>(v);   // row_bcast:31 into rows 2, 3
-        src = 63;
-    }
-    const uint64_t b = (uint64_t)__double_as_longlong(v);
-    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)b, src);
-    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(b >> 32), src);
-    return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
 }
 
 // kd_nearest_flat with the leaf scan spread over the wave: every lane runs the same

@@ -460,6 +460,9 @@ struct CopySeg {
 };
 struct CopySegs {
     CopySeg seg[3];
+    uint64_t *flag;   // with a flag: the last block to finish publishes seq (mapped memory)
+    uint64_t seq;
+    unsigned *done;   // block counter for that (0 on entry, left at 0)
 };
 __global__ __launch_bounds__(256) void copy_out_kernel(CopySegs a) {
 #pragma unroll
@@ -468,15 +471,33 @@ __global__ __launch_bounds__(256) void copy_out_kernel(CopySegs a) {
         for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < c.words; i += (uint64_t)gridDim.x * 256)
             c.dst[i] = c.src[i];
     }
+    if (a.flag) {   // every wave's stores complete, one system-scope release per block, and
+                    // the last block to count itself in publishes the flag
+        __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            __threadfence_system();
+            if (atomicAdd(a.done, 1u) == gridDim.x - 1) {
+                *a.done = 0;
+                __threadfence_system();
+                *reinterpret_cast<volatile uint64_t *>(a.flag) = a.seq;
+            }
+        }
+    }
 }
 
 hipError_t launch_copy_out(hipStream_t s, const void *src0, void *dst0, uint64_t bytes0, const void *src1, void *dst1,
-                           uint64_t bytes1, const void *src2, void *dst2, uint64_t bytes2) {
+                           uint64_t bytes1, const void *src2, void *dst2, uint64_t bytes2, uint64_t *flag,
+                           uint64_t seq, unsigned *done) {
+    if (flag && !done) return hipErrorInvalidValue;
     if ((bytes0 | bytes1 | bytes2) & 3) return hipErrorInvalidValue;
     CopySegs a;
     a.seg[0] = {static_cast<const uint32_t *>(src0), static_cast<uint32_t *>(dst0), bytes0 / 4};
     a.seg[1] = {static_cast<const uint32_t *>(src1), static_cast<uint32_t *>(dst1), bytes1 / 4};
     a.seg[2] = {static_cast<const uint32_t *>(src2), static_cast<uint32_t *>(dst2), bytes2 / 4};
+    a.flag = flag;
+    a.seq = seq;
+    a.done = done;
     const uint64_t words = std::max(bytes0, std::max(bytes1, bytes2)) / 4;
     const int grid = (int)std::min<uint64_t>(std::max<uint64_t>((words + 255) / 256, 1), 256);
     hipLaunchKernelGGL(copy_out_kernel, dim3(grid), dim3(256), 0, s, a);

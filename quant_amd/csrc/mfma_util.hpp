@@ -90,6 +90,51 @@ __device__ inline uint32_t wave_scan_max(uint32_t v) {
     return v;
 }
 
+// fp64 minimum over the wave (or over lanes 0..15 with ROWS = 1) by DPP steps on the two
+// dword halves: VALU-only, no LDS round trips on the walk's serial path.  Uniform result.
+template <int CTRL, int ROW_MASK>
+__device__ inline double dpp_min_step(double v) {
+    const uint64_t b = (uint64_t)__double_as_longlong(v);
+    constexpr uint64_t inf = 0x7FF0000000000000ull;   // what lanes without a source read
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_update_dpp((int)(uint32_t)inf, (int)(uint32_t)b, CTRL, ROW_MASK,
+                                                              0xF, false);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_update_dpp((int)(uint32_t)(inf >> 32), (int)(uint32_t)(b >> 32),
+                                                              CTRL, ROW_MASK, 0xF, false);
+    return fmin(v, __longlong_as_double((long long)(((uint64_t)hi << 32) | lo)));
+}
+template <int ROWS>
+__device__ inline double wave_min_f64(double v) {
+    v = dpp_min_step<0x111, 0xF>(v);   // row_shr:1
+    v = dpp_min_step<0x112, 0xF>(v);   // row_shr:2
+    v = dpp_min_step<0x114, 0xF>(v);   // row_shr:4
+    v = dpp_min_step<0x118, 0xF>(v);   // row_shr:8: lane 15 of each row holds the row's
+    int src = 15;
+    if (ROWS > 1) {
+        v = dpp_min_step<0x142, 0xA>(v);   // row_bcast:15 into rows 1, 3
+        v = dpp_min_step<0x143, 0xC>(v);   // row_bcast:31 into rows 2, 3
+        src = 63;
+    }
+    const uint64_t b = (uint64_t)__double_as_longlong(v);
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)b, src);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(b >> 32), src);
+    return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
+}
+
+// u32 minimum over the wave by DPP steps (lanes without a source read ~0); uniform.
+template <int CTRL, int ROW_MASK>
+__device__ inline uint32_t dpp_min_u32_step(uint32_t v) {
+    return min(v, (uint32_t)__builtin_amdgcn_update_dpp((int)0xFFFFFFFFu, (int)v, CTRL, ROW_MASK, 0xF, false));
+}
+__device__ inline uint32_t wave_min_u32(uint32_t v) {
+    v = dpp_min_u32_step<0x111, 0xF>(v);   // row_shr:1
+    v = dpp_min_u32_step<0x112, 0xF>(v);   // row_shr:2
+    v = dpp_min_u32_step<0x114, 0xF>(v);   // row_shr:4
+    v = dpp_min_u32_step<0x118, 0xF>(v);   // row_shr:8
+    v = dpp_min_u32_step<0x142, 0xA>(v);   // row_bcast:15 into rows 1, 3
+    v = dpp_min_u32_step<0x143, 0xC>(v);   // row_bcast:31 into rows 2, 3
+    return (uint32_t)__builtin_amdgcn_readlane((int)v, 63);
+}
+
 // Centred integer of a byte: w = 2*((int8)b + 128) - 255 = 2*(b ^ 0x80) - 255 (both colour
 // spaces), so v(b) = mu + w*sx.  Exact in f16.
 __device__ inline float byte_w(uint32_t word, int j) {
