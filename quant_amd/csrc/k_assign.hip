@@ -93,7 +93,7 @@ constexpr int MF_SMALL_K = 32;
 // SK > 0 (K <= SK <= MF_SMALL_K, SK a power of two): no MFMA at all -- each lane scans SK
 // code vectors of its row (rows K..SK-1 are zero padding and masked) in the direct fp32 form
 // (the recompute below), cheaper than the MFMA pass's per-chunk fixed work at this size.
-template <bool FUSE, bool STAGED, int SK>
+template <bool FUSE, bool STAGED, int SK, bool U4>
 __global__ __launch_bounds__(MF_THREADS) void assign_mfma_kernel(
     const uint8_t *__restrict__ codes, uint64_t N, const _Float16 *__restrict__ g_rows, uint32_t K,
     const float *__restrict__ g_C32, const uint64_t *__restrict__ g_plut, MfThresholds th, uint32_t *__restrict__ A,
@@ -230,21 +230,21 @@ __global__ __launch_bounds__(MF_THREADS) void assign_mfma_kernel(
             mfma_pair(qa0, qa1);
             next_a(pr + 1);
 #pragma unroll
-            for (int t = 0; t < MF_TILES; t++) pair_update(pa0[t], pa1[t], pr - 1, b1[t], b2[t], bp[t]);
+            for (int t = 0; t < MF_TILES; t++) unit_update<U4>(pa0[t], pa1[t], pr - 1, b1[t], b2[t], bp[t]);
             mfma_pair(pa0, pa1);
             next_a(pr + 2);
 #pragma unroll
-            for (int t = 0; t < MF_TILES; t++) pair_update(qa0[t], qa1[t], pr, b1[t], b2[t], bp[t]);
+            for (int t = 0; t < MF_TILES; t++) unit_update<U4>(qa0[t], qa1[t], pr, b1[t], b2[t], bp[t]);
         }
         if (pr < npairs) {   // npairs even: one pair left
             mfma_pair(qa0, qa1);
 #pragma unroll
-            for (int t = 0; t < MF_TILES; t++) pair_update(pa0[t], pa1[t], pr - 1, b1[t], b2[t], bp[t]);
+            for (int t = 0; t < MF_TILES; t++) unit_update<U4>(pa0[t], pa1[t], pr - 1, b1[t], b2[t], bp[t]);
 #pragma unroll
-            for (int t = 0; t < MF_TILES; t++) pair_update(qa0[t], qa1[t], pr, b1[t], b2[t], bp[t]);
+            for (int t = 0; t < MF_TILES; t++) unit_update<U4>(qa0[t], qa1[t], pr, b1[t], b2[t], bp[t]);
         } else {
 #pragma unroll
-            for (int t = 0; t < MF_TILES; t++) pair_update(pa0[t], pa1[t], pr - 1, b1[t], b2[t], bp[t]);
+            for (int t = 0; t < MF_TILES; t++) unit_update<U4>(pa0[t], pa1[t], pr - 1, b1[t], b2[t], bp[t]);
         }
 
 #elif QVQ_MF_LOOP == 1
@@ -271,7 +271,7 @@ __global__ __launch_bounds__(MF_THREADS) void assign_mfma_kernel(
             a0 = load_a(2 * pn);
             a1 = load_a(2 * pn + 1);
 #pragma unroll
-            for (int t = 0; t < MF_TILES; t++) pair_update(pa0[t], pa1[t], pr - 1, b1[t], b2[t], bp[t]);
+            for (int t = 0; t < MF_TILES; t++) unit_update<U4>(pa0[t], pa1[t], pr - 1, b1[t], b2[t], bp[t]);
 #pragma unroll
             for (int t = 0; t < MF_TILES; t++) {
                 pa0[t] = qa0[t];
@@ -279,7 +279,7 @@ __global__ __launch_bounds__(MF_THREADS) void assign_mfma_kernel(
             }
         }
 #pragma unroll
-        for (int t = 0; t < MF_TILES; t++) pair_update(pa0[t], pa1[t], npairs - 1, b1[t], b2[t], bp[t]);
+        for (int t = 0; t < MF_TILES; t++) unit_update<U4>(pa0[t], pa1[t], npairs - 1, b1[t], b2[t], bp[t]);
 
 #else
         // Tile pairs, ping-pong: the MFMAs of pair i overlap the epilogue of pair i-1.
@@ -301,7 +301,7 @@ __global__ __launch_bounds__(MF_THREADS) void assign_mfma_kernel(
                 qa1[t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a1, b[t], zero, 0, 0, 0);
             }
 #pragma unroll
-            for (int t = 0; t < MF_TILES; t++) pair_update(pa0[t], pa1[t], pr - 1, b1[t], b2[t], bp[t]);
+            for (int t = 0; t < MF_TILES; t++) unit_update<U4>(pa0[t], pa1[t], pr - 1, b1[t], b2[t], bp[t]);
 #pragma unroll
             for (int t = 0; t < MF_TILES; t++) {
                 pa0[t] = qa0[t];
@@ -309,7 +309,7 @@ __global__ __launch_bounds__(MF_THREADS) void assign_mfma_kernel(
             }
         }
 #pragma unroll
-        for (int t = 0; t < MF_TILES; t++) pair_update(pa0[t], pa1[t], npairs - 1, b1[t], b2[t], bp[t]);
+        for (int t = 0; t < MF_TILES; t++) unit_update<U4>(pa0[t], pa1[t], npairs - 1, b1[t], b2[t], bp[t]);
 
 #endif
         // Combine the four lanes of each data row (groups g = 0..3 of every tile) on MFMA
@@ -367,7 +367,7 @@ __global__ __launch_bounds__(MF_THREADS) void assign_mfma_kernel(
                 x[d] = e + th.mu;
             }
             float r1 = INFINITY, r2 = INFINITY;
-            const uint32_t pr = unit >> 2, gg = unit & 3;
+            const uint32_t pr = unit >> 2, gg = unit & 3;   // pair (tile with U4), lane group
 #ifdef QVQ_ABL_NORECOMP   // timing ablation only (wrong results): no recompute, no flags
             constexpr bool skip = !SMALLK;
             rk = (2 * pr) * 16 + 4 * gg;
@@ -379,11 +379,13 @@ __global__ __launch_bounds__(MF_THREADS) void assign_mfma_kernel(
             // a unit is 4 code vectors of each tile of its pair; up to K = 16 the second
             // tile is padding, and below 4 so is the rest of the first
             // SMALLK: the unit is the whole codebook
-            const int jn = SMALLK ? SK : (K <= 16 ? (K < 4 ? (int)K : 4) : 8);
+            // U4: a unit is 4 code vectors of one tile
+            const int jn = SMALLK ? SK : ((U4 || K <= 16) ? (K < 4 ? (int)K : 4) : 8);
 #pragma unroll
-            for (int j = 0; j < (SMALLK ? SK : 8); j++) {
+            for (int j = 0; j < (SMALLK ? SK : (U4 ? 4 : 8)); j++) {
                 if (skip || (!SMALLK && j >= jn)) continue;   // uniform: K is
-                const uint32_t cv = SMALLK ? (uint32_t)j : (2 * pr + (j >> 2)) * 16 + 4 * gg + (j & 3);
+                const uint32_t cv = SMALLK ? (uint32_t)j
+                                           : (U4 ? pr * 16 + 4 * gg + j : (2 * pr + (j >> 2)) * 16 + 4 * gg + (j & 3));
                 const float4 *c4 = reinterpret_cast<const float4 *>(C32 + (size_t)cv * MF_D);
                 float dist = 0.f;
 #pragma unroll
@@ -617,12 +619,12 @@ __global__ __launch_bounds__(MF_THREADS) void assign_small_kernel(
     }
 }
 
-template <bool F, bool S, int SK>
+template <bool F, bool S, int SK, bool U4>
 static void launch_mfma_variant(hipStream_t s, int grid, size_t lds, const uint8_t *codes, uint64_t N,
                                 const _Float16 *cb_rows, uint32_t K, const float *C32, const uint64_t *plut,
                                 const MfThresholds &th, uint32_t *A, uint32_t *flags, unsigned *flag_cnt,
                                 uint64_t *part, uint32_t *part_cnt) {
-    auto kern = assign_mfma_kernel<F, S, SK>;
+    auto kern = assign_mfma_kernel<F, S, SK, U4>;
     hipLaunchKernelGGL(kern, dim3(grid), dim3(MF_THREADS), lds, s, codes, N, cb_rows, K, C32, plut, th, A, flags,
                        flag_cnt, part, part_cnt);
 }
@@ -669,10 +671,16 @@ hipError_t launch_assign_mfma(hipStream_t s, int grid, bool fuse, const uint8_t 
 #undef QVQ_SMALL
         return hipGetLastError();
     }
+    // 4-code-vector units while the pair loop is short (the recompute dominates): up to
+    // K = QVQ_U4_MAXK (default 256)
+    static const uint32_t u4_max = std::getenv("QVQ_U4_MAXK") ? (uint32_t)std::atoi(std::getenv("QVQ_U4_MAXK")) : 256;
+    const bool u4 = K <= u4_max;
     if (fuse) {
-        fn = staged ? launch_mfma_variant<true, true, 0> : launch_mfma_variant<true, false, 0>;
+        if (u4) fn = staged ? launch_mfma_variant<true, true, 0, true> : launch_mfma_variant<true, false, 0, true>;
+        else fn = staged ? launch_mfma_variant<true, true, 0, false> : launch_mfma_variant<true, false, 0, false>;
     } else {
-        fn = staged ? launch_mfma_variant<false, true, 0> : launch_mfma_variant<false, false, 0>;
+        if (u4) fn = staged ? launch_mfma_variant<false, true, 0, true> : launch_mfma_variant<false, false, 0, true>;
+        else fn = staged ? launch_mfma_variant<false, true, 0, false> : launch_mfma_variant<false, false, 0, false>;
     }
     fn(s, grid, lds, codes, N, cb_rows, K, C32, plut, th, A, flags, flag_cnt, part, part_cnt);
     return hipGetLastError();

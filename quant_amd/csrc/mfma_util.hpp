@@ -165,6 +165,27 @@ __device__ inline void pair_update(const f32x4 &p0, const f32x4 &p1, uint32_t pa
     b1 = min2f(b1, m);
 }
 
+// One code tile for one data tile: minimum of the lane's 4 scores, then the running best tile,
+// best score and second-best tile minimum.
+__device__ inline void tile_update(const f32x4 &p, uint32_t tile, float &b1, float &b2, uint32_t &bt) {
+    const float m = min2f(min3f(p[0], p[1], p[2]), p[3]);
+    b2 = med3f(b1, b2, m);
+    bt = m < b1 ? tile : bt;
+    b1 = min2f(b1, m);
+}
+// The search's unit update: 8-code-vector units (a tile pair) or, with U4, 4-code-vector
+// units (one tile; bp then counts tiles) -- half the recompute for 4 more VALU per pair.
+template <bool U4>
+__device__ inline void unit_update(const f32x4 &p0, const f32x4 &p1, uint32_t pair, float &b1, float &b2,
+                                   uint32_t &bp) {
+    if constexpr (U4) {
+        tile_update(p0, 2 * pair, b1, b2, bp);
+        tile_update(p1, 2 * pair + 1, b1, b2, bp);
+    } else {
+        pair_update(p0, p1, pair, b1, b2, bp);
+    }
+}
+
 // Same, keeping the best two pairs (b1 at bp, b2 at bq) and the third-best minimum b3.
 __device__ inline void pair_update2(const f32x4 &p0, const f32x4 &p1, uint32_t pair, float &b1, float &b2, float &b3,
                                     uint32_t &bp, uint32_t &bq) {
