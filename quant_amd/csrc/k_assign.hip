@@ -863,28 +863,36 @@ __device__ inline float d32_row(const float *__restrict__ xr, const float *__res
     return acc;   // padding components are 0 in both x and c
 }
 
-// ref_l2_hd for D = 12 against a code vector in global memory: the row's six 16-byte loads
-// are issued together (the generic loop waits for each group of four), then the reference's
-// order: per group of four (e1^2 + e2^2) + (e0^2 + e3^2), groups added in turn.
-struct Row12 {
-    double2 v[6];
+// ref_l2_hd for D = N (12) against a code vector in global memory: the row's N/2 16-byte
+// loads are issued together (the generic loop waits for each group of four), then the
+// reference's order: per group of four (e1^2 + e2^2) + (e0^2 + e3^2), groups added in turn.
+template <int N>
+struct RowN {
+    double2 v[N / 2];
 };
-__device__ inline Row12 load_row12(const double *c) {
-    Row12 r;
+template <int N>
+__device__ inline RowN<N> load_row(const double *c) {
+    RowN<N> r;
     const double2 *p = reinterpret_cast<const double2 *>(c);
 #pragma unroll
-    for (int i = 0; i < 6; i++) r.v[i] = p[i];
+    for (int i = 0; i < N / 2; i++) r.v[i] = p[i];
     return r;
 }
-__device__ inline double ref_l2_12(const double *a, const Row12 &c) {
+template <int N>
+__device__ inline double ref_l2_n(const double *a, const RowN<N> &c) {
     double r = 0;
 #pragma unroll
-    for (int g = 0; g < 3; g++) {
+    for (int g = 0; g < N / 4; g++) {
         const double e0 = a[4 * g] - c.v[2 * g].x, e1 = a[4 * g + 1] - c.v[2 * g].y;
         const double e2 = a[4 * g + 2] - c.v[2 * g + 1].x, e3 = a[4 * g + 3] - c.v[2 * g + 1].y;
         r += (e1 * e1 + e2 * e2) + (e0 * e0 + e3 * e3);
     }
     return r;
+}
+// fp64 reference distance of row a (LDS) to code vector k of C64 (global), any D
+__device__ inline double ref_l2_cv(const double *a, const double *C64, uint32_t k, uint32_t D) {
+    if (D == 12) return ref_l2_n<12>(a, load_row<12>(C64 + (uint64_t)k * 12));
+    return ref_l2_hd(a, C64 + (uint64_t)k * D, (int)D);   // (a D = 48 row in registers costs the recheck occupancy)
 }
 
 // LDS written by some lanes of a wave and then read by others: order the accesses.
@@ -984,8 +992,7 @@ __global__ __launch_bounds__(RECHECK_THREADS) void recheck_kernel(
         double d1 = INFINITY, d2 = INFINITY;
         uint32_t k1 = 0xFFFFFFFFu;
         auto take = [&](uint32_t k) {
-            const double d = D == 12 ? ref_l2_12(xw, load_row12(C64 + (uint64_t)k * 12))
-                                     : ref_l2_hd(xw, C64 + (uint64_t)k * D, D);
+            const double d = ref_l2_cv(xw, C64, k, D);
             if (d < d1 || (d == d1 && k < k1)) {
                 d2 = d1;
                 d1 = d;
@@ -1216,18 +1223,18 @@ __global__ __launch_bounds__(KDR_MAX_WAVES * 64) void kd_resolve_kernel(
         wave_lds_sync();
         if (D == 12) {   // four points per lane in flight (their 24 loads together)
             for (uint32_t j0 = lane; j0 < K; j0 += 4 * 64) {
-                Row12 c[4];
+                RowN<12> c[4];
 #pragma unroll
                 for (int u = 0; u < 4; u++) {
                     const uint32_t j = j0 + 64 * u;
-                    c[u] = load_row12(C64 + (uint64_t)kv.vind[j < K ? j : j0] * 12);
+                    c[u] = load_row<12>(C64 + (uint64_t)kv.vind[j < K ? j : j0] * 12);
                 }
 #pragma unroll
                 for (int u = 0; u < 4; u++)
-                    if (j0 + 64 * u < K) pv[j0 + 64 * u] = ref_l2_12(xs, c[u]);
+                    if (j0 + 64 * u < K) pv[j0 + 64 * u] = ref_l2_n<12>(xs, c[u]);
             }
         } else {
-            for (uint32_t j = lane; j < K; j += 64) pv[j] = ref_l2_hd(xs, C64 + (uint64_t)kv.vind[j] * D, (int)D);
+            for (uint32_t j = lane; j < K; j += 64) pv[j] = ref_l2_cv(xs, C64, kv.vind[j], D);
         }
         wave_lds_sync();
         const uint32_t k = kd_nearest_wave(xs, D, kv, pv, sd, sn, dl, lane);

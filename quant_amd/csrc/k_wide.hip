@@ -188,57 +188,84 @@ __global__ __launch_bounds__(WD_THREADS) void assign_wide_kernel(
 
         // Combine the four lanes of each data row.  One unit: the winning 8-code-vector unit
         // (pair*4 + g) and the best MFMA score among all other units.  Two units: the best two
-        // units (ordered by score, then unit) and the best score among all other units.
-        uint32_t unit = 0, unit2 = 0;
-        float sec_m = INFINITY;
-#pragma unroll
-        for (int t = 0; t < WD_TILES; t++) {
-            uint32_t u = bp[t] * 4 + g, v = bq[t] * 4 + g;
-#pragma unroll
-            for (int off = 16; off <= 32; off <<= 1) {
-                const float o1 = __shfl_xor(b1[t], off), o2 = __shfl_xor(b2[t], off);
-                const uint32_t ou = __shfl_xor(u, off);
-                if (!TWO) {
-                    if (o1 < b1[t] || (o1 == b1[t] && ou < u)) {
-                        b2[t] = min2f(o2, b1[t]);
-                        b1[t] = o1;
-                        u = ou;
-                    } else {
-                        b2[t] = min2f(b2[t], o1);
-                    }
-                    continue;
-                }
-                const float o3 = __shfl_xor(b3[t], off);
-                const uint32_t ov = __shfl_xor(v, off);
-                // merge (b1,u) <= (b2,v) with (o1,ou) <= (o2,ov); thirds b3, o3
-                auto lt = [](float x, uint32_t xu, float y, uint32_t yu) { return x < y || (x == y && xu < yu); };
-                float n1, n2, n3;
-                uint32_t m1, m2;
-                if (lt(o1, ou, b1[t], u)) {   // partner's best first; then (b1,u) vs (o2,ov)
-                    n1 = o1;
-                    m1 = ou;
-                    const bool mine = lt(b1[t], u, o2, ov);
-                    n2 = mine ? b1[t] : o2;
-                    m2 = mine ? u : ov;
-                    n3 = min3f(mine ? o2 : b1[t], b2[t], min2f(b3[t], o3));
+        // units (ordered by score, then unit) and the best score among all other units.  A
+        // reduce-scatter on the VALU as in assign_mfma_kernel: v_permlane32_swap merges tiles
+        // t and t + 2 across lane ^ 32, v_permlane16_swap the survivors across lane ^ 16, and
+        // lane (g, c) keeps tile g, row c (its own row).  Both merges are order-free.
+        struct St {
+            float b1, b2, b3;
+            uint32_t u, v;
+        };
+        auto lt = [](float x, uint32_t xu, float y, uint32_t yu) { return x < y || (x == y && xu < yu); };
+        auto merge = [&](St &m, const St &o) {
+            if (!TWO) {
+                if (lt(o.b1, o.u, m.b1, m.u)) {
+                    m.b2 = min2f(o.b2, m.b1);
+                    m.b1 = o.b1;
+                    m.u = o.u;
                 } else {
-                    n1 = b1[t];
-                    m1 = u;
-                    const bool mine = lt(b2[t], v, o1, ou);
-                    n2 = mine ? b2[t] : o1;
-                    m2 = mine ? v : ou;
-                    n3 = min3f(mine ? o1 : b2[t], o2, min2f(b3[t], o3));
+                    m.b2 = min2f(m.b2, o.b1);
                 }
-                b1[t] = n1;
-                b2[t] = n2;
-                b3[t] = n3;
-                u = m1;
-                v = m2;
+                return;
             }
-            unit = g == t ? u : unit;
-            unit2 = g == t ? v : unit2;
-            sec_m = g == t ? (TWO ? b3[t] : b2[t]) : sec_m;
+            // merge (b1,u) <= (b2,v) with (o1,ou) <= (o2,ov); thirds b3, o3
+            float n1, n2, n3;
+            uint32_t m1, m2;
+            if (lt(o.b1, o.u, m.b1, m.u)) {   // partner's best first; then (b1,u) vs (o2,ov)
+                n1 = o.b1;
+                m1 = o.u;
+                const bool mine = lt(m.b1, m.u, o.b2, o.v);
+                n2 = mine ? m.b1 : o.b2;
+                m2 = mine ? m.u : o.v;
+                n3 = min3f(mine ? o.b2 : m.b1, m.b2, min2f(m.b3, o.b3));
+            } else {
+                n1 = m.b1;
+                m1 = m.u;
+                const bool mine = lt(m.b2, m.v, o.b1, o.u);
+                n2 = mine ? m.b2 : o.b1;
+                m2 = mine ? m.v : o.u;
+                n3 = min3f(mine ? o.b1 : m.b2, o.b2, min2f(m.b3, o.b3));
+            }
+            m = {n1, n2, n3, m1, m2};
+        };
+        // lo / hi of a swap of every field (x: state of the lower tile, y: of the upper)
+        auto swap_st = [&](const St &x, const St &y, bool by32, St &lo, St &hi) {
+            auto sf = [&](float a, float b, float &l, float &h) {
+                const LanePairF r = by32 ? swap32_f32(a, b) : swap16_f32(a, b);
+                l = r.lo;
+                h = r.hi;
+            };
+            auto su = [&](uint32_t a, uint32_t b, uint32_t &l, uint32_t &h) {
+                const LanePair r = by32 ? swap32_u32(a, b) : swap16_u32(a, b);
+                l = r.lo;
+                h = r.hi;
+            };
+            sf(x.b1, y.b1, lo.b1, hi.b1);
+            sf(x.b2, y.b2, lo.b2, hi.b2);
+            su(x.u, y.u, lo.u, hi.u);
+            if (TWO) {
+                sf(x.b3, y.b3, lo.b3, hi.b3);
+                su(x.v, y.v, lo.v, hi.v);
+            } else {
+                lo.b3 = hi.b3 = INFINITY;
+                lo.v = hi.v = 0;
+            }
+        };
+        St h[2];
+#pragma unroll
+        for (int t = 0; t < 2; t++) {   // lanes < 32 end with tile t, lanes >= 32 with tile t + 2
+            const St x = {b1[t], b2[t], TWO ? b3[t] : INFINITY, bp[t] * 4 + g, TWO ? bq[t] * 4 + g : 0u};
+            const St y = {b1[t + 2], b2[t + 2], TWO ? b3[t + 2] : INFINITY, bp[t + 2] * 4 + g,
+                          TWO ? bq[t + 2] * 4 + g : 0u};
+            St o;
+            swap_st(x, y, true, h[t], o);
+            merge(h[t], o);
         }
+        St fin, o;   // even rows keep h[0] (tile 0 or 2), odd rows h[1] (tile 1 or 3): tile g
+        swap_st(h[0], h[1], false, fin, o);
+        merge(fin, o);
+        const uint32_t unit = fin.u, unit2 = fin.v;
+        const float sec_m = TWO ? fin.b3 : fin.b2;
         // Lane L owns row base + L: direct fp32 (x - c)^2 over the 8 code vectors of its unit.
         const uint64_t row = base + lane;
         if (chunk < nchunks && row < N) {
