@@ -168,11 +168,12 @@ bool env_is(const char *name, const char *val) {
 bool use_mfma(const qvq_ctx *ctx, uint32_t K) {
     return ctx->D == MF_D && mf_can_search(K) && !env_is("QVQ_SEARCH", "valu");
 }
-// MFMA search for D != 12 from K = QVQ_WIDE_MIN_K (default 32) code vectors up.
+// MFMA search for D != 12 from K = QVQ_WIDE_MIN_K (default 128) code vectors up: below it the
+// VALU search wins (C4, D = 48: 82 vs 182 us at K = 32, 154 vs 187 at K = 64; tools/c4_ab.sh).
 bool use_wide(const qvq_ctx *ctx, uint32_t K) {
     static const uint32_t min_k = [] {
         const char *e = std::getenv("QVQ_WIDE_MIN_K");
-        return e ? (uint32_t)std::max(1, std::atoi(e)) : 32u;
+        return e ? (uint32_t)std::max(1, std::atoi(e)) : 128u;
     }();
     return ctx->D != MF_D && wide_can_search(ctx->Dp) && K >= min_k && !env_is("QVQ_SEARCH", "valu");
 }
