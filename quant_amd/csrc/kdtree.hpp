@@ -44,7 +44,6 @@ private:
     // those reads in cache (row-major, every read of a 48-D codebook was a cache miss)
     double pt(size_t i, int d) const { return cols_[(size_t)d * K_ + i]; }
     double ptr(size_t i, int d) const { return pts_[i * (size_t)dim_ + d]; }   // row-major
-    struct Node;
     int divide(size_t left, size_t right, std::vector<Box> &bbox, int level, std::vector<Node> &nodes, int &depth);
     void middle_split(size_t *ind, size_t count, size_t &index, int &cutfeat, double &cutval,
                       const std::vector<Box> &bbox);

@@ -43,6 +43,12 @@ def test_host_kdtree_matches_oracle():
         X, _ = oracle.tile(oracle.gen_image(64), 64, 64, bw, bw)
         C = np.concatenate([X[:50] * 1.2, X[:50] * 0.8, X[:5]])
         np.testing.assert_array_equal(quant_amd.host_kdtree_nn(C, X), oracle.kdtree_nn(C, X))
+    # bigger D = 48 trees (C4-sized codebooks)
+    X, _ = oracle.tile(oracle.gen_image(192), 192, 192, 4, 4)
+    for K in (1100, 3000):
+        base = X[rng.choice(len(X), K // 2, replace=False)]
+        C = np.concatenate([base * (1 + 0.2), base * (1 - 0.2), np.zeros((2, 48))])
+        np.testing.assert_array_equal(quant_amd.host_kdtree_nn(C, X), oracle.kdtree_nn(C, X))
 
 
 @pytest.mark.parametrize("cs", [oracle.SCALED, oracle.NORMAL])
