@@ -51,6 +51,15 @@ def test_s512_n10(engine):
     _check_against_oracle(engine, oracle.gen_image(512), 512, 512, 2, 2, 10)
 
 
+def test_repeated_calls_and_edge_levels(engine):
+    # consecutive quantizes on one context: the per-call state (mean buffer the K=1 finalize
+    # clears, counters the mean kernel clears, the A memset only bits == 0 needs, the
+    # completion flag of the result copy) must not leak from one call into the next
+    rgb = oracle.gen_image(128)
+    for bits in (6, 0, 1, 0, 5):
+        _check_against_oracle(engine, rgb, 128, 128, 2, 2, bits)
+
+
 @pytest.mark.parametrize("bw,bh,bits", [(1, 1, 5), (1, 3, 6), (2, 4, 6), (4, 4, 8), (3, 3, 7)])
 def test_block_shapes(engine, bw, bh, bits):
     _check_against_oracle(engine, oracle.gen_image(96), 96, 96, bw, bh, bits)
