@@ -628,14 +628,20 @@ __global__ __launch_bounds__(256) void finalize_prep_kernel(FinArgs a, double *_
         last = atomicAdd(done, 1u) == gridDim.x - 1;
     }
     __syncthreads();
-    if (last && threadIdx.x == 0) {
-        __threadfence();
-        for (uint32_t i = 0; i < a.n_zero; i++) a.zero_after[i] = 0;
-        if (dist_out) {
+    if (!last) return;
+    __threadfence();
+    if (dist_out) {   // the block partials, loaded in parallel, then added in block order
+        __shared__ double parts[512];
+        for (uint32_t b = threadIdx.x; b < gridDim.x; b += blockDim.x) parts[b] = __builtin_nontemporal_load(&dist_part[b]);
+        __syncthreads();
+        if (threadIdx.x == 0) {
             double t = 0;
-            for (uint32_t b = 0; b < gridDim.x; b++) t += __builtin_nontemporal_load(&dist_part[b]);
+            for (uint32_t b = 0; b < gridDim.x; b++) t += parts[b];
             dist_out[0] = t;
         }
+    }
+    if (threadIdx.x == 0) {
+        for (uint32_t i = 0; i < a.n_zero; i++) a.zero_after[i] = 0;
         *done = 0;
         if (ready) {
             __threadfence_system();
