@@ -123,6 +123,19 @@ QVQ_API qvq_status qvq_update(qvq_ctx *ctx, const uint32_t *assign, uint32_t K, 
 /* Multi-GPU: join an RCCL communicator (unique_id from qvq_comm_unique_id on rank 0,
  * shipped to the other ranks by the caller).  Each level then all-reduces the
  * per-code-vector sums and counts over xGMI. */
+/* Decode (replaces CompressedImage::decompress, reference src/Compressor.cpp:156-165, and the
+ * getImageFromVectors it calls, src/Compressor.cpp:64-85): raster[x*ySize+y] = the code-vector bytes
+ * codebook[assign[block]] laid out as getImageFromVectors does, including the column wrap and
+ * "last block wins" order.  codebook: K x (bw*bh*3) bytes; assign: ceil(xSize/bw)*ceil(ySize/bh)
+ * u32; rgb: xSize*ySize*3 bytes.  An index >= K returns QVQ_EINVAL (the reference throws).
+ * qvq_decode takes host buffers; qvq_decode_device takes device pointers and a hipStream_t
+ * (null = the context's stream) and synchronises that stream before returning. */
+QVQ_API qvq_status qvq_decode(qvq_ctx *ctx, const uint8_t *codebook, uint32_t K, const uint32_t *assign,
+                              uint64_t nblocks, uint32_t xSize, uint32_t ySize, uint32_t bw, uint32_t bh, uint8_t *rgb);
+QVQ_API qvq_status qvq_decode_device(qvq_ctx *ctx, const void *d_codebook, uint32_t K, const void *d_assign,
+                                     uint64_t nblocks, uint32_t xSize, uint32_t ySize, uint32_t bw, uint32_t bh,
+                                     void *d_rgb, void *stream);
+
 QVQ_API qvq_status qvq_comm_unique_id(uint8_t id[128]);
 QVQ_API qvq_status qvq_comm_init(qvq_ctx *ctx, int nranks, int rank, const uint8_t id[128]);
 

@@ -73,6 +73,8 @@ def lib():
             "qvq_host_kdtree_nn": ([P, u32, u32, P, u64, P], i),
             "qvq_host_finalize": ([P, P, P, u32, u32, i, P], i),
             "qvq_host_row_terms": ([P, u32, i, P, P], i),
+            "qvq_decode": ([P, P, u32, P, u64, u32, u32, u32, u32, P], i),
+            "qvq_decode_device": ([P, P, u32, P, u64, u32, u32, u32, u32, P, P], i),
         }
         for name, (args, res) in sig.items():
             fn = getattr(L, name)
@@ -194,6 +196,20 @@ class Engine:
                 "wait_ms": list(t.wait_ms[:max(L, 1)]), "tree_ms": list(t.tree_ms[:max(L, 1)])}
 
     # -- multi-GPU -----------------------------------------------------------------------
+    def decode(self, cb_bytes, A, xSize, ySize, bw, bh):
+        """CompressedImage::decompress (src/Compressor.cpp:156-165) on the device: codebook bytes
+        (K x bw*bh*3 u8) and block indices -> xSize*ySize*3 raster (u8)."""
+        cb = np.ascontiguousarray(cb_bytes, dtype=np.uint8).reshape(-1, bw * bh * 3)
+        A = np.ascontiguousarray(A, dtype=np.uint32).ravel()
+        out = np.empty(xSize * ySize * 3, dtype=np.uint8)
+        _check(lib().qvq_decode(self._h, _p(cb), cb.shape[0], _p(A), A.size, xSize, ySize, bw, bh, _p(out)), self._h)
+        return out
+
+    def decode_device(self, cb_ptr, K, a_ptr, nblocks, xSize, ySize, bw, bh, rgb_ptr, stream=None):
+        """Device-pointer decode on `stream` (a hipStream_t handle; None = the context's stream)."""
+        _check(lib().qvq_decode_device(self._h, cb_ptr, K, a_ptr, nblocks, xSize, ySize, bw, bh, rgb_ptr, stream),
+               self._h)
+
     @staticmethod
     def comm_unique_id():
         buf = (ctypes.c_uint8 * 128)()

@@ -887,6 +887,70 @@ QVQ_API qvq_status qvq_update(qvq_ctx *ctx, const uint32_t *assign, uint32_t K, 
     return QVQ_OK;
 }
 
+// ---------------------------------------------------------------------------------------
+// Decode: CompressedImage::decompress (src/Compressor.cpp:156-165) as one device gather.
+// ---------------------------------------------------------------------------------------
+static qvq_status check_decode_args(qvq_ctx *ctx, uint32_t K, uint64_t nblocks, uint32_t xSize, uint32_t ySize,
+                                    uint32_t bw, uint32_t bh) {
+    if (!ctx) return QVQ_EINVAL;
+    if (K == 0 || bw == 0 || bh == 0 || xSize == 0 || ySize == 0)
+        return fail(ctx, QVQ_EINVAL, "decode: K, block and image sizes must be > 0");
+    const uint64_t wB = ((uint64_t)xSize + bw - 1) / bw, hB = ((uint64_t)ySize + bh - 1) / bh;
+    if (nblocks != wB * hB) return fail(ctx, QVQ_EINVAL, "decode: nblocks != ceil(x/bw)*ceil(y/bh)");
+    if ((uint64_t)bw * bh * 3 > 0xFFFFFFFFull) return fail(ctx, QVQ_EINVAL, "decode: block too large");
+    return QVQ_OK;
+}
+
+QVQ_API qvq_status qvq_decode_device(qvq_ctx *ctx, const void *d_codebook, uint32_t K, const void *d_assign,
+                                     uint64_t nblocks, uint32_t xSize, uint32_t ySize, uint32_t bw, uint32_t bh,
+                                     void *d_rgb, void *stream) {
+    qvq_status st = check_decode_args(ctx, K, nblocks, xSize, ySize, bw, bh);
+    if (st != QVQ_OK) return st;
+    if (!d_codebook || !d_assign || !d_rgb) return fail(ctx, QVQ_EINVAL, "decode: null pointer");
+    HIPCHK(hipSetDevice(ctx->dev));
+    hipStream_t s = stream ? (hipStream_t)stream : ctx->stream;
+    uint32_t *d_bad = nullptr;
+    HIPCHK(hipMalloc(&d_bad, sizeof(uint32_t)));
+    uint32_t bad = 0;
+    hipError_t e = hipMemsetAsync(d_bad, 0, sizeof(uint32_t), s);
+    if (e == hipSuccess)
+        e = launch_decode(s, (const uint8_t *)d_codebook, K, bw * bh * 3, (const uint32_t *)d_assign, xSize, ySize, bw,
+                          bh, (uint8_t *)d_rgb, d_bad);
+    if (e == hipSuccess) e = hipMemcpyAsync(&bad, d_bad, sizeof(uint32_t), hipMemcpyDeviceToHost, s);
+    if (e == hipSuccess) e = hipStreamSynchronize(s);
+    (void)hipFree(d_bad);
+    if (e != hipSuccess) return fail(ctx, QVQ_EDEVICE, std::string("decode: ") + hipGetErrorString(e));
+    if (bad) return fail(ctx, QVQ_EINVAL, "decode: code-vector index out of range");
+    return QVQ_OK;
+}
+
+QVQ_API qvq_status qvq_decode(qvq_ctx *ctx, const uint8_t *codebook, uint32_t K, const uint32_t *assign,
+                              uint64_t nblocks, uint32_t xSize, uint32_t ySize, uint32_t bw, uint32_t bh, uint8_t *rgb) {
+    qvq_status st = check_decode_args(ctx, K, nblocks, xSize, ySize, bw, bh);
+    if (st != QVQ_OK) return st;
+    if (!codebook || !assign || !rgb) return fail(ctx, QVQ_EINVAL, "decode: null pointer");
+    HIPCHK(hipSetDevice(ctx->dev));
+    const uint64_t cbB = (uint64_t)K * bw * bh * 3, aB = nblocks * 4, rB = (uint64_t)xSize * ySize * 3;
+    uint8_t *d = nullptr;
+    HIPCHK(hipMalloc(&d, cbB + aB + rB + 8));
+    uint8_t *d_cb = d, *d_rgb = d + cbB + 4;
+    uint32_t *d_A = (uint32_t *)(d + ((cbB + 3) & ~3ull));
+    d_rgb = (uint8_t *)d_A + aB;
+    hipError_t e = hipMemcpyAsync(d_cb, codebook, cbB, hipMemcpyHostToDevice, ctx->stream);
+    if (e == hipSuccess) e = hipMemcpyAsync(d_A, assign, aB, hipMemcpyHostToDevice, ctx->stream);
+    if (e != hipSuccess) {
+        (void)hipFree(d);
+        return fail(ctx, QVQ_EDEVICE, std::string("decode upload: ") + hipGetErrorString(e));
+    }
+    st = qvq_decode_device(ctx, d_cb, K, d_A, nblocks, xSize, ySize, bw, bh, d_rgb, nullptr);
+    if (st == QVQ_OK) {
+        e = hipMemcpy(rgb, d_rgb, rB, hipMemcpyDeviceToHost);
+        if (e != hipSuccess) st = fail(ctx, QVQ_EDEVICE, std::string("decode download: ") + hipGetErrorString(e));
+    }
+    (void)hipFree(d);
+    return st;
+}
+
 QVQ_API qvq_status qvq_comm_unique_id(uint8_t id[128]) {
     static_assert(sizeof(ncclUniqueId) == 128, "RCCL unique id size");
     ncclUniqueId u;
