@@ -846,21 +846,22 @@ namespace qvq {
 // reference's final write.  Code vectors stay in L2 (K*D <= 12 MB at 2^24 x 12 is the worst
 // case; C3 is 12 KB).  Out-of-range indices (the reference throws from .at()) write 0 and
 // raise *bad.
+// T = uint32_t when the raster's index math fits (64-bit divides are emulated in ~40 VALU).
+template <typename T>
 __global__ __launch_bounds__(256) void decode_kernel(const uint8_t *__restrict__ cb, uint32_t K, uint32_t D,
                                                      const uint32_t *__restrict__ A, uint32_t xs, uint32_t ys,
                                                      uint32_t w, uint32_t h, uint32_t hB, uint8_t *__restrict__ rgb,
                                                      uint32_t *__restrict__ bad) {
-    const uint64_t npix = (uint64_t)xs * ys;
-    const uint64_t yspan = (uint64_t)hB * h;
-    for (uint64_t dst = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; dst < npix;
-         dst += (uint64_t)gridDim.x * blockDim.x) {
-        const uint64_t x = dst / ys;
-        uint64_t bi = 0, bj = 0, bdx = 0, bdy = 0;
+    const T npix = (T)xs * ys;
+    const T yspan = (T)hB * h;
+    for (T dst = blockIdx.x * (T)blockDim.x + threadIdx.x; dst < npix; dst += (T)gridDim.x * blockDim.x) {
+        const T x = dst / ys;
+        T bi = 0, bj = 0, bdx = 0, bdy = 0;
         bool have = false;
-        for (uint64_t xp = x + 1; xp-- > 0;) {
-            const uint64_t yp = dst - xp * ys;
+        for (T xp = x + 1; xp-- > 0;) {
+            const T yp = dst - xp * ys;
             if (yp >= yspan) break;   // grows as xp falls
-            const uint64_t i = xp / w, dx = xp - i * w, j = yp / h, dy = yp - j * h;
+            const T i = xp / w, dx = xp - i * w, j = yp / h, dy = yp - j * h;
             if (!have || i > bi || (i == bi && (j > bj || (j == bj && (dx > bdx || (dx == bdx && dy > bdy)))))) {
                 bi = i, bj = j, bdx = dx, bdy = dy;
                 have = true;
@@ -868,17 +869,16 @@ __global__ __launch_bounds__(256) void decode_kernel(const uint8_t *__restrict__
         }
         uint8_t r = 0, g = 0, b = 0;
         if (have) {
-            const uint32_t a = A[bi * hB + bj];
+            const uint32_t a = A[(uint64_t)bi * hB + bj];
             if (a < K) {
-                const uint8_t *row = cb + (uint64_t)a * D + (bdx * h + bdy) * 3;
+                const uint8_t *row = cb + (uint64_t)a * D + ((uint64_t)bdx * h + bdy) * 3;
                 r = row[0], g = row[1], b = row[2];
             } else {
                 atomicOr(bad, 1u);
             }
         }
-        rgb[dst * 3 + 0] = r;
-        rgb[dst * 3 + 1] = g;
-        rgb[dst * 3 + 2] = b;
+        uint8_t *o = rgb + (uint64_t)dst * 3;
+        o[0] = r, o[1] = g, o[2] = b;
     }
 }
 
@@ -887,7 +887,10 @@ hipError_t launch_decode(hipStream_t s, const uint8_t *cb, uint32_t K, uint32_t 
     const uint64_t npix = (uint64_t)xs * ys;
     const uint32_t hB = (ys + h - 1) / h;
     const int grid = (int)std::max<uint64_t>(1, std::min<uint64_t>((npix + 255) / 256, 1u << 16));
-    hipLaunchKernelGGL(decode_kernel, dim3(grid), dim3(256), 0, s, cb, K, D, A, xs, ys, w, h, hB, rgb, bad);
+    if (((uint64_t)xs + w) * ((uint64_t)ys + h) < (1ull << 32) - (1ull << 25))
+        hipLaunchKernelGGL(decode_kernel<uint32_t>, dim3(grid), dim3(256), 0, s, cb, K, D, A, xs, ys, w, h, hB, rgb, bad);
+    else
+        hipLaunchKernelGGL(decode_kernel<uint64_t>, dim3(grid), dim3(256), 0, s, cb, K, D, A, xs, ys, w, h, hB, rgb, bad);
     return hipGetLastError();
 }
 
