@@ -14,6 +14,16 @@ N images (weak scaling: per-GPU work fixed, one all-reduce per level).
 
 Rank 0 prints one JSON line.  value = Mblocks/s = (blocks on all ranks) x levels x steps
 / max-over-ranks wall time / 1e6 (BASELINE.md section 2 definition).
+
+Sub-objects of the same line (each timed the same way, barrier + synchronize around K steps,
+max over ranks):
+  c5   BASELINE.json config 5 -- the fixed 64-image 4096^2 batch, 2x2, K=1024, split over
+       the N ranks (64/N images each) with the per-level RCCL all-reduce: STRONG scaling, the
+       north-star 1->8 GPU curve.
+  c4   (N = 1) config 4: 4096^2, 4x4 blocks (D=48), K=4096.
+  end_to_end (N = 1) the drop-in's PCIe-inclusive compress: host raster -> H2D + tiling +
+       quantize + the 16.8 MB index download (src/Compressor.cpp:118-123 timed region).
+  cpu_baseline (N = 1) the oracle port, median of 5 at the box's cores and at 8 cores.
 """
 import argparse
 import json
@@ -21,6 +31,8 @@ import os
 import subprocess
 import sys
 import time
+
+import numpy as np
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
@@ -45,28 +57,62 @@ def parse():
     ap.add_argument("--images-per-rank", type=int, default=1)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-threads", type=int, default=0, help="0 = min(16, host cores)")
+    ap.add_argument("--cpu-reps", type=int, default=5)
+    ap.add_argument("--c5-images", type=int, default=64)
+    ap.add_argument("--c5-steps", type=int, default=3, help="0 disables the c5 sub-object")
+    ap.add_argument("--c4-steps", type=int, default=5, help="0 disables the c4 sub-object")
+    ap.add_argument("--e2e-reps", type=int, default=3, help="0 disables the end_to_end sub-object")
     return ap.parse_args()
+
+
+def _oracle_runs(args, threads, reps):
+    cli = os.path.join(ROOT, "oracle", "build", "oracle_cli")
+    if not os.path.exists(cli):
+        subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "oracle")], check=True)
+    out = subprocess.run([cli, "gen", str(args.size), str(0x5EED), str(args.block), str(args.block),
+                          str(args.bits), str(threads), str(reps)], check=True, capture_output=True, text=True,
+                         timeout=900).stdout
+    return [json.loads(l) for l in out.strip().splitlines() if l.startswith("{")]
 
 
 def cpu_baseline(args):
     """The oracle port (lbg_oracle.c, OpenMP on the same loops as the reference) on the
-    same workload, on this host's cores: one full quantize of one image."""
-    from oracle import oracle  # noqa: F401  (builds liboracle if missing)
-    cli = os.path.join(ROOT, "oracle", "build", "oracle_cli")
-    if not os.path.exists(cli):
-        subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "oracle")], check=True)
+    same workload, on this host's cores: median of --cpu-reps full quantizes of one image at
+    the box's core share (16 on the GPU box) and at 8 cores."""
+    import statistics
     threads = args.cpu_threads or min(16, os.cpu_count() or 1)
-    out = subprocess.run([cli, "gen", str(args.size), str(0x5EED), str(args.block), str(args.block),
-                          str(args.bits), str(threads), "1"], check=True, capture_output=True, text=True,
-                         timeout=600).stdout
-    rec = json.loads(out.strip().splitlines()[-1])
-    n = rec["N"]
-    mbps = n * args.bits / rec["quantize_s"] / 1e6
+    runs = {}
+    for t in sorted({threads, min(8, threads)}, reverse=True):
+        recs = _oracle_runs(args, t, args.cpu_reps)
+        runs[t] = (statistics.median(r["quantize_s"] for r in recs), recs[0]["N"],
+                   statistics.median(r["tile_s"] for r in recs))
+    med, n, tile_s = runs[threads]
+    mbps = n * args.bits / med / 1e6
     return {"value": round(mbps, 4), "unit": "Mblocks/s", "cores": threads, "kind": "port",
-            "sample": "one full quantize (tiling excluded) of the rank-0 workload: %dx%d synthetic, %dx%d "
-                      "blocks, %d levels; quantize %.3f s, tiling %.3f s"
-                      % (args.size, args.size, args.block, args.block, args.bits, rec["quantize_s"],
-                         rec["tile_s"])}
+            "sample": "median of %d full quantizes (tiling excluded) of the rank-0 workload: %dx%d synthetic, %dx%d "
+                      "blocks, %d levels, at %d threads: %.3f s (tiling %.3f s)%s"
+                      % (args.cpu_reps, args.size, args.size, args.block, args.block, args.bits, threads, med, tile_s,
+                         "".join("; at %d threads: %.3f s" % (t, v[0]) for t, v in runs.items() if t != threads)),
+            "quantize_s_by_threads": {str(t): round(v[0], 4) for t, v in runs.items()}}
+
+
+def synthetic_raster(S, seed):
+    """SURVEY.md 8(d) generator in numpy (host raster for the PCIe-inclusive leg)."""
+    with np.errstate(over="ignore"):
+        p = np.arange(S * S, dtype=np.uint64)
+        r, c = p // np.uint64(S), p % np.uint64(S)
+        sm = [r * np.uint64(255) // np.uint64(S - 1), c * np.uint64(255) // np.uint64(S - 1),
+              (r + c) * np.uint64(255) // np.uint64(2 * (S - 1))]
+        out = np.empty((S * S, 3), np.uint8)
+        for ch in range(3):
+            z = (np.uint64(seed) << np.uint64(40)) ^ (p * np.uint64(3) + np.uint64(ch))
+            z = z + np.uint64(0x9E3779B97F4A7C15)
+            z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+            z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+            z = z ^ (z >> np.uint64(31))
+            v = sm[ch].astype(np.int64) + (z % np.uint64(33)).astype(np.int64) - 16
+            out[:, ch] = np.clip(v, 0, 255)
+    return out.ravel()
 
 
 def main():
@@ -97,7 +143,6 @@ def main():
     n_local = eng.n
     D = eng.dim
 
-    import numpy as np
     out = (np.empty((1 << args.bits, D), np.float64), np.zeros(1, np.float64))   # reused by every step
     for _ in range(args.warmup):
         eng.lbg(args.bits, want_assign=False, out=out)
@@ -188,6 +233,68 @@ def main():
                           if upd_secs else "fused into the search (LDS u64 atomics of exact integer terms)"),
         "flagged_rows_per_step": flagged[-1],
     }
+    def timed(fn, steps, warmup):
+        """Max-over-ranks wall of `steps` calls of fn after `warmup`, barrier + sync on both sides."""
+        for _ in range(warmup):
+            fn()
+        barrier()
+        torch.cuda.synchronize()
+        t = time.perf_counter()
+        for _ in range(steps):
+            fn()
+        torch.cuda.synchronize()
+        barrier()
+        el = time.perf_counter() - t
+        if world > 1:
+            tt = torch.tensor([el], dtype=torch.float64)
+            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+            el = float(tt[0])
+        return el
+
+    # C5: the fixed 64-image batch split over the ranks, one joint codebook (strong scaling)
+    if args.c5_steps > 0:
+        n_img = args.c5_images
+        share = [n_img // world + (1 if r < n_img % world else 0) for r in range(world)]
+        start = sum(share[:rank])
+        eng.set_synthetic(args.size, 0x5EED + start, share[rank], 2, 2, quant_amd.SCALED)
+        eng.set_timing(-2)
+        out5 = (np.empty((1 << args.bits, eng.dim), np.float64), np.zeros(1, np.float64))
+        el = timed(lambda: eng.lbg(args.bits, want_assign=False, out=out5), args.c5_steps, 1)
+        n5 = n_img * ((args.size + 1) // 2) ** 2
+        result["c5"] = {"workload": "C5: %d x %dx%d synthetic (seeds 0x5EED..+%d), 2x2 blocks, %d code vectors, "
+                                    "one joint codebook, %d image(s) on this rank" % (n_img, args.size, args.size,
+                                                                                       n_img - 1, 1 << args.bits,
+                                                                                       share[rank]),
+                        "value": round(n5 * args.bits * args.c5_steps / el / 1e6, 3), "unit": "Mblocks/s",
+                        "ms_per_step": round(el * 1e3 / args.c5_steps, 3), "steps": args.c5_steps, "warmup": 1,
+                        "n_gpus": world, "scaling": "strong", "blocks_total": n5,
+                        "images_per_rank": share, "collective": "RCCL all-reduce per level" if world > 1 else "none"}
+    if world == 1 and args.c4_steps > 0:
+        eng.set_synthetic(args.size, 0x5EED, 1, 4, 4, quant_amd.SCALED)
+        eng.set_timing(-2)
+        out4 = (np.empty((1 << 12, eng.dim), np.float64), np.zeros(1, np.float64))
+        el = timed(lambda: eng.lbg(12, want_assign=False, out=out4), args.c4_steps, 1)
+        result["c4"] = {"workload": "C4: %dx%d synthetic, 4x4 blocks (D=48), 4096 code vectors" % (args.size, args.size),
+                        "value": round(eng.n * 12 * args.c4_steps / el / 1e6, 3), "unit": "Mblocks/s",
+                        "ms_per_step": round(el * 1e3 / args.c4_steps, 3), "steps": args.c4_steps, "warmup": 1}
+    if world == 1 and args.e2e_reps > 0:
+        # the drop-in's compress region from a host raster: H2D + tiling + quantize + indices D2H
+        rgb = synthetic_raster(args.size, 0x5EED)
+        Cb = np.empty((1 << args.bits, 3 * args.block * args.block), np.float64)
+        times = []
+        for r in range(args.e2e_reps + 1):
+            t = time.perf_counter()
+            eng.set_images(rgb, 1, args.size, args.size, args.block, args.block, quant_amd.SCALED)
+            _, A_host, _ = eng.lbg(args.bits, out=(Cb, np.zeros(1, np.float64)))
+            if r:
+                times.append(time.perf_counter() - t)
+        times.sort()
+        med = times[len(times) // 2]
+        result["end_to_end"] = {"what": "host raster -> qvq_set_images (50 MB H2D + tiling) + qvq_lbg + %d-byte "
+                                        "index download; not the headline" % (A_host.size * 4),
+                                "ms": round(med * 1e3, 3), "Mblocks_per_s": round(n_local * args.bits / med / 1e6, 3),
+                                "reps": args.e2e_reps}
+        result["end_to_end_ms"] = round(med * 1e3, 3)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         try:
             cb = cpu_baseline(args)

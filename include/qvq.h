@@ -120,24 +120,40 @@ QVQ_API const uint32_t *qvq_assign_device(const qvq_ctx *ctx);
 QVQ_API qvq_status qvq_assign(qvq_ctx *ctx, const double *C, uint32_t K, uint32_t *assign);
 QVQ_API qvq_status qvq_update(qvq_ctx *ctx, const uint32_t *assign, uint32_t K, double *C_out, uint64_t *counts);
 
-/* Multi-GPU: join an RCCL communicator (unique_id from qvq_comm_unique_id on rank 0,
- * shipped to the other ranks by the caller).  Each level then all-reduces the
- * per-code-vector sums and counts over xGMI. */
 /* Decode (replaces CompressedImage::decompress, reference src/Compressor.cpp:156-165, and the
  * getImageFromVectors it calls, src/Compressor.cpp:64-85): raster[x*ySize+y] = the code-vector bytes
  * codebook[assign[block]] laid out as getImageFromVectors does, including the column wrap and
  * "last block wins" order.  codebook: K x (bw*bh*3) bytes; assign: ceil(xSize/bw)*ceil(ySize/bh)
- * u32; rgb: xSize*ySize*3 bytes.  An index >= K returns QVQ_EINVAL (the reference throws).
- * qvq_decode takes host buffers; qvq_decode_device takes device pointers and a hipStream_t
- * (null = the context's stream) and synchronises that stream before returning. */
+ * u32; rgb: xSize*ySize*3 bytes.  An index >= K returns QVQ_EINVAL (the reference indexes
+ * codeVectors with operator[], undefined behaviour).  ySize + bh - 1 and xSize + bw - 1 must be
+ * below 2^32.
+ * qvq_decode takes host buffers.  qvq_decode_mse also returns the raport's distortion, the mean
+ * squared difference of the signed bytes of orig and the decoded raster (src/Compressor.cpp:
+ * 133-146), computed in the same device pass (rgb may then be NULL).  qvq_decode_device takes
+ * device pointers and a hipStream_t on which it launches (NULL = the legacy null stream, so
+ * work the caller queued on blocking streams is ordered before it) and synchronises that
+ * stream before returning. */
 QVQ_API qvq_status qvq_decode(qvq_ctx *ctx, const uint8_t *codebook, uint32_t K, const uint32_t *assign,
                               uint64_t nblocks, uint32_t xSize, uint32_t ySize, uint32_t bw, uint32_t bh, uint8_t *rgb);
+QVQ_API qvq_status qvq_decode_mse(qvq_ctx *ctx, const uint8_t *codebook, uint32_t K, const uint32_t *assign,
+                                  uint64_t nblocks, uint32_t xSize, uint32_t ySize, uint32_t bw, uint32_t bh,
+                                  uint8_t *rgb, const uint8_t *orig, double *mse);
 QVQ_API qvq_status qvq_decode_device(qvq_ctx *ctx, const void *d_codebook, uint32_t K, const void *d_assign,
                                      uint64_t nblocks, uint32_t xSize, uint32_t ySize, uint32_t bw, uint32_t bh,
                                      void *d_rgb, void *stream);
 
+/* Multi-GPU: join an RCCL communicator (unique_id from qvq_comm_unique_id on rank 0,
+ * shipped to the other ranks by the caller).  Each level then all-reduces the
+ * per-code-vector sums and counts over xGMI.  nranks = 1 creates a real one-rank
+ * communicator (the collective path with identical results).  A collective that fails, or
+ * a wait that outlasts the timeout (qvq_set_timeout) while a communicator is joined, returns
+ * QVQ_ECOMM and aborts the communicator (the context then runs single-rank until the next
+ * qvq_comm_init). */
 QVQ_API qvq_status qvq_comm_unique_id(uint8_t id[128]);
 QVQ_API qvq_status qvq_comm_init(qvq_ctx *ctx, int nranks, int rank, const uint8_t id[128]);
+/* Bound, in seconds, of every host wait on the context's stream (default 120, or the
+ * QVQ_TIMEOUT_S environment variable at qvq_create). */
+QVQ_API qvq_status qvq_set_timeout(qvq_ctx *ctx, double seconds);
 
 /* Which levels get HIP events around their search kernel (each event record costs a few
  * microseconds of GPU idle): -1 every level (default), -2 none, n >= 0 level n+1 only.
@@ -157,6 +173,12 @@ QVQ_API qvq_status qvq_host_finalize(const uint64_t *hi, const uint64_t *lo, con
  * (dim entries each) -- for the host-side sharding tests. */
 QVQ_API qvq_status qvq_host_row_terms(const uint8_t *codes, uint32_t dim, int colorspace, uint64_t *hi,
                                       uint64_t *lo);
+/* The engine's bounded-wait policy (quant_amd/csrc/wait.hpp) driven by scripted probes, for
+ * tests: scenario 0 the work publishes after ~5 ms; 1 it never does, no communicator; 2 it
+ * never does, a healthy communicator; 3 the communicator reports an error after ~5 ms; 4 the
+ * stream fails; 5 the stream drains without publishing.  Returns the wait's status and its
+ * duration in *elapsed_s. */
+QVQ_API qvq_status qvq_host_wait_probe(int scenario, double timeout_s, double *elapsed_s);
 
 #ifdef __cplusplus
 }

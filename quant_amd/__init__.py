@@ -40,7 +40,8 @@ EXPORTED = ["qvq_create", "qvq_destroy", "qvq_last_error", "qvq_version", "qvq_s
             "qvq_set_images_device", "qvq_set_synthetic", "qvq_set_vectors", "qvq_num_vectors",
             "qvq_dim", "qvq_lbg", "qvq_assign_device", "qvq_assign", "qvq_update",
             "qvq_comm_unique_id", "qvq_comm_init", "qvq_set_timing", "qvq_get_timings", "qvq_host_kdtree_nn",
-            "qvq_host_finalize", "qvq_host_row_terms"]
+            "qvq_host_finalize", "qvq_host_row_terms", "qvq_decode", "qvq_decode_mse", "qvq_decode_device",
+            "qvq_set_timeout", "qvq_host_wait_probe"]
 
 
 def lib():
@@ -74,7 +75,10 @@ def lib():
             "qvq_host_finalize": ([P, P, P, u32, u32, i, P], i),
             "qvq_host_row_terms": ([P, u32, i, P, P], i),
             "qvq_decode": ([P, P, u32, P, u64, u32, u32, u32, u32, P], i),
+            "qvq_decode_mse": ([P, P, u32, P, u64, u32, u32, u32, u32, P, P, P], i),
             "qvq_decode_device": ([P, P, u32, P, u64, u32, u32, u32, u32, P, P], i),
+            "qvq_set_timeout": ([P, ctypes.c_double], i),
+            "qvq_host_wait_probe": ([i, ctypes.c_double, P], i),
         }
         for name, (args, res) in sig.items():
             fn = getattr(L, name)
@@ -205,8 +209,27 @@ class Engine:
         _check(lib().qvq_decode(self._h, _p(cb), cb.shape[0], _p(A), A.size, xSize, ySize, bw, bh, _p(out)), self._h)
         return out
 
+    def decode_mse(self, cb_bytes, A, xSize, ySize, bw, bh, orig, want_image=True):
+        """Decode plus the raport's distortion (src/Compressor.cpp:133-146): mean squared
+        difference of the signed bytes of orig and the decoded raster, in the same device pass.
+        Returns (raster or None, mse)."""
+        cb = np.ascontiguousarray(cb_bytes, dtype=np.uint8).reshape(-1, bw * bh * 3)
+        A = np.ascontiguousarray(A, dtype=np.uint32).ravel()
+        orig = np.ascontiguousarray(orig, dtype=np.uint8).ravel()
+        assert orig.size == xSize * ySize * 3
+        out = np.empty(xSize * ySize * 3, dtype=np.uint8) if want_image else None
+        mse = ctypes.c_double()
+        _check(lib().qvq_decode_mse(self._h, _p(cb), cb.shape[0], _p(A), A.size, xSize, ySize, bw, bh,
+                                    _p(out) if want_image else None, _p(orig), ctypes.byref(mse)), self._h)
+        return out, mse.value
+
+    def set_timeout(self, seconds):
+        """Bound of every host wait on the engine's stream (QVQ_ECOMM / QVQ_EDEVICE past it)."""
+        _check(lib().qvq_set_timeout(self._h, float(seconds)), self._h)
+
     def decode_device(self, cb_ptr, K, a_ptr, nblocks, xSize, ySize, bw, bh, rgb_ptr, stream=None):
-        """Device-pointer decode on `stream` (a hipStream_t handle; None = the context's stream)."""
+        """Device-pointer decode on `stream` (a hipStream_t handle; None or 0 = the legacy null
+        stream, ordered after the caller's work on blocking streams)."""
         _check(lib().qvq_decode_device(self._h, cb_ptr, K, a_ptr, nblocks, xSize, ySize, bw, bh, rgb_ptr, stream),
                self._h)
 
@@ -228,6 +251,13 @@ def host_kdtree_nn(C, Q):
     out = np.empty(Q.shape[0], np.uint32)
     _check(lib().qvq_host_kdtree_nn(_p(C), C.shape[0], C.shape[1], _p(Q), Q.shape[0], _p(out)))
     return out
+
+
+def host_wait_probe(scenario, timeout_s):
+    """The engine's bounded-wait policy under scripted probes (qvq.h): (status, seconds)."""
+    el = ctypes.c_double()
+    st = lib().qvq_host_wait_probe(int(scenario), float(timeout_s), ctypes.byref(el))
+    return st, el.value
 
 
 def host_finalize(hi, lo, cnt, colorspace=SCALED):

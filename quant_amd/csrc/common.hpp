@@ -100,8 +100,10 @@ __host__ __device__ inline uint32_t cb_lo_slot(uint32_t D, uint32_t Dp, uint32_t
 // ---------------------------------------------------------------------------------------
 hipError_t launch_gen(hipStream_t s, uint8_t *rgb, uint32_t S, uint64_t seed0, uint64_t npix);
 // Decode gather (CompressedImage::decompress): codebook bytes [K][D], A [wB*hB] -> raster [xs*ys*3].
+// With orig (the original raster) the squared signed-byte differences are added to *sqerr.
 hipError_t launch_decode(hipStream_t s, const uint8_t *cb, uint32_t K, uint32_t D, const uint32_t *A, uint32_t xs,
-                         uint32_t ys, uint32_t w, uint32_t h, uint8_t *rgb, uint32_t *bad);
+                         uint32_t ys, uint32_t w, uint32_t h, uint8_t *rgb, const uint8_t *orig, uint64_t *sqerr,
+                         uint32_t *bad);
 hipError_t launch_tile(hipStream_t s, const uint8_t *rgb, uint8_t *codes, uint32_t n_images, uint32_t xSize,
                        uint32_t ySize, uint32_t bw, uint32_t bh, uint32_t D, uint32_t Dp, uint8_t pad);
 // VALU fp32 search for any Dp (multiple of 4, <= 64); codebook C32 [K][Dp].

@@ -28,6 +28,7 @@
 #include "common.hpp"
 #include "kdtree.hpp"
 #include "qvq.h"
+#include "wait.hpp"
 
 namespace qvq {
 
@@ -105,6 +106,10 @@ struct qvq_ctx {
     uint64_t out_seq = 0;         // quantizes whose results copy_out has published
     uint32_t *d_scatter = nullptr;
     uint64_t scatter_bytes = 0;
+    uint8_t *d_decode = nullptr;          // qvq_decode scratch (grown on demand)
+    uint64_t decode_bytes = 0;
+    uint64_t *d_decode_stat = nullptr;    // decode: [squared error, bad-index flag]
+    uint64_t *h_decode_stat = nullptr;    // pinned host copy
     // mapped pinned host memory (coherent): the split codebook finalize writes for the
     // host's tree build, its ready sequence number, and two flattened kd-tree images
     double *h_cb = nullptr, *dh_cb = nullptr;
@@ -119,6 +124,8 @@ struct qvq_ctx {
     int timing_level = -1;   // qvq_set_timing: -1 all levels, -2 none, else that level only
     bool upd[32] = {};
     hipEvent_t ev_end = nullptr;
+    hipEvent_t ev_sync = nullptr;   // wait_stream
+    double timeout_s = 120;         // bound of every host wait (qvq_set_timeout, QVQ_TIMEOUT_S)
 
     // multi-GPU
     ncclComm_t comm = nullptr;
@@ -392,24 +399,63 @@ void build_tree(qvq_ctx *ctx, const double *hC, uint32_t K, int buf, KdView &kd)
     kd = v;
 }
 
-// Wait until the stream has published seq in a mapped flag (the ready number of finalize's
-// codebook in h_cb, or copy_out's completion).  Polls the flag; a stream error or a drained
-// stream without the flag ends the wait with an error (never hangs).
-qvq_status wait_flag(qvq_ctx *ctx, volatile uint64_t *flag, uint64_t seq) {
-    // hipStreamQuery submits a marker (a few us of GPU idle), so the stream is consulted
-    // only every ~20 ms of waiting, to catch a failed or drained stream
-    auto next_check = std::chrono::steady_clock::now() + std::chrono::milliseconds(20);
-    while (*flag < seq) {
-        if (std::chrono::steady_clock::now() < next_check) continue;
-        const hipError_t q = hipStreamQuery(ctx->stream);
-        if (q == hipSuccess) {
-            if (*flag >= seq) break;
-            return fail(ctx, QVQ_EDEVICE, "the stream finished without publishing its flag");
-        }
-        if (q != hipErrorNotReady) return fail(ctx, QVQ_EDEVICE, std::string("stream: ") + hipGetErrorString(q));
-        next_check = std::chrono::steady_clock::now() + std::chrono::milliseconds(20);
+// Probes for wait_until (wait.hpp): the stream's state, and the communicator's asynchronous
+// error state (RCCL reports a peer's failure there while our collective is stuck).
+StreamState probe_stream(qvq_ctx *ctx, std::string &msg) {
+    const hipError_t q = hipStreamQuery(ctx->stream);
+    if (q == hipSuccess) return StreamState::Drained;
+    if (q == hipErrorNotReady) return StreamState::Running;
+    msg = hipGetErrorString(q);
+    return StreamState::Failed;
+}
+CommState probe_comm(qvq_ctx *ctx, std::string &msg) {
+    if (!ctx->comm) return CommState::None;
+    ncclResult_t ae = ncclSuccess;
+    const ncclResult_t r = ncclCommGetAsyncError(ctx->comm, &ae);
+    if (r != ncclSuccess) ae = r;
+    if (ae == ncclSuccess || ae == ncclInProgress) return CommState::Healthy;
+    msg = ncclGetErrorString(ae);
+    return CommState::Failed;
+}
+// A failed or timed-out collective leaves the communicator unusable: abort it (which also
+// releases the stream from a stuck RCCL kernel).  The context keeps working single-rank;
+// qvq_comm_init joins a new communicator.
+qvq_status comm_failed(qvq_ctx *ctx, qvq_status st) {
+    if (st == QVQ_ECOMM && ctx->comm) {
+        (void)ncclCommAbort(ctx->comm);
+        ctx->comm = nullptr;
+        ctx->nranks = 1;
+        ctx->rank = 0;
     }
+    return st;
+}
+
+// Wait until the stream has published seq in a mapped flag (the ready number of finalize's
+// codebook in h_ready, or copy_out's completion).  Bounded: a failed or drained stream, a
+// communicator error, or ctx->timeout_s without progress end the wait with a status.
+qvq_status wait_flag(qvq_ctx *ctx, volatile uint64_t *flag, uint64_t seq) {
+    std::string err;
+    const qvq_status st = wait_until([&] { return *flag >= seq; },
+                                     [&](std::string &m) { return probe_stream(ctx, m); },
+                                     [&](std::string &m) { return probe_comm(ctx, m); }, ctx->timeout_s, err);
+    if (st != QVQ_OK) return comm_failed(ctx, fail(ctx, st, err));
     std::atomic_thread_fence(std::memory_order_acquire);
+    return QVQ_OK;
+}
+// Wait for everything enqueued on the stream so far (an event, polled with the same bounds).
+qvq_status wait_stream(qvq_ctx *ctx) {
+    HIPCHK(hipEventRecord(ctx->ev_sync, ctx->stream));
+    std::string err;
+    hipError_t eq = hipSuccess;
+    const qvq_status st = wait_until(
+        [&] {
+            eq = hipEventQuery(ctx->ev_sync);
+            return eq != hipErrorNotReady;
+        },
+        [&](std::string &m) { return probe_stream(ctx, m); }, [&](std::string &m) { return probe_comm(ctx, m); },
+        ctx->timeout_s, err);
+    if (st != QVQ_OK) return comm_failed(ctx, fail(ctx, st, err));
+    if (eq != hipSuccess) return fail(ctx, QVQ_EDEVICE, std::string("stream: ") + hipGetErrorString(eq));
     return QVQ_OK;
 }
 qvq_status wait_codebook(qvq_ctx *ctx, uint64_t seq) { return wait_flag(ctx, ctx->h_ready, seq); }
@@ -590,6 +636,8 @@ QVQ_API qvq_status qvq_create(int hip_device, qvq_ctx **out) {
         return bail(e, "hipHostGetDevicePointer");
     if ((e = hipMalloc(&ctx->d_counters, (2 * 33 + 2) * sizeof(unsigned))) != hipSuccess) return bail(e, "hipMalloc");
     if ((e = hipMalloc(&ctx->d_hist, 256 * 8)) != hipSuccess) return bail(e, "hipMalloc");
+    if ((e = hipMalloc(&ctx->d_decode_stat, 16)) != hipSuccess) return bail(e, "hipMalloc");
+    if ((e = hipHostMalloc(&ctx->h_decode_stat, 16, hipHostMallocDefault)) != hipSuccess) return bail(e, "hipHostMalloc");
     if ((e = hipMalloc(&ctx->d_dist_part, 8192 * 8)) != hipSuccess) return bail(e, "hipMalloc");
     if ((e = hipMalloc(&ctx->d_mean, (2 * 64 + 1) * 8)) != hipSuccess) return bail(e, "hipMalloc");
     if ((e = hipMemset(ctx->d_mean, 0, (2 * 64 + 1) * 8)) != hipSuccess) return bail(e, "hipMemset");
@@ -597,6 +645,9 @@ QVQ_API qvq_status qvq_create(int hip_device, qvq_ctx **out) {
         for (int j = 0; j < 4; j++)
             if ((e = hipEventCreate(&ctx->ev[l][j])) != hipSuccess) return bail(e, "hipEventCreate");
     if ((e = hipEventCreate(&ctx->ev_end)) != hipSuccess) return bail(e, "hipEventCreate");
+    if ((e = hipEventCreateWithFlags(&ctx->ev_sync, hipEventDisableTiming)) != hipSuccess)
+        return bail(e, "hipEventCreate");
+    if (const char *t = std::getenv("QVQ_TIMEOUT_S")) ctx->timeout_s = std::max(0.001, std::atof(t));
     ctx->ev_ready = true;
     *out = ctx;
     return QVQ_OK;
@@ -619,10 +670,14 @@ QVQ_API void qvq_destroy(qvq_ctx *ctx) {
     dfree(ctx->d_dist_part);
     dfree(ctx->d_mean);
     dfree(ctx->d_scatter);
+    dfree(ctx->d_decode);
+    dfree(ctx->d_decode_stat);
+    if (ctx->h_decode_stat) (void)hipHostFree(ctx->h_decode_stat);
     if (ctx->ev_ready)
         for (int l = 0; l < 32; l++)
             for (int j = 0; j < 4; j++) (void)hipEventDestroy(ctx->ev[l][j]);
     if (ctx->ev_end) (void)hipEventDestroy(ctx->ev_end);
+    if (ctx->ev_sync) (void)hipEventDestroy(ctx->ev_sync);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
     delete ctx;
 }
@@ -796,19 +851,19 @@ QVQ_API qvq_status qvq_lbg(qvq_ctx *ctx, uint32_t bits, double eps, double *code
         uint8_t *dh_small = reinterpret_cast<uint8_t *>(ctx->dh_ready) + 64;
         static_assert(sizeof(dres) + sizeof(stats) <= 1024 - 64, "small results exceed the mapped area");
         const uint64_t cb_bytes = codebook ? (uint64_t)Kmax * ctx->D * 8 : 0;
-        // without assign the copy's own flag ends the wait: polling it wakes the host at once,
-        // where a stream synchronize costs tens of us of wake-up
-        uint64_t *done = assign ? nullptr : reinterpret_cast<uint64_t *>(dh_small + (1024 - 64 - 8));
+        // the copy's own flag ends the wait: polling it wakes the host at once (a stream
+        // synchronize costs tens of us of wake-up), and the wait is bounded (wait.hpp), so a
+        // peer rank that dies inside a level's all-reduce ends this call with QVQ_ECOMM
+        uint64_t *done = reinterpret_cast<uint64_t *>(dh_small + (1024 - 64 - 8));
         const uint64_t seq = ++ctx->out_seq;
         HIPCHK(launch_copy_out(ctx->stream, d_dist, dh_small, sizeof(dres), ctx->d_counters, dh_small + sizeof(dres),
                                sizeof(stats), ctx->d_C64_cent, ctx->dh_cb, cb_bytes, done, seq,
                                ctx->d_counters + 2 * 33 + 1));
-        if (assign) {
+        qvq_status ws = wait_flag(ctx, reinterpret_cast<volatile uint64_t *>(h_small + (1024 - 64 - 8)), seq);
+        if (ws != QVQ_OK) return ws;
+        if (assign) {   // every collective of this call is complete: a plain copy
             HIPCHK(hipMemcpyAsync(assign, ctx->d_A, ctx->N * 4, hipMemcpyDeviceToHost, ctx->stream));
             HIPCHK(hipStreamSynchronize(ctx->stream));
-        } else {
-            qvq_status ws = wait_flag(ctx, reinterpret_cast<volatile uint64_t *>(h_small + (1024 - 64 - 8)), seq);
-            if (ws != QVQ_OK) return ws;
         }
         std::memcpy(dres, h_small, sizeof(dres));
         std::memcpy(stats, h_small + sizeof(dres), sizeof(stats));
@@ -883,8 +938,7 @@ QVQ_API qvq_status qvq_update(qvq_ctx *ctx, const uint32_t *assign, uint32_t K, 
     if (counts)
         HIPCHK(hipMemcpyAsync(counts, ctx->d_sums + 2 * (uint64_t)K * ctx->D, (uint64_t)K * 8, hipMemcpyDeviceToHost,
                               ctx->stream));
-    HIPCHK(hipStreamSynchronize(ctx->stream));
-    return QVQ_OK;
+    return wait_stream(ctx);   // bounded: the all-reduce above may wait on peer ranks
 }
 
 // ---------------------------------------------------------------------------------------
@@ -895,9 +949,32 @@ static qvq_status check_decode_args(qvq_ctx *ctx, uint32_t K, uint64_t nblocks, 
     if (!ctx) return QVQ_EINVAL;
     if (K == 0 || bw == 0 || bh == 0 || xSize == 0 || ySize == 0)
         return fail(ctx, QVQ_EINVAL, "decode: K, block and image sizes must be > 0");
+    // the kernel's block-row count and wrap span are 32-bit
+    if ((uint64_t)ySize + bh - 1 > 0xFFFFFFFFull || (uint64_t)xSize + bw - 1 > 0xFFFFFFFFull)
+        return fail(ctx, QVQ_EINVAL, "decode: image size + block size - 1 exceeds 2^32 - 1");
     const uint64_t wB = ((uint64_t)xSize + bw - 1) / bw, hB = ((uint64_t)ySize + bh - 1) / bh;
     if (nblocks != wB * hB) return fail(ctx, QVQ_EINVAL, "decode: nblocks != ceil(x/bw)*ceil(y/bh)");
     if ((uint64_t)bw * bh * 3 > 0xFFFFFFFFull) return fail(ctx, QVQ_EINVAL, "decode: block too large");
+    return QVQ_OK;
+}
+
+// One decode launch on stream s (0 = the legacy null stream, ordered after every blocking
+// stream's work, as in the caller's own torch/HIP code) with the context's persistent
+// out-of-range flag and signed-byte squared-error accumulator; orig (may be null) is the
+// original raster for the raport's MSE.  Synchronises s.
+static qvq_status run_decode(qvq_ctx *ctx, hipStream_t s, const uint8_t *d_cb, uint32_t K, const uint32_t *d_A,
+                             uint32_t xSize, uint32_t ySize, uint32_t bw, uint32_t bh, uint8_t *d_rgb,
+                             const uint8_t *d_orig, double *mse) {
+    uint64_t *d_err = ctx->d_decode_stat;   // [0] squared error, [1] bad-index flag
+    hipError_t e = hipMemsetAsync(d_err, 0, 16, s);
+    if (e == hipSuccess)
+        e = launch_decode(s, d_cb, K, bw * bh * 3, d_A, xSize, ySize, bw, bh, d_rgb, d_orig, d_err,
+                          reinterpret_cast<uint32_t *>(d_err + 1));
+    if (e == hipSuccess) e = hipMemcpyAsync(ctx->h_decode_stat, d_err, 16, hipMemcpyDeviceToHost, s);
+    if (e == hipSuccess) e = hipStreamSynchronize(s);
+    if (e != hipSuccess) return fail(ctx, QVQ_EDEVICE, std::string("decode: ") + hipGetErrorString(e));
+    if (ctx->h_decode_stat[1]) return fail(ctx, QVQ_EINVAL, "decode: code-vector index out of range");
+    if (mse) *mse = (double)ctx->h_decode_stat[0] / ((double)xSize * ySize * 3);
     return QVQ_OK;
 }
 
@@ -908,46 +985,42 @@ QVQ_API qvq_status qvq_decode_device(qvq_ctx *ctx, const void *d_codebook, uint3
     if (st != QVQ_OK) return st;
     if (!d_codebook || !d_assign || !d_rgb) return fail(ctx, QVQ_EINVAL, "decode: null pointer");
     HIPCHK(hipSetDevice(ctx->dev));
-    hipStream_t s = stream ? (hipStream_t)stream : ctx->stream;
-    uint32_t *d_bad = nullptr;
-    HIPCHK(hipMalloc(&d_bad, sizeof(uint32_t)));
-    uint32_t bad = 0;
-    hipError_t e = hipMemsetAsync(d_bad, 0, sizeof(uint32_t), s);
-    if (e == hipSuccess)
-        e = launch_decode(s, (const uint8_t *)d_codebook, K, bw * bh * 3, (const uint32_t *)d_assign, xSize, ySize, bw,
-                          bh, (uint8_t *)d_rgb, d_bad);
-    if (e == hipSuccess) e = hipMemcpyAsync(&bad, d_bad, sizeof(uint32_t), hipMemcpyDeviceToHost, s);
-    if (e == hipSuccess) e = hipStreamSynchronize(s);
-    (void)hipFree(d_bad);
-    if (e != hipSuccess) return fail(ctx, QVQ_EDEVICE, std::string("decode: ") + hipGetErrorString(e));
-    if (bad) return fail(ctx, QVQ_EINVAL, "decode: code-vector index out of range");
-    return QVQ_OK;
+    return run_decode(ctx, (hipStream_t)stream, (const uint8_t *)d_codebook, K, (const uint32_t *)d_assign, xSize,
+                      ySize, bw, bh, (uint8_t *)d_rgb, nullptr, nullptr);
 }
 
 QVQ_API qvq_status qvq_decode(qvq_ctx *ctx, const uint8_t *codebook, uint32_t K, const uint32_t *assign,
                               uint64_t nblocks, uint32_t xSize, uint32_t ySize, uint32_t bw, uint32_t bh, uint8_t *rgb) {
+    return qvq_decode_mse(ctx, codebook, K, assign, nblocks, xSize, ySize, bw, bh, rgb, nullptr, nullptr);
+}
+
+QVQ_API qvq_status qvq_decode_mse(qvq_ctx *ctx, const uint8_t *codebook, uint32_t K, const uint32_t *assign,
+                                  uint64_t nblocks, uint32_t xSize, uint32_t ySize, uint32_t bw, uint32_t bh,
+                                  uint8_t *rgb, const uint8_t *orig, double *mse) {
     qvq_status st = check_decode_args(ctx, K, nblocks, xSize, ySize, bw, bh);
     if (st != QVQ_OK) return st;
-    if (!codebook || !assign || !rgb) return fail(ctx, QVQ_EINVAL, "decode: null pointer");
+    if (!codebook || !assign || (!rgb && !mse) || (mse && !orig))
+        return fail(ctx, QVQ_EINVAL, "decode: null pointer");
     HIPCHK(hipSetDevice(ctx->dev));
+    // one scratch allocation, grown on demand and kept: codebook | indices | raster | original
     const uint64_t cbB = (uint64_t)K * bw * bh * 3, aB = nblocks * 4, rB = (uint64_t)xSize * ySize * 3;
-    uint8_t *d = nullptr;
-    HIPCHK(hipMalloc(&d, cbB + aB + rB + 8));
-    uint8_t *d_cb = d, *d_rgb = d + cbB + 4;
-    uint32_t *d_A = (uint32_t *)(d + ((cbB + 3) & ~3ull));
-    d_rgb = (uint8_t *)d_A + aB;
-    hipError_t e = hipMemcpyAsync(d_cb, codebook, cbB, hipMemcpyHostToDevice, ctx->stream);
-    if (e == hipSuccess) e = hipMemcpyAsync(d_A, assign, aB, hipMemcpyHostToDevice, ctx->stream);
-    if (e != hipSuccess) {
-        (void)hipFree(d);
-        return fail(ctx, QVQ_EDEVICE, std::string("decode upload: ") + hipGetErrorString(e));
+    const uint64_t oA = (cbB + 15) & ~15ull, oR = (oA + aB + 15) & ~15ull, oO = (oR + rB + 15) & ~15ull;
+    const uint64_t need = oO + (orig ? rB : 0);
+    if (ctx->decode_bytes < need) {
+        dfree(ctx->d_decode);
+        HIPCHK(hipMalloc(&ctx->d_decode, need));
+        ctx->decode_bytes = need;
     }
-    st = qvq_decode_device(ctx, d_cb, K, d_A, nblocks, xSize, ySize, bw, bh, d_rgb, nullptr);
-    if (st == QVQ_OK) {
-        e = hipMemcpy(rgb, d_rgb, rB, hipMemcpyDeviceToHost);
-        if (e != hipSuccess) st = fail(ctx, QVQ_EDEVICE, std::string("decode download: ") + hipGetErrorString(e));
+    uint8_t *d = ctx->d_decode;
+    HIPCHK(hipMemcpyAsync(d, codebook, cbB, hipMemcpyHostToDevice, ctx->stream));
+    HIPCHK(hipMemcpyAsync(d + oA, assign, aB, hipMemcpyHostToDevice, ctx->stream));
+    if (orig) HIPCHK(hipMemcpyAsync(d + oO, orig, rB, hipMemcpyHostToDevice, ctx->stream));
+    st = run_decode(ctx, ctx->stream, d, K, reinterpret_cast<const uint32_t *>(d + oA), xSize, ySize, bw, bh, d + oR,
+                    orig ? d + oO : nullptr, mse);
+    if (st == QVQ_OK && rgb) {
+        HIPCHK(hipMemcpyAsync(rgb, d + oR, rB, hipMemcpyDeviceToHost, ctx->stream));
+        HIPCHK(hipStreamSynchronize(ctx->stream));
     }
-    (void)hipFree(d);
     return st;
 }
 
@@ -967,12 +1040,21 @@ QVQ_API qvq_status qvq_comm_init(qvq_ctx *ctx, int nranks, int rank, const uint8
         ncclCommDestroy(ctx->comm);
         ctx->comm = nullptr;
     }
-    ctx->nranks = nranks;
-    ctx->rank = rank;
-    if (nranks == 1) return QVQ_OK;
+    ctx->nranks = 1;
+    ctx->rank = 0;
+    // a communicator even for one rank: the caller asked for the collective path (it is
+    // then a local copy per level, and the results equal the communicator-free run's)
     ncclUniqueId u;
     std::memcpy(&u, id, 128);
     NCCLCHK(ncclCommInitRank(&ctx->comm, nranks, u, rank));
+    ctx->nranks = nranks;
+    ctx->rank = rank;
+    return QVQ_OK;
+}
+
+QVQ_API qvq_status qvq_set_timeout(qvq_ctx *ctx, double seconds) {
+    if (!ctx || !(seconds > 0)) return QVQ_EINVAL;
+    ctx->timeout_s = seconds;
     return QVQ_OK;
 }
 
@@ -1005,6 +1087,34 @@ QVQ_API qvq_status qvq_host_finalize(const uint64_t *hi, const uint64_t *lo, con
         for (uint32_t d = 0; d < dim; d++)
             C_out[k * dim + d] = centroid_value(hi[k * dim + d], lo[k * dim + d], cnt[k], t.R, t.bias, t.scale);
     return QVQ_OK;
+}
+
+QVQ_API qvq_status qvq_host_wait_probe(int scenario, double timeout_s, double *elapsed_s) {
+    if (scenario < 0 || scenario > 5 || !(timeout_s > 0)) return QVQ_EINVAL;
+    using clock = std::chrono::steady_clock;
+    const auto t0 = clock::now();
+    auto after = [&](double s) { return std::chrono::duration<double>(clock::now() - t0).count() >= s; };
+    std::string err;
+    const qvq_status st = wait_until(
+        [&] { return scenario == 0 && after(0.005); },
+        [&](std::string &m) {
+            if (scenario == 4) {
+                m = "scripted stream fault";
+                return StreamState::Failed;
+            }
+            return scenario == 5 ? StreamState::Drained : StreamState::Running;
+        },
+        [&](std::string &m) {
+            if (scenario == 3 && after(0.005)) {
+                m = "scripted peer failure";
+                return CommState::Failed;
+            }
+            return scenario == 2 || scenario == 3 ? CommState::Healthy : CommState::None;
+        },
+        timeout_s, err);
+    if (elapsed_s) *elapsed_s = std::chrono::duration<double>(clock::now() - t0).count();
+    if (st != QVQ_OK) g_static_err = err;
+    return st;
 }
 
 QVQ_API qvq_status qvq_host_row_terms(const uint8_t *codes, uint32_t dim, int colorspace, uint64_t *hi,

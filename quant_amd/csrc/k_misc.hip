@@ -838,59 +838,167 @@ hipError_t launch_byte_hist(hipStream_t s, const uint8_t *codes, uint64_t N, uin
 namespace qvq {
 
 // Decode (CompressedImage::decompress, src/Compressor.cpp:156-165 over getImageFromVectors,
-// src/Compressor.cpp:64-85 there): gather code-vector bytes into the raster.  One thread per
-// output pixel, so no write races.  The reference writes block by block (i, j, dx, dy) in loop
-// order with "last writer wins"; a block column that overhangs ySize wraps into the next
-// raster row(s).  Pixel dst = x*ys + y is written by every (x', y') with x'*ys + y' == dst,
-// x' <= x, y' < hB*h; the winner is the lexicographically largest (i, j, dx, dy), exactly the
-// reference's final write.  Code vectors stay in L2 (K*D <= 12 MB at 2^24 x 12 is the worst
-// case; C3 is 12 KB).  Out-of-range indices (the reference throws from .at()) write 0 and
-// raise *bad.
-// T = uint32_t when the raster's index math fits (64-bit divides are emulated in ~40 VALU).
-template <typename T>
-__global__ __launch_bounds__(256) void decode_kernel(const uint8_t *__restrict__ cb, uint32_t K, uint32_t D,
-                                                     const uint32_t *__restrict__ A, uint32_t xs, uint32_t ys,
-                                                     uint32_t w, uint32_t h, uint32_t hB, uint8_t *__restrict__ rgb,
-                                                     uint32_t *__restrict__ bad) {
-    const T npix = (T)xs * ys;
-    const T yspan = (T)hB * h;
-    for (T dst = blockIdx.x * (T)blockDim.x + threadIdx.x; dst < npix; dst += (T)gridDim.x * blockDim.x) {
-        const T x = dst / ys;
-        T bi = 0, bj = 0, bdx = 0, bdy = 0;
-        bool have = false;
-        for (T xp = x + 1; xp-- > 0;) {
-            const T yp = dst - xp * ys;
-            if (yp >= yspan) break;   // grows as xp falls
-            const T i = xp / w, dx = xp - i * w, j = yp / h, dy = yp - j * h;
-            if (!have || i > bi || (i == bi && (j > bj || (j == bj && (dx > bdx || (dx == bdx && dy > bdy)))))) {
-                bi = i, bj = j, bdx = dx, bdy = dy;
-                have = true;
-            }
-        }
-        uint8_t r = 0, g = 0, b = 0;
-        if (have) {
-            const uint32_t a = A[(uint64_t)bi * hB + bj];
-            if (a < K) {
-                const uint8_t *row = cb + (uint64_t)a * D + ((uint64_t)bdx * h + bdy) * 3;
-                r = row[0], g = row[1], b = row[2];
-            } else {
-                atomicOr(bad, 1u);
-            }
-        }
-        uint8_t *o = rgb + (uint64_t)dst * 3;
-        o[0] = r, o[1] = g, o[2] = b;
+// src/Compressor.cpp:64-85 there): gather code-vector bytes into the raster.  Each output
+// pixel is computed by one thread, so there are no write races.  The reference writes block
+// by block in loop order (i, j, dx, dy), "last writer wins", and a block column that
+// overhangs ySize wraps into the next raster row(s).  Pixel (x, y) = P / ys, P % ys is
+// written by (x - m, y + m*ys) for every m >= 0 with y + m*ys < hB*h; the last of them in
+// that order has the largest block row i, then the largest j, then the largest dx.  Only m
+// <= dx0 = x % w keep i = x / w; j grows with m, and among equal j the smallest m wins:
+//   M = min(dx0, (yspan - 1 - y) / ys),  jM = (y + M*ys) / h,  m* = max(0, ceil((jM*h - y)/ys)).
+// Without an overhang (ys % h == 0) m* = 0 for every pixel: a plain gather.
+// Out-of-range indices (undefined behaviour in the reference, which indexes codeVectors with
+// operator[]) write 0 and raise *bad.  With orig the kernel also sums the raport's squared
+// signed-byte differences (src/Compressor.cpp:137-146) into *sqerr.
+struct DecodeArgs {
+    const uint8_t *cb;
+    uint32_t K, D;
+    const uint32_t *A;
+    uint32_t xs, ys, w, h, hB, yspan, overhang;
+    uint8_t *rgb;
+    const uint8_t *orig;
+    unsigned long long *sqerr;
+    uint32_t *bad;
+};
+
+// (block index, byte offset in its code vector) of the last writer of pixel (x, y)
+__device__ inline void decode_writer(const DecodeArgs &a, uint32_t x, uint32_t y, uint32_t i0, uint32_t dx0,
+                                     uint32_t &blk, uint32_t &off) {
+    uint32_t m = 0;
+    if (y < a.overhang && dx0 > 0) {
+        const uint32_t M = min(dx0, (a.yspan - 1 - y) / a.ys);
+        const uint32_t jM = (y + M * a.ys) / a.h;
+        const uint32_t need = jM * a.h;   // >= y is not guaranteed: clamp at 0
+        m = need > y ? (need - y + a.ys - 1) / a.ys : 0;
+    }
+    const uint32_t yp = y + m * a.ys, j = yp / a.h;
+    blk = i0 * a.hB + j;
+    off = ((dx0 - m) * a.h + (yp - j * a.h)) * 3;
+}
+
+__device__ inline uint32_t decode_pixel(const DecodeArgs &a, const uint8_t *cb, uint32_t blk, uint32_t off,
+                                        bool &bad) {
+    const uint32_t code = a.A[blk];
+    if (code >= a.K) {
+        bad = true;
+        return 0;
+    }
+    const uint8_t *p = cb + code * a.D + off;
+    return (uint32_t)p[0] | (uint32_t)p[1] << 8 | (uint32_t)p[2] << 16;
+}
+
+__device__ inline uint32_t sq_diff_bytes(uint32_t u, uint32_t v) {   // signed bytes, all four
+    uint32_t s = 0;
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        const int d = (int)(int8_t)(u >> (8 * k)) - (int)(int8_t)(v >> (8 * k));
+        s += (uint32_t)(d * d);
+    }
+    return s;
+}
+
+__device__ inline void decode_finish(const DecodeArgs &a, uint64_t sq, bool bad) {
+    if (bad) atomicOr(a.bad, 1u);
+    if (a.orig) {   // one atomic per wave
+#pragma unroll
+        for (int off = 32; off >= 1; off >>= 1) sq += __shfl_xor(sq, off);
+        if ((threadIdx.x & 63) == 0 && sq) atomicAdd(a.sqerr, (unsigned long long)sq);
     }
 }
 
+// Rows of ys % 8 == 0 pixels: thread (x, q) produces pixels y = 8q .. 8q + 7 of raster row x,
+// 24 contiguous 8-byte-aligned bytes stored as three dwordx2 (and the original read the same
+// way for the MSE).  The codebook sits in LDS when it is small (C3: 12 KB).
+template <bool LDSCB>
+__global__ __launch_bounds__(256) void decode_rows_kernel(DecodeArgs a) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t scb[];
+    if (LDSCB) {
+        const uint32_t n4 = (a.K * a.D + 3) / 4;
+        for (uint32_t i = threadIdx.x; i < n4; i += 256)
+            reinterpret_cast<uint32_t *>(scb)[i] = reinterpret_cast<const uint32_t *>(a.cb)[i];
+        __syncthreads();
+    }
+    const uint8_t *cb = LDSCB ? scb : a.cb;
+    const uint32_t qpr = a.ys / 8;
+    const uint64_t total = (uint64_t)a.xs * qpr;
+    uint64_t sq = 0;
+    bool bad = false;
+    for (uint64_t t = blockIdx.x * 256ull + threadIdx.x; t < total; t += (uint64_t)gridDim.x * 256) {
+        const uint32_t x = (uint32_t)(t / qpr), y0 = (uint32_t)(t - (uint64_t)x * qpr) * 8;
+        const uint32_t i0 = x / a.w, dx0 = x - i0 * a.w;
+        uint32_t px[8];
+#pragma unroll
+        for (int k = 0; k < 8; k++) {
+            uint32_t blk, off;
+            decode_writer(a, x, y0 + k, i0, dx0, blk, off);
+            px[k] = decode_pixel(a, cb, blk, off, bad);
+        }
+        // 8 pixels x 3 bytes -> 6 words
+        uint32_t wv[6];
+        wv[0] = px[0] | px[1] << 24;
+        wv[1] = px[1] >> 8 | px[2] << 16;
+        wv[2] = px[2] >> 16 | px[3] << 8;
+        wv[3] = px[4] | px[5] << 24;
+        wv[4] = px[5] >> 8 | px[6] << 16;
+        wv[5] = px[6] >> 16 | px[7] << 8;
+        const uint64_t byte0 = ((uint64_t)x * a.ys + y0) * 3;
+        uint2 *dst = reinterpret_cast<uint2 *>(a.rgb + byte0);
+        dst[0] = make_uint2(wv[0], wv[1]);
+        dst[1] = make_uint2(wv[2], wv[3]);
+        dst[2] = make_uint2(wv[4], wv[5]);
+        if (a.orig) {
+            const uint2 *o = reinterpret_cast<const uint2 *>(a.orig + byte0);
+            const uint2 o0 = o[0], o1 = o[1], o2 = o[2];
+            sq += sq_diff_bytes(wv[0], o0.x) + sq_diff_bytes(wv[1], o0.y) + sq_diff_bytes(wv[2], o1.x) +
+                  sq_diff_bytes(wv[3], o1.y) + sq_diff_bytes(wv[4], o2.x) + sq_diff_bytes(wv[5], o2.y);
+        }
+    }
+    decode_finish(a, sq, bad);
+}
+
+// Any raster: one thread per pixel, byte stores (ys % 8 != 0).
+__global__ __launch_bounds__(256) void decode_pixels_kernel(DecodeArgs a) {
+    const uint64_t npix = (uint64_t)a.xs * a.ys;
+    uint64_t sq = 0;
+    bool bad = false;
+    for (uint64_t P = blockIdx.x * 256ull + threadIdx.x; P < npix; P += (uint64_t)gridDim.x * 256) {
+        const uint32_t x = (uint32_t)(P / a.ys), y = (uint32_t)(P - (uint64_t)x * a.ys);
+        const uint32_t i0 = x / a.w, dx0 = x - i0 * a.w;
+        uint32_t blk, off;
+        decode_writer(a, x, y, i0, dx0, blk, off);
+        const uint32_t v = decode_pixel(a, a.cb, blk, off, bad);
+        uint8_t *o = a.rgb + P * 3;
+        o[0] = (uint8_t)v, o[1] = (uint8_t)(v >> 8), o[2] = (uint8_t)(v >> 16);
+        if (a.orig) {
+            const uint8_t *q = a.orig + P * 3;
+            sq += sq_diff_bytes(v, (uint32_t)q[0] | (uint32_t)q[1] << 8 | (uint32_t)q[2] << 16);
+        }
+    }
+    decode_finish(a, sq, bad);
+}
+
 hipError_t launch_decode(hipStream_t s, const uint8_t *cb, uint32_t K, uint32_t D, const uint32_t *A, uint32_t xs,
-                         uint32_t ys, uint32_t w, uint32_t h, uint8_t *rgb, uint32_t *bad) {
-    const uint64_t npix = (uint64_t)xs * ys;
-    const uint32_t hB = (ys + h - 1) / h;
-    const int grid = (int)std::max<uint64_t>(1, std::min<uint64_t>((npix + 255) / 256, 1u << 16));
-    if (((uint64_t)xs + w) * ((uint64_t)ys + h) < (1ull << 32) - (1ull << 25))
-        hipLaunchKernelGGL(decode_kernel<uint32_t>, dim3(grid), dim3(256), 0, s, cb, K, D, A, xs, ys, w, h, hB, rgb, bad);
-    else
-        hipLaunchKernelGGL(decode_kernel<uint64_t>, dim3(grid), dim3(256), 0, s, cb, K, D, A, xs, ys, w, h, hB, rgb, bad);
+                         uint32_t ys, uint32_t w, uint32_t h, uint8_t *rgb, const uint8_t *orig,
+                         uint64_t *sqerr, uint32_t *bad) {
+    DecodeArgs a;
+    a.cb = cb, a.K = K, a.D = D, a.A = A, a.xs = xs, a.ys = ys, a.w = w, a.h = h;
+    a.hB = (uint32_t)(((uint64_t)ys + h - 1) / h);   // the caller checks ys + h - 1 < 2^32
+    a.yspan = a.hB * h;
+    a.overhang = a.yspan - ys;
+    a.rgb = rgb, a.orig = orig, a.sqerr = (unsigned long long *)sqerr, a.bad = bad;
+    if (ys % 8 == 0 && (uint64_t)xs * ys < (1ull << 40)) {
+        const uint64_t items = (uint64_t)xs * (ys / 8);
+        const int grid = (int)std::max<uint64_t>(1, std::min<uint64_t>((items + 255) / 256, 1u << 16));
+        const size_t cbB = (size_t)K * D;
+        if (cbB <= 48 * 1024)
+            hipLaunchKernelGGL(decode_rows_kernel<true>, dim3(grid), dim3(256), (cbB + 15) & ~(size_t)15, s, a);
+        else
+            hipLaunchKernelGGL(decode_rows_kernel<false>, dim3(grid), dim3(256), 0, s, a);
+    } else {
+        const uint64_t npix = (uint64_t)xs * ys;
+        const int grid = (int)std::max<uint64_t>(1, std::min<uint64_t>((npix + 255) / 256, 1u << 16));
+        hipLaunchKernelGGL(decode_pixels_kernel, dim3(grid), dim3(256), 0, s, a);
+    }
     return hipGetLastError();
 }
 

@@ -62,3 +62,45 @@ def test_decode_device_c3_checksum(engine):
     engine.decode_device(d_cb.data_ptr(), 1024, d_A.data_ptr(), A.size, xs, ys, 2, 2, d_rgb.data_ptr(),
                          torch.cuda.current_stream().cuda_stream)
     np.testing.assert_array_equal(d_rgb.cpu().numpy(), oracle.decode(cb, A, xs, ys, 2, 2).ravel())
+
+
+@pytest.mark.parametrize("xs,ys,bw,bh", [(510, 383, 2, 2), (256, 256, 2, 2), (383, 512, 4, 4), (33, 65, 1, 1)])
+def test_decode_mse_matches_raport(engine, xs, ys, bw, bh):
+    """qvq_decode_mse: the raport's distortion (src/Compressor.cpp:133-146, signed bytes) from
+    the same device pass as the decoded raster."""
+    rng = np.random.default_rng(xs + ys)
+    cb, A = _rand_case(rng, xs, ys, bw, bh, 64)
+    orig = rng.integers(0, 256, size=xs * ys * 3, dtype=np.uint8)
+    img, mse = engine.decode_mse(cb, A, xs, ys, bw, bh, orig)
+    want = oracle.decode(cb, A, xs, ys, bw, bh).ravel()
+    np.testing.assert_array_equal(img, want)
+    assert mse == oracle.raport_distortion(orig, want)   # integer sum / count: exact
+    _, mse2 = engine.decode_mse(cb, A, xs, ys, bw, bh, orig, want_image=False)
+    assert mse2 == mse
+
+
+@pytest.mark.parametrize("which", ["torch_stream", "null_stream"])
+def test_decode_device_orders_after_caller_stream(engine, which):
+    """The decode launches on the caller's stream (0 = the legacy null stream), so indices a
+    device op writes just before the call are the ones decoded."""
+    import torch
+    xs = ys = 1024
+    rng = np.random.default_rng(3)
+    cb, A = _rand_case(rng, xs, ys, 2, 2, 256)
+    d_cb = torch.from_numpy(cb).cuda()
+    src = torch.from_numpy(A.view(np.int32)).cuda()
+    d_A = torch.zeros_like(src)
+    d_rgb = torch.empty(xs * ys * 3, dtype=torch.uint8, device="cuda")
+    torch.cuda.synchronize()
+    if which == "torch_stream":
+        s = torch.cuda.Stream()
+        with torch.cuda.stream(s):
+            torch.cuda._sleep(2_000_000)      # keep the stream busy so an unordered read sees zeros
+            d_A.copy_(src)
+        handle = s.cuda_stream
+    else:
+        torch.cuda._sleep(2_000_000)          # legacy default stream
+        d_A.copy_(src)
+        handle = 0
+    engine.decode_device(d_cb.data_ptr(), 256, d_A.data_ptr(), A.size, xs, ys, 2, 2, d_rgb.data_ptr(), handle)
+    np.testing.assert_array_equal(d_rgb.cpu().numpy(), oracle.decode(cb, A, xs, ys, 2, 2).ravel())

@@ -66,3 +66,23 @@ def test_exact_sum_finaliser(cs):
     cnt = np.bincount(A, minlength=K).astype(np.uint64)
     C = quant_amd.host_finalize(H, Lo, cnt, cs)
     np.testing.assert_array_equal(C, oracle.centroids(X, A, K, sum_mode=1))
+
+
+@pytest.mark.parametrize("scenario,status,max_s", [
+    (0, 0, 0.15),     # the work publishes after ~5 ms
+    (1, 3, 1.0),      # never publishes, no communicator: QVQ_EDEVICE at the timeout
+    (2, 4, 1.0),      # never publishes, communicator joined: QVQ_ECOMM (a peer rank stalled)
+    (3, 4, 0.15),     # the communicator reports a peer failure: QVQ_ECOMM before the timeout
+    (4, 3, 0.15),     # the stream faults: QVQ_EDEVICE
+    (5, 3, 0.15),     # the stream drains without publishing: QVQ_EDEVICE
+])
+def test_bounded_wait_policy(scenario, status, max_s):
+    """Every host wait of the engine on its stream is bounded (failure
+    detection): a dead peer rank or a faulted stream ends the call with a status instead of
+    hanging (quant_amd/csrc/wait.hpp, exercised through qvq_host_wait_probe)."""
+    import quant_amd
+    st, el = quant_amd.host_wait_probe(scenario, 0.25)
+    assert st == status
+    assert el <= max_s
+    if scenario in (1, 2):
+        assert el >= 0.25
