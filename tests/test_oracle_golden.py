@@ -98,3 +98,41 @@ def test_kdtree_restatement_vs_compiled_reference():
         ref = np.empty(len(X), np.uint32)
         R.ref_kdtree_nn(oracle._p(C), len(C), 12, oracle._p(X), len(X), oracle._p(ref))
         np.testing.assert_array_equal(oracle.kdtree_nn(C, X), ref)
+
+
+def _ref_nn(C, Q):
+    import ctypes
+    R = ctypes.CDLL(REF_SO)
+    R.ref_kdtree_nn.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_void_p, ctypes.c_size_t,
+                                ctypes.c_void_p]
+    C = np.ascontiguousarray(C, np.float64)
+    Q = np.ascontiguousarray(Q, np.float64)
+    out = np.empty(len(Q), np.uint32)
+    R.ref_kdtree_nn(oracle._p(C), len(C), C.shape[1], oracle._p(Q), len(Q), oracle._p(out))
+    return out
+
+
+@pytest.mark.skipif(not os.path.exists(REF_SO), reason="oracle/_ref not built (reference not mounted)")
+@pytest.mark.parametrize("case", ["beans_2x2_n8", "s512_2x2_n10", "s320_4x4_n12"])
+def test_per_level_assignments_vs_compiled_nanoflann(case):
+    """Closes the pinning seam between the restated kd-tree and the reference's own nanoflann
+    (VERDICT r1 weak #1): the oracle's per-level split codebooks of real LBG runs -- beans n8,
+    s512 n10, and a 4x4-block image up to n12 (D = 48, K = 4096, where the C4 ties live) --
+    searched by the compiled reference kd-tree for every row of every level must give the
+    indices the oracle's restated search gave (nanoflann.hpp:863-871,1212-1270,
+    KDTreeVectorOfVectorsAdaptor.hpp:59)."""
+    from conftest import load_png_rgb
+    if case == "beans_2x2_n8":
+        rgb, xs, ys = load_png_rgb("beans.png")
+        X, _ = oracle.tile(rgb, xs, ys, 2, 2)
+        bits = 8
+    elif case == "s512_2x2_n10":
+        X, _ = oracle.tile(oracle.gen_image(512), 512, 512, 2, 2)
+        bits = 10
+    else:
+        X, _ = oracle.tile(oracle.gen_image(320), 320, 320, 4, 4)
+        bits = 12
+    _, _, _, splits, assigns = oracle.lbg(X, bits, sum_mode=0, dump=True)
+    for lvl, (Cs, A) in enumerate(zip(splits, assigns), start=1):
+        ref = _ref_nn(Cs, X)
+        np.testing.assert_array_equal(A, ref, err_msg="level %d (K=%d, D=%d)" % (lvl, len(Cs), X.shape[1]))
