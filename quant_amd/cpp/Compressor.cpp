@@ -106,6 +106,22 @@ std::tuple<std::vector<Vector>, std::vector<size_t>, VectorType> quantize_raster
     return std::make_tuple(std::move(codebook), std::vector<size_t>(A.begin(), A.end()), distortion);
 }
 
+// Codebook bytes [K][bw*bh*3] (short entries zero-filled) and u32 indices for qvq_decode.
+void flatten_for_decode(const CompressedImage &c, std::vector<uint8_t> &cb, std::vector<uint32_t> &idx) {
+    const size_t D = c.blockWidth * c.blockHeight * 3, K = c.codeVectors.size();
+    if (K == 0 || K > 0xFFFFFFFFull) throw std::runtime_error("decompress: bad codebook size");
+    cb.assign(K * D, 0);
+    for (size_t k = 0; k < K; k++) {
+        const CharVector &v = c.codeVectors[k];
+        std::copy(v.begin(), v.begin() + std::min(v.size(), D), reinterpret_cast<char *>(cb.data()) + k * D);
+    }
+    idx.resize(c.assignedCodeVector.size());
+    for (size_t i = 0; i < idx.size(); i++) {
+        if (c.assignedCodeVector[i] >= K) throw std::runtime_error("decompress: code-vector index out of range");
+        idx[i] = (uint32_t)c.assignedCodeVector[i];
+    }
+}
+
 std::string pretty_bytes(size_t bytes) {   // src/Compressor.cpp:270-287, remainder quirk kept
     std::ostringstream s;
     if (bytes < 1024) {
@@ -150,16 +166,21 @@ std::pair<CompressedImage, CompressionRaport> CompressedImage::compress(const RG
     out.colorSpace = colorSpace;
     out.quantizer = quantizer;
 
-    // distortion of the decoded image in signed byte units (src/Compressor.cpp:133-144)
-    const RGBImage dec = decompress(out);
-    double err = 0;
-    for (size_t i = 0; i < image.img.size(); i++)
-        for (int c = 0; c < 3; c++) {
-            const double e = (double)image.img[i][c] - (double)dec.img[i][c];
-            err += e * e;
-        }
+    // distortion of the decoded image in signed byte units (src/Compressor.cpp:133-146), from
+    // one device decode pass that also sums the squared differences (qvq_decode_mse)
+    double mse = 0;
+    {
+        std::vector<uint8_t> cb;
+        std::vector<uint32_t> idx;
+        flatten_for_decode(out, cb, idx);
+        EngineHandle::check(qvq_decode_mse(EngineHandle::get(), cb.data(), (uint32_t)out.codeVectors.size(), idx.data(),
+                                           idx.size(), (uint32_t)out.xSize, (uint32_t)out.ySize,
+                                           (uint32_t)out.blockWidth, (uint32_t)out.blockHeight, nullptr,
+                                           reinterpret_cast<const uint8_t *>(image.img.data()), &mse),
+                            "qvq_decode_mse");
+    }
     CompressionRaport r;
-    r.distortion = err / (double)(image.img.size() * 3);
+    r.distortion = mse;
     r.bitsPerPixel = (float)out.sizeInBits() / (float)(image.xSize * image.ySize);
     r.uncompressedSize = image.sizeInBytes();
     r.compressedSize = out.sizeInBits() / 8;
@@ -167,11 +188,20 @@ std::pair<CompressedImage, CompressionRaport> CompressedImage::compress(const RG
     return std::make_pair(std::move(out), r);
 }
 
-// src/Compressor.cpp:156-165
+// src/Compressor.cpp:156-165 (+ getImageFromVectors, :64-92): one device gather (qvq_decode).
 RGBImage CompressedImage::decompress(const CompressedImage &c) {
-    std::vector<CharVector> blocks(c.assignedCodeVector.size());
-    for (size_t i = 0; i < blocks.size(); i++) blocks[i] = c.codeVectors.at(c.assignedCodeVector[i]);
-    return getImageFromVectors(blocks, (int)c.xSize, (int)c.ySize, (int)c.blockWidth, (int)c.blockHeight);
+    std::vector<uint8_t> cb;
+    std::vector<uint32_t> idx;
+    flatten_for_decode(c, cb, idx);
+    RGBImage img;
+    img.xSize = (int)c.xSize;
+    img.ySize = (int)c.ySize;
+    img.img.assign(c.xSize * c.ySize, RGB{0, 0, 0});
+    EngineHandle::check(qvq_decode(EngineHandle::get(), cb.data(), (uint32_t)c.codeVectors.size(), idx.data(), idx.size(),
+                                   (uint32_t)c.xSize, (uint32_t)c.ySize, (uint32_t)c.blockWidth,
+                                   (uint32_t)c.blockHeight, reinterpret_cast<uint8_t *>(img.img.data())),
+                        "qvq_decode");
+    return img;
 }
 
 // src/Compressor.cpp:174-183
