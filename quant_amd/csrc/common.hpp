@@ -137,10 +137,22 @@ struct MfThresholds {
     float inv_scale;   // 2^-t
     float mu, sx;      // x = mu + w * sx
     uint32_t runs_max_k;   // fused sums: wave run reduction up to this K, plain LDS atomics above
+    // small-K scan (expanded fp32 scores): flag when second - best <= e0 + e1 * sum_d |w_d|
+    float e0, e1;
 };
 uint32_t mf_fuse_max_k();
 bool mf_can_search(uint32_t K);
+// K <= 32: expanded fp32 scores from E32 [Kp][16] = [c''(0..11) | n | 0 0 0] (the MFMA row's
+// terms in fp32; padding rows n = 1e30).
 hipError_t launch_assign_mfma(hipStream_t s, int grid, bool fuse, const uint8_t *codes, uint64_t N,
+                              const _Float16 *cb_rows, const float *E32, uint32_t K, const float *C32,
+                              const uint64_t *plut,
+                              const MfThresholds &th, uint32_t *A, uint32_t *flags, unsigned *flag_cnt,
+                              uint64_t *part, uint32_t *part_cnt);
+// The same search on v_mfma_f32_32x32x16_f16 tiles (k_mf32.hip); launch_assign_mfma uses it
+// for K above the small-K scan whenever mf32_fits.
+bool mf32_fits(uint32_t K, bool fuse);
+hipError_t launch_assign_mf32(hipStream_t s, int grid, bool fuse, const uint8_t *codes, uint64_t N,
                               const _Float16 *cb_rows, uint32_t K, const float *C32, const uint64_t *plut,
                               const MfThresholds &th, uint32_t *A, uint32_t *flags, unsigned *flag_cnt,
                               uint64_t *part, uint32_t *part_cnt);
@@ -191,14 +203,15 @@ hipError_t launch_mean_sums(hipStream_t s, uint32_t Dp, const uint8_t *codes, ui
 // holds the per-block partials (<= 8000).
 hipError_t launch_finalize_prep(hipStream_t s, const uint64_t *sums, uint32_t K, uint32_t D, uint32_t Dp, int64_t R,
                                 int64_t bias, int scale, double *C_cent, bool split, double *C64n, uint32_t Kpad_next,
-                                double mu, double sx, int t, float *C32, _Float16 *cb_rows, double *host_cb,
-                                double *dist_part, unsigned *done, double *dist_out, uint64_t *ready, uint64_t seq,
+                                double mu, double sx, int t, float *C32, _Float16 *cb_rows, float *E32,
+                                double *host_cb, double *dist_part, unsigned *done, double *dist_out, uint64_t *ready, uint64_t seq,
                                 bool zero_sums);
 hipError_t launch_finalize(hipStream_t s, const uint64_t *sums, uint32_t K, uint32_t D, int64_t R, int64_t bias,
                            int scale, double *C_cent);
 // f16 MFMA tables (D = 12) and fp32 VALU table from an fp64 codebook of K code vectors.
+// With E32 (D = 12) also the expanded fp32 table of launch_assign_mfma.
 hipError_t launch_prep(hipStream_t s, const double *C64, uint32_t K, uint32_t Kpad, uint32_t D, uint32_t Dp,
-                       double mu, double sx, int t, float *C32, _Float16 *cb_rows);
+                       double mu, double sx, int t, float *C32, _Float16 *cb_rows, float *E32);
 hipError_t launch_gather_codes(hipStream_t s, const uint8_t *codes, uint32_t Dp, const uint32_t *rows, uint32_t n,
                                uint8_t *out);
 // Host-resolved rows: A[rows[i]] = vals[i]; with xslab their terms move from the

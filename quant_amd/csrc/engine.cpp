@@ -98,6 +98,7 @@ struct qvq_ctx {
     uint32_t G = 0;   // workgroup slabs
     double *d_C64_cent = nullptr, *d_C64_split = nullptr;
     float *d_C32 = nullptr;
+    float *d_E32 = nullptr;   // D = 12: expanded fp32 terms for the small-K scan
     _Float16 *d_rows = nullptr;   // MFMA code-vector rows
     uint64_t *d_part = nullptr, *d_sums = nullptr;
     uint32_t *d_part_cnt = nullptr;
@@ -201,6 +202,7 @@ void free_levels(qvq_ctx *ctx) {
     dfree(ctx->d_C64_cent);
     dfree(ctx->d_C64_split);
     dfree(ctx->d_C32);
+    dfree(ctx->d_E32);
     dfree(ctx->d_rows);
     dfree(ctx->d_part);
     dfree(ctx->d_part_cnt);
@@ -258,6 +260,15 @@ void mfma_setup(qvq_ctx *ctx) {
     ctx->mf_th.beta = (float)(2.0 * ((ctx->Dp + 4) * u * 1.01 + 4e-15));
     ctx->mf_th.gamma = (float)(2.0 * 4.01 * u * u * L * L + 1e-30);
     ctx->mf_th.inv_scale = (float)std::ldexp(1.0, -tt);
+    // small-K scan (assign_small_kernel): each expanded score is an fp32 fma chain from n over
+    // the D terms w_d * c''_d, with n and c'' rounded to fp32 once and w exact, so its error is
+    // at most (D + 1) u (1 + u)^D (n + sum_d |w_d| |c''_d|) <= (D + 2) u S_row; two scores are
+    // compared.  S_row <= 2^t (n_max + c2_max sum_d |w_d|), plus a 1e-11 relative floor for the
+    // reference's own fp64 rounding (as e_conv above).
+    const double sc = std::ldexp(1.0, tt);
+    const double ks = 2.0 * (D + 2) * u * 1.01;
+    ctx->mf_th.e0 = (float)((ks * n_max + 1e-11 * s_bound) * sc * 1.0001);
+    ctx->mf_th.e1 = (float)(ks * c2_max * sc * 1.0001);
     ctx->mf_th.mu = (float)t.mu;
     ctx->mf_th.sx = (float)t.sx;
     {
@@ -301,6 +312,7 @@ qvq_status ensure_levels(qvq_ctx *ctx, uint32_t Kmax) {
     HIPCHK(hipMalloc(&ctx->d_C64_cent, KD * 8));
     HIPCHK(hipMalloc(&ctx->d_C64_split, KD * 8));
     HIPCHK(hipMalloc(&ctx->d_C32, Kp * ctx->Dp * 4));
+    if (ctx->D == MF_D) HIPCHK(hipMalloc(&ctx->d_E32, Kp * 16 * 4));
     HIPCHK(hipMalloc(&ctx->d_rows, Kp * 2 * cb_row_f16(ctx->D, ctx->Dp)));
     // G per-CU slabs + two correction slabs (fused path: rows the recheck / kd-tree move, at
     // the new index (+) and at the search's provisional one (-))
@@ -323,7 +335,7 @@ qvq_status ensure_levels(qvq_ctx *ctx, uint32_t Kmax) {
 // Search tables for the K code vectors in d_C64_split.
 qvq_status run_prep(qvq_ctx *ctx, uint32_t K) {
     HIPCHK(launch_prep(ctx->stream, ctx->d_C64_split, K, pad32(K), ctx->D, ctx->Dp, ctx->terms.mu, ctx->terms.sx,
-                       ctx->mf_t, ctx->d_C32, ctx->d_rows));
+                       ctx->mf_t, ctx->d_C32, ctx->d_rows, ctx->d_E32));
     return QVQ_OK;
 }
 
@@ -514,7 +526,7 @@ qvq_status run_level(qvq_ctx *ctx, uint32_t K, int slot, bool sums_out, const do
     const bool timing = ctx->timing_level == -1 || ctx->timing_level == slot;
     if (timing) HIPCHK(hipEventRecord(ctx->ev[slot][0], ctx->stream));
     if (use_mfma(ctx, K)) {
-        HIPCHK(launch_assign_mfma(ctx->stream, ctx->num_cu, fused, ctx->d_codes, ctx->N, ctx->d_rows, K,
+        HIPCHK(launch_assign_mfma(ctx->stream, ctx->num_cu, fused, ctx->d_codes, ctx->N, ctx->d_rows, ctx->d_E32, K,
                                   ctx->d_C32, ctx->d_plut, ctx->mf_th, ctx->d_A, ctx->d_flags, &cnt[0],
                                   ctx->d_part, ctx->d_part_cnt));
     } else if (use_wide(ctx, K)) {
@@ -819,7 +831,8 @@ QVQ_API qvq_status qvq_lbg(qvq_ctx *ctx, uint32_t bits, double eps, double *code
         return launch_finalize_prep(ctx->stream, K == 1 ? ctx->d_mean : ctx->d_sums, K, ctx->D, ctx->Dp, T.R, T.bias,
                                     T.scale,
                                     ctx->d_C64_cent, split, ctx->d_C64_split, pad32(2 * K), T.mu, T.sx, ctx->mf_t,
-                                    ctx->d_C32, ctx->d_rows, split ? ctx->dh_cb : nullptr, d_dist + 8, dist_done,
+                                    ctx->d_C32, ctx->d_rows, ctx->d_E32, split ? ctx->dh_cb : nullptr, d_dist + 8,
+                                    dist_done,
                                     split ? nullptr : d_dist + 2, split ? ctx->dh_ready : nullptr, ctx->seq,
                                     K == 1);
     };

@@ -403,7 +403,10 @@ __global__ __launch_bounds__(MF_THREADS) void assign_mfma_kernel(
                 r1 = min2f(r1, dist);
             }
             const float sec = SMALLK ? r2 : min2f(__fmaf_rn(sec_m, th.inv_scale, xn), r2);
-            const float thr = (SMALLK ? 0.f : th.mfma) + 2.f * (th.alpha * sqrtf(sec) + th.beta * sec) + th.gamma;
+            // sec from an MFMA score can be slightly negative (a row on a code vector): the
+            // row is flagged then anyway (r1 >= 0), and no NaN reaches the -fno-honor-nans compare
+            const float sp = fmaxf(sec, 0.f);
+            const float thr = (SMALLK ? 0.f : th.mfma) + 2.f * (th.alpha * sqrtf(sp) + th.beta * sp) + th.gamma;
             A[row] = rk;
             flagged = !(sec - r1 > thr);
             if (flagged) flags[atomicAdd(flag_cnt, 1u)] = (uint32_t)row;
@@ -470,7 +473,7 @@ static size_t small_lds(uint32_t SK, uint32_t C) { return (size_t)C * small_copy
 
 template <int SK, bool FUSE>
 __global__ __launch_bounds__(MF_THREADS) void assign_small_kernel(
-    const uint8_t *__restrict__ codes, uint64_t N, uint32_t K, const float *__restrict__ g_C32,
+    const uint8_t *__restrict__ codes, uint64_t N, uint32_t K, const float *__restrict__ g_E32,
     const uint64_t *__restrict__ g_plut, MfThresholds th, uint64_t rows_per_lane, uint32_t copies,
     uint32_t *__restrict__ A, uint32_t *__restrict__ flags, unsigned *__restrict__ flag_cnt,
     uint64_t *__restrict__ part, uint32_t *__restrict__ part_cnt) {
@@ -528,15 +531,19 @@ __global__ __launch_bounds__(MF_THREADS) void assign_small_kernel(
             w[r][2] = p[2];
         }
     };
-    // Rows r0 + 64 r (r < 4) of this lane, their words in w.
+    // Rows r0 + 64 r (r < 4) of this lane, their words in w.  Expanded scores (the MFMA
+    // search's, in fp32): score = n + sum_d w_d c''_d = 2^t (||x-c||^2 - ||x-mu||^2), with w
+    // the exact centred byte integers -- 12 FMAs per code vector instead of the direct form's
+    // 24 VALU.  Error bound (engine.cpp mfma_setup, e0 / e1): per row from sum_d |w_d|, which
+    // is at most 2 sum_d |u_d - 127| + D (v_sad_u8 of the u = b ^ 0x80 bytes against 127).
     auto process = [&](const uint32_t (&w)[4][3], uint64_t r0) {
-        // four rows at once: each code vector's 12 values are loaded once (scalar) for all
-        // four, and the four distance chains are independent
+        // four rows at once: each code vector's terms are loaded once (scalar) for all four,
+        // and the four score chains are independent
         float x[4][MF_D];
 #pragma unroll
         for (int r = 0; r < 4; r++)
 #pragma unroll
-            for (int d = 0; d < MF_D; d++) x[r][d] = __fmaf_rn(byte_w(w[r][d / 4], d % 4), th.sx, th.mu);
+            for (int d = 0; d < MF_D; d++) x[r][d] = byte_w(w[r][d / 4], d % 4);
         float r1[4], r2[4];
         uint32_t idx[4];
 #pragma unroll
@@ -548,31 +555,31 @@ __global__ __launch_bounds__(MF_THREADS) void assign_small_kernel(
 #pragma unroll 2
         for (int j = 0; j < SK; j++) {
             // wave-uniform: scalar loads into SGPRs (VALU reads them as operands), not LDS
-            // broadcasts, which cost the full 64-lane return bandwidth
-            const float *cj = g_C32 + j * MF_D;
-            float cr[MF_D];
+            // broadcasts, which cost the full 64-lane return bandwidth.  Padding rows (j >= K)
+            // have n = 1e30 and never win.
+            const float *cj = g_E32 + j * 16;
+            float cr[MF_D + 1];
 #pragma unroll
-            for (int d = 0; d < MF_D; d++) cr[d] = cj[d];
+            for (int d = 0; d <= MF_D; d++) cr[d] = cj[d];
 #pragma unroll
             for (int r = 0; r < 4; r++) {
-                float dist = 0.f;
+                float s = cr[MF_D];
 #pragma unroll
-                for (int d = 0; d < MF_D; d++) {
-                    const float e = x[r][d] - cr[d];
-                    dist = __fmaf_rn(e, e, dist);
-                }
-                dist = (uint32_t)j < K ? dist : INFINITY;
-                r2[r] = med3f(r1[r], r2[r], dist);
-                idx[r] = dist < r1[r] ? (uint32_t)j : idx[r];
-                r1[r] = min2f(r1[r], dist);
+                for (int d = 0; d < MF_D; d++) s = __fmaf_rn(x[r][d], cr[d], s);
+                r2[r] = med3f(r1[r], r2[r], s);
+                idx[r] = s < r1[r] ? (uint32_t)j : idx[r];
+                r1[r] = min2f(r1[r], s);
             }
         }
 #pragma unroll
         for (int r = 0; r < 4; r++) {
             const uint64_t row = r0 + 64 * r;
             const uint32_t rk = idx[r];
-            const float thr = 2.f * (th.alpha * sqrtf(r2[r]) + th.beta * r2[r]) + th.gamma;
             const bool valid = row < wend;
+            uint32_t sad = 0;
+#pragma unroll
+            for (int q = 0; q < 3; q++) sad = __builtin_amdgcn_sad_u8(w[r][q] ^ 0x80808080u, 0x7F7F7F7Fu, sad);
+            const float thr = __fmaf_rn((float)(2 * sad + MF_D), th.e1, th.e0);
             const bool flagged = valid && !(r2[r] - r1[r] > thr);
             if (flagged) flags[atomicAdd(flag_cnt, 1u)] = (uint32_t)row;
             if (FUSE && valid) {   // provisional index, as in assign_mfma_kernel
@@ -635,7 +642,8 @@ uint32_t mf_small_k() {
 }
 
 hipError_t launch_assign_mfma(hipStream_t s, int grid, bool fuse, const uint8_t *codes, uint64_t N,
-                              const _Float16 *cb_rows, uint32_t K, const float *C32, const uint64_t *plut,
+                              const _Float16 *cb_rows, const float *E32, uint32_t K, const float *C32,
+                              const uint64_t *plut,
                               const MfThresholds &th, uint32_t *A, uint32_t *flags, unsigned *flag_cnt,
                               uint64_t *part, uint32_t *part_cnt) {
     static const bool no_stage = std::getenv("QVQ_NOSTAGE") != nullptr;   // ablation
@@ -645,7 +653,7 @@ hipError_t launch_assign_mfma(hipStream_t s, int grid, bool fuse, const uint8_t 
                         const uint64_t *, const MfThresholds &, uint32_t *, uint32_t *, unsigned *, uint64_t *,
                         uint32_t *);
     Fn fn;
-    if (K <= mf_small_k() && staged) {   // C32 is padded with zero rows up to 32
+    if (K <= mf_small_k() && E32) {   // E32 is padded up to 32 rows (n = 1e30)
         const uint32_t sk = K <= 2 ? 2 : K <= 4 ? 4 : K <= 8 ? 8 : K <= 16 ? 16 : 32;
         // rows per lane: a multiple of 4 covering N over grid x 16 waves x 64 lanes
         const uint64_t lanes = (uint64_t)grid * MF_WAVES * 64;
@@ -656,10 +664,10 @@ hipError_t launch_assign_mfma(hipStream_t s, int grid, bool fuse, const uint8_t 
     do {                                                                                                          \
         if (fuse)                                                                                                 \
             hipLaunchKernelGGL((assign_small_kernel<V, true>), dim3(grid), dim3(MF_THREADS), slds, s, codes, N, K, \
-                               C32, plut, th, rpl, copies, A, flags, flag_cnt, part, part_cnt);                  \
+                               E32, plut, th, rpl, copies, A, flags, flag_cnt, part, part_cnt);                  \
         else                                                                                                      \
             hipLaunchKernelGGL((assign_small_kernel<V, false>), dim3(grid), dim3(MF_THREADS), slds, s, codes, N,  \
-                               K, C32, plut, th, rpl, copies, A, flags, flag_cnt, part, part_cnt);                \
+                               K, E32, plut, th, rpl, copies, A, flags, flag_cnt, part, part_cnt);                \
     } while (0)
         switch (sk) {
         case 2: QVQ_SMALL(2); break;
@@ -671,6 +679,11 @@ hipError_t launch_assign_mfma(hipStream_t s, int grid, bool fuse, const uint8_t 
 #undef QVQ_SMALL
         return hipGetLastError();
     }
+    // the 32x32x16 form (k_mf32.hip) unless QVQ_MF32=0 (A/B: this file's 16x16x32 form)
+    static const bool mf32 = !(std::getenv("QVQ_MF32") && std::getenv("QVQ_MF32")[0] == '0');
+    if (mf32 && mf32_fits(K, fuse))
+        return launch_assign_mf32(s, grid, fuse, codes, N, cb_rows, K, C32, plut, th, A, flags, flag_cnt, part,
+                                  part_cnt);
     // 4-code-vector units while the pair loop is short (the recompute dominates): up to
     // K = QVQ_U4_MAXK (default 256)
     static const uint32_t u4_max = std::getenv("QVQ_U4_MAXK") ? (uint32_t)std::atoi(std::getenv("QVQ_U4_MAXK")) : 256;

@@ -1,0 +1,362 @@
+// k_mf32.hip -- D = 12 nearest-code-vector search on v_mfma_f32_32x32x16_f16
+// (src/Quantizer.cpp:24-32 semantics; nanoflann's exact answer via the recheck).
+//
+// Same scores as assign_mfma_kernel (k_assign.hip): score = 2^t (||x-c||^2 - ||x-mu||^2) from
+// f16 hi/lo code-vector terms against the exact centred byte integers w of the data row, but
+// on 32 x 32 tiles: one (code tile, data tile) pair is two chained 32x32x16 MFMAs
+//   MFMA 1, k-slots 0..15: A = [hi(0..7) | lo(0..7)]          B = [w(0..7) | w(0..7)]
+//   MFMA 2, k-slots 0..15: A = [hi(8..11) n_hi n_lo 0 0 | lo(8..11) * * * *]
+//                          B = [w(8..11) 1 1 0 0 | w(8..11) 0 0 0 0]
+// (the '*' slots meet zeros in B: any finite f16 does).  Per 1024 scores that is half the
+// MFMA instructions of the 16x16x32 form, so half the vector-issue cycles the matrix pipe
+// holds (MI355X_MICROARCH.md, 'vector-instruction ISSUE cost': 8 per MFMA either shape), and
+// a lane's 16 results all belong to one data row, so its epilogue covers 8-code-vector units
+// (two per tile) or 4-code-vector units (four per tile) without lane traffic.
+//
+// LDS image of the codebook (staged from the 56-byte rows of common.hpp):
+//   P [Kp][32 B]  [hi(0..7) | lo(0..7)], the two 16-byte halves swapped when bit 3 of the
+//                 code vector's index is set: the ds_read_b128 lane groups {0-3,12-15,20-27}
+//                 and {4-11,16-19,28-31} then cover the 64 banks once (MI355X_MICROARCH.md, LDS)
+//   Q [Kp][24 B]  [lo(8..11) | hi(8..11) | n_hi n_lo 0 0]: half h = 0 reads bytes 8..23,
+//                 h = 1 bytes 0..15 (two ds_read_b64: a 24-byte stride is bank-conflict free)
+// The rest (fp32 recompute of the winning unit, rigorous near-tie flag, fused exact centroid
+// sums) follows assign_mfma_kernel.
+#include <cstdlib>
+
+#include "common.hpp"
+#include "mfma_util.hpp"
+
+namespace qvq {
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef uint32_t u32x4v __attribute__((ext_vector_type(4)));
+typedef uint64_t u64x2v __attribute__((ext_vector_type(2)));
+
+constexpr int M32_THREADS = 1024;   // 16 waves, 4 per SIMD, one workgroup per CU
+constexpr int M32_WAVES = M32_THREADS / 64;
+constexpr int M32_ROWS = 64;        // rows per wave and chunk: two 32-row data tiles
+constexpr uint32_t M32_LDS_MAX = 160 * 1024;
+
+struct M32Lds {
+    uint32_t q, c32, sums, cnt, plut, total;
+};
+__host__ __device__ inline M32Lds m32_lds_layout(uint32_t K, bool fuse, bool staged) {
+    const uint32_t Kp = (K + 31) & ~31u;
+    M32Lds L;
+    uint32_t o = Kp * 32;
+    L.q = o;
+    o += Kp * 24;
+    L.c32 = o;
+    if (staged) o += Kp * MF_D * 4;
+    L.sums = o;
+    if (fuse) o += K * MF_D * 8;
+    L.cnt = o;
+    if (fuse) o += ((K + 1) & ~1u) * 4;
+    L.plut = o;
+    if (fuse) o += 256;
+    L.total = o;
+    return L;
+}
+
+// Per-run sums over consecutive lanes with equal key (as in k_assign.hip): returns true on the
+// last lane of each run, which then holds the run's sums.
+__device__ inline bool m32_runs_reduce(uint32_t key, uint32_t (&v)[MF_D + 1], int lane) {
+    const uint32_t prev = wave_prev_u32(key);
+    const uint32_t next = wave_next_u32(key);
+    const bool head = lane == 0 || prev != key;
+    const uint32_t h = wave_scan_max(head ? (uint32_t)lane : 0u);
+    const int src = h == 0 ? 0 : (int)h - 1;
+#pragma unroll
+    for (int i = 0; i <= MF_D; i++) {
+        const uint32_t pre = wave_scan_add(v[i]);
+        const uint32_t before = __shfl(pre, src);
+        v[i] = pre - (h == 0 ? 0u : before);
+    }
+    return lane == 63 || next != key;
+}
+
+// Running best unit / best score / second-best unit minimum of one lane and data tile.
+__device__ inline void m32_track(float m, uint32_t u, float &b1, float &b2, uint32_t &bu) {
+    b2 = med3f(b1, b2, m);
+    bu = m < b1 ? u : bu;
+    b1 = min2f(b1, m);
+}
+
+template <bool FUSE, bool STAGED, int U>
+__global__ __launch_bounds__(M32_THREADS) void assign_mf32_kernel(
+    const uint8_t *__restrict__ codes, uint64_t N, const _Float16 *__restrict__ g_rows, uint32_t K,
+    const float *__restrict__ g_C32, const uint64_t *__restrict__ g_plut, MfThresholds th, uint32_t *__restrict__ A,
+    uint32_t *__restrict__ flags, unsigned *__restrict__ flag_cnt, uint64_t *__restrict__ part,
+    uint32_t *__restrict__ part_cnt) {
+    static_assert(U == 4 || U == 8, "unit of 4 or 8 code vectors");
+    constexpr int NU = 16 / U;   // units per lane and code tile
+    extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+    const uint32_t Kp = (K + 31) & ~31u;
+    const M32Lds L = m32_lds_layout(K, FUSE, STAGED);
+    float *c32s = reinterpret_cast<float *>(lds + L.c32);
+    uint64_t *sums = reinterpret_cast<uint64_t *>(lds + L.sums);   // [d][k]
+    uint32_t *cnt = reinterpret_cast<uint32_t *>(lds + L.cnt);
+    uint8_t *lo8 = lds + L.plut;   // low part of each byte's exact term (high part: b ^ 0x80)
+    const int tid = threadIdx.x;
+    {   // P / Q from the 56-byte rows [hi0..3 lo0..3 | hi4..7 lo4..7 | hi8..11 lo8..11 | n]
+        const uint64_t *src = reinterpret_cast<const uint64_t *>(g_rows);
+        for (uint32_t i = tid; i < Kp; i += M32_THREADS) {
+            const uint64_t *r = src + (size_t)i * 7;
+            const uint64_t w0 = r[0], w1 = r[1], w2 = r[2], w3 = r[3], w4 = r[4], w5 = r[5], w6 = r[6];
+            const bool sw = (i >> 3) & 1;
+            u64x2v *p = reinterpret_cast<u64x2v *>(lds + (size_t)i * 32);
+            const u64x2v hi = {w0, w2}, lo = {w1, w3};
+            p[0] = sw ? lo : hi;
+            p[1] = sw ? hi : lo;
+            uint64_t *q = reinterpret_cast<uint64_t *>(lds + L.q + (size_t)i * 24);
+            q[0] = w5;
+            q[1] = w4;
+            q[2] = w6;
+        }
+    }
+    if (STAGED) {
+        const float4 *src = reinterpret_cast<const float4 *>(g_C32);
+        float4 *dst = reinterpret_cast<float4 *>(c32s);
+        for (uint32_t i = tid; i < Kp * (MF_D / 4); i += M32_THREADS) dst[i] = src[i];
+    }
+    if (FUSE) {
+        for (uint32_t i = tid; i < K * MF_D; i += M32_THREADS) sums[i] = 0;
+        for (uint32_t i = tid; i < K; i += M32_THREADS) cnt[i] = 0;
+        if (tid < 256) lo8[tid] = (uint8_t)(g_plut[tid] & 0xFF);
+        if (blockIdx.x == 0) {   // the correction slabs G (+) and G + 1 (-), after all G others
+            for (uint32_t i = tid; i < 2 * K * MF_D; i += M32_THREADS) part[(uint64_t)gridDim.x * K * MF_D + i] = 0;
+            for (uint32_t i = tid; i < 2 * K; i += M32_THREADS) part_cnt[(uint64_t)gridDim.x * K + i] = 0;
+        }
+    }
+    __syncthreads();
+    const float *C32 = STAGED ? c32s : g_C32;
+
+    const int lane = tid & 63, wave = tid >> 6;
+    const int r32 = lane & 31, h = lane >> 5;
+    const uint32_t ntiles = Kp / 32;
+    const uint64_t nchunks = (N + M32_ROWS - 1) / M32_ROWS;
+    // A fragments of code tile t: P half h of code vector 32t + r32 (halves swapped on bit 3),
+    // Q bytes 8(1-h) .. +15
+    const unsigned char *pa = lds + r32 * 32 + 16 * (h ^ ((r32 >> 3) & 1));
+    const unsigned char *qa = lds + L.q + r32 * 24 + 8 * (1 - h);
+    auto load_a = [&](uint32_t t, half8 &a1, half8 &a2) {
+        const u32x4v v1 = *reinterpret_cast<const u32x4v *>(pa + (size_t)t * (32 * 32));
+        const uint64_t *q = reinterpret_cast<const uint64_t *>(qa + (size_t)t * (32 * 24));
+        const u64x2v v2 = {q[0], q[1]};
+        a1 = __builtin_bit_cast(half8, v1);
+        a2 = __builtin_bit_cast(half8, v2);
+    };
+    // lane (r32, h) loads row r32 of both data tiles (the words of data tile T in q[3T..3T+2]);
+    // its own row base + lane is the one of tile h.  Branch-free: rows past N read row N - 1.
+    auto load_codes = [&](uint64_t chunk, uint32_t (&q)[6]) {
+#pragma unroll
+        for (int T = 0; T < 2; T++) {
+            uint64_t row = chunk * M32_ROWS + 32 * T + r32;
+            row = row < N ? row : N - 1;
+            const uint32_t *p = reinterpret_cast<const uint32_t *>(codes + row * MF_D);
+            q[3 * T] = p[0];
+            q[3 * T + 1] = p[1];
+            q[3 * T + 2] = p[2];
+        }
+    };
+    const uint32_t ones = h ? 0u : 0x3C003C00u;   // f16 (1, 1) on the n_hi n_lo slots of half 0
+
+    uint64_t chunk = (uint64_t)blockIdx.x * M32_WAVES + wave;
+    const uint64_t stride = (uint64_t)gridDim.x * M32_WAVES;
+    uint32_t qn[6];
+    load_codes(chunk, qn);
+    for (; chunk < nchunks; chunk += stride) {
+        const uint64_t base = chunk * M32_ROWS;
+        uint32_t q[6];
+#pragma unroll
+        for (int i = 0; i < 6; i++) q[i] = qn[i];
+        load_codes(chunk + stride, qn);   // prefetch the next chunk under this one's search
+        const uint32_t own[3] = {h ? q[3] : q[0], h ? q[4] : q[1], h ? q[5] : q[2]};
+        half8 b1[2], b2[2];
+#pragma unroll
+        for (int T = 0; T < 2; T++) {
+            uint32_t w01, w23, w45, w67, w89, wab;
+            byte_quad_w(q[3 * T], w01, w23);
+            byte_quad_w(q[3 * T + 1], w45, w67);
+            byte_quad_w(q[3 * T + 2], w89, wab);
+            const u32x4v v1 = {w01, w23, w45, w67};
+            const u32x4v v2 = {w89, wab, ones, 0u};
+            b1[T] = __builtin_bit_cast(half8, v1);
+            b2[T] = __builtin_bit_cast(half8, v2);
+        }
+        float s1[2], s2[2];
+        uint32_t su[2];
+#pragma unroll
+        for (int T = 0; T < 2; T++) {
+            s1[T] = INFINITY;
+            s2[T] = INFINITY;
+            su[T] = 0;
+        }
+        half8 a1, a2;
+        load_a(0, a1, a2);
+        const f32x16 zero16 = {};
+        for (uint32_t t = 0; t < ntiles; t++) {
+            f32x16 c[2];
+            c[0] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a1, b1[0], zero16, 0, 0, 0);
+            c[1] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a1, b1[1], zero16, 0, 0, 0);
+            c[0] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a2, b2[0], c[0], 0, 0, 0);
+            c[1] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a2, b2[1], c[1], 0, 0, 0);
+            load_a(t + 1 < ntiles ? t + 1 : t, a1, a2);   // the next tile's fragments under these
+#pragma unroll
+            for (int T = 0; T < 2; T++) {
+#pragma unroll
+                for (int qq = 0; qq < NU; qq++) {
+                    const int o = qq * U;
+                    float m;
+                    if constexpr (U == 8)
+                        m = min2f(min3f(min3f(min3f(c[T][o], c[T][o + 1], c[T][o + 2]), c[T][o + 3], c[T][o + 4]),
+                                        c[T][o + 5], c[T][o + 6]),
+                                  c[T][o + 7]);
+                    else
+                        m = min2f(min3f(c[T][o], c[T][o + 1], c[T][o + 2]), c[T][o + 3]);
+                    m32_track(m, t * NU + qq, s1[T], s2[T], su[T]);
+                }
+            }
+        }
+        // Merge the two halves of every data row: swap32(x = tile 0, y = tile 1) leaves lanes
+        // < 32 with tile 0 row r32 (lo: own half, hi: half 1 of lane + 32) and lanes >= 32
+        // with tile 1 row r32 (lo: half 0 of lane - 32, hi: own half) -- the own row base +
+        // lane in both.  Units carry their half: unit * 2 + h.
+        float sec_m;
+        uint32_t unit;
+        {
+            const auto p1 = swap32_f32(s1[0], s1[1]);
+            const auto p2 = swap32_f32(s2[0], s2[1]);
+            const auto pu = swap32_u32(su[0] * 2 + h, su[1] * 2 + h);
+            float m1 = p1.lo;
+            sec_m = p2.lo;
+            unit = pu.lo;
+            if (p1.hi < m1 || (p1.hi == m1 && pu.hi < unit)) {
+                sec_m = min2f(p2.hi, m1);
+                m1 = p1.hi;
+                unit = pu.hi;
+            } else {
+                sec_m = min2f(sec_m, p1.hi);
+            }
+        }
+        // Recompute the winning unit's code vectors in the direct fp32 form (x - c)^2.
+        const uint64_t row = base + lane;
+        const bool valid = row < N;
+        uint32_t rk = 0;
+        if (valid) {
+            float x[MF_D];
+            float xn = 0.f;   // ||x - mu||^2
+#pragma unroll
+            for (int d = 0; d < MF_D; d++) {
+                const float e = byte_w(own[d / 4], d % 4) * th.sx;
+                xn = __fmaf_rn(e, e, xn);
+                x[d] = e + th.mu;
+            }
+            // unit = ((tile * NU + q) * 2 + hh): 8-unit q covers rows 16q + 4hh + {0..3, 8..11}
+            // of the tile, 4-unit q rows 8q + 4hh + {0..3}
+            const uint32_t hh = unit & 1, qq = (unit >> 1) % NU, tile = (unit >> 1) / NU;
+            const uint32_t cb = tile * 32 + (U == 8 ? 16 * qq : 8 * qq) + 4 * hh;
+            float r1 = INFINITY, r2 = INFINITY;
+#pragma unroll
+            for (int j = 0; j < U; j++) {
+                const uint32_t cv = cb + (j & 3) + 8 * (j >> 2);
+                const float4 *c4 = reinterpret_cast<const float4 *>(C32 + (size_t)cv * MF_D);
+                float dist = 0.f;
+#pragma unroll
+                for (int k4 = 0; k4 < 3; k4++) {
+                    const float4 cq = c4[k4];
+                    float e;
+                    e = x[4 * k4 + 0] - cq.x; dist = __fmaf_rn(e, e, dist);
+                    e = x[4 * k4 + 1] - cq.y; dist = __fmaf_rn(e, e, dist);
+                    e = x[4 * k4 + 2] - cq.z; dist = __fmaf_rn(e, e, dist);
+                    e = x[4 * k4 + 3] - cq.w; dist = __fmaf_rn(e, e, dist);
+                }
+                dist = cv < K ? dist : INFINITY;   // padding code vectors never win
+                r2 = med3f(r1, r2, dist);
+                rk = dist < r1 ? cv : rk;
+                r1 = min2f(r1, dist);
+            }
+            const float sec = min2f(__fmaf_rn(sec_m, th.inv_scale, xn), r2);
+            // sec from an MFMA score can be slightly negative (a row on a code vector): the
+            // row is flagged then anyway (r1 >= 0), and no NaN reaches the -fno-honor-nans compare
+            const float sp = fmaxf(sec, 0.f);
+            const float thr = th.mfma + 2.f * (th.alpha * sqrtf(sp) + th.beta * sp) + th.gamma;
+            A[row] = rk;
+            if (!(sec - r1 > thr)) flags[atomicAdd(flag_cnt, 1u)] = (uint32_t)row;
+        }
+        if (FUSE) {
+            // every row at its provisional index; the recheck / kd-tree move re-assigned ones
+            if (K <= th.runs_max_k) {
+                uint32_t v[MF_D + 1];
+#pragma unroll
+                for (int d = 0; d < MF_D; d++) {
+                    const uint32_t b = (own[d / 4] >> (8 * (d % 4))) & 0xFF;
+                    v[d] = valid ? ((b ^ 0x80u) << 16 | lo8[b]) : 0u;   // <= 64 rows: no carry
+                }
+                v[MF_D] = valid ? 1u : 0u;
+                const bool tail = m32_runs_reduce(valid ? rk : 0xFFFFFFFFu, v, lane);
+                if (tail && valid) {
+#pragma unroll
+                    for (int d = 0; d < MF_D; d++)
+                        atomicAdd((unsigned long long *)&sums[(uint32_t)d * K + rk],
+                                  (unsigned long long)((((uint64_t)(v[d] >> 16)) << 32) | (v[d] & 0xFFFF)));
+                    atomicAdd(&cnt[rk], v[MF_D]);
+                }
+            } else if (valid) {
+#pragma unroll
+                for (int d = 0; d < MF_D; d++) {
+                    const uint32_t b = (own[d / 4] >> (8 * (d % 4))) & 0xFF;
+                    atomicAdd((unsigned long long *)&sums[(uint32_t)d * K + rk],
+                              (unsigned long long)((uint64_t)(b ^ 0x80u) << 32 | lo8[b]));
+                }
+                atomicAdd(&cnt[rk], 1u);
+            }
+        }
+    }
+    if (FUSE) {
+        __syncthreads();
+        uint64_t *pdst = part + (uint64_t)blockIdx.x * K * MF_D;   // slab layout [d][k]
+        for (uint32_t i = tid; i < K * MF_D; i += M32_THREADS) pdst[i] = sums[i];
+        uint32_t *cdst = part_cnt + (uint64_t)blockIdx.x * K;
+        for (uint32_t i = tid; i < K; i += M32_THREADS) cdst[i] = cnt[i];
+    }
+}
+
+template <bool F, bool S, int U>
+static void launch_mf32_variant(hipStream_t s, int grid, size_t lds, const uint8_t *codes, uint64_t N,
+                                const _Float16 *cb_rows, uint32_t K, const float *C32, const uint64_t *plut,
+                                const MfThresholds &th, uint32_t *A, uint32_t *flags, unsigned *flag_cnt,
+                                uint64_t *part, uint32_t *part_cnt) {
+    hipLaunchKernelGGL((assign_mf32_kernel<F, S, U>), dim3(grid), dim3(M32_THREADS), lds, s, codes, N, cb_rows, K,
+                       C32, plut, th, A, flags, flag_cnt, part, part_cnt);
+}
+
+bool mf32_fits(uint32_t K, bool fuse) { return m32_lds_layout(K, fuse, false).total <= M32_LDS_MAX; }
+
+hipError_t launch_assign_mf32(hipStream_t s, int grid, bool fuse, const uint8_t *codes, uint64_t N,
+                              const _Float16 *cb_rows, uint32_t K, const float *C32, const uint64_t *plut,
+                              const MfThresholds &th, uint32_t *A, uint32_t *flags, unsigned *flag_cnt,
+                              uint64_t *part, uint32_t *part_cnt) {
+    if (!mf32_fits(K, fuse)) return hipErrorInvalidValue;
+    const bool staged = m32_lds_layout(K, fuse, true).total <= M32_LDS_MAX;
+    const size_t lds = m32_lds_layout(K, fuse, staged).total;
+    // 4-code-vector units while the tile loop is short (the recompute dominates)
+    static const uint32_t u4_max =
+        std::getenv("QVQ_U4_MAXK") ? (uint32_t)std::atoi(std::getenv("QVQ_U4_MAXK")) : 256;
+    const bool u4 = K <= u4_max;
+    using Fn = void (*)(hipStream_t, int, size_t, const uint8_t *, uint64_t, const _Float16 *, uint32_t, const float *,
+                        const uint64_t *, const MfThresholds &, uint32_t *, uint32_t *, unsigned *, uint64_t *,
+                        uint32_t *);
+    Fn fn;
+    if (fuse) {
+        if (u4) fn = staged ? launch_mf32_variant<true, true, 4> : launch_mf32_variant<true, false, 4>;
+        else fn = staged ? launch_mf32_variant<true, true, 8> : launch_mf32_variant<true, false, 8>;
+    } else {
+        if (u4) fn = staged ? launch_mf32_variant<false, true, 4> : launch_mf32_variant<false, false, 4>;
+        else fn = staged ? launch_mf32_variant<false, true, 8> : launch_mf32_variant<false, false, 8>;
+    }
+    fn(s, grid, lds, codes, N, cb_rows, K, C32, plut, th, A, flags, flag_cnt, part, part_cnt);
+    return hipGetLastError();
+}
+
+}  // namespace qvq

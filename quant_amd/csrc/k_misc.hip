@@ -525,6 +525,7 @@ struct FinArgs {
     double mu, sx, scale_t;
     float *C32;
     _Float16 *rows;
+    float *E32;   // D = 12: expanded fp32 terms [c''(12) | n | 0 0 0] (small-K scan)
     double *host_cb;
     bool dist;
     uint64_t *zero_after;   // cleared by the last block once every block has read sums (mean)
@@ -570,9 +571,13 @@ __device__ inline double finalize_item(const FinArgs &a, uint32_t j, uint32_t d,
                 const _Float16 l = (_Float16)(float)(n - (double)(float)h);
                 for (uint32_t i = 2 * LO + d; i < RF; i += L)
                     row[i] = i == 2 * LO ? h : (i == 2 * LO + 1 ? l : (_Float16)0.f);
+                if (a.E32 && d < 16)   // L = 16 lanes for D = 12
+                    a.E32[(uint64_t)j * 16 + d] =
+                        d < D ? (float)(-2.0 * a.sx * cp * a.scale_t) : (d == D ? (float)n : 0.f);
             }
         } else if (j < a.Kpad_next) {
             if (d < Dp) a.C32[(uint64_t)j * Dp + d] = 0.f;
+            if (a.E32 && d < 16) a.E32[(uint64_t)j * 16 + d] = d == D ? 1e30f : 0.f;   // never wins
             if (a.rows) {
                 const uint32_t RF = cb_row_f16(D, Dp), LO = cb_lo_off(D, Dp);
                 _Float16 *row = a.rows + (uint64_t)j * RF;
@@ -652,7 +657,7 @@ __global__ __launch_bounds__(256) void finalize_prep_kernel(FinArgs a, double *_
 
 static FinArgs fin_args(const uint64_t *sums, uint32_t K, uint32_t D, uint32_t Dp, int64_t R, int64_t bias,
                         int scale, double *C_cent, bool split, double *C64n, uint32_t Kpad_next, double mu, double sx,
-                        int t, float *C32, _Float16 *cb_rows, double *host_cb, bool dist) {
+                        int t, float *C32, _Float16 *cb_rows, float *E32, double *host_cb, bool dist) {
     FinArgs a;
     a.sums = sums;
     a.K = K;
@@ -670,6 +675,7 @@ static FinArgs fin_args(const uint64_t *sums, uint32_t K, uint32_t D, uint32_t D
     a.scale_t = std::ldexp(1.0, t);
     a.C32 = C32;
     a.rows = cb_rows;
+    a.E32 = D == MF_D ? E32 : nullptr;
     a.host_cb = host_cb;
     a.dist = dist;
     a.zero_after = nullptr;
@@ -679,16 +685,16 @@ static FinArgs fin_args(const uint64_t *sums, uint32_t K, uint32_t D, uint32_t D
 
 hipError_t launch_finalize_prep(hipStream_t s, const uint64_t *sums, uint32_t K, uint32_t D, uint32_t Dp, int64_t R,
                                 int64_t bias, int scale, double *C_cent, bool split, double *C64n, uint32_t Kpad_next,
-                                double mu, double sx, int t, float *C32, _Float16 *cb_rows, double *host_cb,
-                                double *dist_part, unsigned *done, double *dist_out, uint64_t *ready, uint64_t seq,
-                                bool zero_sums) {
+                                double mu, double sx, int t, float *C32, _Float16 *cb_rows, float *E32,
+                                double *host_cb, double *dist_part, unsigned *done, double *dist_out, uint64_t *ready,
+                                uint64_t seq, bool zero_sums) {
     if (D == 0 || D > 64) return hipErrorInvalidValue;
     if (zero_sums && !done) return hipErrorInvalidValue;   // the clearing is the last block's
     const uint32_t L = D <= 16 ? 16 : (D <= 32 ? 32 : 64);
     const uint32_t n = split ? std::max(2 * K, Kpad_next) : K;
     const uint32_t grid = std::min<uint32_t>((n + 256 / L - 1) / (256 / L), 512);   // <= dist_part capacity
     FinArgs a = fin_args(sums, K, D, Dp, R, bias, scale, C_cent, split, C64n, Kpad_next, mu, sx, t, C32, cb_rows,
-                         host_cb, dist_out != nullptr);
+                         E32, host_cb, dist_out != nullptr);
     if (zero_sums) {
         a.zero_after = const_cast<uint64_t *>(sums);
         a.n_zero = 2 * K * D + K;
@@ -702,14 +708,14 @@ hipError_t launch_finalize_prep(hipStream_t s, const uint64_t *sums, uint32_t K,
 hipError_t launch_finalize(hipStream_t s, const uint64_t *sums, uint32_t K, uint32_t D, int64_t R, int64_t bias,
                            int scale, double *C_cent) {
     return launch_finalize_prep(s, sums, K, D, (D + 3) & ~3u, R, bias, scale, C_cent, false, nullptr, 0, 0, 0, 0,
-                                nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, 0, false);
+                                nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, 0, false);
 }
 
 // Search tables from an fp64 codebook: fp32 [Kpad][Dp] (VALU path and the MFMA recompute)
 // and the f16 MFMA rows (D = 12 or wide layout, common.hpp).  Code vectors K..Kpad-1 are padding
 // that never wins.
 __device__ inline void prep_row(const double *v, uint32_t D, uint32_t Dp, double mu, double sx, double scale_t,
-                                float *__restrict__ c32, _Float16 *__restrict__ r) {
+                                float *__restrict__ c32, _Float16 *__restrict__ r, float *__restrict__ e32) {
     const uint32_t RF = cb_row_f16(D, Dp), LO = cb_lo_off(D, Dp);
     double n = 0;
     for (uint32_t i = 0; i < RF; i++) r[i] = (_Float16)0.f;
@@ -723,17 +729,23 @@ __device__ inline void prep_row(const double *v, uint32_t D, uint32_t Dp, double
             const _Float16 h = (_Float16)(float)c2;
             r[cb_hi_slot(D, Dp, d)] = h;
             r[cb_lo_slot(D, Dp, d)] = (_Float16)(float)(c2 - (double)(float)h);
+            if (e32) e32[d] = (float)c2;
         }
     }
     n *= scale_t;
+    if (e32)
+        for (uint32_t d = D; d < 16; d++) e32[d] = d == D ? (float)n : 0.f;
     const _Float16 h = (_Float16)(float)n;
     r[2 * LO] = h;
     r[2 * LO + 1] = (_Float16)(float)(n - (double)(float)h);
 }
 
-__device__ inline void prep_pad_row(uint32_t D, uint32_t Dp, float *__restrict__ c32, _Float16 *__restrict__ r) {
+__device__ inline void prep_pad_row(uint32_t D, uint32_t Dp, float *__restrict__ c32, _Float16 *__restrict__ r,
+                                    float *__restrict__ e32) {
     const uint32_t RF = cb_row_f16(D, Dp), LO = cb_lo_off(D, Dp);
     for (uint32_t d = 0; d < Dp; d++) c32[d] = 0.f;
+    if (e32)
+        for (uint32_t d = 0; d < 16; d++) e32[d] = d == D ? 1e30f : 0.f;   // never wins
     for (uint32_t i = 0; i < RF; i++) r[i] = (_Float16)0.f;
     r[2 * LO] = (_Float16)MF_PAD_SCORE;
     r[2 * LO + 1] = (_Float16)MF_PAD_SCORE;
@@ -741,23 +753,24 @@ __device__ inline void prep_pad_row(uint32_t D, uint32_t Dp, float *__restrict__
 
 __global__ void prep_kernel(const double *__restrict__ C64, uint32_t K, uint32_t Kpad, uint32_t D, uint32_t Dp,
                             double mu, double sx, double scale_t, float *__restrict__ C32,
-                            _Float16 *__restrict__ rows) {
+                            _Float16 *__restrict__ rows, float *__restrict__ E32) {
     const uint32_t RF = cb_row_f16(D, Dp);
     for (uint32_t k = blockIdx.x * blockDim.x + threadIdx.x; k < Kpad; k += gridDim.x * blockDim.x) {
+        float *e32 = E32 ? E32 + (uint64_t)k * 16 : nullptr;
         if (k >= K) {
-            prep_pad_row(D, Dp, C32 + (uint64_t)k * Dp, rows + (uint64_t)k * RF);
+            prep_pad_row(D, Dp, C32 + (uint64_t)k * Dp, rows + (uint64_t)k * RF, e32);
             continue;
         }
         double v[64];
         for (uint32_t d = 0; d < D; d++) v[d] = C64[(uint64_t)k * D + d];
-        prep_row(v, D, Dp, mu, sx, scale_t, C32 + (uint64_t)k * Dp, rows + (uint64_t)k * RF);
+        prep_row(v, D, Dp, mu, sx, scale_t, C32 + (uint64_t)k * Dp, rows + (uint64_t)k * RF, e32);
     }
 }
 
 hipError_t launch_prep(hipStream_t s, const double *C64, uint32_t K, uint32_t Kpad, uint32_t D, uint32_t Dp,
-                       double mu, double sx, int t, float *C32, _Float16 *cb_rows) {
+                       double mu, double sx, int t, float *C32, _Float16 *cb_rows, float *E32) {
     hipLaunchKernelGGL(prep_kernel, dim3((Kpad + 255) / 256), dim3(256), 0, s, C64, K, Kpad, D, Dp, mu, sx,
-                       std::ldexp(1.0, t), C32, cb_rows);
+                       std::ldexp(1.0, t), C32, cb_rows, D == MF_D ? E32 : nullptr);
     return hipGetLastError();
 }
 

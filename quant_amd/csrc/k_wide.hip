@@ -306,7 +306,10 @@ __global__ __launch_bounds__(WD_THREADS) void assign_wide_kernel(
                 rk = dist < r1 ? cv : rk;
                 r1 = min2f(r1, dist);
             }
-            const float rest = __fmaf_rn(sec_m, th.inv_scale, xn);   // best unit not recomputed
+            // best unit not recomputed; from an MFMA score it can be slightly negative (a row on a
+            // code vector): clamped, so no NaN reaches the -fno-honor-nans compares (r1 >= 0
+            // flags such a row anyway)
+            const float rest = fmaxf(__fmaf_rn(sec_m, th.inv_scale, xn), 0.f);
             bool flag;
             if (TWO) {   // recomputed runner-up (direct fp32 error), rest (plus the MFMA error)
                 const float thr2 = 2.f * (th.alpha * sqrtf(r2) + th.beta * r2) + th.gamma;
