@@ -10,26 +10,30 @@
 
 namespace qvq {
 
+
 double ref_l2(const double *a, const double *b, int dim) { return ref_l2_hd(a, b, dim); }
 
 RefKDTree::RefKDTree(const double *pts, size_t K, int dim) : pts_(pts), dim_(dim), K_(K) {
     static thread_local std::vector<double> cols;   // reused: a fresh 1.5 MB buffer per level page-faults
     if (cols.size() < K * (size_t)dim) cols.resize(K * (size_t)dim);
-    double *const cbuf = cols.data();   // (thread_local: the helper threads must not name `cols`)
+    double *const cbuf = cols.data();
     cols_ = cbuf;
     vind_.resize(K);
     for (size_t i = 0; i < K; i++) vind_[i] = i;
     root_bbox_.resize(dim);
-    // column-major copy and root box (threads measured slower here: ~30 us per spawn)
-    {
+    // column-major copy and root box, 64 points at a time (their rows stay in L1 while
+    // every column takes its 64 values)
+    for (int d = 0; d < dim; d++) root_bbox_[d].low = root_bbox_[d].high = pts[d];
+    for (size_t k0 = 0; k0 < K; k0 += 64) {
+        const size_t k1 = std::min(K, k0 + 64);
         for (int d = 0; d < dim; d++) {
             double *col = cbuf + (size_t)d * K;
-            double lo = pts[d], hi = lo;
-            for (size_t k = 0; k < K; k++) {
+            double lo = root_bbox_[d].low, hi = root_bbox_[d].high;
+            for (size_t k = k0; k < k1; k++) {
                 const double v = pts[k * (size_t)dim + d];
                 col[k] = v;
-                if (v < lo) lo = v;
-                if (v > hi) hi = v;
+                lo = v < lo ? v : lo;
+                hi = v > hi ? v : hi;
             }
             root_bbox_[d].low = lo;
             root_bbox_[d].high = hi;
@@ -45,13 +49,17 @@ RefKDTree::RefKDTree(const double *pts, size_t K, int dim) : pts_(pts), dim_(dim
     cols_ = nullptr;
 }
 
+// Branch-free minima and maxima: the comparisons are data-dependent, and mispredicted
+// branches dominated the build (min / max are exact, so any form gives the same values).
 void RefKDTree::min_max(const size_t *ind, size_t count, int e, double &mn, double &mx) const {
-    mn = mx = pt(ind[0], e);
+    double a = pt(ind[0], e), b = a;
     for (size_t i = 1; i < count; i++) {
         const double v = pt(ind[i], e);
-        if (v < mn) mn = v;
-        if (v > mx) mx = v;
+        a = v < a ? v : a;
+        b = v > b ? v : b;
     }
+    mn = a;
+    mx = b;
 }
 
 void RefKDTree::plane_split(size_t *ind, size_t count, int cutfeat, double cutval, size_t &lim1,
@@ -92,7 +100,27 @@ void RefKDTree::middle_split(size_t *ind, size_t count, size_t &index, int &cutf
     for (int i = 0; i < dim_; i++)
         if (bbox[i].high - bbox[i].low > (1 - EPS) * max_span) q[nq++] = i;
     double qmn[64], qmx[64];
-    for (int j = 0; j < nq; j++) min_max(ind, count, q[j], qmn[j], qmx[j]);
+    if (nq * 4 >= dim_ && dim_ >= 8) {
+        // most dimensions are candidates (real codebooks: every dimension not yet cut on the
+        // path keeps the root's span): one row-major pass over the node's points gives all
+        // of them -- each point's contiguous row once, instead of nq column gathers
+        double mn[64], mx[64];
+        const double *p0 = pts_ + ind[0] * (size_t)dim_;
+        for (int d = 0; d < dim_; d++) mn[d] = mx[d] = p0[d];
+        for (size_t i = 1; i < count; i++) {
+            const double *p = pts_ + ind[i] * (size_t)dim_;
+            for (int d = 0; d < dim_; d++) {
+                mn[d] = p[d] < mn[d] ? p[d] : mn[d];
+                mx[d] = p[d] > mx[d] ? p[d] : mx[d];
+            }
+        }
+        for (int j = 0; j < nq; j++) {
+            qmn[j] = mn[q[j]];
+            qmx[j] = mx[q[j]];
+        }
+    } else {
+        for (int j = 0; j < nq; j++) min_max(ind, count, q[j], qmn[j], qmx[j]);
+    }
     double max_spread = -1, mn = 0, mx = 0;
     cutfeat = 0;
     bool have = false;
@@ -126,13 +154,20 @@ int RefKDTree::divide(size_t left, size_t right, std::vector<Box> &bbox, int lev
         n.left = left;
         n.right = right;
         n.child1 = n.child2 = -1;
-        for (int d = 0; d < dim_; d++) bbox[d].low = bbox[d].high = ptr(vind_[left], d);
-        for (size_t k = left + 1; k < right; k++)   // row-major: one point's coordinates are contiguous
+        double mn[64], mx[64];
+        const double *p0 = pts_ + vind_[left] * (size_t)dim_;
+        for (int d = 0; d < dim_; d++) mn[d] = mx[d] = p0[d];
+        for (size_t k = left + 1; k < right; k++) {   // row-major: one point's coordinates are contiguous
+            const double *p = pts_ + vind_[k] * (size_t)dim_;
             for (int d = 0; d < dim_; d++) {
-                const double v = ptr(vind_[k], d);
-                if (bbox[d].low > v) bbox[d].low = v;
-                if (bbox[d].high < v) bbox[d].high = v;
+                mn[d] = p[d] < mn[d] ? p[d] : mn[d];
+                mx[d] = p[d] > mx[d] ? p[d] : mx[d];
             }
+        }
+        for (int d = 0; d < dim_; d++) {
+            bbox[d].low = mn[d];
+            bbox[d].high = mx[d];
+        }
         return me;
     }
     size_t idx;

@@ -86,3 +86,4 @@ def test_bounded_wait_policy(scenario, status, max_s):
     assert el <= max_s
     if scenario in (1, 2):
         assert el >= 0.25
+
