@@ -191,7 +191,11 @@ hipError_t launch_reduce(hipStream_t s, const uint64_t *part, const uint32_t *pa
 hipError_t launch_copy_out(hipStream_t s, const void *src0, void *dst0, uint64_t bytes0, const void *src1, void *dst1,
                            uint64_t bytes1, const void *src2, void *dst2, uint64_t bytes2, uint64_t *flag = nullptr,
                            uint64_t seq = 0, unsigned *done = nullptr);
-// Mean sums (K = 1) into sums[0..2D]; also clears zero[0..n_zero) and sets dist[0..1] = x0, x1.
+// Mean sums (K = 1): block b adds into copy b mod MEAN_COPIES of [hi D][lo D][n] (stride
+// 2D + 1; n in copy 0 only), so the blocks' closing atomics spread over MEAN_COPIES addresses
+// per component; the K = 1 finalize adds the copies.  Also clears zero[0..n_zero) and sets
+// dist[0..1] = x0, x1.
+constexpr uint32_t MEAN_COPIES = 8;
 hipError_t launch_mean_sums(hipStream_t s, uint32_t Dp, const uint8_t *codes, uint64_t N, uint32_t D,
                             const uint64_t *plut, uint64_t *sums, unsigned *zero, uint32_t n_zero, double *dist,
                             double x0, double x1);
@@ -205,7 +209,7 @@ hipError_t launch_finalize_prep(hipStream_t s, const uint64_t *sums, uint32_t K,
                                 int64_t bias, int scale, double *C_cent, bool split, double *C64n, uint32_t Kpad_next,
                                 double mu, double sx, int t, float *C32, _Float16 *cb_rows, float *E32,
                                 double *host_cb, double *dist_part, unsigned *done, double *dist_out, uint64_t *ready, uint64_t seq,
-                                bool zero_sums);
+                                bool zero_sums, uint32_t ncopy = 1);
 hipError_t launch_finalize(hipStream_t s, const uint64_t *sums, uint32_t K, uint32_t D, int64_t R, int64_t bias,
                            int scale, double *C_cent);
 // f16 MFMA tables (D = 12) and fp32 VALU table from an fp64 codebook of K code vectors.

@@ -103,7 +103,7 @@ struct qvq_ctx {
     uint64_t *d_part = nullptr, *d_sums = nullptr;
     uint32_t *d_part_cnt = nullptr;
     double *d_dist_part = nullptr;
-    uint64_t *d_mean = nullptr;   // mean sums [hi D][lo D][n]: zero between quantizes (the finalize clears it)
+    uint64_t *d_mean = nullptr;   // MEAN_COPIES x mean sums [hi D][lo D][n]: zero between quantizes (the finalize clears them)
     uint64_t out_seq = 0;         // quantizes whose results copy_out has published
     uint32_t *d_scatter = nullptr;
     uint64_t scatter_bytes = 0;
@@ -349,10 +349,11 @@ void valu_coeffs(const qvq_ctx *ctx, float &alpha, float &beta, float &gamma) {
     gamma = (float)(2.0 * 4.01 * u * u * L * L + 1e-30);
 }
 
-qvq_status all_reduce_sums(qvq_ctx *ctx, uint32_t K, uint64_t *sums = nullptr) {
+qvq_status all_reduce_sums(qvq_ctx *ctx, uint32_t K, uint64_t *sums = nullptr, uint32_t copies = 1) {
     if (!sums) sums = ctx->d_sums;
     if (ctx->comm)
-        NCCLCHK(ncclAllReduce(sums, sums, 2 * (uint64_t)K * ctx->D + K, ncclUint64, ncclSum, ctx->comm, ctx->stream));
+        NCCLCHK(ncclAllReduce(sums, sums, copies * (2 * (uint64_t)K * ctx->D + K), ncclUint64, ncclSum, ctx->comm,
+                              ctx->stream));
     return QVQ_OK;
 }
 
@@ -651,8 +652,8 @@ QVQ_API qvq_status qvq_create(int hip_device, qvq_ctx **out) {
     if ((e = hipMalloc(&ctx->d_decode_stat, 16)) != hipSuccess) return bail(e, "hipMalloc");
     if ((e = hipHostMalloc(&ctx->h_decode_stat, 16, hipHostMallocDefault)) != hipSuccess) return bail(e, "hipHostMalloc");
     if ((e = hipMalloc(&ctx->d_dist_part, 8192 * 8)) != hipSuccess) return bail(e, "hipMalloc");
-    if ((e = hipMalloc(&ctx->d_mean, (2 * 64 + 1) * 8)) != hipSuccess) return bail(e, "hipMalloc");
-    if ((e = hipMemset(ctx->d_mean, 0, (2 * 64 + 1) * 8)) != hipSuccess) return bail(e, "hipMemset");
+    if ((e = hipMalloc(&ctx->d_mean, MEAN_COPIES * (2 * 64 + 1) * 8)) != hipSuccess) return bail(e, "hipMalloc");
+    if ((e = hipMemset(ctx->d_mean, 0, MEAN_COPIES * (2 * 64 + 1) * 8)) != hipSuccess) return bail(e, "hipMemset");
     for (int l = 0; l < 32; l++)
         for (int j = 0; j < 4; j++)
             if ((e = hipEventCreate(&ctx->ev[l][j])) != hipSuccess) return bail(e, "hipEventCreate");
@@ -819,8 +820,8 @@ QVQ_API qvq_status qvq_lbg(qvq_ctx *ctx, uint32_t bits, double eps, double *code
     HIPCHK(launch_mean_sums(ctx->stream, ctx->Dp, ctx->d_codes, ctx->N, ctx->D, ctx->d_plut, ctx->d_mean,
                             ctx->d_counters, 2 * 33 + 2, d_dist, ctx->xsq, (double)ctx->N));
     if (ctx->comm) NCCLCHK(ncclAllReduce(d_dist, d_dist, 2, ncclDouble, ncclSum, ctx->comm, ctx->stream));
-    if ((st = all_reduce_sums(ctx, 1, ctx->d_mean)) != QVQ_OK) {
-        (void)hipMemsetAsync(ctx->d_mean, 0, (2 * 64 + 1) * 8, ctx->stream);   // keep it clear for the next call
+    if ((st = all_reduce_sums(ctx, 1, ctx->d_mean, MEAN_COPIES)) != QVQ_OK) {
+        (void)hipMemsetAsync(ctx->d_mean, 0, MEAN_COPIES * (2 * 64 + 1) * 8, ctx->stream);   // keep it clear for the next call
         return st;
     }
     unsigned *dist_done = ctx->d_counters + 2 * 33;
@@ -834,7 +835,7 @@ QVQ_API qvq_status qvq_lbg(qvq_ctx *ctx, uint32_t bits, double eps, double *code
                                     ctx->d_C32, ctx->d_rows, ctx->d_E32, split ? ctx->dh_cb : nullptr, d_dist + 8,
                                     dist_done,
                                     split ? nullptr : d_dist + 2, split ? ctx->dh_ready : nullptr, ctx->seq,
-                                    K == 1);
+                                    K == 1, K == 1 ? MEAN_COPIES : 1);
     };
     HIPCHK(finalize(1, bits > 0));
     // with bits >= 1 the first search writes every row's index

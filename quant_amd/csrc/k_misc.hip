@@ -337,19 +337,26 @@ hipError_t launch_reduce(hipStream_t s, const uint64_t *part, const uint32_t *pa
 // distortion inputs, zeroed counters), which saves two host calls per quantize.
 constexpr int MEAN_THREADS = 1024;
 constexpr uint64_t MEAN_ROWS_PER_THREAD = 256;
+constexpr int MEAN_U = 4;   // groups of 4 rows in flight per thread
 struct MeanInit {
     unsigned *zero;     // n_zero counters to clear
     uint32_t n_zero;
     double *dist;       // dist[0..1] = x0, x1
     double x0, x1;
 };
+// Per thread: the high parts u = b ^ 0x80 of the four components of a word are added two at a
+// time as 16-bit fields (u of components 4q, 4q+2 in ue[q], of 4q+1, 4q+3 in uo[q]: three VALU
+// per word), the low parts (<= 128 each) from a 256-BYTE LDS table (ds_read_u8: at most two
+// lanes' dwords per bank, where a dword table conflicts up to 8-way), also as 16-bit fields.
+// <= MEAN_ROWS_PER_THREAD rows per thread keep every field from carrying.
 template <int DP>
 __global__ __launch_bounds__(MEAN_THREADS) void mean_sums_kernel(const uint8_t *__restrict__ codes, uint64_t N,
                                                                  uint32_t D, const uint64_t *__restrict__ plut,
                                                                  uint64_t *__restrict__ sums, MeanInit init) {
-    __shared__ uint32_t lo8[256];
+    constexpr int Q3 = DP / 4;   // component quads (words per row)
+    __shared__ uint8_t lo8[256];
     __shared__ uint32_t red[MEAN_THREADS / 64][DP][2];
-    if (threadIdx.x < 256) lo8[threadIdx.x] = (uint32_t)(plut[threadIdx.x] & 0xFF);
+    if (threadIdx.x < 256) lo8[threadIdx.x] = (uint8_t)(plut[threadIdx.x] & 0xFF);
     if (blockIdx.x == 0) {
         if (threadIdx.x == 0) {
             sums[2 * D] = N;   // cnt[0]
@@ -359,42 +366,111 @@ __global__ __launch_bounds__(MEAN_THREADS) void mean_sums_kernel(const uint8_t *
         if (threadIdx.x < init.n_zero) init.zero[threadIdx.x] = 0;
     }
     __syncthreads();
-    uint32_t acc[DP];
+    // low parts two components per register too: lo2[2q] = (4q, 4q+1), lo2[2q+1] = (4q+2, 4q+3)
+    uint32_t ue[Q3], uo[Q3], lo2[DP / 2];
 #pragma unroll
-    for (int d = 0; d < DP; d++) acc[d] = 0;
-    auto add_word = [&](uint32_t w, int d0) {
+    for (int q = 0; q < Q3; q++) ue[q] = uo[q] = 0;
 #pragma unroll
-        for (int j = 0; j < 4; j++) {
-            const uint32_t b = (w >> (8 * j)) & 0xFF;
-            acc[d0 + j] += ((b ^ 0x80u) << 16) | lo8[b];
-        }
+    for (int d = 0; d < DP / 2; d++) lo2[d] = 0;
+    auto add_word = [&](uint32_t w, int q) {
+        const uint32_t u = w ^ 0x80808080u;
+        ue[q] += u & 0x00FF00FFu;
+        uo[q] += (u >> 8) & 0x00FF00FFu;
+#pragma unroll
+        for (int j = 0; j < 4; j++) lo2[2 * q + j / 2] += (uint32_t)lo8[(w >> (8 * j)) & 0xFF] << (16 * (j & 1));
     };
     constexpr int Q = DP / 4;   // 16-byte loads per group of 4 rows
-    const uint64_t groups = N / 4, stride = (uint64_t)gridDim.x * MEAN_THREADS;
-    for (uint64_t g = (uint64_t)blockIdx.x * MEAN_THREADS + threadIdx.x; g < groups; g += 2 * stride) {
-        const uint64_t g2 = g + stride < groups ? g + stride : g;
-        const uint4 *p = reinterpret_cast<const uint4 *>(codes + g * 4 * DP);
-        const uint4 *p2 = reinterpret_cast<const uint4 *>(codes + g2 * 4 * DP);
-        uint4 v[Q], v2[Q];
+    const uint64_t groups = N / 4;
+    uint64_t g_begin = 0;   // groups before this are done by the wave-chunk loop
+    if constexpr (Q <= 4) {
+        // Wave chunks of 64 groups (64 Q 16-byte words), loaded lane-contiguously: load j of lane
+        // l is 16-byte word 64 j + l of the chunk, whose 4-byte word k is word 4(64 j + l) + k,
+        // i.e. component quad (256 j + 4 l + k) mod Q.  Words go to slot (256 j + k) mod Q; the
+        // lane's slots are rotated by 4 l mod Q at the end.  MEAN_U chunks per trip in flight.
+        const uint64_t chunks = groups / 64;
+        const uint64_t wave_id = (uint64_t)blockIdx.x * (MEAN_THREADS / 64) + (threadIdx.x >> 6);
+        const uint64_t nwaves = (uint64_t)gridDim.x * (MEAN_THREADS / 64);
+        const int lane = threadIdx.x & 63;
+        for (uint64_t c = wave_id; c < chunks; c += MEAN_U * nwaves) {
+            uint4 v[MEAN_U][Q];
 #pragma unroll
-        for (int q = 0; q < Q; q++) v[q] = p[q];
+            for (int u = 0; u < MEAN_U; u++) {
+                const uint64_t cu = c + u * nwaves < chunks ? c + u * nwaves : c;   // repeats skipped
+                const uint4 *p = reinterpret_cast<const uint4 *>(codes + cu * 64 * 4 * DP);
 #pragma unroll
-        for (int q = 0; q < Q; q++) v2[q] = p2[q];
-        // word i of the group is component (i mod DP/4)*4.. of row i / (DP/4)
+                for (int j = 0; j < Q; j++) v[u][j] = p[64 * j + lane];
+            }
 #pragma unroll
-        for (int q = 0; q < Q; q++) {
-            add_word(v[q].x, ((4 * q + 0) % (DP / 4)) * 4);
-            add_word(v[q].y, ((4 * q + 1) % (DP / 4)) * 4);
-            add_word(v[q].z, ((4 * q + 2) % (DP / 4)) * 4);
-            add_word(v[q].w, ((4 * q + 3) % (DP / 4)) * 4);
+            for (int u = 0; u < MEAN_U; u++) {
+                if (u > 0 && c + u * nwaves >= chunks) break;
+#pragma unroll
+                for (int j = 0; j < Q; j++) {
+                    add_word(v[u][j].x, (256 * j + 0) % Q);
+                    add_word(v[u][j].y, (256 * j + 1) % Q);
+                    add_word(v[u][j].z, (256 * j + 2) % Q);
+                    add_word(v[u][j].w, (256 * j + 3) % Q);
+                }
+            }
         }
-        if (g2 != g) {
+        // slot s of this lane holds quad (s + 4 lane) mod Q
+        const uint32_t r = (4u * (uint32_t)lane) % Q;
+        uint32_t e2[Q], o2[Q], l2[DP / 2];
+#pragma unroll
+        for (int qd = 0; qd < Q; qd++) {
+            e2[qd] = o2[qd] = l2[2 * qd] = l2[2 * qd + 1] = 0;
+#pragma unroll
+            for (int sl = 0; sl < Q; sl++) {
+                const bool hit = (uint32_t)((sl + r) % Q) == (uint32_t)qd;
+                e2[qd] += hit ? ue[sl] : 0u;
+                o2[qd] += hit ? uo[sl] : 0u;
+                l2[2 * qd] += hit ? lo2[2 * sl] : 0u;
+                l2[2 * qd + 1] += hit ? lo2[2 * sl + 1] : 0u;
+            }
+        }
+#pragma unroll
+        for (int qd = 0; qd < Q; qd++) {
+            ue[qd] = e2[qd];
+            uo[qd] = o2[qd];
+            lo2[2 * qd] = l2[2 * qd];
+            lo2[2 * qd + 1] = l2[2 * qd + 1];
+        }
+        g_begin = chunks * 64;
+    }
+    // groups past the wave chunks (every group for wide rows): one group per thread, MEAN_U
+    // groups per trip with all their loads issued first
+    constexpr int U = DP <= 16 ? MEAN_U : (DP <= 32 ? 2 : 1);   // (wide rows: fewer, by registers)
+    const uint64_t stride = (uint64_t)gridDim.x * MEAN_THREADS;
+    for (uint64_t g = g_begin + (uint64_t)blockIdx.x * MEAN_THREADS + threadIdx.x; g < groups; g += U * stride) {
+        if constexpr (DP > 32) {   // wide rows: the group's 16-byte loads one by one (registers)
+            const uint4 *p = reinterpret_cast<const uint4 *>(codes + g * 4 * DP);
 #pragma unroll
             for (int q = 0; q < Q; q++) {
-                add_word(v2[q].x, ((4 * q + 0) % (DP / 4)) * 4);
-                add_word(v2[q].y, ((4 * q + 1) % (DP / 4)) * 4);
-                add_word(v2[q].z, ((4 * q + 2) % (DP / 4)) * 4);
-                add_word(v2[q].w, ((4 * q + 3) % (DP / 4)) * 4);
+                const uint4 w = p[q];
+                add_word(w.x, (4 * q + 0) % Q3);
+                add_word(w.y, (4 * q + 1) % Q3);
+                add_word(w.z, (4 * q + 2) % Q3);
+                add_word(w.w, (4 * q + 3) % Q3);
+            }
+            continue;
+        }
+        uint4 v[U][Q];
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            const uint64_t gu = g + u * stride < groups ? g + u * stride : g;   // repeats are skipped
+            const uint4 *p = reinterpret_cast<const uint4 *>(codes + gu * 4 * DP);
+#pragma unroll
+            for (int q = 0; q < Q; q++) v[u][q] = p[q];
+        }
+        // word i of the group holds components (i mod DP/4)*4 .. +3 of row i / (DP/4)
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            if (u > 0 && g + u * stride >= groups) break;
+#pragma unroll
+            for (int q = 0; q < Q; q++) {
+                add_word(v[u][q].x, (4 * q + 0) % Q3);
+                add_word(v[u][q].y, (4 * q + 1) % Q3);
+                add_word(v[u][q].z, (4 * q + 2) % Q3);
+                add_word(v[u][q].w, (4 * q + 3) % Q3);
             }
         }
     }
@@ -402,13 +478,15 @@ __global__ __launch_bounds__(MEAN_THREADS) void mean_sums_kernel(const uint8_t *
     if (blockIdx.x == 0 && threadIdx.x < N % 4) {
         const uint32_t *w = reinterpret_cast<const uint32_t *>(codes + (groups * 4 + threadIdx.x) * DP);
 #pragma unroll
-        for (int q = 0; q < DP / 4; q++) add_word(w[q], 4 * q);
+        for (int q = 0; q < Q3; q++) add_word(w[q], q);
     }
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
 #pragma unroll
     for (int d = 0; d < DP; d++) {
         // wave totals (< 2^22) by DPP scans on the VALU: lane 63 holds them
-        const uint32_t h = wave_scan_add(acc[d] >> 16), l = wave_scan_add(acc[d] & 0xFFFF);
+        const uint32_t f = (d & 1 ? uo[d / 4] : ue[d / 4]) >> (d & 2 ? 16 : 0);
+        const uint32_t g = lo2[d / 2] >> (d & 1 ? 16 : 0);
+        const uint32_t h = wave_scan_add(f & 0xFFFF), l = wave_scan_add(g & 0xFFFF);
         if (lane == 63) {
             red[wave][d][0] = h;
             red[wave][d][1] = l;
@@ -421,8 +499,9 @@ __global__ __launch_bounds__(MEAN_THREADS) void mean_sums_kernel(const uint8_t *
             h += red[w][threadIdx.x][0];
             l += red[w][threadIdx.x][1];
         }
-        atomicAdd((unsigned long long *)&sums[threadIdx.x], (unsigned long long)h);
-        atomicAdd((unsigned long long *)&sums[D + threadIdx.x], (unsigned long long)l);
+        uint64_t *dst = sums + (blockIdx.x % MEAN_COPIES) * (2 * (uint64_t)D + 1);
+        atomicAdd((unsigned long long *)&dst[threadIdx.x], (unsigned long long)h);
+        atomicAdd((unsigned long long *)&dst[D + threadIdx.x], (unsigned long long)l);
     }
 }
 
@@ -530,6 +609,7 @@ struct FinArgs {
     bool dist;
     uint64_t *zero_after;   // cleared by the last block once every block has read sums (mean)
     uint32_t n_zero;
+    uint32_t ncopy;         // copies of the sums to add (stride 2KD + K): the mean's MEAN_COPIES
 };
 
 // One (row j, component lane d) item of the finalize; L lanes per row (16 when D == 12: the
@@ -537,14 +617,18 @@ struct FinArgs {
 __device__ inline double finalize_item(const FinArgs &a, uint32_t j, uint32_t d, uint32_t L) {
     const uint32_t K = a.K, D = a.D, Dp = a.Dp;
     const uint64_t KD = (uint64_t)K * D;
-    const uint64_t *sums = a.sums;
+    auto sums_at = [&](uint64_t i) {   // the sum of the ncopy copies
+        uint64_t v = a.sums[i];
+        for (uint32_t c = 1; c < a.ncopy; c++) v += a.sums[c * (2 * KD + K) + i];
+        return v;
+    };
     if (a.split) {
         if (j < 2 * K) {
             const uint32_t k = j < K ? j : j - K;
             double v = 0;
             if (d < D) {
                 const uint64_t c = (uint64_t)d * K + k;
-                const double cv = centroid_value(sums[c], sums[KD + c], sums[2 * KD + k], a.R, a.bias, a.scale);
+                const double cv = centroid_value(sums_at(c), sums_at(KD + c), sums_at(2 * KD + k), a.R, a.bias, a.scale);
                 if (j < K) a.C_cent[(uint64_t)k * D + d] = cv;
                 v = cv * (j < K ? (double)(1 + 0.2) : (double)(1 - 0.2));
                 a.C64n[(uint64_t)j * D + d] = v;
@@ -589,12 +673,11 @@ __device__ inline double finalize_item(const FinArgs &a, uint32_t j, uint32_t d,
     }
     if (j < K && d < D) {
         const uint64_t c = (uint64_t)d * K + j;
-        const uint64_t cnt = sums[2 * KD + j];
-        const double cv = centroid_value(sums[c], sums[KD + c], cnt, a.R, a.bias, a.scale);
+        const uint64_t cnt = sums_at(2 * KD + j), hs = sums_at(c), ls = sums_at(KD + c);
+        const double cv = centroid_value(hs, ls, cnt, a.R, a.bias, a.scale);
         a.C_cent[(uint64_t)j * D + d] = cv;
         if (a.dist && cnt) {
-            const __int128 Sq =
-                (__int128)a.R * (__int128)sums[c] + (__int128)sums[KD + c] - (__int128)a.bias * (__int128)cnt;
+            const __int128 Sq = (__int128)a.R * (__int128)hs + (__int128)ls - (__int128)a.bias * (__int128)cnt;
             const double S = ldexp(i128_to_double(Sq), -a.scale);
             return 2.0 * cv * S - (double)cnt * cv * cv;
         }
@@ -645,8 +728,8 @@ __global__ __launch_bounds__(256) void finalize_prep_kernel(FinArgs a, double *_
             dist_out[0] = t;
         }
     }
+    for (uint32_t i = threadIdx.x; i < a.n_zero; i += blockDim.x) a.zero_after[i] = 0;
     if (threadIdx.x == 0) {
-        for (uint32_t i = 0; i < a.n_zero; i++) a.zero_after[i] = 0;
         *done = 0;
         if (ready) {
             __threadfence_system();
@@ -680,6 +763,7 @@ static FinArgs fin_args(const uint64_t *sums, uint32_t K, uint32_t D, uint32_t D
     a.dist = dist;
     a.zero_after = nullptr;
     a.n_zero = 0;
+    a.ncopy = 1;
     return a;
 }
 
@@ -687,7 +771,7 @@ hipError_t launch_finalize_prep(hipStream_t s, const uint64_t *sums, uint32_t K,
                                 int64_t bias, int scale, double *C_cent, bool split, double *C64n, uint32_t Kpad_next,
                                 double mu, double sx, int t, float *C32, _Float16 *cb_rows, float *E32,
                                 double *host_cb, double *dist_part, unsigned *done, double *dist_out, uint64_t *ready,
-                                uint64_t seq, bool zero_sums) {
+                                uint64_t seq, bool zero_sums, uint32_t ncopy) {
     if (D == 0 || D > 64) return hipErrorInvalidValue;
     if (zero_sums && !done) return hipErrorInvalidValue;   // the clearing is the last block's
     const uint32_t L = D <= 16 ? 16 : (D <= 32 ? 32 : 64);
@@ -695,9 +779,10 @@ hipError_t launch_finalize_prep(hipStream_t s, const uint64_t *sums, uint32_t K,
     const uint32_t grid = std::min<uint32_t>((n + 256 / L - 1) / (256 / L), 512);   // <= dist_part capacity
     FinArgs a = fin_args(sums, K, D, Dp, R, bias, scale, C_cent, split, C64n, Kpad_next, mu, sx, t, C32, cb_rows,
                          E32, host_cb, dist_out != nullptr);
+    a.ncopy = ncopy ? ncopy : 1;
     if (zero_sums) {
         a.zero_after = const_cast<uint64_t *>(sums);
-        a.n_zero = 2 * K * D + K;
+        a.n_zero = a.ncopy * (2 * K * D + K);
     }
     hipLaunchKernelGGL(finalize_prep_kernel, dim3(grid), dim3(256), 0, s, a, dist_part, done, dist_out,
                        (volatile uint64_t *)ready, seq, L);
@@ -969,6 +1054,100 @@ __global__ __launch_bounds__(256) void decode_rows_kernel(DecodeArgs a) {
     decode_finish(a, sq, bad);
 }
 
+// No overhang (ys % h == 0) and h dividing 8: the 8 pixels (x, 8q .. 8q+7) of a thread are the
+// column dx0 = x mod w of 8 / H consecutive blocks of one block column -- 3H contiguous bytes of
+// each block's code vector at byte 3 H dx0 -- so no per-pixel divisions: one vector load of the
+// 8 / H consecutive indices (16-byte aligned: hB = ys / H and 8q / H are multiples of 8 / H),
+// 16-bit codebook reads from LDS (3H is even for H >= 2), three dwordx2 stores.
+template <int H, bool LDSCB>
+__global__ __launch_bounds__(256) void decode_rows_h_kernel(DecodeArgs a) {
+    constexpr int NB = 8 / H;   // blocks per thread
+    extern __shared__ __attribute__((aligned(16))) uint8_t scb[];
+    if (LDSCB) {
+        const uint32_t n4 = (a.K * a.D + 3) / 4;
+        for (uint32_t i = threadIdx.x; i < n4; i += 256)
+            reinterpret_cast<uint32_t *>(scb)[i] = reinterpret_cast<const uint32_t *>(a.cb)[i];
+        __syncthreads();
+    }
+    const uint8_t *cb = LDSCB ? scb : a.cb;
+    const uint32_t qpr = a.ys / 8;
+    const uint64_t total = (uint64_t)a.xs * qpr;
+    uint64_t sq = 0;
+    bool bad = false;
+    const bool small = total < (1ull << 32);   // 32-bit index math (C3: 2M items)
+    for (uint64_t t = blockIdx.x * 256ull + threadIdx.x; t < total; t += (uint64_t)gridDim.x * 256) {
+        uint32_t x, q;
+        if (small) {
+            x = (uint32_t)t / qpr;
+            q = (uint32_t)t - x * qpr;
+        } else {
+            x = (uint32_t)(t / qpr);
+            q = (uint32_t)(t - (uint64_t)x * qpr);
+        }
+        const uint32_t i0 = x / a.w, dx0 = x - i0 * a.w;
+        const uint32_t *ap = a.A + (uint64_t)i0 * a.hB + (uint64_t)q * NB;
+        uint32_t code[NB];
+        if constexpr (NB == 8) {
+            const uint4 c0 = reinterpret_cast<const uint4 *>(ap)[0], c1 = reinterpret_cast<const uint4 *>(ap)[1];
+            code[0] = c0.x, code[1] = c0.y, code[2] = c0.z, code[3] = c0.w;
+            code[4] = c1.x, code[5] = c1.y, code[6] = c1.z, code[7] = c1.w;
+        } else if constexpr (NB == 4) {
+            const uint4 c0 = reinterpret_cast<const uint4 *>(ap)[0];
+            code[0] = c0.x, code[1] = c0.y, code[2] = c0.z, code[3] = c0.w;
+        } else if constexpr (NB == 2) {
+            const uint2 c0 = reinterpret_cast<const uint2 *>(ap)[0];
+            code[0] = c0.x, code[1] = c0.y;
+        } else {
+            code[0] = ap[0];
+        }
+        // branch-free: an out-of-range index reads code vector 0 and is masked to zero
+        uint32_t wv[6];
+        if constexpr (H == 1) {
+            uint32_t px[8];
+#pragma unroll
+            for (int b = 0; b < NB; b++) {
+                const bool ok = code[b] < a.K;
+                bad |= !ok;
+                const uint8_t *src = cb + (ok ? code[b] : 0u) * a.D + 3 * dx0;
+                const uint32_t v = (uint32_t)src[0] | (uint32_t)src[1] << 8 | (uint32_t)src[2] << 16;
+                px[b] = ok ? v : 0u;
+            }
+            wv[0] = px[0] | px[1] << 24;
+            wv[1] = px[1] >> 8 | px[2] << 16;
+            wv[2] = px[2] >> 16 | px[3] << 8;
+            wv[3] = px[4] | px[5] << 24;
+            wv[4] = px[5] >> 8 | px[6] << 16;
+            wv[5] = px[6] >> 16 | px[7] << 8;
+        } else {
+            constexpr int HB = 3 * H / 2;   // 16-bit halves per block
+            uint32_t hv[12];
+#pragma unroll
+            for (int b = 0; b < NB; b++) {
+                const bool ok = code[b] < a.K;
+                bad |= !ok;
+                const uint16_t *src = reinterpret_cast<const uint16_t *>(cb + (ok ? code[b] : 0u) * a.D + 3 * H * dx0);
+                const uint32_t m = ok ? 0xFFFFu : 0u;
+#pragma unroll
+                for (int k = 0; k < HB; k++) hv[HB * b + k] = (uint32_t)src[k] & m;
+            }
+#pragma unroll
+            for (int k = 0; k < 6; k++) wv[k] = hv[2 * k] | hv[2 * k + 1] << 16;
+        }
+        const uint64_t byte0 = ((uint64_t)x * a.ys + 8ull * q) * 3;
+        uint2 *dst = reinterpret_cast<uint2 *>(a.rgb + byte0);
+        dst[0] = make_uint2(wv[0], wv[1]);
+        dst[1] = make_uint2(wv[2], wv[3]);
+        dst[2] = make_uint2(wv[4], wv[5]);
+        if (a.orig) {
+            const uint2 *o = reinterpret_cast<const uint2 *>(a.orig + byte0);
+            const uint2 o0 = o[0], o1 = o[1], o2 = o[2];
+            sq += sq_diff_bytes(wv[0], o0.x) + sq_diff_bytes(wv[1], o0.y) + sq_diff_bytes(wv[2], o1.x) +
+                  sq_diff_bytes(wv[3], o1.y) + sq_diff_bytes(wv[4], o2.x) + sq_diff_bytes(wv[5], o2.y);
+        }
+    }
+    decode_finish(a, sq, bad);
+}
+
 // Any raster: one thread per pixel, byte stores (ys % 8 != 0).
 __global__ __launch_bounds__(256) void decode_pixels_kernel(DecodeArgs a) {
     const uint64_t npix = (uint64_t)a.xs * a.ys;
@@ -1003,10 +1182,21 @@ hipError_t launch_decode(hipStream_t s, const uint8_t *cb, uint32_t K, uint32_t 
         const uint64_t items = (uint64_t)xs * (ys / 8);
         const int grid = (int)std::max<uint64_t>(1, std::min<uint64_t>((items + 255) / 256, 1u << 16));
         const size_t cbB = (size_t)K * D;
-        if (cbB <= 48 * 1024)
-            hipLaunchKernelGGL(decode_rows_kernel<true>, dim3(grid), dim3(256), (cbB + 15) & ~(size_t)15, s, a);
-        else
+        const bool lds = cbB <= 48 * 1024;
+        const size_t ldsB = lds ? (cbB + 15) & ~(size_t)15 : 0;
+        if (a.overhang == 0 && (h == 1 || h == 2 || h == 4 || h == 8) && !std::getenv("QVQ_DECODE_GENERIC")) {
+#define QVQ_DEC_H(HV)                                                                                         \
+    if (h == HV) {                                                                                            \
+        if (lds) hipLaunchKernelGGL((decode_rows_h_kernel<HV, true>), dim3(grid), dim3(256), ldsB, s, a);      \
+        else hipLaunchKernelGGL((decode_rows_h_kernel<HV, false>), dim3(grid), dim3(256), 0, s, a);            \
+    }
+            QVQ_DEC_H(1) QVQ_DEC_H(2) QVQ_DEC_H(4) QVQ_DEC_H(8)
+#undef QVQ_DEC_H
+        } else if (lds) {
+            hipLaunchKernelGGL(decode_rows_kernel<true>, dim3(grid), dim3(256), ldsB, s, a);
+        } else {
             hipLaunchKernelGGL(decode_rows_kernel<false>, dim3(grid), dim3(256), 0, s, a);
+        }
     } else {
         const uint64_t npix = (uint64_t)xs * ys;
         const int grid = (int)std::max<uint64_t>(1, std::min<uint64_t>((npix + 255) / 256, 1u << 16));
