@@ -10,6 +10,7 @@ There is no CPU fallback: every compute call goes to the GPU through libqvq.so a
 QVQError when the library or the device is missing.
 """
 import ctypes
+import sys
 import enum
 import os
 
@@ -98,10 +99,25 @@ def _check(st, ctx=None):
         raise QVQError(st, msg.decode() if msg else "")
 
 
+def _torch_runtime_first():
+    """PyTorch-ROCm wheels bundle their own HIP/HSA runtime next to the /opt/rocm one libqvq.so
+    links.  When libqvq.so opens the device first, the bundled runtime's later device discovery
+    fails ("No HIP GPUs are available"); the other order works.  So if torch is already loaded,
+    let it open the device before the engine does."""
+    torch = sys.modules.get("torch")
+    if torch is not None:
+        try:
+            if torch.cuda.is_available():
+                torch.cuda.init()
+        except Exception:   # no device for torch: the engine's own error says why
+            pass
+
+
 class Engine:
     """One qvq context: one GPU, one HIP stream, one resident training set."""
 
     def __init__(self, device=0):
+        _torch_runtime_first()
         h = ctypes.c_void_p()
         _check(lib().qvq_create(device, ctypes.byref(h)))
         self._h = h

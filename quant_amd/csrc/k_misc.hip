@@ -1059,10 +1059,16 @@ __global__ __launch_bounds__(256) void decode_rows_kernel(DecodeArgs a) {
 // each block's code vector at byte 3 H dx0 -- so no per-pixel divisions: one vector load of the
 // 8 / H consecutive indices (16-byte aligned: hB = ys / H and 8q / H are multiples of 8 / H),
 // 16-bit codebook reads from LDS (3H is even for H >= 2), three dwordx2 stores.
-template <int H, bool LDSCB>
-__global__ __launch_bounds__(256) void decode_rows_h_kernel(DecodeArgs a) {
+// COAL (ys % 512 == 0: a wave's 64 threads are 1536 contiguous output bytes of one raster row):
+// the wave stages its three 8-byte pieces per lane in LDS and stores the chunk lane-contiguously,
+// 512 bytes per store instruction (the direct stores have a 24-byte lane stride); the raport's
+// original bytes are read the same coalesced way.
+template <int H, bool LDSCB, bool COAL>
+__global__ __launch_bounds__(256) void decode_rows_h_kernel(DecodeArgs a, uint32_t stage_off) {
     constexpr int NB = 8 / H;   // blocks per thread
     extern __shared__ __attribute__((aligned(16))) uint8_t scb[];
+    const int lane = threadIdx.x & 63;
+    uint2 *stage = reinterpret_cast<uint2 *>(scb + stage_off) + (threadIdx.x >> 6) * 192;   // 1536 B per wave
     if (LDSCB) {
         const uint32_t n4 = (a.K * a.D + 3) / 4;
         for (uint32_t i = threadIdx.x; i < n4; i += 256)
@@ -1134,15 +1140,44 @@ __global__ __launch_bounds__(256) void decode_rows_h_kernel(DecodeArgs a) {
             for (int k = 0; k < 6; k++) wv[k] = hv[2 * k] | hv[2 * k + 1] << 16;
         }
         const uint64_t byte0 = ((uint64_t)x * a.ys + 8ull * q) * 3;
-        uint2 *dst = reinterpret_cast<uint2 *>(a.rgb + byte0);
-        dst[0] = make_uint2(wv[0], wv[1]);
-        dst[1] = make_uint2(wv[2], wv[3]);
-        dst[2] = make_uint2(wv[4], wv[5]);
-        if (a.orig) {
-            const uint2 *o = reinterpret_cast<const uint2 *>(a.orig + byte0);
-            const uint2 o0 = o[0], o1 = o[1], o2 = o[2];
-            sq += sq_diff_bytes(wv[0], o0.x) + sq_diff_bytes(wv[1], o0.y) + sq_diff_bytes(wv[2], o1.x) +
-                  sq_diff_bytes(wv[3], o1.y) + sq_diff_bytes(wv[4], o2.x) + sq_diff_bytes(wv[5], o2.y);
+        if constexpr (COAL) {
+            // lane l's 24 bytes are chunk bytes [24 l, 24 l + 24); stored piece k of lane l is
+            // chunk bytes [512 k + 8 l, + 8) (ds_write_b64 at a 24-byte stride is conflict-free)
+            stage[3 * lane] = make_uint2(wv[0], wv[1]);
+            stage[3 * lane + 1] = make_uint2(wv[2], wv[3]);
+            stage[3 * lane + 2] = make_uint2(wv[4], wv[5]);
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            uint2 pc[3];
+#pragma unroll
+            for (int k = 0; k < 3; k++) pc[k] = stage[64 * k + lane];
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");   // reads before the next writes
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            const uint64_t c0 = byte0 - 24ull * lane;   // the wave's chunk start (lane 0's byte0)
+            uint2 *dst = reinterpret_cast<uint2 *>(a.rgb + c0);
+#pragma unroll
+            for (int k = 0; k < 3; k++) dst[64 * k + lane] = pc[k];
+            if (a.orig) {
+                const uint2 *o = reinterpret_cast<const uint2 *>(a.orig + c0);
+#pragma unroll
+                for (int k = 0; k < 3; k++) {
+                    const uint2 ov = o[64 * k + lane];
+                    sq += sq_diff_bytes(pc[k].x, ov.x) + sq_diff_bytes(pc[k].y, ov.y);
+                }
+            }
+        } else {
+            uint2 *dst = reinterpret_cast<uint2 *>(a.rgb + byte0);
+            dst[0] = make_uint2(wv[0], wv[1]);
+            dst[1] = make_uint2(wv[2], wv[3]);
+            dst[2] = make_uint2(wv[4], wv[5]);
+            if (a.orig) {
+                const uint2 *o = reinterpret_cast<const uint2 *>(a.orig + byte0);
+                const uint2 o0 = o[0], o1 = o[1], o2 = o[2];
+                sq += sq_diff_bytes(wv[0], o0.x) + sq_diff_bytes(wv[1], o0.y) + sq_diff_bytes(wv[2], o1.x) +
+                      sq_diff_bytes(wv[3], o1.y) + sq_diff_bytes(wv[4], o2.x) + sq_diff_bytes(wv[5], o2.y);
+            }
         }
     }
     decode_finish(a, sq, bad);
@@ -1180,15 +1215,27 @@ hipError_t launch_decode(hipStream_t s, const uint8_t *cb, uint32_t K, uint32_t 
     a.rgb = rgb, a.orig = orig, a.sqerr = (unsigned long long *)sqerr, a.bad = bad;
     if (ys % 8 == 0 && (uint64_t)xs * ys < (1ull << 40)) {
         const uint64_t items = (uint64_t)xs * (ys / 8);
-        const int grid = (int)std::max<uint64_t>(1, std::min<uint64_t>((items + 255) / 256, 1u << 16));
         const size_t cbB = (size_t)K * D;
         const bool lds = cbB <= 48 * 1024;
+        // with the codebook staged in LDS, a block loops over several 256-item rounds (C3: 8192
+        // one-round blocks staged 100 MB of codebook copies for 67 MB of output)
+        static const uint64_t cap = std::getenv("QVQ_DECODE_GRID") ? std::atoll(std::getenv("QVQ_DECODE_GRID")) : 2048;
+        const int grid = (int)std::max<uint64_t>(1, std::min<uint64_t>((items + 255) / 256, lds ? cap : 1u << 16));
         const size_t ldsB = lds ? (cbB + 15) & ~(size_t)15 : 0;
         if (a.overhang == 0 && (h == 1 || h == 2 || h == 4 || h == 8) && !std::getenv("QVQ_DECODE_GENERIC")) {
-#define QVQ_DEC_H(HV)                                                                                         \
-    if (h == HV) {                                                                                            \
-        if (lds) hipLaunchKernelGGL((decode_rows_h_kernel<HV, true>), dim3(grid), dim3(256), ldsB, s, a);      \
-        else hipLaunchKernelGGL((decode_rows_h_kernel<HV, false>), dim3(grid), dim3(256), 0, s, a);            \
+            // wave-contiguous output chunks need whole waves inside one raster row: 64 | ys / 8
+            const bool coal = (ys / 8) % 64 == 0 && !std::getenv("QVQ_DECODE_NOCOAL");
+            const uint32_t soff = (uint32_t)ldsB;
+            const size_t lb = ldsB + (coal ? 4 * 1536 : 0);
+#define QVQ_DEC_H(HV)                                                                                                  \
+    if (h == HV) {                                                                                                     \
+        if (coal) {                                                                                                    \
+            if (lds) hipLaunchKernelGGL((decode_rows_h_kernel<HV, true, true>), dim3(grid), dim3(256), lb, s, a, soff); \
+            else hipLaunchKernelGGL((decode_rows_h_kernel<HV, false, true>), dim3(grid), dim3(256), lb, s, a, soff);    \
+        } else {                                                                                                       \
+            if (lds) hipLaunchKernelGGL((decode_rows_h_kernel<HV, true, false>), dim3(grid), dim3(256), lb, s, a, soff);\
+            else hipLaunchKernelGGL((decode_rows_h_kernel<HV, false, false>), dim3(grid), dim3(256), lb, s, a, soff);   \
+        }                                                                                                              \
     }
             QVQ_DEC_H(1) QVQ_DEC_H(2) QVQ_DEC_H(4) QVQ_DEC_H(8)
 #undef QVQ_DEC_H

@@ -24,6 +24,7 @@ def load_png_rgb(name):
 
 @pytest.fixture(scope="session")
 def engine():
+    import torch   # noqa: F401  (torch's bundled HIP runtime opens the device first: quant_amd.Engine)
     import quant_amd
     eng = quant_amd.Engine(0)
     yield eng

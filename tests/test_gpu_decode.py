@@ -21,6 +21,8 @@ def _rand_case(rng, xs, ys, bw, bh, K):
 @pytest.mark.parametrize("xs,ys,bw,bh,K", [
     (64, 64, 2, 2, 16), (510, 383, 2, 2, 64), (383, 510, 3, 5, 32), (7, 5, 4, 4, 8),
     (1, 1, 2, 2, 2), (3, 1, 1, 4, 4), (2, 3, 5, 7, 4), (129, 97, 4, 4, 1024), (33, 65, 1, 1, 256),
+    # heights 1/2/4/8 without overhang, ys % 512 == 0: the LDS-staged coalesced store path
+    (65, 512, 3, 1, 64), (130, 1024, 2, 2, 700), (7, 512, 4, 4, 33), (9, 1536, 2, 8, 5),
 ])
 def test_decode_random_vs_oracle(engine, xs, ys, bw, bh, K):
     rng = np.random.default_rng(xs * 1000 + ys * 10 + bw)
@@ -64,7 +66,8 @@ def test_decode_device_c3_checksum(engine):
     np.testing.assert_array_equal(d_rgb.cpu().numpy(), oracle.decode(cb, A, xs, ys, 2, 2).ravel())
 
 
-@pytest.mark.parametrize("xs,ys,bw,bh", [(510, 383, 2, 2), (256, 256, 2, 2), (383, 512, 4, 4), (33, 65, 1, 1)])
+@pytest.mark.parametrize("xs,ys,bw,bh", [(510, 383, 2, 2), (256, 256, 2, 2), (383, 512, 4, 4), (33, 65, 1, 1),
+                                         (130, 1024, 2, 2), (17, 512, 1, 1), (5, 512, 3, 8)])
 def test_decode_mse_matches_raport(engine, xs, ys, bw, bh):
     """qvq_decode_mse: the raport's distortion (src/Compressor.cpp:133-146, signed bytes) from
     the same device pass as the decoded raster."""
