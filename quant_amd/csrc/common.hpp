@@ -139,6 +139,8 @@ struct MfThresholds {
     uint32_t runs_max_k;   // fused sums: wave run reduction up to this K, plain LDS atomics above
     // small-K scan (expanded fp32 scores): flag when second - best <= e0 + e1 * sum_d |w_d|
     float e0, e1;
+    // the mfma bound for one row (k_mf32.hip): m0 + m1 * sum_d |w_d| <= mfma
+    float m0, m1;
 };
 uint32_t mf_fuse_max_k();
 bool mf_can_search(uint32_t K);

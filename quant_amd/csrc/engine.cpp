@@ -254,6 +254,16 @@ void mfma_setup(qvq_ctx *ctx) {
                          n_max * std::ldexp(1.0, -22) + std::ldexp(1.0, -25 - tt);
     const double e_conv = 4 * u * (s_bound + D * cp * cp) + 1e-12 * s_bound;
     ctx->mf_th.mfma = (float)(1.25 * (e_acc + e_rep + e_conv));
+    // The same bound for one row, with sum_d |w_d| of that row in place of D * wmax (every term
+    // above is linear in it): S_row = n_max + c2_max * sum|w| replaces s_bound.
+    {
+        const double ew = std::ldexp(1.0, -25 - tt);
+        const double a0 = rounds * u * n_max + (n_max * std::ldexp(1.0, -22) + ew) + 4 * u * (n_max + D * cp * cp) +
+                          1e-12 * n_max;
+        const double a1 = rounds * u * c2_max + (c2_max * std::ldexp(1.0, -22) + ew) + 4 * u * c2_max + 1e-12 * c2_max;
+        ctx->mf_th.m0 = (float)(1.25 * a0 * 1.0001);
+        ctx->mf_th.m1 = (float)(1.25 * a1 * 1.0001);
+    }
     // direct-form fp32 recompute (same bound as the VALU search)
     const double L = std::sqrt(D) * (std::max(std::fabs(vmin), std::fabs(vmax)) + std::max(std::fabs(cmin), std::fabs(cmax))) * 1.001;
     ctx->mf_th.alpha = (float)(3.0 * 4.01 * u * L);   // x in fp32 is mu + w*sx: <= 2u relative

@@ -81,13 +81,28 @@ __device__ inline void m32_track(float m, uint32_t u, float &b1, float &b2, uint
     bu = m < b1 ? u : bu;
     b1 = min2f(b1, m);
 }
+// The same with the unit index u in the low `idbits` mantissa bits of the unit minimum
+// (v_and_or_b32): tracking is min + med3, and b1's low bits name its unit.  A tagged value
+// differs from the score by < 2^idbits ulps, i.e. relatively by < 2^(idbits - 23); the flag
+// threshold carries that (orrel, below).
+__device__ inline void m32_track_tagged(float m, uint32_t keep, uint32_t u, float &b1, float &b2) {
+    // one v_and_or_b32 (the compiler splits (m & keep) | u into and + or); m comes from VALU
+    // min3s, never straight from an MFMA, so no hazard hides inside the asm
+    uint32_t r;
+    asm("v_and_or_b32 %0, %1, %2, %3" : "=v"(r) : "v"(__float_as_uint(m)), "v"(keep), "s"(u));
+    const float t = __uint_as_float(r);
+    b2 = med3f(b1, b2, t);
+    b1 = min2f(b1, t);
+}
 
-template <bool FUSE, bool STAGED, int U>
+// TAG: unit indices in the scores' low bits (idbits of them, idbits >= log2 of the units per
+// lane; orrel = 2^(idbits - 22) bounds twice the relative change).
+template <bool FUSE, bool STAGED, int U, bool TAG>
 __global__ __launch_bounds__(M32_THREADS) void assign_mf32_kernel(
     const uint8_t *__restrict__ codes, uint64_t N, const _Float16 *__restrict__ g_rows, uint32_t K,
-    const float *__restrict__ g_C32, const uint64_t *__restrict__ g_plut, MfThresholds th, uint32_t *__restrict__ A,
-    uint32_t *__restrict__ flags, unsigned *__restrict__ flag_cnt, uint64_t *__restrict__ part,
-    uint32_t *__restrict__ part_cnt) {
+    const float *__restrict__ g_C32, const uint64_t *__restrict__ g_plut, MfThresholds th, uint32_t idbits,
+    float orrel, uint32_t *__restrict__ A, uint32_t *__restrict__ flags, unsigned *__restrict__ flag_cnt,
+    uint64_t *__restrict__ part, uint32_t *__restrict__ part_cnt) {
     static_assert(U == 4 || U == 8, "unit of 4 or 8 code vectors");
     constexpr int NU = 16 / U;   // units per lane and code tile
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
@@ -195,6 +210,7 @@ __global__ __launch_bounds__(M32_THREADS) void assign_mf32_kernel(
         half8 a1, a2;
         load_a(0, a1, a2);
         const f32x16 zero16 = {};
+        const uint32_t idmask = (1u << idbits) - 1, keep = ~idmask;
         for (uint32_t t = 0; t < ntiles; t++) {
             f32x16 c[2];
             c[0] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a1, b1[0], zero16, 0, 0, 0);
@@ -214,9 +230,17 @@ __global__ __launch_bounds__(M32_THREADS) void assign_mf32_kernel(
                                   c[T][o + 7]);
                     else
                         m = min2f(min3f(c[T][o], c[T][o + 1], c[T][o + 2]), c[T][o + 3]);
-                    m32_track(m, t * NU + qq, s1[T], s2[T], su[T]);
+                    // (the id as one scalar operand: v_and_or_b32, not and + or3 of its parts)
+                    if constexpr (TAG)
+                        m32_track_tagged(m, keep, (uint32_t)__builtin_amdgcn_readfirstlane((int)(t * NU + qq)), s1[T],
+                                         s2[T]);
+                    else m32_track(m, t * NU + qq, s1[T], s2[T], su[T]);
                 }
             }
+        }
+        if constexpr (TAG) {
+#pragma unroll
+            for (int T = 0; T < 2; T++) su[T] = __float_as_uint(s1[T]) & idmask;
         }
         // Merge the two halves of every data row: swap32(x = tile 0, y = tile 1) leaves lanes
         // < 32 with tile 0 row r32 (lo: own half, hi: half 1 of lane + 32) and lanes >= 32
@@ -277,10 +301,18 @@ __global__ __launch_bounds__(M32_THREADS) void assign_mf32_kernel(
                 r1 = min2f(r1, dist);
             }
             const float sec = min2f(__fmaf_rn(sec_m, th.inv_scale, xn), r2);
+            // per-row MFMA bound: sum_d |w_d| <= 2 sum_d |u_d - 127| + D (v_sad_u8 of the bytes)
+            uint32_t sad = 0;
+#pragma unroll
+            for (int k4 = 0; k4 < 3; k4++) sad = __builtin_amdgcn_sad_u8(own[k4] ^ 0x80808080u, 0x7F7F7F7Fu, sad);
+            const float thm = __fmaf_rn((float)(2 * sad + MF_D), th.m1, th.m0);
             // sec from an MFMA score can be slightly negative (a row on a code vector): the
             // row is flagged then anyway (r1 >= 0), and no NaN reaches the -fno-honor-nans compare
             const float sp = fmaxf(sec, 0.f);
-            const float thr = th.mfma + 2.f * (th.alpha * sqrtf(sp) + th.beta * sp) + th.gamma;
+            float thr = thm + 2.f * (th.alpha * sqrtf(sp) + th.beta * sp) + th.gamma;
+            // tagged unit minima: sec_m (and the choice of the best unit) is off by at most
+            // orrel / 2 relative, in distance units |sec_m| 2^-t
+            if (TAG) thr = __fmaf_rn(orrel * th.inv_scale, fabsf(sec_m), thr);
             A[row] = rk;
             if (!(sec - r1 > thr)) flags[atomicAdd(flag_cnt, 1u)] = (uint32_t)row;
         }
@@ -322,13 +354,13 @@ __global__ __launch_bounds__(M32_THREADS) void assign_mf32_kernel(
     }
 }
 
-template <bool F, bool S, int U>
+template <bool F, bool S, int U, bool TAG>
 static void launch_mf32_variant(hipStream_t s, int grid, size_t lds, const uint8_t *codes, uint64_t N,
                                 const _Float16 *cb_rows, uint32_t K, const float *C32, const uint64_t *plut,
-                                const MfThresholds &th, uint32_t *A, uint32_t *flags, unsigned *flag_cnt,
-                                uint64_t *part, uint32_t *part_cnt) {
-    hipLaunchKernelGGL((assign_mf32_kernel<F, S, U>), dim3(grid), dim3(M32_THREADS), lds, s, codes, N, cb_rows, K,
-                       C32, plut, th, A, flags, flag_cnt, part, part_cnt);
+                                const MfThresholds &th, uint32_t idbits, float orrel, uint32_t *A, uint32_t *flags,
+                                unsigned *flag_cnt, uint64_t *part, uint32_t *part_cnt) {
+    hipLaunchKernelGGL((assign_mf32_kernel<F, S, U, TAG>), dim3(grid), dim3(M32_THREADS), lds, s, codes, N, cb_rows,
+                       K, C32, plut, th, idbits, orrel, A, flags, flag_cnt, part, part_cnt);
 }
 
 bool mf32_fits(uint32_t K, bool fuse) { return m32_lds_layout(K, fuse, false).total <= M32_LDS_MAX; }
@@ -344,18 +376,31 @@ hipError_t launch_assign_mf32(hipStream_t s, int grid, bool fuse, const uint8_t 
     static const uint32_t u4_max =
         std::getenv("QVQ_U4_MAXK") ? (uint32_t)std::atoi(std::getenv("QVQ_U4_MAXK")) : 256;
     const bool u4 = K <= u4_max;
+    // unit tags: ids t * NU + q < (Kp / 32) * NU per lane; QVQ_MF32_TAG=0 tracks them apart
+    static const bool tag = !(std::getenv("QVQ_MF32_TAG") && std::getenv("QVQ_MF32_TAG")[0] == '0');
+    const uint32_t units = ((K + 31) / 32) * (u4 ? 4 : 2);
+    uint32_t idbits = 0;
+    while ((1u << idbits) < units) idbits++;
+    const float orrel = std::ldexp(1.0f, (int)idbits - 22);
     using Fn = void (*)(hipStream_t, int, size_t, const uint8_t *, uint64_t, const _Float16 *, uint32_t, const float *,
-                        const uint64_t *, const MfThresholds &, uint32_t *, uint32_t *, unsigned *, uint64_t *,
-                        uint32_t *);
-    Fn fn;
-    if (fuse) {
-        if (u4) fn = staged ? launch_mf32_variant<true, true, 4> : launch_mf32_variant<true, false, 4>;
-        else fn = staged ? launch_mf32_variant<true, true, 8> : launch_mf32_variant<true, false, 8>;
-    } else {
-        if (u4) fn = staged ? launch_mf32_variant<false, true, 4> : launch_mf32_variant<false, false, 4>;
-        else fn = staged ? launch_mf32_variant<false, true, 8> : launch_mf32_variant<false, false, 8>;
+                        const uint64_t *, const MfThresholds &, uint32_t, float, uint32_t *, uint32_t *, unsigned *,
+                        uint64_t *, uint32_t *);
+#define QVQ_MF32_PICK(TG)                                                                                          \
+    if (fuse) {                                                                                                    \
+        if (u4) fn = staged ? launch_mf32_variant<true, true, 4, TG> : launch_mf32_variant<true, false, 4, TG>;    \
+        else fn = staged ? launch_mf32_variant<true, true, 8, TG> : launch_mf32_variant<true, false, 8, TG>;       \
+    } else {                                                                                                       \
+        if (u4) fn = staged ? launch_mf32_variant<false, true, 4, TG> : launch_mf32_variant<false, false, 4, TG>;  \
+        else fn = staged ? launch_mf32_variant<false, true, 8, TG> : launch_mf32_variant<false, false, 8, TG>;     \
     }
-    fn(s, grid, lds, codes, N, cb_rows, K, C32, plut, th, A, flags, flag_cnt, part, part_cnt);
+    Fn fn;
+    if (tag && idbits <= 12) {
+        QVQ_MF32_PICK(true)
+    } else {
+        QVQ_MF32_PICK(false)
+    }
+#undef QVQ_MF32_PICK
+    fn(s, grid, lds, codes, N, cb_rows, K, C32, plut, th, idbits, orrel, A, flags, flag_cnt, part, part_cnt);
     return hipGetLastError();
 }
 
