@@ -174,6 +174,14 @@ hipError_t launch_recheck(hipStream_t s, int num_cu, const uint8_t *codes, uint3
                           uint32_t K, const double *lut64, float alpha, float beta, float gamma, double tie_rel,
                           uint32_t *A, uint32_t *ties, unsigned *tie_cnt, uint64_t *xslab, uint32_t *xcnt,
                           const uint64_t *plut);
+// The recheck on the search's MFMA scores (D = 12, k_mf32.hip): same contract as launch_recheck
+// (the band from th.m0 / th.m1), for K with recheck_mf32_fits.
+bool recheck_mf32_fits(uint32_t K);
+hipError_t launch_recheck_mf32(hipStream_t s, int num_cu, const uint8_t *codes, const uint32_t *flags,
+                               const unsigned *flag_cnt, const _Float16 *cb_rows, const double *C64, uint32_t K,
+                               const double *lut64, const MfThresholds &th, double tie_rel, uint32_t *A,
+                               uint32_t *ties, unsigned *tie_cnt, uint64_t *xslab, uint32_t *xcnt,
+                               const uint64_t *plut);
 // Device kd-tree answers for the listed ties (tree image in mapped host memory); adds their
 // terms to sums when given.  kd_resolve_fits: the tree, stacks and one wave's point
 // distances fit the LDS.

@@ -550,7 +550,18 @@ qvq_status run_level(qvq_ctx *ctx, uint32_t K, int slot, bool sums_out, const do
                                   ctx->d_lut32, alpha, beta, gamma, ctx->d_A, ctx->d_flags, &cnt[0]));
     }
     if (timing) HIPCHK(hipEventRecord(ctx->ev[slot][1], ctx->stream));
-    {
+    // the MFMA recheck from K = QVQ_RECHECK_MF_MINK (512; below it the fp32 pass over K code
+    // vectors is cheaper than staging the MFMA tables); QVQ_RECHECK=fp32 turns it off (A/B)
+    static const uint32_t rc_min_k = [] {
+        const char *v = std::getenv("QVQ_RECHECK_MF_MINK");
+        return v ? (uint32_t)std::atoi(v) : 512u;
+    }();
+    static const bool rc_mf32 = !env_is("QVQ_RECHECK", "fp32");
+    if (rc_mf32 && K >= rc_min_k && use_mfma(ctx, K) && recheck_mf32_fits(K)) {
+        HIPCHK(launch_recheck_mf32(ctx->stream, ctx->num_cu, ctx->d_codes, ctx->d_flags, &cnt[0], ctx->d_rows,
+                                   ctx->d_C64_split, K, ctx->d_lut64, ctx->mf_th, 1e-12, ctx->d_A, ctx->d_ties,
+                                   &cnt[1], xslab, xcnt, ctx->d_plut));
+    } else {
         float alpha, beta, gamma;
         valu_coeffs(ctx, alpha, beta, gamma);
         HIPCHK(launch_recheck(ctx->stream, ctx->num_cu, ctx->d_codes, ctx->Dp, ctx->D, ctx->d_flags, &cnt[0],

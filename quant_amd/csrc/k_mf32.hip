@@ -75,6 +75,25 @@ __device__ inline bool m32_runs_reduce(uint32_t key, uint32_t (&v)[MF_D + 1], in
     return lane == 63 || next != key;
 }
 
+// P / Q (LDS, layout above) from the 56-byte rows [hi0..3 lo0..3 | hi4..7 lo4..7 | hi8..11
+// lo8..11 | n] of Kp code vectors.
+__device__ inline void m32_stage_pq(unsigned char *lds, uint32_t qoff, const _Float16 *g_rows, uint32_t Kp, int tid) {
+    const uint64_t *src = reinterpret_cast<const uint64_t *>(g_rows);
+    for (uint32_t i = tid; i < Kp; i += M32_THREADS) {
+        const uint64_t *r = src + (size_t)i * 7;
+        const uint64_t w0 = r[0], w1 = r[1], w2 = r[2], w3 = r[3], w4 = r[4], w5 = r[5], w6 = r[6];
+        const bool sw = (i >> 3) & 1;
+        u64x2v *p = reinterpret_cast<u64x2v *>(lds + (size_t)i * 32);
+        const u64x2v hi = {w0, w2}, lo = {w1, w3};
+        p[0] = sw ? lo : hi;
+        p[1] = sw ? hi : lo;
+        uint64_t *q = reinterpret_cast<uint64_t *>(lds + qoff + (size_t)i * 24);
+        q[0] = w5;
+        q[1] = w4;
+        q[2] = w6;
+    }
+}
+
 // Running best unit / best score / second-best unit minimum of one lane and data tile.
 __device__ inline void m32_track(float m, uint32_t u, float &b1, float &b2, uint32_t &bu) {
     b2 = med3f(b1, b2, m);
@@ -113,22 +132,7 @@ __global__ __launch_bounds__(M32_THREADS) void assign_mf32_kernel(
     uint32_t *cnt = reinterpret_cast<uint32_t *>(lds + L.cnt);
     uint8_t *lo8 = lds + L.plut;   // low part of each byte's exact term (high part: b ^ 0x80)
     const int tid = threadIdx.x;
-    {   // P / Q from the 56-byte rows [hi0..3 lo0..3 | hi4..7 lo4..7 | hi8..11 lo8..11 | n]
-        const uint64_t *src = reinterpret_cast<const uint64_t *>(g_rows);
-        for (uint32_t i = tid; i < Kp; i += M32_THREADS) {
-            const uint64_t *r = src + (size_t)i * 7;
-            const uint64_t w0 = r[0], w1 = r[1], w2 = r[2], w3 = r[3], w4 = r[4], w5 = r[5], w6 = r[6];
-            const bool sw = (i >> 3) & 1;
-            u64x2v *p = reinterpret_cast<u64x2v *>(lds + (size_t)i * 32);
-            const u64x2v hi = {w0, w2}, lo = {w1, w3};
-            p[0] = sw ? lo : hi;
-            p[1] = sw ? hi : lo;
-            uint64_t *q = reinterpret_cast<uint64_t *>(lds + L.q + (size_t)i * 24);
-            q[0] = w5;
-            q[1] = w4;
-            q[2] = w6;
-        }
-    }
+    m32_stage_pq(lds, L.q, g_rows, Kp, tid);
     if (STAGED) {
         const float4 *src = reinterpret_cast<const float4 *>(g_C32);
         float4 *dst = reinterpret_cast<float4 *>(c32s);
@@ -352,6 +356,203 @@ __global__ __launch_bounds__(M32_THREADS) void assign_mf32_kernel(
         uint32_t *cdst = part_cnt + (uint64_t)blockIdx.x * K;
         for (uint32_t i = tid; i < K; i += M32_THREADS) cdst[i] = cnt[i];
     }
+}
+
+// =======================================================================================
+// Recheck of flagged rows on the same MFMA scores (D = 12).  A wave takes 32 flagged rows (one
+// data tile, both lane halves) through every code tile twice: pass 1 takes each row's minimum
+// score m; pass 2 lists the code vectors whose score is within m + 2E, E the row's MFMA bound
+// (m0 + m1 sum|w|, scaled) -- every other code vector is farther than the best in exact
+// arithmetic by more than the tie tolerance.  Those candidates (a few per row) get the fp64
+// distance in the reference's order (ref_l2_hd; lut64 values, C64); the row then takes the
+// lexicographic (distance, index) minimum, or goes to the kd-tree tie list when its best two
+// are within tie_rel.  Replaces the fp32 pass over all K per row (a wave per row) of
+// recheck_kernel: ~16 VALU per row and code tile pair instead of ~28 per code vector.
+// =======================================================================================
+constexpr int RC_CAP = 16;   // candidates listed per row; more: the row's lane scans all K in fp64
+
+struct RcLds {
+    uint32_t q, lut, cand, ncand, total;
+};
+__host__ __device__ inline RcLds rc_lds_layout(uint32_t K) {
+    const uint32_t Kp = (K + 31) & ~31u;
+    RcLds L;
+    uint32_t o = Kp * 32;
+    L.q = o;
+    o += Kp * 24;
+    o = (o + 15) & ~15u;
+    L.lut = o;
+    o += 256 * 8;
+    L.cand = o;
+    o += M32_WAVES * 32 * RC_CAP * 4;
+    L.ncand = o;
+    o += M32_WAVES * 32 * 4;
+    L.total = o;
+    return L;
+}
+bool recheck_mf32_fits(uint32_t K) { return rc_lds_layout(K).total <= M32_LDS_MAX; }
+
+__global__ __launch_bounds__(M32_THREADS) void recheck_mf32_kernel(
+    const uint8_t *__restrict__ codes, const uint32_t *__restrict__ flags, const unsigned *__restrict__ flag_cnt,
+    const _Float16 *__restrict__ g_rows, const double *__restrict__ C64, uint32_t K,
+    const double *__restrict__ g_lut64, MfThresholds th, double tie_rel, uint32_t *__restrict__ A,
+    uint32_t *__restrict__ ties, unsigned *__restrict__ tie_cnt, uint64_t *__restrict__ xslab,
+    uint32_t *__restrict__ xcnt, const uint64_t *__restrict__ plut) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+    const unsigned nflag = *flag_cnt;
+    const uint32_t ntile_rows = (nflag + 31) / 32;
+    if (blockIdx.x * M32_WAVES >= ntile_rows) return;   // (uniform) no rows for this block
+    const uint32_t Kp = (K + 31) & ~31u;
+    const RcLds L = rc_lds_layout(K);
+    const int tid = threadIdx.x;
+    m32_stage_pq(lds, L.q, g_rows, Kp, tid);
+    double *lut = reinterpret_cast<double *>(lds + L.lut);
+    for (uint32_t i = tid; i < 256; i += M32_THREADS) lut[i] = g_lut64[i];
+    const int lane = tid & 63, wave = tid >> 6;
+    const int r32 = lane & 31, h = lane >> 5;
+    uint32_t *cand = reinterpret_cast<uint32_t *>(lds + L.cand) + wave * 32 * RC_CAP;
+    uint32_t *ncand = reinterpret_cast<uint32_t *>(lds + L.ncand) + wave * 32;
+    if (h == 0) ncand[r32] = 0;
+    __syncthreads();
+    const uint32_t ntiles = Kp / 32;
+    const unsigned char *pa = lds + r32 * 32 + 16 * (h ^ ((r32 >> 3) & 1));
+    const unsigned char *qa = lds + L.q + r32 * 24 + 8 * (1 - h);
+    auto load_a = [&](uint32_t t, half8 &a1, half8 &a2) {
+        const u32x4v v1 = *reinterpret_cast<const u32x4v *>(pa + (size_t)t * (32 * 32));
+        const uint64_t *q = reinterpret_cast<const uint64_t *>(qa + (size_t)t * (32 * 24));
+        const u64x2v v2 = {q[0], q[1]};
+        a1 = __builtin_bit_cast(half8, v1);
+        a2 = __builtin_bit_cast(half8, v2);
+    };
+    const uint32_t ones = h ? 0u : 0x3C003C00u;
+    const f32x16 zero16 = {};
+    const float scale_t = 1.0f / th.inv_scale;
+    for (uint32_t tr = blockIdx.x * M32_WAVES + wave; tr < ntile_rows; tr += gridDim.x * M32_WAVES) {
+        const uint32_t f = tr * 32 + r32;
+        const bool valid = f < nflag;
+        const uint32_t row = flags[valid ? f : nflag - 1];
+        const uint32_t *cw = reinterpret_cast<const uint32_t *>(codes + (uint64_t)row * MF_D);
+        const uint32_t w0 = cw[0], w1 = cw[1], w2 = cw[2];
+        half8 b1, b2;
+        {
+            uint32_t w01, w23, w45, w67, w89, wab;
+            byte_quad_w(w0, w01, w23);
+            byte_quad_w(w1, w45, w67);
+            byte_quad_w(w2, w89, wab);
+            const u32x4v v1 = {w01, w23, w45, w67};
+            const u32x4v v2 = {w89, wab, ones, 0u};
+            b1 = __builtin_bit_cast(half8, v1);
+            b2 = __builtin_bit_cast(half8, v2);
+        }
+        uint32_t sad = __builtin_amdgcn_sad_u8(w0 ^ 0x80808080u, 0x7F7F7F7Fu, 0);
+        sad = __builtin_amdgcn_sad_u8(w1 ^ 0x80808080u, 0x7F7F7F7Fu, sad);
+        sad = __builtin_amdgcn_sad_u8(w2 ^ 0x80808080u, 0x7F7F7F7Fu, sad);
+        // two scores' MFMA bounds, scaled, with a margin for the fp32 band arithmetic
+        const float band_add = 2.002f * scale_t * __fmaf_rn((float)(2 * sad + MF_D), th.m1, th.m0);
+        auto min16 = [](const f32x16 &c) {
+            return min2f(min3f(min3f(min3f(c[0], c[1], c[2]), min3f(c[3], c[4], c[5]), min3f(c[6], c[7], c[8])),
+                               min3f(c[9], c[10], c[11]), min3f(c[12], c[13], c[14])),
+                         c[15]);
+        };
+        // scores of code tiles t and t + 1 (clamped: an odd count repeats the last tile), both
+        // tiles' MFMAs issued before either result is read
+        half8 a1, a2, a3, a4;
+        auto pair = [&](uint32_t t, f32x16 &c, f32x16 &d) {
+            load_a(t, a1, a2);
+            load_a(t + 1 < ntiles ? t + 1 : t, a3, a4);
+            c = __builtin_amdgcn_mfma_f32_32x32x16_f16(a1, b1, zero16, 0, 0, 0);
+            d = __builtin_amdgcn_mfma_f32_32x32x16_f16(a3, b1, zero16, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f32_32x32x16_f16(a2, b2, c, 0, 0, 0);
+            d = __builtin_amdgcn_mfma_f32_32x32x16_f16(a4, b2, d, 0, 0, 0);
+        };
+        // pass 1: the row's minimum score
+        float m = INFINITY;
+        for (uint32_t t = 0; t < ntiles; t += 2) {
+            f32x16 c, d;
+            pair(t, c, d);
+            m = min3f(m, min16(c), min16(d));
+        }
+        m = min2f(m, xor32_f32(m));
+        const float band = m + band_add * (1.0f + 1e-6f) + fabsf(m) * 1e-6f;
+        // pass 2: list the code vectors inside the band
+        auto list = [&](const f32x16 &c, uint32_t t) {
+            if (valid && min16(c) <= band) {   // rare
+#pragma unroll
+                for (int v = 0; v < 16; v++) {
+                    if (c[v] <= band) {
+                        const uint32_t cv = t * 32 + (v & 3) + 8 * (v >> 2) + 4 * h;
+                        const uint32_t slot = atomicAdd(&ncand[r32], 1u);
+                        if (slot < RC_CAP) cand[r32 * RC_CAP + slot] = cv;
+                    }
+                }
+            }
+        };
+        for (uint32_t t = 0; t < ntiles; t += 2) {
+            f32x16 c, d;
+            pair(t, c, d);
+            list(c, t);
+            if (t + 1 < ntiles) list(d, t + 1);
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        if (valid && h == 0) {
+            // the row's fp64 values, and its candidates (all K if the list overflowed)
+            double x[MF_D];
+#pragma unroll
+            for (int d = 0; d < MF_D; d++) x[d] = lut[((d < 4 ? w0 : d < 8 ? w1 : w2) >> (8 * (d % 4))) & 0xFF];
+            const uint32_t nc = ncand[r32];
+            const bool all = nc > RC_CAP;
+            const uint32_t n = all ? K : nc;
+            double d1 = INFINITY, d2 = INFINITY;
+            uint32_t k1 = 0xFFFFFFFFu;
+            for (uint32_t i = 0; i < n; i++) {
+                const uint32_t k = all ? i : cand[r32 * RC_CAP + i];
+                if (k >= K) continue;
+                const double d = ref_l2_hd(x, C64 + (uint64_t)k * MF_D, MF_D);
+                if (d < d1 || (d == d1 && k < k1)) {
+                    d2 = d1;
+                    d1 = d;
+                    k1 = k;
+                } else if (d < d2) {
+                    d2 = d;
+                }
+            }
+            if (d2 - d1 <= tie_rel * d1) {   // exact tie for the reference: the kd-tree decides
+                ties[atomicAdd(tie_cnt, 1u)] = row;   // A keeps the provisional index
+            } else {
+                const uint32_t from = A[row];   // the search's index (its terms are in the slabs when fused)
+                if (k1 != from) {
+                    if (xslab) {
+                        for (int d = 0; d < MF_D; d++) {
+                            const unsigned long long tm =
+                                plut[((d < 4 ? w0 : d < 8 ? w1 : w2) >> (8 * (d % 4))) & 0xFF];
+                            atomicAdd((unsigned long long *)&xslab[(uint64_t)d * K + k1], tm);
+                            atomicAdd((unsigned long long *)&xslab[(uint64_t)K * MF_D + (uint64_t)d * K + from], tm);
+                        }
+                        atomicAdd(&xcnt[k1], 1u);
+                        atomicAdd(&xcnt[K + from], 1u);
+                    }
+                    A[row] = k1;
+                }
+            }
+            ncand[r32] = 0;
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
+}
+
+hipError_t launch_recheck_mf32(hipStream_t s, int num_cu, const uint8_t *codes, const uint32_t *flags,
+                               const unsigned *flag_cnt, const _Float16 *cb_rows, const double *C64, uint32_t K,
+                               const double *lut64, const MfThresholds &th, double tie_rel, uint32_t *A,
+                               uint32_t *ties, unsigned *tie_cnt, uint64_t *xslab, uint32_t *xcnt,
+                               const uint64_t *plut) {
+    if (!recheck_mf32_fits(K)) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(recheck_mf32_kernel, dim3(num_cu), dim3(M32_THREADS), rc_lds_layout(K).total, s, codes, flags,
+                       flag_cnt, cb_rows, C64, K, lut64, th, tie_rel, A, ties, tie_cnt, xslab, xcnt, plut);
+    return hipGetLastError();
 }
 
 template <bool F, bool S, int U, bool TAG>
