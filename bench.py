@@ -178,14 +178,22 @@ def main():
     value = n_total * levels * args.steps / elapsed / 1e6
     ms_per_step = elapsed * 1e3 / args.steps
 
-    # Roofline of the dominant kernel, the search (assign_mfma_kernel: f16 MFMA 16x16x32 for
-    # K >= 64, assign_small_kernel: direct fp32 for K <= 32; centroid sums fused), from HIP
-    # events around the launches on the engine's stream.  Algorithmic work per launch =
-    # 3*K_l*D flop per block x blocks.
+    # Roofline of the dominant kernel, the search (assign_mf32_kernel: v_mfma_f32_32x32x16_f16
+    # for K >= 64, assign_small_kernel: expanded fp32 scores for K <= 32; centroid sums fused),
+    # from HIP events around the launches on the engine's stream.  Algorithmic work per launch
+    # = 3*K_l*D flop per block x blocks.
     flops = sum(3.0 * K * D * n_local for K, _ in launches)
     secs = sum(ms for _, ms in launches) * 1e-3
     achieved = flops / secs / 1e12
     avg_launch_s = secs / len(launches)
+    # per level (K): the largest K is the dominant launch of a quantize
+    by_k = {}
+    for K, ms in launches:
+        by_k.setdefault(K, []).append(ms)
+    per_level = {str(K): {"avg_launch_ms": round(sum(v) / len(v), 5),
+                          "TFLOPs": round(3.0 * K * D * n_local / (sum(v) / len(v) * 1e-3) / 1e12, 2),
+                          "frac": round(3.0 * K * D * n_local / (sum(v) / len(v) * 1e-3) / 1e12 / PEAK_F16_TFLOPS, 4)}
+                 for K, v in sorted(by_k.items())}
     # its HBM view: codes in (Dp bytes per block) + index out (4 bytes per block)
     assign_bytes = n_local * (((D + 3) & ~3) + 4)
     traffic, traffic_src = None, None
@@ -218,13 +226,14 @@ def main():
                                                                          args.block, D, 1 << args.bits, ipr),
                    "blocks_per_rank": n_local, "levels": levels, "parallelism": "dp%d" % world},
         "lbg_iters_per_s": round(levels * args.steps / elapsed, 3),
-        "roofline": {"bound": "mfma", "kernel": "search: qvq::assign_mfma_kernel (v_mfma_f32_16x16x32_f16, K >= 64) / "
-                                                 "qvq::assign_small_kernel (direct fp32, K <= 32), fused sums",
+        "roofline": {"bound": "mfma", "kernel": "search: qvq::assign_mf32_kernel (v_mfma_f32_32x32x16_f16, K >= 64) / "
+                                                 "qvq::assign_small_kernel (expanded fp32, K <= 32), fused sums",
                      "achieved": round(achieved, 3), "peak": PEAK_F16_TFLOPS, "unit": "TFLOP/s",
                      "frac": round(achieved / PEAK_F16_TFLOPS, 4), "traffic": traffic,
                      "traffic_source": traffic_src, "avg_launch_ms": round(avg_launch_s * 1e3, 5),
                      "launches": len(launches), "flop_per_block": "3*K*D",
                      "timing": "HIP events around one level's search per step, levels in rotation",
+                     "per_level": per_level,
                      "hbm_view": {"algorithmic_bytes_per_launch": assign_bytes,
                                   "achieved_GBps": round(assign_bytes / avg_launch_s / 1e9, 1),
                                   "peak_GBps": PEAK_HBM_GBS}},
