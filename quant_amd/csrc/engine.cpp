@@ -173,6 +173,12 @@ bool env_is(const char *name, const char *val) {
     const char *v = std::getenv(name);
     return v && std::strcmp(v, val) == 0;
 }
+// Timing ablation only (results are wrong with it): QVQ_ABL_SKIP bit 1 drops the recheck,
+// bit 2 the kd-tree launch, bit 4 the reduce -- the marginal cost of each per-level launch.
+uint32_t abl_skip() {
+    static const uint32_t v = std::getenv("QVQ_ABL_SKIP") ? (uint32_t)std::atoi(std::getenv("QVQ_ABL_SKIP")) : 0u;
+    return v;
+}
 bool use_mfma(const qvq_ctx *ctx, uint32_t K) {
     return ctx->D == MF_D && mf_can_search(K) && !env_is("QVQ_SEARCH", "valu");
 }
@@ -557,7 +563,8 @@ qvq_status run_level(qvq_ctx *ctx, uint32_t K, int slot, bool sums_out, const do
         return v ? (uint32_t)std::atoi(v) : 512u;
     }();
     static const bool rc_mf32 = !env_is("QVQ_RECHECK", "fp32");
-    if (rc_mf32 && K >= rc_min_k && use_mfma(ctx, K) && recheck_mf32_fits(K)) {
+    if (abl_skip() & 1) {
+    } else if (rc_mf32 && K >= rc_min_k && use_mfma(ctx, K) && recheck_mf32_fits(K)) {
         HIPCHK(launch_recheck_mf32(ctx->stream, ctx->num_cu, ctx->d_codes, ctx->d_flags, &cnt[0], ctx->d_rows,
                                    ctx->d_C64_split, K, ctx->d_lut64, ctx->mf_th, 1e-12, ctx->d_A, ctx->d_ties,
                                    &cnt[1], xslab, xcnt, ctx->d_plut));
@@ -577,7 +584,8 @@ qvq_status run_level(qvq_ctx *ctx, uint32_t K, int slot, bool sums_out, const do
     build_tree(ctx, hC, K, slot & 1, kd);
     ctx->tm.wait_ms[slot] = std::chrono::duration<double, std::milli>(tw1 - tw0).count();
     ctx->tm.tree_ms[slot] = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tw1).count();
-    if (kd.depth > 0) {
+    if (abl_skip() & 2) {
+    } else if (kd.depth > 0) {
         HIPCHK(launch_kd_resolve(ctx->stream, ctx->d_codes, ctx->Dp, ctx->D, ctx->d_ties, &cnt[1], ctx->d_C64_split,
                                  K, ctx->d_lut64, kd, ctx->d_A, xslab, xcnt, ctx->d_plut));
     } else {   // ties answered on the host
@@ -868,8 +876,9 @@ QVQ_API qvq_status qvq_lbg(qvq_ctx *ctx, uint32_t bits, double eps, double *code
         if ((st = run_level(ctx, K, slot, true, ctx->h_cb, ctx->seq)) != QVQ_OK) return st;
         const bool split = lvl < bits;
         {
-            HIPCHK(launch_reduce(ctx->stream, ctx->d_part, ctx->d_part_cnt, ctx->nslabs, ctx->nsub, K, ctx->D,
-                                 ctx->d_sums));
+            if (!(abl_skip() & 4))
+                HIPCHK(launch_reduce(ctx->stream, ctx->d_part, ctx->d_part_cnt, ctx->nslabs, ctx->nsub, K, ctx->D,
+                                     ctx->d_sums));
             if ((st = all_reduce_sums(ctx, K)) != QVQ_OK) return st;
             HIPCHK(finalize(K, split));
         }

@@ -16,6 +16,7 @@
 
 #include "common.hpp"
 #include "mfma_util.hpp"
+#include "kd_walk.hpp"
 
 namespace qvq {
 
@@ -65,6 +66,7 @@ bool mf_can_search(uint32_t K) { return mf_lds_layout(K, false, false).total <= 
 
 typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
 
 // Per-run sums over consecutive lanes with equal key (lanes hold consecutive rows): plain
 // prefix sums, then each run's last lane takes prefix[last] - prefix[first - 1].  The
@@ -538,12 +540,17 @@ __global__ __launch_bounds__(MF_THREADS) void assign_small_kernel(
     // is at most 2 sum_d |u_d - 127| + D (v_sad_u8 of the u = b ^ 0x80 bytes against 127).
     auto process = [&](const uint32_t (&w)[4][3], uint64_t r0) {
         // four rows at once: each code vector's terms are loaded once (scalar) for all four,
-        // and the four score chains are independent
-        float x[4][MF_D];
+        // and the four score chains are independent.  From SK = 32 rows go in pairs through
+        // v_pk_fma_f32 (two fp32 FMAs per lane and instruction, each rounded as fmaf: the
+        // scores are the scalar chain's bit for bit): K = 32 81 -> 75 us at C3; below it the
+        // per-row sums dominate and the packed form measured 2-14 % slower (profiles/r02h).
+        constexpr bool PK = SK >= 32;
+        f32x2 x[2][MF_D];
 #pragma unroll
-        for (int r = 0; r < 4; r++)
+        for (int p = 0; p < 2; p++)
 #pragma unroll
-            for (int d = 0; d < MF_D; d++) x[r][d] = byte_w(w[r][d / 4], d % 4);
+            for (int d = 0; d < MF_D; d++)
+                x[p][d] = f32x2{byte_w(w[2 * p][d / 4], d % 4), byte_w(w[2 * p + 1][d / 4], d % 4)};
         float r1[4], r2[4];
         uint32_t idx[4];
 #pragma unroll
@@ -562,13 +569,25 @@ __global__ __launch_bounds__(MF_THREADS) void assign_small_kernel(
 #pragma unroll
             for (int d = 0; d <= MF_D; d++) cr[d] = cj[d];
 #pragma unroll
-            for (int r = 0; r < 4; r++) {
-                float s = cr[MF_D];
+            for (int p = 0; p < 2; p++) {
+                f32x2 s = f32x2{cr[MF_D], cr[MF_D]};
+                if (PK) {
 #pragma unroll
-                for (int d = 0; d < MF_D; d++) s = __fmaf_rn(x[r][d], cr[d], s);
-                r2[r] = med3f(r1[r], r2[r], s);
-                idx[r] = s < r1[r] ? (uint32_t)j : idx[r];
-                r1[r] = min2f(r1[r], s);
+                    for (int d = 0; d < MF_D; d++) s = __builtin_elementwise_fma(x[p][d], f32x2{cr[d], cr[d]}, s);
+                } else {
+#pragma unroll
+                    for (int d = 0; d < MF_D; d++) {
+                        s.x = __fmaf_rn(x[p][d].x, cr[d], s.x);
+                        s.y = __fmaf_rn(x[p][d].y, cr[d], s.y);
+                    }
+                }
+#pragma unroll
+                for (int h = 0; h < 2; h++) {
+                    const int r = 2 * p + h;
+                    r2[r] = med3f(r1[r], r2[r], s[h]);
+                    idx[r] = s[h] < r1[r] ? (uint32_t)j : idx[r];
+                    r1[r] = min2f(r1[r], s[h]);
+                }
             }
         }
 #pragma unroll
@@ -876,45 +895,6 @@ __device__ inline float d32_row(const float *__restrict__ xr, const float *__res
     return acc;   // padding components are 0 in both x and c
 }
 
-// ref_l2_hd for D = N (12) against a code vector in global memory: the row's N/2 16-byte
-// loads are issued together (the generic loop waits for each group of four), then the
-// reference's order: per group of four (e1^2 + e2^2) + (e0^2 + e3^2), groups added in turn.
-template <int N>
-struct RowN {
-    double2 v[N / 2];
-};
-template <int N>
-__device__ inline RowN<N> load_row(const double *c) {
-    RowN<N> r;
-    const double2 *p = reinterpret_cast<const double2 *>(c);
-#pragma unroll
-    for (int i = 0; i < N / 2; i++) r.v[i] = p[i];
-    return r;
-}
-template <int N>
-__device__ inline double ref_l2_n(const double *a, const RowN<N> &c) {
-    double r = 0;
-#pragma unroll
-    for (int g = 0; g < N / 4; g++) {
-        const double e0 = a[4 * g] - c.v[2 * g].x, e1 = a[4 * g + 1] - c.v[2 * g].y;
-        const double e2 = a[4 * g + 2] - c.v[2 * g + 1].x, e3 = a[4 * g + 3] - c.v[2 * g + 1].y;
-        r += (e1 * e1 + e2 * e2) + (e0 * e0 + e3 * e3);
-    }
-    return r;
-}
-// fp64 reference distance of row a (LDS) to code vector k of C64 (global), any D
-__device__ inline double ref_l2_cv(const double *a, const double *C64, uint32_t k, uint32_t D) {
-    if (D == 12) return ref_l2_n<12>(a, load_row<12>(C64 + (uint64_t)k * 12));
-    return ref_l2_hd(a, C64 + (uint64_t)k * D, (int)D);   // (a D = 48 row in registers costs the recheck occupancy)
-}
-
-// LDS written by some lanes of a wave and then read by others: order the accesses.
-__device__ inline void wave_lds_sync() {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-}
-
 // LDS: byte LUT (256 doubles) | per wave the fp64 row and the fp32 row | staged fp32 codebook.
 constexpr size_t RECHECK_LDS_BASE = 256 * 8 + (size_t)RECHECK_WAVES * 64 * 12;
 
@@ -1077,187 +1057,13 @@ hipError_t launch_recheck(hipStream_t s, int num_cu, const uint8_t *codes, uint3
     return hipGetLastError();
 }
 
-// kd_nearest_flat with the leaf scan spread over the wave: every lane runs the same
-// descent (uniform values), lane i takes leaf point i, and the leaf's winner is the first
-// point in leaf order with the smallest distance below the leaf-entry worst -- what the
-// sequential strict-'<' scan picks.  Leaves hold at most 10 points (< 64 lanes).  pv holds
-// every point's distance in vind order; subtrees none of whose points is below best are
-// skipped (same result).
-__device__ uint32_t kd_nearest_wave(const double *q, uint32_t D, const KdView &t, const double *pv, double *sd,
-                                    int32_t *sn, double *dl, int lane) {
-    double distsq = 0;   // dl: per-dimension cell distances (LDS, uniform across lanes)
-    for (uint32_t d = 0; d < D; d++) {
-        const double x = q[d];
-        dl[d] = 0;
-        if (x < t.lo[d]) {
-            dl[d] = (x - t.lo[d]) * (x - t.lo[d]);
-            distsq += dl[d];
-        }
-        if (x > t.hi[d]) {
-            dl[d] = (x - t.hi[d]) * (x - t.hi[d]);
-            distsq += dl[d];
-        }
-    }
-    double best = 1.7976931348623157e308;
-    uint32_t best_idx = 0;
-    int sp = 0;
-    sd[0] = distsq;
-    sn[0] = 0;
-    while (sp >= 0) {
-        const int32_t node = sn[sp] >> 2, phase = sn[sp] & 3;
-        const KdNodeDev n = t.nodes[node];
-        // A subtree none of whose points is below best cannot change best (updates need
-        // dist < worst <= best) and its walk has no other effect: skip it.  Its points are
-        // vind[first, b), so the test is a range minimum of pv.
-        if (phase == 0 && n.child1 >= 0 && best < 1.7976931348623157e308) {
-            double m = INFINITY;
-            for (int32_t j = kd_first(n) + lane; j < n.b; j += 64) m = fmin(m, pv[j]);
-            m = wave_min_f64<4>(m);
-            if (m >= best) {
-                sp--;
-                continue;
-            }
-        }
-        if (n.child1 < 0) {
-            const double worst = best;
-            const int32_t cnt = n.b - n.a;
-            double dist = INFINITY;
-            if (lane < cnt) {
-                const double dd = pv[n.a + lane];   // ref_l2_hd(q, point vind[n.a + lane])
-                if (dd < worst) dist = dd;
-            }
-            // leaves hold <= 10 points: lanes 0..15 suffice; the winner is the lowest lane
-            // with the minimum
-            const double m = wave_min_f64<1>(dist);
-            if (m < worst) {
-                const uint64_t hit = __ballot(dist == m);
-                best = m;
-                best_idx = t.vind[n.a + __ffsll((unsigned long long)hit) - 1];
-            }
-            sp--;
-            continue;
-        }
-        const int f = kd_feat(n);
-        const double val = q[f];
-        const double diff1 = val - n.lo, diff2 = val - n.hi;
-        const bool left_first = (diff1 + diff2) < 0;
-        if (phase == 0) {
-            sn[sp] = node << 2 | 1;
-            sd[sp + 1] = sd[sp];
-            sn[sp + 1] = (left_first ? n.child1 : n.child2) << 2;
-            sp++;
-            continue;
-        }
-        if (phase == 1) {
-            const double cut_dist = left_first ? (val - n.hi) * (val - n.hi) : (val - n.lo) * (val - n.lo);
-            const double dst = dl[f];
-            const double m2 = (sd[sp] - dst) + cut_dist;
-            dl[f] = cut_dist;
-            sd[sp] = dst;
-            sn[sp] = node << 2 | 2;
-            if (m2 <= best) {
-                sd[sp + 1] = m2;
-                sn[sp + 1] = (left_first ? n.child2 : n.child1) << 2;
-                sp++;
-                continue;
-            }
-        }
-        dl[f] = sd[sp];
-        sp--;
-    }
-    return best_idx;
-}
-
-// Exact ties listed by the recheck, answered by the reference kd-tree traversal
-// (kd_nearest_flat).  The tree image (kd.lo .. ) lives in mapped pinned host memory and is
-// staged into LDS by each block that has tie rows; one lane per wave walks it.
-constexpr int KDR_MAX_WAVES = 16;
-constexpr int KDR_BLOCKS = 16;
-
-// LDS: per wave the row, cell distances, stack and the K point distances; plus the tree.
-static size_t kd_wave_bytes(const KdView &kd, uint32_t K) {
-    return 128 * 8 + (((size_t)kd.depth * KD_FRAME_BYTES + 7) & ~(size_t)7) + (size_t)K * 8;
-}
-static size_t kd_tree_bytes(const KdView &kd) { return ((size_t)kd.bytes + 7) & ~(size_t)7; }
-static int kd_waves(const KdView &kd, uint32_t K) {
-    const size_t wb = kd_wave_bytes(kd, K), tb = kd_tree_bytes(kd);
-    if (tb + wb > RECHECK_LDS) return 0;
-    return (int)std::min<size_t>(KDR_MAX_WAVES, (RECHECK_LDS - tb) / wb);
-}
+static int kd_waves(const KdView &kd, uint32_t K) { return kd_waves_within(kd, K, RECHECK_LDS); }
 
 bool kd_resolve_fits(const KdView &kd, uint32_t K) { return kd.depth > 0 && kd_waves(kd, K) > 0; }
 
-__global__ __launch_bounds__(KDR_MAX_WAVES * 64) void kd_resolve_kernel(
-    const uint8_t *__restrict__ codes, uint32_t Dp, uint32_t D, const uint32_t *__restrict__ ties,
-    const unsigned *__restrict__ tie_cnt, const double *__restrict__ C64, uint32_t K,
-    const double *__restrict__ lut64, KdView kd, uint32_t *__restrict__ A, uint64_t *__restrict__ xslab,
-    uint32_t *__restrict__ xcnt, const uint64_t *__restrict__ plut) {
+__global__ __launch_bounds__(KDR_MAX_WAVES * 64) void kd_resolve_kernel(KdArgs a, const unsigned *__restrict__ tie_cnt) {
     extern __shared__ __attribute__((aligned(16))) double ksm[];
-    const int W = blockDim.x / 64;
-    const int Z = kd.depth;
-    const unsigned nt = *tie_cnt;
-    if (blockIdx.x * W >= nt) return;
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    double *tr = ksm;   // tree image
-    double *wb = ksm + ((size_t)kd.bytes + 7) / 8 + (size_t)wave * (128 + ((size_t)Z * KD_FRAME_BYTES + 7) / 8 + K);
-    double *xs = wb, *dl = wb + 64;
-    double *sd = wb + 128;
-    int32_t *sn = reinterpret_cast<int32_t *>(sd + Z);
-    double *pv = wb + 128 + ((size_t)Z * KD_FRAME_BYTES + 7) / 8;   // [K] distances in vind order
-    {   // stage the tree image: 16-byte loads, eight in flight per lane (one round trip over
-        // PCIe when the image is read in place from mapped host memory)
-        const uint4 *src = reinterpret_cast<const uint4 *>(kd.lo);
-        uint4 *dst = reinterpret_cast<uint4 *>(tr);
-        const uint32_t n16 = kd.bytes / 16;
-        constexpr int U = 8;
-        for (uint32_t i0 = threadIdx.x; i0 < n16; i0 += U * blockDim.x) {
-            uint4 v[U];
-#pragma unroll
-            for (int u = 0; u < U; u++)
-                if (i0 + u * blockDim.x < n16) v[u] = src[i0 + u * blockDim.x];
-#pragma unroll
-            for (int u = 0; u < U; u++)
-                if (i0 + u * blockDim.x < n16) dst[i0 + u * blockDim.x] = v[u];
-        }
-        const uint32_t tail = (kd.bytes & 15) / 4;   // the image is a whole number of dwords
-        if (threadIdx.x < tail)
-            reinterpret_cast<uint32_t *>(tr)[n16 * 4 + threadIdx.x] =
-                reinterpret_cast<const uint32_t *>(kd.lo)[n16 * 4 + threadIdx.x];
-    }
-    KdView kv = kd;
-    kv.lo = tr;
-    kv.hi = tr + D;
-    kv.nodes = reinterpret_cast<const KdNodeDev *>(tr + 2 * D);
-    kv.vind = reinterpret_cast<const uint32_t *>(kv.nodes + kd.n_nodes);
-    __syncthreads();
-    for (unsigned f = blockIdx.x * W + wave; f < nt; f += gridDim.x * W) {
-        const uint32_t row = ties[f];
-        if (lane < (int)D) xs[lane] = lut64[codes[(uint64_t)row * Dp + lane]];
-        wave_lds_sync();
-        if (D == 12) {   // four points per lane in flight (their 24 loads together)
-            for (uint32_t j0 = lane; j0 < K; j0 += 4 * 64) {
-                RowN<12> c[4];
-#pragma unroll
-                for (int u = 0; u < 4; u++) {
-                    const uint32_t j = j0 + 64 * u;
-                    c[u] = load_row<12>(C64 + (uint64_t)kv.vind[j < K ? j : j0] * 12);
-                }
-#pragma unroll
-                for (int u = 0; u < 4; u++)
-                    if (j0 + 64 * u < K) pv[j0 + 64 * u] = ref_l2_n<12>(xs, c[u]);
-            }
-        } else {
-            for (uint32_t j = lane; j < K; j += 64) pv[j] = ref_l2_cv(xs, C64, kv.vind[j], D);
-        }
-        wave_lds_sync();
-        const uint32_t k = kd_nearest_wave(xs, D, kv, pv, sd, sn, dl, lane);
-        const uint32_t from = __builtin_amdgcn_readfirstlane(A[row]);   // the search's index
-        if (k != from) {
-            if (xslab) move_row_terms(codes, Dp, D, row, from, k, K, xslab, xcnt, plut, lane);
-            if (lane == 0) A[row] = k;
-        }
-        wave_lds_sync();
-    }
+    kd_resolve_block(a, *tie_cnt, blockIdx.x, gridDim.x, blockDim.x / 64, ksm);
 }
 
 hipError_t launch_kd_resolve(hipStream_t s, const uint8_t *codes, uint32_t Dp, uint32_t D, const uint32_t *ties,
@@ -1266,8 +1072,8 @@ hipError_t launch_kd_resolve(hipStream_t s, const uint8_t *codes, uint32_t Dp, u
     const int W = kd.depth > 0 ? kd_waves(kd, K) : 0;
     if (W == 0) return hipErrorInvalidValue;
     const size_t lds = kd_tree_bytes(kd) + (size_t)W * kd_wave_bytes(kd, K);
-    hipLaunchKernelGGL(kd_resolve_kernel, dim3(KDR_BLOCKS), dim3(64 * W), lds, s, codes, Dp, D, ties, tie_cnt, C64,
-                       K, lut64, kd, A, xslab, xcnt, plut);
+    const KdArgs a{codes, Dp, D, ties, C64, K, lut64, kd, A, xslab, xcnt, plut};
+    hipLaunchKernelGGL(kd_resolve_kernel, dim3(KDR_BLOCKS), dim3(64 * W), lds, s, a, tie_cnt);
     return hipGetLastError();
 }
 
