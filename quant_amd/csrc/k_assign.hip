@@ -1073,7 +1073,9 @@ hipError_t launch_kd_resolve(hipStream_t s, const uint8_t *codes, uint32_t Dp, u
     if (W == 0) return hipErrorInvalidValue;
     const size_t lds = kd_tree_bytes(kd) + (size_t)W * kd_wave_bytes(kd, K);
     const KdArgs a{codes, Dp, D, ties, C64, K, lut64, kd, A, xslab, xcnt, plut};
-    hipLaunchKernelGGL(kd_resolve_kernel, dim3(KDR_BLOCKS), dim3(64 * W), lds, s, a, tie_cnt);
+    static const int blocks = std::getenv("QVQ_KDR_BLOCKS") ? std::max(1, std::atoi(std::getenv("QVQ_KDR_BLOCKS")))
+                                                             : KDR_BLOCKS;   // ablation
+    hipLaunchKernelGGL(kd_resolve_kernel, dim3(blocks), dim3(64 * W), lds, s, a, tie_cnt);
     return hipGetLastError();
 }
 
