@@ -1116,7 +1116,7 @@ QVQ_API qvq_status qvq_get_timings(const qvq_ctx *ctx, qvq_timings *out) {
 
 QVQ_API qvq_status qvq_host_kdtree_nn(const double *C, uint32_t K, uint32_t dim, const double *Q, uint64_t nq,
                                       uint32_t *out) {
-    if (!C || !Q || !out || K == 0 || dim == 0) return QVQ_EINVAL;
+    if (!C || !Q || !out || K == 0 || dim == 0 || dim > 64) return QVQ_EINVAL;
     RefKDTree tree(C, K, (int)dim);
     for (uint64_t i = 0; i < nq; i++) out[i] = tree.nearest(Q + i * dim);
     return QVQ_OK;

@@ -7,11 +7,47 @@
 
 #include <algorithm>
 #include <limits>
+#include <memory>
 
 namespace qvq {
 
 
 double ref_l2(const double *a, const double *b, int dim) { return ref_l2_hd(a, b, dim); }
+
+namespace {
+constexpr int KD_MAX_DIM = 64;
+
+// children's boxes per tree level, [2][KD_MAX_DIM] each: allocated on first use and kept
+// (duplicated points make degenerate trees hundreds of levels deep)
+Box *level_boxes(int level) {
+    static thread_local std::vector<std::unique_ptr<Box[]>> levels;
+    while ((int)levels.size() <= level) levels.emplace_back(new Box[2 * KD_MAX_DIM]);
+    return levels[level].get();
+}
+
+// Per-dimension minima and maxima over the rows ind[0..count) of a row-major point set (the
+// inner loop over a row's contiguous coordinates vectorises; built for AVX2 and baseline
+// x86-64, picked at load time).  Exact min / max, so any instruction set gives the same values.
+template <int DIM>
+inline void rows_min_max_t(const double *pts, const size_t *ind, size_t count, int dim, double *mn, double *mx) {
+    const int D = DIM ? DIM : dim;
+    const double *p0 = pts + ind[0] * (size_t)D;
+    for (int d = 0; d < D; d++) mn[d] = mx[d] = p0[d];
+    for (size_t i = 1; i < count; i++) {
+        const double *p = pts + ind[i] * (size_t)D;
+        for (int d = 0; d < D; d++) {
+            mn[d] = p[d] < mn[d] ? p[d] : mn[d];
+            mx[d] = p[d] > mx[d] ? p[d] : mx[d];
+        }
+    }
+}
+__attribute__((target_clones("avx2", "default"))) void rows_min_max(const double *pts, const size_t *ind,
+                                                                     size_t count, int dim, double *mn, double *mx) {
+    if (dim == 48) rows_min_max_t<48>(pts, ind, count, dim, mn, mx);
+    else if (dim == 12) rows_min_max_t<12>(pts, ind, count, dim, mn, mx);
+    else rows_min_max_t<0>(pts, ind, count, dim, mn, mx);
+}
+}  // namespace
 
 RefKDTree::RefKDTree(const double *pts, size_t K, int dim) : pts_(pts), dim_(dim), K_(K) {
     static thread_local std::vector<double> cols;   // reused: a fresh 1.5 MB buffer per level page-faults
@@ -41,7 +77,7 @@ RefKDTree::RefKDTree(const double *pts, size_t K, int dim) : pts_(pts), dim_(dim
     }
     nodes_.reserve(2 * (K / 5 + 1));
     std::vector<Box> box(root_bbox_);
-    divide(0, K, box, 1, nodes_, depth_);
+    divide(0, K, box.data(), 1, nodes_, depth_);
     flat_nodes_.resize(nodes_.size());
     flat_vind_.resize(K);
     flat_box_.resize(2 * (size_t)dim);
@@ -89,7 +125,7 @@ void RefKDTree::plane_split(size_t *ind, size_t count, int cutfeat, double cutva
 }
 
 void RefKDTree::middle_split(size_t *ind, size_t count, size_t &index, int &cutfeat, double &cutval,
-                             const std::vector<Box> &bbox) {
+                             const Box *bbox) {
     const double EPS = 0.00001;
     double max_span = bbox[0].high - bbox[0].low;
     for (int i = 1; i < dim_; i++) max_span = std::max(max_span, bbox[i].high - bbox[i].low);
@@ -105,15 +141,7 @@ void RefKDTree::middle_split(size_t *ind, size_t count, size_t &index, int &cutf
         // path keeps the root's span): one row-major pass over the node's points gives all
         // of them -- each point's contiguous row once, instead of nq column gathers
         double mn[64], mx[64];
-        const double *p0 = pts_ + ind[0] * (size_t)dim_;
-        for (int d = 0; d < dim_; d++) mn[d] = mx[d] = p0[d];
-        for (size_t i = 1; i < count; i++) {
-            const double *p = pts_ + ind[i] * (size_t)dim_;
-            for (int d = 0; d < dim_; d++) {
-                mn[d] = p[d] < mn[d] ? p[d] : mn[d];
-                mx[d] = p[d] > mx[d] ? p[d] : mx[d];
-            }
-        }
+        rows_min_max(pts_, ind, count, dim_, mn, mx);
         for (int j = 0; j < nq; j++) {
             qmn[j] = mn[q[j]];
             qmx[j] = mx[q[j]];
@@ -143,8 +171,7 @@ void RefKDTree::middle_split(size_t *ind, size_t count, size_t &index, int &cutf
 }
 
 // bbox is in/out: the caller's cell box on entry, the node's actual point box on exit.
-int RefKDTree::divide(size_t left, size_t right, std::vector<Box> &bbox, int level, std::vector<Node> &nodes,
-                      int &depth) {
+int RefKDTree::divide(size_t left, size_t right, Box *bbox, int level, std::vector<Node> &nodes, int &depth) {
     const int me = (int)nodes.size();
     depth = std::max(depth, level);
     nodes.push_back(Node());
@@ -155,15 +182,7 @@ int RefKDTree::divide(size_t left, size_t right, std::vector<Box> &bbox, int lev
         n.right = right;
         n.child1 = n.child2 = -1;
         double mn[64], mx[64];
-        const double *p0 = pts_ + vind_[left] * (size_t)dim_;
-        for (int d = 0; d < dim_; d++) mn[d] = mx[d] = p0[d];
-        for (size_t k = left + 1; k < right; k++) {   // row-major: one point's coordinates are contiguous
-            const double *p = pts_ + vind_[k] * (size_t)dim_;
-            for (int d = 0; d < dim_; d++) {
-                mn[d] = p[d] < mn[d] ? p[d] : mn[d];
-                mx[d] = p[d] > mx[d] ? p[d] : mx[d];
-            }
-        }
+        rows_min_max(pts_, vind_.data() + left, right - left, dim_, mn, mx);   // row-major: a point's coordinates are contiguous
         for (int d = 0; d < dim_; d++) {
             bbox[d].low = mn[d];
             bbox[d].high = mx[d];
@@ -174,7 +193,10 @@ int RefKDTree::divide(size_t left, size_t right, std::vector<Box> &bbox, int lev
     int cutfeat;
     double cutval;
     middle_split(vind_.data() + left, right - left, idx, cutfeat, cutval, bbox);
-    std::vector<Box> lb(bbox), rb(bbox);
+    // children's boxes (a vector per node cost two heap allocations each)
+    Box *lb = level_boxes(level), *rb = lb + dim_;
+    std::copy(bbox, bbox + dim_, lb);
+    std::copy(bbox, bbox + dim_, rb);
     lb[cutfeat].high = cutval;
     rb[cutfeat].low = cutval;
     const int c1 = divide(left, left + idx, lb, level + 1, nodes, depth);

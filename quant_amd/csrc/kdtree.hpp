@@ -19,6 +19,8 @@ namespace qvq {
 // Squared L2 in the reference build's order (kdtree_dev.hpp, ref_l2_hd).
 double ref_l2(const double *a, const double *b, int dim);
 
+struct Box { double low, high; };
+
 class RefKDTree {
 public:
     // pts: K x dim, row-major, borrowed for the lifetime of the tree.
@@ -32,7 +34,6 @@ public:
     void flatten(KdNodeDev *nodes, uint32_t *vind, double *lo, double *hi) const;
 
 private:
-    struct Box { double low, high; };
     struct Node {
         bool leaf;
         size_t left, right;      // the node's points: vind[left, right)
@@ -44,9 +45,9 @@ private:
     // those reads in cache (row-major, every read of a 48-D codebook was a cache miss)
     double pt(size_t i, int d) const { return cols_[(size_t)d * K_ + i]; }
     double ptr(size_t i, int d) const { return pts_[i * (size_t)dim_ + d]; }   // row-major
-    int divide(size_t left, size_t right, std::vector<Box> &bbox, int level, std::vector<Node> &nodes, int &depth);
-    void middle_split(size_t *ind, size_t count, size_t &index, int &cutfeat, double &cutval,
-                      const std::vector<Box> &bbox);
+    // bbox: the node's cell box (dim entries); children's boxes live in boxes_ at their level
+    int divide(size_t left, size_t right, Box *bbox, int level, std::vector<Node> &nodes, int &depth);
+    void middle_split(size_t *ind, size_t count, size_t &index, int &cutfeat, double &cutval, const Box *bbox);
     void plane_split(size_t *ind, size_t count, int cutfeat, double cutval, size_t &lim1, size_t &lim2);
     void min_max(const size_t *ind, size_t count, int e, double &mn, double &mx) const;
     const double *pts_;
