@@ -876,7 +876,7 @@ __host__ __device__ inline uint32_t recheck_stride(uint32_t D) { return D | 1u; 
 
 // LDS row stride in floats: Dp, or Dp + 4 so that it is 4 mod 8 dwords (16-lane b128 reads
 // of 16 consecutive rows then cover all 64 banks once).
-__host__ __device__ inline uint32_t recheck_c32_stride(uint32_t Dp) { return (Dp % 8 == 4) ? Dp : Dp + 4; }
+__host__ __device__ constexpr uint32_t recheck_c32_stride(uint32_t Dp) { return (Dp % 8 == 4) ? Dp : Dp + 4; }
 
 template <int DT>
 __device__ inline float d32_row(const float *__restrict__ xr, const float *__restrict__ c, uint32_t Dp) {
@@ -1023,6 +1023,124 @@ __global__ __launch_bounds__(RECHECK_THREADS) void recheck_kernel(
     }
 }
 
+// The recheck for codebooks too big for LDS (C4: K = 4096, D = 48, 850 KB of fp32 rows):
+// the block's 16 waves take 16 flagged rows at a time and sweep the codebook together in
+// staged chunks of RC_CHUNK code vectors, so each chunk crosses L2 once per 16 rows instead
+// of once per row (recheck_kernel<false> streamed the whole table per row: C4 level 12 spent
+// ~450 us there).  Same per-row logic as recheck_kernel; the rare row with two candidates on
+// one lane rescans the table from global memory.
+constexpr uint32_t RC_CHUNK = 512;
+template <int DT>
+__global__ __launch_bounds__(RECHECK_THREADS) void recheck_chunked_kernel(
+    const uint8_t *__restrict__ codes, uint32_t Dp, uint32_t D, const uint32_t *__restrict__ flags,
+    const unsigned int *__restrict__ flag_cnt, const double *__restrict__ C64, const float *__restrict__ g_C32,
+    uint32_t K, const double *__restrict__ lut64, float alpha, float beta, float gamma, double tie_rel,
+    uint32_t *__restrict__ A, uint32_t *__restrict__ ties, unsigned int *__restrict__ tie_cnt,
+    uint64_t *__restrict__ xslab, uint32_t *__restrict__ xcnt, const uint64_t *__restrict__ plut) {
+    static_assert(DT > 0 && DT % 4 == 0, "a known padded width");
+    extern __shared__ __attribute__((aligned(16))) double rsm[];
+    constexpr int W = RECHECK_WAVES;
+    constexpr int NQ = DT / 4;
+    constexpr uint32_t CS = recheck_c32_stride(DT);
+    double *lut = rsm;                                     // [256] exact byte values
+    double *xs = rsm + 256;                                // [W][64] fp64 row
+    float *x32 = reinterpret_cast<float *>(xs + W * 64);   // [W][64] fp32 row (zero padded)
+    float *cch = x32 + W * 64;                             // [RC_CHUNK][CS] staged chunk
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const unsigned nflag = *flag_cnt;
+    if (nflag == 0 || blockIdx.x * W >= nflag) return;
+    for (uint32_t i = threadIdx.x; i < 256; i += RECHECK_THREADS) lut[i] = lut64[i];
+    double *xw = xs + wave * 64;
+    float *xr = x32 + wave * 64;
+    auto within = [&](float d, float m) { return d - m <= 2.f * (alpha * sqrtf(d) + beta * d) + gamma; };
+    auto d32_at = [&](const float *c, const float4 (&xq)[NQ]) {
+        const float4 *c4 = reinterpret_cast<const float4 *>(c);
+        float acc = 0.f;
+#pragma unroll
+        for (int q = 0; q < NQ; q++) {
+            const float4 cq = c4[q];
+            float e;
+            e = xq[q].x - cq.x; acc = __fmaf_rn(e, e, acc);
+            e = xq[q].y - cq.y; acc = __fmaf_rn(e, e, acc);
+            e = xq[q].z - cq.z; acc = __fmaf_rn(e, e, acc);
+            e = xq[q].w - cq.w; acc = __fmaf_rn(e, e, acc);
+        }
+        return acc;
+    };
+    // groups of W rows: block-uniform trip count (every wave joins every chunk's barriers)
+    for (uint32_t g = blockIdx.x; g * W < nflag; g += gridDim.x) {
+        const uint32_t f = g * W + wave;
+        const bool have = f < nflag;
+        const uint32_t crow = have ? flags[f] : 0;
+        const uint32_t cbyte = (have && lane < (int)D) ? codes[(uint64_t)crow * Dp + lane] : 0;
+        const uint32_t carow = have ? A[crow] : 0;
+        const double v = lane < (int)D ? lut[cbyte] : 0.0;
+        __syncthreads();   // lut staged; the previous group's reads of xw / xr are done
+        xw[lane] = v;
+        xr[lane] = (float)v;
+        wave_lds_sync();
+        float4 xq[NQ];
+#pragma unroll
+        for (int q = 0; q < NQ; q++) xq[q] = reinterpret_cast<const float4 *>(xr)[q];
+        float b1 = INFINITY, b2 = INFINITY;
+        uint32_t kb = 0;
+        for (uint32_t c0 = 0; c0 < K; c0 += RC_CHUNK) {
+            const uint32_t n = min(RC_CHUNK, K - c0);
+            __syncthreads();   // the previous chunk's reads are done
+            for (uint32_t i = threadIdx.x; i < n * NQ; i += RECHECK_THREADS) {
+                const uint32_t k = i / NQ, q = i - k * NQ;
+                reinterpret_cast<float4 *>(cch + (size_t)k * CS)[q] =
+                    reinterpret_cast<const float4 *>(g_C32 + (size_t)(c0 + k) * Dp)[q];
+            }
+            __syncthreads();
+            if (have)
+                for (uint32_t k = lane; k < n; k += 64) {
+                    const float d = d32_at(cch + (size_t)k * CS, xq);
+                    b2 = med3f(b1, b2, d);
+                    kb = d < b1 ? c0 + k : kb;
+                    b1 = min2f(b1, d);
+                }
+        }
+        if (!have) continue;
+        const float m = __uint_as_float(wave_min_u32(__float_as_uint(b1)));   // distances >= 0
+        double d1 = INFINITY, d2 = INFINITY;
+        uint32_t k1 = 0xFFFFFFFFu;
+        auto take = [&](uint32_t k) {
+            const double d = ref_l2_cv(xw, C64, k, D);
+            if (d < d1 || (d == d1 && k < k1)) {
+                d2 = d1;
+                d1 = d;
+                k1 = k;
+            } else if (d < d2) {
+                d2 = d;
+            }
+        };
+        if (within(b2, m)) {   // rare: more than one candidate on this lane
+            for (uint32_t k = lane; k < K; k += 64)
+                if (within(d32_at(g_C32 + (size_t)k * Dp, xq), m)) take(k);
+        } else if (within(b1, m)) {
+            take(kb);
+        }
+        {   // wave merge: (d1, k1) the lexicographic minimum, d2 the second-smallest candidate
+            const double m1 = wave_min_f64<4>(d1);
+            const uint32_t mk = wave_min_u32(d1 == m1 ? k1 : 0xFFFFFFFFu);
+            const bool win = d1 == m1 && k1 == mk;
+            d2 = wave_min_f64<4>(win ? d2 : d1);
+            d1 = m1;
+            k1 = mk;
+        }
+        if (d2 - d1 <= tie_rel * d1) {   // exact tie for the reference: the kd-tree decides
+            if (lane == 0) ties[atomicAdd(tie_cnt, 1u)] = crow;
+        } else {
+            const uint32_t from = __builtin_amdgcn_readfirstlane(carow);
+            if (k1 != from) {
+                if (xslab) move_row_terms(codes, Dp, D, crow, from, k1, K, xslab, xcnt, plut, lane);
+                if (lane == 0) A[crow] = k1;
+            }
+        }
+    }
+}
+
 template <bool S, int DT>
 static void launch_recheck_variant(hipStream_t s, int grid, size_t lds, const uint8_t *codes, uint32_t Dp, uint32_t D,
                                    const uint32_t *flags, const unsigned *flag_cnt, const double *C64,
@@ -1043,6 +1161,20 @@ hipError_t launch_recheck(hipStream_t s, int num_cu, const uint8_t *codes, uint3
     const size_t cb = (size_t)K * recheck_c32_stride(Dp) * 4;
     const bool staged = base + cb <= RECHECK_LDS;
     const size_t lds = base + (staged ? cb : 0);
+    // too big for LDS: the chunked sweep for the widths it is built for (QVQ_RECHECK_CHUNKED=0: A/B)
+    static const bool chunked = !(std::getenv("QVQ_RECHECK_CHUNKED") && std::getenv("QVQ_RECHECK_CHUNKED")[0] == '0');
+    if (!staged && chunked && (Dp == 12 || Dp == 48)) {
+        const size_t clds = base + (size_t)RC_CHUNK * recheck_c32_stride(Dp) * 4;
+        if (Dp == 12)
+            hipLaunchKernelGGL(recheck_chunked_kernel<12>, dim3(num_cu), dim3(RECHECK_THREADS), clds, s, codes, Dp, D,
+                               flags, flag_cnt, C64, C32, K, lut64, alpha, beta, gamma, tie_rel, A, ties, tie_cnt,
+                               xslab, xcnt, plut);
+        else
+            hipLaunchKernelGGL(recheck_chunked_kernel<48>, dim3(num_cu), dim3(RECHECK_THREADS), clds, s, codes, Dp, D,
+                               flags, flag_cnt, C64, C32, K, lut64, alpha, beta, gamma, tie_rel, A, ties, tie_cnt,
+                               xslab, xcnt, plut);
+        return hipGetLastError();
+    }
 #define QVQ_RC(SS, DT)                                                                                             \
     launch_recheck_variant<SS, DT>(s, num_cu, lds, codes, Dp, D, flags, flag_cnt, C64, C32, K, lut64, alpha, beta, \
                                    gamma, tie_rel, A, ties, tie_cnt, xslab, xcnt, plut)
