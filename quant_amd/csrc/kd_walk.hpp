@@ -174,15 +174,19 @@ struct KdArgs {
 };
 
 // Block b of nb answers ties f = b W + wave, + nb W, ... (waves >= W only help staging).
+// whole_block (W = 1): ties f = b, b + nb, ..., the block's waves compute the tie's K point
+// distances together and wave 0 walks (big K * D: one wave spent most of a tie on them).
 // Uniform per block (it contains __syncthreads); ksm: kd_tree_bytes + W kd_wave_bytes of LDS.
-__device__ inline void kd_resolve_block(const KdArgs &a, unsigned nt, uint32_t b, uint32_t nb, int W, double *ksm) {
+__device__ inline void kd_resolve_block(const KdArgs &a, unsigned nt, uint32_t b, uint32_t nb, int W, double *ksm,
+                                        bool whole_block = false) {
     if (b * (uint32_t)W >= nt) return;
     const KdView &kd = a.kd;
     const uint32_t D = a.D, K = a.K;
     const int Z = kd.depth;
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     double *tr = ksm;   // tree image
-    double *wb = ksm + ((size_t)kd.bytes + 7) / 8 + (size_t)wave * (128 + ((size_t)Z * KD_FRAME_BYTES + 7) / 8 + K);
+    double *wb = ksm + ((size_t)kd.bytes + 7) / 8 +
+                 (size_t)(whole_block ? 0 : wave) * (128 + ((size_t)Z * KD_FRAME_BYTES + 7) / 8 + K);
     double *xs = wb, *dl = wb + 64;
     double *sd = wb + 128;
     int32_t *sn = reinterpret_cast<int32_t *>(sd + Z);
@@ -213,6 +217,25 @@ __device__ inline void kd_resolve_block(const KdArgs &a, unsigned nt, uint32_t b
     kv.nodes = reinterpret_cast<const KdNodeDev *>(tr + 2 * D);
     kv.vind = reinterpret_cast<const uint32_t *>(kv.nodes + kd.n_nodes);
     __syncthreads();
+    if (whole_block) {
+        for (unsigned f = b; f < nt; f += nb) {
+            const uint32_t row = a.ties[f];
+            if (threadIdx.x < D) xs[threadIdx.x] = a.lut64[a.codes[(uint64_t)row * a.Dp + threadIdx.x]];
+            __syncthreads();
+            for (uint32_t j = threadIdx.x; j < K; j += blockDim.x) pv[j] = ref_l2_cv(xs, a.C64, kv.vind[j], D);
+            __syncthreads();
+            if (wave == 0) {
+                const uint32_t k = kd_nearest_wave(xs, D, kv, pv, sd, sn, dl, lane);
+                const uint32_t from = __builtin_amdgcn_readfirstlane(a.A[row]);
+                if (k != from) {
+                    if (a.xslab) move_row_terms(a.codes, a.Dp, D, row, from, k, K, a.xslab, a.xcnt, a.plut, lane);
+                    if (lane == 0) a.A[row] = k;
+                }
+            }
+            __syncthreads();
+        }
+        return;
+    }
     if (wave >= W) return;
     for (unsigned f = b * W + wave; f < nt; f += nb * W) {
         const uint32_t row = a.ties[f];
