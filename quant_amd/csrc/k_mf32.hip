@@ -40,7 +40,7 @@ constexpr uint32_t M32_LDS_MAX = 160 * 1024;
 struct M32Lds {
     uint32_t q, c32, sums, cnt, plut, total;
 };
-__host__ __device__ inline M32Lds m32_lds_layout(uint32_t K, bool fuse, bool staged) {
+__host__ __device__ inline M32Lds m32_lds_layout(uint32_t K, bool fuse, bool staged, uint32_t copies = 1) {
     const uint32_t Kp = (K + 31) & ~31u;
     M32Lds L;
     uint32_t o = Kp * 32;
@@ -49,9 +49,9 @@ __host__ __device__ inline M32Lds m32_lds_layout(uint32_t K, bool fuse, bool sta
     L.c32 = o;
     if (staged) o += Kp * MF_D * 4;
     L.sums = o;
-    if (fuse) o += K * MF_D * 8;
+    if (fuse) o += copies * K * MF_D * 8;
     L.cnt = o;
-    if (fuse) o += ((K + 1) & ~1u) * 4;
+    if (fuse) o += copies * ((K + 1) & ~1u) * 4;
     L.plut = o;
     if (fuse) o += 256;
     L.total = o;
@@ -116,17 +116,20 @@ __device__ inline void m32_track_tagged(float m, uint32_t keep, uint32_t u, floa
 
 // TAG: unit indices in the scores' low bits (idbits of them, idbits >= log2 of the units per
 // lane; orrel = 2^(idbits - 22) bounds twice the relative change).
+// copies > 1 (fused): every row adds its terms straight into LDS copy lane % copies of the
+// sums (runs of equal indices then meet copies instead of one address); copies = 1: the
+// wave run reduction first, then one atomic set per run.
 template <bool FUSE, bool STAGED, int U, bool TAG>
 __global__ __launch_bounds__(M32_THREADS) void assign_mf32_kernel(
     const uint8_t *__restrict__ codes, uint64_t N, const _Float16 *__restrict__ g_rows, uint32_t K,
     const float *__restrict__ g_C32, const uint64_t *__restrict__ g_plut, MfThresholds th, uint32_t idbits,
     float orrel, uint32_t *__restrict__ A, uint32_t *__restrict__ flags, unsigned *__restrict__ flag_cnt,
-    uint64_t *__restrict__ part, uint32_t *__restrict__ part_cnt) {
+    uint64_t *__restrict__ part, uint32_t *__restrict__ part_cnt, uint32_t copies) {
     static_assert(U == 4 || U == 8, "unit of 4 or 8 code vectors");
     constexpr int NU = 16 / U;   // units per lane and code tile
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
     const uint32_t Kp = (K + 31) & ~31u;
-    const M32Lds L = m32_lds_layout(K, FUSE, STAGED);
+    const M32Lds L = m32_lds_layout(K, FUSE, STAGED, copies);
     float *c32s = reinterpret_cast<float *>(lds + L.c32);
     uint64_t *sums = reinterpret_cast<uint64_t *>(lds + L.sums);   // [d][k]
     uint32_t *cnt = reinterpret_cast<uint32_t *>(lds + L.cnt);
@@ -139,8 +142,8 @@ __global__ __launch_bounds__(M32_THREADS) void assign_mf32_kernel(
         for (uint32_t i = tid; i < Kp * (MF_D / 4); i += M32_THREADS) dst[i] = src[i];
     }
     if (FUSE) {
-        for (uint32_t i = tid; i < K * MF_D; i += M32_THREADS) sums[i] = 0;
-        for (uint32_t i = tid; i < K; i += M32_THREADS) cnt[i] = 0;
+        for (uint32_t i = tid; i < copies * K * MF_D; i += M32_THREADS) sums[i] = 0;
+        for (uint32_t i = tid; i < copies * K; i += M32_THREADS) cnt[i] = 0;
         if (tid < 256) lo8[tid] = (uint8_t)(g_plut[tid] & 0xFF);
         if (blockIdx.x == 0) {   // the correction slabs G (+) and G + 1 (-), after all G others
             for (uint32_t i = tid; i < 2 * K * MF_D; i += M32_THREADS) part[(uint64_t)gridDim.x * K * MF_D + i] = 0;
@@ -322,7 +325,19 @@ __global__ __launch_bounds__(M32_THREADS) void assign_mf32_kernel(
         }
         if (FUSE) {
             // every row at its provisional index; the recheck / kd-tree move re-assigned ones
-            if (K <= th.runs_max_k) {
+            if (copies > 1) {
+                if (valid) {
+                    const uint32_t cp = (uint32_t)lane & (copies - 1);
+                    uint64_t *my = sums + (size_t)cp * K * MF_D;
+#pragma unroll
+                    for (int d = 0; d < MF_D; d++) {
+                        const uint32_t b = (own[d / 4] >> (8 * (d % 4))) & 0xFF;
+                        atomicAdd((unsigned long long *)&my[(uint32_t)d * K + rk],
+                                  (unsigned long long)((uint64_t)(b ^ 0x80u) << 32 | lo8[b]));
+                    }
+                    atomicAdd(&cnt[cp * K + rk], 1u);
+                }
+            } else if (K <= th.runs_max_k) {
                 uint32_t v[MF_D + 1];
 #pragma unroll
                 for (int d = 0; d < MF_D; d++) {
@@ -352,9 +367,17 @@ __global__ __launch_bounds__(M32_THREADS) void assign_mf32_kernel(
     if (FUSE) {
         __syncthreads();
         uint64_t *pdst = part + (uint64_t)blockIdx.x * K * MF_D;   // slab layout [d][k]
-        for (uint32_t i = tid; i < K * MF_D; i += M32_THREADS) pdst[i] = sums[i];
+        for (uint32_t i = tid; i < K * MF_D; i += M32_THREADS) {
+            uint64_t v = 0;
+            for (uint32_t c = 0; c < copies; c++) v += sums[(size_t)c * K * MF_D + i];
+            pdst[i] = v;
+        }
         uint32_t *cdst = part_cnt + (uint64_t)blockIdx.x * K;
-        for (uint32_t i = tid; i < K; i += M32_THREADS) cdst[i] = cnt[i];
+        for (uint32_t i = tid; i < K; i += M32_THREADS) {
+            uint32_t v = 0;
+            for (uint32_t c = 0; c < copies; c++) v += cnt[c * K + i];
+            cdst[i] = v;
+        }
     }
 }
 
@@ -559,9 +582,9 @@ template <bool F, bool S, int U, bool TAG>
 static void launch_mf32_variant(hipStream_t s, int grid, size_t lds, const uint8_t *codes, uint64_t N,
                                 const _Float16 *cb_rows, uint32_t K, const float *C32, const uint64_t *plut,
                                 const MfThresholds &th, uint32_t idbits, float orrel, uint32_t *A, uint32_t *flags,
-                                unsigned *flag_cnt, uint64_t *part, uint32_t *part_cnt) {
+                                unsigned *flag_cnt, uint64_t *part, uint32_t *part_cnt, uint32_t copies) {
     hipLaunchKernelGGL((assign_mf32_kernel<F, S, U, TAG>), dim3(grid), dim3(M32_THREADS), lds, s, codes, N, cb_rows,
-                       K, C32, plut, th, idbits, orrel, A, flags, flag_cnt, part, part_cnt);
+                       K, C32, plut, th, idbits, orrel, A, flags, flag_cnt, part, part_cnt, copies);
 }
 
 bool mf32_fits(uint32_t K, bool fuse) { return m32_lds_layout(K, fuse, false).total <= M32_LDS_MAX; }
@@ -572,7 +595,17 @@ hipError_t launch_assign_mf32(hipStream_t s, int grid, bool fuse, const uint8_t 
                               uint64_t *part, uint32_t *part_cnt) {
     if (!mf32_fits(K, fuse)) return hipErrorInvalidValue;
     const bool staged = m32_lds_layout(K, fuse, true).total <= M32_LDS_MAX;
-    const size_t lds = m32_lds_layout(K, fuse, staged).total;
+    // sums copies (fused, 256 <= K <= 512 by default: QVQ_SUM_COPIES_MINK / _MAXK): the most, up
+    // to 16, that fit.  C3: K = 256 / 512 -4.5 us each; K = 64 +5 us (long runs: the run
+    // reduction's one atomic set per run wins), K = 1024 has no room for a second copy.
+    static const uint32_t copies_mink =
+        std::getenv("QVQ_SUM_COPIES_MINK") ? (uint32_t)std::atoi(std::getenv("QVQ_SUM_COPIES_MINK")) : 256;
+    static const uint32_t copies_maxk =
+        std::getenv("QVQ_SUM_COPIES_MAXK") ? (uint32_t)std::atoi(std::getenv("QVQ_SUM_COPIES_MAXK")) : 512;
+    uint32_t copies = 1;
+    if (fuse && K >= copies_mink && K <= copies_maxk)
+        while (copies < 16 && m32_lds_layout(K, fuse, staged, copies * 2).total <= M32_LDS_MAX) copies *= 2;
+    const size_t lds = m32_lds_layout(K, fuse, staged, copies).total;
     // 4-code-vector units while the tile loop is short (the recompute dominates)
     static const uint32_t u4_max =
         std::getenv("QVQ_U4_MAXK") ? (uint32_t)std::atoi(std::getenv("QVQ_U4_MAXK")) : 256;
@@ -585,7 +618,7 @@ hipError_t launch_assign_mf32(hipStream_t s, int grid, bool fuse, const uint8_t 
     const float orrel = std::ldexp(1.0f, (int)idbits - 22);
     using Fn = void (*)(hipStream_t, int, size_t, const uint8_t *, uint64_t, const _Float16 *, uint32_t, const float *,
                         const uint64_t *, const MfThresholds &, uint32_t, float, uint32_t *, uint32_t *, unsigned *,
-                        uint64_t *, uint32_t *);
+                        uint64_t *, uint32_t *, uint32_t);
 #define QVQ_MF32_PICK(TG)                                                                                          \
     if (fuse) {                                                                                                    \
         if (u4) fn = staged ? launch_mf32_variant<true, true, 4, TG> : launch_mf32_variant<true, false, 4, TG>;    \
@@ -601,7 +634,7 @@ hipError_t launch_assign_mf32(hipStream_t s, int grid, bool fuse, const uint8_t 
         QVQ_MF32_PICK(false)
     }
 #undef QVQ_MF32_PICK
-    fn(s, grid, lds, codes, N, cb_rows, K, C32, plut, th, idbits, orrel, A, flags, flag_cnt, part, part_cnt);
+    fn(s, grid, lds, codes, N, cb_rows, K, C32, plut, th, idbits, orrel, A, flags, flag_cnt, part, part_cnt, copies);
     return hipGetLastError();
 }
 
