@@ -191,6 +191,12 @@ hipError_t launch_kd_resolve(hipStream_t s, const uint8_t *codes, uint32_t Dp, u
                              const KdView &kd, uint32_t *A, uint64_t *xslab, uint32_t *xcnt, const uint64_t *plut);
 hipError_t launch_update(hipStream_t s, uint32_t Dp, uint32_t G, const uint8_t *codes, uint64_t N, const uint32_t *A,
                          uint32_t K, uint32_t D, const uint64_t *plut, uint64_t *part, uint32_t *part_cnt);
+// Sums of a final assignment straight into sums [hi KD][lo KD][cnt K] (no slabs, no reduce)
+// through a counting sort of the rows by index: hist [G][K], scratch 2K + 1, idx / ks [N].
+bool sorted_sums_fits(uint32_t K);
+hipError_t launch_sorted_sums(hipStream_t s, uint32_t Dp, uint32_t G, const uint8_t *codes, uint64_t N,
+                              const uint32_t *A, uint32_t K, uint32_t D, const uint64_t *plut, uint32_t *hist,
+                              uint32_t *scratch, uint32_t *idx, uint32_t *ks, uint64_t *sums);
 // Sums of G slabs, the last nsub of them subtracted (fused path: slab G + 1 holds the terms
 // of re-assigned rows at their provisional index).
 hipError_t launch_reduce(hipStream_t s, const uint64_t *part, const uint32_t *part_cnt, uint32_t G, uint32_t nsub,

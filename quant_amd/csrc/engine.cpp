@@ -106,6 +106,7 @@ struct qvq_ctx {
     uint64_t *d_mean = nullptr;   // MEAN_COPIES x mean sums [hi D][lo D][n]: zero between quantizes (the finalize clears them)
     uint64_t out_seq = 0;         // quantizes whose results copy_out has published
     uint32_t *d_scatter = nullptr;
+    uint32_t *d_sortbuf = nullptr;   // sorted-order sums: idx [N] | ks [N]
     uint64_t scatter_bytes = 0;
     uint8_t *d_decode = nullptr;          // qvq_decode scratch (grown on demand)
     uint64_t decode_bytes = 0;
@@ -196,6 +197,7 @@ bool use_fused(const qvq_ctx *ctx, uint32_t K) {
 }
 
 void free_training(qvq_ctx *ctx) {
+    dfree(ctx->d_sortbuf);
     dfree(ctx->d_codes);
     dfree(ctx->d_A);
     dfree(ctx->d_flags);
@@ -373,17 +375,35 @@ qvq_status all_reduce_sums(qvq_ctx *ctx, uint32_t K, uint64_t *sums = nullptr, u
     return QVQ_OK;
 }
 
-// Slabs of the centroid sums under assignment d_A (no reduce).
+// Sums of a final assignment through the counting sort (k_misc.hip) for big K * D: from K * D
+// = 16384 (C4 from K = 512), where the LDS update's passes and slabs cost most
+// (QVQ_SORTED_SUMS=0: A/B).
+bool use_sorted_sums(const qvq_ctx *ctx, uint32_t K) {
+    static const bool on = !env_is("QVQ_SORTED_SUMS", "0");
+    return on && (uint64_t)K * ctx->D >= 16384 && sorted_sums_fits(K) && ctx->N <= 0xFFFFFFFFull;
+}
+
+// Centroid sums under assignment d_A: slabs in d_part (ctx->nslabs of them, for the reduce),
+// or with the sort straight into d_sums (ctx->nslabs = 0).
 qvq_status run_update_slabs(qvq_ctx *ctx, const uint32_t *d_A, uint32_t K) {
+    if (use_sorted_sums(ctx, K)) {
+        if (!ctx->d_sortbuf) HIPCHK(hipMalloc(&ctx->d_sortbuf, ctx->N * 2 * sizeof(uint32_t)));
+        HIPCHK(launch_sorted_sums(ctx->stream, ctx->Dp, ctx->G, ctx->d_codes, ctx->N, d_A, K, ctx->D, ctx->d_plut,
+                                  ctx->d_part_cnt, reinterpret_cast<uint32_t *>(ctx->d_part), ctx->d_sortbuf,
+                                  ctx->d_sortbuf + ctx->N, ctx->d_sums));
+        ctx->nslabs = 0;
+        return QVQ_OK;
+    }
     HIPCHK(launch_update(ctx->stream, ctx->Dp, ctx->G, ctx->d_codes, ctx->N, d_A, K, ctx->D, ctx->d_plut, ctx->d_part,
                          ctx->d_part_cnt));
+    ctx->nslabs = ctx->G;
     return QVQ_OK;
 }
 
 qvq_status run_update(qvq_ctx *ctx, const uint32_t *d_A, uint32_t K) {
     qvq_status st = run_update_slabs(ctx, d_A, K);
     if (st != QVQ_OK) return st;
-    HIPCHK(launch_reduce(ctx->stream, ctx->d_part, ctx->d_part_cnt, ctx->G, 0, K, ctx->D, ctx->d_sums));
+    if (ctx->nslabs) HIPCHK(launch_reduce(ctx->stream, ctx->d_part, ctx->d_part_cnt, ctx->nslabs, 0, K, ctx->D, ctx->d_sums));
     return QVQ_OK;
 }
 
@@ -876,7 +896,7 @@ QVQ_API qvq_status qvq_lbg(qvq_ctx *ctx, uint32_t bits, double eps, double *code
         if ((st = run_level(ctx, K, slot, true, ctx->h_cb, ctx->seq)) != QVQ_OK) return st;
         const bool split = lvl < bits;
         {
-            if (!(abl_skip() & 4))
+            if (!(abl_skip() & 4) && ctx->nslabs)   // nslabs 0: the sorted sums are in d_sums already
                 HIPCHK(launch_reduce(ctx->stream, ctx->d_part, ctx->d_part_cnt, ctx->nslabs, ctx->nsub, K, ctx->D,
                                      ctx->d_sums));
             if ((st = all_reduce_sums(ctx, K)) != QVQ_OK) return st;

@@ -272,6 +272,236 @@ hipError_t launch_update(hipStream_t s, uint32_t Dp, uint32_t G, const uint8_t *
     return hipErrorInvalidValue;
 }
 
+// ---------------------------------------------------------------------------------------
+// Centroid sums of a final assignment for big K * D (the non-fused levels of 4x4 blocks): a
+// counting sort of the rows by index, then every lane folds 8 consecutive rows of the order
+// (mostly one code vector) in registers, a wave sums its lanes' runs, and each run's last lane
+// adds it to sums [hi KD][lo KD][cnt K] with global atomics.  The LDS update needs one pass per KR code vectors and leaves G slabs of
+// K*D u64 for reduce_kernel (C4, K = 4096: 400 MB written and read again per level).
+// ---------------------------------------------------------------------------------------
+constexpr int SRT_THREADS = 1024;
+constexpr int SRT_UB = 8;                    // row indices in flight per thread
+constexpr uint32_t SRT_ROWS_PER_LANE = 8;    // consecutive sorted rows per lane, gathered at once
+
+// hist[g][k]: rows of block g's range with index k
+__global__ __launch_bounds__(SRT_THREADS) void sort_hist_kernel(const uint32_t *__restrict__ A, uint64_t N, uint32_t K,
+                                                                uint64_t rpg, uint32_t *__restrict__ hist) {
+    extern __shared__ uint32_t h[];
+    for (uint32_t i = threadIdx.x; i < K; i += SRT_THREADS) h[i] = 0;
+    __syncthreads();
+    const uint64_t start = (uint64_t)blockIdx.x * rpg, end = min(N, start + rpg);
+    for (uint64_t r0 = start + threadIdx.x; r0 < end; r0 += (uint64_t)SRT_UB * SRT_THREADS) {
+        uint32_t a[SRT_UB];
+#pragma unroll
+        for (int u = 0; u < SRT_UB; u++) a[u] = A[min(r0 + (uint64_t)u * SRT_THREADS, end - 1)];
+#pragma unroll
+        for (int u = 0; u < SRT_UB; u++)
+            if (r0 + (uint64_t)u * SRT_THREADS < end) atomicAdd(&h[a[u]], 1u);
+    }
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < K; i += SRT_THREADS) hist[(uint64_t)blockIdx.x * K + i] = h[i];
+}
+
+// hist[g][k] <- rows of blocks g' < g with index k; tot[k] = all rows with index k
+__global__ __launch_bounds__(256) void sort_colscan_kernel(uint32_t *__restrict__ hist, uint32_t G, uint32_t K,
+                                                           uint32_t *__restrict__ tot) {
+    const uint32_t k = blockIdx.x * 256 + threadIdx.x;
+    if (k >= K) return;
+    uint32_t s = 0;
+    constexpr uint32_t CU = 16;   // loads in flight (a dependent load per block was ~60 us)
+    for (uint32_t g0 = 0; g0 < G; g0 += CU) {
+        uint32_t v[CU];
+#pragma unroll
+        for (uint32_t u = 0; u < CU; u++) v[u] = hist[(uint64_t)min(g0 + u, G - 1) * K + k];
+#pragma unroll
+        for (uint32_t u = 0; u < CU; u++)
+            if (g0 + u < G) {
+                hist[(uint64_t)(g0 + u) * K + k] = s;
+                s += v[u];
+            }
+    }
+    tot[k] = s;
+}
+
+// koff[k] = rows with index < k (exclusive scan of tot in one block)
+__global__ __launch_bounds__(SRT_THREADS) void sort_koff_kernel(const uint32_t *__restrict__ tot, uint32_t K,
+                                                                uint32_t *__restrict__ koff) {
+    __shared__ uint32_t part[SRT_THREADS];
+    const uint32_t seg = (K + SRT_THREADS - 1) / SRT_THREADS;
+    const uint32_t b = min(K, threadIdx.x * seg), e = min(K, b + seg);
+    uint32_t s = 0;
+    for (uint32_t i = b; i < e; i++) s += tot[i];
+    part[threadIdx.x] = s;
+    __syncthreads();
+    for (int off = 1; off < SRT_THREADS; off <<= 1) {   // inclusive scan of the segment sums
+        const uint32_t v = threadIdx.x >= (uint32_t)off ? part[threadIdx.x - off] : 0u;
+        __syncthreads();
+        part[threadIdx.x] += v;
+        __syncthreads();
+    }
+    uint32_t base = part[threadIdx.x] - s;
+    for (uint32_t i = b; i < e; i++) {
+        koff[i] = base;
+        base += tot[i];
+    }
+}
+
+// idx[pos] = row, ks[pos] = its index, pos = koff[k] + hist[g][k] + rank within block g
+// (any order within a code vector: the sums are exact integers)
+__global__ __launch_bounds__(SRT_THREADS) void sort_scatter_kernel(const uint32_t *__restrict__ A, uint64_t N, uint32_t K,
+                                                                   uint64_t rpg, const uint32_t *__restrict__ hist,
+                                                                   const uint32_t *__restrict__ koff,
+                                                                   uint32_t *__restrict__ idx, uint32_t *__restrict__ ks) {
+    extern __shared__ uint32_t cur[];
+    for (uint32_t i = threadIdx.x; i < K; i += SRT_THREADS) cur[i] = koff[i] + hist[(uint64_t)blockIdx.x * K + i];
+    __syncthreads();
+    const uint64_t start = (uint64_t)blockIdx.x * rpg, end = min(N, start + rpg);
+    for (uint64_t r0 = start + threadIdx.x; r0 < end; r0 += (uint64_t)SRT_UB * SRT_THREADS) {
+        uint32_t a[SRT_UB];
+#pragma unroll
+        for (int u = 0; u < SRT_UB; u++) a[u] = A[min(r0 + (uint64_t)u * SRT_THREADS, end - 1)];
+#pragma unroll
+        for (int u = 0; u < SRT_UB; u++) {
+            const uint64_t row = r0 + (uint64_t)u * SRT_THREADS;
+            if (row < end) {
+                const uint32_t pos = atomicAdd(&cur[a[u]], 1u);
+                idx[pos] = (uint32_t)row;
+                ks[pos] = a[u];
+            }
+        }
+    }
+}
+
+template <int DP>
+__global__ __launch_bounds__(256) void sorted_sums_kernel(const uint8_t *__restrict__ codes, uint64_t N,
+                                                          const uint32_t *__restrict__ idx, const uint32_t *__restrict__ ks,
+                                                          uint32_t K, uint32_t D, const uint64_t *__restrict__ plut,
+                                                          uint64_t *__restrict__ sums) {
+    constexpr int W4 = DP / 4;
+    constexpr int B = (int)SRT_ROWS_PER_LANE;   // rows gathered together
+    __shared__ uint8_t lo8[256];
+    if (threadIdx.x < 256) lo8[threadIdx.x] = (uint8_t)(plut[threadIdx.x] & 0xFF);
+    __syncthreads();
+    const uint64_t p0 = ((uint64_t)blockIdx.x * 256 + threadIdx.x) * SRT_ROWS_PER_LANE;
+    const uint64_t p1 = min(N, p0 + SRT_ROWS_PER_LANE);   // p0 >= N: no rows (the lane still joins the wave sums)
+    const uint64_t KD = (uint64_t)K * D;
+    uint32_t acc[DP + 1];
+    uint32_t cur = 0xFFFFFFFFu;
+#pragma unroll
+    for (int i = 0; i <= DP; i++) acc[i] = 0;
+    auto flush = [&]() {   // a run ending inside the lane's rows (a code vector boundary)
+        if (acc[DP]) {
+#pragma unroll
+            for (int d = 0; d < DP; d++)
+                if ((uint32_t)d < D) {
+                    atomicAdd((unsigned long long *)&sums[(uint64_t)d * K + cur], (unsigned long long)(acc[d] >> 16));
+                    atomicAdd((unsigned long long *)&sums[KD + (uint64_t)d * K + cur],
+                              (unsigned long long)(acc[d] & 0xFFFF));
+                }
+            atomicAdd((unsigned long long *)&sums[2 * KD + cur], (unsigned long long)acc[DP]);
+        }
+#pragma unroll
+        for (int i = 0; i <= DP; i++) acc[i] = 0;
+    };
+    for (uint64_t p = p0; p < p1; p += B) {   // <= 8 rows per lane: the 16-bit fields never carry
+        uint32_t r[B], k[B], w[B][W4];
+#pragma unroll
+        for (int u = 0; u < B; u++) {
+            const uint64_t q = min(p + u, p1 - 1);
+            r[u] = idx[q];
+            k[u] = ks[q];
+        }
+#pragma unroll
+        for (int u = 0; u < B; u++) {
+            if constexpr (DP % 16 == 0) {   // 16-byte rows: vector loads
+                const uint4 *src = reinterpret_cast<const uint4 *>(codes + (uint64_t)r[u] * DP);
+#pragma unroll
+                for (int i = 0; i < W4 / 4; i++) {
+                    const uint4 v = src[i];
+                    w[u][4 * i] = v.x;
+                    w[u][4 * i + 1] = v.y;
+                    w[u][4 * i + 2] = v.z;
+                    w[u][4 * i + 3] = v.w;
+                }
+            } else {
+                const uint32_t *src = reinterpret_cast<const uint32_t *>(codes + (uint64_t)r[u] * DP);
+#pragma unroll
+                for (int i = 0; i < W4; i++) w[u][i] = src[i];
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < B; u++) {
+            if (p + u >= p1) break;
+            if (k[u] != cur) {
+                flush();
+                cur = k[u];
+            }
+#pragma unroll
+            for (int d = 0; d < DP; d++) {
+                const uint32_t b = (w[u][d / 4] >> (8 * (d % 4))) & 0xFF;
+                acc[d] += (b ^ 0x80u) << 16 | lo8[b];
+            }
+            acc[DP] += 1;
+        }
+    }
+    // The lanes' last runs: consecutive lanes mostly share a code vector (the order is sorted),
+    // so they are summed over the wave first and only each run's last lane adds to the global
+    // sums (device-scope atomics on one address serialise: a large cell's thousands of lanes
+    // cost ~400 us per level that way).  hi and lo apart (up to 512 rows per run).
+    {
+        const int lane = threadIdx.x & 63;
+        const uint32_t key = acc[DP] ? cur : 0xFFFFFFFFu;
+        const uint32_t prev = wave_prev_u32(key), next = wave_next_u32(key);
+        const bool head = lane == 0 || prev != key;
+        const uint32_t h = wave_scan_max(head ? (uint32_t)lane : 0u);
+        const int src = h == 0 ? 0 : (int)h - 1;
+        const bool tail = lane == 63 || next != key;
+        auto seg = [&](uint32_t v) {   // the run's sum on its last lane
+            const uint32_t pre = wave_scan_add(v);
+            const uint32_t before = __shfl(pre, src);
+            return pre - (h == 0 ? 0u : before);
+        };
+#pragma unroll
+        for (int d = 0; d < DP; d++) {
+            if ((uint32_t)d >= D) break;
+            const uint32_t hs = seg(acc[d] >> 16), ls = seg(acc[d] & 0xFFFF);
+            if (tail && key != 0xFFFFFFFFu) {
+                atomicAdd((unsigned long long *)&sums[(uint64_t)d * K + key], (unsigned long long)hs);
+                atomicAdd((unsigned long long *)&sums[KD + (uint64_t)d * K + key], (unsigned long long)ls);
+            }
+        }
+        const uint32_t cs = seg(acc[DP]);
+        if (tail && key != 0xFFFFFFFFu) atomicAdd((unsigned long long *)&sums[2 * KD + key], (unsigned long long)cs);
+    }
+}
+
+bool sorted_sums_fits(uint32_t K) { return (size_t)K * 4 <= 64 * 1024; }
+
+hipError_t launch_sorted_sums(hipStream_t s, uint32_t Dp, uint32_t G, const uint8_t *codes, uint64_t N,
+                              const uint32_t *A, uint32_t K, uint32_t D, const uint64_t *plut, uint32_t *hist,
+                              uint32_t *scratch, uint32_t *idx, uint32_t *ks, uint64_t *sums) {
+    if (!sorted_sums_fits(K) || N == 0 || N > 0xFFFFFFFFull) return hipErrorInvalidValue;
+    uint32_t *tot = scratch, *koff = scratch + K;
+    const uint64_t rpg = (N + G - 1) / G;
+    hipError_t e = hipMemsetAsync(sums, 0, (2 * (size_t)K * D + K) * 8, s);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(sort_hist_kernel, dim3(G), dim3(SRT_THREADS), K * 4, s, A, N, K, rpg, hist);
+    hipLaunchKernelGGL(sort_colscan_kernel, dim3((K + 255) / 256), dim3(256), 0, s, hist, G, K, tot);
+    hipLaunchKernelGGL(sort_koff_kernel, dim3(1), dim3(SRT_THREADS), 0, s, tot, K, koff);
+    hipLaunchKernelGGL(sort_scatter_kernel, dim3(G), dim3(SRT_THREADS), K * 4, s, A, N, K, rpg, hist, koff, idx, ks);
+    const uint64_t lanes = (N + SRT_ROWS_PER_LANE - 1) / SRT_ROWS_PER_LANE;
+    const uint32_t grid = (uint32_t)((lanes + 255) / 256);
+    switch (Dp) {
+#define X(DPV)                                                                                                     \
+    case DPV:                                                                                                      \
+        hipLaunchKernelGGL(sorted_sums_kernel<DPV>, dim3(grid), dim3(256), 0, s, codes, N, idx, ks, K, D, plut, sums); \
+        return hipGetLastError();
+        QVQ_FOR_EACH_DP(X)
+#undef X
+    }
+    return hipErrorInvalidValue;
+}
+
 // Column reduce of G slabs into sums (layout in the file header).  A workgroup owns 64
 // columns; its 16 waves each add every 16th slab, then combine through LDS.  The last nsub
 // slabs are subtracted (hi and lo separately: the corrections of re-assigned rows, whose
