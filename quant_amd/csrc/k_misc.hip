@@ -282,6 +282,7 @@ hipError_t launch_update(hipStream_t s, uint32_t Dp, uint32_t G, const uint8_t *
 constexpr int SRT_THREADS = 1024;
 constexpr int SRT_UB = 8;                    // row indices in flight per thread
 constexpr uint32_t SRT_ROWS_PER_LANE = 8;    // consecutive sorted rows per lane, gathered at once
+constexpr uint32_t SRT_SLOTS = 64;           // code vectors a block sums in LDS before the global atomics
 
 // hist[g][k]: rows of block g's range with index k
 __global__ __launch_bounds__(SRT_THREADS) void sort_hist_kernel(const uint32_t *__restrict__ A, uint64_t N, uint32_t K,
@@ -379,8 +380,15 @@ __global__ __launch_bounds__(256) void sorted_sums_kernel(const uint8_t *__restr
                                                           uint64_t *__restrict__ sums) {
     constexpr int W4 = DP / 4;
     constexpr int B = (int)SRT_ROWS_PER_LANE;   // rows gathered together
+    constexpr uint32_t NS = 2 * DP + 1;         // hi | lo | count per code vector
     __shared__ uint8_t lo8[256];
+    // the block's runs: its positions cover code vectors kbase .. (sorted), the first
+    // SRT_SLOTS of them summed here and added to the global sums once per block
+    __shared__ uint32_t tab[SRT_SLOTS * NS];
     if (threadIdx.x < 256) lo8[threadIdx.x] = (uint8_t)(plut[threadIdx.x] & 0xFF);
+    for (uint32_t i = threadIdx.x; i < SRT_SLOTS * NS; i += 256) tab[i] = 0;
+    const uint64_t bp = (uint64_t)blockIdx.x * 256 * SRT_ROWS_PER_LANE;
+    const uint32_t kbase = ks[bp < N ? bp : N - 1];
     __syncthreads();
     const uint64_t p0 = ((uint64_t)blockIdx.x * 256 + threadIdx.x) * SRT_ROWS_PER_LANE;
     const uint64_t p1 = min(N, p0 + SRT_ROWS_PER_LANE);   // p0 >= N: no rows (the lane still joins the wave sums)
@@ -431,7 +439,7 @@ __global__ __launch_bounds__(256) void sorted_sums_kernel(const uint8_t *__restr
         }
 #pragma unroll
         for (int u = 0; u < B; u++) {
-            if (p + u >= p1) break;
+            if (p + u >= p1) continue;
             if (k[u] != cur) {
                 flush();
                 cur = k[u];
@@ -461,17 +469,45 @@ __global__ __launch_bounds__(256) void sorted_sums_kernel(const uint8_t *__restr
             const uint32_t before = __shfl(pre, src);
             return pre - (h == 0 ? 0u : before);
         };
+        const bool mine = tail && key != 0xFFFFFFFFu;
+        const uint32_t slot = key - kbase;   // < SRT_SLOTS: the block table (u32: <= 2048 rows)
 #pragma unroll
         for (int d = 0; d < DP; d++) {
-            if ((uint32_t)d >= D) break;
+            if ((uint32_t)d >= D) continue;   // (uniform; continue keeps the loop unrolled)
             const uint32_t hs = seg(acc[d] >> 16), ls = seg(acc[d] & 0xFFFF);
-            if (tail && key != 0xFFFFFFFFu) {
-                atomicAdd((unsigned long long *)&sums[(uint64_t)d * K + key], (unsigned long long)hs);
-                atomicAdd((unsigned long long *)&sums[KD + (uint64_t)d * K + key], (unsigned long long)ls);
+            if (mine) {
+                if (slot < SRT_SLOTS) {
+                    atomicAdd(&tab[slot * NS + d], hs);
+                    atomicAdd(&tab[slot * NS + DP + d], ls);
+                } else {
+                    atomicAdd((unsigned long long *)&sums[(uint64_t)d * K + key], (unsigned long long)hs);
+                    atomicAdd((unsigned long long *)&sums[KD + (uint64_t)d * K + key], (unsigned long long)ls);
+                }
             }
         }
         const uint32_t cs = seg(acc[DP]);
-        if (tail && key != 0xFFFFFFFFu) atomicAdd((unsigned long long *)&sums[2 * KD + key], (unsigned long long)cs);
+        if (mine) {
+            if (slot < SRT_SLOTS) atomicAdd(&tab[slot * NS + 2 * DP], cs);
+            else atomicAdd((unsigned long long *)&sums[2 * KD + key], (unsigned long long)cs);
+        }
+    }
+    __syncthreads();
+    // the block's table to the global sums: one atomic per (code vector, term) per block
+    for (uint32_t i = threadIdx.x; i < SRT_SLOTS * NS; i += 256) {
+        const uint32_t slot = i / NS, c = i - slot * NS;
+        if (tab[slot * NS + 2 * DP] == 0 || kbase + slot >= K) continue;   // no rows of it here
+        const uint32_t k = kbase + slot;
+        uint64_t *dst;
+        if (c < DP) {
+            if (c >= D) continue;
+            dst = &sums[(uint64_t)c * K + k];
+        } else if (c < 2 * DP) {
+            if (c - DP >= D) continue;
+            dst = &sums[KD + (uint64_t)(c - DP) * K + k];
+        } else {
+            dst = &sums[2 * KD + k];
+        }
+        atomicAdd((unsigned long long *)dst, (unsigned long long)tab[i]);
     }
 }
 
