@@ -375,12 +375,13 @@ qvq_status all_reduce_sums(qvq_ctx *ctx, uint32_t K, uint64_t *sums = nullptr, u
     return QVQ_OK;
 }
 
-// Sums of a final assignment through the counting sort (k_misc.hip) for big K * D: from K * D
-// = 16384 (C4 from K = 512), where the LDS update's passes and slabs cost most
-// (QVQ_SORTED_SUMS=0: A/B).
+// Sums of a final assignment through the counting sort (k_misc.hip) from K * D = 1536 (C4 from
+// K = 32: 5.52 -> 5.23 ms against 16384; QVQ_SORTED_MIN_KD, QVQ_SORTED_SUMS=0: A/B).
 bool use_sorted_sums(const qvq_ctx *ctx, uint32_t K) {
     static const bool on = !env_is("QVQ_SORTED_SUMS", "0");
-    return on && (uint64_t)K * ctx->D >= 16384 && sorted_sums_fits(K) && ctx->N <= 0xFFFFFFFFull;
+    static const uint64_t min_kd =
+        std::getenv("QVQ_SORTED_MIN_KD") ? (uint64_t)std::atoll(std::getenv("QVQ_SORTED_MIN_KD")) : 1536;
+    return on && (uint64_t)K * ctx->D >= min_kd && sorted_sums_fits(K) && ctx->N <= 0xFFFFFFFFull;
 }
 
 // Centroid sums under assignment d_A: slabs in d_part (ctx->nslabs of them, for the reduce),
