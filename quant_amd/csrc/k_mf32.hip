@@ -40,6 +40,11 @@ constexpr uint32_t M32_LDS_MAX = 160 * 1024;
 struct M32Lds {
     uint32_t q, c32, sums, cnt, plut, total;
 };
+// Sums copies (fused, copies > 1): strides one u64 / u32 past K * D / K, so the copies of one
+// (component, code vector) fall on different LDS banks (a 256-byte multiple put them all on
+// one: K = 256 / 512 showed 3x the bank-conflict cycles of the other levels)
+__host__ __device__ inline uint32_t m32_sum_stride(uint32_t K, uint32_t copies) { return K * MF_D + (copies > 1 ? 1 : 0); }
+__host__ __device__ inline uint32_t m32_cnt_stride(uint32_t K, uint32_t copies) { return K + (copies > 1 ? 1 : 0); }
 __host__ __device__ inline M32Lds m32_lds_layout(uint32_t K, bool fuse, bool staged, uint32_t copies = 1) {
     const uint32_t Kp = (K + 31) & ~31u;
     M32Lds L;
@@ -49,9 +54,9 @@ __host__ __device__ inline M32Lds m32_lds_layout(uint32_t K, bool fuse, bool sta
     L.c32 = o;
     if (staged) o += Kp * MF_D * 4;
     L.sums = o;
-    if (fuse) o += copies * K * MF_D * 8;
+    if (fuse) o += copies * m32_sum_stride(K, copies) * 8;
     L.cnt = o;
-    if (fuse) o += copies * ((K + 1) & ~1u) * 4;
+    if (fuse) o += copies * ((m32_cnt_stride(K, copies) + 1) & ~1u) * 4;
     L.plut = o;
     if (fuse) o += 256;
     L.total = o;
@@ -142,8 +147,8 @@ __global__ __launch_bounds__(M32_THREADS) void assign_mf32_kernel(
         for (uint32_t i = tid; i < Kp * (MF_D / 4); i += M32_THREADS) dst[i] = src[i];
     }
     if (FUSE) {
-        for (uint32_t i = tid; i < copies * K * MF_D; i += M32_THREADS) sums[i] = 0;
-        for (uint32_t i = tid; i < copies * K; i += M32_THREADS) cnt[i] = 0;
+        for (uint32_t i = tid; i < copies * m32_sum_stride(K, copies); i += M32_THREADS) sums[i] = 0;
+        for (uint32_t i = tid; i < copies * m32_cnt_stride(K, copies); i += M32_THREADS) cnt[i] = 0;
         if (tid < 256) lo8[tid] = (uint8_t)(g_plut[tid] & 0xFF);
         if (blockIdx.x == 0) {   // the correction slabs G (+) and G + 1 (-), after all G others
             for (uint32_t i = tid; i < 2 * K * MF_D; i += M32_THREADS) part[(uint64_t)gridDim.x * K * MF_D + i] = 0;
@@ -328,14 +333,14 @@ __global__ __launch_bounds__(M32_THREADS) void assign_mf32_kernel(
             if (copies > 1) {
                 if (valid) {
                     const uint32_t cp = (uint32_t)lane & (copies - 1);
-                    uint64_t *my = sums + (size_t)cp * K * MF_D;
+                    uint64_t *my = sums + (size_t)cp * m32_sum_stride(K, copies);
 #pragma unroll
                     for (int d = 0; d < MF_D; d++) {
                         const uint32_t b = (own[d / 4] >> (8 * (d % 4))) & 0xFF;
                         atomicAdd((unsigned long long *)&my[(uint32_t)d * K + rk],
                                   (unsigned long long)((uint64_t)(b ^ 0x80u) << 32 | lo8[b]));
                     }
-                    atomicAdd(&cnt[cp * K + rk], 1u);
+                    atomicAdd(&cnt[cp * m32_cnt_stride(K, copies) + rk], 1u);
                 }
             } else if (K <= th.runs_max_k) {
                 uint32_t v[MF_D + 1];
@@ -369,13 +374,13 @@ __global__ __launch_bounds__(M32_THREADS) void assign_mf32_kernel(
         uint64_t *pdst = part + (uint64_t)blockIdx.x * K * MF_D;   // slab layout [d][k]
         for (uint32_t i = tid; i < K * MF_D; i += M32_THREADS) {
             uint64_t v = 0;
-            for (uint32_t c = 0; c < copies; c++) v += sums[(size_t)c * K * MF_D + i];
+            for (uint32_t c = 0; c < copies; c++) v += sums[(size_t)c * m32_sum_stride(K, copies) + i];
             pdst[i] = v;
         }
         uint32_t *cdst = part_cnt + (uint64_t)blockIdx.x * K;
         for (uint32_t i = tid; i < K; i += M32_THREADS) {
             uint32_t v = 0;
-            for (uint32_t c = 0; c < copies; c++) v += cnt[c * K + i];
+            for (uint32_t c = 0; c < copies; c++) v += cnt[c * m32_cnt_stride(K, copies) + i];
             cdst[i] = v;
         }
     }
@@ -595,11 +600,11 @@ hipError_t launch_assign_mf32(hipStream_t s, int grid, bool fuse, const uint8_t 
                               uint64_t *part, uint32_t *part_cnt) {
     if (!mf32_fits(K, fuse)) return hipErrorInvalidValue;
     const bool staged = m32_lds_layout(K, fuse, true).total <= M32_LDS_MAX;
-    // sums copies (fused, 256 <= K <= 512 by default: QVQ_SUM_COPIES_MINK / _MAXK): the most, up
-    // to 16, that fit.  C3: K = 256 / 512 -4.5 us each; K = 64 +5 us (long runs: the run
-    // reduction's one atomic set per run wins), K = 1024 has no room for a second copy.
+    // sums copies (fused, 64 <= K <= 512 by default: QVQ_SUM_COPIES_MINK / _MAXK): the most, up
+    // to 16, that fit.  With the padded copy strides, C3: K = 64 / 128 / 256 / 512 -6 / -22 /
+    // -19 / -16 us against the wave run reduction; K = 1024 has no room for a second copy.
     static const uint32_t copies_mink =
-        std::getenv("QVQ_SUM_COPIES_MINK") ? (uint32_t)std::atoi(std::getenv("QVQ_SUM_COPIES_MINK")) : 256;
+        std::getenv("QVQ_SUM_COPIES_MINK") ? (uint32_t)std::atoi(std::getenv("QVQ_SUM_COPIES_MINK")) : 64;
     static const uint32_t copies_maxk =
         std::getenv("QVQ_SUM_COPIES_MAXK") ? (uint32_t)std::atoi(std::getenv("QVQ_SUM_COPIES_MAXK")) : 512;
     uint32_t copies = 1;
