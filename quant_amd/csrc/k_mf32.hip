@@ -43,7 +43,12 @@ struct M32Lds {
 // Sums copies (fused, copies > 1): strides one u64 / u32 past K * D / K, so the copies of one
 // (component, code vector) fall on different LDS banks (a 256-byte multiple put them all on
 // one: K = 256 / 512 showed 3x the bank-conflict cycles of the other levels)
-__host__ __device__ inline uint32_t m32_sum_stride(uint32_t K, uint32_t copies) { return K * MF_D + (copies > 1 ? 1 : 0); }
+// component rows of the LDS sums [d][k] are K + 1 apart (QVQ_SUMS_KPAD builds: A/B)
+#ifndef QVQ_SUMS_KPAD
+#define QVQ_SUMS_KPAD 1
+#endif
+__host__ __device__ inline uint32_t m32_kstride(uint32_t K) { return K + QVQ_SUMS_KPAD; }
+__host__ __device__ inline uint32_t m32_sum_stride(uint32_t K, uint32_t copies) { return m32_kstride(K) * MF_D + (copies > 1 ? 1 : 0); }
 __host__ __device__ inline uint32_t m32_cnt_stride(uint32_t K, uint32_t copies) { return K + (copies > 1 ? 1 : 0); }
 __host__ __device__ inline M32Lds m32_lds_layout(uint32_t K, bool fuse, bool staged, uint32_t copies = 1) {
     const uint32_t Kp = (K + 31) & ~31u;
@@ -337,7 +342,7 @@ __global__ __launch_bounds__(M32_THREADS) void assign_mf32_kernel(
 #pragma unroll
                     for (int d = 0; d < MF_D; d++) {
                         const uint32_t b = (own[d / 4] >> (8 * (d % 4))) & 0xFF;
-                        atomicAdd((unsigned long long *)&my[(uint32_t)d * K + rk],
+                        atomicAdd((unsigned long long *)&my[(uint32_t)d * m32_kstride(K) + rk],
                                   (unsigned long long)((uint64_t)(b ^ 0x80u) << 32 | lo8[b]));
                     }
                     atomicAdd(&cnt[cp * m32_cnt_stride(K, copies) + rk], 1u);
@@ -354,7 +359,7 @@ __global__ __launch_bounds__(M32_THREADS) void assign_mf32_kernel(
                 if (tail && valid) {
 #pragma unroll
                     for (int d = 0; d < MF_D; d++)
-                        atomicAdd((unsigned long long *)&sums[(uint32_t)d * K + rk],
+                        atomicAdd((unsigned long long *)&sums[(uint32_t)d * m32_kstride(K) + rk],
                                   (unsigned long long)((((uint64_t)(v[d] >> 16)) << 32) | (v[d] & 0xFFFF)));
                     atomicAdd(&cnt[rk], v[MF_D]);
                 }
@@ -362,7 +367,7 @@ __global__ __launch_bounds__(M32_THREADS) void assign_mf32_kernel(
 #pragma unroll
                 for (int d = 0; d < MF_D; d++) {
                     const uint32_t b = (own[d / 4] >> (8 * (d % 4))) & 0xFF;
-                    atomicAdd((unsigned long long *)&sums[(uint32_t)d * K + rk],
+                    atomicAdd((unsigned long long *)&sums[(uint32_t)d * m32_kstride(K) + rk],
                               (unsigned long long)((uint64_t)(b ^ 0x80u) << 32 | lo8[b]));
                 }
                 atomicAdd(&cnt[rk], 1u);
@@ -373,8 +378,9 @@ __global__ __launch_bounds__(M32_THREADS) void assign_mf32_kernel(
         __syncthreads();
         uint64_t *pdst = part + (uint64_t)blockIdx.x * K * MF_D;   // slab layout [d][k]
         for (uint32_t i = tid; i < K * MF_D; i += M32_THREADS) {
+            const uint32_t d = i / K, j = d * m32_kstride(K) + (i - d * K);
             uint64_t v = 0;
-            for (uint32_t c = 0; c < copies; c++) v += sums[(size_t)c * m32_sum_stride(K, copies) + i];
+            for (uint32_t c = 0; c < copies; c++) v += sums[(size_t)c * m32_sum_stride(K, copies) + j];
             pdst[i] = v;
         }
         uint32_t *cdst = part_cnt + (uint64_t)blockIdx.x * K;
