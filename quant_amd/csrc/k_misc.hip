@@ -140,8 +140,12 @@ constexpr size_t URUN_LDS = 160 * 1024;
 // wide rows keep 4 + DP/4 + DP registers per lane live: fewer waves, up to 256 VGPRs
 __host__ __device__ constexpr int urun_threads(int DP) { return DP > 32 ? 512 : 1024; }
 
+// copies' strides one word past K*D (u64) and an even K (u32): the copies of one term then sit
+// on different LDS banks (as the MFMA search's, k_mf32.hip)
+__host__ __device__ inline uint32_t urun_sstride(uint32_t K, uint32_t D) { return K * D + 1; }
+__host__ __device__ inline uint32_t urun_cstride(uint32_t K) { return ((K + 1) & ~1u) + 2; }
 static size_t urun_bytes(uint32_t K, uint32_t D, uint32_t C) {
-    return (size_t)C * K * D * 8 + (size_t)C * ((K + 1) & ~1u) * 4 + 256;
+    return (size_t)C * urun_sstride(K, D) * 8 + (size_t)C * urun_cstride(K) * 4 + 256;
 }
 static uint32_t urun_copies(uint32_t K, uint32_t D) {
     for (uint32_t C : {16u, 8u, 4u, 2u})
@@ -160,14 +164,14 @@ __global__ __launch_bounds__(urun_threads(DP)) void update_runs_kernel(const uin
     constexpr int R = DP <= 16 ? 4 : (DP <= 32 ? 2 : 1);   // rows per lane and round
     constexpr int W4 = DP / 4;                               // code words per row
     extern __shared__ __attribute__((aligned(16))) uint64_t usm[];
-    const uint32_t K2 = (K + 1) & ~1u;
-    uint64_t *sums_all = usm;                                                         // [C][D][K]
-    uint32_t *cnt_all = reinterpret_cast<uint32_t *>(usm + (size_t)C * K * D);       // [C][K2]
+    const uint32_t SS = urun_sstride(K, D), K2 = urun_cstride(K);
+    uint64_t *sums_all = usm;                                                         // [C][SS] ([D][K] each)
+    uint32_t *cnt_all = reinterpret_cast<uint32_t *>(usm + (size_t)C * SS);          // [C][K2]
     uint8_t *lo8 = reinterpret_cast<uint8_t *>(cnt_all + (size_t)C * K2);            // [256]
     const int tid = threadIdx.x, lane = tid & 63;
-    for (uint32_t i = tid; i < C * K * D; i += T) sums_all[i] = 0;
+    for (uint32_t i = tid; i < C * SS; i += T) sums_all[i] = 0;
     for (uint32_t i = tid; i < C * K2; i += T) cnt_all[i] = 0;
-    uint64_t *sums = sums_all + (size_t)(lane % C) * K * D;   // this lane's copy
+    uint64_t *sums = sums_all + (size_t)(lane % C) * SS;   // this lane's copy
     uint32_t *cnt = cnt_all + (size_t)(lane % C) * K2;
     if (tid < 256) lo8[tid] = (uint8_t)(plut[tid] & 0xFF);
     __syncthreads();
@@ -227,7 +231,7 @@ __global__ __launch_bounds__(urun_threads(DP)) void update_runs_kernel(const uin
     uint64_t *pdst = part + (uint64_t)blockIdx.x * K * D;
     for (uint32_t i = tid; i < K * D; i += T) {
         uint64_t t = 0;
-        for (uint32_t c = 0; c < C; c++) t += sums_all[(size_t)c * K * D + i];
+        for (uint32_t c = 0; c < C; c++) t += sums_all[(size_t)c * SS + i];
         pdst[i] = t;
     }
     uint32_t *cdst = part_cnt + (uint64_t)blockIdx.x * K;
