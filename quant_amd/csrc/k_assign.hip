@@ -480,14 +480,19 @@ __global__ __launch_bounds__(MF_THREADS) void assign_small_kernel(
     uint32_t *__restrict__ A, uint32_t *__restrict__ flags, unsigned *__restrict__ flag_cnt,
     uint64_t *__restrict__ part, uint32_t *__restrict__ part_cnt) {
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
-    // LDS: C copies of the sums, copy c = [d][k] (SK*D u64) then counts [k] (SK u64), stride
-    // S = SK*(D+1) + 1 (odd: the copies of 16 consecutive lanes sit on different banks) | lo8.
+    // LDS: lo8 (256 B, first: a byte's lookup address is the byte itself, no base add) | C
+    // copies of the sums, copy c = [d][k] (SK*D u64) then counts [k] (SK u64), stride
+    // S = SK*(D+1) + 1 (odd: the copies of 16 consecutive lanes sit on different banks).
     // SK-strided, so a flush addresses copy + d*SK + cur with immediate offsets.
     // Lane L flushes into copy L mod C, so the flushes of a wave's lanes -- all at once at
     // the end, mostly to the same code vector at small K -- rarely hit one address.
     constexpr uint32_t S = small_copy_stride(SK);
-    uint64_t *cps = reinterpret_cast<uint64_t *>(lds);
-    uint8_t *lo8 = lds + (size_t)copies * S * 8;   // low part of each byte's exact term (high part: b ^ 0x80)
+    uint8_t *lo8 = lds;   // low part of each byte's exact term (high part: b ^ 0x80)
+    // The same table addressed as LDS byte 0 (the kernel has no static LDS, so the dynamic
+    // block starts there): lookups take the byte as their address, with no base add per byte.
+    const __attribute__((address_space(3))) uint8_t *lo8_at0 =
+        (const __attribute__((address_space(3))) uint8_t *)(uintptr_t)0;
+    uint64_t *cps = reinterpret_cast<uint64_t *>(lds + 256);
     const int tid = threadIdx.x;
     if (FUSE) {
         for (uint32_t i = tid; i < copies * S; i += MF_THREADS) cps[i] = 0;
@@ -550,7 +555,10 @@ __global__ __launch_bounds__(MF_THREADS) void assign_small_kernel(
         for (int p = 0; p < 2; p++)
 #pragma unroll
             for (int d = 0; d < MF_D; d++)
-                x[p][d] = f32x2{byte_w(w[2 * p][d / 4], d % 4), byte_w(w[2 * p + 1][d / 4], d % 4)};
+                x[p][d] = __builtin_elementwise_fma(   // byte_w of both rows, one v_pk_fma_f32
+                    f32x2{(float)(((w[2 * p][d / 4] ^ 0x80808080u) >> (8 * (d % 4))) & 0xFF),
+                          (float)(((w[2 * p + 1][d / 4] ^ 0x80808080u) >> (8 * (d % 4))) & 0xFF)},
+                    f32x2{2.f, 2.f}, f32x2{-255.f, -255.f});
         float r1[4], r2[4];
         uint32_t idx[4];
 #pragma unroll
@@ -609,7 +617,7 @@ __global__ __launch_bounds__(MF_THREADS) void assign_small_kernel(
 #pragma unroll
                 for (int d = 0; d < MF_D; d++) {
                     const uint32_t b = (w[r][d / 4] >> (8 * (d % 4))) & 0xFF;
-                    acc[d] += (b ^ 0x80u) << 16 | lo8[b];
+                    acc[d] += (b ^ 0x80u) << 16 | lo8_at0[b];
                 }
                 acc[MF_D] += 1;
             }
