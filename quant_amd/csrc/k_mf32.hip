@@ -53,7 +53,10 @@ __host__ __device__ inline uint32_t m32_cnt_stride(uint32_t K, uint32_t copies) 
 __host__ __device__ inline M32Lds m32_lds_layout(uint32_t K, bool fuse, bool staged, uint32_t copies = 1) {
     const uint32_t Kp = (K + 31) & ~31u;
     M32Lds L;
-    uint32_t o = Kp * 32;
+    // fused: the byte LUT first (LDS address 0: a lookup's address is the byte itself, no
+    // base add per byte), the code-vector rows after it (ROWS0 in the kernel)
+    uint32_t o = fuse ? 256 : 0;
+    o += Kp * 32;
     L.q = o;
     o += Kp * 24;
     L.c32 = o;
@@ -62,8 +65,7 @@ __host__ __device__ inline M32Lds m32_lds_layout(uint32_t K, bool fuse, bool sta
     if (fuse) o += copies * m32_sum_stride(K, copies) * 8;
     L.cnt = o;
     if (fuse) o += copies * ((m32_cnt_stride(K, copies) + 1) & ~1u) * 4;
-    L.plut = o;
-    if (fuse) o += 256;
+    L.plut = 0;
     L.total = o;
     return L;
 }
@@ -87,13 +89,14 @@ __device__ inline bool m32_runs_reduce(uint32_t key, uint32_t (&v)[MF_D + 1], in
 
 // P / Q (LDS, layout above) from the 56-byte rows [hi0..3 lo0..3 | hi4..7 lo4..7 | hi8..11
 // lo8..11 | n] of Kp code vectors.
-__device__ inline void m32_stage_pq(unsigned char *lds, uint32_t qoff, const _Float16 *g_rows, uint32_t Kp, int tid) {
+__device__ inline void m32_stage_pq(unsigned char *lds, uint32_t qoff, const _Float16 *g_rows, uint32_t Kp, int tid,
+                                    uint32_t rows0 = 0) {
     const uint64_t *src = reinterpret_cast<const uint64_t *>(g_rows);
     for (uint32_t i = tid; i < Kp; i += M32_THREADS) {
         const uint64_t *r = src + (size_t)i * 7;
         const uint64_t w0 = r[0], w1 = r[1], w2 = r[2], w3 = r[3], w4 = r[4], w5 = r[5], w6 = r[6];
         const bool sw = (i >> 3) & 1;
-        u64x2v *p = reinterpret_cast<u64x2v *>(lds + (size_t)i * 32);
+        u64x2v *p = reinterpret_cast<u64x2v *>(lds + rows0 + (size_t)i * 32);
         const u64x2v hi = {w0, w2}, lo = {w1, w3};
         p[0] = sw ? lo : hi;
         p[1] = sw ? hi : lo;
@@ -144,8 +147,13 @@ __global__ __launch_bounds__(M32_THREADS) void assign_mf32_kernel(
     uint64_t *sums = reinterpret_cast<uint64_t *>(lds + L.sums);   // [d][k]
     uint32_t *cnt = reinterpret_cast<uint32_t *>(lds + L.cnt);
     uint8_t *lo8 = lds + L.plut;   // low part of each byte's exact term (high part: b ^ 0x80)
+    // The same table addressed as LDS byte 0 (the kernel has no static LDS, so the dynamic
+    // block starts there): lookups take the byte as their address.
+    const __attribute__((address_space(3))) uint8_t *lo8_at0 =
+        (const __attribute__((address_space(3))) uint8_t *)(uintptr_t)0;
+    constexpr uint32_t ROWS0 = FUSE ? 256 : 0;   // m32_lds_layout
     const int tid = threadIdx.x;
-    m32_stage_pq(lds, L.q, g_rows, Kp, tid);
+    m32_stage_pq(lds, L.q, g_rows, Kp, tid, ROWS0);
     if (STAGED) {
         const float4 *src = reinterpret_cast<const float4 *>(g_C32);
         float4 *dst = reinterpret_cast<float4 *>(c32s);
@@ -169,7 +177,7 @@ __global__ __launch_bounds__(M32_THREADS) void assign_mf32_kernel(
     const uint64_t nchunks = (N + M32_ROWS - 1) / M32_ROWS;
     // A fragments of code tile t: P half h of code vector 32t + r32 (halves swapped on bit 3),
     // Q bytes 8(1-h) .. +15
-    const unsigned char *pa = lds + r32 * 32 + 16 * (h ^ ((r32 >> 3) & 1));
+    const unsigned char *pa = lds + ROWS0 + r32 * 32 + 16 * (h ^ ((r32 >> 3) & 1));
     const unsigned char *qa = lds + L.q + r32 * 24 + 8 * (1 - h);
     auto load_a = [&](uint32_t t, half8 &a1, half8 &a2) {
         const u32x4v v1 = *reinterpret_cast<const u32x4v *>(pa + (size_t)t * (32 * 32));
@@ -343,7 +351,7 @@ __global__ __launch_bounds__(M32_THREADS) void assign_mf32_kernel(
                     for (int d = 0; d < MF_D; d++) {
                         const uint32_t b = (own[d / 4] >> (8 * (d % 4))) & 0xFF;
                         atomicAdd((unsigned long long *)&my[(uint32_t)d * m32_kstride(K) + rk],
-                                  (unsigned long long)((uint64_t)(b ^ 0x80u) << 32 | lo8[b]));
+                                  (unsigned long long)((uint64_t)(b ^ 0x80u) << 32 | lo8_at0[b]));
                     }
                     atomicAdd(&cnt[cp * m32_cnt_stride(K, copies) + rk], 1u);
                 }
@@ -352,7 +360,7 @@ __global__ __launch_bounds__(M32_THREADS) void assign_mf32_kernel(
 #pragma unroll
                 for (int d = 0; d < MF_D; d++) {
                     const uint32_t b = (own[d / 4] >> (8 * (d % 4))) & 0xFF;
-                    v[d] = valid ? ((b ^ 0x80u) << 16 | lo8[b]) : 0u;   // <= 64 rows: no carry
+                    v[d] = valid ? ((b ^ 0x80u) << 16 | lo8_at0[b]) : 0u;   // <= 64 rows: no carry
                 }
                 v[MF_D] = valid ? 1u : 0u;
                 const bool tail = m32_runs_reduce(valid ? rk : 0xFFFFFFFFu, v, lane);
@@ -368,7 +376,7 @@ __global__ __launch_bounds__(M32_THREADS) void assign_mf32_kernel(
                 for (int d = 0; d < MF_D; d++) {
                     const uint32_t b = (own[d / 4] >> (8 * (d % 4))) & 0xFF;
                     atomicAdd((unsigned long long *)&sums[(uint32_t)d * m32_kstride(K) + rk],
-                              (unsigned long long)((uint64_t)(b ^ 0x80u) << 32 | lo8[b]));
+                              (unsigned long long)((uint64_t)(b ^ 0x80u) << 32 | lo8_at0[b]));
                 }
                 atomicAdd(&cnt[rk], 1u);
             }
