@@ -12,6 +12,12 @@ N images (weak scaling: per-GPU work fixed, one all-reduce per level).
     python bench.py [--gpus N] [--steps K] [--warmup W]
     torchrun --nproc-per-node N bench.py --gpus N ...
 
+With --gpus N > 1 and no launcher environment (WORLD_SIZE unset), this script starts the N
+rank processes itself (one per GPU, LOCAL_RANK = device index) before anything touches a GPU,
+passes rank 0's JSON line through and exits with the worst rank status.  Under a launcher
+WORLD_SIZE must equal --gpus.  --dry-run (CPU only): the ranks join the gloo control plane and
+rank 0 prints what it would run, without touching a GPU.
+
 Rank 0 prints one JSON line.  value = Mblocks/s = (blocks on all ranks) x levels x steps
 / max-over-ranks wall time / 1e6 (BASELINE.md section 2 definition).
 
@@ -62,7 +68,65 @@ def parse():
     ap.add_argument("--c5-steps", type=int, default=3, help="0 disables the c5 sub-object")
     ap.add_argument("--c4-steps", type=int, default=5, help="0 disables the c4 sub-object")
     ap.add_argument("--e2e-reps", type=int, default=3, help="0 disables the end_to_end sub-object")
+    ap.add_argument("--dry-run", action="store_true", help="CPU only: start the ranks, join gloo, print the plan")
     return ap.parse_args()
+
+
+def _free_port():
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(n):
+    """Start n rank processes of this script (RANK = LOCAL_RANK = r, WORLD_SIZE = n, rendezvous
+    on 127.0.0.1) and wait for them.  The parent never touches a GPU, so the children start
+    clean.  Rank 0's stdout (the JSON line) is the parent's; the other ranks' stdout goes to
+    stderr.  If a rank fails, the others are stopped (they would wait at the next barrier)."""
+    port = os.environ.get("MASTER_PORT") or str(_free_port())
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=port)
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env,
+                                      stdout=None if r == 0 else sys.stderr))
+    rc = 0
+    while procs:
+        for p in list(procs):
+            code = p.poll()
+            if code is None:
+                continue
+            procs.remove(p)
+            if code != 0:
+                rc = rc or code
+                for q in procs:
+                    q.terminate()
+        time.sleep(0.05)
+    return rc
+
+
+def dry_run(args, world, rank):
+    """--dry-run: the ranks join the gloo control plane and agree on the shard plan; rank 0
+    prints it.  No GPU is touched (tests/test_multirank_cpu.py runs this on the CPU box)."""
+    import torch
+    import torch.distributed as dist
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+    n_img = args.c5_images
+    share = [n_img // world + (1 if r < n_img % world else 0) for r in range(world)]
+    t = torch.tensor([rank, os.getpid()], dtype=torch.int64)
+    got = [torch.zeros_like(t) for _ in range(world)] if world > 1 else [t]
+    if world > 1:
+        dist.all_gather(got, t)
+    if rank == 0:
+        print(json.dumps({"dry_run": True, "n_gpus": world, "ranks_joined": sorted(int(g[0]) for g in got),
+                          "pids": [int(g[1]) for g in got], "c5_images_per_rank": share,
+                          "headline": "one %dx%d image per rank, joint codebook" % (args.size, args.size)}),
+              flush=True)
+    if world > 1:
+        dist.destroy_process_group()
 
 
 def _oracle_runs(args, threads, reps):
@@ -117,9 +181,15 @@ def synthetic_raster(S, seed):
 
 def main():
     args = parse()
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch_ranks(args.gpus))   # before anything touches a GPU
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        sys.exit("bench.py: WORLD_SIZE=%d but --gpus %d: launch one rank per GPU" % (world, args.gpus))
+    if args.dry_run:
+        return dry_run(args, world, rank)
     import torch
     import torch.distributed as dist
     import quant_amd
@@ -138,6 +208,10 @@ def main():
         uid = [quant_amd.Engine.comm_unique_id() if rank == 0 else None]
         dist.broadcast_object_list(uid, src=0)
         eng.comm_init(world, rank, uid[0])   # RCCL over xGMI for the per-level sums
+    comm_n, _, comm_kind = eng.comm_info()
+    rccl_ranks = comm_n if comm_kind == quant_amd.COMM_RCCL else 0
+    if world > 1 and rccl_ranks != world:
+        sys.exit("bench.py: the engine joined %d RCCL ranks, expected %d" % (rccl_ranks, world))
     ipr = args.images_per_rank
     eng.set_synthetic(args.size, 0x5EED + rank * ipr, ipr, args.block, args.block, quant_amd.SCALED)
     n_local = eng.n
@@ -220,6 +294,7 @@ def main():
         "value": round(value, 3),
         "unit": "Mblocks/s",
         "n_gpus": world,
+        "rccl_ranks": rccl_ranks,
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": round(ms_per_step, 4),

@@ -131,8 +131,10 @@ QVQ_API qvq_status qvq_update(qvq_ctx *ctx, const uint32_t *assign, uint32_t K, 
  * squared difference of the signed bytes of orig and the decoded raster (src/Compressor.cpp:
  * 133-146), computed in the same device pass (rgb may then be NULL).  qvq_decode_device takes
  * device pointers and a hipStream_t on which it launches (NULL = the legacy null stream, so
- * work the caller queued on blocking streams is ordered before it) and synchronises that
- * stream before returning. */
+ * work the caller queued on blocking streams is ordered before it; the engine's own queued work
+ * is ordered before it on any stream) and synchronises that stream before returning.  d_assign
+ * must be 4-byte aligned; other alignments are accepted (unaligned rasters and index arrays take
+ * a per-pixel kernel). */
 QVQ_API qvq_status qvq_decode(qvq_ctx *ctx, const uint8_t *codebook, uint32_t K, const uint32_t *assign,
                               uint64_t nblocks, uint32_t xSize, uint32_t ySize, uint32_t bw, uint32_t bh, uint8_t *rgb);
 QVQ_API qvq_status qvq_decode_mse(qvq_ctx *ctx, const uint8_t *codebook, uint32_t K, const uint32_t *assign,
@@ -151,8 +153,21 @@ QVQ_API qvq_status qvq_decode_device(qvq_ctx *ctx, const void *d_codebook, uint3
  * qvq_comm_init). */
 QVQ_API qvq_status qvq_comm_unique_id(uint8_t id[128]);
 QVQ_API qvq_status qvq_comm_init(qvq_ctx *ctx, int nranks, int rank, const uint8_t id[128]);
+/* Test-only communicator: every per-level exchange (the same buffers the RCCL all-reduce
+ * sums: the mean's and the level's per-code-vector sums and counts as u64, dtype 0; the two
+ * distortion terms as double, dtype 1) is copied to pinned host memory, fn(buf, count, dtype,
+ * user) must replace it in place by the sum over the nranks ranks and return 0, and the
+ * result is copied back.  Lets several processes share one GPU (RCCL refuses two ranks on one
+ * device) so the sharded schedule runs in tests on a one-GPU box.  Replaces any communicator. */
+typedef int (*qvq_allreduce_fn)(void *buf, uint64_t count, int dtype, void *user);
+QVQ_API qvq_status qvq_comm_init_host(qvq_ctx *ctx, int nranks, int rank, qvq_allreduce_fn fn, void *user);
+/* The joined communicator: ranks, this rank, kind (QVQ_COMM_NONE: single rank). */
+enum { QVQ_COMM_NONE = 0, QVQ_COMM_RCCL = 1, QVQ_COMM_HOST = 2 };
+QVQ_API qvq_status qvq_comm_info(const qvq_ctx *ctx, int *nranks, int *rank, int *kind);
 /* Bound, in seconds, of every host wait on the context's stream (default 120, or the
- * QVQ_TIMEOUT_S environment variable at qvq_create). */
+ * QVQ_TIMEOUT_S environment variable at qvq_create).  A wait that fails while the stream
+ * cannot be drained poisons the context: results are never copied into caller memory after
+ * the call returned, and every later call but qvq_destroy returns QVQ_ESTATE. */
 QVQ_API qvq_status qvq_set_timeout(qvq_ctx *ctx, double seconds);
 
 /* Which levels get HIP events around their search kernel (each event record costs a few

@@ -42,7 +42,11 @@ EXPORTED = ["qvq_create", "qvq_destroy", "qvq_last_error", "qvq_version", "qvq_s
             "qvq_dim", "qvq_lbg", "qvq_assign_device", "qvq_assign", "qvq_update",
             "qvq_comm_unique_id", "qvq_comm_init", "qvq_set_timing", "qvq_get_timings", "qvq_host_kdtree_nn",
             "qvq_host_finalize", "qvq_host_row_terms", "qvq_decode", "qvq_decode_mse", "qvq_decode_device",
-            "qvq_set_timeout", "qvq_host_wait_probe"]
+            "qvq_set_timeout", "qvq_host_wait_probe", "qvq_comm_init_host", "qvq_comm_info"]
+
+COMM_NONE, COMM_RCCL, COMM_HOST = 0, 1, 2
+# int fn(void *buf, uint64_t count, int dtype, void *user) (qvq.h, qvq_comm_init_host)
+ALLREDUCE_FN = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_int, ctypes.c_void_p)
 
 
 def lib():
@@ -80,6 +84,8 @@ def lib():
             "qvq_decode_device": ([P, P, u32, P, u64, u32, u32, u32, u32, P, P], i),
             "qvq_set_timeout": ([P, ctypes.c_double], i),
             "qvq_host_wait_probe": ([i, ctypes.c_double, P], i),
+            "qvq_comm_init_host": ([P, i, i, ALLREDUCE_FN, P], i),
+            "qvq_comm_info": ([P, ctypes.POINTER(i), ctypes.POINTER(i), ctypes.POINTER(i)], i),
         }
         for name, (args, res) in sig.items():
             fn = getattr(L, name)
@@ -258,6 +264,29 @@ class Engine:
     def comm_init(self, nranks, rank, uid):
         buf = (ctypes.c_uint8 * 128).from_buffer_copy(uid)
         _check(lib().qvq_comm_init(self._h, nranks, rank, buf), self._h)
+
+    def comm_init_host(self, nranks, rank, allreduce):
+        """Test-only communicator (qvq_comm_init_host): allreduce(arr) must replace the numpy
+        array arr (uint64 or float64) in place by its sum over the ranks, e.g. through
+        torch.distributed's gloo backend.  Lets several processes share one GPU."""
+        def cb(ptr, count, dtype, user):
+            try:
+                ct = ctypes.c_uint64 if dtype == 0 else ctypes.c_double
+                arr = np.ctypeslib.as_array(ctypes.cast(ptr, ctypes.POINTER(ct)), shape=(count,))
+                allreduce(arr)
+                return 0
+            except Exception:   # noqa: BLE001  (no exception may cross the C ABI)
+                import traceback
+                traceback.print_exc()
+                return 1
+        self._ar_cb = ALLREDUCE_FN(cb)   # kept alive with the engine
+        _check(lib().qvq_comm_init_host(self._h, nranks, rank, self._ar_cb, None), self._h)
+
+    def comm_info(self):
+        """(nranks, rank, kind) of the joined communicator; kind COMM_NONE/COMM_RCCL/COMM_HOST."""
+        n, r, k = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+        _check(lib().qvq_comm_info(self._h, ctypes.byref(n), ctypes.byref(r), ctypes.byref(k)), self._h)
+        return n.value, r.value, k.value
 
 
 # -- host-only helpers (no GPU) ------------------------------------------------------------

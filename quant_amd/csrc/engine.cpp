@@ -129,9 +129,19 @@ struct qvq_ctx {
     hipEvent_t ev_sync = nullptr;   // wait_stream
     double timeout_s = 120;         // bound of every host wait (qvq_set_timeout, QVQ_TIMEOUT_S)
 
-    // multi-GPU
+    // multi-GPU: an RCCL communicator, or (tests) a host all-reduce callback
     ncclComm_t comm = nullptr;
+    qvq_allreduce_fn host_ar = nullptr;
+    void *host_ar_user = nullptr;
+    void *h_ar_stage = nullptr;   // pinned staging of the host all-reduce
+    uint64_t ar_stage_bytes = 0;
     int nranks = 1, rank = 0;
+    // a bounded wait failed while work may still be queued on the stream: every later call
+    // returns QVQ_ESTATE until qvq_destroy (results must not land in freed memory,
+    // and the stream's scratch must not be reused under running kernels)
+    bool poisoned = false;
+    void *h_stage = nullptr;      // pinned staging of qvq_update's results
+    uint64_t stage_bytes = 0;
 
     qvq_timings tm;
     hipEvent_t ev[32][4];
@@ -147,6 +157,14 @@ qvq_status fail(qvq_ctx *c, qvq_status st, const std::string &msg) {
     else g_static_err = msg;
     return st;
 }
+
+// Entry points that use the device refuse a poisoned context (wait_failed).
+#define GUARD(ctx)                                                                                    \
+    do {                                                                                              \
+        if (!(ctx)) return QVQ_EINVAL;                                                                \
+        if ((ctx)->poisoned)                                                                          \
+            return fail((ctx), QVQ_ESTATE, "context poisoned by an earlier failed wait; destroy it"); \
+    } while (0)
 
 #define HIPCHK(expr)                                                                                  \
     do {                                                                                              \
@@ -367,12 +385,43 @@ void valu_coeffs(const qvq_ctx *ctx, float &alpha, float &beta, float &gamma) {
     gamma = (float)(2.0 * 4.01 * u * u * L * L + 1e-30);
 }
 
+// Grow a pinned host buffer (h, bytes) to at least need bytes.
+qvq_status ensure_pinned(qvq_ctx *ctx, void *&h, uint64_t &bytes, uint64_t need) {
+    if (bytes >= need) return QVQ_OK;
+    if (h) (void)hipHostFree(h);
+    h = nullptr;
+    bytes = 0;
+    HIPCHK(hipHostMalloc(&h, need, hipHostMallocDefault));
+    bytes = need;
+    return QVQ_OK;
+}
+
+qvq_status wait_stream(qvq_ctx *ctx);
+
+// Sum of count u64 (f64 = false) or double values at device pointer buf over the ranks, in
+// place, on the context's stream: ncclAllReduce over xGMI, or -- the test-only host
+// communicator of qvq_comm_init_host -- a copy to pinned memory, the caller's callback, and a
+// copy back (the stream is drained around the callback).  No communicator: nothing to do.
+qvq_status all_reduce(qvq_ctx *ctx, void *buf, uint64_t count, bool f64) {
+    if (ctx->comm) {
+        NCCLCHK(ncclAllReduce(buf, buf, count, f64 ? ncclDouble : ncclUint64, ncclSum, ctx->comm, ctx->stream));
+        return QVQ_OK;
+    }
+    if (!ctx->host_ar) return QVQ_OK;
+    qvq_status st = ensure_pinned(ctx, ctx->h_ar_stage, ctx->ar_stage_bytes, count * 8);
+    if (st != QVQ_OK) return st;
+    HIPCHK(hipMemcpyAsync(ctx->h_ar_stage, buf, count * 8, hipMemcpyDeviceToHost, ctx->stream));
+    if ((st = wait_stream(ctx)) != QVQ_OK) return st;
+    const int rc = ctx->host_ar(ctx->h_ar_stage, count, f64 ? 1 : 0, ctx->host_ar_user);
+    if (rc != 0) return fail(ctx, QVQ_ECOMM, "host all-reduce callback failed (" + std::to_string(rc) + ")");
+    // stream-ordered: the next all-reduce's download (and callback) come after this upload
+    HIPCHK(hipMemcpyAsync(buf, ctx->h_ar_stage, count * 8, hipMemcpyHostToDevice, ctx->stream));
+    return QVQ_OK;
+}
+
 qvq_status all_reduce_sums(qvq_ctx *ctx, uint32_t K, uint64_t *sums = nullptr, uint32_t copies = 1) {
     if (!sums) sums = ctx->d_sums;
-    if (ctx->comm)
-        NCCLCHK(ncclAllReduce(sums, sums, copies * (2 * (uint64_t)K * ctx->D + K), ncclUint64, ncclSum, ctx->comm,
-                              ctx->stream));
-    return QVQ_OK;
+    return all_reduce(ctx, sums, copies * (2 * (uint64_t)K * ctx->D + K), false);
 }
 
 // Sums of a final assignment through the counting sort (k_misc.hip) from K * D = 1536 (C4 from
@@ -467,15 +516,28 @@ CommState probe_comm(qvq_ctx *ctx, std::string &msg) {
     msg = ncclGetErrorString(ae);
     return CommState::Failed;
 }
-// A failed or timed-out collective leaves the communicator unusable: abort it (which also
-// releases the stream from a stuck RCCL kernel).  The context keeps working single-rank;
-// qvq_comm_init joins a new communicator.
-qvq_status comm_failed(qvq_ctx *ctx, qvq_status st) {
+// A failed or timed-out wait: a communicator is aborted (which also releases the stream from
+// a stuck RCCL kernel) and the context runs single-rank until the next qvq_comm_init.  Then
+// the stream gets one more bounded chance to drain; if it does not (a timeout without a
+// communicator, a kernel still running), the context is poisoned: work that may still write
+// the context's scratch or copy into caller memory is queued, so every later call but
+// qvq_destroy returns QVQ_ESTATE.
+qvq_status wait_failed(qvq_ctx *ctx, qvq_status st) {
     if (st == QVQ_ECOMM && ctx->comm) {
         (void)ncclCommAbort(ctx->comm);
         ctx->comm = nullptr;
         ctx->nranks = 1;
         ctx->rank = 0;
+    }
+    using clock = std::chrono::steady_clock;
+    // after an abort the RCCL kernels exit: give the stream 2 s to drain; a timeout without a
+    // communicator means a long or stuck kernel: one query
+    const auto until = clock::now() + std::chrono::milliseconds(st == QVQ_ECOMM ? 2000 : 0);
+    hipError_t q = hipStreamQuery(ctx->stream);
+    while (q == hipErrorNotReady && clock::now() < until) q = hipStreamQuery(ctx->stream);
+    if (q != hipSuccess) {
+        ctx->poisoned = true;
+        ctx->err += " (context poisoned: destroy it)";
     }
     return st;
 }
@@ -488,7 +550,7 @@ qvq_status wait_flag(qvq_ctx *ctx, volatile uint64_t *flag, uint64_t seq) {
     const qvq_status st = wait_until([&] { return *flag >= seq; },
                                      [&](std::string &m) { return probe_stream(ctx, m); },
                                      [&](std::string &m) { return probe_comm(ctx, m); }, ctx->timeout_s, err);
-    if (st != QVQ_OK) return comm_failed(ctx, fail(ctx, st, err));
+    if (st != QVQ_OK) return wait_failed(ctx, fail(ctx, st, err));
     std::atomic_thread_fence(std::memory_order_acquire);
     return QVQ_OK;
 }
@@ -504,7 +566,7 @@ qvq_status wait_stream(qvq_ctx *ctx) {
         },
         [&](std::string &m) { return probe_stream(ctx, m); }, [&](std::string &m) { return probe_comm(ctx, m); },
         ctx->timeout_s, err);
-    if (st != QVQ_OK) return comm_failed(ctx, fail(ctx, st, err));
+    if (st != QVQ_OK) return wait_failed(ctx, fail(ctx, st, err));
     if (eq != hipSuccess) return fail(ctx, QVQ_EDEVICE, std::string("stream: ") + hipGetErrorString(eq));
     return QVQ_OK;
 }
@@ -736,6 +798,8 @@ QVQ_API void qvq_destroy(qvq_ctx *ctx) {
     dfree(ctx->d_decode);
     dfree(ctx->d_decode_stat);
     if (ctx->h_decode_stat) (void)hipHostFree(ctx->h_decode_stat);
+    if (ctx->h_stage) (void)hipHostFree(ctx->h_stage);
+    if (ctx->h_ar_stage) (void)hipHostFree(ctx->h_ar_stage);
     if (ctx->ev_ready)
         for (int l = 0; l < 32; l++)
             for (int j = 0; j < 4; j++) (void)hipEventDestroy(ctx->ev[l][j]);
@@ -755,6 +819,7 @@ QVQ_API qvq_status qvq_set_images_device(qvq_ctx *ctx, const void *d_rgb, uint32
     uint32_t D;
     qvq_status st = check_image_args(ctx, n_images, xSize, ySize, bw, bh, N, D);
     if (st != QVQ_OK) return st;
+    GUARD(ctx);
     if (!d_rgb) return fail(ctx, QVQ_EINVAL, "null raster");
     HIPCHK(hipSetDevice(ctx->dev));
     if ((st = alloc_training(ctx, N, D, colorspace)) != QVQ_OK) return st;
@@ -768,6 +833,7 @@ QVQ_API qvq_status qvq_set_images(qvq_ctx *ctx, const uint8_t *rgb, uint32_t n_i
     uint32_t D;
     qvq_status st = check_image_args(ctx, n_images, xSize, ySize, bw, bh, N, D);
     if (st != QVQ_OK) return st;
+    GUARD(ctx);
     if (!rgb) return fail(ctx, QVQ_EINVAL, "null raster");
     HIPCHK(hipSetDevice(ctx->dev));
     const uint64_t bytes = (uint64_t)xSize * ySize * 3 * n_images;
@@ -789,6 +855,7 @@ QVQ_API qvq_status qvq_set_synthetic(qvq_ctx *ctx, uint32_t S, uint64_t seed0, u
     uint64_t N;
     uint32_t D;
     if (!ctx) return QVQ_EINVAL;
+    GUARD(ctx);
     if (S < 2) return fail(ctx, QVQ_EINVAL, "synthetic images need S >= 2");
     qvq_status st = check_image_args(ctx, n_images, S, S, bw, bh, N, D);
     if (st != QVQ_OK) return st;
@@ -809,6 +876,7 @@ QVQ_API qvq_status qvq_set_synthetic(qvq_ctx *ctx, uint32_t S, uint64_t seed0, u
 
 QVQ_API qvq_status qvq_set_vectors(qvq_ctx *ctx, const double *X, uint64_t n, uint32_t dim) {
     if (!ctx) return QVQ_EINVAL;
+    GUARD(ctx);
     if (!X || n == 0 || dim == 0) return fail(ctx, QVQ_EINVAL, "empty training set");
     if (dim > 64) return fail(ctx, QVQ_EINVAL, "block dimension above 64 (3*w*h) is not supported");
     // Recognise the colour space from the values: every value must be a byte's image
@@ -853,6 +921,7 @@ QVQ_API qvq_status qvq_lbg(qvq_ctx *ctx, uint32_t bits, double eps, double *code
                            double *distortion) {
     (void)eps;   // cannot change the outputs: one Lloyd step per level
     if (!ctx) return QVQ_EINVAL;
+    GUARD(ctx);
     if (ctx->N == 0) return fail(ctx, QVQ_ESTATE, "no training set");
     if (bits > 20) return fail(ctx, QVQ_EINVAL, "bits must be <= 20");
     HIPCHK(hipSetDevice(ctx->dev));
@@ -869,7 +938,7 @@ QVQ_API qvq_status qvq_lbg(qvq_ctx *ctx, uint32_t bits, double eps, double *code
     double *d_dist = ctx->d_dist_part;
     HIPCHK(launch_mean_sums(ctx->stream, ctx->Dp, ctx->d_codes, ctx->N, ctx->D, ctx->d_plut, ctx->d_mean,
                             ctx->d_counters, 2 * 33 + 2, d_dist, ctx->xsq, (double)ctx->N));
-    if (ctx->comm) NCCLCHK(ncclAllReduce(d_dist, d_dist, 2, ncclDouble, ncclSum, ctx->comm, ctx->stream));
+    if ((st = all_reduce(ctx, d_dist, 2, true)) != QVQ_OK) return st;
     if ((st = all_reduce_sums(ctx, 1, ctx->d_mean, MEAN_COPIES)) != QVQ_OK) {
         (void)hipMemsetAsync(ctx->d_mean, 0, MEAN_COPIES * (2 * 64 + 1) * 8, ctx->stream);   // keep it clear for the next call
         return st;
@@ -964,6 +1033,7 @@ QVQ_API qvq_status qvq_lbg(qvq_ctx *ctx, uint32_t bits, double eps, double *code
 
 QVQ_API qvq_status qvq_assign(qvq_ctx *ctx, const double *C, uint32_t K, uint32_t *assign) {
     if (!ctx) return QVQ_EINVAL;
+    GUARD(ctx);
     if (ctx->N == 0) return fail(ctx, QVQ_ESTATE, "no training set");
     if (!C || K == 0) return fail(ctx, QVQ_EINVAL, "empty codebook");
     HIPCHK(hipSetDevice(ctx->dev));
@@ -986,6 +1056,7 @@ QVQ_API qvq_status qvq_assign(qvq_ctx *ctx, const double *C, uint32_t K, uint32_
 
 QVQ_API qvq_status qvq_update(qvq_ctx *ctx, const uint32_t *assign, uint32_t K, double *C_out, uint64_t *counts) {
     if (!ctx) return QVQ_EINVAL;
+    GUARD(ctx);
     if (ctx->N == 0) return fail(ctx, QVQ_ESTATE, "no training set");
     if (!assign || K == 0) return fail(ctx, QVQ_EINVAL, "empty assignment");
     for (uint64_t i = 0; i < ctx->N; i++)
@@ -998,12 +1069,17 @@ QVQ_API qvq_status qvq_update(qvq_ctx *ctx, const uint32_t *assign, uint32_t K, 
     if ((st = all_reduce_sums(ctx, K)) != QVQ_OK) return st;
     const Terms &T = ctx->terms;
     HIPCHK(launch_finalize(ctx->stream, ctx->d_sums, K, ctx->D, T.R, T.bias, T.scale, ctx->d_C64_cent));
-    if (C_out)
-        HIPCHK(hipMemcpyAsync(C_out, ctx->d_C64_cent, (uint64_t)K * ctx->D * 8, hipMemcpyDeviceToHost, ctx->stream));
-    if (counts)
-        HIPCHK(hipMemcpyAsync(counts, ctx->d_sums + 2 * (uint64_t)K * ctx->D, (uint64_t)K * 8, hipMemcpyDeviceToHost,
-                              ctx->stream));
-    return wait_stream(ctx);   // bounded: the all-reduce above may wait on peer ranks
+    // results land in context-owned pinned memory and reach the caller only after the bounded
+    // wait succeeds (a failed wait can leave these copies queued: wait_failed)
+    const uint64_t cB = (uint64_t)K * ctx->D * 8, nB = (uint64_t)K * 8;
+    if ((st = ensure_pinned(ctx, ctx->h_stage, ctx->stage_bytes, cB + nB)) != QVQ_OK) return st;
+    uint8_t *stage = static_cast<uint8_t *>(ctx->h_stage);
+    HIPCHK(hipMemcpyAsync(stage, ctx->d_C64_cent, cB, hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(hipMemcpyAsync(stage + cB, ctx->d_sums + 2 * (uint64_t)K * ctx->D, nB, hipMemcpyDeviceToHost, ctx->stream));
+    if ((st = wait_stream(ctx)) != QVQ_OK) return st;   // bounded: the all-reduce may wait on peer ranks
+    if (C_out) std::memcpy(C_out, stage, cB);
+    if (counts) std::memcpy(counts, stage + cB, nB);
+    return QVQ_OK;
 }
 
 // ---------------------------------------------------------------------------------------
@@ -1048,8 +1124,14 @@ QVQ_API qvq_status qvq_decode_device(qvq_ctx *ctx, const void *d_codebook, uint3
                                      void *d_rgb, void *stream) {
     qvq_status st = check_decode_args(ctx, K, nblocks, xSize, ySize, bw, bh);
     if (st != QVQ_OK) return st;
+    GUARD(ctx);
     if (!d_codebook || !d_assign || !d_rgb) return fail(ctx, QVQ_EINVAL, "decode: null pointer");
+    if ((uintptr_t)d_assign % 4) return fail(ctx, QVQ_EINVAL, "decode: assignment pointer not 4-byte aligned");
     HIPCHK(hipSetDevice(ctx->dev));
+    // ordered after the engine's own queued work (e.g. the qvq_lbg that wrote d_assign) on
+    // any stream the caller names, the legacy null stream included
+    HIPCHK(hipEventRecord(ctx->ev_sync, ctx->stream));
+    HIPCHK(hipStreamWaitEvent((hipStream_t)stream, ctx->ev_sync, 0));
     return run_decode(ctx, (hipStream_t)stream, (const uint8_t *)d_codebook, K, (const uint32_t *)d_assign, xSize,
                       ySize, bw, bh, (uint8_t *)d_rgb, nullptr, nullptr);
 }
@@ -1064,6 +1146,7 @@ QVQ_API qvq_status qvq_decode_mse(qvq_ctx *ctx, const uint8_t *codebook, uint32_
                                   uint8_t *rgb, const uint8_t *orig, double *mse) {
     qvq_status st = check_decode_args(ctx, K, nblocks, xSize, ySize, bw, bh);
     if (st != QVQ_OK) return st;
+    GUARD(ctx);
     if (!codebook || !assign || (!rgb && !mse) || (mse && !orig))
         return fail(ctx, QVQ_EINVAL, "decode: null pointer");
     HIPCHK(hipSetDevice(ctx->dev));
@@ -1099,12 +1182,15 @@ QVQ_API qvq_status qvq_comm_unique_id(uint8_t id[128]) {
 }
 
 QVQ_API qvq_status qvq_comm_init(qvq_ctx *ctx, int nranks, int rank, const uint8_t id[128]) {
-    if (!ctx || !id || nranks < 1 || rank < 0 || rank >= nranks) return QVQ_EINVAL;
+    GUARD(ctx);
+    if (!id || nranks < 1 || rank < 0 || rank >= nranks) return QVQ_EINVAL;
     HIPCHK(hipSetDevice(ctx->dev));
     if (ctx->comm) {
         ncclCommDestroy(ctx->comm);
         ctx->comm = nullptr;
     }
+    ctx->host_ar = nullptr;
+    ctx->host_ar_user = nullptr;
     ctx->nranks = 1;
     ctx->rank = 0;
     // a communicator even for one rank: the caller asked for the collective path (it is
@@ -1114,6 +1200,29 @@ QVQ_API qvq_status qvq_comm_init(qvq_ctx *ctx, int nranks, int rank, const uint8
     NCCLCHK(ncclCommInitRank(&ctx->comm, nranks, u, rank));
     ctx->nranks = nranks;
     ctx->rank = rank;
+    return QVQ_OK;
+}
+
+QVQ_API qvq_status qvq_comm_init_host(qvq_ctx *ctx, int nranks, int rank, qvq_allreduce_fn fn, void *user) {
+    GUARD(ctx);
+    if (!fn || nranks < 1 || rank < 0 || rank >= nranks) return QVQ_EINVAL;
+    if (ctx->comm) {
+        HIPCHK(hipSetDevice(ctx->dev));
+        ncclCommDestroy(ctx->comm);
+        ctx->comm = nullptr;
+    }
+    ctx->host_ar = fn;
+    ctx->host_ar_user = user;
+    ctx->nranks = nranks;
+    ctx->rank = rank;
+    return QVQ_OK;
+}
+
+QVQ_API qvq_status qvq_comm_info(const qvq_ctx *ctx, int *nranks, int *rank, int *kind) {
+    if (!ctx) return QVQ_EINVAL;
+    if (nranks) *nranks = ctx->nranks;
+    if (rank) *rank = ctx->rank;
+    if (kind) *kind = ctx->comm ? QVQ_COMM_RCCL : ctx->host_ar ? QVQ_COMM_HOST : QVQ_COMM_NONE;
     return QVQ_OK;
 }
 

@@ -1274,6 +1274,19 @@ __device__ inline void decode_finish(const DecodeArgs &a, uint64_t sq, bool bad)
     }
 }
 
+// The codebook's n bytes into LDS: whole words when the source is 4-byte aligned, the tail
+// (n % 4 bytes) and any unaligned source byte by byte -- never past cb + n (a
+// caller's device codebook may be a slice of odd length).
+__device__ inline void stage_codebook(uint8_t *scb, const uint8_t *cb, uint32_t n) {
+    uint32_t head = 0;
+    if (((uintptr_t)cb & 3) == 0) {
+        head = n & ~3u;
+        for (uint32_t i = threadIdx.x; i < head / 4; i += blockDim.x)
+            reinterpret_cast<uint32_t *>(scb)[i] = reinterpret_cast<const uint32_t *>(cb)[i];
+    }
+    for (uint32_t i = head + threadIdx.x; i < n; i += blockDim.x) scb[i] = cb[i];
+}
+
 // Rows of ys % 8 == 0 pixels: thread (x, q) produces pixels y = 8q .. 8q + 7 of raster row x,
 // 24 contiguous 8-byte-aligned bytes stored as three dwordx2 (and the original read the same
 // way for the MSE).  The codebook sits in LDS when it is small (C3: 12 KB).
@@ -1281,9 +1294,7 @@ template <bool LDSCB>
 __global__ __launch_bounds__(256) void decode_rows_kernel(DecodeArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t scb[];
     if (LDSCB) {
-        const uint32_t n4 = (a.K * a.D + 3) / 4;
-        for (uint32_t i = threadIdx.x; i < n4; i += 256)
-            reinterpret_cast<uint32_t *>(scb)[i] = reinterpret_cast<const uint32_t *>(a.cb)[i];
+        stage_codebook(scb, a.cb, a.K * a.D);
         __syncthreads();
     }
     const uint8_t *cb = LDSCB ? scb : a.cb;
@@ -1340,9 +1351,7 @@ __global__ __launch_bounds__(256) void decode_rows_h_kernel(DecodeArgs a, uint32
     const int lane = threadIdx.x & 63;
     uint2 *stage = reinterpret_cast<uint2 *>(scb + stage_off) + (threadIdx.x >> 6) * 192;   // 1536 B per wave
     if (LDSCB) {
-        const uint32_t n4 = (a.K * a.D + 3) / 4;
-        for (uint32_t i = threadIdx.x; i < n4; i += 256)
-            reinterpret_cast<uint32_t *>(scb)[i] = reinterpret_cast<const uint32_t *>(a.cb)[i];
+        stage_codebook(scb, a.cb, a.K * a.D);
         __syncthreads();
     }
     const uint8_t *cb = LDSCB ? scb : a.cb;
@@ -1483,7 +1492,11 @@ hipError_t launch_decode(hipStream_t s, const uint8_t *cb, uint32_t K, uint32_t 
     a.yspan = a.hB * h;
     a.overhang = a.yspan - ys;
     a.rgb = rgb, a.orig = orig, a.sqerr = (unsigned long long *)sqerr, a.bad = bad;
-    if (ys % 8 == 0 && (uint64_t)xs * ys < (1ull << 40)) {
+    // the row kernels store (and read the original) in 8-byte pieces and load 8 / H indices per
+    // vector load: caller pointers (qvq_decode_device) without that alignment take the
+    // per-pixel kernel
+    const bool aligned = (uintptr_t)rgb % 8 == 0 && (!orig || (uintptr_t)orig % 8 == 0) && (uintptr_t)A % 16 == 0;
+    if (aligned && ys % 8 == 0 && (uint64_t)xs * ys < (1ull << 40)) {
         const uint64_t items = (uint64_t)xs * (ys / 8);
         const size_t cbB = (size_t)K * D;
         const bool lds = cbB <= 48 * 1024;

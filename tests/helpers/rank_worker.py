@@ -1,0 +1,56 @@
+"""One rank of the world-N GPU test (tests/test_gpu_multigpu.py): N of these processes share
+GPU 0, exchange the per-level sums through the engine's test-only host communicator
+(qvq_comm_init_host) over torch.distributed's gloo backend, and each runs qvq_lbg on its own
+shard of the rows -- the sharded schedule of SURVEY.md 8(e) (reference loops
+src/Quantizer.cpp:27-31 assign, :80-86 fix), executed for real.
+
+    python rank_worker.py RANK WORLD PORT CASE OUT.npz
+CASE: c2 -- the C2 image (512^2, 2x2) split into contiguous row ranges (qvq_set_vectors);
+      c5 -- the reduced C5 batch (4 x 512^2 images, 2x2), whole images per rank (qvq_set_synthetic).
+"""
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, ROOT)
+
+
+def shard(n, world, rank):
+    return n * rank // world, n * (rank + 1) // world
+
+
+def main():
+    rank, world, port, case, out = int(sys.argv[1]), int(sys.argv[2]), sys.argv[3], sys.argv[4], sys.argv[5]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=port)
+    import torch
+    import torch.distributed as dist
+    import quant_amd
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+
+    def allreduce(arr):
+        t = torch.from_numpy(arr.view(np.int64) if arr.dtype == np.uint64 else arr)   # shares arr's memory
+        dist.all_reduce(t)   # int64 sums wrap like the engine's u64 sums
+
+    eng = quant_amd.Engine(0)
+    eng.comm_init_host(world, rank, allreduce)
+    if case == "c2":
+        from oracle import oracle
+        X, _ = oracle.tile(oracle.gen_image(512, 0x5EED), 512, 512, 2, 2)
+        lo, hi = shard(X.shape[0], world, rank)
+        eng.set_vectors(X[lo:hi])
+    elif case == "c5":
+        lo, hi = shard(4, world, rank)
+        eng.set_synthetic(512, 0x5EED + lo, hi - lo, 2, 2)
+    else:
+        raise SystemExit("unknown case " + case)
+    C, A, d = eng.lbg(10)
+    C2, cnt = eng.update(A, 1 << 10)   # the single-step update goes through the exchange too
+    np.savez(out, C=C, A=A, d=np.array([d]), C2=C2, cnt=cnt, info=np.array(eng.comm_info()))
+    eng.close()
+    dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -7,6 +7,11 @@ exchange runs here through a real one-rank RCCL communicator (qvq_comm_init(1, 0
 results must equal the communicator-free run bit for bit -- the property that makes the
 1/2/4/8-GPU codebooks identical (exact integer sums).  The reference loops
 being sharded are src/Quantizer.cpp:24-32 (assign) and :72-87 (centroids)."""
+import os
+import socket
+import subprocess
+import sys
+
 import numpy as np
 import pytest
 
@@ -75,3 +80,84 @@ def test_c5_full_batch_properties():
         C4, A4, d4 = eng.lbg(bits)
         np.testing.assert_array_equal(C, C4)
         assert oracle.sha16(A4) == h_first
+
+
+def _run_ranks(world, case, tmp_path):
+    """world rank processes (tests/helpers/rank_worker.py) sharing GPU 0 through the host
+    communicator; returns each rank's results."""
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = str(s.getsockname()[1])
+    worker = os.path.join(os.path.dirname(os.path.abspath(__file__)), "helpers", "rank_worker.py")
+    outs = [str(tmp_path / ("rank%d.npz" % r)) for r in range(world)]
+    procs = [subprocess.Popen([sys.executable, worker, str(r), str(world), port, case, outs[r]]) for r in range(world)]
+    try:
+        codes = [p.wait(timeout=240) for p in procs]
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+    assert codes == [0] * world, codes
+    return [dict(np.load(o)) for o in outs]
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("world", [2, 3])
+def test_sharded_ranks_bit_identical_c2(engine, tmp_path, world):
+    """The N>1 schedule executed: C2's rows split over `world` processes (contiguous ranges,
+    one shared GPU, the per-level exchange through gloo).  Every rank gets the 1-rank codebook
+    and distortion bit for bit, the ranks' indices concatenate to the 1-rank indices, and all
+    equal the oracle (exact-sum rule; the Kahan rule's indices too)."""
+    X, _ = oracle.tile(oracle.gen_image(512, 0x5EED), 512, 512, 2, 2)
+    engine.set_vectors(X)
+    C0, A0, d0 = engine.lbg(10)
+    C_x, A_x, d_x = oracle.lbg(X, 10, sum_mode=1)
+    np.testing.assert_array_equal(A0, A_x)
+    np.testing.assert_array_equal(C0, C_x)
+    res = _run_ranks(world, "c2", tmp_path)
+    for r in res:
+        assert r["info"][0] == world and r["info"][2] == 2   # host communicator, world ranks
+        np.testing.assert_array_equal(r["C"], C0)
+        np.testing.assert_array_equal(r["C2"], C0)
+        assert float(r["d"][0]) == d0
+        assert int(r["cnt"].sum()) == X.shape[0]
+    np.testing.assert_array_equal(np.concatenate([r["A"] for r in res]), A0)
+
+
+@pytest.mark.timeout(300)
+def test_sharded_ranks_bit_identical_c5_slice(engine, tmp_path):
+    """The reduced C5 batch (4 x 512^2) with whole images per rank, world 2: identical to the
+    one-rank run over the concatenation and to the oracle."""
+    engine.set_synthetic(512, 0x5EED, 4, 2, 2)
+    C0, A0, d0 = engine.lbg(10)
+    imgs = [oracle.gen_image(512, 0x5EED + b) for b in range(4)]
+    X = np.concatenate([oracle.tile(im, 512, 512, 2, 2)[0] for im in imgs])
+    C_x, A_x, _ = oracle.lbg(X, 10, sum_mode=1)
+    np.testing.assert_array_equal(A0, A_x)
+    np.testing.assert_array_equal(C0, C_x)
+    res = _run_ranks(2, "c5", tmp_path)
+    for r in res:
+        np.testing.assert_array_equal(r["C"], C0)
+        assert float(r["d"][0]) == d0
+    np.testing.assert_array_equal(np.concatenate([r["A"] for r in res]), A0)
+
+
+def test_failed_wait_poisons_the_context():
+    """a bounded wait that fails while work is still queued must not let results land
+    in caller memory later nor let the next call reuse the context's scratch under running kernels.
+    A 128-image quantize (~130 ms; the wait consults its deadline every 20 ms) against a 1 us timeout: the call fails, the context refuses
+    further work with QVQ_ESTATE, and a fresh context works."""
+    import quant_amd
+    with quant_amd.Engine(0) as eng:
+        eng.set_synthetic(4096, 0x5EED, 128, 2, 2)
+        eng.set_timeout(1e-6)
+        with pytest.raises(quant_amd.QVQError) as e:
+            eng.lbg(10, want_assign=False)
+        assert e.value.status == 3   # QVQ_EDEVICE: timed out without a communicator
+        with pytest.raises(quant_amd.QVQError) as e2:
+            eng.lbg(10, want_assign=False)
+        assert e2.value.status == 6   # QVQ_ESTATE
+    with quant_amd.Engine(0) as eng:
+        eng.set_synthetic(512, 0x5EED, 1, 2, 2)
+        C, A, d = eng.lbg(4)
+        assert A.max() < 16

@@ -60,3 +60,31 @@ def test_sharded_sums_equal_single_process():
     ref = oracle.centroids(X, A, 32, sum_mode=1)
     for r in range(world):
         np.testing.assert_array_equal(res[r], ref)
+
+
+def test_bench_launches_ranks_dry_run():
+    """bench.py --gpus N without a launcher starts N rank processes that join the gloo control
+    plane (the driver's `python bench.py --gpus N` form); --dry-run keeps them off the GPU."""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    for n in (2, 3):
+        out = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", str(n), "--dry-run"],
+                             capture_output=True, text=True, timeout=300, env=env, cwd=root)
+        assert out.returncode == 0, out.stderr[-2000:]
+        line = json.loads([l for l in out.stdout.splitlines() if l.startswith("{")][-1])
+        assert line["n_gpus"] == n and line["ranks_joined"] == list(range(n))
+        assert len(set(line["pids"])) == n and sum(line["c5_images_per_rank"]) == 64
+
+
+def test_bench_refuses_mismatched_world():
+    """Under a launcher, WORLD_SIZE must equal --gpus (a mis-launched run must not look valid)."""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
+    out = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--dry-run"],
+                         capture_output=True, text=True, timeout=120, env=env, cwd=root)
+    assert out.returncode != 0 and "WORLD_SIZE=1 but --gpus 2" in out.stderr
