@@ -210,11 +210,11 @@ hipError_t launch_copy_out(hipStream_t s, const void *src0, void *dst0, uint64_t
 // Mean sums (K = 1): block b adds into copy b mod MEAN_COPIES of [hi D][lo D][n] (stride
 // 2D + 1; n in copy 0 only), so the blocks' closing atomics spread over MEAN_COPIES addresses
 // per component; the K = 1 finalize adds the copies.  Also clears zero[0..n_zero) and sets
-// dist[0..1] = x0, x1.
+// dist[0] = sum ||x||^2 and dist[1] = rows from the byte histogram hist (values v64).
 constexpr uint32_t MEAN_COPIES = 8;
 hipError_t launch_mean_sums(hipStream_t s, uint32_t Dp, const uint8_t *codes, uint64_t N, uint32_t D,
                             const uint64_t *plut, uint64_t *sums, unsigned *zero, uint32_t n_zero, double *dist,
-                            double x0, double x1);
+                            const uint64_t *hist, const double *v64);
 // Centroids of the reduced sums (C_cent [K][D]); with split also the next level's K' = 2K
 // code vectors (C64n and, if host_cb, mapped host memory) and their search tables (see
 // launch_prep) padded to Kpad_next; without split, given dist_out, dist_out[0] =

@@ -90,8 +90,7 @@ struct qvq_ctx {
     uint64_t *d_plut = nullptr;
     uint32_t *d_A = nullptr, *d_flags = nullptr, *d_ties = nullptr;
     unsigned *d_counters = nullptr;   // per level: [2l] flagged rows, [2l+1] kd-tree ties; [66], [67] block counters
-    double xsq = 0;                   // sum over rows of ||x||^2 (closed-form distortion)
-    uint64_t *d_hist = nullptr;
+    uint64_t *d_hist = nullptr;       // byte histogram [256] | its all-reduced copy [256]
 
     // level buffers
     uint32_t Kcap = 0;
@@ -686,15 +685,11 @@ qvq_status run_level(qvq_ctx *ctx, uint32_t K, int slot, bool sums_out, const do
     return QVQ_OK;
 }
 
-// sum ||x||^2 over the resident rows, exactly from the byte histogram.
+// The byte histogram of the resident rows (kept on the device: qvq_lbg derives sum ||x||^2 and
+// the row count from it, after summing it over the ranks).
 qvq_status compute_xsq(qvq_ctx *ctx) {
-    uint64_t hist[256];
     HIPCHK(launch_byte_hist(ctx->stream, ctx->d_codes, ctx->N, ctx->D, ctx->Dp, ctx->d_hist));
-    HIPCHK(hipMemcpyAsync(hist, ctx->d_hist, sizeof(hist), hipMemcpyDeviceToHost, ctx->stream));
     HIPCHK(hipStreamSynchronize(ctx->stream));
-    long double x = 0;
-    for (int b = 0; b < 256; b++) x += (long double)hist[b] * ctx->terms.v64[b] * ctx->terms.v64[b];
-    ctx->xsq = (double)x;
     return QVQ_OK;
 }
 
@@ -760,7 +755,7 @@ QVQ_API qvq_status qvq_create(int hip_device, qvq_ctx **out) {
     if ((e = hipHostGetDevicePointer((void **)&ctx->dh_ready, ctx->h_ready, 0)) != hipSuccess)
         return bail(e, "hipHostGetDevicePointer");
     if ((e = hipMalloc(&ctx->d_counters, (2 * 33 + 2) * sizeof(unsigned))) != hipSuccess) return bail(e, "hipMalloc");
-    if ((e = hipMalloc(&ctx->d_hist, 256 * 8)) != hipSuccess) return bail(e, "hipMalloc");
+    if ((e = hipMalloc(&ctx->d_hist, 512 * 8)) != hipSuccess) return bail(e, "hipMalloc");
     if ((e = hipMalloc(&ctx->d_decode_stat, 16)) != hipSuccess) return bail(e, "hipMalloc");
     if ((e = hipHostMalloc(&ctx->h_decode_stat, 16, hipHostMallocDefault)) != hipSuccess) return bail(e, "hipHostMalloc");
     if ((e = hipMalloc(&ctx->d_dist_part, 8192 * 8)) != hipSuccess) return bail(e, "hipMalloc");
@@ -936,9 +931,16 @@ QVQ_API qvq_status qvq_lbg(qvq_ctx *ctx, uint32_t bits, double eps, double *code
     // The mean kernel also clears the counters and writes [sum ||x||^2, rows] for the
     // closed-form distortion (summed over all ranks below).
     double *d_dist = ctx->d_dist_part;
+    // sum ||x||^2 and the row count come from the byte histogram (qvq_set_*), all-reduced as
+    // integers first: the distortion is then the same bits for every rank count
+    const uint64_t *hist = ctx->d_hist;
+    if (ctx->comm || ctx->host_ar) {
+        HIPCHK(hipMemcpyAsync(ctx->d_hist + 256, ctx->d_hist, 256 * 8, hipMemcpyDeviceToDevice, ctx->stream));
+        if ((st = all_reduce(ctx, ctx->d_hist + 256, 256, false)) != QVQ_OK) return st;
+        hist = ctx->d_hist + 256;
+    }
     HIPCHK(launch_mean_sums(ctx->stream, ctx->Dp, ctx->d_codes, ctx->N, ctx->D, ctx->d_plut, ctx->d_mean,
-                            ctx->d_counters, 2 * 33 + 2, d_dist, ctx->xsq, (double)ctx->N));
-    if ((st = all_reduce(ctx, d_dist, 2, true)) != QVQ_OK) return st;
+                            ctx->d_counters, 2 * 33 + 2, d_dist, hist, ctx->d_lut64));
     if ((st = all_reduce_sums(ctx, 1, ctx->d_mean, MEAN_COPIES)) != QVQ_OK) {
         (void)hipMemsetAsync(ctx->d_mean, 0, MEAN_COPIES * (2 * 64 + 1) * 8, ctx->stream);   // keep it clear for the next call
         return st;

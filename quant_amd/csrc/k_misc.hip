@@ -611,9 +611,49 @@ constexpr int MEAN_U = 4;   // groups of 4 rows in flight per thread
 struct MeanInit {
     unsigned *zero;     // n_zero counters to clear
     uint32_t n_zero;
-    double *dist;       // dist[0..1] = x0, x1
-    double x0, x1;
+    double *dist;       // dist[0..1] = sum ||x||^2, rows (from the byte histogram)
+    const uint64_t *hist;   // byte histogram of the training set (over all ranks)
+    const double *v64;      // byte -> value
 };
+
+// dist[0] = sum_b hist[b] v(b)^2 and dist[1] = sum_b hist[b] / D, by one wave in a fixed order
+// (double-double terms and a fixed lane tree): a function of the histogram only, so every rank
+// count gives the same bits (the histogram is all-reduced exactly, as integers).
+__device__ inline void dd_add(double &h, double &l, double b, double bl) {
+    const double s = h + b, bb = s - h;
+    const double e = (h - (s - bb)) + (b - bb);
+    const double t = e + l + bl;
+    h = s + t;
+    l = t - (h - s);
+}
+__device__ void hist_moments(const uint64_t *hist, const double *v64, uint32_t D, double *dist) {
+    const int lane = threadIdx.x;   // wave 0
+    double h = 0, l = 0;
+    uint64_t n = 0;
+    for (int b = lane; b < 256; b += 64) {
+        const double c = (double)hist[b];   // exact: < 2^53
+        const double v2 = v64[b] * v64[b], v2l = __fma_rn(v64[b], v64[b], -v2);
+        const double p = c * v2, pl = __fma_rn(c, v2, -p) + c * v2l;
+        dd_add(h, l, p, pl);
+        n += hist[b];
+    }
+    for (int off = 32; off >= 1; off >>= 1) {
+        const double oh = __shfl_xor(h, off), ol = __shfl_xor(l, off);
+        const uint64_t on = __shfl_xor(n, off);
+        // both partners add the same pair in the same order: lane-independent result
+        if (lane & off) dd_add(h, l, oh, ol);
+        else {
+            double hh = oh, ll = ol;
+            dd_add(hh, ll, h, l);
+            h = hh, l = ll;
+        }
+        n += on;
+    }
+    if (lane == 0) {
+        dist[0] = h + l;
+        dist[1] = (double)(n / D);
+    }
+}
 // Per thread: the high parts u = b ^ 0x80 of the four components of a word are added two at a
 // time as 16-bit fields (u of components 4q, 4q+2 in ue[q], of 4q+1, 4q+3 in uo[q]: three VALU
 // per word), the low parts (<= 128 each) from a 256-BYTE LDS table (ds_read_u8: at most two
@@ -628,11 +668,8 @@ __global__ __launch_bounds__(MEAN_THREADS) void mean_sums_kernel(const uint8_t *
     __shared__ uint32_t red[MEAN_THREADS / 64][DP][2];
     if (threadIdx.x < 256) lo8[threadIdx.x] = (uint8_t)(plut[threadIdx.x] & 0xFF);
     if (blockIdx.x == 0) {
-        if (threadIdx.x == 0) {
-            sums[2 * D] = N;   // cnt[0]
-            init.dist[0] = init.x0;
-            init.dist[1] = init.x1;
-        }
+        if (threadIdx.x == 0) sums[2 * D] = N;   // cnt[0]
+        if (threadIdx.x < 64) hist_moments(init.hist, init.v64, D, init.dist);
         if (threadIdx.x < init.n_zero) init.zero[threadIdx.x] = 0;
     }
     __syncthreads();
@@ -777,7 +814,7 @@ __global__ __launch_bounds__(MEAN_THREADS) void mean_sums_kernel(const uint8_t *
 
 hipError_t launch_mean_sums(hipStream_t s, uint32_t Dp, const uint8_t *codes, uint64_t N, uint32_t D,
                             const uint64_t *plut, uint64_t *sums, unsigned *zero, uint32_t n_zero, double *dist,
-                            double x0, double x1) {
+                            const uint64_t *hist, const double *v64) {
     if (n_zero > MEAN_THREADS) return hipErrorInvalidValue;
     // one block per CU (few same-address atomics at the end), more only where a thread would
     // otherwise take over MEAN_ROWS_PER_THREAD rows (u32 fields)
@@ -787,7 +824,7 @@ hipError_t launch_mean_sums(hipStream_t s, uint32_t Dp, const uint8_t *codes, ui
     const uint64_t grid = std::max<uint64_t>(std::max<uint64_t>(grid_min, 1),
                                              std::min<uint64_t>((N + 4 * MEAN_THREADS - 1) / (4 * MEAN_THREADS), grid_cap));
     if (grid > 0x7FFFFFFFull) return hipErrorInvalidValue;
-    const MeanInit init{zero, n_zero, dist, x0, x1};
+    const MeanInit init{zero, n_zero, dist, hist, v64};
     switch (Dp) {
 #define X(DPV)                                                                                              \
     case DPV:                                                                                               \
