@@ -87,11 +87,21 @@ QVQ_API qvq_status qvq_set_images_device(qvq_ctx *ctx, const void *d_rgb, uint32
 QVQ_API qvq_status qvq_set_synthetic(qvq_ctx *ctx, uint32_t S, uint64_t seed0, uint32_t n_images, uint32_t bw,
                                      uint32_t bh, int colorspace);
 /*
- * Training set, way 2: flat fp64 N x dim (the AbstractQuantizer path).  Every value must
- * be one the NORMAL or SCALED colour space produces from a byte (or 0.0); other data
- * returns QVQ_EUNSUPPORTED.
+ * Training set, way 2: flat fp64 N x dim (the AbstractQuantizer path, include/Quantizer.hpp:10-16).
+ * When every value is one the NORMAL or SCALED colour space produces from a byte (or 0.0) the
+ * fast path applies (exact integer sums: centroids within 1 ulp of the reference's Kahan sums).
+ * Any other data (arbitrary finite doubles, CIE1931 values) takes the exact mode of
+ * qvq_set_vectors_exact.
  */
 QVQ_API qvq_status qvq_set_vectors(qvq_ctx *ctx, const double *X, uint64_t n, uint32_t dim);
+/*
+ * Training set in exact mode, any finite fp64 data: the reference's arithmetic bit for bit
+ * -- fp64 search in nanoflann's order with kd-tree ties, centroids as the Kahan sum of each
+ * cell's rows in ascending order times fl(1/n) (src/Quantizer.cpp:46-87), so codebook and
+ * indices equal the reference's exactly.  Sequential Kahan chains make it slower than the
+ * byte path; one rank only (QVQ_EUNSUPPORTED with a communicator).  n < 2^31.
+ */
+QVQ_API qvq_status qvq_set_vectors_exact(qvq_ctx *ctx, const double *X, uint64_t n, uint32_t dim);
 
 QVQ_API uint64_t qvq_num_vectors(const qvq_ctx *ctx);
 QVQ_API uint32_t qvq_dim(const qvq_ctx *ctx);

@@ -42,7 +42,7 @@ EXPORTED = ["qvq_create", "qvq_destroy", "qvq_last_error", "qvq_version", "qvq_s
             "qvq_dim", "qvq_lbg", "qvq_assign_device", "qvq_assign", "qvq_update",
             "qvq_comm_unique_id", "qvq_comm_init", "qvq_set_timing", "qvq_get_timings", "qvq_host_kdtree_nn",
             "qvq_host_finalize", "qvq_host_row_terms", "qvq_decode", "qvq_decode_mse", "qvq_decode_device",
-            "qvq_set_timeout", "qvq_host_wait_probe", "qvq_comm_init_host", "qvq_comm_info"]
+            "qvq_set_timeout", "qvq_host_wait_probe", "qvq_comm_init_host", "qvq_comm_info", "qvq_set_vectors_exact"]
 
 COMM_NONE, COMM_RCCL, COMM_HOST = 0, 1, 2
 # int fn(void *buf, uint64_t count, int dtype, void *user) (qvq.h, qvq_comm_init_host)
@@ -66,6 +66,7 @@ def lib():
             "qvq_set_images_device": ([P, P, u32, u32, u32, u32, u32, i], i),
             "qvq_set_synthetic": ([P, u32, u64, u32, u32, u32, i], i),
             "qvq_set_vectors": ([P, P, u64, u32], i),
+            "qvq_set_vectors_exact": ([P, P, u64, u32], i),
             "qvq_num_vectors": ([P], u64),
             "qvq_dim": ([P], u32),
             "qvq_lbg": ([P, u32, ctypes.c_double, P, P, P], i),
@@ -154,9 +155,12 @@ class Engine:
     def set_synthetic(self, S, seed0=0x5EED, n_images=1, bw=2, bh=2, colorspace=SCALED):
         _check(lib().qvq_set_synthetic(self._h, S, seed0, n_images, bw, bh, colorspace), self._h)
 
-    def set_vectors(self, X):
+    def set_vectors(self, X, exact=False):
+        """fp64 training set N x dim.  Byte-image values (NORMAL/SCALED) take the fast path; any
+        other data -- or exact=True -- the exact mode (the reference's Kahan arithmetic, qvq.h)."""
         X = np.ascontiguousarray(X, np.float64)
-        _check(lib().qvq_set_vectors(self._h, _p(X), X.shape[0], X.shape[1]), self._h)
+        fn = lib().qvq_set_vectors_exact if exact else lib().qvq_set_vectors
+        _check(fn(self._h, _p(X), X.shape[0], X.shape[1]), self._h)
 
     @property
     def n(self):

@@ -242,4 +242,19 @@ hipError_t launch_fix_rows(hipStream_t s, const uint8_t *codes, uint32_t Dp, uin
 // 256-bin histogram of the first D bytes of every row (hist zeroed first).
 hipError_t launch_byte_hist(hipStream_t s, const uint8_t *codes, uint64_t N, uint32_t D, uint32_t Dp,
                             uint64_t *hist);
+// Exact mode (k_exact.hip): fp64 rows X [N][D].
+hipError_t launch_exact_assign(hipStream_t s, const double *X, uint64_t N, uint32_t D, const double *C, uint32_t K,
+                               double tie_rel, uint32_t *A, uint32_t *ties, unsigned *tie_cnt);
+size_t exact_sort_temp_bytes(uint64_t N);
+hipError_t launch_exact_iota(hipStream_t s, uint32_t *v, uint64_t N);
+// Kahan centroids of assignment A (nullptr: the mean of all rows, K = 1) into C [K][D] and
+// counts cnt [K] (may be null); keys_out / order [N], koff [K + 1] and temp are scratch.
+hipError_t launch_exact_centroids(hipStream_t s, const double *X, uint64_t N, uint32_t D, const uint32_t *A, uint32_t K,
+                                  uint32_t *keys_out, uint32_t *iota, uint32_t *order, uint32_t *koff, void *temp,
+                                  size_t temp_bytes, double *C, uint64_t *cnt);
+hipError_t launch_exact_distortion(hipStream_t s, const double *X, uint64_t N, uint32_t D, const double *C,
+                                   const uint32_t *A, double *part, double *out);
+hipError_t launch_exact_gather(hipStream_t s, const double *X, uint32_t D, const uint32_t *rows, uint32_t n,
+                               double *out);
+hipError_t launch_exact_fix(hipStream_t s, uint32_t *A, const uint32_t *rows, const uint32_t *vals, uint32_t n);
 }  // namespace qvq

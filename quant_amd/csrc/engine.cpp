@@ -80,6 +80,15 @@ struct qvq_ctx {
     // training set
     uint64_t N = 0;
     uint32_t D = 0, Dp = 0;
+    // exact mode (qvq_set_vectors_exact, or qvq_set_vectors on values that are not byte images):
+    // the fp64 rows themselves and the reference's Kahan arithmetic (k_exact.hip)
+    bool exact = false;
+    double *d_X64 = nullptr;
+    uint32_t *d_ex_keys = nullptr, *d_ex_iota = nullptr, *d_ex_order = nullptr;
+    void *d_ex_temp = nullptr;
+    size_t ex_temp_bytes = 0;
+    uint32_t *d_ex_koff = nullptr;
+    uint32_t ex_kcap = 0;
     int cs = -1;
     Terms terms;
     int mf_t = 0;            // MFMA score scale exponent
@@ -214,6 +223,16 @@ bool use_fused(const qvq_ctx *ctx, uint32_t K) {
 }
 
 void free_training(qvq_ctx *ctx) {
+    dfree(ctx->d_X64);
+    dfree(ctx->d_ex_keys);
+    dfree(ctx->d_ex_iota);
+    dfree(ctx->d_ex_order);
+    if (ctx->d_ex_temp) (void)hipFree(ctx->d_ex_temp);
+    ctx->d_ex_temp = nullptr;
+    ctx->ex_temp_bytes = 0;
+    dfree(ctx->d_ex_koff);
+    ctx->ex_kcap = 0;
+    ctx->exact = false;
     dfree(ctx->d_sortbuf);
     dfree(ctx->d_codes);
     dfree(ctx->d_A);
@@ -902,15 +921,152 @@ QVQ_API qvq_status qvq_set_vectors(qvq_ctx *ctx, const double *X, uint64_t n, ui
             break;
         }
     }
-    if (cs_found < 0)
-        return fail(ctx, QVQ_EUNSUPPORTED,
-                    "training values are not NORMAL/SCALED colour-space values; exact device sums need them");
+    // other values (arbitrary fp64 data, CIE1931): the reference's own arithmetic (exact mode)
+    if (cs_found < 0) return qvq_set_vectors_exact(ctx, X, n, dim);
     HIPCHK(hipSetDevice(ctx->dev));
     qvq_status st = alloc_training(ctx, n, dim, cs_found);
     if (st != QVQ_OK) return st;
     HIPCHK(hipMemcpy(ctx->d_codes, codes.data(), codes.size(), hipMemcpyHostToDevice));
     return compute_xsq(ctx);
 }
+
+// ---------------------------------------------------------------------------------------
+// Exact mode (k_exact.hip): any fp64 training set, the reference's arithmetic bit for bit --
+// fp64 search in nanoflann's order with kd-tree ties, Kahan sums over each cell's rows in
+// ascending order times fl(1/n) (src/Quantizer.cpp:46-87).  One rank; host-driven levels.
+// ---------------------------------------------------------------------------------------
+QVQ_API qvq_status qvq_set_vectors_exact(qvq_ctx *ctx, const double *X, uint64_t n, uint32_t dim) {
+    if (!ctx) return QVQ_EINVAL;
+    GUARD(ctx);
+    if (!X || n == 0 || dim == 0) return fail(ctx, QVQ_EINVAL, "empty training set");
+    if (dim > 64) return fail(ctx, QVQ_EINVAL, "block dimension above 64 (3*w*h) is not supported");
+    if (n >= (1ull << 31)) return fail(ctx, QVQ_EINVAL, "exact mode: more than 2^31-1 rows");
+    for (uint64_t i = 0; i < n * dim; i++)
+        if (!std::isfinite(X[i])) return fail(ctx, QVQ_EINVAL, "exact mode: training values must be finite");
+    HIPCHK(hipSetDevice(ctx->dev));
+    free_training(ctx);
+    free_levels(ctx);
+    ctx->N = n;
+    ctx->D = dim;
+    ctx->Dp = (dim + 3) & ~3u;
+    ctx->cs = -1;
+    ctx->exact = true;
+    HIPCHK(hipMalloc(&ctx->d_X64, n * dim * 8));
+    HIPCHK(hipMalloc(&ctx->d_A, n * 4));
+    HIPCHK(hipMalloc(&ctx->d_ties, n * 4));
+    HIPCHK(hipMalloc(&ctx->d_ex_keys, n * 4));
+    HIPCHK(hipMalloc(&ctx->d_ex_iota, n * 4));
+    HIPCHK(hipMalloc(&ctx->d_ex_order, n * 4));
+    ctx->ex_temp_bytes = exact_sort_temp_bytes(n);
+    HIPCHK(hipMalloc(&ctx->d_ex_temp, std::max<size_t>(ctx->ex_temp_bytes, 16)));
+    HIPCHK(hipMemcpy(ctx->d_X64, X, n * dim * 8, hipMemcpyHostToDevice));
+    HIPCHK(launch_exact_iota(ctx->stream, ctx->d_ex_iota, n));
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+    return QVQ_OK;
+}
+
+namespace {
+
+qvq_status exact_single_rank(qvq_ctx *ctx) {
+    if (ctx->comm || ctx->host_ar)
+        return fail(ctx, QVQ_EUNSUPPORTED, "exact mode runs on one rank (Kahan sums do not split across ranks)");
+    return QVQ_OK;
+}
+
+qvq_status exact_koff(qvq_ctx *ctx, uint32_t K) {
+    if (ctx->ex_kcap >= K + 1) return QVQ_OK;
+    dfree(ctx->d_ex_koff);
+    HIPCHK(hipMalloc(&ctx->d_ex_koff, ((size_t)K + 1) * 4));
+    ctx->ex_kcap = K + 1;
+    return QVQ_OK;
+}
+
+// Assignment of every row against the K code vectors at d_C64_split (host copy hC): the
+// fp64 argmin, exact ties answered by the host kd-tree over hC.  Returns the tie count.
+qvq_status exact_assign(qvq_ctx *ctx, const double *hC, uint32_t K, unsigned &nties) {
+    const uint32_t D = ctx->D;
+    unsigned *cnt = ctx->d_counters + 1;
+    HIPCHK(hipMemsetAsync(cnt, 0, sizeof(unsigned), ctx->stream));
+    HIPCHK(launch_exact_assign(ctx->stream, ctx->d_X64, ctx->N, D, ctx->d_C64_split, K, 1e-12, ctx->d_A, ctx->d_ties,
+                               cnt));
+    HIPCHK(hipMemcpyAsync(&nties, cnt, sizeof(unsigned), hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+    if (nties == 0) return QVQ_OK;
+    const uint64_t need = (uint64_t)nties * (8 + 8ull * D);
+    if (ctx->scatter_bytes < need) {
+        dfree(ctx->d_scatter);
+        HIPCHK(hipMalloc(&ctx->d_scatter, need));
+        ctx->scatter_bytes = need;
+    }
+    uint32_t *d_vals = ctx->d_scatter;
+    double *d_rows = reinterpret_cast<double *>(ctx->d_scatter + 2 * (uint64_t)nties);
+    std::vector<uint32_t> rows(nties), vals(nties);
+    std::vector<double> q((size_t)nties * D);
+    HIPCHK(launch_exact_gather(ctx->stream, ctx->d_X64, D, ctx->d_ties, nties, d_rows));
+    HIPCHK(hipMemcpyAsync(rows.data(), ctx->d_ties, nties * 4, hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(hipMemcpyAsync(q.data(), d_rows, q.size() * 8, hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+    RefKDTree tree(hC, K, (int)D);
+    for (unsigned i = 0; i < nties; i++) vals[i] = tree.nearest(q.data() + (size_t)i * D);
+    HIPCHK(hipMemcpyAsync(d_vals, vals.data(), nties * 4, hipMemcpyHostToDevice, ctx->stream));
+    HIPCHK(launch_exact_fix(ctx->stream, ctx->d_A, ctx->d_ties, d_vals, nties));
+    HIPCHK(hipStreamSynchronize(ctx->stream));   // the host vectors must outlive the copies
+    return QVQ_OK;
+}
+
+// Centroids of assignment d_A (nullptr: the mean) into d_C64_cent, counts into cnt (device, may be null).
+qvq_status exact_centroids(qvq_ctx *ctx, bool mean, uint32_t K, uint64_t *cnt) {
+    qvq_status st = exact_koff(ctx, K);
+    if (st != QVQ_OK) return st;
+    HIPCHK(launch_exact_centroids(ctx->stream, ctx->d_X64, ctx->N, ctx->D, mean ? nullptr : ctx->d_A, K,
+                                  ctx->d_ex_keys, ctx->d_ex_iota, ctx->d_ex_order, ctx->d_ex_koff, ctx->d_ex_temp,
+                                  ctx->ex_temp_bytes, ctx->d_C64_cent, cnt));
+    return QVQ_OK;
+}
+
+qvq_status lbg_exact(qvq_ctx *ctx, uint32_t bits, double *codebook, uint32_t *assign, double *distortion) {
+    qvq_status st = exact_single_rank(ctx);
+    if (st != QVQ_OK) return st;
+    const auto t0 = std::chrono::steady_clock::now();
+    const uint32_t Kmax = 1u << bits, D = ctx->D;
+    if ((st = ensure_levels(ctx, std::max<uint32_t>(Kmax, 2))) != QVQ_OK) return st;
+    std::memset(&ctx->tm, 0, sizeof(ctx->tm));
+    ctx->tm.levels = (int)bits;
+    // codeVectors[0] = trainingSetSum() / N (src/Quantizer.cpp:129-130)
+    std::vector<double> hC((size_t)Kmax * D), hS((size_t)Kmax * D);
+    if ((st = exact_centroids(ctx, true, 1, nullptr)) != QVQ_OK) return st;
+    HIPCHK(hipMemcpyAsync(hC.data(), ctx->d_C64_cent, (size_t)D * 8, hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+    if (bits == 0) HIPCHK(hipMemsetAsync(ctx->d_A, 0, ctx->N * 4, ctx->stream));
+    for (uint32_t lvl = 1; lvl <= bits; lvl++) {
+        const uint32_t K = 1u << lvl, H = K / 2;
+        // concat(C, C), then the halves scaled by (1 + 0.2) and (1 - 0.2) (src/Quantizer.cpp:134-138)
+        for (size_t i = 0; i < (size_t)H * D; i++) {
+            hS[i] = hC[i] * (double)(1 + 0.2);
+            hS[(size_t)H * D + i] = hC[i] * (double)(1 - 0.2);
+        }
+        HIPCHK(hipMemcpyAsync(ctx->d_C64_split, hS.data(), (size_t)K * D * 8, hipMemcpyHostToDevice, ctx->stream));
+        unsigned nt = 0;
+        if ((st = exact_assign(ctx, hS.data(), K, nt)) != QVQ_OK) return st;
+        ctx->tm.host_ties[lvl - 1] = nt;
+        if ((st = exact_centroids(ctx, false, K, nullptr)) != QVQ_OK) return st;
+        HIPCHK(hipMemcpyAsync(hC.data(), ctx->d_C64_cent, (size_t)K * D * 8, hipMemcpyDeviceToHost, ctx->stream));
+        HIPCHK(hipStreamSynchronize(ctx->stream));
+    }
+    // updateDistortion after the last fix (src/Quantizer.cpp:9-22)
+    double dist = 0;
+    HIPCHK(launch_exact_distortion(ctx->stream, ctx->d_X64, ctx->N, D, ctx->d_C64_cent, ctx->d_A, ctx->d_dist_part,
+                                   ctx->d_dist_part + 4096));
+    HIPCHK(hipMemcpyAsync(&dist, ctx->d_dist_part + 4096, 8, hipMemcpyDeviceToHost, ctx->stream));
+    if (assign) HIPCHK(hipMemcpyAsync(assign, ctx->d_A, ctx->N * 4, hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+    if (codebook) std::memcpy(codebook, hC.data(), (size_t)Kmax * D * 8);
+    if (distortion) *distortion = dist;
+    ctx->tm.total_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    return QVQ_OK;
+}
+
+}  // namespace
 
 QVQ_API qvq_status qvq_lbg(qvq_ctx *ctx, uint32_t bits, double eps, double *codebook, uint32_t *assign,
                            double *distortion) {
@@ -920,6 +1076,7 @@ QVQ_API qvq_status qvq_lbg(qvq_ctx *ctx, uint32_t bits, double eps, double *code
     if (ctx->N == 0) return fail(ctx, QVQ_ESTATE, "no training set");
     if (bits > 20) return fail(ctx, QVQ_EINVAL, "bits must be <= 20");
     HIPCHK(hipSetDevice(ctx->dev));
+    if (ctx->exact) return lbg_exact(ctx, bits, codebook, assign, distortion);
     const auto t0 = std::chrono::steady_clock::now();
     const uint32_t Kmax = 1u << bits;
     qvq_status st = ensure_levels(ctx, std::max<uint32_t>(Kmax, 2));
@@ -1043,6 +1200,14 @@ QVQ_API qvq_status qvq_assign(qvq_ctx *ctx, const double *C, uint32_t K, uint32_
     if (st != QVQ_OK) return st;
     std::memset(&ctx->tm, 0, sizeof(ctx->tm));
     HIPCHK(hipMemcpy(ctx->d_C64_split, C, (uint64_t)K * ctx->D * 8, hipMemcpyHostToDevice));
+    if (ctx->exact) {
+        unsigned nt = 0;
+        if ((st = exact_assign(ctx, C, K, nt)) != QVQ_OK) return st;
+        ctx->tm.levels = 1;
+        ctx->tm.host_ties[0] = nt;
+        if (assign) HIPCHK(hipMemcpy(assign, ctx->d_A, ctx->N * 4, hipMemcpyDeviceToHost));
+        return QVQ_OK;
+    }
     HIPCHK(hipMemsetAsync(ctx->d_counters, 0, 2 * sizeof(unsigned), ctx->stream));
     if ((st = run_prep(ctx, K)) != QVQ_OK) return st;
     if ((st = run_level(ctx, K, 0, false, C, 0)) != QVQ_OK) return st;
@@ -1067,6 +1232,14 @@ QVQ_API qvq_status qvq_update(qvq_ctx *ctx, const uint32_t *assign, uint32_t K, 
     qvq_status st = ensure_levels(ctx, K);
     if (st != QVQ_OK) return st;
     HIPCHK(hipMemcpy(ctx->d_A, assign, ctx->N * 4, hipMemcpyHostToDevice));
+    if (ctx->exact) {
+        if ((st = exact_single_rank(ctx)) != QVQ_OK) return st;
+        uint64_t *d_cnt = ctx->d_sums;   // K u64 of scratch (2KD + K)
+        if ((st = exact_centroids(ctx, false, K, d_cnt)) != QVQ_OK) return st;
+        if (C_out) HIPCHK(hipMemcpyAsync(C_out, ctx->d_C64_cent, (uint64_t)K * ctx->D * 8, hipMemcpyDeviceToHost, ctx->stream));
+        if (counts) HIPCHK(hipMemcpyAsync(counts, d_cnt, (uint64_t)K * 8, hipMemcpyDeviceToHost, ctx->stream));
+        return wait_stream(ctx);
+    }
     if ((st = run_update(ctx, ctx->d_A, K)) != QVQ_OK) return st;
     if ((st = all_reduce_sums(ctx, K)) != QVQ_OK) return st;
     const Terms &T = ctx->terms;

@@ -1,0 +1,217 @@
+// k_exact.hip -- the general training-set mode: qvq_set_vectors with values that are not byte
+// images of a colour space (arbitrary fp64 data, CIE1931-like values).  The exact integer sums
+// of the byte path do not apply, so this mode reproduces the reference's own arithmetic:
+//   assign   every row against every code vector in fp64 in nanoflann's order (ref_l2_hd,
+//            nanoflann.hpp:320-345), the lexicographic (distance, index) minimum; rows whose best
+//            two are within tie_rel are exact ties and get the kd-tree's answer (host RefKDTree),
+//   update   the rows of each code vector in ascending order (a stable radix sort of the
+//            assignment, hipCUB) and one Kahan sum per (code vector, component) in that order,
+//            times fl(1/n) -- sumInArea + operator/= (src/Quantizer.cpp:59-87) under
+//            -freciprocal-math; an empty cell is the zero vector,
+//   mean     the same Kahan over all rows in order (trainingSetSum, src/Quantizer.cpp:46-57).
+// Kahan is sequential by definition: one thread per (code vector, component) chain, the row
+// loads prefetched ahead of the dependent adds.  Built with -ffp-contract=off (no FMA
+// contraction inside the compensation).
+#include <hipcub/hipcub.hpp>
+
+#include "common.hpp"
+
+namespace qvq {
+
+constexpr int EX_THREADS = 256;
+
+// A[row] = the lexicographic (fp64 distance, index) minimum over the K code vectors of C
+// ([K][D], staged in LDS when lds); rows whose best two distances are within tie_rel go to ties.
+__global__ __launch_bounds__(EX_THREADS) void exact_assign_kernel(const double *__restrict__ X, uint64_t N, uint32_t D,
+                                                                  const double *__restrict__ C, uint32_t K, bool lds,
+                                                                  double tie_rel, uint32_t *__restrict__ A,
+                                                                  uint32_t *__restrict__ ties,
+                                                                  unsigned *__restrict__ tie_cnt) {
+    extern __shared__ double cs[];
+    if (lds) {
+        for (uint32_t i = threadIdx.x; i < K * D; i += EX_THREADS) cs[i] = C[i];
+        __syncthreads();
+    }
+    const double *cb = lds ? cs : C;
+    for (uint64_t row = (uint64_t)blockIdx.x * EX_THREADS + threadIdx.x; row < N;
+         row += (uint64_t)gridDim.x * EX_THREADS) {
+        const double *x = X + row * D;
+        double d1 = INFINITY, d2 = INFINITY;
+        uint32_t k1 = 0;
+        for (uint32_t k = 0; k < K; k++) {
+            const double d = ref_l2_hd(x, cb + (size_t)k * D, (int)D);
+            if (d < d1) {   // ascending k: the first minimum is the lowest index
+                d2 = d1;
+                d1 = d;
+                k1 = k;
+            } else if (d < d2) {
+                d2 = d;
+            }
+        }
+        A[row] = k1;
+        if (d2 - d1 <= tie_rel * d1) ties[atomicAdd(tie_cnt, 1u)] = (uint32_t)row;
+    }
+}
+
+// koff[k] = first position of code vector k in the sorted keys (lower bound), koff[K] = N.
+__global__ void exact_koff_kernel(const uint32_t *__restrict__ keys, uint64_t N, uint32_t K, uint32_t *__restrict__ koff) {
+    const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k > K) return;
+    uint64_t lo = 0, hi = N;
+    while (lo < hi) {
+        const uint64_t mid = (lo + hi) / 2;
+        if (keys[mid] < k) lo = mid + 1;
+        else hi = mid;
+    }
+    koff[k] = (uint32_t)lo;
+}
+
+// C[k][d] = Kahan sum of X[row][d] over the rows of code vector k in ascending order (order
+// positions koff[k] .. koff[k+1]; order = nullptr: rows 0 .. N-1, K = 1), times fl(1/n); an
+// empty cell is 0 (sumInArea of nothing, no division).  One thread per (k, d) chain.
+__global__ __launch_bounds__(EX_THREADS) void kahan_centroids_kernel(const double *__restrict__ X, uint64_t N,
+                                                                     uint32_t D, const uint32_t *__restrict__ order,
+                                                                     const uint32_t *__restrict__ koff, uint32_t K,
+                                                                     double *__restrict__ C, uint64_t *__restrict__ cnt) {
+    const uint64_t t = (uint64_t)blockIdx.x * EX_THREADS + threadIdx.x;
+    if (t >= (uint64_t)K * D) return;
+    const uint32_t k = (uint32_t)(t / D), d = (uint32_t)(t - (uint64_t)k * D);
+    const uint64_t b = order ? koff[k] : 0, e = order ? koff[k + 1] : N;
+    double sum = 0.0, c = 0.0;
+    constexpr int U = 16;   // loads in flight ahead of the dependent Kahan chain
+    uint64_t i = b;
+    for (; i + U <= e; i += U) {
+        double v[U];
+#pragma unroll
+        for (int u = 0; u < U; u++) v[u] = X[(uint64_t)(order ? order[i + u] : i + u) * D + d];
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            const double y = v[u] - c;
+            const double s = sum + y;
+            c = (s - sum) - y;
+            sum = s;
+        }
+    }
+    for (; i < e; i++) {
+        const double y = X[(uint64_t)(order ? order[i] : i) * D + d] - c;
+        const double s = sum + y;
+        c = (s - sum) - y;
+        sum = s;
+    }
+    const uint64_t n = e - b;
+    if (n) sum *= 1.0 / (double)n;   // operator/= by a scalar under -freciprocal-math
+    C[t] = sum;
+    if (cnt && d == 0) cnt[k] = n;
+}
+
+// Per-block partials of sum_rows ||x - C[A[row]]||^2 (norm of the difference: squares added in
+// component order, include/VectorOperations.hpp:107-111); exact_sum_kernel adds them in order.
+__global__ __launch_bounds__(EX_THREADS) void exact_dist_kernel(const double *__restrict__ X, uint64_t N, uint32_t D,
+                                                                const double *__restrict__ C,
+                                                                const uint32_t *__restrict__ A,
+                                                                double *__restrict__ part) {
+    __shared__ double red[EX_THREADS];
+    double acc = 0.0;
+    for (uint64_t row = (uint64_t)blockIdx.x * EX_THREADS + threadIdx.x; row < N;
+         row += (uint64_t)gridDim.x * EX_THREADS) {
+        const double *x = X + row * D, *c = C + (uint64_t)A[row] * D;
+        double r = 0.0;
+        for (uint32_t d = 0; d < D; d++) {
+            const double e = x[d] - c[d];
+            r += e * e;
+        }
+        acc += r;
+    }
+    red[threadIdx.x] = acc;
+    __syncthreads();
+    for (int s = EX_THREADS / 2; s > 0; s >>= 1) {
+        if ((int)threadIdx.x < s) red[threadIdx.x] += red[threadIdx.x + s];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) part[blockIdx.x] = red[0];
+}
+__global__ void exact_sum_kernel(const double *__restrict__ part, uint32_t n, double scale, double *__restrict__ out) {
+    double s = 0.0;
+    for (uint32_t i = 0; i < n; i++) s += part[i];
+    *out = s * scale;
+}
+
+// out[i][d] = X[rows[i]][d] (the tie rows for the host kd-tree); A[rows[i]] = vals[i].
+__global__ void exact_gather_kernel(const double *__restrict__ X, uint32_t D, const uint32_t *__restrict__ rows,
+                                    uint32_t n, double *__restrict__ out) {
+    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t < (uint64_t)n * D) out[t] = X[(uint64_t)rows[t / D] * D + t % D];
+}
+__global__ void exact_fix_kernel(uint32_t *__restrict__ A, const uint32_t *__restrict__ rows,
+                                 const uint32_t *__restrict__ vals, uint32_t n) {
+    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t < n) A[rows[t]] = vals[t];
+}
+
+static int grid_for(uint64_t items, int cap = 4096) {
+    return (int)std::max<uint64_t>(1, std::min<uint64_t>((items + EX_THREADS - 1) / EX_THREADS, (uint64_t)cap));
+}
+
+hipError_t launch_exact_assign(hipStream_t s, const double *X, uint64_t N, uint32_t D, const double *C, uint32_t K,
+                               double tie_rel, uint32_t *A, uint32_t *ties, unsigned *tie_cnt) {
+    const bool lds = (size_t)K * D * 8 <= 64 * 1024;
+    hipLaunchKernelGGL(exact_assign_kernel, dim3(grid_for(N, 8192)), dim3(EX_THREADS), lds ? (size_t)K * D * 8 : 0, s, X,
+                       N, D, C, K, lds, tie_rel, A, ties, tie_cnt);
+    return hipGetLastError();
+}
+
+size_t exact_sort_temp_bytes(uint64_t N) {
+    size_t bytes = 0;
+    (void)hipcub::DeviceRadixSort::SortPairs(nullptr, bytes, (const uint32_t *)nullptr, (uint32_t *)nullptr,
+                                             (const uint32_t *)nullptr, (uint32_t *)nullptr, (int)N);
+    return bytes;
+}
+
+hipError_t launch_exact_centroids(hipStream_t s, const double *X, uint64_t N, uint32_t D, const uint32_t *A, uint32_t K,
+                                  uint32_t *keys_out, uint32_t *iota, uint32_t *order, uint32_t *koff, void *temp,
+                                  size_t temp_bytes, double *C, uint64_t *cnt) {
+    if (!A) {   // the mean: every row, in order
+        hipLaunchKernelGGL(kahan_centroids_kernel, dim3(grid_for((uint64_t)D)), dim3(EX_THREADS), 0, s, X, N, D,
+                           (const uint32_t *)nullptr, (const uint32_t *)nullptr, 1u, C, cnt);
+        return hipGetLastError();
+    }
+    int bits = 1;
+    while (bits < 32 && (1ull << bits) < K) bits++;
+    // stable: equal keys keep the input (ascending row) order
+    hipError_t e = hipcub::DeviceRadixSort::SortPairs(temp, temp_bytes, A, keys_out, iota, order, (int)N, 0, bits, s);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(exact_koff_kernel, dim3((K + 1 + 255) / 256), dim3(256), 0, s, keys_out, N, K, koff);
+    hipLaunchKernelGGL(kahan_centroids_kernel, dim3(grid_for((uint64_t)K * D, 1u << 30)), dim3(EX_THREADS), 0, s, X, N,
+                       D, order, koff, K, C, cnt);
+    return hipGetLastError();
+}
+
+__global__ void exact_iota_kernel(uint32_t *__restrict__ v, uint64_t N) {
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < N; i += (uint64_t)gridDim.x * blockDim.x)
+        v[i] = (uint32_t)i;
+}
+hipError_t launch_exact_iota(hipStream_t s, uint32_t *v, uint64_t N) {
+    hipLaunchKernelGGL(exact_iota_kernel, dim3(grid_for(N)), dim3(EX_THREADS), 0, s, v, N);
+    return hipGetLastError();
+}
+
+hipError_t launch_exact_distortion(hipStream_t s, const double *X, uint64_t N, uint32_t D, const double *C,
+                                   const uint32_t *A, double *part, double *out) {
+    const int g = grid_for(N, 1024);
+    hipLaunchKernelGGL(exact_dist_kernel, dim3(g), dim3(EX_THREADS), 0, s, X, N, D, C, A, part);
+    hipLaunchKernelGGL(exact_sum_kernel, dim3(1), dim3(1), 0, s, part, (uint32_t)g, 1.0 / ((double)N * (double)D), out);
+    return hipGetLastError();
+}
+
+hipError_t launch_exact_gather(hipStream_t s, const double *X, uint32_t D, const uint32_t *rows, uint32_t n,
+                               double *out) {
+    hipLaunchKernelGGL(exact_gather_kernel, dim3((unsigned)(((uint64_t)n * D + 255) / 256)), dim3(256), 0, s, X, D,
+                       rows, n, out);
+    return hipGetLastError();
+}
+hipError_t launch_exact_fix(hipStream_t s, uint32_t *A, const uint32_t *rows, const uint32_t *vals, uint32_t n) {
+    hipLaunchKernelGGL(exact_fix_kernel, dim3((n + 255) / 256), dim3(256), 0, s, A, rows, vals, n);
+    return hipGetLastError();
+}
+
+}  // namespace qvq

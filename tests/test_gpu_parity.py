@@ -99,10 +99,14 @@ def test_set_vectors_path(engine):
     np.testing.assert_array_equal(C, C_x)
 
 
-def test_set_vectors_rejects_general_data(engine):
+def test_set_vectors_rejects_bad_data(engine):
+    """Non-finite values have no reference answer to match (the exact mode, which takes any other
+    data, is tests/test_gpu_exact.py)."""
     import quant_amd
+    X = np.random.rand(100, 12)
+    X[5, 3] = np.nan
     with pytest.raises(quant_amd.QVQError):
-        engine.set_vectors(np.random.rand(100, 12))
+        engine.set_vectors(X)
 
 
 @pytest.fixture(params=["device", "host"])
