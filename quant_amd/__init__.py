@@ -89,6 +89,8 @@ def lib():
             "qvq_comm_info": ([P, ctypes.POINTER(i), ctypes.POINTER(i), ctypes.POINTER(i)], i),
         }
         for name, (args, res) in sig.items():
+            if os.environ.get("QVQ_LIB") and not hasattr(L, name):
+                continue   # an older A/B build (tools/) without this entry point
             fn = getattr(L, name)
             fn.argtypes = args
             fn.restype = res

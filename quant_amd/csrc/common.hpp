@@ -146,18 +146,24 @@ uint32_t mf_fuse_max_k();
 bool mf_can_search(uint32_t K);
 // K <= 32: expanded fp32 scores from E32 [Kp][16] = [c''(0..11) | n | 0 0 0] (the MFMA row's
 // terms in fp32; padding rows n = 1e30).
+// perm / tint (finalize's prune_order, K <= PRUNE_MAXK): the pruned tile order of the MFMA
+// search (assign_mf32_kernel PRUNE); null: every tile in index order.
 hipError_t launch_assign_mfma(hipStream_t s, int grid, bool fuse, const uint8_t *codes, uint64_t N,
                               const _Float16 *cb_rows, const float *E32, uint32_t K, const float *C32,
                               const uint64_t *plut,
                               const MfThresholds &th, uint32_t *A, uint32_t *flags, unsigned *flag_cnt,
-                              uint64_t *part, uint32_t *part_cnt);
+                              uint64_t *part, uint32_t *part_cnt, const uint32_t *perm = nullptr,
+                              const int32_t *tint = nullptr);
 // The same search on v_mfma_f32_32x32x16_f16 tiles (k_mf32.hip); launch_assign_mfma uses it
 // for K above the small-K scan whenever mf32_fits.
 bool mf32_fits(uint32_t K, bool fuse);
+bool mf32_prune_fits(uint32_t K, bool fuse);
 hipError_t launch_assign_mf32(hipStream_t s, int grid, bool fuse, const uint8_t *codes, uint64_t N,
                               const _Float16 *cb_rows, uint32_t K, const float *C32, const uint64_t *plut,
                               const MfThresholds &th, uint32_t *A, uint32_t *flags, unsigned *flag_cnt,
-                              uint64_t *part, uint32_t *part_cnt);
+                              uint64_t *part, uint32_t *part_cnt, const uint32_t *perm = nullptr,
+                              const int32_t *tint = nullptr);
+constexpr uint32_t PRUNE_MAXK_HOST = 1024;   // prune_order's capacity (k_misc.hip PRUNE_MAXK)
 // MFMA f16 search for D != 12 (wide layout), no fused sums: K >= 32, codebook staged in LDS
 // whole or in double-buffered slices.  Same flag rule as launch_assign_mfma.
 bool wide_can_search(uint32_t Dp);
@@ -225,7 +231,7 @@ hipError_t launch_finalize_prep(hipStream_t s, const uint64_t *sums, uint32_t K,
                                 int64_t bias, int scale, double *C_cent, bool split, double *C64n, uint32_t Kpad_next,
                                 double mu, double sx, int t, float *C32, _Float16 *cb_rows, float *E32,
                                 double *host_cb, double *dist_part, unsigned *done, double *dist_out, uint64_t *ready, uint64_t seq,
-                                bool zero_sums, uint32_t ncopy = 1);
+                                bool zero_sums, uint32_t ncopy = 1, uint32_t *perm = nullptr, int32_t *tint = nullptr);
 hipError_t launch_finalize(hipStream_t s, const uint64_t *sums, uint32_t K, uint32_t D, int64_t R, int64_t bias,
                            int scale, double *C_cent);
 // f16 MFMA tables (D = 12) and fp32 VALU table from an fp64 codebook of K code vectors.

@@ -108,6 +108,9 @@ struct qvq_ctx {
     float *d_C32 = nullptr;
     float *d_E32 = nullptr;   // D = 12: expanded fp32 terms for the small-K scan
     _Float16 *d_rows = nullptr;   // MFMA code-vector rows
+    uint32_t *d_perm = nullptr;   // pruned search: tile order of the split codebook (finalize's prune_order)
+    int32_t *d_tint = nullptr;    // ... and the tiles' projection envelopes
+    uint32_t perm_k = 0;          // the K whose order d_perm holds (0: none)
     uint64_t *d_part = nullptr, *d_sums = nullptr;
     uint32_t *d_part_cnt = nullptr;
     double *d_dist_part = nullptr;
@@ -116,6 +119,8 @@ struct qvq_ctx {
     uint32_t *d_scatter = nullptr;
     uint32_t *d_sortbuf = nullptr;   // sorted-order sums: idx [N] | ks [N]
     uint64_t scatter_bytes = 0;
+    uint8_t *d_raster = nullptr;          // qvq_set_images' raster upload buffer (grown on demand)
+    uint64_t raster_bytes = 0;
     uint8_t *d_decode = nullptr;          // qvq_decode scratch (grown on demand)
     uint64_t decode_bytes = 0;
     uint64_t *d_decode_stat = nullptr;    // decode: [squared error, bad-index flag]
@@ -221,6 +226,14 @@ bool use_wide(const qvq_ctx *ctx, uint32_t K) {
 bool use_fused(const qvq_ctx *ctx, uint32_t K) {
     return use_mfma(ctx, K) && K <= mf_fuse_max_k() && !env_is("QVQ_FUSE", "0");
 }
+// Pruned MFMA search (k_mf32.hip PRUNE: tiles visited outward from a chunk's projection,
+// stopped by a provable bound) for D = 12 from K = QVQ_PRUNE_MINK (default 512; 0 = off) up to
+// prune_order's capacity.  Its order is computed by the previous level's finalize.
+bool use_prune(const qvq_ctx *ctx, uint32_t K) {
+    static const uint32_t mink = std::getenv("QVQ_PRUNE_MINK") ? (uint32_t)std::atoi(std::getenv("QVQ_PRUNE_MINK")) : 512u;
+    return mink && K >= mink && K <= PRUNE_MAXK_HOST && ctx->D == MF_D && use_mfma(ctx, K) &&
+           mf32_prune_fits(K, use_fused(ctx, K));
+}
 
 void free_training(qvq_ctx *ctx) {
     dfree(ctx->d_X64);
@@ -248,6 +261,9 @@ void free_levels(qvq_ctx *ctx) {
     dfree(ctx->d_C32);
     dfree(ctx->d_E32);
     dfree(ctx->d_rows);
+    dfree(ctx->d_perm);
+    dfree(ctx->d_tint);
+    ctx->perm_k = 0;
     dfree(ctx->d_part);
     dfree(ctx->d_part_cnt);
     dfree(ctx->d_sums);
@@ -333,13 +349,15 @@ void mfma_setup(qvq_ctx *ctx) {
 
 // Allocate the per-row buffers and upload the colour-space tables.
 qvq_status alloc_training(qvq_ctx *ctx, uint64_t N, uint32_t D, int cs) {
-    free_training(ctx);
-    free_levels(ctx);
-    if (!make_terms(cs, ctx->terms)) return fail(ctx, QVQ_EUNSUPPORTED, "colour space has no exact byte sums");
     if (N == 0 || D == 0) return fail(ctx, QVQ_EINVAL, "empty training set");
     if (N >= (1ull << 32)) return fail(ctx, QVQ_EINVAL, "more than 2^32-1 rows per rank");
     const uint32_t Dp = (D + 3) & ~3u;
     if (Dp > 64) return fail(ctx, QVQ_EINVAL, "block dimension above 64 (3*w*h) is not supported");
+    // the same shape again (repeated compresses of one image size): keep every buffer
+    if (!ctx->exact && ctx->d_codes && ctx->N == N && ctx->D == D && ctx->cs == cs) return QVQ_OK;
+    free_training(ctx);
+    free_levels(ctx);
+    if (!make_terms(cs, ctx->terms)) return fail(ctx, QVQ_EUNSUPPORTED, "colour space has no exact byte sums");
     ctx->N = N;
     ctx->D = D;
     ctx->Dp = Dp;
@@ -368,6 +386,8 @@ qvq_status ensure_levels(qvq_ctx *ctx, uint32_t Kmax) {
     HIPCHK(hipMalloc(&ctx->d_C32, Kp * ctx->Dp * 4));
     if (ctx->D == MF_D) HIPCHK(hipMalloc(&ctx->d_E32, Kp * 16 * 4));
     HIPCHK(hipMalloc(&ctx->d_rows, Kp * 2 * cb_row_f16(ctx->D, ctx->Dp)));
+    HIPCHK(hipMalloc(&ctx->d_perm, Kp * 4));
+    HIPCHK(hipMalloc(&ctx->d_tint, (Kp / 32 + 1) * 8));
     // G per-CU slabs + two correction slabs (fused path: rows the recheck / kd-tree move, at
     // the new index (+) and at the search's provisional one (-))
     HIPCHK(hipMalloc(&ctx->d_part, (uint64_t)(ctx->G + 2) * KD * 8));
@@ -516,6 +536,22 @@ void build_tree(qvq_ctx *ctx, const double *hC, uint32_t K, int buf, KdView &kd)
     kd = v;
 }
 
+// Copy between a caller's host buffer and device memory at DMA speed: the host range is pinned
+// in place for the copy (hipHostRegister; a pageable hipMemcpy goes through bounce buffers at a
+// fraction of PCIe bandwidth: the 50 MB C3 raster took ~3 ms), with a plain copy as the fallback
+// (already pinned memory, or registration refused).  QVQ_H2D=pageable: the plain copy (A/B).
+// Synchronous on the context's stream.
+hipError_t host_copy(qvq_ctx *ctx, void *dst, const void *src, uint64_t bytes, hipMemcpyKind kind) {
+    static const bool pageable = env_is("QVQ_H2D", "pageable");
+    void *host = const_cast<void *>(kind == hipMemcpyHostToDevice ? src : dst);
+    const bool reg = !pageable && bytes >= (1u << 20) && hipHostRegister(host, bytes, hipHostRegisterDefault) == hipSuccess;
+    if (!reg) (void)hipGetLastError();
+    hipError_t e = hipMemcpyAsync(dst, src, bytes, kind, ctx->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+    if (reg) (void)hipHostUnregister(host);
+    return e;
+}
+
 // Probes for wait_until (wait.hpp): the stream's state, and the communicator's asynchronous
 // error state (RCCL reports a peer's failure there while our collective is stuck).
 StreamState probe_stream(qvq_ctx *ctx, std::string &msg) {
@@ -644,9 +680,11 @@ qvq_status run_level(qvq_ctx *ctx, uint32_t K, int slot, bool sums_out, const do
     const bool timing = ctx->timing_level == -1 || ctx->timing_level == slot;
     if (timing) HIPCHK(hipEventRecord(ctx->ev[slot][0], ctx->stream));
     if (use_mfma(ctx, K)) {
+        const bool prune = ctx->perm_k == K;   // the order qvq_lbg's finalize left for this level
         HIPCHK(launch_assign_mfma(ctx->stream, ctx->num_cu, fused, ctx->d_codes, ctx->N, ctx->d_rows, ctx->d_E32, K,
                                   ctx->d_C32, ctx->d_plut, ctx->mf_th, ctx->d_A, ctx->d_flags, &cnt[0],
-                                  ctx->d_part, ctx->d_part_cnt));
+                                  ctx->d_part, ctx->d_part_cnt, prune ? ctx->d_perm : nullptr,
+                                  prune ? ctx->d_tint : nullptr));
     } else if (use_wide(ctx, K)) {
         HIPCHK(launch_assign_wide(ctx->stream, ctx->num_cu, ctx->Dp, ctx->D, ctx->d_codes, ctx->N, ctx->d_rows, K,
                                   ctx->d_C32, ctx->mf_th, ctx->d_A, ctx->d_flags, &cnt[0]));
@@ -810,6 +848,7 @@ QVQ_API void qvq_destroy(qvq_ctx *ctx) {
     dfree(ctx->d_mean);
     dfree(ctx->d_scatter);
     dfree(ctx->d_decode);
+    dfree(ctx->d_raster);
     dfree(ctx->d_decode_stat);
     if (ctx->h_decode_stat) (void)hipHostFree(ctx->h_decode_stat);
     if (ctx->h_stage) (void)hipHostFree(ctx->h_stage);
@@ -851,17 +890,17 @@ QVQ_API qvq_status qvq_set_images(qvq_ctx *ctx, const uint8_t *rgb, uint32_t n_i
     if (!rgb) return fail(ctx, QVQ_EINVAL, "null raster");
     HIPCHK(hipSetDevice(ctx->dev));
     const uint64_t bytes = (uint64_t)xSize * ySize * 3 * n_images;
-    uint8_t *d_rgb = nullptr;
-    HIPCHK(hipMalloc(&d_rgb, bytes));
-    st = QVQ_OK;
-    const hipError_t e = hipMemcpy(d_rgb, rgb, bytes, hipMemcpyHostToDevice);
-    if (e != hipSuccess) st = fail(ctx, QVQ_EDEVICE, std::string("raster upload: ") + hipGetErrorString(e));
-    if (st == QVQ_OK) st = alloc_training(ctx, N, D, colorspace);
-    if (st == QVQ_OK) st = tile_into(ctx, d_rgb, n_images, xSize, ySize, bw, bh);
-    if (st == QVQ_OK) st = compute_xsq(ctx);
-    (void)hipStreamSynchronize(ctx->stream);
-    (void)hipFree(d_rgb);
-    return st;
+    if (ctx->raster_bytes < bytes) {   // kept across calls (repeated compresses)
+        dfree(ctx->d_raster);
+        ctx->raster_bytes = 0;
+        HIPCHK(hipMalloc(&ctx->d_raster, bytes));
+        ctx->raster_bytes = bytes;
+    }
+    const hipError_t e = host_copy(ctx, ctx->d_raster, rgb, bytes, hipMemcpyHostToDevice);
+    if (e != hipSuccess) return fail(ctx, QVQ_EDEVICE, std::string("raster upload: ") + hipGetErrorString(e));
+    if ((st = alloc_training(ctx, N, D, colorspace)) != QVQ_OK) return st;
+    if ((st = tile_into(ctx, ctx->d_raster, n_images, xSize, ySize, bw, bh)) != QVQ_OK) return st;
+    return compute_xsq(ctx);
 }
 
 QVQ_API qvq_status qvq_set_synthetic(qvq_ctx *ctx, uint32_t S, uint64_t seed0, uint32_t n_images, uint32_t bw,
@@ -1107,13 +1146,16 @@ QVQ_API qvq_status qvq_lbg(qvq_ctx *ctx, uint32_t bits, double eps, double *code
     // (K = 1 reads the mean sums and leaves them cleared for the next quantize)
     auto finalize = [&](uint32_t K, bool split) {
         if (split) ctx->seq++;
+        const bool prune = split && use_prune(ctx, 2 * K);   // the next search's tile order
+        ctx->perm_k = prune ? 2 * K : 0;
         return launch_finalize_prep(ctx->stream, K == 1 ? ctx->d_mean : ctx->d_sums, K, ctx->D, ctx->Dp, T.R, T.bias,
                                     T.scale,
                                     ctx->d_C64_cent, split, ctx->d_C64_split, pad32(2 * K), T.mu, T.sx, ctx->mf_t,
                                     ctx->d_C32, ctx->d_rows, ctx->d_E32, split ? ctx->dh_cb : nullptr, d_dist + 8,
                                     dist_done,
                                     split ? nullptr : d_dist + 2, split ? ctx->dh_ready : nullptr, ctx->seq,
-                                    K == 1, K == 1 ? MEAN_COPIES : 1);
+                                    K == 1, K == 1 ? MEAN_COPIES : 1, prune ? ctx->d_perm : nullptr,
+                                    prune ? ctx->d_tint : nullptr);
     };
     HIPCHK(finalize(1, bits > 0));
     // with bits >= 1 the first search writes every row's index
@@ -1154,10 +1196,8 @@ QVQ_API qvq_status qvq_lbg(qvq_ctx *ctx, uint32_t bits, double eps, double *code
                                ctx->d_counters + 2 * 33 + 1));
         qvq_status ws = wait_flag(ctx, reinterpret_cast<volatile uint64_t *>(h_small + (1024 - 64 - 8)), seq);
         if (ws != QVQ_OK) return ws;
-        if (assign) {   // every collective of this call is complete: a plain copy
-            HIPCHK(hipMemcpyAsync(assign, ctx->d_A, ctx->N * 4, hipMemcpyDeviceToHost, ctx->stream));
-            HIPCHK(hipStreamSynchronize(ctx->stream));
-        }
+        if (assign)   // every collective of this call is complete: a plain copy
+            HIPCHK(host_copy(ctx, assign, ctx->d_A, ctx->N * 4, hipMemcpyDeviceToHost));
         std::memcpy(dres, h_small, sizeof(dres));
         std::memcpy(stats, h_small + sizeof(dres), sizeof(stats));
         if (codebook) std::memcpy(codebook, ctx->h_cb, cb_bytes);
@@ -1210,6 +1250,7 @@ QVQ_API qvq_status qvq_assign(qvq_ctx *ctx, const double *C, uint32_t K, uint32_
     }
     HIPCHK(hipMemsetAsync(ctx->d_counters, 0, 2 * sizeof(unsigned), ctx->stream));
     if ((st = run_prep(ctx, K)) != QVQ_OK) return st;
+    ctx->perm_k = 0;   // (prep writes no tile order)
     if ((st = run_level(ctx, K, 0, false, C, 0)) != QVQ_OK) return st;
     unsigned stats[2];
     HIPCHK(hipMemcpyAsync(stats, ctx->d_counters, sizeof(stats), hipMemcpyDeviceToHost, ctx->stream));

@@ -672,7 +672,7 @@ hipError_t launch_assign_mfma(hipStream_t s, int grid, bool fuse, const uint8_t 
                               const _Float16 *cb_rows, const float *E32, uint32_t K, const float *C32,
                               const uint64_t *plut,
                               const MfThresholds &th, uint32_t *A, uint32_t *flags, unsigned *flag_cnt,
-                              uint64_t *part, uint32_t *part_cnt) {
+                              uint64_t *part, uint32_t *part_cnt, const uint32_t *perm, const int32_t *tint) {
     static const bool no_stage = std::getenv("QVQ_NOSTAGE") != nullptr;   // ablation
     const bool staged = mf_lds_layout(K, fuse, true).total <= MF_LDS_MAX && (!no_stage || K <= mf_small_k());
     const size_t lds = mf_lds_layout(K, fuse, staged).total;
@@ -710,7 +710,7 @@ hipError_t launch_assign_mfma(hipStream_t s, int grid, bool fuse, const uint8_t 
     static const bool mf32 = !(std::getenv("QVQ_MF32") && std::getenv("QVQ_MF32")[0] == '0');
     if (mf32 && mf32_fits(K, fuse))
         return launch_assign_mf32(s, grid, fuse, codes, N, cb_rows, K, C32, plut, th, A, flags, flag_cnt, part,
-                                  part_cnt);
+                                  part_cnt, perm, tint);
     // 4-code-vector units while the pair loop is short (the recompute dominates): up to
     // K = QVQ_U4_MAXK (default 256)
     static const uint32_t u4_max = std::getenv("QVQ_U4_MAXK") ? (uint32_t)std::atoi(std::getenv("QVQ_U4_MAXK")) : 256;

@@ -38,7 +38,7 @@ constexpr int M32_ROWS = 64;        // rows per wave and chunk: two 32-row data 
 constexpr uint32_t M32_LDS_MAX = 160 * 1024;
 
 struct M32Lds {
-    uint32_t q, c32, sums, cnt, plut, total;
+    uint32_t q, c32, sums, cnt, perm, plut, total;
 };
 // Sums copies (fused, copies > 1): strides one u64 / u32 past K * D / K, so the copies of one
 // (component, code vector) fall on different LDS banks (a 256-byte multiple put them all on
@@ -50,7 +50,8 @@ struct M32Lds {
 __host__ __device__ inline uint32_t m32_kstride(uint32_t K) { return K + QVQ_SUMS_KPAD; }
 __host__ __device__ inline uint32_t m32_sum_stride(uint32_t K, uint32_t copies) { return m32_kstride(K) * MF_D + (copies > 1 ? 1 : 0); }
 __host__ __device__ inline uint32_t m32_cnt_stride(uint32_t K, uint32_t copies) { return K + (copies > 1 ? 1 : 0); }
-__host__ __device__ inline M32Lds m32_lds_layout(uint32_t K, bool fuse, bool staged, uint32_t copies = 1) {
+__host__ __device__ inline M32Lds m32_lds_layout(uint32_t K, bool fuse, bool staged, uint32_t copies = 1,
+                                                  bool prune = false) {
     const uint32_t Kp = (K + 31) & ~31u;
     M32Lds L;
     // fused: the byte LUT first (LDS address 0: a lookup's address is the byte itself, no
@@ -65,6 +66,8 @@ __host__ __device__ inline M32Lds m32_lds_layout(uint32_t K, bool fuse, bool sta
     if (fuse) o += copies * m32_sum_stride(K, copies) * 8;
     L.cnt = o;
     if (fuse) o += copies * ((m32_cnt_stride(K, copies) + 1) & ~1u) * 4;
+    L.perm = o;   // pruned searches: the code vector at each tile position (u16)
+    if (prune) o += ((Kp * 2 + 7) & ~7u);
     L.plut = 0;
     L.total = o;
     return L;
@@ -90,10 +93,10 @@ __device__ inline bool m32_runs_reduce(uint32_t key, uint32_t (&v)[MF_D + 1], in
 // P / Q (LDS, layout above) from the 56-byte rows [hi0..3 lo0..3 | hi4..7 lo4..7 | hi8..11
 // lo8..11 | n] of Kp code vectors.
 __device__ inline void m32_stage_pq(unsigned char *lds, uint32_t qoff, const _Float16 *g_rows, uint32_t Kp, int tid,
-                                    uint32_t rows0 = 0) {
+                                    uint32_t rows0 = 0, const uint32_t *perm = nullptr) {
     const uint64_t *src = reinterpret_cast<const uint64_t *>(g_rows);
     for (uint32_t i = tid; i < Kp; i += M32_THREADS) {
-        const uint64_t *r = src + (size_t)i * 7;
+        const uint64_t *r = src + (size_t)(perm ? perm[i] : i) * 7;   // position i holds code vector perm[i]
         const uint64_t w0 = r[0], w1 = r[1], w2 = r[2], w3 = r[3], w4 = r[4], w5 = r[5], w6 = r[6];
         const bool sw = (i >> 3) & 1;
         u64x2v *p = reinterpret_cast<u64x2v *>(lds + rows0 + (size_t)i * 32);
@@ -132,17 +135,22 @@ __device__ inline void m32_track_tagged(float m, uint32_t keep, uint32_t u, floa
 // copies > 1 (fused): every row adds its terms straight into LDS copy lane % copies of the
 // sums (runs of equal indices then meet copies instead of one address); copies = 1: the
 // wave run reduction first, then one atomic set per run.
-template <bool FUSE, bool STAGED, int U, bool TAG>
+// PRUNE (tiles in the order of perm, tint: finalize's prune_order): a chunk visits its code
+// tiles outward from the one nearest its rows' projection and stops once the tiles left on both
+// sides are provably farther than every row's current best (see the tile loop).
+template <bool FUSE, bool STAGED, int U, bool TAG, bool PRUNE>
 __global__ __launch_bounds__(M32_THREADS) void assign_mf32_kernel(
     const uint8_t *__restrict__ codes, uint64_t N, const _Float16 *__restrict__ g_rows, uint32_t K,
     const float *__restrict__ g_C32, const uint64_t *__restrict__ g_plut, MfThresholds th, uint32_t idbits,
     float orrel, uint32_t *__restrict__ A, uint32_t *__restrict__ flags, unsigned *__restrict__ flag_cnt,
-    uint64_t *__restrict__ part, uint32_t *__restrict__ part_cnt, uint32_t copies) {
+    uint64_t *__restrict__ part, uint32_t *__restrict__ part_cnt, uint32_t copies,
+    const uint32_t *__restrict__ g_perm, const int32_t *__restrict__ g_tint) {
     static_assert(U == 4 || U == 8, "unit of 4 or 8 code vectors");
     constexpr int NU = 16 / U;   // units per lane and code tile
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
     const uint32_t Kp = (K + 31) & ~31u;
-    const M32Lds L = m32_lds_layout(K, FUSE, STAGED, copies);
+    const M32Lds L = m32_lds_layout(K, FUSE, STAGED, copies, PRUNE);
+    uint16_t *perm_l = reinterpret_cast<uint16_t *>(lds + L.perm);
     float *c32s = reinterpret_cast<float *>(lds + L.c32);
     uint64_t *sums = reinterpret_cast<uint64_t *>(lds + L.sums);   // [d][k]
     uint32_t *cnt = reinterpret_cast<uint32_t *>(lds + L.cnt);
@@ -153,7 +161,9 @@ __global__ __launch_bounds__(M32_THREADS) void assign_mf32_kernel(
         (const __attribute__((address_space(3))) uint8_t *)(uintptr_t)0;
     constexpr uint32_t ROWS0 = FUSE ? 256 : 0;   // m32_lds_layout
     const int tid = threadIdx.x;
-    m32_stage_pq(lds, L.q, g_rows, Kp, tid, ROWS0);
+    m32_stage_pq(lds, L.q, g_rows, Kp, tid, ROWS0, PRUNE ? g_perm : nullptr);
+    if (PRUNE)
+        for (uint32_t i = tid; i < Kp; i += M32_THREADS) perm_l[i] = (uint16_t)g_perm[i];
     if (STAGED) {
         const float4 *src = reinterpret_cast<const float4 *>(g_C32);
         float4 *dst = reinterpret_cast<float4 *>(c32s);
@@ -200,6 +210,10 @@ __global__ __launch_bounds__(M32_THREADS) void assign_mf32_kernel(
         }
     };
     const uint32_t ones = h ? 0u : 0x3C003C00u;   // f16 (1, 1) on the n_hi n_lo slots of half 0
+    // PRUNE: lane l < ntiles keeps tile l's projection envelope [tlo, thi] (row-sum units)
+    const int32_t tlo = PRUNE && lane < (int)ntiles ? g_tint[2 * lane] : 0x7FFFFFFF;
+    const int32_t thi = PRUNE && lane < (int)ntiles ? g_tint[2 * lane + 1] : (int32_t)0x80000000;
+    const float sx2 = th.sx * th.sx, dsx = (float)MF_D / sx2;
 
     uint64_t chunk = (uint64_t)blockIdx.x * M32_WAVES + wave;
     const uint64_t stride = (uint64_t)gridDim.x * M32_WAVES;
@@ -233,16 +247,9 @@ __global__ __launch_bounds__(M32_THREADS) void assign_mf32_kernel(
             su[T] = 0;
         }
         half8 a1, a2;
-        load_a(0, a1, a2);
         const f32x16 zero16 = {};
         const uint32_t idmask = (1u << idbits) - 1, keep = ~idmask;
-        for (uint32_t t = 0; t < ntiles; t++) {
-            f32x16 c[2];
-            c[0] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a1, b1[0], zero16, 0, 0, 0);
-            c[1] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a1, b1[1], zero16, 0, 0, 0);
-            c[0] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a2, b2[0], c[0], 0, 0, 0);
-            c[1] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a2, b2[1], c[1], 0, 0, 0);
-            load_a(t + 1 < ntiles ? t + 1 : t, a1, a2);   // the next tile's fragments under these
+        auto tile_step = [&](uint32_t t, const f32x16 (&c)[2]) {
 #pragma unroll
             for (int T = 0; T < 2; T++) {
 #pragma unroll
@@ -261,6 +268,81 @@ __global__ __launch_bounds__(M32_THREADS) void assign_mf32_kernel(
                                          s2[T]);
                     else m32_track(m, t * NU + qq, s1[T], s2[T], su[T]);
                 }
+            }
+        };
+        auto mfma4 = [&](f32x16 (&c)[2]) {
+            c[0] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a1, b1[0], zero16, 0, 0, 0);
+            c[1] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a1, b1[1], zero16, 0, 0, 0);
+            c[0] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a2, b2[0], c[0], 0, 0, 0);
+            c[1] = __builtin_amdgcn_mfma_f32_32x32x16_f16(a2, b2[1], c[1], 0, 0, 0);
+        };
+        if constexpr (PRUNE) {
+            // ||x - c||^2 >= (sum_d (x_d - c_d))^2 / D = sx^2 (sum w - q_c)^2 / D: with the rows'
+            // sums of w in [qmn, qmx] and a tile's q in [lo, hi], a tile whose gap g satisfies
+            // sx^2 g^2 / D > every row's current best distance (plus its MFMA error) holds no
+            // code vector that can be any row's answer or tie with it -- strictly farther.
+            int qmn, qmx;
+            float xn2[2];   // ||x - mu||^2 of this lane's two rows
+            {
+                int qw[2];
+#pragma unroll
+                for (int T = 0; T < 2; T++) {
+                    const uint32_t u0 = q[3 * T] ^ 0x80808080u, u1 = q[3 * T + 1] ^ 0x80808080u,
+                                   u2 = q[3 * T + 2] ^ 0x80808080u;
+                    const uint32_t su =
+                        __builtin_amdgcn_sad_u8(u0, 0u, __builtin_amdgcn_sad_u8(u1, 0u, __builtin_amdgcn_sad_u8(u2, 0u, 0u)));
+                    const uint32_t s2q = __builtin_amdgcn_udot4(u0, u0, __builtin_amdgcn_udot4(u1, u1,
+                                         __builtin_amdgcn_udot4(u2, u2, 0u, false), false), false);
+                    qw[T] = 2 * (int)su - 2 * 1530;   // sum_d w_d, w = 2u - 255
+                    xn2[T] = (float)(int)(4 * s2q - 1020 * su + 12 * 65025) * sx2;   // sum w^2 exact
+                }
+                qmn = (int)(wave_min_u32((uint32_t)min(qw[0], qw[1]) ^ 0x80000000u) ^ 0x80000000u);
+                qmx = (int)(~wave_min_u32(~((uint32_t)max(qw[0], qw[1]) ^ 0x80000000u)) ^ 0x80000000u);
+            }
+            // first tile: the first whose envelope reaches the rows' centre
+            int R = (int)__popcll(__ballot(lane < (int)ntiles && thi < ((qmn + qmx) >> 1)));
+            R = min(R, (int)ntiles - 1);
+            int Lt = R - 1;
+            int64_t bw = 0x7FFFFFFFFFFFll;   // skip a tile when gap^2 > bw (none before a first bound)
+            uint32_t t = (uint32_t)R++;
+            load_a(t, a1, a2);
+            constexpr int BIG = 1 << 20;
+            for (;;) {
+                f32x16 c[2];
+                mfma4(c);
+                // the next tile: the nearer side, unless both are beyond the bound (a stale bound is
+                // valid: rows' bests only decrease)
+                const int gR = R < (int)ntiles ? max(0, __builtin_amdgcn_readlane(tlo, R) - qmx) : BIG;
+                const int gL = Lt >= 0 ? max(0, qmn - __builtin_amdgcn_readlane(thi, Lt)) : BIG;
+                const int g = min(gR, gL);
+                const bool more = g < BIG && (int64_t)g * g <= bw;
+                uint32_t tn = 0;
+                if (more) {
+                    tn = gR <= gL ? (uint32_t)R++ : (uint32_t)Lt--;
+                    load_a(tn, a1, a2);   // under this tile's MFMAs and epilogue
+                }
+                tile_step(t, c);
+                if (!more) break;
+                // every row's best distance, bounded above: the lane's two tagged bests (tag error
+                // orrel relative), the MFMA error th.mfma; max over the wave
+                float ub = 0.f;
+#pragma unroll
+                for (int T = 0; T < 2; T++) {
+                    const float v = __fmaf_rn(s1[T], th.inv_scale, xn2[T]);
+                    ub = fmaxf(ub, __fmaf_rn(orrel * th.inv_scale, fabsf(s1[T]), v + th.mfma));
+                }
+                ub = __uint_as_float(~wave_min_u32(~__float_as_uint(fmaxf(ub, 0.f))));   // >= 0: bits order as values
+                const float bwf = ub * dsx * 1.00001f + 1.0f;
+                bw = bwf < 1e15f ? (int64_t)bwf : 0x7FFFFFFFFFFFll;
+                t = tn;
+            }
+        } else {
+            load_a(0, a1, a2);
+            for (uint32_t t = 0; t < ntiles; t++) {
+                f32x16 c[2];
+                mfma4(c);
+                load_a(t + 1 < ntiles ? t + 1 : t, a1, a2);   // the next tile's fragments under these
+                tile_step(t, c);
             }
         }
         if constexpr (TAG) {
@@ -308,7 +390,8 @@ __global__ __launch_bounds__(M32_THREADS) void assign_mf32_kernel(
             float r1 = INFINITY, r2 = INFINITY;
 #pragma unroll
             for (int j = 0; j < U; j++) {
-                const uint32_t cv = cb + (j & 3) + 8 * (j >> 2);
+                const uint32_t cp = cb + (j & 3) + 8 * (j >> 2);   // tile position
+                const uint32_t cv = PRUNE ? perm_l[cp] : cp;         // its code vector
                 const float4 *c4 = reinterpret_cast<const float4 *>(C32 + (size_t)cv * MF_D);
                 float dist = 0.f;
 #pragma unroll
@@ -597,23 +680,30 @@ hipError_t launch_recheck_mf32(hipStream_t s, int num_cu, const uint8_t *codes, 
     return hipGetLastError();
 }
 
-template <bool F, bool S, int U, bool TAG>
+template <bool F, bool S, int U, bool TAG, bool P = false>
 static void launch_mf32_variant(hipStream_t s, int grid, size_t lds, const uint8_t *codes, uint64_t N,
                                 const _Float16 *cb_rows, uint32_t K, const float *C32, const uint64_t *plut,
                                 const MfThresholds &th, uint32_t idbits, float orrel, uint32_t *A, uint32_t *flags,
-                                unsigned *flag_cnt, uint64_t *part, uint32_t *part_cnt, uint32_t copies) {
-    hipLaunchKernelGGL((assign_mf32_kernel<F, S, U, TAG>), dim3(grid), dim3(M32_THREADS), lds, s, codes, N, cb_rows,
-                       K, C32, plut, th, idbits, orrel, A, flags, flag_cnt, part, part_cnt, copies);
+                                unsigned *flag_cnt, uint64_t *part, uint32_t *part_cnt, uint32_t copies,
+                                const uint32_t *perm, const int32_t *tint) {
+    hipLaunchKernelGGL((assign_mf32_kernel<F, S, U, TAG, P>), dim3(grid), dim3(M32_THREADS), lds, s, codes, N, cb_rows,
+                       K, C32, plut, th, idbits, orrel, A, flags, flag_cnt, part, part_cnt, copies, perm, tint);
 }
 
 bool mf32_fits(uint32_t K, bool fuse) { return m32_lds_layout(K, fuse, false).total <= M32_LDS_MAX; }
 
+bool mf32_prune_fits(uint32_t K, bool fuse) {
+    return K <= 65536 && m32_lds_layout(K, fuse, false, 1, true).total <= M32_LDS_MAX;
+}
+
 hipError_t launch_assign_mf32(hipStream_t s, int grid, bool fuse, const uint8_t *codes, uint64_t N,
                               const _Float16 *cb_rows, uint32_t K, const float *C32, const uint64_t *plut,
                               const MfThresholds &th, uint32_t *A, uint32_t *flags, unsigned *flag_cnt,
-                              uint64_t *part, uint32_t *part_cnt) {
+                              uint64_t *part, uint32_t *part_cnt, const uint32_t *perm, const int32_t *tint) {
     if (!mf32_fits(K, fuse)) return hipErrorInvalidValue;
-    const bool staged = m32_lds_layout(K, fuse, true).total <= M32_LDS_MAX;
+    const bool prune = perm && tint;
+    if (prune && !mf32_prune_fits(K, fuse)) return hipErrorInvalidValue;
+    const bool staged = m32_lds_layout(K, fuse, true, 1, prune).total <= M32_LDS_MAX;
     // sums copies (fused, 64 <= K <= 512 by default: QVQ_SUM_COPIES_MINK / _MAXK): the most, up
     // to 16, that fit.  With the padded copy strides, C3: K = 64 / 128 / 256 / 512 -6 / -22 /
     // -19 / -16 us against the wave run reduction; K = 1024 has no room for a second copy.
@@ -623,8 +713,8 @@ hipError_t launch_assign_mf32(hipStream_t s, int grid, bool fuse, const uint8_t 
         std::getenv("QVQ_SUM_COPIES_MAXK") ? (uint32_t)std::atoi(std::getenv("QVQ_SUM_COPIES_MAXK")) : 512;
     uint32_t copies = 1;
     if (fuse && K >= copies_mink && K <= copies_maxk)
-        while (copies < 16 && m32_lds_layout(K, fuse, staged, copies * 2).total <= M32_LDS_MAX) copies *= 2;
-    const size_t lds = m32_lds_layout(K, fuse, staged, copies).total;
+        while (copies < 16 && m32_lds_layout(K, fuse, staged, copies * 2, prune).total <= M32_LDS_MAX) copies *= 2;
+    const size_t lds = m32_lds_layout(K, fuse, staged, copies, prune).total;
     // 4-code-vector units while the tile loop is short (the recompute dominates)
     static const uint32_t u4_max =
         std::getenv("QVQ_U4_MAXK") ? (uint32_t)std::atoi(std::getenv("QVQ_U4_MAXK")) : 256;
@@ -637,7 +727,7 @@ hipError_t launch_assign_mf32(hipStream_t s, int grid, bool fuse, const uint8_t 
     const float orrel = std::ldexp(1.0f, (int)idbits - 22);
     using Fn = void (*)(hipStream_t, int, size_t, const uint8_t *, uint64_t, const _Float16 *, uint32_t, const float *,
                         const uint64_t *, const MfThresholds &, uint32_t, float, uint32_t *, uint32_t *, unsigned *,
-                        uint64_t *, uint32_t *, uint32_t);
+                        uint64_t *, uint32_t *, uint32_t, const uint32_t *, const int32_t *);
 #define QVQ_MF32_PICK(TG)                                                                                          \
     if (fuse) {                                                                                                    \
         if (u4) fn = staged ? launch_mf32_variant<true, true, 4, TG> : launch_mf32_variant<true, false, 4, TG>;    \
@@ -647,13 +737,18 @@ hipError_t launch_assign_mf32(hipStream_t s, int grid, bool fuse, const uint8_t 
         else fn = staged ? launch_mf32_variant<false, true, 8, TG> : launch_mf32_variant<false, false, 8, TG>;     \
     }
     Fn fn;
-    if (tag && idbits <= 12) {
+    if (prune && !u4 && idbits <= 12) {   // pruned search: 8-code-vector units, tagged
+        if (fuse) fn = staged ? launch_mf32_variant<true, true, 8, true, true> : launch_mf32_variant<true, false, 8, true, true>;
+        else fn = staged ? launch_mf32_variant<false, true, 8, true, true> : launch_mf32_variant<false, false, 8, true, true>;
+    } else if (tag && idbits <= 12) {
         QVQ_MF32_PICK(true)
     } else {
         QVQ_MF32_PICK(false)
     }
 #undef QVQ_MF32_PICK
-    fn(s, grid, lds, codes, N, cb_rows, K, C32, plut, th, idbits, orrel, A, flags, flag_cnt, part, part_cnt, copies);
+    if (!(prune && !u4 && idbits <= 12)) perm = nullptr, tint = nullptr;   // (the unpruned order: identity)
+    fn(s, grid, lds, codes, N, cb_rows, K, C32, plut, th, idbits, orrel, A, flags, flag_cnt, part, part_cnt, copies, perm,
+       tint);
     return hipGetLastError();
 }
 

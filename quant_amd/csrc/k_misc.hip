@@ -67,8 +67,44 @@ __global__ void tile_kernel(const uint8_t *__restrict__ rgb, uint8_t *__restrict
     }
 }
 
+// The 2x2 case without wrap or padding (xSize even, ySize % 4 == 0: every block inside its image,
+// raster rows 4-byte aligned): a thread takes two horizontally adjacent blocks -- 12 bytes of
+// raster row 2i and 12 of row 2i + 1, three dword loads each -- and writes their 24 code bytes
+// with six dword stores (block j: row 2i pixels 2j, 2j+1, then row 2i+1's; D = Dp = 12).  The
+// generic kernel moved these 100 MB (C3) at ~2 TB/s with byte stores and 64-bit divisions.
+__global__ __launch_bounds__(256) void tile22_kernel(const uint32_t *__restrict__ rgb, uint32_t *__restrict__ codes,
+                                                     uint64_t pairs_total, uint32_t pairs_per_row, uint32_t words_per_row,
+                                                     uint64_t pairs_per_image, uint64_t words_per_image) {
+    for (uint64_t t = blockIdx.x * (uint64_t)blockDim.x + threadIdx.x; t < pairs_total;
+         t += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t img = t / pairs_per_image, r = t - img * pairs_per_image;
+        const uint32_t i = (uint32_t)(r / pairs_per_row), jp = (uint32_t)(r - (uint64_t)i * pairs_per_row);
+        const uint32_t *a = rgb + img * words_per_image + (uint64_t)(2 * i) * words_per_row + 3 * jp;
+        const uint32_t *b = a + words_per_row;
+        const uint32_t a0 = a[0], a1 = a[1], a2 = a[2], b0 = b[0], b1 = b[1], b2 = b[2];
+        // row bytes a0..a11: block j = a[0..5] b[0..5], block j+1 = a[6..11] b[6..11]
+        uint32_t *o = codes + t * 6;
+        o[0] = a0;
+        o[1] = __builtin_amdgcn_perm(b0, a1, 0x05040100u);   // a4 a5 b0 b1
+        o[2] = __builtin_amdgcn_alignbyte(b1, b0, 2);        // b2 b3 b4 b5
+        o[3] = __builtin_amdgcn_alignbyte(a2, a1, 2);        // a6 a7 a8 a9
+        o[4] = __builtin_amdgcn_perm(b1, a2, 0x07060302u);   // a10 a11 b6 b7
+        o[5] = b2;                                           // b8 b9 b10 b11
+    }
+}
+
 hipError_t launch_tile(hipStream_t s, const uint8_t *rgb, uint8_t *codes, uint32_t n_images, uint32_t xSize,
                        uint32_t ySize, uint32_t bw, uint32_t bh, uint32_t D, uint32_t Dp, uint8_t pad) {
+    static const bool generic = std::getenv("QVQ_TILE_GENERIC") != nullptr;   // A/B
+    if (!generic && bw == 2 && bh == 2 && xSize % 2 == 0 && ySize % 4 == 0 && ((uintptr_t)rgb & 3) == 0) {
+        const uint32_t ppr = ySize / 4, wpr = ySize * 3 / 4;
+        const uint64_t ppi = (uint64_t)(xSize / 2) * ppr, wpi = (uint64_t)xSize * wpr;
+        const uint64_t total = ppi * n_images;
+        hipLaunchKernelGGL(tile22_kernel, dim3((int)std::min<uint64_t>((total + 255) / 256, 1u << 16)), dim3(256), 0, s,
+                           reinterpret_cast<const uint32_t *>(rgb), reinterpret_cast<uint32_t *>(codes), total, ppr,
+                           wpr, ppi, wpi);
+        return hipGetLastError();
+    }
     const uint64_t nb = (uint64_t)((xSize + bw - 1) / bw) * ((ySize + bh - 1) / bh) * n_images;
     hipLaunchKernelGGL(tile_kernel, dim3((int)std::min<uint64_t>((nb + 255) / 256, 65536)), dim3(256), 0, s, rgb,
                        codes, n_images, xSize, ySize, bw, bh, D, Dp, pad);
@@ -205,7 +241,39 @@ __global__ __launch_bounds__(urun_threads(DP)) void update_runs_kernel(const uin
     };
     const uint64_t wave_g = ((uint64_t)blockIdx.x * T + tid) >> 6;
     const uint64_t n_waves = ((uint64_t)gridDim.x * T) >> 6;
-    for (uint64_t r0 = wave_g * 64 * R; r0 < N; r0 += n_waves * 64 * R) {
+    const uint64_t rstep = n_waves * 64 * R;
+    // Full rounds with the next round's rows and indices loaded under this round's adds (a
+    // wave-lane holds one round in flight: the loop was latency-bound, C4's 4x4 levels 36-145 us
+    // for 50 MB); the ragged last round after.
+    const uint64_t full_end = N / (64 * R) * (64 * R);
+    uint64_t r0 = wave_g * 64 * R;
+    if (r0 + 64 * R <= full_end) {
+        uint32_t w[R * W4], a[R];
+        auto load = [&](uint64_t rb, uint32_t (&wv)[R * W4], uint32_t (&av)[R]) {
+            const uint64_t row = rb + (uint64_t)R * lane;
+            const uint32_t *p = reinterpret_cast<const uint32_t *>(codes + row * DP);
+#pragma unroll
+            for (int i = 0; i < R * W4; i++) wv[i] = p[i];
+#pragma unroll
+            for (int r = 0; r < R; r++) av[r] = A[row + r];
+        };
+        load(r0, w, a);
+        for (;;) {
+            const uint64_t rn = r0 + rstep;
+            const bool more = rn + 64 * R <= full_end;   // (uniform)
+            uint32_t wn[R * W4], an[R];
+            if (more) load(rn, wn, an);
+#pragma unroll
+            for (int r = 0; r < R; r++) add_row(w + r * W4, a[r]);
+            r0 = rn;
+            if (!more) break;
+#pragma unroll
+            for (int i = 0; i < R * W4; i++) w[i] = wn[i];
+#pragma unroll
+            for (int r = 0; r < R; r++) a[r] = an[r];
+        }
+    }
+    for (; r0 < N; r0 += rstep) {   // rounds past the last full one (at most one per wave)
         const uint64_t row = r0 + (uint64_t)R * lane;
         if (r0 + 64 * R <= N) {
             uint32_t w[R * W4];
@@ -917,6 +985,8 @@ struct FinArgs {
     uint64_t *zero_after;   // cleared by the last block once every block has read sums (mean)
     uint32_t n_zero;
     uint32_t ncopy;         // copies of the sums to add (stride 2KD + K): the mean's MEAN_COPIES
+    uint32_t *perm;         // split, D = 12: the next search's tile order (prune_order), or null
+    int32_t *tint;
 };
 
 // One (row j, component lane d) item of the finalize; L lanes per row (16 when D == 12: the
@@ -992,6 +1062,84 @@ __device__ inline double finalize_item(const FinArgs &a, uint32_t j, uint32_t d,
     return 0.0;
 }
 
+// The next D = 12 search's code-vector order for tile pruning (assign_mf32_kernel, PRUNE): the
+// K2 split code vectors bucket-sorted by their projection q = sum_d (c_d - mu) / sx on the
+// all-ones direction (in the units of a row's sum_d w_d, w the centred byte integers), so that
+// each 32-code-vector tile spans a short q interval.  perm[p] = the code vector at position p
+// (padding positions K2 .. Kpad map to themselves); tint[2t], tint[2t + 1] = the floor / ceil
+// of tile t's q interval widened by 1 (empty tile: INT_MAX, INT_MIN).  Any grouping keeps the
+// search exact (the bound holds for every tile); the sort only makes it prune.  Run by the
+// finalize's last block (256 threads), K2 <= PRUNE_MAXK.
+constexpr uint32_t PRUNE_MAXK = 1024, PRUNE_NB = 256;
+__device__ void prune_order(const double *__restrict__ C64n, uint32_t K2, uint32_t Kpad, double mu, double sx,
+                            uint32_t *__restrict__ perm, int32_t *__restrict__ tint) {
+    __shared__ float q[PRUNE_MAXK];
+    __shared__ uint32_t pos_of[PRUNE_MAXK];
+    __shared__ uint32_t hist[PRUNE_NB];
+    __shared__ float qr[2][256];
+    const uint32_t tid = threadIdx.x;
+    float mn = INFINITY, mx = -INFINITY;
+    for (uint32_t j = tid; j < K2; j += 256) {
+        double sum = 0;
+        for (uint32_t d = 0; d < MF_D; d++) sum += C64n[(uint64_t)j * MF_D + d] - mu;
+        q[j] = (float)(sum / sx);
+        mn = fminf(mn, q[j]);
+        mx = fmaxf(mx, q[j]);
+    }
+    for (uint32_t b = tid; b < PRUNE_NB; b += 256) hist[b] = 0;
+    qr[0][tid] = mn;
+    qr[1][tid] = mx;
+    __syncthreads();
+    for (int w = 128; w > 0; w >>= 1) {
+        if ((int)tid < w) {
+            qr[0][tid] = fminf(qr[0][tid], qr[0][tid + w]);
+            qr[1][tid] = fmaxf(qr[1][tid], qr[1][tid + w]);
+        }
+        __syncthreads();
+    }
+    const float qmin = qr[0][0], inv = (float)PRUNE_NB / (qr[1][0] - qmin + 1.0f);
+    auto bucket = [&](float v) { return min((uint32_t)((v - qmin) * inv), PRUNE_NB - 1); };
+    for (uint32_t j = tid; j < K2; j += 256) atomicAdd(&hist[bucket(q[j])], 1u);
+    __syncthreads();
+    if (tid == 0) {   // exclusive scan (256 entries)
+        uint32_t run = 0;
+        for (uint32_t b = 0; b < PRUNE_NB; b++) {
+            const uint32_t c = hist[b];
+            hist[b] = run;
+            run += c;
+        }
+    }
+    __syncthreads();
+    for (uint32_t j = tid; j < K2; j += 256) {   // (order inside a bucket: any)
+        const uint32_t p = atomicAdd(&hist[bucket(q[j])], 1u);
+        perm[p] = j;
+        pos_of[p] = j;
+    }
+    for (uint32_t p = K2 + tid; p < Kpad; p += 256) perm[p] = p;
+    __syncthreads();
+    __shared__ int32_t tlo[PRUNE_MAXK / 32], thi[PRUNE_MAXK / 32];
+    const uint32_t nt = Kpad / 32;
+    for (uint32_t t = tid; t < nt; t += 256) {
+        float lo = INFINITY, hi = -INFINITY;
+        for (uint32_t p = t * 32; p < min(t * 32 + 32, K2); p++) {
+            lo = fminf(lo, q[pos_of[p]]);
+            hi = fmaxf(hi, q[pos_of[p]]);
+        }
+        tlo[t] = lo <= hi ? (int32_t)floorf(lo) - 1 : 0x7FFFFFFF;
+        thi[t] = lo <= hi ? (int32_t)ceilf(hi) + 1 : (int32_t)0x80000000;
+    }
+    __syncthreads();
+    // Tiles sharing a bucket can overlap out of order: store monotone envelopes (lo: the suffix
+    // minimum, hi: the prefix maximum; still bounds of every tile), so that a scan leaving tile t
+    // may skip every tile beyond it on that side.
+    if (tid == 0) {
+        int32_t m = 0x7FFFFFFF;
+        for (int t = (int)nt - 1; t >= 0; t--) tint[2 * t] = m = min(m, tlo[t]);
+        m = (int32_t)0x80000000;
+        for (uint32_t t = 0; t < nt; t++) tint[2 * t + 1] = m = max(m, thi[t]);
+    }
+}
+
 __device__ inline uint32_t fin_rows(const FinArgs &a) { return a.split ? max(2 * a.K, a.Kpad_next) : a.K; }
 
 // Grid-stride over groups of 256/L rows.  Each wave fences its mapped-host writes once, after
@@ -1036,6 +1184,7 @@ __global__ __launch_bounds__(256) void finalize_prep_kernel(FinArgs a, double *_
         }
     }
     for (uint32_t i = threadIdx.x; i < a.n_zero; i += blockDim.x) a.zero_after[i] = 0;
+    if (a.perm) prune_order(a.C64n, 2 * a.K, a.Kpad_next, a.mu, a.sx, a.perm, a.tint);
     if (threadIdx.x == 0) {
         *done = 0;
         if (ready) {
@@ -1071,6 +1220,8 @@ static FinArgs fin_args(const uint64_t *sums, uint32_t K, uint32_t D, uint32_t D
     a.zero_after = nullptr;
     a.n_zero = 0;
     a.ncopy = 1;
+    a.perm = nullptr;
+    a.tint = nullptr;
     return a;
 }
 
@@ -1078,7 +1229,7 @@ hipError_t launch_finalize_prep(hipStream_t s, const uint64_t *sums, uint32_t K,
                                 int64_t bias, int scale, double *C_cent, bool split, double *C64n, uint32_t Kpad_next,
                                 double mu, double sx, int t, float *C32, _Float16 *cb_rows, float *E32,
                                 double *host_cb, double *dist_part, unsigned *done, double *dist_out, uint64_t *ready,
-                                uint64_t seq, bool zero_sums, uint32_t ncopy) {
+                                uint64_t seq, bool zero_sums, uint32_t ncopy, uint32_t *perm, int32_t *tint) {
     if (D == 0 || D > 64) return hipErrorInvalidValue;
     if (zero_sums && !done) return hipErrorInvalidValue;   // the clearing is the last block's
     const uint32_t L = D <= 16 ? 16 : (D <= 32 ? 32 : 64);
@@ -1087,6 +1238,11 @@ hipError_t launch_finalize_prep(hipStream_t s, const uint64_t *sums, uint32_t K,
     FinArgs a = fin_args(sums, K, D, Dp, R, bias, scale, C_cent, split, C64n, Kpad_next, mu, sx, t, C32, cb_rows,
                          E32, host_cb, dist_out != nullptr);
     a.ncopy = ncopy ? ncopy : 1;
+    if (perm) {   // the last block orders the next search's code vectors (needs the done counter)
+        if (!done || !split || D != MF_D || 2 * K > PRUNE_MAXK || Kpad_next % 32) return hipErrorInvalidValue;
+        a.perm = perm;
+        a.tint = tint;
+    }
     if (zero_sums) {
         a.zero_after = const_cast<uint64_t *>(sums);
         a.n_zero = a.ncopy * (2 * K * D + K);
@@ -1100,7 +1256,8 @@ hipError_t launch_finalize_prep(hipStream_t s, const uint64_t *sums, uint32_t K,
 hipError_t launch_finalize(hipStream_t s, const uint64_t *sums, uint32_t K, uint32_t D, int64_t R, int64_t bias,
                            int scale, double *C_cent) {
     return launch_finalize_prep(s, sums, K, D, (D + 3) & ~3u, R, bias, scale, C_cent, false, nullptr, 0, 0, 0, 0,
-                                nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, 0, false);
+                                nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, 0, false, 1,
+                                nullptr, nullptr);
 }
 
 // Search tables from an fp64 codebook: fp32 [Kpad][Dp] (VALU path and the MFMA recompute)
