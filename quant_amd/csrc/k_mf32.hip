@@ -299,42 +299,43 @@ __global__ __launch_bounds__(M32_THREADS) void assign_mf32_kernel(
                 qmn = (int)(wave_min_u32((uint32_t)min(qw[0], qw[1]) ^ 0x80000000u) ^ 0x80000000u);
                 qmx = (int)(~wave_min_u32(~((uint32_t)max(qw[0], qw[1]) ^ 0x80000000u)) ^ 0x80000000u);
             }
-            // first tile: the first whose envelope reaches the rows' centre
-            int R = (int)__popcll(__ballot(lane < (int)ntiles && thi < ((qmn + qmx) >> 1)));
-            R = min(R, (int)ntiles - 1);
-            int Lt = R - 1;
-            int64_t bw = 0x7FFFFFFFFFFFll;   // skip a tile when gap^2 > bw (none before a first bound)
-            uint32_t t = (uint32_t)R++;
-            load_a(t, a1, a2);
-            constexpr int BIG = 1 << 20;
-            for (;;) {
+            // The nearest tile first (the first whose envelope reaches the rows' centre), then one
+            // bound from it -- every row's best distance so far, from above: the lane's two tagged
+            // bests (tag error orrel relative) plus the MFMA error, max over the wave -- and the
+            // window of tiles within it: the tiles' gaps grow away from the centre (monotone
+            // envelopes), so the window is one contiguous range.  One decision per chunk keeps
+            // the tile loop free of per-tile dependencies (a per-tile bound measured no faster).
+            const int t0 = min((int)__popcll(__ballot(lane < (int)ntiles && thi < ((qmn + qmx) >> 1))), (int)ntiles - 1);
+            {
+                load_a((uint32_t)t0, a1, a2);
                 f32x16 c[2];
                 mfma4(c);
-                // the next tile: the nearer side, unless both are beyond the bound (a stale bound is
-                // valid: rows' bests only decrease)
-                const int gR = R < (int)ntiles ? max(0, __builtin_amdgcn_readlane(tlo, R) - qmx) : BIG;
-                const int gL = Lt >= 0 ? max(0, qmn - __builtin_amdgcn_readlane(thi, Lt)) : BIG;
-                const int g = min(gR, gL);
-                const bool more = g < BIG && (int64_t)g * g <= bw;
-                uint32_t tn = 0;
-                if (more) {
-                    tn = gR <= gL ? (uint32_t)R++ : (uint32_t)Lt--;
-                    load_a(tn, a1, a2);   // under this tile's MFMAs and epilogue
-                }
-                tile_step(t, c);
-                if (!more) break;
-                // every row's best distance, bounded above: the lane's two tagged bests (tag error
-                // orrel relative), the MFMA error th.mfma; max over the wave
-                float ub = 0.f;
+                tile_step((uint32_t)t0, c);
+            }
+            float ub = 0.f;
 #pragma unroll
-                for (int T = 0; T < 2; T++) {
-                    const float v = __fmaf_rn(s1[T], th.inv_scale, xn2[T]);
-                    ub = fmaxf(ub, __fmaf_rn(orrel * th.inv_scale, fabsf(s1[T]), v + th.mfma));
+            for (int T = 0; T < 2; T++) {   // the row's bound: the better of its two halves (lane ^ 32)
+                const float v = __fmaf_rn(s1[T], th.inv_scale, xn2[T]);
+                const float b = __fmaf_rn(orrel * th.inv_scale, fabsf(s1[T]), v + th.mfma);
+                ub = fmaxf(ub, fminf(b, xor32_f32(b)));
+            }
+            ub = __uint_as_float(~wave_min_u32(~__float_as_uint(fmaxf(ub, 0.f))));   // >= 0: bits order as values
+            const float bw = ub * dsx * 1.00001f + 1.0f;
+            const float gap = (float)max(0, max(tlo - qmx, qmn - thi));   // this lane's tile
+            const uint64_t win = __ballot(lane < (int)ntiles && gap * gap <= bw);
+            const int lo_t = win ? __ffsll((unsigned long long)win) - 1 : t0;
+            const int hi_t = win ? 63 - __clzll((long long)win) : t0;
+            // [lo_t, hi_t] without t0, in two runs, the next tile's fragments under each tile's work
+            for (int seg = 0; seg < 2; seg++) {
+                const int b = seg ? t0 + 1 : lo_t, e = seg ? hi_t : t0 - 1;   // inclusive
+                if (b > e) continue;
+                load_a((uint32_t)b, a1, a2);
+                for (int t = b; t <= e; t++) {
+                    f32x16 c[2];
+                    mfma4(c);
+                    load_a((uint32_t)(t < e ? t + 1 : t), a1, a2);
+                    tile_step((uint32_t)t, c);
                 }
-                ub = __uint_as_float(~wave_min_u32(~__float_as_uint(fmaxf(ub, 0.f))));   // >= 0: bits order as values
-                const float bwf = ub * dsx * 1.00001f + 1.0f;
-                bw = bwf < 1e15f ? (int64_t)bwf : 0x7FFFFFFFFFFFll;
-                t = tn;
             }
         } else {
             load_a(0, a1, a2);

@@ -241,39 +241,9 @@ __global__ __launch_bounds__(urun_threads(DP)) void update_runs_kernel(const uin
     };
     const uint64_t wave_g = ((uint64_t)blockIdx.x * T + tid) >> 6;
     const uint64_t n_waves = ((uint64_t)gridDim.x * T) >> 6;
-    const uint64_t rstep = n_waves * 64 * R;
-    // Full rounds with the next round's rows and indices loaded under this round's adds (a
-    // wave-lane holds one round in flight: the loop was latency-bound, C4's 4x4 levels 36-145 us
-    // for 50 MB); the ragged last round after.
-    const uint64_t full_end = N / (64 * R) * (64 * R);
-    uint64_t r0 = wave_g * 64 * R;
-    if (r0 + 64 * R <= full_end) {
-        uint32_t w[R * W4], a[R];
-        auto load = [&](uint64_t rb, uint32_t (&wv)[R * W4], uint32_t (&av)[R]) {
-            const uint64_t row = rb + (uint64_t)R * lane;
-            const uint32_t *p = reinterpret_cast<const uint32_t *>(codes + row * DP);
-#pragma unroll
-            for (int i = 0; i < R * W4; i++) wv[i] = p[i];
-#pragma unroll
-            for (int r = 0; r < R; r++) av[r] = A[row + r];
-        };
-        load(r0, w, a);
-        for (;;) {
-            const uint64_t rn = r0 + rstep;
-            const bool more = rn + 64 * R <= full_end;   // (uniform)
-            uint32_t wn[R * W4], an[R];
-            if (more) load(rn, wn, an);
-#pragma unroll
-            for (int r = 0; r < R; r++) add_row(w + r * W4, a[r]);
-            r0 = rn;
-            if (!more) break;
-#pragma unroll
-            for (int i = 0; i < R * W4; i++) w[i] = wn[i];
-#pragma unroll
-            for (int r = 0; r < R; r++) a[r] = an[r];
-        }
-    }
-    for (; r0 < N; r0 += rstep) {   // rounds past the last full one (at most one per wave)
+    // (a prefetching loop holding the next round in registers measured slower: C4's update
+    // 102 -> 132 us per quantize)
+    for (uint64_t r0 = wave_g * 64 * R; r0 < N; r0 += n_waves * 64 * R) {
         const uint64_t row = r0 + (uint64_t)R * lane;
         if (r0 + 64 * R <= N) {
             uint32_t w[R * W4];
@@ -989,10 +959,62 @@ struct FinArgs {
     int32_t *tint;
 };
 
+// A split row j (< 2K: child of code vector j mod K, from that code vector's sums hs, ls, cnt of
+// component d; Kpad_next > j >= 2K: padding) -- its C64n / C32 / host values and the MFMA tables.
+__device__ inline void finalize_split_item(const FinArgs &a, uint32_t j, uint32_t d, uint32_t L, uint64_t hs,
+                                           uint64_t ls, uint64_t cnt) {
+    const uint32_t K = a.K, D = a.D, Dp = a.Dp;
+    if (j < 2 * K) {
+        const uint32_t k = j < K ? j : j - K;
+        double v = 0;
+        if (d < D) {
+            const double cv = centroid_value(hs, ls, cnt, a.R, a.bias, a.scale);
+            if (j < K) a.C_cent[(uint64_t)k * D + d] = cv;
+            v = cv * (j < K ? (double)(1 + 0.2) : (double)(1 - 0.2));
+            a.C64n[(uint64_t)j * D + d] = v;
+            if (a.host_cb) a.host_cb[(uint64_t)j * D + d] = v;
+        }
+        if (d < Dp) a.C32[(uint64_t)j * Dp + d] = (float)v;
+        if (a.rows) {   // MFMA row (common.hpp): hi / lo at their slots, norm at 2 LO
+            const uint32_t RF = cb_row_f16(D, Dp), LO = cb_lo_off(D, Dp);
+            _Float16 *row = a.rows + (uint64_t)j * RF;
+            const double cp = d < D ? v - a.mu : 0.0;
+            double n = cp * cp;   // L >= LO lanes per row
+            for (uint32_t off = L / 2; off >= 1; off >>= 1) n += __shfl_xor(n, (int)off, (int)L);
+            if (d < D) {
+                const double c2 = -2.0 * a.sx * cp * a.scale_t;
+                const _Float16 h = (_Float16)(float)c2;
+                row[cb_hi_slot(D, Dp, d)] = h;
+                row[cb_lo_slot(D, Dp, d)] = (_Float16)(float)(c2 - (double)(float)h);
+            } else if (d < LO) {
+                row[cb_hi_slot(D, Dp, d)] = (_Float16)0.f;
+                row[cb_lo_slot(D, Dp, d)] = (_Float16)0.f;
+            }
+            n *= a.scale_t;
+            const _Float16 h = (_Float16)(float)n;
+            const _Float16 l = (_Float16)(float)(n - (double)(float)h);
+            for (uint32_t i = 2 * LO + d; i < RF; i += L)
+                row[i] = i == 2 * LO ? h : (i == 2 * LO + 1 ? l : (_Float16)0.f);
+            if (a.E32 && d < 16)   // L = 16 lanes for D = 12
+                a.E32[(uint64_t)j * 16 + d] =
+                    d < D ? (float)(-2.0 * a.sx * cp * a.scale_t) : (d == D ? (float)n : 0.f);
+        }
+    } else if (j < a.Kpad_next) {
+        if (d < Dp) a.C32[(uint64_t)j * Dp + d] = 0.f;
+        if (a.E32 && d < 16) a.E32[(uint64_t)j * 16 + d] = d == D ? 1e30f : 0.f;   // never wins
+        if (a.rows) {
+            const uint32_t RF = cb_row_f16(D, Dp), LO = cb_lo_off(D, Dp);
+            _Float16 *row = a.rows + (uint64_t)j * RF;
+            for (uint32_t i = d; i < RF; i += L)
+                row[i] = (_Float16)(i == 2 * LO || i == 2 * LO + 1 ? MF_PAD_SCORE : 0.f);
+        }
+    }
+}
+
 // One (row j, component lane d) item of the finalize; L lanes per row (16 when D == 12: the
 // norm of a row is a 16-lane butterfly).  Returns the item's distortion term (no split).
 __device__ inline double finalize_item(const FinArgs &a, uint32_t j, uint32_t d, uint32_t L) {
-    const uint32_t K = a.K, D = a.D, Dp = a.Dp;
+    const uint32_t K = a.K, D = a.D;
     const uint64_t KD = (uint64_t)K * D;
     auto sums_at = [&](uint64_t i) {   // the sum of the ncopy copies
         uint64_t v = a.sums[i];
@@ -1000,52 +1022,11 @@ __device__ inline double finalize_item(const FinArgs &a, uint32_t j, uint32_t d,
         return v;
     };
     if (a.split) {
-        if (j < 2 * K) {
-            const uint32_t k = j < K ? j : j - K;
-            double v = 0;
-            if (d < D) {
-                const uint64_t c = (uint64_t)d * K + k;
-                const double cv = centroid_value(sums_at(c), sums_at(KD + c), sums_at(2 * KD + k), a.R, a.bias, a.scale);
-                if (j < K) a.C_cent[(uint64_t)k * D + d] = cv;
-                v = cv * (j < K ? (double)(1 + 0.2) : (double)(1 - 0.2));
-                a.C64n[(uint64_t)j * D + d] = v;
-                if (a.host_cb) a.host_cb[(uint64_t)j * D + d] = v;
-            }
-            if (d < Dp) a.C32[(uint64_t)j * Dp + d] = (float)v;
-            if (a.rows) {   // MFMA row (common.hpp): hi / lo at their slots, norm at 2 LO
-                const uint32_t RF = cb_row_f16(D, Dp), LO = cb_lo_off(D, Dp);
-                _Float16 *row = a.rows + (uint64_t)j * RF;
-                const double cp = d < D ? v - a.mu : 0.0;
-                double n = cp * cp;   // L >= LO lanes per row
-                for (uint32_t off = L / 2; off >= 1; off >>= 1) n += __shfl_xor(n, (int)off, (int)L);
-                if (d < D) {
-                    const double c2 = -2.0 * a.sx * cp * a.scale_t;
-                    const _Float16 h = (_Float16)(float)c2;
-                    row[cb_hi_slot(D, Dp, d)] = h;
-                    row[cb_lo_slot(D, Dp, d)] = (_Float16)(float)(c2 - (double)(float)h);
-                } else if (d < LO) {
-                    row[cb_hi_slot(D, Dp, d)] = (_Float16)0.f;
-                    row[cb_lo_slot(D, Dp, d)] = (_Float16)0.f;
-                }
-                n *= a.scale_t;
-                const _Float16 h = (_Float16)(float)n;
-                const _Float16 l = (_Float16)(float)(n - (double)(float)h);
-                for (uint32_t i = 2 * LO + d; i < RF; i += L)
-                    row[i] = i == 2 * LO ? h : (i == 2 * LO + 1 ? l : (_Float16)0.f);
-                if (a.E32 && d < 16)   // L = 16 lanes for D = 12
-                    a.E32[(uint64_t)j * 16 + d] =
-                        d < D ? (float)(-2.0 * a.sx * cp * a.scale_t) : (d == D ? (float)n : 0.f);
-            }
-        } else if (j < a.Kpad_next) {
-            if (d < Dp) a.C32[(uint64_t)j * Dp + d] = 0.f;
-            if (a.E32 && d < 16) a.E32[(uint64_t)j * 16 + d] = d == D ? 1e30f : 0.f;   // never wins
-            if (a.rows) {
-                const uint32_t RF = cb_row_f16(D, Dp), LO = cb_lo_off(D, Dp);
-                _Float16 *row = a.rows + (uint64_t)j * RF;
-                for (uint32_t i = d; i < RF; i += L)
-                    row[i] = (_Float16)(i == 2 * LO || i == 2 * LO + 1 ? MF_PAD_SCORE : 0.f);
-            }
-        }
+        const uint32_t k = j < K ? j : j - K;
+        const uint64_t c = (uint64_t)d * K + k;
+        const bool have = j < 2 * K && d < D;
+        finalize_split_item(a, j, d, L, have ? sums_at(c) : 0, have ? sums_at(KD + c) : 0,
+                            j < 2 * K ? sums_at(2 * KD + k) : 0);
         return 0.0;
     }
     if (j < K && d < D) {
@@ -1073,22 +1054,34 @@ __device__ inline double finalize_item(const FinArgs &a, uint32_t j, uint32_t d,
 constexpr uint32_t PRUNE_MAXK = 1024, PRUNE_NB = 256;
 __device__ void prune_order(const double *__restrict__ C64n, uint32_t K2, uint32_t Kpad, double mu, double sx,
                             uint32_t *__restrict__ perm, int32_t *__restrict__ tint) {
+    // (any block size >= 256: threads past 256 only meet the barriers)
     __shared__ float q[PRUNE_MAXK];
-    __shared__ uint32_t pos_of[PRUNE_MAXK];
+    __shared__ float qs[PRUNE_MAXK];   // q by position
     __shared__ uint32_t hist[PRUNE_NB];
     __shared__ float qr[2][256];
     const uint32_t tid = threadIdx.x;
+    const bool act = tid < 256;
     float mn = INFINITY, mx = -INFINITY;
-    for (uint32_t j = tid; j < K2; j += 256) {
-        double sum = 0;
-        for (uint32_t d = 0; d < MF_D; d++) sum += C64n[(uint64_t)j * MF_D + d] - mu;
-        q[j] = (float)(sum / sx);
-        mn = fminf(mn, q[j]);
-        mx = fmaxf(mx, q[j]);
+#pragma unroll
+    for (uint32_t i = 0; i < PRUNE_MAXK / 256; i++) {   // (all loads of a thread in flight)
+        const uint32_t j = tid + 256 * i;
+        if (act && j < K2) {
+            double c[MF_D];
+#pragma unroll
+            for (uint32_t d = 0; d < MF_D; d++) c[d] = C64n[(uint64_t)j * MF_D + d];
+            double sum = 0;
+#pragma unroll
+            for (uint32_t d = 0; d < MF_D; d++) sum += c[d] - mu;
+            q[j] = (float)(sum / sx);
+            mn = fminf(mn, q[j]);
+            mx = fmaxf(mx, q[j]);
+        }
     }
-    for (uint32_t b = tid; b < PRUNE_NB; b += 256) hist[b] = 0;
-    qr[0][tid] = mn;
-    qr[1][tid] = mx;
+    if (act) {
+        hist[tid] = 0;
+        qr[0][tid] = mn;
+        qr[1][tid] = mx;
+    }
     __syncthreads();
     for (int w = 128; w > 0; w >>= 1) {
         if ((int)tid < w) {
@@ -1099,44 +1092,72 @@ __device__ void prune_order(const double *__restrict__ C64n, uint32_t K2, uint32
     }
     const float qmin = qr[0][0], inv = (float)PRUNE_NB / (qr[1][0] - qmin + 1.0f);
     auto bucket = [&](float v) { return min((uint32_t)((v - qmin) * inv), PRUNE_NB - 1); };
-    for (uint32_t j = tid; j < K2; j += 256) atomicAdd(&hist[bucket(q[j])], 1u);
+    if (act)
+        for (uint32_t j = tid; j < K2; j += 256) atomicAdd(&hist[bucket(q[j])], 1u);
     __syncthreads();
-    if (tid == 0) {   // exclusive scan (256 entries)
-        uint32_t run = 0;
-        for (uint32_t b = 0; b < PRUNE_NB; b++) {
-            const uint32_t c = hist[b];
-            hist[b] = run;
-            run += c;
+    {   // exclusive scan of the 256 bucket counts (one per thread, Hillis-Steele)
+        static_assert(PRUNE_NB == 256, "one bucket per thread");
+        const uint32_t own = act ? hist[tid] : 0u;
+        uint32_t v = own;
+        for (uint32_t off = 1; off < PRUNE_NB; off <<= 1) {
+            __syncthreads();
+            const uint32_t add = act && tid >= off ? hist[tid - off] : 0u;
+            __syncthreads();
+            v += add;
+            if (act) hist[tid] = v;
         }
+        __syncthreads();
+        if (act) hist[tid] = v - own;
     }
     __syncthreads();
-    for (uint32_t j = tid; j < K2; j += 256) {   // (order inside a bucket: any)
-        const uint32_t p = atomicAdd(&hist[bucket(q[j])], 1u);
-        perm[p] = j;
-        pos_of[p] = j;
+    if (act) {
+        for (uint32_t j = tid; j < K2; j += 256) {   // (order inside a bucket: any)
+            const uint32_t p = atomicAdd(&hist[bucket(q[j])], 1u);
+            perm[p] = j;
+            qs[p] = q[j];
+        }
+        for (uint32_t p = K2 + tid; p < Kpad; p += 256) perm[p] = p;
     }
-    for (uint32_t p = K2 + tid; p < Kpad; p += 256) perm[p] = p;
     __syncthreads();
+    // tile t = positions 32t .. 32t + 31: four per thread, then over 8 lanes
     __shared__ int32_t tlo[PRUNE_MAXK / 32], thi[PRUNE_MAXK / 32];
     const uint32_t nt = Kpad / 32;
-    for (uint32_t t = tid; t < nt; t += 256) {
+    if (act) {
         float lo = INFINITY, hi = -INFINITY;
-        for (uint32_t p = t * 32; p < min(t * 32 + 32, K2); p++) {
-            lo = fminf(lo, q[pos_of[p]]);
-            hi = fmaxf(hi, q[pos_of[p]]);
+#pragma unroll
+        for (uint32_t i = 0; i < 4; i++) {
+            const uint32_t p = 4 * tid + i;
+            if (p < K2) {
+                lo = fminf(lo, qs[p]);
+                hi = fmaxf(hi, qs[p]);
+            }
         }
-        tlo[t] = lo <= hi ? (int32_t)floorf(lo) - 1 : 0x7FFFFFFF;
-        thi[t] = lo <= hi ? (int32_t)ceilf(hi) + 1 : (int32_t)0x80000000;
+#pragma unroll
+        for (int m = 1; m < 8; m <<= 1) {
+            lo = fminf(lo, __shfl_xor(lo, m));
+            hi = fmaxf(hi, __shfl_xor(hi, m));
+        }
+        if ((tid & 7) == 0 && tid / 8 < nt) {
+            tlo[tid / 8] = lo <= hi ? (int32_t)floorf(lo) - 1 : 0x7FFFFFFF;
+            thi[tid / 8] = lo <= hi ? (int32_t)ceilf(hi) + 1 : (int32_t)0x80000000;
+        }
     }
     __syncthreads();
     // Tiles sharing a bucket can overlap out of order: store monotone envelopes (lo: the suffix
     // minimum, hi: the prefix maximum; still bounds of every tile), so that a scan leaving tile t
-    // may skip every tile beyond it on that side.
-    if (tid == 0) {
-        int32_t m = 0x7FFFFFFF;
-        for (int t = (int)nt - 1; t >= 0; t--) tint[2 * t] = m = min(m, tlo[t]);
-        m = (int32_t)0x80000000;
-        for (uint32_t t = 0; t < nt; t++) tint[2 * t + 1] = m = max(m, thi[t]);
+    // may skip every tile beyond it on that side.  One wave, lane t = tile t (nt <= 32).
+    if (tid < 64) {
+        int32_t m = tid < nt ? tlo[tid] : 0x7FFFFFFF, M = tid < nt ? thi[tid] : (int32_t)0x80000000;
+#pragma unroll
+        for (int o = 1; o < 32; o <<= 1) {
+            const int32_t dn = __shfl_down(m, o), up = __shfl_up(M, o);
+            if ((int)tid + o < 64) m = min(m, dn);
+            if ((int)tid >= o) M = max(M, up);
+        }
+        if (tid < nt) {
+            tint[2 * tid] = m;
+            tint[2 * tid + 1] = M;
+        }
     }
 }
 
@@ -1144,28 +1165,27 @@ __device__ inline uint32_t fin_rows(const FinArgs &a) { return a.split ? max(2 *
 
 // Grid-stride over groups of 256/L rows.  Each wave fences its mapped-host writes once, after
 // its last row (a system fence writes back the L2: per row it cost ~25 ns x rows).
-__global__ __launch_bounds__(256) void finalize_prep_kernel(FinArgs a, double *__restrict__ dist_part,
-                                                            unsigned *__restrict__ done, double *__restrict__ dist_out,
-                                                            volatile uint64_t *ready, uint64_t seq, uint32_t L) {
-    const uint32_t d = threadIdx.x % L, r = threadIdx.x / L;
-    const uint32_t per = 256 / L, n = fin_rows(a);
-    double term = 0.0;
-    for (uint32_t j0 = blockIdx.x * per; j0 < n; j0 += gridDim.x * per) term += finalize_item(a, j0 + r, d, L);
-    if (!done) return;
-    __shared__ double red[256];
+// The end of a finalize block: its distortion partial (red: blockDim doubles of LDS, tree order
+// over the block's threads; none without red), the done count, and in the last block the
+// distortion total (block order), the clearing, the next search's tile order and the host's
+// ready number.
+__device__ void finalize_block_done(const FinArgs &a, double term, double *red, double *__restrict__ dist_part,
+                                    unsigned *__restrict__ done, double *__restrict__ dist_out,
+                                    volatile uint64_t *ready, uint64_t seq) {
     __shared__ bool last;
-    red[threadIdx.x] = term;
+    if (red) red[threadIdx.x] = term;
     // host_cb: every wave's mapped stores complete before the barrier, and thread 0's
     // system-scope fence below releases them with the block's count (MI355X guide's
     // producer pattern: one fence per block, not one per thread)
     if (a.host_cb) __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    for (int w = 128; w > 0; w >>= 1) {
-        if ((int)threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
-        __syncthreads();
-    }
+    if (red)
+        for (int w = (int)blockDim.x / 2; w > 0; w >>= 1) {
+            if ((int)threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
+            __syncthreads();
+        }
     if (threadIdx.x == 0) {
-        dist_part[blockIdx.x] = red[0];
+        if (red) dist_part[blockIdx.x] = red[0];
         if (a.host_cb) __threadfence_system();
         else __threadfence();
         last = atomicAdd(done, 1u) == gridDim.x - 1;
@@ -1192,6 +1212,20 @@ __global__ __launch_bounds__(256) void finalize_prep_kernel(FinArgs a, double *_
             *ready = seq;
         }
     }
+}
+
+// Grid-stride over groups of 256/L rows.  Each wave fences its mapped-host writes once, after
+// its last row (a system fence writes back the L2: per row it cost ~25 ns x rows).
+__global__ __launch_bounds__(256) void finalize_prep_kernel(FinArgs a, double *__restrict__ dist_part,
+                                                            unsigned *__restrict__ done, double *__restrict__ dist_out,
+                                                            volatile uint64_t *ready, uint64_t seq, uint32_t L) {
+    const uint32_t d = threadIdx.x % L, r = threadIdx.x / L;
+    const uint32_t per = 256 / L, n = fin_rows(a);
+    double term = 0.0;
+    for (uint32_t j0 = blockIdx.x * per; j0 < n; j0 += gridDim.x * per) term += finalize_item(a, j0 + r, d, L);
+    if (!done) return;
+    __shared__ double red[256];
+    finalize_block_done(a, term, red, dist_part, done, dist_out, ready, seq);
 }
 
 static FinArgs fin_args(const uint64_t *sums, uint32_t K, uint32_t D, uint32_t Dp, int64_t R, int64_t bias,

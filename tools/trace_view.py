@@ -8,7 +8,7 @@ import sys
 
 SHORT = [("assign_small", "search"), ("assign_mfma", "search"), ("assign_mf32", "search"), ("assign_wide", "search"),
          ("assign_valu", "search"), ("recheck", "recheck"), ("kd_resolve", "kd"), ("reduce_kernel", "reduce"),
-         ("finalize_prep", "final"), ("finalize_kernel", "final"), ("update_runs", "update")]
+         ("finalize_prep", "final"), ("finalize_kernel", "final"), ("reduce_split", "final"), ("update_runs", "update")]
 
 
 def short(name):
