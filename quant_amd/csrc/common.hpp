@@ -132,6 +132,71 @@ __device__ inline void move_row_terms(const uint8_t *codes, uint32_t Dp, uint32_
     }
 }
 
+// The same move into a second copy of the final sums (layout hi[D][K] | lo[D][K] | cnt[K], u64,
+// added mod 2^64 to copy 0 by the finalize): kd_reduce_kernel's ties, concurrent with the
+// reduce of the slabs into copy 0.
+__device__ inline void move_row_sums(const uint8_t *codes, uint32_t Dp, uint32_t D, uint32_t row, uint32_t from,
+                                     uint32_t to, uint32_t K, uint64_t *xs, const uint64_t *plut, uint32_t lane) {
+    const uint64_t KD = (uint64_t)K * D;
+    if (lane < D) {
+        const uint64_t t = plut[codes[(uint64_t)row * Dp + lane]];
+        const unsigned long long hi = t >> 32, lo = t & 0xFFFFFFFFull;
+        atomicAdd((unsigned long long *)&xs[(uint64_t)lane * K + to], hi);
+        atomicAdd((unsigned long long *)&xs[KD + (uint64_t)lane * K + to], lo);
+        atomicAdd((unsigned long long *)&xs[(uint64_t)lane * K + from], 0ull - hi);
+        atomicAdd((unsigned long long *)&xs[KD + (uint64_t)lane * K + from], 0ull - lo);
+    }
+    if (lane == 0) {
+        atomicAdd((unsigned long long *)&xs[2 * KD + to], 1ull);
+        atomicAdd((unsigned long long *)&xs[2 * KD + from], ~0ull);
+    }
+}
+
+// Column reduce of G slabs into sums (copy 0 of the final layout) by one 1024-thread block: 64
+// columns, 16 waves each adding every 16th slab, combined through red (2 x 16 x 64 u64).  The
+// last nsub slabs are subtracted (hi and lo separately: the corrections of re-assigned rows,
+// whose terms the search had added at their provisional index); every total stays >= 0.
+__device__ inline void reduce_columns_block(const uint64_t *__restrict__ part, const uint32_t *__restrict__ part_cnt,
+                                            uint32_t G, uint32_t nsub, uint32_t K, uint32_t D,
+                                            uint64_t *__restrict__ sums, uint32_t bid, uint64_t *red) {
+    uint64_t(*red_hi)[64] = reinterpret_cast<uint64_t(*)[64]>(red);
+    uint64_t(*red_lo)[64] = reinterpret_cast<uint64_t(*)[64]>(red + 16 * 64);
+    const uint64_t KD = (uint64_t)K * D;
+    const uint64_t col = (uint64_t)bid * 64 + (threadIdx.x & 63);
+    const int sg = threadIdx.x >> 6;
+    uint64_t hi = 0, lo = 0;
+    if (col < KD) {
+#pragma unroll 4
+        for (uint32_t g = sg; g < G; g += 16) {
+            const uint64_t p = part[g * KD + col];
+            const uint64_t sgn = g < G - nsub ? 0 : ~0ull;   // x ^ sgn - sgn: +x or -x (mod 2^64)
+            hi += ((p >> 32) ^ sgn) - sgn;
+            lo += ((p & 0xFFFFFFFFull) ^ sgn) - sgn;
+        }
+    } else if (col < KD + K) {
+#pragma unroll 4
+        for (uint32_t g = sg; g < G; g += 16) {
+            const uint64_t c = part_cnt[(uint64_t)g * K + (col - KD)];
+            hi += g < G - nsub ? c : 0ull - c;
+        }
+    }
+    red_hi[sg][threadIdx.x & 63] = hi;
+    red_lo[sg][threadIdx.x & 63] = lo;
+    __syncthreads();
+    if (sg == 0) {
+        for (int i = 1; i < 16; i++) {
+            hi += red_hi[i][threadIdx.x];
+            lo += red_lo[i][threadIdx.x];
+        }
+        if (col < KD) {
+            sums[col] = hi;
+            sums[KD + col] = lo;
+        } else if (col < KD + K) {
+            sums[2 * KD + (col - KD)] = hi;
+        }
+    }
+}
+
 struct MfThresholds {
     float mfma, alpha, beta, gamma;
     float inv_scale;   // 2^-t
@@ -192,6 +257,12 @@ hipError_t launch_recheck_mf32(hipStream_t s, int num_cu, const uint8_t *codes, 
 // terms to sums when given.  kd_resolve_fits: the tree, stacks and one wave's point
 // distances fit the LDS.
 bool kd_resolve_fits(const KdView &kd, uint32_t K);
+// kd_reduce_kernel: launch_kd_resolve (ties into copy 1 of sums) + launch_reduce (into copy 0).
+bool kd_reduce_fits(const KdView &kd, uint32_t K);
+hipError_t launch_kd_reduce(hipStream_t s, const uint8_t *codes, uint32_t Dp, uint32_t D, const uint32_t *ties,
+                            const unsigned *tie_cnt, const double *C64, uint32_t K, const double *lut64,
+                            const KdView &kd, uint32_t *A, const uint64_t *plut, const uint64_t *part,
+                            const uint32_t *part_cnt, uint32_t G, uint32_t nsub, uint64_t *sums, uint64_t *sums1);
 hipError_t launch_kd_resolve(hipStream_t s, const uint8_t *codes, uint32_t Dp, uint32_t D, const uint32_t *ties,
                              const unsigned *tie_cnt, const double *C64, uint32_t K, const double *lut64,
                              const KdView &kd, uint32_t *A, uint64_t *xslab, uint32_t *xcnt, const uint64_t *plut);
@@ -231,7 +302,10 @@ hipError_t launch_finalize_prep(hipStream_t s, const uint64_t *sums, uint32_t K,
                                 int64_t bias, int scale, double *C_cent, bool split, double *C64n, uint32_t Kpad_next,
                                 double mu, double sx, int t, float *C32, _Float16 *cb_rows, float *E32,
                                 double *host_cb, double *dist_part, unsigned *done, double *dist_out, uint64_t *ready, uint64_t seq,
-                                bool zero_sums, uint32_t ncopy = 1, uint32_t *perm = nullptr, int32_t *tint = nullptr);
+                                bool zero_sums, uint32_t ncopy = 1, uint32_t *perm = nullptr, int32_t *tint = nullptr,
+                                uint32_t zero_skip = 0, uint64_t copy_stride = 0, const unsigned *copy_gate = nullptr);
+// (zero_sums: clears copies zero_skip .. ncopy - 1; copy_stride 0: the copies follow each other,
+// 2KD + K apart; copy_gate: copies past the first are read and cleared only if *copy_gate != 0)
 hipError_t launch_finalize(hipStream_t s, const uint64_t *sums, uint32_t K, uint32_t D, int64_t R, int64_t bias,
                            int scale, double *C_cent);
 // f16 MFMA tables (D = 12) and fp32 VALU table from an fp64 codebook of K code vectors.

@@ -135,6 +135,10 @@ struct qvq_ctx {
     std::vector<double> cb_local;   // host copy of the published codebook for the tree build
     uint64_t tree_cap = 0;
     uint32_t nslabs = 0;   // slabs holding the last run_level's sums
+    bool kd_pend = false;      // run_level left its kd-tree ties to kd_reduce_kernel (pend_kd)
+    KdView pend_kd{};
+    bool sums1_dirty = false;  // copy 1 of d_sums may hold moves (a quantize that stopped early)
+    uint64_t sums_bytes = 0;
     uint32_t nsub = 0;     // ... of which the last nsub are subtracted
     int timing_level = -1;   // qvq_set_timing: -1 all levels, -2 none, else that level only
     bool upd[32] = {};
@@ -392,7 +396,11 @@ qvq_status ensure_levels(qvq_ctx *ctx, uint32_t Kmax) {
     // the new index (+) and at the search's provisional one (-))
     HIPCHK(hipMalloc(&ctx->d_part, (uint64_t)(ctx->G + 2) * KD * 8));
     HIPCHK(hipMalloc(&ctx->d_part_cnt, (uint64_t)(ctx->G + 2) * Kmax * 4));
-    HIPCHK(hipMalloc(&ctx->d_sums, (2 * KD + Kmax) * 8));
+    // two copies of the final sums: copy 1 takes the kd-tree ties' moves (kd_reduce_kernel) and
+    // is zero between levels (the finalize that adds it clears it)
+    HIPCHK(hipMalloc(&ctx->d_sums, 2 * (2 * KD + Kmax) * 8));
+    HIPCHK(hipMemset(ctx->d_sums, 0, 2 * (2 * KD + Kmax) * 8));
+    ctx->sums_bytes = 2 * (2 * KD + Kmax) * 8;
     const unsigned mflags = hipHostMallocMapped | hipHostMallocCoherent;
     HIPCHK(hipHostMalloc(&ctx->h_cb, KD * 8, mflags));
     HIPCHK(hipHostGetDevicePointer((void **)&ctx->dh_cb, ctx->h_cb, 0));
@@ -668,8 +676,19 @@ qvq_status resolve_host_ties(qvq_ctx *ctx, const double *hC, uint32_t K, uint32_
 // to be subtracted (fused: the search's G slabs with every row at its provisional index, slab
 // G with the rows the recheck and the kd-tree move at their new index, slab G + 1 with the
 // same rows at the provisional one; otherwise the update's G).
+// Copy 1 of d_sums sits one capacity-sized copy in, where no level's copy 0 reaches.
+uint64_t sums_cap_stride(const qvq_ctx *ctx) { return 2 * (uint64_t)ctx->Kcap * ctx->D + ctx->Kcap; }
+
+// One rank, fused sums: the kd-tree ties go with the reduce (kd_reduce_kernel: one launch fewer
+// per level; QVQ_KD_REDUCE=0 keeps launch_kd_resolve + launch_reduce, A/B).
+bool kd_merge(const qvq_ctx *ctx) {
+    static const bool on = !env_is("QVQ_KD_REDUCE", "0");
+    return on && !ctx->comm && !ctx->host_ar && !(abl_skip() & 4);
+}
+
 qvq_status run_level(qvq_ctx *ctx, uint32_t K, int slot, bool sums_out, const double *hC, uint64_t wait_seq) {
     const bool fused = sums_out && use_fused(ctx, K);
+    ctx->kd_pend = false;
     uint64_t *xslab = fused ? ctx->d_part + (uint64_t)ctx->G * K * ctx->D : nullptr;
     uint32_t *xcnt = fused ? ctx->d_part_cnt + (uint64_t)ctx->G * K : nullptr;
     ctx->nslabs = fused ? ctx->G + 2 : ctx->G;
@@ -724,6 +743,9 @@ qvq_status run_level(qvq_ctx *ctx, uint32_t K, int slot, bool sums_out, const do
     ctx->tm.wait_ms[slot] = std::chrono::duration<double, std::milli>(tw1 - tw0).count();
     ctx->tm.tree_ms[slot] = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tw1).count();
     if (abl_skip() & 2) {
+    } else if (kd.depth > 0 && fused && kd_merge(ctx) && kd_reduce_fits(kd, K)) {
+        ctx->kd_pend = true;   // with the reduce (qvq_lbg)
+        ctx->pend_kd = kd;
     } else if (kd.depth > 0) {
         HIPCHK(launch_kd_resolve(ctx->stream, ctx->d_codes, ctx->Dp, ctx->D, ctx->d_ties, &cnt[1], ctx->d_C64_split,
                                  K, ctx->d_lut64, kd, ctx->d_A, xslab, xcnt, ctx->d_plut));
@@ -1144,7 +1166,12 @@ QVQ_API qvq_status qvq_lbg(qvq_ctx *ctx, uint32_t bits, double eps, double *code
     unsigned *dist_done = ctx->d_counters + 2 * 33;
     // finalize (+ split, tables, host codebook and its ready number) / final distortion
     // (K = 1 reads the mean sums and leaves them cleared for the next quantize)
-    auto finalize = [&](uint32_t K, bool split) {
+    if (ctx->sums1_dirty) {   // a quantize stopped between a kd_reduce and its finalize
+        HIPCHK(hipMemsetAsync(ctx->d_sums, 0, ctx->sums_bytes, ctx->stream));
+        ctx->sums1_dirty = false;
+    }
+    // copies 2: copy 1 holds the ties' moves (added, then cleared by the finalize's last block)
+    auto finalize = [&](uint32_t K, bool split, uint32_t copies = 1, const unsigned *gate = nullptr) {
         if (split) ctx->seq++;
         const bool prune = split && use_prune(ctx, 2 * K);   // the next search's tile order
         ctx->perm_k = prune ? 2 * K : 0;
@@ -1154,8 +1181,10 @@ QVQ_API qvq_status qvq_lbg(qvq_ctx *ctx, uint32_t bits, double eps, double *code
                                     ctx->d_C32, ctx->d_rows, ctx->d_E32, split ? ctx->dh_cb : nullptr, d_dist + 8,
                                     dist_done,
                                     split ? nullptr : d_dist + 2, split ? ctx->dh_ready : nullptr, ctx->seq,
-                                    K == 1, K == 1 ? MEAN_COPIES : 1, prune ? ctx->d_perm : nullptr,
-                                    prune ? ctx->d_tint : nullptr);
+                                    K == 1 || copies > 1, K == 1 ? MEAN_COPIES : copies,
+                                    prune ? ctx->d_perm : nullptr, prune ? ctx->d_tint : nullptr, K == 1 ? 0 : 1,
+                                    copies > 1 ? sums_cap_stride(ctx) : 0,
+                                    gate);
     };
     HIPCHK(finalize(1, bits > 0));
     // with bits >= 1 the first search writes every row's index
@@ -1167,11 +1196,23 @@ QVQ_API qvq_status qvq_lbg(qvq_ctx *ctx, uint32_t bits, double eps, double *code
         if ((st = run_level(ctx, K, slot, true, ctx->h_cb, ctx->seq)) != QVQ_OK) return st;
         const bool split = lvl < bits;
         {
-            if (!(abl_skip() & 4) && ctx->nslabs)   // nslabs 0: the sorted sums are in d_sums already
+            uint32_t copies = 1;
+            const unsigned *tcnt = ctx->d_counters + 2 * ((int)lvl - 1) + 1;   // the level's ties
+            if (ctx->kd_pend) {   // the level's ties and the reduce together
+                HIPCHK(launch_kd_reduce(ctx->stream, ctx->d_codes, ctx->Dp, ctx->D, ctx->d_ties, tcnt,
+                                        ctx->d_C64_split, K, ctx->d_lut64, ctx->pend_kd, ctx->d_A, ctx->d_plut,
+                                        ctx->d_part, ctx->d_part_cnt, ctx->nslabs, ctx->nsub, ctx->d_sums,
+                                        ctx->d_sums + sums_cap_stride(ctx)));
+                ctx->kd_pend = false;
+                ctx->sums1_dirty = true;
+                copies = 2;
+            } else if (!(abl_skip() & 4) && ctx->nslabs) {   // nslabs 0: the sorted sums are in d_sums already
                 HIPCHK(launch_reduce(ctx->stream, ctx->d_part, ctx->d_part_cnt, ctx->nslabs, ctx->nsub, K, ctx->D,
                                      ctx->d_sums));
+            }
             if ((st = all_reduce_sums(ctx, K)) != QVQ_OK) return st;
-            HIPCHK(finalize(K, split));
+            HIPCHK(finalize(K, split, copies, copies > 1 ? tcnt : nullptr));
+            if (copies > 1) ctx->sums1_dirty = false;
         }
     }
     // Returned distortion: updateDistortion after the last fix (src/Quantizer.cpp:9-22,103),

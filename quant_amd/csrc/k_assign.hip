@@ -1226,4 +1226,42 @@ hipError_t launch_kd_resolve(hipStream_t s, const uint8_t *codes, uint32_t Dp, u
     return hipGetLastError();
 }
 
+// The kd-tree ties and the slabs' column reduce in one launch (fused sums, one rank): blocks
+// below KDR_BLOCKS answer ties (kd_resolve_block; their moves go to copy 1 of the sums, which the
+// finalize adds), the others reduce 64 columns each into copy 0.  The two touch disjoint data
+// (the slabs hold the search's and the recheck's terms only), so neither waits for the other,
+// and a level without ties pays one launch instead of two.
+__global__ __launch_bounds__(1024) void kd_reduce_kernel(KdArgs a, const unsigned *__restrict__ tie_cnt, int W,
+                                                         int whole_block, const uint64_t *__restrict__ part,
+                                                         const uint32_t *__restrict__ part_cnt, uint32_t G,
+                                                         uint32_t nsub, uint64_t *__restrict__ sums) {
+    extern __shared__ __attribute__((aligned(16))) double ksm[];
+    if (blockIdx.x < (uint32_t)KDR_BLOCKS) {
+        kd_resolve_block(a, *tie_cnt, blockIdx.x, KDR_BLOCKS, W, ksm, whole_block != 0);
+        return;
+    }
+    reduce_columns_block(part, part_cnt, G, nsub, a.K, a.D, sums, blockIdx.x - KDR_BLOCKS,
+                         reinterpret_cast<uint64_t *>(ksm));
+}
+
+bool kd_reduce_fits(const KdView &kd, uint32_t K) { return kd_resolve_fits(kd, K); }
+
+hipError_t launch_kd_reduce(hipStream_t s, const uint8_t *codes, uint32_t Dp, uint32_t D, const uint32_t *ties,
+                            const unsigned *tie_cnt, const double *C64, uint32_t K, const double *lut64,
+                            const KdView &kd, uint32_t *A, const uint64_t *plut, const uint64_t *part,
+                            const uint32_t *part_cnt, uint32_t G, uint32_t nsub, uint64_t *sums, uint64_t *sums1) {
+    int W = kd.depth > 0 ? kd_waves(kd, K) : 0;
+    if (W == 0 || nsub > G) return hipErrorInvalidValue;
+    static const bool whole_ok = !(std::getenv("QVQ_KDR_WHOLE") && std::getenv("QVQ_KDR_WHOLE")[0] == '0');
+    const bool whole = whole_ok && (size_t)K * D >= 8192;
+    if (whole) W = 1;
+    const size_t lds = std::max(kd_tree_bytes(kd) + (size_t)W * kd_wave_bytes(kd, K), (size_t)2 * 16 * 64 * 8);
+    // sums1 (the finalize's copy 1) takes the ties' moves
+    const KdArgs a{codes, Dp, D, ties, C64, K, lut64, kd, A, nullptr, nullptr, plut, sums1};
+    const uint64_t cols = (uint64_t)K * D + K;
+    hipLaunchKernelGGL(kd_reduce_kernel, dim3((int)(KDR_BLOCKS + (cols + 63) / 64)), dim3(1024), lds, s, a, tie_cnt,
+                       W, whole ? 1 : 0, part, part_cnt, G, nsub, sums);
+    return hipGetLastError();
+}
+
 }  // namespace qvq

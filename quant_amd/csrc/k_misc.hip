@@ -580,50 +580,14 @@ hipError_t launch_sorted_sums(hipStream_t s, uint32_t Dp, uint32_t G, const uint
     return hipErrorInvalidValue;
 }
 
-// Column reduce of G slabs into sums (layout in the file header).  A workgroup owns 64
-// columns; its 16 waves each add every 16th slab, then combine through LDS.  The last nsub
-// slabs are subtracted (hi and lo separately: the corrections of re-assigned rows, whose
-// terms the search had added at their provisional index); every total stays >= 0.
+// Column reduce of G slabs into sums (layout in the file header; common.hpp reduce_columns_block).
 constexpr int REDUCE_THREADS = 1024;
 __global__ __launch_bounds__(REDUCE_THREADS) void reduce_kernel(const uint64_t *__restrict__ part,
                                                                 const uint32_t *__restrict__ part_cnt, uint32_t G,
                                                                 uint32_t nsub, uint32_t K, uint32_t D,
                                                                 uint64_t *__restrict__ sums) {
-    __shared__ uint64_t red_hi[16][64], red_lo[16][64];
-    const uint64_t KD = (uint64_t)K * D;
-    const uint64_t col = (uint64_t)blockIdx.x * 64 + (threadIdx.x & 63);
-    const int sg = threadIdx.x >> 6;
-    uint64_t hi = 0, lo = 0;
-    if (col < KD) {
-#pragma unroll 4
-        for (uint32_t g = sg; g < G; g += 16) {
-            const uint64_t p = part[g * KD + col];
-            const uint64_t sgn = g < G - nsub ? 0 : ~0ull;   // x ^ sgn - sgn: +x or -x (mod 2^64)
-            hi += ((p >> 32) ^ sgn) - sgn;
-            lo += ((p & 0xFFFFFFFFull) ^ sgn) - sgn;
-        }
-    } else if (col < KD + K) {
-#pragma unroll 4
-        for (uint32_t g = sg; g < G; g += 16) {
-            const uint64_t c = part_cnt[(uint64_t)g * K + (col - KD)];
-            hi += g < G - nsub ? c : 0ull - c;
-        }
-    }
-    red_hi[sg][threadIdx.x & 63] = hi;
-    red_lo[sg][threadIdx.x & 63] = lo;
-    __syncthreads();
-    if (sg == 0) {
-        for (int i = 1; i < 16; i++) {
-            hi += red_hi[i][threadIdx.x];
-            lo += red_lo[i][threadIdx.x];
-        }
-        if (col < KD) {
-            sums[col] = hi;
-            sums[KD + col] = lo;
-        } else if (col < KD + K) {
-            sums[2 * KD + (col - KD)] = hi;
-        }
-    }
+    __shared__ uint64_t red[2 * 16 * 64];
+    reduce_columns_block(part, part_cnt, G, nsub, K, D, sums, blockIdx.x, red);
 }
 
 hipError_t launch_reduce(hipStream_t s, const uint64_t *part, const uint32_t *part_cnt, uint32_t G, uint32_t nsub,
@@ -954,7 +918,10 @@ struct FinArgs {
     bool dist;
     uint64_t *zero_after;   // cleared by the last block once every block has read sums (mean)
     uint32_t n_zero;
-    uint32_t ncopy;         // copies of the sums to add (stride 2KD + K): the mean's MEAN_COPIES
+    uint32_t ncopy;         // copies of the sums to add: the mean's MEAN_COPIES, or 2 (kd_reduce_kernel)
+    uint64_t cstride;       // u64 from one copy to the next (2KD + K, or the capacity's)
+    const unsigned *gate;   // non-null: copies past the first only when *gate != 0 (the level's
+                            // tie count: without ties copy 1 is all zero, read nor cleared)
     uint32_t *perm;         // split, D = 12: the next search's tile order (prune_order), or null
     int32_t *tint;
 };
@@ -1016,9 +983,10 @@ __device__ inline void finalize_split_item(const FinArgs &a, uint32_t j, uint32_
 __device__ inline double finalize_item(const FinArgs &a, uint32_t j, uint32_t d, uint32_t L) {
     const uint32_t K = a.K, D = a.D;
     const uint64_t KD = (uint64_t)K * D;
+    const uint32_t ncopy = a.gate && *a.gate == 0 ? 1 : a.ncopy;
     auto sums_at = [&](uint64_t i) {   // the sum of the ncopy copies
         uint64_t v = a.sums[i];
-        for (uint32_t c = 1; c < a.ncopy; c++) v += a.sums[c * (2 * KD + K) + i];
+        for (uint32_t c = 1; c < ncopy; c++) v += a.sums[c * a.cstride + i];
         return v;
     };
     if (a.split) {
@@ -1203,7 +1171,8 @@ __device__ void finalize_block_done(const FinArgs &a, double term, double *red, 
             dist_out[0] = t;
         }
     }
-    for (uint32_t i = threadIdx.x; i < a.n_zero; i += blockDim.x) a.zero_after[i] = 0;
+    if (!a.gate || *a.gate)
+        for (uint32_t i = threadIdx.x; i < a.n_zero; i += blockDim.x) a.zero_after[i] = 0;
     if (a.perm) prune_order(a.C64n, 2 * a.K, a.Kpad_next, a.mu, a.sx, a.perm, a.tint);
     if (threadIdx.x == 0) {
         *done = 0;
@@ -1254,6 +1223,8 @@ static FinArgs fin_args(const uint64_t *sums, uint32_t K, uint32_t D, uint32_t D
     a.zero_after = nullptr;
     a.n_zero = 0;
     a.ncopy = 1;
+    a.cstride = 2 * (uint64_t)K * D + K;
+    a.gate = nullptr;
     a.perm = nullptr;
     a.tint = nullptr;
     return a;
@@ -1263,7 +1234,8 @@ hipError_t launch_finalize_prep(hipStream_t s, const uint64_t *sums, uint32_t K,
                                 int64_t bias, int scale, double *C_cent, bool split, double *C64n, uint32_t Kpad_next,
                                 double mu, double sx, int t, float *C32, _Float16 *cb_rows, float *E32,
                                 double *host_cb, double *dist_part, unsigned *done, double *dist_out, uint64_t *ready,
-                                uint64_t seq, bool zero_sums, uint32_t ncopy, uint32_t *perm, int32_t *tint) {
+                                uint64_t seq, bool zero_sums, uint32_t ncopy, uint32_t *perm, int32_t *tint,
+                                uint32_t zero_skip, uint64_t copy_stride, const unsigned *copy_gate) {
     if (D == 0 || D > 64) return hipErrorInvalidValue;
     if (zero_sums && !done) return hipErrorInvalidValue;   // the clearing is the last block's
     const uint32_t L = D <= 16 ? 16 : (D <= 32 ? 32 : 64);
@@ -1272,14 +1244,20 @@ hipError_t launch_finalize_prep(hipStream_t s, const uint64_t *sums, uint32_t K,
     FinArgs a = fin_args(sums, K, D, Dp, R, bias, scale, C_cent, split, C64n, Kpad_next, mu, sx, t, C32, cb_rows,
                          E32, host_cb, dist_out != nullptr);
     a.ncopy = ncopy ? ncopy : 1;
+    a.gate = copy_gate;
+    if (copy_stride) {
+        if (copy_stride < 2 * (uint64_t)K * D + K) return hipErrorInvalidValue;
+        a.cstride = copy_stride;
+    }
     if (perm) {   // the last block orders the next search's code vectors (needs the done counter)
         if (!done || !split || D != MF_D || 2 * K > PRUNE_MAXK || Kpad_next % 32) return hipErrorInvalidValue;
         a.perm = perm;
         a.tint = tint;
     }
-    if (zero_sums) {
-        a.zero_after = const_cast<uint64_t *>(sums);
-        a.n_zero = a.ncopy * (2 * K * D + K);
+    if (zero_sums) {   // copies zero_skip .. ncopy - 1
+        if (zero_skip >= a.ncopy) return hipErrorInvalidValue;
+        a.zero_after = const_cast<uint64_t *>(sums) + (uint64_t)zero_skip * a.cstride;
+        a.n_zero = (uint32_t)((a.ncopy - zero_skip - 1) * a.cstride + 2 * (uint64_t)K * D + K);
     }
     hipLaunchKernelGGL(finalize_prep_kernel, dim3(grid), dim3(256), 0, s, a, dist_part, done, dist_out,
                        (volatile uint64_t *)ready, seq, L);
@@ -1291,7 +1269,7 @@ hipError_t launch_finalize(hipStream_t s, const uint64_t *sums, uint32_t K, uint
                            int scale, double *C_cent) {
     return launch_finalize_prep(s, sums, K, D, (D + 3) & ~3u, R, bias, scale, C_cent, false, nullptr, 0, 0, 0, 0,
                                 nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, 0, false, 1,
-                                nullptr, nullptr);
+                                nullptr, nullptr, 0, 0, nullptr);
 }
 
 // Search tables from an fp64 codebook: fp32 [Kpad][Dp] (VALU path and the MFMA recompute)

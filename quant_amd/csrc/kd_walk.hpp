@@ -171,6 +171,7 @@ struct KdArgs {
     uint64_t *xslab;     // fused sums: the correction slabs (move_row_terms), else nullptr
     uint32_t *xcnt;
     const uint64_t *plut;
+    uint64_t *xsums;     // or: copy 1 of the final sums (move_row_sums; kd_reduce_kernel), else nullptr
 };
 
 // Block b of nb answers ties f = b W + wave, + nb W, ... (waves >= W only help staging).
@@ -229,6 +230,7 @@ __device__ inline void kd_resolve_block(const KdArgs &a, unsigned nt, uint32_t b
                 const uint32_t from = __builtin_amdgcn_readfirstlane(a.A[row]);
                 if (k != from) {
                     if (a.xslab) move_row_terms(a.codes, a.Dp, D, row, from, k, K, a.xslab, a.xcnt, a.plut, lane);
+                    else if (a.xsums) move_row_sums(a.codes, a.Dp, D, row, from, k, K, a.xsums, a.plut, lane);
                     if (lane == 0) a.A[row] = k;
                 }
             }
@@ -261,6 +263,7 @@ __device__ inline void kd_resolve_block(const KdArgs &a, unsigned nt, uint32_t b
         const uint32_t from = __builtin_amdgcn_readfirstlane(a.A[row]);   // the search's index
         if (k != from) {
             if (a.xslab) move_row_terms(a.codes, a.Dp, D, row, from, k, K, a.xslab, a.xcnt, a.plut, lane);
+            else if (a.xsums) move_row_sums(a.codes, a.Dp, D, row, from, k, K, a.xsums, a.plut, lane);
             if (lane == 0) a.A[row] = k;
         }
         wave_lds_sync();
