@@ -265,7 +265,8 @@ hipError_t launch_kd_reduce(hipStream_t s, const uint8_t *codes, uint32_t Dp, ui
                             const uint32_t *part_cnt, uint32_t G, uint32_t nsub, uint64_t *sums, uint64_t *sums1);
 hipError_t launch_kd_resolve(hipStream_t s, const uint8_t *codes, uint32_t Dp, uint32_t D, const uint32_t *ties,
                              const unsigned *tie_cnt, const double *C64, uint32_t K, const double *lut64,
-                             const KdView &kd, uint32_t *A, uint64_t *xslab, uint32_t *xcnt, const uint64_t *plut);
+                             const KdView &kd, uint32_t *A, uint64_t *xslab, uint32_t *xcnt, const uint64_t *plut,
+                             uint64_t *xsums = nullptr);   // xsums: moves into a final-sums copy (move_row_sums)
 hipError_t launch_update(hipStream_t s, uint32_t Dp, uint32_t G, const uint8_t *codes, uint64_t N, const uint32_t *A,
                          uint32_t K, uint32_t D, const uint64_t *plut, uint64_t *part, uint32_t *part_cnt);
 // Sums of a final assignment straight into sums [hi KD][lo KD][cnt K] (no slabs, no reduce)
@@ -318,7 +319,7 @@ hipError_t launch_gather_codes(hipStream_t s, const uint8_t *codes, uint32_t Dp,
 // provisional index (A before) to the new one (move_row_terms).
 hipError_t launch_fix_rows(hipStream_t s, const uint8_t *codes, uint32_t Dp, uint32_t D, uint32_t *A,
                            const uint32_t *rows, const uint32_t *vals, uint32_t n, uint32_t K, uint64_t *xslab,
-                           uint32_t *xcnt, const uint64_t *plut);
+                           uint32_t *xcnt, const uint64_t *plut, uint64_t *xsums = nullptr);
 // 256-bin histogram of the first D bytes of every row (hist zeroed first).
 hipError_t launch_byte_hist(hipStream_t s, const uint8_t *codes, uint64_t N, uint32_t D, uint32_t Dp,
                             uint64_t *hist);

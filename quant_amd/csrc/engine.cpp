@@ -136,6 +136,7 @@ struct qvq_ctx {
     uint64_t tree_cap = 0;
     uint32_t nslabs = 0;   // slabs holding the last run_level's sums
     bool kd_pend = false;      // run_level left its kd-tree ties to kd_reduce_kernel (pend_kd)
+    uint32_t sums_copies = 1;  // 2: run_level's tie moves are in copy 1 of d_sums (the finalize adds it)
     KdView pend_kd{};
     bool sums1_dirty = false;  // copy 1 of d_sums may hold moves (a quantize that stopped early)
     uint64_t sums_bytes = 0;
@@ -637,7 +638,8 @@ qvq_status wait_codebook(qvq_ctx *ctx, uint64_t seq) { return wait_flag(ctx, ctx
 // Tie rows listed by the recheck when no device tree was available: answer them with the
 // host tree over hC and write A; with accumulate their terms move from the search's
 // provisional index to the answer (launch_fix_rows).  Synchronous.
-qvq_status resolve_host_ties(qvq_ctx *ctx, const double *hC, uint32_t K, uint32_t nt, bool accumulate) {
+qvq_status resolve_host_ties(qvq_ctx *ctx, const double *hC, uint32_t K, uint32_t nt, bool accumulate,
+                             uint64_t *xsums = nullptr) {
     const uint32_t D = ctx->D, Dp = ctx->Dp;
     const uint64_t need = (uint64_t)nt * (8 + Dp);
     if (ctx->scatter_bytes < need) {
@@ -664,7 +666,7 @@ qvq_status resolve_host_ties(qvq_ctx *ctx, const double *hC, uint32_t K, uint32_
     uint64_t *xslab = accumulate ? ctx->d_part + (uint64_t)ctx->G * K * D : nullptr;
     uint32_t *xcnt = accumulate ? ctx->d_part_cnt + (uint64_t)ctx->G * K : nullptr;
     HIPCHK(launch_fix_rows(ctx->stream, ctx->d_codes, Dp, D, ctx->d_A, d_rows, d_vals, nt, K, xslab, xcnt,
-                           ctx->d_plut));
+                           ctx->d_plut, xsums));
     HIPCHK(hipStreamSynchronize(ctx->stream));   // the host vectors must outlive the copies
     return QVQ_OK;
 }
@@ -689,6 +691,12 @@ bool kd_merge(const qvq_ctx *ctx) {
 qvq_status run_level(qvq_ctx *ctx, uint32_t K, int slot, bool sums_out, const double *hC, uint64_t wait_seq) {
     const bool fused = sums_out && use_fused(ctx, K);
     ctx->kd_pend = false;
+    ctx->sums_copies = 1;
+    // one rank, sums from a separate pass: that pass (and its reduce) runs before the tree is
+    // built -- it overlaps the host build instead of waiting behind it -- and the ties' moves are
+    // then applied to the finished sums (move_row_sums)
+    const bool early_upd = sums_out && !fused && kd_merge(ctx);
+    uint64_t *sums1 = early_upd ? ctx->d_sums : nullptr;
     uint64_t *xslab = fused ? ctx->d_part + (uint64_t)ctx->G * K * ctx->D : nullptr;
     uint32_t *xcnt = fused ? ctx->d_part_cnt + (uint64_t)ctx->G * K : nullptr;
     ctx->nslabs = fused ? ctx->G + 2 : ctx->G;
@@ -733,8 +741,14 @@ qvq_status run_level(qvq_ctx *ctx, uint32_t K, int slot, bool sums_out, const do
                               ctx->d_C64_split, ctx->d_C32, K, ctx->d_lut64, alpha, beta, gamma, 1e-12, ctx->d_A,
                               ctx->d_ties, &cnt[1], xslab, xcnt, ctx->d_plut));
     }
-    // the tree build overlaps the search just enqueued
     qvq_status st;
+    if (early_upd) {
+        HIPCHK(hipEventRecord(ctx->ev[slot][2], ctx->stream));
+        if ((st = run_update(ctx, ctx->d_A, K)) != QVQ_OK) return st;
+        ctx->nslabs = 0;   // reduced already
+        HIPCHK(hipEventRecord(ctx->ev[slot][3], ctx->stream));
+    }
+    // the tree build overlaps the search just enqueued
     const auto tw0 = std::chrono::steady_clock::now();
     if (wait_seq && (st = wait_codebook(ctx, wait_seq)) != QVQ_OK) return st;
     const auto tw1 = std::chrono::steady_clock::now();
@@ -746,17 +760,18 @@ qvq_status run_level(qvq_ctx *ctx, uint32_t K, int slot, bool sums_out, const do
     } else if (kd.depth > 0 && fused && kd_merge(ctx) && kd_reduce_fits(kd, K)) {
         ctx->kd_pend = true;   // with the reduce (qvq_lbg)
         ctx->pend_kd = kd;
+        ctx->sums_copies = 2;
     } else if (kd.depth > 0) {
         HIPCHK(launch_kd_resolve(ctx->stream, ctx->d_codes, ctx->Dp, ctx->D, ctx->d_ties, &cnt[1], ctx->d_C64_split,
-                                 K, ctx->d_lut64, kd, ctx->d_A, xslab, xcnt, ctx->d_plut));
+                                 K, ctx->d_lut64, kd, ctx->d_A, xslab, xcnt, ctx->d_plut, sums1));
     } else {   // ties answered on the host
         unsigned nt = 0;
         HIPCHK(hipMemcpyAsync(&nt, &cnt[1], sizeof(nt), hipMemcpyDeviceToHost, ctx->stream));
         HIPCHK(hipStreamSynchronize(ctx->stream));
-        if (nt && (st = resolve_host_ties(ctx, hC, K, nt, fused)) != QVQ_OK) return st;
+        if (nt && (st = resolve_host_ties(ctx, hC, K, nt, fused, sums1)) != QVQ_OK) return st;
     }
     ctx->upd[slot] = sums_out && !fused;
-    if (ctx->upd[slot]) {
+    if (ctx->upd[slot] && !early_upd) {
         HIPCHK(hipEventRecord(ctx->ev[slot][2], ctx->stream));
         if ((st = run_update_slabs(ctx, ctx->d_A, K)) != QVQ_OK) return st;
         HIPCHK(hipEventRecord(ctx->ev[slot][3], ctx->stream));
@@ -1196,7 +1211,8 @@ QVQ_API qvq_status qvq_lbg(qvq_ctx *ctx, uint32_t bits, double eps, double *code
         if ((st = run_level(ctx, K, slot, true, ctx->h_cb, ctx->seq)) != QVQ_OK) return st;
         const bool split = lvl < bits;
         {
-            uint32_t copies = 1;
+            const uint32_t copies = ctx->sums_copies;
+            if (copies > 1) ctx->sums1_dirty = true;
             const unsigned *tcnt = ctx->d_counters + 2 * ((int)lvl - 1) + 1;   // the level's ties
             if (ctx->kd_pend) {   // the level's ties and the reduce together
                 HIPCHK(launch_kd_reduce(ctx->stream, ctx->d_codes, ctx->Dp, ctx->D, ctx->d_ties, tcnt,
@@ -1204,8 +1220,6 @@ QVQ_API qvq_status qvq_lbg(qvq_ctx *ctx, uint32_t bits, double eps, double *code
                                         ctx->d_part, ctx->d_part_cnt, ctx->nslabs, ctx->nsub, ctx->d_sums,
                                         ctx->d_sums + sums_cap_stride(ctx)));
                 ctx->kd_pend = false;
-                ctx->sums1_dirty = true;
-                copies = 2;
             } else if (!(abl_skip() & 4) && ctx->nslabs) {   // nslabs 0: the sorted sums are in d_sums already
                 HIPCHK(launch_reduce(ctx->stream, ctx->d_part, ctx->d_part_cnt, ctx->nslabs, ctx->nsub, K, ctx->D,
                                      ctx->d_sums));

@@ -1209,7 +1209,8 @@ __global__ __launch_bounds__(KDR_MAX_WAVES * 64) void kd_resolve_kernel(KdArgs a
 
 hipError_t launch_kd_resolve(hipStream_t s, const uint8_t *codes, uint32_t Dp, uint32_t D, const uint32_t *ties,
                              const unsigned *tie_cnt, const double *C64, uint32_t K, const double *lut64,
-                             const KdView &kd, uint32_t *A, uint64_t *xslab, uint32_t *xcnt, const uint64_t *plut) {
+                             const KdView &kd, uint32_t *A, uint64_t *xslab, uint32_t *xcnt, const uint64_t *plut,
+                             uint64_t *xsums) {
     int W = kd.depth > 0 ? kd_waves(kd, K) : 0;
     if (W == 0) return hipErrorInvalidValue;
     // big K * D (C3 level 10, C4 from K = 256): a block per tie, its 16 waves on the point
@@ -1218,7 +1219,7 @@ hipError_t launch_kd_resolve(hipStream_t s, const uint8_t *codes, uint32_t Dp, u
     const bool whole = whole_ok && (size_t)K * D >= 8192;
     if (whole) W = 1;
     const size_t lds = kd_tree_bytes(kd) + (size_t)W * kd_wave_bytes(kd, K);
-    const KdArgs a{codes, Dp, D, ties, C64, K, lut64, kd, A, xslab, xcnt, plut};
+    const KdArgs a{codes, Dp, D, ties, C64, K, lut64, kd, A, xslab, xcnt, plut, xsums};
     static const int blocks = std::getenv("QVQ_KDR_BLOCKS") ? std::max(1, std::atoi(std::getenv("QVQ_KDR_BLOCKS")))
                                                              : KDR_BLOCKS;   // ablation
     hipLaunchKernelGGL(kd_resolve_kernel, dim3(blocks), dim3(whole ? 64 * KDR_MAX_WAVES : 64 * W), lds, s, a, tie_cnt,

@@ -1360,23 +1360,24 @@ hipError_t launch_gather_codes(hipStream_t s, const uint8_t *codes, uint32_t Dp,
 __global__ void fix_rows_kernel(const uint8_t *__restrict__ codes, uint32_t Dp, uint32_t D, uint32_t *__restrict__ A,
                                 const uint32_t *__restrict__ rows, const uint32_t *__restrict__ vals, uint32_t n,
                                 uint32_t K, uint64_t *__restrict__ xslab, uint32_t *__restrict__ xcnt,
-                                const uint64_t *__restrict__ plut) {
+                                const uint64_t *__restrict__ plut, uint64_t *__restrict__ xsums) {
     const uint32_t lane = threadIdx.x & 63;
     for (uint32_t i = (blockIdx.x * blockDim.x + threadIdx.x) / 64; i < n; i += gridDim.x * blockDim.x / 64) {
         const uint32_t row = rows[i], to = vals[i];
         const uint32_t from = A[row];
         if (from != to && xslab) move_row_terms(codes, Dp, D, row, from, to, K, xslab, xcnt, plut, lane);
+        else if (from != to && xsums) move_row_sums(codes, Dp, D, row, from, to, K, xsums, plut, lane);
         if (lane == 0) A[row] = to;
     }
 }
 
 hipError_t launch_fix_rows(hipStream_t s, const uint8_t *codes, uint32_t Dp, uint32_t D, uint32_t *A,
                            const uint32_t *rows, const uint32_t *vals, uint32_t n, uint32_t K, uint64_t *xslab,
-                           uint32_t *xcnt, const uint64_t *plut) {
+                           uint32_t *xcnt, const uint64_t *plut, uint64_t *xsums) {
     if (n == 0) return hipSuccess;
     const int blocks = (int)std::min<uint32_t>((n + 3) / 4, 1024);
     hipLaunchKernelGGL(fix_rows_kernel, dim3(blocks), dim3(256), 0, s, codes, Dp, D, A, rows, vals, n, K, xslab, xcnt,
-                       plut);
+                       plut, xsums);
     return hipGetLastError();
 }
 

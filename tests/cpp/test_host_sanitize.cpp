@@ -36,7 +36,7 @@ static int failures = 0;
 static void test_kdtree() {
     std::mt19937_64 rng(7);
     for (int D : {1, 3, 12, 48}) {
-        for (size_t K : {1, 2, 5, 11, 64, 300, 1024}) {
+        for (size_t K : {1, 2, 5, 11, 64, 300, 1024, 4096}) {   // (>= 1024: the forked build)
             std::vector<double> C(K * D), Q;
             std::uniform_int_distribution<int> q8(0, 7);
             for (size_t i = 0; i < K; i++)
