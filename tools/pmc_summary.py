@@ -21,17 +21,19 @@ def short(name):
         sk = m3.group(1) or m3.group(3)
         fused = m3.group(2) == "1" or m3.group(4) == "true"
         return "assign_small_kernel<%s,%s>" % (sk, "fused" if fused else "plain")
-    m4 = re.search(r"assign_mf32_kernelILb([01])ELb([01])ELi(\d+)ELb([01])E", name)
+    m4 = re.search(r"assign_mf32_kernelILb([01])ELb([01])ELi(\d+)ELb([01])ELb([01])E", name)
     if m4:
-        return "assign_mf32_kernel<%s,%s,U%s%s>" % ("fused" if m4.group(1) == "1" else "plain",
-                                                   "staged" if m4.group(2) == "1" else "global", m4.group(3),
-                                                   ",tag" if m4.group(4) == "1" else "")
+        return "assign_mf32_kernel<%s,%s,U%s%s%s>" % ("fused" if m4.group(1) == "1" else "plain",
+                                                     "staged" if m4.group(2) == "1" else "global", m4.group(3),
+                                                     ",tag" if m4.group(4) == "1" else "",
+                                                     ",prune" if m4.group(5) == "1" else "")
     m2 = re.search(r"assign_mfma_kernelILb([01])ELb([01])E", name)
     if m2:
         return "assign_mfma_kernel<%s,%s>" % ("fused" if m2.group(1) == "1" else "plain",
                                               "staged" if m2.group(2) == "1" else "global")
     for key in ["mean_sums_kernel", "finalize_prep_kernel", "recheck_mf32_kernel", "recheck_kernel",
-                "decode_rows_h_kernel", "decode_rows_kernel", "decode_pixels_kernel", "kd_resolve_kernel", "reduce_kernel",
+                "decode_rows_h_kernel", "decode_rows_kernel", "decode_pixels_kernel", "kd_resolve_kernel", "kd_reduce_kernel",
+                "reduce_kernel",
                 "update_kernel", "assign_valu_kernel", "tile_kernel", "gen_kernel", "byte_hist_kernel",
                 "prep_kernel", "copyBuffer", "fillBuffer"]:
         if key in name:
