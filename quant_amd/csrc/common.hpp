@@ -228,13 +228,21 @@ hipError_t launch_assign_mf32(hipStream_t s, int grid, bool fuse, const uint8_t 
                               const MfThresholds &th, uint32_t *A, uint32_t *flags, unsigned *flag_cnt,
                               uint64_t *part, uint32_t *part_cnt, const uint32_t *perm = nullptr,
                               const int32_t *tint = nullptr);
-constexpr uint32_t PRUNE_MAXK_HOST = 1024;   // prune_order's capacity (k_misc.hip PRUNE_MAXK)
+constexpr uint32_t PRUNE_MAXK_HOST = 4096;   // prune_order's capacity (k_misc.hip PRUNE_MAXK)
+// d_tint: the envelopes (2 int32 per tile, PRUNE_MAXK_HOST / 32 tiles), then Kpad floats of
+// projections (finalize -> prune_order)
+inline size_t tint_bytes(uint32_t Kp) { return (size_t)2 * (PRUNE_MAXK_HOST / 32) * 4 + (size_t)Kp * 4; }
 // MFMA f16 search for D != 12 (wide layout), no fused sums: K >= 32, codebook staged in LDS
 // whole or in double-buffered slices.  Same flag rule as launch_assign_mfma.
+// perm / tint (prune_order): the pruned variant for streamed codebooks (wide_prune_fits); cpr:
+// 64-row chunks per image column of blocks (the workgroup's chunks stack across it; 1 = none).
 bool wide_can_search(uint32_t Dp);
+bool wide_prune_fits(uint32_t Dp, uint32_t K);
 hipError_t launch_assign_wide(hipStream_t s, int num_cu, uint32_t Dp, uint32_t D, const uint8_t *codes, uint64_t N,
                               const _Float16 *cb_rows, uint32_t K, const float *C32, const MfThresholds &th,
-                              uint32_t *A, uint32_t *flags, unsigned *flag_cnt);
+                              uint32_t *A, uint32_t *flags, unsigned *flag_cnt, const uint32_t *perm = nullptr,
+                              const int32_t *tint = nullptr, uint32_t cpr = 1, unsigned *sched = nullptr);
+// (sched: two zeroed u32 the pruned variant's task counter uses and leaves zeroed)
 // Recheck of flagged rows: fp32 distances to all K code vectors (C32 [Kpad][Dp]), fp64 in
 // the reference's order for those inside the fp32 error band (alpha, beta, gamma as the VALU
 // search's); exact ties are listed in ties (tie_cnt) for launch_kd_resolve or the host.

@@ -71,6 +71,8 @@ bool make_terms(int cs, Terms &t) {
 
 using namespace qvq;
 
+constexpr uint32_t SCHED_COUNTERS = 2 * 33 + 2, N_COUNTERS = SCHED_COUNTERS + 2;
+
 struct qvq_ctx {
     int dev = 0;
     int num_cu = 256;
@@ -98,7 +100,8 @@ struct qvq_ctx {
     double *d_lut64 = nullptr;
     uint64_t *d_plut = nullptr;
     uint32_t *d_A = nullptr, *d_flags = nullptr, *d_ties = nullptr;
-    unsigned *d_counters = nullptr;   // per level: [2l] flagged rows, [2l+1] kd-tree ties; [66], [67] block counters
+    unsigned *d_counters = nullptr;   // per level: [2l] flagged rows, [2l+1] kd-tree ties; [66], [67] block counters;
+                                      // [68], [69] the pruned wide search's task counters (SCHED_COUNTERS)
     uint64_t *d_hist = nullptr;       // byte histogram [256] | its all-reduced copy [256]
 
     // level buffers
@@ -135,6 +138,7 @@ struct qvq_ctx {
     std::vector<double> cb_local;   // host copy of the published codebook for the tree build
     uint64_t tree_cap = 0;
     uint32_t nslabs = 0;   // slabs holding the last run_level's sums
+    uint32_t col_blocks = 0;   // blocks per image column (consecutive rows run down a column); 0: no image
     bool kd_pend = false;      // run_level left its kd-tree ties to kd_reduce_kernel (pend_kd)
     uint32_t sums_copies = 1;  // 2: run_level's tie moves are in copy 1 of d_sums (the finalize adds it)
     KdView pend_kd{};
@@ -234,10 +238,16 @@ bool use_fused(const qvq_ctx *ctx, uint32_t K) {
 // Pruned MFMA search (k_mf32.hip PRUNE: tiles visited outward from a chunk's projection,
 // stopped by a provable bound) for D = 12 from K = QVQ_PRUNE_MINK (default 512; 0 = off) up to
 // prune_order's capacity.  Its order is computed by the previous level's finalize.
+// Other D (assign_wide_kernel, streamed codebooks): from K = QVQ_WPRUNE_MINK (default 1024).
+// The D = 12 kernel keeps one tile envelope per lane: at most 64 tiles (K <= 2048).
 bool use_prune(const qvq_ctx *ctx, uint32_t K) {
     static const uint32_t mink = std::getenv("QVQ_PRUNE_MINK") ? (uint32_t)std::atoi(std::getenv("QVQ_PRUNE_MINK")) : 512u;
-    return mink && K >= mink && K <= PRUNE_MAXK_HOST && ctx->D == MF_D && use_mfma(ctx, K) &&
-           mf32_prune_fits(K, use_fused(ctx, K));
+    static const uint32_t wmink =
+        std::getenv("QVQ_WPRUNE_MINK") ? (uint32_t)std::atoi(std::getenv("QVQ_WPRUNE_MINK")) : 1024u;
+    if (K > PRUNE_MAXK_HOST) return false;
+    if (ctx->D == MF_D)
+        return mink && K >= mink && K <= 2048 && use_mfma(ctx, K) && mf32_prune_fits(K, use_fused(ctx, K));
+    return wmink && K >= wmink && use_wide(ctx, K) && wide_prune_fits(ctx->Dp, K);
 }
 
 void free_training(qvq_ctx *ctx) {
@@ -392,7 +402,7 @@ qvq_status ensure_levels(qvq_ctx *ctx, uint32_t Kmax) {
     if (ctx->D == MF_D) HIPCHK(hipMalloc(&ctx->d_E32, Kp * 16 * 4));
     HIPCHK(hipMalloc(&ctx->d_rows, Kp * 2 * cb_row_f16(ctx->D, ctx->Dp)));
     HIPCHK(hipMalloc(&ctx->d_perm, Kp * 4));
-    HIPCHK(hipMalloc(&ctx->d_tint, (Kp / 32 + 1) * 8));
+    HIPCHK(hipMalloc(&ctx->d_tint, tint_bytes((uint32_t)Kp)));
     // G per-CU slabs + two correction slabs (fused path: rows the recheck / kd-tree move, at
     // the new index (+) and at the search's provisional one (-))
     HIPCHK(hipMalloc(&ctx->d_part, (uint64_t)(ctx->G + 2) * KD * 8));
@@ -713,8 +723,11 @@ qvq_status run_level(qvq_ctx *ctx, uint32_t K, int slot, bool sums_out, const do
                                   ctx->d_part, ctx->d_part_cnt, prune ? ctx->d_perm : nullptr,
                                   prune ? ctx->d_tint : nullptr));
     } else if (use_wide(ctx, K)) {
+        const bool prune = ctx->perm_k == K;
         HIPCHK(launch_assign_wide(ctx->stream, ctx->num_cu, ctx->Dp, ctx->D, ctx->d_codes, ctx->N, ctx->d_rows, K,
-                                  ctx->d_C32, ctx->mf_th, ctx->d_A, ctx->d_flags, &cnt[0]));
+                                  ctx->d_C32, ctx->mf_th, ctx->d_A, ctx->d_flags, &cnt[0],
+                                  prune ? ctx->d_perm : nullptr, prune ? ctx->d_tint : nullptr,
+                                  std::max<uint32_t>(1, (ctx->col_blocks + 32) / 64), ctx->d_counters + SCHED_COUNTERS));
     } else {
         float alpha, beta, gamma;
         valu_coeffs(ctx, alpha, beta, gamma);
@@ -799,6 +812,7 @@ qvq_status check_image_args(qvq_ctx *ctx, uint32_t n_images, uint32_t xSize, uin
 
 qvq_status tile_into(qvq_ctx *ctx, const uint8_t *d_rgb, uint32_t n_images, uint32_t xSize, uint32_t ySize,
                      uint32_t bw, uint32_t bh) {
+    ctx->col_blocks = (ySize + bh - 1) / bh;   // the pruned wide search stacks its chunks across columns
     HIPCHK(launch_tile(ctx->stream, d_rgb, ctx->d_codes, n_images, xSize, ySize, bw, bh, ctx->D, ctx->Dp,
                        ctx->terms.pad_code));
     return QVQ_OK;
@@ -848,7 +862,8 @@ QVQ_API qvq_status qvq_create(int hip_device, qvq_ctx **out) {
     *ctx->h_ready = 0;
     if ((e = hipHostGetDevicePointer((void **)&ctx->dh_ready, ctx->h_ready, 0)) != hipSuccess)
         return bail(e, "hipHostGetDevicePointer");
-    if ((e = hipMalloc(&ctx->d_counters, (2 * 33 + 2) * sizeof(unsigned))) != hipSuccess) return bail(e, "hipMalloc");
+    if ((e = hipMalloc(&ctx->d_counters, N_COUNTERS * sizeof(unsigned))) != hipSuccess) return bail(e, "hipMalloc");
+    if ((e = hipMemset(ctx->d_counters, 0, N_COUNTERS * sizeof(unsigned))) != hipSuccess) return bail(e, "hipMemset");
     if ((e = hipMalloc(&ctx->d_hist, 512 * 8)) != hipSuccess) return bail(e, "hipMalloc");
     if ((e = hipMalloc(&ctx->d_decode_stat, 16)) != hipSuccess) return bail(e, "hipMalloc");
     if ((e = hipHostMalloc(&ctx->h_decode_stat, 16, hipHostMallocDefault)) != hipSuccess) return bail(e, "hipHostMalloc");
@@ -969,6 +984,7 @@ QVQ_API qvq_status qvq_set_vectors(qvq_ctx *ctx, const double *X, uint64_t n, ui
     GUARD(ctx);
     if (!X || n == 0 || dim == 0) return fail(ctx, QVQ_EINVAL, "empty training set");
     if (dim > 64) return fail(ctx, QVQ_EINVAL, "block dimension above 64 (3*w*h) is not supported");
+    ctx->col_blocks = 0;   // rows without image geometry
     // Recognise the colour space from the values: every value must be a byte's image
     // under NORMAL or SCALED (0.0 included), so the exact sums apply.
     int cs_found = -1;
@@ -1173,7 +1189,7 @@ QVQ_API qvq_status qvq_lbg(qvq_ctx *ctx, uint32_t bits, double eps, double *code
         hist = ctx->d_hist + 256;
     }
     HIPCHK(launch_mean_sums(ctx->stream, ctx->Dp, ctx->d_codes, ctx->N, ctx->D, ctx->d_plut, ctx->d_mean,
-                            ctx->d_counters, 2 * 33 + 2, d_dist, hist, ctx->d_lut64));
+                            ctx->d_counters, N_COUNTERS, d_dist, hist, ctx->d_lut64));
     if ((st = all_reduce_sums(ctx, 1, ctx->d_mean, MEAN_COPIES)) != QVQ_OK) {
         (void)hipMemsetAsync(ctx->d_mean, 0, MEAN_COPIES * (2 * 64 + 1) * 8, ctx->stream);   // keep it clear for the next call
         return st;

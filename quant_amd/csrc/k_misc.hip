@@ -967,8 +967,9 @@ struct FinArgs {
     uint64_t cstride;       // u64 from one copy to the next (2KD + K, or the capacity's)
     const unsigned *gate;   // non-null: copies past the first only when *gate != 0 (the level's
                             // tie count: without ties copy 1 is all zero, read nor cleared)
-    uint32_t *perm;         // split, D = 12: the next search's tile order (prune_order), or null
+    uint32_t *perm;         // split: the next search's tile order (prune_order), or null
     int32_t *tint;
+    float *qproj;           // with perm: the split code vectors' projections (finalize_split_item)
 };
 
 // A split row j (< 2K: child of code vector j mod K, from that code vector's sums hs, ls, cnt of
@@ -991,6 +992,12 @@ __device__ inline void finalize_split_item(const FinArgs &a, uint32_t j, uint32_
             const uint32_t RF = cb_row_f16(D, Dp), LO = cb_lo_off(D, Dp);
             _Float16 *row = a.rows + (uint64_t)j * RF;
             const double cp = d < D ? v - a.mu : 0.0;
+            if (a.qproj) {   // the projection sum_d (c_d - mu) / sx for prune_order (any order: it
+                             // is widened by 1 there)
+                double qs = cp;
+                for (uint32_t off = L / 2; off >= 1; off >>= 1) qs += __shfl_xor(qs, (int)off, (int)L);
+                if (d == 0) a.qproj[j] = (float)(qs / a.sx);
+            }
             double n = cp * cp;   // L >= LO lanes per row
             for (uint32_t off = L / 2; off >= 1; off >>= 1) n += __shfl_xor(n, (int)off, (int)L);
             if (d < D) {
@@ -1056,39 +1063,30 @@ __device__ inline double finalize_item(const FinArgs &a, uint32_t j, uint32_t d,
     return 0.0;
 }
 
-// The next D = 12 search's code-vector order for tile pruning (assign_mf32_kernel, PRUNE): the
-// K2 split code vectors bucket-sorted by their projection q = sum_d (c_d - mu) / sx on the
-// all-ones direction (in the units of a row's sum_d w_d, w the centred byte integers), so that
+// The next search's code-vector order for tile pruning (assign_mf32_kernel / assign_wide_kernel
+// PRUNE): the K2 split code vectors bucket-sorted by their projection q = sum_d (c_d - mu) / sx on
+// the all-ones direction (in the units of a row's sum_d w_d, w the centred byte integers), so that
 // each 32-code-vector tile spans a short q interval.  perm[p] = the code vector at position p
-// (padding positions K2 .. Kpad map to themselves); tint[2t], tint[2t + 1] = the floor / ceil
-// of tile t's q interval widened by 1 (empty tile: INT_MAX, INT_MIN).  Any grouping keeps the
-// search exact (the bound holds for every tile); the sort only makes it prune.  Run by the
-// finalize's last block (256 threads), K2 <= PRUNE_MAXK.
-constexpr uint32_t PRUNE_MAXK = 1024, PRUNE_NB = 256;
-__device__ void prune_order(const double *__restrict__ C64n, uint32_t K2, uint32_t Kpad, double mu, double sx,
-                            uint32_t *__restrict__ perm, int32_t *__restrict__ tint) {
-    // (any block size >= 256: threads past 256 only meet the barriers)
+// (padding positions K2 .. Kpad map to themselves); tint[2t], tint[2t + 1] = tile t's envelope:
+// the floor / ceil of its q interval widened by 1 (empty tile: INT_MAX, INT_MIN), then the suffix
+// minimum of the lows and the prefix maximum of the highs.  Any grouping keeps the search exact
+// (the bound holds for every tile); the sort only makes it prune.  Run by the finalize's last
+// block (any size >= 256: threads past 256 only meet the barriers), K2 <= PRUNE_MAXK.
+constexpr uint32_t PRUNE_MAXK = 4096, PRUNE_NB = 256, PRUNE_MAXT = PRUNE_MAXK / 32;
+__device__ void prune_order(const float *__restrict__ qproj, uint32_t K2, uint32_t Kpad, uint32_t *__restrict__ perm,
+                            int32_t *__restrict__ tint) {
     __shared__ float q[PRUNE_MAXK];
     __shared__ float qs[PRUNE_MAXK];   // q by position
     __shared__ uint32_t hist[PRUNE_NB];
     __shared__ float qr[2][256];
+    __shared__ int32_t tlo[PRUNE_MAXT], thi[PRUNE_MAXT];
     const uint32_t tid = threadIdx.x;
     const bool act = tid < 256;
     float mn = INFINITY, mx = -INFINITY;
-#pragma unroll
-    for (uint32_t i = 0; i < PRUNE_MAXK / 256; i++) {   // (all loads of a thread in flight)
-        const uint32_t j = tid + 256 * i;
-        if (act && j < K2) {
-            double c[MF_D];
-#pragma unroll
-            for (uint32_t d = 0; d < MF_D; d++) c[d] = C64n[(uint64_t)j * MF_D + d];
-            double sum = 0;
-#pragma unroll
-            for (uint32_t d = 0; d < MF_D; d++) sum += c[d] - mu;
-            q[j] = (float)(sum / sx);
-            mn = fminf(mn, q[j]);
-            mx = fmaxf(mx, q[j]);
-        }
+    for (uint32_t j = tid; act && j < K2; j += 256) {   // (the finalize items wrote them)
+        q[j] = __builtin_nontemporal_load(&qproj[j]);
+        mn = fminf(mn, q[j]);
+        mx = fmaxf(mx, q[j]);
     }
     if (act) {
         hist[tid] = 0;
@@ -1132,45 +1130,37 @@ __device__ void prune_order(const double *__restrict__ C64n, uint32_t K2, uint32
         for (uint32_t p = K2 + tid; p < Kpad; p += 256) perm[p] = p;
     }
     __syncthreads();
-    // tile t = positions 32t .. 32t + 31: four per thread, then over 8 lanes
-    __shared__ int32_t tlo[PRUNE_MAXK / 32], thi[PRUNE_MAXK / 32];
+    // tile t = positions 32t .. 32t + 31: thread t < nt scans its tile
     const uint32_t nt = Kpad / 32;
-    if (act) {
+    if (act && tid < nt) {
         float lo = INFINITY, hi = -INFINITY;
-#pragma unroll
-        for (uint32_t i = 0; i < 4; i++) {
-            const uint32_t p = 4 * tid + i;
-            if (p < K2) {
-                lo = fminf(lo, qs[p]);
-                hi = fmaxf(hi, qs[p]);
-            }
+        for (uint32_t p = 32 * tid; p < min(32 * tid + 32, K2); p++) {
+            lo = fminf(lo, qs[p]);
+            hi = fmaxf(hi, qs[p]);
         }
-#pragma unroll
-        for (int m = 1; m < 8; m <<= 1) {
-            lo = fminf(lo, __shfl_xor(lo, m));
-            hi = fmaxf(hi, __shfl_xor(hi, m));
+        tlo[tid] = lo <= hi ? (int32_t)floorf(lo) - 1 : 0x7FFFFFFF;
+        thi[tid] = lo <= hi ? (int32_t)ceilf(hi) + 1 : (int32_t)0x80000000;
+    }
+    // Tiles sharing a bucket can overlap out of order: monotone envelopes (lo: the suffix
+    // minimum, hi: the prefix maximum; still bounds of every tile), so that the tiles a bound
+    // admits form one contiguous range.  Hillis-Steele over nt <= 128 entries.
+    for (uint32_t off = 1; off < nt; off <<= 1) {
+        __syncthreads();
+        int32_t m = 0, M = 0;
+        if (act && tid < nt) {
+            m = tid + off < nt ? min(tlo[tid], tlo[tid + off]) : tlo[tid];
+            M = tid >= off ? max(thi[tid], thi[tid - off]) : thi[tid];
         }
-        if ((tid & 7) == 0 && tid / 8 < nt) {
-            tlo[tid / 8] = lo <= hi ? (int32_t)floorf(lo) - 1 : 0x7FFFFFFF;
-            thi[tid / 8] = lo <= hi ? (int32_t)ceilf(hi) + 1 : (int32_t)0x80000000;
+        __syncthreads();
+        if (act && tid < nt) {
+            tlo[tid] = m;
+            thi[tid] = M;
         }
     }
     __syncthreads();
-    // Tiles sharing a bucket can overlap out of order: store monotone envelopes (lo: the suffix
-    // minimum, hi: the prefix maximum; still bounds of every tile), so that a scan leaving tile t
-    // may skip every tile beyond it on that side.  One wave, lane t = tile t (nt <= 32).
-    if (tid < 64) {
-        int32_t m = tid < nt ? tlo[tid] : 0x7FFFFFFF, M = tid < nt ? thi[tid] : (int32_t)0x80000000;
-#pragma unroll
-        for (int o = 1; o < 32; o <<= 1) {
-            const int32_t dn = __shfl_down(m, o), up = __shfl_up(M, o);
-            if ((int)tid + o < 64) m = min(m, dn);
-            if ((int)tid >= o) M = max(M, up);
-        }
-        if (tid < nt) {
-            tint[2 * tid] = m;
-            tint[2 * tid + 1] = M;
-        }
+    if (act && tid < nt) {
+        tint[2 * tid] = tlo[tid];
+        tint[2 * tid + 1] = thi[tid];
     }
 }
 
@@ -1218,7 +1208,7 @@ __device__ void finalize_block_done(const FinArgs &a, double term, double *red, 
     }
     if (!a.gate || *a.gate)
         for (uint32_t i = threadIdx.x; i < a.n_zero; i += blockDim.x) a.zero_after[i] = 0;
-    if (a.perm) prune_order(a.C64n, 2 * a.K, a.Kpad_next, a.mu, a.sx, a.perm, a.tint);
+    if (a.perm) prune_order(a.qproj, 2 * a.K, a.Kpad_next, a.perm, a.tint);
     if (threadIdx.x == 0) {
         *done = 0;
         if (ready) {
@@ -1272,6 +1262,7 @@ static FinArgs fin_args(const uint64_t *sums, uint32_t K, uint32_t D, uint32_t D
     a.gate = nullptr;
     a.perm = nullptr;
     a.tint = nullptr;
+    a.qproj = nullptr;
     return a;
 }
 
@@ -1295,9 +1286,10 @@ hipError_t launch_finalize_prep(hipStream_t s, const uint64_t *sums, uint32_t K,
         a.cstride = copy_stride;
     }
     if (perm) {   // the last block orders the next search's code vectors (needs the done counter)
-        if (!done || !split || D != MF_D || 2 * K > PRUNE_MAXK || Kpad_next % 32) return hipErrorInvalidValue;
+        if (!done || !split || 2 * K > PRUNE_MAXK || Kpad_next % 32 || Kpad_next > PRUNE_MAXK) return hipErrorInvalidValue;
         a.perm = perm;
         a.tint = tint;
+        a.qproj = reinterpret_cast<float *>(tint + 2 * PRUNE_MAXT);   // (the envelopes' region is fixed)
     }
     if (zero_sums) {   // copies zero_skip .. ncopy - 1
         if (zero_skip >= a.ncopy) return hipErrorInvalidValue;

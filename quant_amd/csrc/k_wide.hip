@@ -44,11 +44,25 @@ __host__ __device__ inline bool wide_resident(uint32_t K) {
     return (uint64_t)((K + 31) & ~31u) * WideCfg<DP>::LSTR <= WD_LDS_MAX;
 }
 
-template <int DP>
+// PRUNE (streamed codebooks; code vectors in the order of perm with tile envelopes tint,
+// finalize's prune_order): the workgroup's 8 waves take 8 chunks stacked across image rows
+// (chunk stride cpr, the chunks per image column of blocks) so that their rows are one compact
+// image region; the workgroup searches the slice holding the tile nearest its rows' projection
+// first, takes one distance bound from it (every row's best so far, max over the workgroup) and
+// then streams only the slices whose tiles the projection bound cannot exclude (DESIGN.md
+// 3.1.1: ||x - c||^2 >= sx^2 (sum w - q_c)^2 / D).
+__host__ __device__ inline uint64_t wide_chunk(uint64_t task, uint32_t wave, uint64_t ntask, uint32_t cpr) {
+    const uint64_t full = ntask / cpr * cpr;   // tasks in whole groups of cpr
+    if (task < full) return task / cpr * cpr * WD_WAVES + task % cpr + (uint64_t)wave * cpr;
+    return task * WD_WAVES + wave;
+}
+
+template <int DP, bool PRUNE>
 __global__ __launch_bounds__(WD_THREADS) void assign_wide_kernel(
     const uint8_t *__restrict__ codes, uint64_t N, uint32_t D, const _Float16 *__restrict__ g_rows, uint32_t K,
     const float *__restrict__ g_C32, MfThresholds th, uint32_t *__restrict__ A, uint32_t *__restrict__ flags,
-    unsigned *__restrict__ flag_cnt) {
+    unsigned *__restrict__ flag_cnt, const uint32_t *__restrict__ g_perm, const int32_t *__restrict__ g_tint,
+    uint32_t cpr, unsigned *__restrict__ sched) {
     using C = WideCfg<DP>;
     constexpr int KS = C::KS, LSTR = C::LSTR, UPR = C::UPR, NH = C::DH / 8;
     constexpr bool TWO = KS >= 2;   // keep two units
@@ -61,13 +75,18 @@ __global__ __launch_bounds__(WD_THREADS) void assign_wide_kernel(
     const int g = lane >> 4, c = lane & 15;
     const unsigned char *gsrc = reinterpret_cast<const unsigned char *>(g_rows);
     unsigned char *buf0 = lds, *buf1 = lds + (resident ? 0 : WD_SLICE * LSTR);
+    // PRUNE: perm (u16 per position) and the tile envelopes after the two slice buffers
+    uint16_t *perm_l = reinterpret_cast<uint16_t *>(lds + 2 * WD_SLICE * LSTR);
+    int32_t *tint_l = reinterpret_cast<int32_t *>(lds + 2 * WD_SLICE * LSTR + ((2 * Kp + 15) & ~15u));
+    const uint32_t ntiles = Kp / 32;
 
     // slice s: code vectors s*WD_SLICE.. (KS 16-byte units per thread, staged in registers)
     uint4 stage[KS];
 #define WD_STAGE_LOAD(S)                                                                                         \
     _Pragma("unroll") for (int i = 0; i < KS; i++) {                                                            \
         const uint32_t u = tid + i * WD_THREADS, row = (S) * WD_SLICE + u / UPR, col = u % UPR;                  \
-        stage[i] = row < Kp ? *reinterpret_cast<const uint4 *>(gsrc + (size_t)row * C::GROW + col * 16)          \
+        const uint32_t src = PRUNE && row < Kp ? (uint32_t)perm_l[row] : row;                                    \
+        stage[i] = row < Kp ? *reinterpret_cast<const uint4 *>(gsrc + (size_t)src * C::GROW + col * 16)          \
                             : make_uint4(0, 0, 0, 0);                                                             \
     }
 #define WD_STAGE_STORE(S, BUF)                                                                                   \
@@ -75,7 +94,11 @@ __global__ __launch_bounds__(WD_THREADS) void assign_wide_kernel(
         const uint32_t u = tid + i * WD_THREADS, row = u / UPR, col = u % UPR;                                   \
         if ((S) * WD_SLICE + row < Kp) *reinterpret_cast<uint4 *>((BUF) + row * LSTR + col * 16) = stage[i];      \
     }
-    if (resident) {
+    if (PRUNE) {
+        for (uint32_t i = tid; i < Kp; i += WD_THREADS) perm_l[i] = (uint16_t)g_perm[i];
+        for (uint32_t i = tid; i < 2 * ntiles; i += WD_THREADS) tint_l[i] = g_tint[i];
+        __syncthreads();
+    } else if (resident) {
         for (uint32_t u = tid; u < Kp * UPR; u += WD_THREADS) {
             const uint32_t row = u / UPR, col = u % UPR;
             *reinterpret_cast<uint4 *>(buf0 + row * LSTR + col * 16) =
@@ -88,13 +111,29 @@ __global__ __launch_bounds__(WD_THREADS) void assign_wide_kernel(
     __syncthreads();
 
     const uint64_t nchunks = (N + WD_ROWS - 1) / WD_ROWS;
-    const uint64_t wg_stride = (uint64_t)gridDim.x * WD_WAVES;
+    const uint64_t ntask = (nchunks + WD_WAVES - 1) / WD_WAVES;
     const f32x4 zero = {0.f, 0.f, 0.f, 0.f};
     uint32_t it = 0;   // slices consumed (buffer parity)
-    for (uint64_t cb = (uint64_t)blockIdx.x * WD_WAVES; cb < nchunks; cb += wg_stride) {
-        const uint64_t chunk = cb + wave;
+    __shared__ int32_t red_i[2][WD_WAVES];
+    __shared__ float red_f[WD_WAVES];
+    __shared__ int32_t win_lo, win_hi;
+    // PRUNE: tasks from a counter (sched[0]; the windows differ per task, and a static split left
+    // the busiest workgroup ~1.5x the mean), the next one fetched while this one runs
+    __shared__ uint32_t sched_next;
+    uint64_t task = blockIdx.x;
+    if (PRUNE) {
+        if (tid == 0) sched_next = atomicAdd(&sched[0], 1u);
+        __syncthreads();
+        task = sched_next;
+    }
+    while (task < ntask) {
+        const uint64_t chunk = PRUNE ? wide_chunk(task, wave, ntask, cpr) : task * WD_WAVES + wave;
         const uint64_t base = chunk * WD_ROWS;
-        const bool more = cb + wg_stride < nchunks;   // uniform over the workgroup
+        const bool more = !PRUNE && task + gridDim.x < ntask;   // uniform over the workgroup
+        if (PRUNE) {
+            __syncthreads();   // (every thread has read sched_next)
+            if (tid == 0) sched_next = atomicAdd(&sched[0], 1u);
+        }
 
         // B fragments: lane (g, c) holds k-slots 32ks + 8g .. +7 of row c of each tile, i.e.
         // 8-slot group G = 4ks + g: hi components 8G.., lo components 8(G-NH).., the two ones
@@ -137,15 +176,9 @@ __global__ __launch_bounds__(WD_THREADS) void assign_wide_kernel(
             bp[t] = 0;
             bq[t] = 0;
         }
-        for (uint32_t s = 0; s < ns; s++) {
-            const unsigned char *cur = (it & 1) ? buf1 : buf0;
-            const bool pre = !resident && (s + 1 < ns || more);
-            const uint32_t snext = s + 1 < ns ? s + 1 : 0;
-            if (pre) {
-                WD_STAGE_LOAD(snext)
-            }
-            const uint32_t r0 = resident ? 0 : s * WD_SLICE;
-            const uint32_t np = min(SL, Kp - r0) / 32;
+        // one streamed or resident slice of code vectors (positions r0 .. r0 + np*32) against the
+        // wave's 64 rows
+        auto search_slice = [&](const unsigned char *cur, uint32_t r0, uint32_t np) {
             const unsigned char *abase = cur + c * LSTR + 16 * g;
 #pragma unroll 2
             for (uint32_t p = 0; p < np; p++) {
@@ -176,14 +209,131 @@ __global__ __launch_bounds__(WD_THREADS) void assign_wide_kernel(
                         pair_update(p0[t], p1[t], r0 / 32 + p, b1[t], b2[t], bp[t]);
                 }
             }
-            if (!resident) {
-                if (pre) {
-                    unsigned char *nb = (it & 1) ? buf0 : buf1;
-                    WD_STAGE_STORE(snext, nb)
+        };
+        if constexpr (PRUNE) {
+            // the rows' sum w (exact integers) and ||x - mu||^2: lane (g, c) takes row c of each tile
+            int32_t qmn = 0x7FFFFFFF, qmx = (int32_t)0x80000000;
+            float xn2[WD_TILES];
+            const float sx2 = th.sx * th.sx;
+#pragma unroll
+            for (int t = 0; t < WD_TILES; t++) {
+                const uint64_t row = base + t * 16 + c;
+                const bool valid = chunk < nchunks && row < N;
+                const uint32_t *rw = reinterpret_cast<const uint32_t *>(codes + (valid ? row : 0) * DP);
+                uint32_t su = 0, s2 = 0;
+#pragma unroll
+                for (int q = 0; q < DP / 4; q++) {
+                    uint32_t u = rw[q] ^ 0x80808080u;
+                    const int rem = (int)D - 4 * q;   // real components in this word
+                    u = rem >= 4 ? u : (rem <= 0 ? 0u : u & (0xFFFFFFFFu >> (8 * (4 - rem))));
+                    su = __builtin_amdgcn_sad_u8(u, 0u, su);
+                    s2 = __builtin_amdgcn_udot4(u, u, s2, false);
+                }
+                const int32_t qw = 2 * (int32_t)su - 255 * (int32_t)D;   // sum_d (2u - 255)
+                xn2[t] = valid ? (float)(4.0 * (double)s2 - 1020.0 * (double)su + 65025.0 * (double)D) * sx2 : 0.f;
+                qmn = valid ? min(qmn, qw) : qmn;
+                qmx = valid ? max(qmx, qw) : qmx;
+            }
+            qmn = (int32_t)(wave_min_u32((uint32_t)qmn ^ 0x80000000u) ^ 0x80000000u);
+            qmx = (int32_t)(~wave_min_u32(~((uint32_t)qmx ^ 0x80000000u)) ^ 0x80000000u);
+            if (lane == 0) {
+                red_i[0][wave] = qmn;
+                red_i[1][wave] = qmx;
+            }
+            __syncthreads();
+            int32_t Qmn = red_i[0][0], Qmx = red_i[1][0];
+#pragma unroll
+            for (int w = 1; w < WD_WAVES; w++) {
+                Qmn = min(Qmn, red_i[0][w]);
+                Qmx = max(Qmx, red_i[1][w]);
+            }
+            if (Qmn <= Qmx) {   // (uniform) the workgroup has rows
+                // the tile whose envelope reaches the rows' centre, and its slice first
+                const int32_t mid = (int32_t)(((int64_t)Qmn + Qmx) >> 1);
+                const uint32_t below = __syncthreads_count(tid < ntiles && tint_l[2 * tid + 1] < mid);
+                const uint32_t t0 = min(below, ntiles - 1), s0 = t0 * 32 / WD_SLICE;
+                auto stage_now = [&](uint32_t sl, unsigned char *dst) {
+                    WD_STAGE_LOAD(sl)
+                    WD_STAGE_STORE(sl, dst)
+                };
+                stage_now(s0, buf0);
+                __syncthreads();
+                search_slice(buf0, s0 * WD_SLICE, min(WD_SLICE, Kp - s0 * WD_SLICE) / 32);
+                // one bound: every row's best distance so far from above (its best MFMA score over
+                // the four lane groups, plus the score error), max over the workgroup
+                float ub = 0.f;
+#pragma unroll
+                for (int t = 0; t < WD_TILES; t++) {
+                    float v = __fmaf_rn(b1[t], th.inv_scale, xn2[t]) + th.mfma;
+                    v = fminf(v, xor16_f32(v));
+                    v = fminf(v, xor32_f32(v));
+                    const uint64_t row = base + t * 16 + c;
+                    ub = chunk < nchunks && row < N ? fmaxf(ub, v) : ub;
+                }
+                ub = __uint_as_float(~wave_min_u32(~__float_as_uint(fmaxf(ub, 0.f))));   // >= 0: bits order as values
+                if (tid == 0) {
+                    win_lo = 0x7FFFFFFF;
+                    win_hi = -1;
+                }
+                if (lane == 0) red_f[wave] = ub;
+                __syncthreads();
+                float B = red_f[0];
+#pragma unroll
+                for (int w = 1; w < WD_WAVES; w++) B = fmaxf(B, red_f[w]);
+                const float bw = B * ((float)D / sx2) * 1.00001f + 1.0f;
+                if (tid < ntiles) {   // the tiles' gaps grow away from the centre: one range
+                    const float gap = (float)max(0, max(tint_l[2 * tid] - Qmx, Qmn - tint_l[2 * tid + 1]));
+                    if (gap * gap <= bw) {
+                        atomicMin(&win_lo, (int32_t)tid);
+                        atomicMax(&win_hi, (int32_t)tid);
+                    }
                 }
                 __syncthreads();
-                it++;
+                const uint32_t slo = min(s0, (uint32_t)(win_lo == 0x7FFFFFFF ? t0 : win_lo) * 32 / WD_SLICE);
+                const uint32_t shi = max(s0, (uint32_t)(win_hi < 0 ? t0 : win_hi) * 32 / WD_SLICE);
+                // the window's other slices, the next one staged under each one's MFMAs
+                uint32_t sl = slo == s0 ? s0 + 1 : slo;
+                if (sl <= shi) {
+                    stage_now(sl, buf1);
+                    __syncthreads();
+                    uint32_t par = 1;
+                    for (;;) {
+                        const uint32_t nx = sl + 1 == s0 ? sl + 2 : sl + 1;
+                        const bool pre = nx <= shi;
+                        if (pre) {
+                            WD_STAGE_LOAD(nx)
+                        }
+                        search_slice(par ? buf1 : buf0, sl * WD_SLICE, min(WD_SLICE, Kp - sl * WD_SLICE) / 32);
+                        if (!pre) break;
+                        WD_STAGE_STORE(nx, par ? buf0 : buf1)
+                        __syncthreads();
+                        par ^= 1;
+                        sl = nx;
+                    }
+                }
+                __syncthreads();   // (the buffers are free for the next task)
             }
+        } else {
+            for (uint32_t s = 0; s < ns; s++) {
+                const unsigned char *cur = (it & 1) ? buf1 : buf0;
+                const bool pre = !resident && (s + 1 < ns || more);
+                const uint32_t snext = s + 1 < ns ? s + 1 : 0;
+                if (pre) {
+                    WD_STAGE_LOAD(snext)
+                }
+                const uint32_t r0 = resident ? 0 : s * WD_SLICE;
+                const uint32_t np = min(SL, Kp - r0) / 32;
+                search_slice(cur, r0, np);
+                if (!resident) {
+                    if (pre) {
+                        unsigned char *nb = (it & 1) ? buf0 : buf1;
+                        WD_STAGE_STORE(snext, nb)
+                    }
+                    __syncthreads();
+                    it++;
+                }
+            }
+
         }
 
         // Combine the four lanes of each data row.  One unit: the winning 8-code-vector unit
@@ -289,7 +439,8 @@ __global__ __launch_bounds__(WD_THREADS) void assign_wide_kernel(
 #pragma unroll 2
             for (int j = 0; j < (TWO ? 16 : 8); j++) {
                 const uint32_t un = j < 8 ? unit : unit2, jj = j & 7;
-                const uint32_t cv = (2 * (un >> 2) + (jj >> 2)) * 16 + 4 * (un & 3) + (jj & 3);
+                const uint32_t pos = (2 * (un >> 2) + (jj >> 2)) * 16 + 4 * (un & 3) + (jj & 3);
+                const uint32_t cv = PRUNE ? (uint32_t)perm_l[pos] : pos;   // the code vector at that position
                 const float4 *c4 = reinterpret_cast<const float4 *>(g_C32 + (size_t)cv * DP);
                 float dist = 0.f;
 #pragma unroll
@@ -323,6 +474,19 @@ __global__ __launch_bounds__(WD_THREADS) void assign_wide_kernel(
             A[row] = rk;
             if (flag) flags[atomicAdd(flag_cnt, 1u)] = (uint32_t)row;
         }
+        if (PRUNE) {
+            __syncthreads();
+            task = sched_next;
+        } else {
+            task += gridDim.x;
+        }
+    }
+    if (PRUNE && tid == 0) {   // the last workgroup out resets the counters for the next launch
+        __threadfence();
+        if (atomicAdd(&sched[1], 1u) == gridDim.x - 1) {
+            sched[0] = 0;
+            sched[1] = 0;
+        }
     }
 }
 
@@ -330,26 +494,56 @@ __global__ __launch_bounds__(WD_THREADS) void assign_wide_kernel(
 #undef WD_STAGE_STORE
 
 template <int DP>
+static size_t wide_prune_lds(uint32_t K) {
+    const uint32_t Kp = (K + 31) & ~31u;
+    return 2 * (size_t)WD_SLICE * WideCfg<DP>::LSTR + ((2 * Kp + 15) & ~15u) + 8 * (size_t)(Kp / 32);
+}
+template <int DP>
+static bool wide_prune_fits_dp(uint32_t K) {
+    return !wide_resident<DP>(K) && K <= 65536 && wide_prune_lds<DP>(K) <= WD_LDS_MAX;
+}
+
+template <int DP>
 static hipError_t launch_wide_dp(hipStream_t s, int num_cu, uint32_t D, const uint8_t *codes, uint64_t N,
                                  const _Float16 *cb_rows, uint32_t K, const float *C32, const MfThresholds &th,
-                                 uint32_t *A, uint32_t *flags, unsigned *flag_cnt) {
+                                 uint32_t *A, uint32_t *flags, unsigned *flag_cnt, const uint32_t *perm,
+                                 const int32_t *tint, uint32_t cpr, unsigned *sched) {
     using C = WideCfg<DP>;
     const uint32_t Kp = (K + 31) & ~31u;
-    const size_t lds = wide_resident<DP>(K) ? (size_t)Kp * C::LSTR : 2 * (size_t)WD_SLICE * C::LSTR;
+    const bool prune = perm && tint && sched;
+    if (prune && !wide_prune_fits_dp<DP>(K)) return hipErrorInvalidValue;
+    const size_t lds = prune ? wide_prune_lds<DP>(K)
+                             : (wide_resident<DP>(K) ? (size_t)Kp * C::LSTR : 2 * (size_t)WD_SLICE * C::LSTR);
     const uint64_t nchunks = (N + WD_ROWS - 1) / WD_ROWS;
     const int grid = (int)std::max<uint64_t>(1, std::min<uint64_t>((nchunks + WD_WAVES - 1) / WD_WAVES, num_cu));
-    hipLaunchKernelGGL(assign_wide_kernel<DP>, dim3(grid), dim3(WD_THREADS), lds, s, codes, N, D, cb_rows, K, C32, th,
-                       A, flags, flag_cnt);
+    if (prune)
+        hipLaunchKernelGGL((assign_wide_kernel<DP, true>), dim3(grid), dim3(WD_THREADS), lds, s, codes, N, D, cb_rows, K,
+                           C32, th, A, flags, flag_cnt, perm, tint, std::max(1u, cpr), sched);
+    else
+        hipLaunchKernelGGL((assign_wide_kernel<DP, false>), dim3(grid), dim3(WD_THREADS), lds, s, codes, N, D, cb_rows,
+                           K, C32, th, A, flags, flag_cnt, nullptr, nullptr, 1u, nullptr);
     return hipGetLastError();
+}
+
+bool wide_prune_fits(uint32_t Dp, uint32_t K) {
+    switch (Dp) {
+#define X(DPV) \
+    case DPV: return wide_prune_fits_dp<DPV>(K);
+        X(4) X(8) X(12) X(16) X(20) X(24) X(28) X(32) X(36) X(40) X(44) X(48) X(52) X(56) X(60) X(64)
+#undef X
+    }
+    return false;
 }
 
 hipError_t launch_assign_wide(hipStream_t s, int num_cu, uint32_t Dp, uint32_t D, const uint8_t *codes, uint64_t N,
                               const _Float16 *cb_rows, uint32_t K, const float *C32, const MfThresholds &th,
-                              uint32_t *A, uint32_t *flags, unsigned *flag_cnt) {
+                              uint32_t *A, uint32_t *flags, unsigned *flag_cnt, const uint32_t *perm,
+                              const int32_t *tint, uint32_t cpr, unsigned *sched) {
     if (K == 0 || !wide_can_search(Dp) || D > Dp || D + 4 <= Dp) return hipErrorInvalidValue;
     switch (Dp) {
 #define X(DPV) \
-    case DPV: return launch_wide_dp<DPV>(s, num_cu, D, codes, N, cb_rows, K, C32, th, A, flags, flag_cnt);
+    case DPV: return launch_wide_dp<DPV>(s, num_cu, D, codes, N, cb_rows, K, C32, th, A, flags, flag_cnt, perm, tint, cpr, \
+                                         sched);
         X(4) X(8) X(12) X(16) X(20) X(24) X(28) X(32) X(36) X(40) X(44) X(48) X(52) X(56) X(60) X(64)
 #undef X
     }

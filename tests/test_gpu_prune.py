@@ -42,3 +42,23 @@ def test_pruned_search_matches_reference(engine, kind, cs):
     np.testing.assert_array_equal(A, A_x)
     np.testing.assert_array_equal(C, C_x)
     assert abs(d - d_x) <= 1e-9 * abs(d_x)
+
+
+# The wide search (D = 48, 4x4 blocks) prunes from K = 1024 with streamed codebook slices: a
+# workgroup's 8 chunks stacked down the image columns share one window of slices (k_wide.hip
+# PRUNE).  Same reference rule; the set_vectors case has no image geometry (consecutive chunks).
+@pytest.mark.parametrize("kind,S,bits,vectors", [("smooth", 512, 12, False), ("flat", 512, 12, False),
+                                                 ("noise", 512, 11, False), ("smooth", 1024, 11, True)])
+def test_wide_pruned_search_matches_reference(engine, kind, S, bits, vectors):
+    import quant_amd
+    rgb = _image(kind, S, seed=3)
+    X, _ = oracle.tile(rgb, S, S, 4, 4)
+    C_x, A_x, d_x = oracle.lbg(X, bits, sum_mode=1)
+    if vectors:
+        engine.set_vectors(X)
+    else:
+        engine.set_images(rgb, 1, S, S, 4, 4, quant_amd.SCALED)
+    C, A, d = engine.lbg(bits)
+    np.testing.assert_array_equal(A, A_x)
+    np.testing.assert_array_equal(C, C_x)
+    assert abs(d - d_x) <= 1e-9 * abs(d_x)
