@@ -75,9 +75,10 @@ __global__ __launch_bounds__(WD_THREADS) void assign_wide_kernel(
     const int g = lane >> 4, c = lane & 15;
     const unsigned char *gsrc = reinterpret_cast<const unsigned char *>(g_rows);
     unsigned char *buf0 = lds, *buf1 = lds + (resident ? 0 : WD_SLICE * LSTR);
-    // PRUNE: perm (u16 per position) and the tile envelopes after the two slice buffers
-    uint16_t *perm_l = reinterpret_cast<uint16_t *>(lds + 2 * WD_SLICE * LSTR);
-    int32_t *tint_l = reinterpret_cast<int32_t *>(lds + 2 * WD_SLICE * LSTR + ((2 * Kp + 15) & ~15u));
+    // PRUNE: perm (u16 per position) and the tile envelopes after the codebook / slice buffers
+    const uint32_t cb_bytes = resident ? Kp * LSTR : 2 * WD_SLICE * LSTR;
+    uint16_t *perm_l = reinterpret_cast<uint16_t *>(lds + cb_bytes);
+    int32_t *tint_l = reinterpret_cast<int32_t *>(lds + cb_bytes + ((2 * Kp + 15) & ~15u));
     const uint32_t ntiles = Kp / 32;
 
     // slice s: code vectors s*WD_SLICE.. (KS 16-byte units per thread, staged in registers)
@@ -98,13 +99,15 @@ __global__ __launch_bounds__(WD_THREADS) void assign_wide_kernel(
         for (uint32_t i = tid; i < Kp; i += WD_THREADS) perm_l[i] = (uint16_t)g_perm[i];
         for (uint32_t i = tid; i < 2 * ntiles; i += WD_THREADS) tint_l[i] = g_tint[i];
         __syncthreads();
-    } else if (resident) {
+    }
+    if (resident) {   // (PRUNE: in the order of perm)
         for (uint32_t u = tid; u < Kp * UPR; u += WD_THREADS) {
             const uint32_t row = u / UPR, col = u % UPR;
+            const uint32_t src = PRUNE ? (uint32_t)perm_l[row] : row;
             *reinterpret_cast<uint4 *>(buf0 + row * LSTR + col * 16) =
-                *reinterpret_cast<const uint4 *>(gsrc + (size_t)row * C::GROW + col * 16);
+                *reinterpret_cast<const uint4 *>(gsrc + (size_t)src * C::GROW + col * 16);
         }
-    } else {
+    } else if (!PRUNE) {
         WD_STAGE_LOAD(0u)
         WD_STAGE_STORE(0u, buf0)
     }
@@ -236,6 +239,36 @@ __global__ __launch_bounds__(WD_THREADS) void assign_wide_kernel(
             }
             qmn = (int32_t)(wave_min_u32((uint32_t)qmn ^ 0x80000000u) ^ 0x80000000u);
             qmx = (int32_t)(~wave_min_u32(~((uint32_t)qmx ^ 0x80000000u)) ^ 0x80000000u);
+            // the row's best distance so far from above: its best MFMA score over the four lane
+            // groups plus the score error, max over the wave's rows
+            auto wave_bound = [&]() {
+                float ub = 0.f;
+#pragma unroll
+                for (int t = 0; t < WD_TILES; t++) {
+                    float v = __fmaf_rn(b1[t], th.inv_scale, xn2[t]) + th.mfma;
+                    v = fminf(v, xor16_f32(v));
+                    v = fminf(v, xor32_f32(v));
+                    const uint64_t row = base + t * 16 + c;
+                    ub = chunk < nchunks && row < N ? fmaxf(ub, v) : ub;
+                }
+                return __uint_as_float(~wave_min_u32(~__float_as_uint(fmaxf(ub, 0.f))));   // >= 0: bits order as values
+            };
+            if (resident) {   // the whole codebook in LDS: every wave its own window, no barriers
+                const int32_t tlo = lane < (int)ntiles ? tint_l[2 * lane] : 0x7FFFFFFF;
+                const int32_t thi = lane < (int)ntiles ? tint_l[2 * lane + 1] : (int32_t)0x80000000;
+                if (qmn <= qmx) {
+                    const int32_t mid = (int32_t)(((int64_t)qmn + qmx) >> 1);
+                    const uint32_t t0 = min((uint32_t)__popcll(__ballot(lane < (int)ntiles && thi < mid)), ntiles - 1);
+                    search_slice(buf0 + (size_t)t0 * 32 * LSTR, t0 * 32, 1);
+                    const float bw = wave_bound() * ((float)D / sx2) * 1.00001f + 1.0f;
+                    const float gap = (float)max(0, max(tlo - qmx, qmn - thi));
+                    const uint64_t win = __ballot(lane < (int)ntiles && gap * gap <= bw);
+                    const uint32_t lo = min(t0, win ? (uint32_t)(__ffsll((unsigned long long)win) - 1) : t0);
+                    const uint32_t hi = max(t0, win ? (uint32_t)(63 - __clzll((long long)win)) : t0);
+                    if (t0 > lo) search_slice(buf0 + (size_t)lo * 32 * LSTR, lo * 32, t0 - lo);
+                    if (hi > t0) search_slice(buf0 + (size_t)(t0 + 1) * 32 * LSTR, (t0 + 1) * 32, hi - t0);
+                }
+            } else {
             if (lane == 0) {
                 red_i[0][wave] = qmn;
                 red_i[1][wave] = qmx;
@@ -261,16 +294,7 @@ __global__ __launch_bounds__(WD_THREADS) void assign_wide_kernel(
                 search_slice(buf0, s0 * WD_SLICE, min(WD_SLICE, Kp - s0 * WD_SLICE) / 32);
                 // one bound: every row's best distance so far from above (its best MFMA score over
                 // the four lane groups, plus the score error), max over the workgroup
-                float ub = 0.f;
-#pragma unroll
-                for (int t = 0; t < WD_TILES; t++) {
-                    float v = __fmaf_rn(b1[t], th.inv_scale, xn2[t]) + th.mfma;
-                    v = fminf(v, xor16_f32(v));
-                    v = fminf(v, xor32_f32(v));
-                    const uint64_t row = base + t * 16 + c;
-                    ub = chunk < nchunks && row < N ? fmaxf(ub, v) : ub;
-                }
-                ub = __uint_as_float(~wave_min_u32(~__float_as_uint(fmaxf(ub, 0.f))));   // >= 0: bits order as values
+                const float ub = wave_bound();
                 if (tid == 0) {
                     win_lo = 0x7FFFFFFF;
                     win_hi = -1;
@@ -313,6 +337,7 @@ __global__ __launch_bounds__(WD_THREADS) void assign_wide_kernel(
                 }
                 __syncthreads();   // (the buffers are free for the next task)
             }
+            }   // (streamed)
         } else {
             for (uint32_t s = 0; s < ns; s++) {
                 const unsigned char *cur = (it & 1) ? buf1 : buf0;
@@ -496,11 +521,13 @@ __global__ __launch_bounds__(WD_THREADS) void assign_wide_kernel(
 template <int DP>
 static size_t wide_prune_lds(uint32_t K) {
     const uint32_t Kp = (K + 31) & ~31u;
-    return 2 * (size_t)WD_SLICE * WideCfg<DP>::LSTR + ((2 * Kp + 15) & ~15u) + 8 * (size_t)(Kp / 32);
+    const size_t cb = wide_resident<DP>(K) ? (size_t)Kp * WideCfg<DP>::LSTR : 2 * (size_t)WD_SLICE * WideCfg<DP>::LSTR;
+    return cb + ((2 * Kp + 15) & ~15u) + 8 * (size_t)(Kp / 32);
 }
 template <int DP>
-static bool wide_prune_fits_dp(uint32_t K) {
-    return !wide_resident<DP>(K) && K <= 65536 && wide_prune_lds<DP>(K) <= WD_LDS_MAX;
+static bool wide_prune_fits_dp(uint32_t K) {   // (resident: one envelope per lane, <= 64 tiles)
+    const uint32_t Kp = (K + 31) & ~31u;
+    return K <= 65536 && wide_prune_lds<DP>(K) <= WD_LDS_MAX && (!wide_resident<DP>(K) || Kp / 32 <= 64);
 }
 
 template <int DP>
