@@ -243,6 +243,8 @@ hipError_t launch_assign_wide(hipStream_t s, int num_cu, uint32_t Dp, uint32_t D
                               uint32_t *A, uint32_t *flags, unsigned *flag_cnt, const uint32_t *perm = nullptr,
                               const int32_t *tint = nullptr, uint32_t cpr = 1, unsigned *sched = nullptr);
 // (sched: two zeroed u32 the pruned variant's task counter uses and leaves zeroed)
+// perm / tint / qscale = D / sx^2 (the level's pruned order; the chunked sweep only): only the
+// positions the projection bound admits for the rows' fp32 bands are swept.
 // Recheck of flagged rows: fp32 distances to all K code vectors (C32 [Kpad][Dp]), fp64 in
 // the reference's order for those inside the fp32 error band (alpha, beta, gamma as the VALU
 // search's); exact ties are listed in ties (tie_cnt) for launch_kd_resolve or the host.
@@ -252,7 +254,8 @@ hipError_t launch_recheck(hipStream_t s, int num_cu, const uint8_t *codes, uint3
                           const uint32_t *flags, const unsigned *flag_cnt, const double *C64, const float *C32,
                           uint32_t K, const double *lut64, float alpha, float beta, float gamma, double tie_rel,
                           uint32_t *A, uint32_t *ties, unsigned *tie_cnt, uint64_t *xslab, uint32_t *xcnt,
-                          const uint64_t *plut);
+                          const uint64_t *plut,
+                          const uint32_t *perm = nullptr, const int32_t *tint = nullptr, float qscale = 0.f);
 // The recheck on the search's MFMA scores (D = 12, k_mf32.hip): same contract as launch_recheck
 // (the band from th.m0 / th.m1), for K with recheck_mf32_fits.
 bool recheck_mf32_fits(uint32_t K);

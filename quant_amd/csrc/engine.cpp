@@ -750,9 +750,12 @@ qvq_status run_level(qvq_ctx *ctx, uint32_t K, int slot, bool sums_out, const do
     } else {
         float alpha, beta, gamma;
         valu_coeffs(ctx, alpha, beta, gamma);
+        const bool pruned = ctx->perm_k == K;   // the search's order is valid for the recheck too
         HIPCHK(launch_recheck(ctx->stream, ctx->num_cu, ctx->d_codes, ctx->Dp, ctx->D, ctx->d_flags, &cnt[0],
                               ctx->d_C64_split, ctx->d_C32, K, ctx->d_lut64, alpha, beta, gamma, 1e-12, ctx->d_A,
-                              ctx->d_ties, &cnt[1], xslab, xcnt, ctx->d_plut));
+                              ctx->d_ties, &cnt[1], xslab, xcnt, ctx->d_plut, pruned ? ctx->d_perm : nullptr,
+                              pruned ? ctx->d_tint : nullptr,
+                              (float)((double)ctx->D / (ctx->terms.sx * ctx->terms.sx))));
     }
     qvq_status st;
     if (early_upd) {

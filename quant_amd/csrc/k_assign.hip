@@ -1044,9 +1044,11 @@ __global__ __launch_bounds__(RECHECK_THREADS) void recheck_chunked_kernel(
     const unsigned int *__restrict__ flag_cnt, const double *__restrict__ C64, const float *__restrict__ g_C32,
     uint32_t K, const double *__restrict__ lut64, float alpha, float beta, float gamma, double tie_rel,
     uint32_t *__restrict__ A, uint32_t *__restrict__ ties, unsigned int *__restrict__ tie_cnt,
-    uint64_t *__restrict__ xslab, uint32_t *__restrict__ xcnt, const uint64_t *__restrict__ plut) {
+    uint64_t *__restrict__ xslab, uint32_t *__restrict__ xcnt, const uint64_t *__restrict__ plut,
+    const uint32_t *__restrict__ perm, const int32_t *__restrict__ tint, float qscale) {
     static_assert(DT > 0 && DT % 4 == 0, "a known padded width");
     extern __shared__ __attribute__((aligned(16))) double rsm[];
+    __shared__ int32_t win_lo, win_hi;
     constexpr int W = RECHECK_WAVES;
     constexpr int NQ = DT / 4;
     constexpr uint32_t CS = recheck_c32_stride(DT);
@@ -1092,23 +1094,69 @@ __global__ __launch_bounds__(RECHECK_THREADS) void recheck_chunked_kernel(
         for (int q = 0; q < NQ; q++) xq[q] = reinterpret_cast<const float4 *>(xr)[q];
         float b1 = INFINITY, b2 = INFINITY;
         uint32_t kb = 0;
-        for (uint32_t c0 = 0; c0 < K; c0 += RC_CHUNK) {
-            const uint32_t n = min(RC_CHUNK, K - c0);
+        // perm (the search's pruned order): only the positions whose tiles the projection bound
+        // admits for some row of the group.  A row's best distance is at most its distance to the
+        // search's index (fp32, d_A); every candidate of the fp32 band below lies within d_A plus
+        // the band plus its own fp32 error, so a tile whose envelope gap g has sx^2 g^2 / D above
+        // that holds none.
+        uint32_t P0 = 0, P1 = K;
+        if (perm) {
+            if (threadIdx.x == 0) {
+                win_lo = 0x7FFFFFFF;
+                win_hi = -1;
+            }
+            __syncthreads();
+            if (have) {
+                uint32_t su = lane < (int)D ? (cbyte ^ 0x80u) : 0u;
+                float e = lane < (int)D ? xr[lane] - g_C32[(size_t)carow * Dp + lane] : 0.f;
+                float dA = e * e;
+#pragma unroll
+                for (int o = 32; o >= 1; o >>= 1) {
+                    su += __shfl_xor(su, o);
+                    dA += __shfl_xor(dA, o);
+                }
+                const int32_t qw = 2 * (int32_t)su - 255 * (int32_t)D;
+                const float U = (dA + 4.f * (alpha * sqrtf(dA) + beta * dA) + 4.f * gamma) * 1.001f;
+                const float bw = U * qscale * 1.00001f + 1.0f;
+                const uint32_t nt = (K + 31) / 32;
+                int32_t lo = 0x7FFFFFFF, hi = -1;
+                for (uint32_t t = lane; t < nt; t += 64) {
+                    const float gap = (float)max(0, max(tint[2 * t] - qw, qw - tint[2 * t + 1]));
+                    if (gap * gap <= bw) {
+                        lo = min(lo, (int32_t)t);
+                        hi = max(hi, (int32_t)t);
+                    }
+                }
+                lo = (int32_t)(wave_min_u32((uint32_t)lo ^ 0x80000000u) ^ 0x80000000u);
+                hi = (int32_t)(~wave_min_u32(~((uint32_t)hi ^ 0x80000000u)) ^ 0x80000000u);
+                if (lane == 0 && hi >= 0) {
+                    atomicMin(&win_lo, lo);
+                    atomicMax(&win_hi, hi);
+                }
+            }
+            __syncthreads();
+            P0 = win_hi >= 0 ? 32 * (uint32_t)win_lo : 0;
+            P1 = win_hi >= 0 ? min(K, 32 * (uint32_t)win_hi + 32) : 0;   // (positions >= K: padding)
+        }
+        for (uint32_t c0 = P0; c0 < P1; c0 += RC_CHUNK) {
+            const uint32_t n = min(RC_CHUNK, P1 - c0);
             __syncthreads();   // the previous chunk's reads are done
             for (uint32_t i = threadIdx.x; i < n * NQ; i += RECHECK_THREADS) {
                 const uint32_t k = i / NQ, q = i - k * NQ;
+                const uint32_t src = perm ? perm[c0 + k] : c0 + k;
                 reinterpret_cast<float4 *>(cch + (size_t)k * CS)[q] =
-                    reinterpret_cast<const float4 *>(g_C32 + (size_t)(c0 + k) * Dp)[q];
+                    src < K ? reinterpret_cast<const float4 *>(g_C32 + (size_t)src * Dp)[q] : make_float4(1e18f, 1e18f, 1e18f, 1e18f);
             }
             __syncthreads();
             if (have)
                 for (uint32_t k = lane; k < n; k += 64) {
                     const float d = d32_at(cch + (size_t)k * CS, xq);
                     b2 = med3f(b1, b2, d);
-                    kb = d < b1 ? c0 + k : kb;
+                    kb = d < b1 ? c0 + k : kb;   // a position
                     b1 = min2f(b1, d);
                 }
         }
+        if (perm && have) kb = perm[kb];   // the position's code vector
         if (!have) continue;
         const float m = __uint_as_float(wave_min_u32(__float_as_uint(b1)));   // distances >= 0
         double d1 = INFINITY, d2 = INFINITY;
@@ -1123,9 +1171,11 @@ __global__ __launch_bounds__(RECHECK_THREADS) void recheck_chunked_kernel(
                 d2 = d;
             }
         };
-        if (within(b2, m)) {   // rare: more than one candidate on this lane
-            for (uint32_t k = lane; k < K; k += 64)
+        if (within(b2, m)) {   // rare: more than one candidate on this lane: its positions again
+            for (uint32_t p = P0 + lane; p < P1; p += 64) {
+                const uint32_t k = perm ? perm[p] : p;
                 if (within(d32_at(g_C32 + (size_t)k * Dp, xq), m)) take(k);
+            }
         } else if (within(b1, m)) {
             take(kb);
         }
@@ -1163,7 +1213,7 @@ hipError_t launch_recheck(hipStream_t s, int num_cu, const uint8_t *codes, uint3
                           const uint32_t *flags, const unsigned *flag_cnt, const double *C64, const float *C32,
                           uint32_t K, const double *lut64, float alpha, float beta, float gamma, double tie_rel,
                           uint32_t *A, uint32_t *ties, unsigned *tie_cnt, uint64_t *xslab, uint32_t *xcnt,
-                          const uint64_t *plut) {
+                          const uint64_t *plut, const uint32_t *perm, const int32_t *tint, float qscale) {
     if (Dp % 4 || Dp > 64) return hipErrorInvalidValue;
     const size_t base = RECHECK_LDS_BASE;
     const size_t cb = (size_t)K * recheck_c32_stride(Dp) * 4;
@@ -1176,11 +1226,11 @@ hipError_t launch_recheck(hipStream_t s, int num_cu, const uint8_t *codes, uint3
         if (Dp == 12)
             hipLaunchKernelGGL(recheck_chunked_kernel<12>, dim3(num_cu), dim3(RECHECK_THREADS), clds, s, codes, Dp, D,
                                flags, flag_cnt, C64, C32, K, lut64, alpha, beta, gamma, tie_rel, A, ties, tie_cnt,
-                               xslab, xcnt, plut);
+                               xslab, xcnt, plut, perm, tint, qscale);
         else
             hipLaunchKernelGGL(recheck_chunked_kernel<48>, dim3(num_cu), dim3(RECHECK_THREADS), clds, s, codes, Dp, D,
                                flags, flag_cnt, C64, C32, K, lut64, alpha, beta, gamma, tie_rel, A, ties, tie_cnt,
-                               xslab, xcnt, plut);
+                               xslab, xcnt, plut, perm, tint, qscale);
         return hipGetLastError();
     }
 #define QVQ_RC(SS, DT)                                                                                             \
