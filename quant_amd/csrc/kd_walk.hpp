@@ -42,6 +42,42 @@ __device__ inline double ref_l2_cv(const double *a, const double *C64, uint32_t 
     return ref_l2_hd(a, C64 + (uint64_t)k * D, (int)D);   // (a D = 48 row in registers costs the recheck occupancy)
 }
 
+// The same for D = 48 with the row's loads in flight two 8-component chunks ahead (the generic
+// loop waits for every group of four: 12 dependent round trips per point); the kd kernels'
+// point distances only (not inlined: its rows get their own register allocation).
+static __device__ __attribute__((noinline)) double ref_l2_48(const double *a, const double *c) {
+    const double2 *p = reinterpret_cast<const double2 *>(c);
+    double2 b[2][4];
+#pragma unroll
+    for (int i = 0; i < 4; i++) b[0][i] = p[i];
+#pragma unroll
+    for (int i = 0; i < 4; i++) b[1][i] = p[4 + i];
+    double r = 0;
+#pragma unroll
+    for (int ch = 0; ch < 6; ch++) {   // chunk ch: components 8 ch .. 8 ch + 7, two groups of four
+        const double2 *v = b[ch & 1];
+#pragma unroll
+        for (int g = 0; g < 2; g++) {
+            const int d = 8 * ch + 4 * g;
+            const double e0 = a[d] - v[2 * g].x, e1 = a[d + 1] - v[2 * g].y;
+            const double e2 = a[d + 2] - v[2 * g + 1].x, e3 = a[d + 3] - v[2 * g + 1].y;
+            r += (e1 * e1 + e2 * e2) + (e0 * e0 + e3 * e3);
+        }
+        if (ch + 2 < 6) {
+#pragma unroll
+            for (int i = 0; i < 4; i++) b[ch & 1][i] = p[4 * (ch + 2) + i];
+        }
+    }
+    return r;
+}
+// pv[j] for j = j0, j0 + step, ... < K: the fp64 reference distance of row a to point vind[j]
+__device__ inline void kd_point_dists(const double *a, const double *C64, const uint32_t *vind, uint32_t K, uint32_t D,
+                                      uint32_t j0, uint32_t step, double *pv) {
+#pragma unroll 1
+    for (uint32_t j = j0; j < K; j += step)
+        pv[j] = D == 48 ? ref_l2_48(a, C64 + (uint64_t)vind[j] * 48) : ref_l2_cv(a, C64, vind[j], D);
+}
+
 // LDS written by some lanes of a wave and then read by others: order the accesses.
 __device__ inline void wave_lds_sync() {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -54,9 +90,10 @@ __device__ inline void wave_lds_sync() {
 // point in leaf order with the smallest distance below the leaf-entry worst -- what the
 // sequential strict-'<' scan picks.  Leaves hold at most 10 points (< 64 lanes).  pv holds
 // every point's distance in vind order; subtrees none of whose points is below best are
-// skipped (same result).
+// skipped (same result), and the walk stops once best is gmin, the smallest of all K
+// distances (when known; -inf: never).
 __device__ inline uint32_t kd_nearest_wave(const double *q, uint32_t D, const KdView &t, const double *pv, double *sd,
-                                    int32_t *sn, double *dl, int lane) {
+                                    int32_t *sn, double *dl, int lane, double gmin = -INFINITY) {
     double distsq = 0;   // dl: per-dimension cell distances (LDS, uniform across lanes)
     for (uint32_t d = 0; d < D; d++) {
         const double x = q[d];
@@ -105,6 +142,7 @@ __device__ inline uint32_t kd_nearest_wave(const double *q, uint32_t D, const Kd
                 const uint64_t hit = __ballot(dist == m);
                 best = m;
                 best_idx = t.vind[n.a + __ffsll((unsigned long long)hit) - 1];
+                if (m == gmin) break;   // the smallest of all K distances: nothing can follow
             }
             sp--;
             continue;
@@ -138,6 +176,128 @@ __device__ inline uint32_t kd_nearest_wave(const double *q, uint32_t D, const Kd
         sp--;
     }
     return best_idx;
+}
+
+// Wave-uniform doubles held one per lane (lane l = element l), read and written by lane index.
+__device__ inline double lane_get_f64(double v, int l) {
+    const uint64_t b = (uint64_t)__double_as_longlong(v);
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)b, l);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(b >> 32), l);
+    return __longlong_as_double((long long)((uint64_t)hi << 32 | lo));
+}
+__device__ inline double lane_set_f64(double v, double x, int l) { return (int)__lane_id() == l ? x : v; }
+
+// Direct answer for a tie row, without the walk.  The walk (nanoflann's search) ends on the
+// first point it reaches among T, the points at the smallest of all K distances gmin: later
+// points need dist < best.  Before it reaches one, best is >= gnext, the smallest distance
+// above gmin, so a point p of T is reached whenever every cell bound m2 on p's root-to-leaf
+// path where p lies in the far child is <= gnext (near children are always entered; a far
+// child's test reads dists[] as at its node's entry: the near subtree restores what it
+// changes).  Ignoring pruning the walk meets the points of T in path order: at the node where
+// two paths part, the near child's first, and in vind order within a leaf.  So: the first of T
+// in path order, if its own path passes the test, is the walk's answer.  Otherwise (or more
+// than 64 points in T, or D > 64) returns false and the walk decides.  Lane d holds query
+// component d and the root cell distance of dimension d; candl: 64 ints of LDS.  gmin is
+// returned either way (the walk stops at it).
+__device__ inline bool kd_tie_direct(const double *q, uint32_t D, const KdView &t, const double *pv, uint32_t K,
+                                     int32_t *candl, int lane, uint32_t &out, double &gmin_out) {
+    double a1 = INFINITY, a2 = INFINITY;   // this lane's smallest distance and its smallest above a1
+    for (uint32_t j0 = 0; j0 < K; j0 += 256) {
+        double p[4];
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const uint32_t j = j0 + 64 * u + lane;
+            p[u] = j < K ? pv[j] : INFINITY;
+        }
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            if (p[u] < a1) {
+                a2 = a1;
+                a1 = p[u];
+            } else if (p[u] > a1 && p[u] < a2) {
+                a2 = p[u];
+            }
+        }
+    }
+    const double gmin = wave_min_f64<4>(a1);
+    const double gnext = wave_min_f64<4>(a1 > gmin ? a1 : a2);
+    gmin_out = gmin;
+    if (D > 64) return false;
+    int nt = 0;
+    for (uint32_t j0 = 0; j0 < K && nt <= 64; j0 += 64) {
+        const uint32_t j = j0 + lane;
+        const bool take = j < K && pv[j] == gmin;
+        const uint64_t bal = __ballot(take);
+        const int pre = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(bal >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bal, 0u));
+        if (take && nt + pre < 64) candl[nt + pre] = (int32_t)j;
+        nt += __popcll(bal);
+    }
+    wave_lds_sync();
+    if (nt < 1 || nt > 64) return false;
+    const int32_t mine = lane < nt ? candl[lane] : -1;
+    wave_lds_sync();
+    const double ql = lane < (int)D ? q[lane] : 0.0;
+    double dll = 0.0;
+    if (lane < (int)D) {
+        const double lo = t.lo[lane], hi = t.hi[lane];
+        if (ql < lo) dll = (ql - lo) * (ql - lo);
+        if (ql > hi) dll = (ql - hi) * (ql - hi);
+    }
+    double sdv = 0;   // the root's cell bound, in dimension order (zero terms add exactly)
+    for (uint32_t d = 0; d < D; d++) sdv += lane_get_f64(dll, (int)d);
+    const int max_steps = t.depth + 1;
+    // the first of T in path order: each point against the current first, both positions
+    // descending together to the node where they part
+    int32_t w = __builtin_amdgcn_readlane(mine, 0);
+    for (int c = 1; c < nt; c++) {
+        const int32_t j = __builtin_amdgcn_readlane(mine, c);
+        bool j_first = j < w;   // one leaf: vind order
+        KdNodeDev n = t.nodes[0];
+        for (int it = 0; it < max_steps && n.child1 >= 0; it++) {
+            const KdNodeDev c1 = t.nodes[n.child1], c2 = t.nodes[n.child2];
+            const bool wl = w < c1.b, jl = j < c1.b;   // child1 holds vind[first, c1.b)
+            if (wl != jl) {
+                const double val = lane_get_f64(ql, kd_feat(n));
+                j_first = jl == (((val - n.lo) + (val - n.hi)) < 0);   // j in the near child
+                break;
+            }
+            n = wl ? c1 : c2;
+        }
+        if (j_first) w = j;
+    }
+    // w's path: the cell-bound test at every far step
+    bool ok = true;
+    KdNodeDev n = t.nodes[0];
+    for (int it = 0; it < max_steps && n.child1 >= 0; it++) {
+        const KdNodeDev c1 = t.nodes[n.child1], c2 = t.nodes[n.child2];
+        const bool go_left = w < c1.b;
+        const int f = kd_feat(n);
+        const double val = lane_get_f64(ql, f);
+        const bool left_first = ((val - n.lo) + (val - n.hi)) < 0;
+        if (go_left != left_first) {
+            const double cut_dist = left_first ? (val - n.hi) * (val - n.hi) : (val - n.lo) * (val - n.lo);
+            const double m2 = (sdv - lane_get_f64(dll, f)) + cut_dist;
+            ok = ok && m2 <= gnext;
+            dll = lane_set_f64(dll, cut_dist, f);
+            sdv = m2;
+        }
+        n = go_left ? c1 : c2;
+    }
+    if (!ok || n.child1 >= 0) return false;
+    out = t.vind[w];
+    return true;
+}
+
+// The direct answer when it applies, else the walk, which stops at gmin (QVQ_KDWALK_LDS
+// builds: the walk always, A/B).
+__device__ inline uint32_t kd_walk(const double *q, uint32_t D, const KdView &t, const double *pv, uint32_t K, double *sd,
+                                   int32_t *sn, double *dl, int lane) {
+    double gmin = -INFINITY;
+#ifndef QVQ_KDWALK_LDS
+    uint32_t k;
+    if (kd_tie_direct(q, D, t, pv, K, reinterpret_cast<int32_t *>(dl), lane, k, gmin)) return k;
+#endif
+    return kd_nearest_wave(q, D, t, pv, sd, sn, dl, lane, gmin);
 }
 
 // Exact ties listed by the recheck, answered by the reference kd-tree traversal
@@ -223,10 +383,10 @@ __device__ inline void kd_resolve_block(const KdArgs &a, unsigned nt, uint32_t b
             const uint32_t row = a.ties[f];
             if (threadIdx.x < D) xs[threadIdx.x] = a.lut64[a.codes[(uint64_t)row * a.Dp + threadIdx.x]];
             __syncthreads();
-            for (uint32_t j = threadIdx.x; j < K; j += blockDim.x) pv[j] = ref_l2_cv(xs, a.C64, kv.vind[j], D);
+            kd_point_dists(xs, a.C64, kv.vind, K, D, threadIdx.x, blockDim.x, pv);
             __syncthreads();
             if (wave == 0) {
-                const uint32_t k = kd_nearest_wave(xs, D, kv, pv, sd, sn, dl, lane);
+                const uint32_t k = kd_walk(xs, D, kv, pv, K, sd, sn, dl, lane);
                 const uint32_t from = __builtin_amdgcn_readfirstlane(a.A[row]);
                 if (k != from) {
                     if (a.xslab) move_row_terms(a.codes, a.Dp, D, row, from, k, K, a.xslab, a.xcnt, a.plut, lane);
@@ -256,10 +416,10 @@ __device__ inline void kd_resolve_block(const KdArgs &a, unsigned nt, uint32_t b
                     if (j0 + 64 * u < K) pv[j0 + 64 * u] = ref_l2_n<12>(xs, c[u]);
             }
         } else {
-            for (uint32_t j = lane; j < K; j += 64) pv[j] = ref_l2_cv(xs, a.C64, kv.vind[j], D);
+            kd_point_dists(xs, a.C64, kv.vind, K, D, lane, 64, pv);
         }
         wave_lds_sync();
-        const uint32_t k = kd_nearest_wave(xs, D, kv, pv, sd, sn, dl, lane);
+        const uint32_t k = kd_walk(xs, D, kv, pv, K, sd, sn, dl, lane);
         const uint32_t from = __builtin_amdgcn_readfirstlane(a.A[row]);   // the search's index
         if (k != from) {
             if (a.xslab) move_row_terms(a.codes, a.Dp, D, row, from, k, K, a.xslab, a.xcnt, a.plut, lane);
