@@ -134,6 +134,28 @@ def test_assign_ties_and_duplicates(engine, kdmode):
     assert t["host_ties"][0] > 0      # rows equal to base[:4] tie between the two copies
 
 
+@pytest.mark.parametrize("bw,bh", [(2, 2), (4, 4)])
+def test_kd_tie_sets_across_leaves(engine, bw, bh):
+    """Rows with many exactly equidistant code vectors spread over several kd-tree leaves
+    (x +- 2^-12 along every component: the differences, hence the distances, are exact),
+    next to 100 duplicate zero code vectors (a deep tree) and scaled rows.  The device
+    answers such ties from the path order of the tied points (kd_tie_direct), falling back
+    to the walk; both must pick the reference kd-tree's first-visited point."""
+    rng = np.random.default_rng(19)
+    X, _ = oracle.tile(oracle.gen_image(128), 128, 128, bw, bh)
+    D = X.shape[1]
+    engine.set_vectors(X)
+    centres = X[rng.choice(len(X), 24, replace=False)]
+    v = 2.0 ** -12
+    star = np.concatenate([np.concatenate([c + v * np.eye(D), c - v * np.eye(D)]) for c in centres])
+    others = X[rng.choice(len(X), 200, replace=False)] * 0.9
+    C = np.concatenate([others[:100], star, np.zeros((100, D)), others[100:]])
+    C = C[rng.permutation(len(C))]
+    A = engine.assign(C)
+    np.testing.assert_array_equal(A, oracle.kdtree_nn(C, X))
+    assert engine.timings()["host_ties"][0] >= 24   # at least every centre row ties
+
+
 def test_update_exact(engine):
     X, codes = oracle.tile(oracle.gen_image(128), 128, 128, 2, 2)
     engine.set_vectors(X)
