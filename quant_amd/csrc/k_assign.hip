@@ -473,8 +473,13 @@ static uint32_t small_copies(uint32_t SK) {
 }
 static size_t small_lds(uint32_t SK, uint32_t C) { return (size_t)C * small_copy_stride(SK) * 8 + 256; }
 
-template <int SK, bool FUSE>
-__global__ __launch_bounds__(MF_THREADS) void assign_small_kernel(
+// PACK: the run registers hold two components per register and part.  For word q of a row
+// (components 4q..4q+3, u = byte ^ 0x80): au[2q] += u bytes 0 and 2 as 16-bit fields, au[2q+1]
+// += bytes 1 and 3 (one v_and / v_perm of the centred word each, no per-component extract), and
+// al[2q], al[2q+1] the lo8 lookups of the same pairs.  A run holds <= 256 rows, so every field
+// stays below 2^16.  ~14 VALU per row fewer than one (u << 16 | lo) register per component.
+template <int SK, bool FUSE, bool PACK, int NW>
+__global__ __launch_bounds__(NW * 64) void assign_small_kernel(
     const uint8_t *__restrict__ codes, uint64_t N, uint32_t K, const float *__restrict__ g_E32,
     const uint64_t *__restrict__ g_plut, MfThresholds th, uint64_t rows_per_lane, uint32_t copies,
     uint32_t *__restrict__ A, uint32_t *__restrict__ flags, unsigned *__restrict__ flag_cnt,
@@ -494,37 +499,11 @@ __global__ __launch_bounds__(MF_THREADS) void assign_small_kernel(
         (const __attribute__((address_space(3))) uint8_t *)(uintptr_t)0;
     uint64_t *cps = reinterpret_cast<uint64_t *>(lds + 256);
     const int tid = threadIdx.x;
-    if (FUSE) {
-        for (uint32_t i = tid; i < copies * S; i += MF_THREADS) cps[i] = 0;
-        if (tid < 256) lo8[tid] = (uint8_t)(g_plut[tid] & 0xFF);
-        if (blockIdx.x == 0) {   // the correction slabs G (+) and G + 1 (-), after all G others
-            for (uint32_t i = tid; i < 2 * K * MF_D; i += MF_THREADS) part[(uint64_t)gridDim.x * K * MF_D + i] = 0;
-            for (uint32_t i = tid; i < 2 * K; i += MF_THREADS) part_cnt[(uint64_t)gridDim.x * K + i] = 0;
-        }
-    }
-    __syncthreads();
-    uint64_t *mine = cps + (size_t)((tid & 63) % copies) * S;
-
     const int lane = tid & 63, wave = tid >> 6;
     // The wave owns rows [wbase, wend); lane L takes rows wbase + L + 64 t, so every load and
     // store instruction of the wave covers 64 consecutive rows (768 contiguous bytes).
-    const uint64_t wbase = ((uint64_t)blockIdx.x * MF_WAVES + wave) * 64 * rows_per_lane;
+    const uint64_t wbase = ((uint64_t)blockIdx.x * NW + wave) * 64 * rows_per_lane;
     const uint64_t wend = min(wbase + 64 * rows_per_lane, N);
-    uint32_t acc[MF_D + 1];
-    uint32_t cur = 0xFFFFFFFFu;
-#pragma unroll
-    for (int i = 0; i <= MF_D; i++) acc[i] = 0;
-    auto flush = [&]() {
-        if (cur != 0xFFFFFFFFu && acc[MF_D]) {
-#pragma unroll
-            for (int d = 0; d < MF_D; d++)
-                atomicAdd((unsigned long long *)&mine[d * SK + cur],
-                          (unsigned long long)((((uint64_t)(acc[d] >> 16)) << 32) | (acc[d] & 0xFFFF)));
-            atomicAdd((unsigned long long *)&mine[MF_D * SK + cur], (unsigned long long)acc[MF_D]);
-        }
-#pragma unroll
-        for (int i = 0; i <= MF_D; i++) acc[i] = 0;
-    };
     // four rows of this lane (base + 64 r), two iterations ahead; branch-free (rows past N
     // read row N - 1 and are masked later), so the loads stay in flight across iterations
     auto load4 = [&](uint64_t r0, uint32_t (&w)[4][3]) {
@@ -537,6 +516,44 @@ __global__ __launch_bounds__(MF_THREADS) void assign_small_kernel(
             w[r][1] = p[1];
             w[r][2] = p[2];
         }
+    };
+    // the first group's loads go out before the LDS set-up, under its latency
+    uint32_t wa[4][3], wb[4][3];
+    load4(wbase + lane, wa);
+    if (FUSE) {
+        for (uint32_t i = tid; i < copies * S; i += (NW * 64)) cps[i] = 0;
+        if (tid < 256) lo8[tid] = (uint8_t)(g_plut[tid] & 0xFF);
+        if (blockIdx.x == 0) {   // the correction slabs G (+) and G + 1 (-), after all G others
+            for (uint32_t i = tid; i < 2 * K * MF_D; i += (NW * 64)) part[(uint64_t)gridDim.x * K * MF_D + i] = 0;
+            for (uint32_t i = tid; i < 2 * K; i += (NW * 64)) part_cnt[(uint64_t)gridDim.x * K + i] = 0;
+        }
+    }
+    __syncthreads();
+    uint64_t *mine = cps + (size_t)((tid & 63) % copies) * S;
+
+    uint32_t acc[MF_D + 1];
+    uint32_t cur = 0xFFFFFFFFu;
+#pragma unroll
+    for (int i = 0; i <= MF_D; i++) acc[i] = 0;
+    auto flush = [&]() {
+        if (cur != 0xFFFFFFFFu && acc[MF_D]) {
+#pragma unroll
+            for (int d = 0; d < MF_D; d++) {
+                uint32_t u, lo;
+                if (PACK) {   // component 4q + j: register 2q + (j & 1), field j >> 1
+                    const int reg = 2 * (d / 4) + (d & 1), sh = 16 * ((d % 4) >> 1);
+                    u = (acc[reg] >> sh) & 0xFFFF;
+                    lo = (acc[6 + reg] >> sh) & 0xFFFF;
+                } else {
+                    u = acc[d] >> 16;
+                    lo = acc[d] & 0xFFFF;
+                }
+                atomicAdd((unsigned long long *)&mine[d * SK + cur], (unsigned long long)(((uint64_t)u << 32) | lo));
+            }
+            atomicAdd((unsigned long long *)&mine[MF_D * SK + cur], (unsigned long long)acc[MF_D]);
+        }
+#pragma unroll
+        for (int i = 0; i <= MF_D; i++) acc[i] = 0;
     };
     // Rows r0 + 64 r (r < 4) of this lane, their words in w.  Expanded scores (the MFMA
     // search's, in fp32): score = n + sum_d w_d c''_d = 2^t (||x-c||^2 - ||x-mu||^2), with w
@@ -614,10 +631,21 @@ __global__ __launch_bounds__(MF_THREADS) void assign_small_kernel(
                     flush();
                     cur = rk;
                 }
+                if (PACK) {
 #pragma unroll
-                for (int d = 0; d < MF_D; d++) {
-                    const uint32_t b = (w[r][d / 4] >> (8 * (d % 4))) & 0xFF;
-                    acc[d] += (b ^ 0x80u) << 16 | lo8_at0[b];
+                    for (int q = 0; q < 3; q++) {
+                        const uint32_t wq = w[r][q], c = wq ^ 0x80808080u;
+                        acc[2 * q] += c & 0x00FF00FFu;                                // u of 4q, 4q + 2
+                        acc[2 * q + 1] += __builtin_amdgcn_perm(0u, c, 0x0C030C01u);  // u of 4q + 1, 4q + 3
+                        acc[6 + 2 * q] += (uint32_t)lo8_at0[wq & 0xFF] | (uint32_t)lo8_at0[(wq >> 16) & 0xFF] << 16;
+                        acc[7 + 2 * q] += (uint32_t)lo8_at0[(wq >> 8) & 0xFF] | (uint32_t)lo8_at0[wq >> 24] << 16;
+                    }
+                } else {
+#pragma unroll
+                    for (int d = 0; d < MF_D; d++) {
+                        const uint32_t b = (w[r][d / 4] >> (8 * (d % 4))) & 0xFF;
+                        acc[d] += (b ^ 0x80u) << 16 | lo8_at0[b];
+                    }
                 }
                 acc[MF_D] += 1;
             }
@@ -629,8 +657,6 @@ __global__ __launch_bounds__(MF_THREADS) void assign_small_kernel(
     // Two row groups per trip, each group's words loaded one group ahead into the other
     // buffer (no register copies, so the loads stay in flight under the previous group).
     // The trip count is wave-uniform; rows past wend are masked inside process.
-    uint32_t wa[4][3], wb[4][3];
-    load4(wbase + lane, wa);
     for (uint64_t ru = wbase; ru < wend; ru += 512) {
         load4(ru + 256 + lane, wb);
         process(wa, ru + lane);
@@ -643,7 +669,7 @@ __global__ __launch_bounds__(MF_THREADS) void assign_small_kernel(
         __syncthreads();
         uint64_t *pdst = part + (uint64_t)blockIdx.x * K * MF_D;   // slab layout [d][k]
         uint32_t *cdst = part_cnt + (uint64_t)blockIdx.x * K;
-        for (uint32_t i = tid; i < K * (MF_D + 1); i += MF_THREADS) {   // [d][k] of the slab
+        for (uint32_t i = tid; i < K * (MF_D + 1); i += (NW * 64)) {   // [d][k] of the slab
             const uint32_t d = i / K, k = i - d * K;
             uint64_t v = 0;
             for (uint32_t c = 0; c < copies; c++) v += cps[(size_t)c * S + d * SK + k];
@@ -682,19 +708,30 @@ hipError_t launch_assign_mfma(hipStream_t s, int grid, bool fuse, const uint8_t 
     Fn fn;
     if (K <= mf_small_k() && E32) {   // E32 is padded up to 32 rows (n = 1e30)
         const uint32_t sk = K <= 2 ? 2 : K <= 4 ? 4 : K <= 8 ? 8 : K <= 16 ? 16 : 32;
-        // rows per lane: a multiple of 4 covering N over grid x 16 waves x 64 lanes
-        const uint64_t lanes = (uint64_t)grid * MF_WAVES * 64;
-        const uint64_t rpl = ((N + lanes - 1) / lanes + 3) / 4 * 4;
+        // rows per lane: a multiple of 4 covering N over grid x waves x 64 lanes
         const uint32_t copies = fuse ? small_copies(sk) : 1;
         const size_t slds = fuse ? small_lds(sk, copies) : 256;
+        // packed run registers (QVQ_SMALL_PACK=0: one register per component, A/B); QVQ_SMALL_NW:
+        // waves per block (16: 4 per SIMD, 128 VGPRs; 12: 3 per SIMD, 168 VGPRs, no spills)
+        static const bool pack = !(std::getenv("QVQ_SMALL_PACK") && std::getenv("QVQ_SMALL_PACK")[0] == '0');
+        static const int nw = std::getenv("QVQ_SMALL_NW") && std::atoi(std::getenv("QVQ_SMALL_NW")) == 12 ? 12 : 16;
+        const int sw = fuse && pack ? nw : 16;
+        const uint64_t lanes = (uint64_t)grid * sw * 64;
+        const uint64_t rpl = ((N + lanes - 1) / lanes + 3) / 4 * 4;
 #define QVQ_SMALL(V)                                                                                              \
     do {                                                                                                          \
-        if (fuse)                                                                                                 \
-            hipLaunchKernelGGL((assign_small_kernel<V, true>), dim3(grid), dim3(MF_THREADS), slds, s, codes, N, K, \
-                               E32, plut, th, rpl, copies, A, flags, flag_cnt, part, part_cnt);                  \
+        if (fuse && pack && sw == 12)                                                                             \
+            hipLaunchKernelGGL((assign_small_kernel<V, true, true, 12>), dim3(grid), dim3(12 * 64), slds, s,      \
+                               codes, N, K, E32, plut, th, rpl, copies, A, flags, flag_cnt, part, part_cnt);     \
+        else if (fuse && pack)                                                                                    \
+            hipLaunchKernelGGL((assign_small_kernel<V, true, true, 16>), dim3(grid), dim3(16 * 64), slds, s,      \
+                               codes, N, K, E32, plut, th, rpl, copies, A, flags, flag_cnt, part, part_cnt);     \
+        else if (fuse)                                                                                            \
+            hipLaunchKernelGGL((assign_small_kernel<V, true, false, 16>), dim3(grid), dim3(16 * 64), slds, s,     \
+                               codes, N, K, E32, plut, th, rpl, copies, A, flags, flag_cnt, part, part_cnt);     \
         else                                                                                                      \
-            hipLaunchKernelGGL((assign_small_kernel<V, false>), dim3(grid), dim3(MF_THREADS), slds, s, codes, N,  \
-                               K, E32, plut, th, rpl, copies, A, flags, flag_cnt, part, part_cnt);                \
+            hipLaunchKernelGGL((assign_small_kernel<V, false, false, 16>), dim3(grid), dim3(16 * 64), slds, s,    \
+                               codes, N, K, E32, plut, th, rpl, copies, A, flags, flag_cnt, part, part_cnt);     \
     } while (0)
         switch (sk) {
         case 2: QVQ_SMALL(2); break;
@@ -924,10 +961,12 @@ __global__ __launch_bounds__(RECHECK_THREADS) void recheck_kernel(
     float *c32s = x32 + W * 64;                                    // [K][CS] when staged
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const unsigned nflag = *flag_cnt;
-    if (nflag == 0 || blockIdx.x * W >= nflag) return;
+    // rows go round the blocks first (f = blockIdx + grid * wave ...), so a level's few flagged
+    // rows spread over the CUs instead of 16 to a CU on the first few
+    if (nflag == 0 || blockIdx.x >= nflag) return;
     const uint32_t CS = STAGED ? recheck_c32_stride(Dp) : Dp;
     const unsigned fstride = gridDim.x * W;
-    unsigned f = blockIdx.x * W + wave;
+    unsigned f = blockIdx.x + gridDim.x * wave;
     // two-deep prefetch: row index of f + fstride, bytes of row f
     uint32_t row = f < nflag ? flags[f] : 0;
     uint32_t byte = (f < nflag && lane < (int)D) ? codes[(uint64_t)row * Dp + lane] : 0;

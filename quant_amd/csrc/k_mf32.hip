@@ -161,6 +161,26 @@ __global__ __launch_bounds__(M32_THREADS) void assign_mf32_kernel(
         (const __attribute__((address_space(3))) uint8_t *)(uintptr_t)0;
     constexpr uint32_t ROWS0 = FUSE ? 256 : 0;   // m32_lds_layout
     const int tid = threadIdx.x;
+    const int lane = tid & 63, wave = tid >> 6;
+    const int r32 = lane & 31, h = lane >> 5;
+    const uint64_t nchunks = (N + M32_ROWS - 1) / M32_ROWS;
+    // lane (r32, h) loads row r32 of both data tiles (the words of data tile T in q[3T..3T+2]);
+    // its own row base + lane is the one of tile h.  Branch-free: rows past N read row N - 1.
+    auto load_codes = [&](uint64_t chunk, uint32_t (&q)[6]) {
+#pragma unroll
+        for (int T = 0; T < 2; T++) {
+            uint64_t row = chunk * M32_ROWS + 32 * T + r32;
+            row = row < N ? row : N - 1;
+            const uint32_t *p = reinterpret_cast<const uint32_t *>(codes + row * MF_D);
+            q[3 * T] = p[0];
+            q[3 * T + 1] = p[1];
+            q[3 * T + 2] = p[2];
+        }
+    };
+    uint64_t chunk = (uint64_t)blockIdx.x * M32_WAVES + wave;
+    const uint64_t stride = (uint64_t)gridDim.x * M32_WAVES;
+    uint32_t qn[6];
+    load_codes(chunk, qn);   // the first chunk's rows go out before the LDS staging, under its latency
     m32_stage_pq(lds, L.q, g_rows, Kp, tid, ROWS0, PRUNE ? g_perm : nullptr);
     if (PRUNE)
         for (uint32_t i = tid; i < Kp; i += M32_THREADS) perm_l[i] = (uint16_t)g_perm[i];
@@ -181,10 +201,7 @@ __global__ __launch_bounds__(M32_THREADS) void assign_mf32_kernel(
     __syncthreads();
     const float *C32 = STAGED ? c32s : g_C32;
 
-    const int lane = tid & 63, wave = tid >> 6;
-    const int r32 = lane & 31, h = lane >> 5;
     const uint32_t ntiles = Kp / 32;
-    const uint64_t nchunks = (N + M32_ROWS - 1) / M32_ROWS;
     // A fragments of code tile t: P half h of code vector 32t + r32 (halves swapped on bit 3),
     // Q bytes 8(1-h) .. +15
     const unsigned char *pa = lds + ROWS0 + r32 * 32 + 16 * (h ^ ((r32 >> 3) & 1));
@@ -196,29 +213,12 @@ __global__ __launch_bounds__(M32_THREADS) void assign_mf32_kernel(
         a1 = __builtin_bit_cast(half8, v1);
         a2 = __builtin_bit_cast(half8, v2);
     };
-    // lane (r32, h) loads row r32 of both data tiles (the words of data tile T in q[3T..3T+2]);
-    // its own row base + lane is the one of tile h.  Branch-free: rows past N read row N - 1.
-    auto load_codes = [&](uint64_t chunk, uint32_t (&q)[6]) {
-#pragma unroll
-        for (int T = 0; T < 2; T++) {
-            uint64_t row = chunk * M32_ROWS + 32 * T + r32;
-            row = row < N ? row : N - 1;
-            const uint32_t *p = reinterpret_cast<const uint32_t *>(codes + row * MF_D);
-            q[3 * T] = p[0];
-            q[3 * T + 1] = p[1];
-            q[3 * T + 2] = p[2];
-        }
-    };
     const uint32_t ones = h ? 0u : 0x3C003C00u;   // f16 (1, 1) on the n_hi n_lo slots of half 0
     // PRUNE: lane l < ntiles keeps tile l's projection envelope [tlo, thi] (row-sum units)
     const int32_t tlo = PRUNE && lane < (int)ntiles ? g_tint[2 * lane] : 0x7FFFFFFF;
     const int32_t thi = PRUNE && lane < (int)ntiles ? g_tint[2 * lane + 1] : (int32_t)0x80000000;
     const float sx2 = th.sx * th.sx, dsx = (float)MF_D / sx2;
 
-    uint64_t chunk = (uint64_t)blockIdx.x * M32_WAVES + wave;
-    const uint64_t stride = (uint64_t)gridDim.x * M32_WAVES;
-    uint32_t qn[6];
-    load_codes(chunk, qn);
     for (; chunk < nchunks; chunk += stride) {
         const uint64_t base = chunk * M32_ROWS;
         uint32_t q[6];
@@ -527,7 +527,9 @@ __global__ __launch_bounds__(M32_THREADS) void recheck_mf32_kernel(
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
     const unsigned nflag = *flag_cnt;
     const uint32_t ntile_rows = (nflag + 31) / 32;
-    if (blockIdx.x * M32_WAVES >= ntile_rows) return;   // (uniform) no rows for this block
+    // tile-rows go round the blocks first (tr = blockIdx + grid * wave ...): a level's few
+    // hundred tile-rows spread over every CU, not packed 16 to a CU on the first few
+    if (blockIdx.x >= ntile_rows) return;   // (uniform) no rows for this block
     const uint32_t Kp = (K + 31) & ~31u;
     const RcLds L = rc_lds_layout(K);
     const int tid = threadIdx.x;
@@ -553,7 +555,7 @@ __global__ __launch_bounds__(M32_THREADS) void recheck_mf32_kernel(
     const uint32_t ones = h ? 0u : 0x3C003C00u;
     const f32x16 zero16 = {};
     const float scale_t = 1.0f / th.inv_scale;
-    for (uint32_t tr = blockIdx.x * M32_WAVES + wave; tr < ntile_rows; tr += gridDim.x * M32_WAVES) {
+    for (uint32_t tr = blockIdx.x + gridDim.x * wave; tr < ntile_rows; tr += gridDim.x * M32_WAVES) {
         const uint32_t f = tr * 32 + r32;
         const bool valid = f < nflag;
         const uint32_t row = flags[valid ? f : nflag - 1];

@@ -334,13 +334,14 @@ struct KdArgs {
     uint64_t *xsums;     // or: copy 1 of the final sums (move_row_sums; kd_reduce_kernel), else nullptr
 };
 
-// Block b of nb answers ties f = b W + wave, + nb W, ... (waves >= W only help staging).
+// Block b of nb answers ties f = b + nb wave, + nb W, ... (waves >= W only help staging): ties
+// go round the blocks first, so a level's few hundred spread over all nb blocks' CUs.
 // whole_block (W = 1): ties f = b, b + nb, ..., the block's waves compute the tie's K point
 // distances together and wave 0 walks (big K * D: one wave spent most of a tie on them).
 // Uniform per block (it contains __syncthreads); ksm: kd_tree_bytes + W kd_wave_bytes of LDS.
 __device__ inline void kd_resolve_block(const KdArgs &a, unsigned nt, uint32_t b, uint32_t nb, int W, double *ksm,
                                         bool whole_block = false) {
-    if (b * (uint32_t)W >= nt) return;
+    if (b >= nt) return;
     const KdView &kd = a.kd;
     const uint32_t D = a.D, K = a.K;
     const int Z = kd.depth;
@@ -399,7 +400,7 @@ __device__ inline void kd_resolve_block(const KdArgs &a, unsigned nt, uint32_t b
         return;
     }
     if (wave >= W) return;
-    for (unsigned f = b * W + wave; f < nt; f += nb * W) {
+    for (unsigned f = b + nb * wave; f < nt; f += nb * W) {
         const uint32_t row = a.ties[f];
         if (lane < (int)D) xs[lane] = a.lut64[a.codes[(uint64_t)row * a.Dp + lane]];
         wave_lds_sync();
