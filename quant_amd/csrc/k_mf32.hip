@@ -25,6 +25,7 @@
 
 #include "common.hpp"
 #include "mfma_util.hpp"
+#include "kd_walk.hpp"   // RowN, load_row, ref_l2_n
 
 namespace qvq {
 
@@ -634,10 +635,8 @@ __global__ __launch_bounds__(M32_THREADS) void recheck_mf32_kernel(
             const uint32_t n = all ? K : nc;
             double d1 = INFINITY, d2 = INFINITY;
             uint32_t k1 = 0xFFFFFFFFu;
-            for (uint32_t i = 0; i < n; i++) {
-                const uint32_t k = all ? i : cand[r32 * RC_CAP + i];
-                if (k >= K) continue;
-                const double d = ref_l2_hd(x, C64 + (uint64_t)k * MF_D, MF_D);
+            auto take = [&](uint32_t k, double d) {
+                if (k >= K) return;   // padding positions
                 if (d < d1 || (d == d1 && k < k1)) {
                     d2 = d1;
                     d1 = d;
@@ -645,6 +644,17 @@ __global__ __launch_bounds__(M32_THREADS) void recheck_mf32_kernel(
                 } else if (d < d2) {
                     d2 = d;
                 }
+            };
+            // two candidates per trip, both rows' loads in flight together (one round trip each
+            // through L2 was the chain of a row with several candidates)
+            for (uint32_t i = 0; i < n; i += 2) {
+                const uint32_t ka = all ? i : cand[r32 * RC_CAP + i];
+                const bool two = i + 1 < n;
+                const uint32_t kb = two ? (all ? i + 1 : cand[r32 * RC_CAP + i + 1]) : ka;
+                const RowN<MF_D> ra = load_row<MF_D>(C64 + (uint64_t)min(ka, K - 1) * MF_D);
+                const RowN<MF_D> rb = load_row<MF_D>(C64 + (uint64_t)min(kb, K - 1) * MF_D);
+                take(ka, ref_l2_n<MF_D>(x, ra));
+                if (two) take(kb, ref_l2_n<MF_D>(x, rb));
             }
             if (d2 - d1 <= tie_rel * d1) {   // exact tie for the reference: the kd-tree decides
                 ties[atomicAdd(tie_cnt, 1u)] = row;   // A keeps the provisional index
