@@ -377,13 +377,22 @@ __global__ __launch_bounds__(M32_THREADS) void assign_mf32_kernel(
         const bool valid = row < N;
         uint32_t rk = 0;
         if (valid) {
+            // x_d = mu + w_d sx = (mu - 255 sx) + u_d (2 sx) in one fma from the centred byte u,
+            // and ||x - mu||^2 = sx^2 sum_d w_d^2 from the exact integer sum (v_sad_u8 / v_dot4:
+            // sum w^2 = 4 sum u^2 - 1020 sum u + D 255^2): 2 VALU per component instead of 5,
+            // and both within the recompute's error model (one rounding per x_d, two for xn)
             float x[MF_D];
-            float xn = 0.f;   // ||x - mu||^2
+            const uint32_t uq[3] = {own[0] ^ 0x80808080u, own[1] ^ 0x80808080u, own[2] ^ 0x80808080u};
+            const uint32_t su = __builtin_amdgcn_sad_u8(uq[0], 0u, __builtin_amdgcn_sad_u8(uq[1], 0u,
+                                __builtin_amdgcn_sad_u8(uq[2], 0u, 0u)));
+            const uint32_t s2q = __builtin_amdgcn_udot4(uq[0], uq[0], __builtin_amdgcn_udot4(uq[1], uq[1],
+                                 __builtin_amdgcn_udot4(uq[2], uq[2], 0u, false), false), false);
+            const float xn = (float)(int)(4 * s2q - 1020 * su + MF_D * 65025) * (th.sx * th.sx);   // ||x - mu||^2
+            {
+                const float two_sx = 2.f * th.sx, x0 = __fmaf_rn(-255.f, th.sx, th.mu);
 #pragma unroll
-            for (int d = 0; d < MF_D; d++) {
-                const float e = byte_w(own[d / 4], d % 4) * th.sx;
-                xn = __fmaf_rn(e, e, xn);
-                x[d] = e + th.mu;
+                for (int d = 0; d < MF_D; d++)
+                    x[d] = __fmaf_rn((float)((uq[d / 4] >> (8 * (d % 4))) & 0xFF), two_sx, x0);
             }
             // unit = ((tile * NU + q) * 2 + hh): 8-unit q covers rows 16q + 4hh + {0..3, 8..11}
             // of the tile, 4-unit q rows 8q + 4hh + {0..3}
