@@ -711,19 +711,15 @@ hipError_t launch_assign_mfma(hipStream_t s, int grid, bool fuse, const uint8_t 
         // rows per lane: a multiple of 4 covering N over grid x waves x 64 lanes
         const uint32_t copies = fuse ? small_copies(sk) : 1;
         const size_t slds = fuse ? small_lds(sk, copies) : 256;
-        // packed run registers (QVQ_SMALL_PACK=0: one register per component, A/B); QVQ_SMALL_NW:
-        // waves per block (16: 4 per SIMD, 128 VGPRs; 12: 3 per SIMD, 168 VGPRs, no spills)
+        // packed run registers (QVQ_SMALL_PACK=0: one register per component, A/B).  Blocks of 16
+        // waves (4 per SIMD, 13 VGPRs spilled from K = 4): 12-wave blocks without spills (168 VGPRs)
+        // measured 1-10 % slower, also with three row groups in flight (profiles/r03d/ab_small.txt)
         static const bool pack = !(std::getenv("QVQ_SMALL_PACK") && std::getenv("QVQ_SMALL_PACK")[0] == '0');
-        static const int nw = std::getenv("QVQ_SMALL_NW") && std::atoi(std::getenv("QVQ_SMALL_NW")) == 12 ? 12 : 16;
-        const int sw = fuse && pack ? nw : 16;
-        const uint64_t lanes = (uint64_t)grid * sw * 64;
+        const uint64_t lanes = (uint64_t)grid * 16 * 64;
         const uint64_t rpl = ((N + lanes - 1) / lanes + 3) / 4 * 4;
 #define QVQ_SMALL(V)                                                                                              \
     do {                                                                                                          \
-        if (fuse && pack && sw == 12)                                                                             \
-            hipLaunchKernelGGL((assign_small_kernel<V, true, true, 12>), dim3(grid), dim3(12 * 64), slds, s,      \
-                               codes, N, K, E32, plut, th, rpl, copies, A, flags, flag_cnt, part, part_cnt);     \
-        else if (fuse && pack)                                                                                    \
+        if (fuse && pack)                                                                                         \
             hipLaunchKernelGGL((assign_small_kernel<V, true, true, 16>), dim3(grid), dim3(16 * 64), slds, s,      \
                                codes, N, K, E32, plut, th, rpl, copies, A, flags, flag_cnt, part, part_cnt);     \
         else if (fuse)                                                                                            \
