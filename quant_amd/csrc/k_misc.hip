@@ -1078,8 +1078,8 @@ __device__ void prune_order(const float *__restrict__ qproj, uint32_t K2, uint32
     __shared__ float q[PRUNE_MAXK];
     __shared__ float qs[PRUNE_MAXK];   // q by position
     __shared__ uint32_t hist[PRUNE_NB];
-    __shared__ float qr[2][256];
     __shared__ int32_t tlo[PRUNE_MAXT], thi[PRUNE_MAXT];
+    __shared__ uint32_t wtot[4], wlo[4], whi[4];
     const uint32_t tid = threadIdx.x;
     const bool act = tid < 256;
     float mn = INFINITY, mx = -INFINITY;
@@ -1088,37 +1088,38 @@ __device__ void prune_order(const float *__restrict__ qproj, uint32_t K2, uint32
         mn = fminf(mn, q[j]);
         mx = fmaxf(mx, q[j]);
     }
+    // the range of q: DPP wave minima of the floats as order-preserving u32, then the four waves'
+    auto ford = [](float f) {
+        const uint32_t b = __float_as_uint(f);
+        return b ^ ((b >> 31) ? 0xFFFFFFFFu : 0x80000000u);
+    };
+    auto fdec = [](uint32_t u) { return __uint_as_float(u ^ ((u >> 31) ? 0x80000000u : 0xFFFFFFFFu)); };
+    const uint32_t umn = wave_min_u32(ford(mn)), umx = ~wave_min_u32(~ford(mx));
     if (act) {
         hist[tid] = 0;
-        qr[0][tid] = mn;
-        qr[1][tid] = mx;
+        if ((tid & 63) == 0) {
+            wlo[tid >> 6] = umn;
+            whi[tid >> 6] = umx;
+        }
     }
     __syncthreads();
-    for (int w = 128; w > 0; w >>= 1) {
-        if ((int)tid < w) {
-            qr[0][tid] = fminf(qr[0][tid], qr[0][tid + w]);
-            qr[1][tid] = fmaxf(qr[1][tid], qr[1][tid + w]);
-        }
-        __syncthreads();
-    }
-    const float qmin = qr[0][0], inv = (float)PRUNE_NB / (qr[1][0] - qmin + 1.0f);
+    const float qmin = fdec(min(min(wlo[0], wlo[1]), min(wlo[2], wlo[3])));
+    const float qmax = fdec(max(max(whi[0], whi[1]), max(whi[2], whi[3])));
+    const float inv = (float)PRUNE_NB / (qmax - qmin + 1.0f);
     auto bucket = [&](float v) { return min((uint32_t)((v - qmin) * inv), PRUNE_NB - 1); };
     if (act)
         for (uint32_t j = tid; j < K2; j += 256) atomicAdd(&hist[bucket(q[j])], 1u);
     __syncthreads();
-    {   // exclusive scan of the 256 bucket counts (one per thread, Hillis-Steele)
+    {   // exclusive scan of the 256 bucket counts (one per thread): DPP scans within the four
+        // waves, then each wave adds the totals of the waves before it (two barriers, not 16)
         static_assert(PRUNE_NB == 256, "one bucket per thread");
         const uint32_t own = act ? hist[tid] : 0u;
-        uint32_t v = own;
-        for (uint32_t off = 1; off < PRUNE_NB; off <<= 1) {
-            __syncthreads();
-            const uint32_t add = act && tid >= off ? hist[tid - off] : 0u;
-            __syncthreads();
-            v += add;
-            if (act) hist[tid] = v;
-        }
+        const uint32_t inc = wave_scan_add(own);
+        if (act && (tid & 63) == 63) wtot[tid >> 6] = inc;
         __syncthreads();
-        if (act) hist[tid] = v - own;
+        uint32_t pre = 0;
+        for (uint32_t w = 0; act && w < (tid >> 6); w++) pre += wtot[w];
+        if (act) hist[tid] = pre + inc - own;
     }
     __syncthreads();
     if (act) {
@@ -1143,25 +1144,26 @@ __device__ void prune_order(const float *__restrict__ qproj, uint32_t K2, uint32
     }
     // Tiles sharing a bucket can overlap out of order: monotone envelopes (lo: the suffix
     // minimum, hi: the prefix maximum; still bounds of every tile), so that the tiles a bound
-    // admits form one contiguous range.  Hillis-Steele over nt <= 128 entries.
-    for (uint32_t off = 1; off < nt; off <<= 1) {
-        __syncthreads();
-        int32_t m = 0, M = 0;
-        if (act && tid < nt) {
-            m = tid + off < nt ? min(tlo[tid], tlo[tid + off]) : tlo[tid];
-            M = tid >= off ? max(thi[tid], thi[tid - off]) : thi[tid];
-        }
-        __syncthreads();
-        if (act && tid < nt) {
-            tlo[tid] = m;
-            thi[tid] = M;
-        }
+    // admits form one contiguous range.  DPP max-scans over nt <= 128 entries in two waves (the
+    // lows in reversed tile order, mapped so that a smaller int is a larger u32; 0 is the
+    // neutral value of both maps, as INT_MAX / INT_MIN are of the envelopes).
+    __syncthreads();
+    const int r = (int)nt - 1 - (int)tid;   // this thread's tile for the suffix scan
+    uint32_t hm = act && tid < nt ? (uint32_t)thi[tid] ^ 0x80000000u : 0u;
+    uint32_t lm = act && r >= 0 ? ~((uint32_t)tlo[r] ^ 0x80000000u) : 0u;
+    hm = wave_scan_max(hm);
+    lm = wave_scan_max(lm);
+    if (act && (tid & 63) == 63) {
+        whi[tid >> 6] = hm;
+        wlo[tid >> 6] = lm;
     }
     __syncthreads();
-    if (act && tid < nt) {
-        tint[2 * tid] = tlo[tid];
-        tint[2 * tid + 1] = thi[tid];
+    for (uint32_t w = 0; act && w < (tid >> 6); w++) {
+        hm = max(hm, whi[w]);
+        lm = max(lm, wlo[w]);
     }
+    if (act && tid < nt) tint[2 * tid + 1] = (int32_t)(hm ^ 0x80000000u);
+    if (act && r >= 0) tint[2 * r] = (int32_t)(~lm ^ 0x80000000u);
 }
 
 __device__ inline uint32_t fin_rows(const FinArgs &a) { return a.split ? max(2 * a.K, a.Kpad_next) : a.K; }
@@ -1229,7 +1231,8 @@ __global__ __launch_bounds__(256) void finalize_prep_kernel(FinArgs a, double *_
     for (uint32_t j0 = blockIdx.x * per; j0 < n; j0 += gridDim.x * per) term += finalize_item(a, j0 + r, d, L);
     if (!done) return;
     __shared__ double red[256];
-    finalize_block_done(a, term, red, dist_part, done, dist_out, ready, seq);
+    // (the distortion's block tree only on the level that returns it: 8 barriers fewer elsewhere)
+    finalize_block_done(a, term, a.dist ? red : nullptr, dist_part, done, dist_out, ready, seq);
 }
 
 static FinArgs fin_args(const uint64_t *sums, uint32_t K, uint32_t D, uint32_t Dp, int64_t R, int64_t bias,
