@@ -218,7 +218,8 @@ hipError_t launch_assign_mfma(hipStream_t s, int grid, bool fuse, const uint8_t 
                               const uint64_t *plut,
                               const MfThresholds &th, uint32_t *A, uint32_t *flags, unsigned *flag_cnt,
                               uint64_t *part, uint32_t *part_cnt, const uint32_t *perm = nullptr,
-                              const int32_t *tint = nullptr);
+                              const int32_t *tint = nullptr, uint64_t *z1 = nullptr, uint32_t nz1 = 0);
+// (z1, nz1: fused searches also clear these nz1 u64 -- copy 1 of the final sums -- spread over the grid)
 // The same search on v_mfma_f32_32x32x16_f16 tiles (k_mf32.hip); launch_assign_mfma uses it
 // for K above the small-K scan whenever mf32_fits.
 bool mf32_fits(uint32_t K, bool fuse);
@@ -227,7 +228,8 @@ hipError_t launch_assign_mf32(hipStream_t s, int grid, bool fuse, const uint8_t 
                               const _Float16 *cb_rows, uint32_t K, const float *C32, const uint64_t *plut,
                               const MfThresholds &th, uint32_t *A, uint32_t *flags, unsigned *flag_cnt,
                               uint64_t *part, uint32_t *part_cnt, const uint32_t *perm = nullptr,
-                              const int32_t *tint = nullptr);
+                              const int32_t *tint = nullptr,
+                              uint64_t *z1 = nullptr, uint32_t nz1 = 0);
 constexpr uint32_t PRUNE_MAXK_HOST = 4096;   // prune_order's capacity (k_misc.hip PRUNE_MAXK)
 // d_tint: the envelopes (2 int32 per tile, PRUNE_MAXK_HOST / 32 tiles), then Kpad floats of
 // projections (finalize -> prune_order)

@@ -718,10 +718,14 @@ qvq_status run_level(qvq_ctx *ctx, uint32_t K, int slot, bool sums_out, const do
     if (timing) HIPCHK(hipEventRecord(ctx->ev[slot][0], ctx->stream));
     if (use_mfma(ctx, K)) {
         const bool prune = ctx->perm_k == K;   // the order qvq_lbg's finalize left for this level
+        // one rank, fused sums: the search clears copy 1 of the final sums (the kd ties' moves,
+        // added by the previous level's finalize), covering every smaller level's layout
+        const bool clear1 = fused && kd_merge(ctx);
         HIPCHK(launch_assign_mfma(ctx->stream, ctx->num_cu, fused, ctx->d_codes, ctx->N, ctx->d_rows, ctx->d_E32, K,
                                   ctx->d_C32, ctx->d_plut, ctx->mf_th, ctx->d_A, ctx->d_flags, &cnt[0],
                                   ctx->d_part, ctx->d_part_cnt, prune ? ctx->d_perm : nullptr,
-                                  prune ? ctx->d_tint : nullptr));
+                                  prune ? ctx->d_tint : nullptr, clear1 ? ctx->d_sums + sums_cap_stride(ctx) : nullptr,
+                                  clear1 ? (uint32_t)(2 * (uint64_t)K * ctx->D + K) : 0u));
     } else if (use_wide(ctx, K)) {
         const bool prune = ctx->perm_k == K;
         HIPCHK(launch_assign_wide(ctx->stream, ctx->num_cu, ctx->Dp, ctx->D, ctx->d_codes, ctx->N, ctx->d_rows, K,
@@ -1215,7 +1219,7 @@ QVQ_API qvq_status qvq_lbg(qvq_ctx *ctx, uint32_t bits, double eps, double *code
                                     ctx->d_C32, ctx->d_rows, ctx->d_E32, split ? ctx->dh_cb : nullptr, d_dist + 8,
                                     dist_done,
                                     split ? nullptr : d_dist + 2, split ? ctx->dh_ready : nullptr, ctx->seq,
-                                    K == 1 || copies > 1, K == 1 ? MEAN_COPIES : copies,
+                                    K == 1, K == 1 ? MEAN_COPIES : copies,
                                     prune ? ctx->d_perm : nullptr, prune ? ctx->d_tint : nullptr, K == 1 ? 0 : 1,
                                     copies > 1 ? sums_cap_stride(ctx) : 0,
                                     gate);

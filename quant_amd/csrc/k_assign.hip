@@ -483,7 +483,7 @@ __global__ __launch_bounds__(NW * 64) void assign_small_kernel(
     const uint8_t *__restrict__ codes, uint64_t N, uint32_t K, const float *__restrict__ g_E32,
     const uint64_t *__restrict__ g_plut, MfThresholds th, uint64_t rows_per_lane, uint32_t copies,
     uint32_t *__restrict__ A, uint32_t *__restrict__ flags, unsigned *__restrict__ flag_cnt,
-    uint64_t *__restrict__ part, uint32_t *__restrict__ part_cnt) {
+    uint64_t *__restrict__ part, uint32_t *__restrict__ part_cnt, uint64_t *__restrict__ z1, uint32_t nz1) {
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
     // LDS: lo8 (256 B, first: a byte's lookup address is the byte itself, no base add) | C
     // copies of the sums, copy c = [d][k] (SK*D u64) then counts [k] (SK u64), stride
@@ -527,6 +527,8 @@ __global__ __launch_bounds__(NW * 64) void assign_small_kernel(
             for (uint32_t i = tid; i < 2 * K * MF_D; i += (NW * 64)) part[(uint64_t)gridDim.x * K * MF_D + i] = 0;
             for (uint32_t i = tid; i < 2 * K; i += (NW * 64)) part_cnt[(uint64_t)gridDim.x * K + i] = 0;
         }
+        // copy 1 of the final sums (assign_mf32_kernel's note)
+        for (uint32_t i = blockIdx.x * (NW * 64) + tid; i < nz1; i += gridDim.x * (NW * 64)) z1[i] = 0;
     }
     __syncthreads();
     uint64_t *mine = cps + (size_t)((tid & 63) % copies) * S;
@@ -698,7 +700,9 @@ hipError_t launch_assign_mfma(hipStream_t s, int grid, bool fuse, const uint8_t 
                               const _Float16 *cb_rows, const float *E32, uint32_t K, const float *C32,
                               const uint64_t *plut,
                               const MfThresholds &th, uint32_t *A, uint32_t *flags, unsigned *flag_cnt,
-                              uint64_t *part, uint32_t *part_cnt, const uint32_t *perm, const int32_t *tint) {
+                              uint64_t *part, uint32_t *part_cnt, const uint32_t *perm, const int32_t *tint,
+                              uint64_t *z1, uint32_t nz1) {
+    if (!fuse) z1 = nullptr, nz1 = 0;   // (cleared by the fused kernels' set-up only)
     static const bool no_stage = std::getenv("QVQ_NOSTAGE") != nullptr;   // ablation
     const bool staged = mf_lds_layout(K, fuse, true).total <= MF_LDS_MAX && (!no_stage || K <= mf_small_k());
     const size_t lds = mf_lds_layout(K, fuse, staged).total;
@@ -721,13 +725,16 @@ hipError_t launch_assign_mfma(hipStream_t s, int grid, bool fuse, const uint8_t 
     do {                                                                                                          \
         if (fuse && pack)                                                                                         \
             hipLaunchKernelGGL((assign_small_kernel<V, true, true, 16>), dim3(grid), dim3(16 * 64), slds, s,      \
-                               codes, N, K, E32, plut, th, rpl, copies, A, flags, flag_cnt, part, part_cnt);     \
+                               codes, N, K, E32, plut, th, rpl, copies, A, flags, flag_cnt, part, part_cnt, z1,  \
+                               nz1);                                                                      \
         else if (fuse)                                                                                            \
             hipLaunchKernelGGL((assign_small_kernel<V, true, false, 16>), dim3(grid), dim3(16 * 64), slds, s,     \
-                               codes, N, K, E32, plut, th, rpl, copies, A, flags, flag_cnt, part, part_cnt);     \
+                               codes, N, K, E32, plut, th, rpl, copies, A, flags, flag_cnt, part, part_cnt, z1,  \
+                               nz1);                                                                      \
         else                                                                                                      \
             hipLaunchKernelGGL((assign_small_kernel<V, false, false, 16>), dim3(grid), dim3(16 * 64), slds, s,    \
-                               codes, N, K, E32, plut, th, rpl, copies, A, flags, flag_cnt, part, part_cnt);     \
+                               codes, N, K, E32, plut, th, rpl, copies, A, flags, flag_cnt, part, part_cnt, z1,  \
+                               nz1);                                                                      \
     } while (0)
         switch (sk) {
         case 2: QVQ_SMALL(2); break;
@@ -743,7 +750,11 @@ hipError_t launch_assign_mfma(hipStream_t s, int grid, bool fuse, const uint8_t 
     static const bool mf32 = !(std::getenv("QVQ_MF32") && std::getenv("QVQ_MF32")[0] == '0');
     if (mf32 && mf32_fits(K, fuse))
         return launch_assign_mf32(s, grid, fuse, codes, N, cb_rows, K, C32, plut, th, A, flags, flag_cnt, part,
-                                  part_cnt, perm, tint);
+                                  part_cnt, perm, tint, z1, nz1);
+    if (nz1) {   // the 16x16x32 form (ablation) does not clear copy 1 itself
+        const hipError_t e = hipMemsetAsync(z1, 0, (size_t)nz1 * 8, s);
+        if (e != hipSuccess) return e;
+    }
     // 4-code-vector units while the pair loop is short (the recompute dominates): up to
     // K = QVQ_U4_MAXK (default 256)
     static const uint32_t u4_max = std::getenv("QVQ_U4_MAXK") ? (uint32_t)std::atoi(std::getenv("QVQ_U4_MAXK")) : 256;

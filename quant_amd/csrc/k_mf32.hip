@@ -145,7 +145,8 @@ __global__ __launch_bounds__(M32_THREADS) void assign_mf32_kernel(
     const float *__restrict__ g_C32, const uint64_t *__restrict__ g_plut, MfThresholds th, uint32_t idbits,
     float orrel, uint32_t *__restrict__ A, uint32_t *__restrict__ flags, unsigned *__restrict__ flag_cnt,
     uint64_t *__restrict__ part, uint32_t *__restrict__ part_cnt, uint32_t copies,
-    const uint32_t *__restrict__ g_perm, const int32_t *__restrict__ g_tint) {
+    const uint32_t *__restrict__ g_perm, const int32_t *__restrict__ g_tint, uint64_t *__restrict__ z1,
+    uint32_t nz1) {
     static_assert(U == 4 || U == 8, "unit of 4 or 8 code vectors");
     constexpr int NU = 16 / U;   // units per lane and code tile
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
@@ -198,6 +199,9 @@ __global__ __launch_bounds__(M32_THREADS) void assign_mf32_kernel(
             for (uint32_t i = tid; i < 2 * K * MF_D; i += M32_THREADS) part[(uint64_t)gridDim.x * K * MF_D + i] = 0;
             for (uint32_t i = tid; i < 2 * K; i += M32_THREADS) part_cnt[(uint64_t)gridDim.x * K + i] = 0;
         }
+        // copy 1 of the final sums (the kd ties' moves, kd_reduce_kernel), spread over the grid:
+        // the finalize that added it no longer clears it in one block
+        for (uint32_t i = blockIdx.x * M32_THREADS + tid; i < nz1; i += gridDim.x * M32_THREADS) z1[i] = 0;
     }
     __syncthreads();
     const float *C32 = STAGED ? c32s : g_C32;
@@ -707,9 +711,9 @@ static void launch_mf32_variant(hipStream_t s, int grid, size_t lds, const uint8
                                 const _Float16 *cb_rows, uint32_t K, const float *C32, const uint64_t *plut,
                                 const MfThresholds &th, uint32_t idbits, float orrel, uint32_t *A, uint32_t *flags,
                                 unsigned *flag_cnt, uint64_t *part, uint32_t *part_cnt, uint32_t copies,
-                                const uint32_t *perm, const int32_t *tint) {
+                                const uint32_t *perm, const int32_t *tint, uint64_t *z1, uint32_t nz1) {
     hipLaunchKernelGGL((assign_mf32_kernel<F, S, U, TAG, P>), dim3(grid), dim3(M32_THREADS), lds, s, codes, N, cb_rows,
-                       K, C32, plut, th, idbits, orrel, A, flags, flag_cnt, part, part_cnt, copies, perm, tint);
+                       K, C32, plut, th, idbits, orrel, A, flags, flag_cnt, part, part_cnt, copies, perm, tint, z1, nz1);
 }
 
 bool mf32_fits(uint32_t K, bool fuse) { return m32_lds_layout(K, fuse, false).total <= M32_LDS_MAX; }
@@ -721,8 +725,10 @@ bool mf32_prune_fits(uint32_t K, bool fuse) {
 hipError_t launch_assign_mf32(hipStream_t s, int grid, bool fuse, const uint8_t *codes, uint64_t N,
                               const _Float16 *cb_rows, uint32_t K, const float *C32, const uint64_t *plut,
                               const MfThresholds &th, uint32_t *A, uint32_t *flags, unsigned *flag_cnt,
-                              uint64_t *part, uint32_t *part_cnt, const uint32_t *perm, const int32_t *tint) {
+                              uint64_t *part, uint32_t *part_cnt, const uint32_t *perm, const int32_t *tint,
+                              uint64_t *z1, uint32_t nz1) {
     if (!mf32_fits(K, fuse)) return hipErrorInvalidValue;
+    if (!fuse) z1 = nullptr, nz1 = 0;   // (cleared in the fused set-up block only)
     const bool prune = perm && tint;
     if (prune && !mf32_prune_fits(K, fuse)) return hipErrorInvalidValue;
     const bool staged = m32_lds_layout(K, fuse, true, 1, prune).total <= M32_LDS_MAX;
@@ -749,7 +755,7 @@ hipError_t launch_assign_mf32(hipStream_t s, int grid, bool fuse, const uint8_t 
     const float orrel = std::ldexp(1.0f, (int)idbits - 22);
     using Fn = void (*)(hipStream_t, int, size_t, const uint8_t *, uint64_t, const _Float16 *, uint32_t, const float *,
                         const uint64_t *, const MfThresholds &, uint32_t, float, uint32_t *, uint32_t *, unsigned *,
-                        uint64_t *, uint32_t *, uint32_t, const uint32_t *, const int32_t *);
+                        uint64_t *, uint32_t *, uint32_t, const uint32_t *, const int32_t *, uint64_t *, uint32_t);
 #define QVQ_MF32_PICK(TG)                                                                                          \
     if (fuse) {                                                                                                    \
         if (u4) fn = staged ? launch_mf32_variant<true, true, 4, TG> : launch_mf32_variant<true, false, 4, TG>;    \
@@ -770,7 +776,7 @@ hipError_t launch_assign_mf32(hipStream_t s, int grid, bool fuse, const uint8_t 
 #undef QVQ_MF32_PICK
     if (!(prune && !u4 && idbits <= 12)) perm = nullptr, tint = nullptr;   // (the unpruned order: identity)
     fn(s, grid, lds, codes, N, cb_rows, K, C32, plut, th, idbits, orrel, A, flags, flag_cnt, part, part_cnt, copies, perm,
-       tint);
+       tint, z1, nz1);
     return hipGetLastError();
 }
 
