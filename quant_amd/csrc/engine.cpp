@@ -408,7 +408,7 @@ qvq_status ensure_levels(qvq_ctx *ctx, uint32_t Kmax) {
     HIPCHK(hipMalloc(&ctx->d_part, (uint64_t)(ctx->G + 2) * KD * 8));
     HIPCHK(hipMalloc(&ctx->d_part_cnt, (uint64_t)(ctx->G + 2) * Kmax * 4));
     // two copies of the final sums: copy 1 takes the kd-tree ties' moves (kd_reduce_kernel) and
-    // is zero between levels (the finalize that adds it clears it)
+    // is cleared, over the level's region, by each fused search before the level's kd_reduce
     HIPCHK(hipMalloc(&ctx->d_sums, 2 * (2 * KD + Kmax) * 8));
     HIPCHK(hipMemset(ctx->d_sums, 0, 2 * (2 * KD + Kmax) * 8));
     ctx->sums_bytes = 2 * (2 * KD + Kmax) * 8;
@@ -1208,7 +1208,7 @@ QVQ_API qvq_status qvq_lbg(qvq_ctx *ctx, uint32_t bits, double eps, double *code
         HIPCHK(hipMemsetAsync(ctx->d_sums, 0, ctx->sums_bytes, ctx->stream));
         ctx->sums1_dirty = false;
     }
-    // copies 2: copy 1 holds the ties' moves (added, then cleared by the finalize's last block)
+    // copies 2: copy 1 holds the ties' moves (added here; the next level's search clears it)
     auto finalize = [&](uint32_t K, bool split, uint32_t copies = 1, const unsigned *gate = nullptr) {
         if (split) ctx->seq++;
         const bool prune = split && use_prune(ctx, 2 * K);   // the next search's tile order
