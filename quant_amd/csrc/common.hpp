@@ -197,6 +197,15 @@ __device__ inline void reduce_columns_block(const uint64_t *__restrict__ part, c
     }
 }
 
+// Rows the kd-tree answers: their best two fp64 distances are within tie_rel relative (ties of
+// the reference's own arithmetic), or close enough that the reference's centroid bits -- which
+// may differ from the exact sums' by tie_abs / (2 sqrt(D)) per component -- can decide them
+// (DESIGN.md 3.8): |d' - d| <= tie_abs sqrt(d) + tie_abs^2 / 2 for each distance.
+__host__ __device__ inline bool in_tie_band(double d1, double d2, double tie_rel, double tie_abs) {
+    const double band = tie_abs * (sqrt(d1) + sqrt(d2)) + tie_abs * tie_abs;
+    return d2 - d1 <= tie_rel * d1 || d2 - d1 <= band;
+}
+
 struct MfThresholds {
     float mfma, alpha, beta, gamma;
     float inv_scale;   // 2^-t
@@ -254,7 +263,7 @@ hipError_t launch_assign_wide(hipStream_t s, int num_cu, uint32_t Dp, uint32_t D
 // and its count to xcnt [k] (the search's extra slab G).
 hipError_t launch_recheck(hipStream_t s, int num_cu, const uint8_t *codes, uint32_t Dp, uint32_t D,
                           const uint32_t *flags, const unsigned *flag_cnt, const double *C64, const float *C32,
-                          uint32_t K, const double *lut64, float alpha, float beta, float gamma, double tie_rel,
+                          uint32_t K, const double *lut64, float alpha, float beta, float gamma, double tie_rel, double tie_abs,
                           uint32_t *A, uint32_t *ties, unsigned *tie_cnt, uint64_t *xslab, uint32_t *xcnt,
                           const uint64_t *plut,
                           const uint32_t *perm = nullptr, const int32_t *tint = nullptr, float qscale = 0.f);
@@ -263,7 +272,7 @@ hipError_t launch_recheck(hipStream_t s, int num_cu, const uint8_t *codes, uint3
 bool recheck_mf32_fits(uint32_t K);
 hipError_t launch_recheck_mf32(hipStream_t s, int num_cu, const uint8_t *codes, const uint32_t *flags,
                                const unsigned *flag_cnt, const _Float16 *cb_rows, const double *C64, uint32_t K,
-                               const double *lut64, const MfThresholds &th, double tie_rel, uint32_t *A,
+                               const double *lut64, const MfThresholds &th, double tie_rel, double tie_abs, uint32_t *A,
                                uint32_t *ties, unsigned *tie_cnt, uint64_t *xslab, uint32_t *xcnt,
                                const uint64_t *plut);
 // Device kd-tree answers for the listed ties (tree image in mapped host memory); adds their
@@ -351,4 +360,30 @@ hipError_t launch_exact_distortion(hipStream_t s, const double *X, uint64_t N, u
 hipError_t launch_exact_gather(hipStream_t s, const double *X, uint32_t D, const uint32_t *rows, uint32_t n,
                                double *out);
 hipError_t launch_exact_fix(hipStream_t s, uint32_t *A, const uint32_t *rows, const uint32_t *vals, uint32_t n);
+// The reference's Kahan centroids on the device (k_kahan.hip, kahan_par.hpp): scratch for one
+// computation over N rows and K cells (KahanWork::caps sizes the function tables).
+struct KahanWork {
+    uint32_t L = 128, S = 32;          // steps per segment, segments per group (groups per supergroup)
+    uint32_t *keys = nullptr, *iota = nullptr, *order = nullptr;   // [N] each (sort)
+    void *temp = nullptr;
+    size_t temp_bytes = 0;
+    uint32_t *koff = nullptr;          // [K + 1]
+    uint32_t *off = nullptr;           // [3][K + 1]
+    uint8_t *planes = nullptr;         // [D][N]
+    void *fn0 = nullptr, *fn1 = nullptr, *fn2 = nullptr;   // [D][NS], [D][NG], [D][NU] functions
+    void *P0 = nullptr, *Etr = nullptr;                    // [D][NS] 128-bit states
+    unsigned *stats = nullptr;         // [3] table misses (segments, groups, supergroups)
+    uint64_t n_cap = 0;
+    uint32_t k_cap = 0, d_cap = 0;
+    static size_t fn_bytes();
+    static void caps(uint64_t N, uint32_t K, uint32_t L, uint32_t S, uint32_t &NS, uint32_t &NG, uint32_t &NU);
+};
+size_t kahan_sort_temp_bytes(uint64_t N);
+// C [K][D] = the reference's centroids of assignment A (nullptr: K = 1, the mean of every row):
+// Kahan sums in ascending row order times fl(1/n), empty cells 0.  Xt[b] = value of byte b in
+// units of 2^-60 (SCALED).  With split_out also the split [2K][D] (x1.2 | x0.8).  passes 2: a
+// trusted walk re-estimates the segment tables' states first (fewer table misses).
+hipError_t launch_kahan_centroids(hipStream_t s, const KahanWork &w, const uint8_t *codes, uint32_t Dp, uint32_t D,
+                                  uint64_t N, const uint32_t *A, uint32_t K, const uint64_t *Xt, double *C,
+                                  double *split_out, int passes);
 }  // namespace qvq

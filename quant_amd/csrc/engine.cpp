@@ -100,6 +100,16 @@ struct qvq_ctx {
     double *d_lut64 = nullptr;
     uint64_t *d_plut = nullptr;
     uint32_t *d_A = nullptr, *d_flags = nullptr, *d_ties = nullptr;
+    // the previous level's final assignment (qvq_lbg swaps the two each level): the input of
+    // the reference-bit (Kahan) centroids a level with kd-tree ties needs
+    uint32_t *d_A_alt = nullptr;
+    KahanWork kw;
+    uint64_t *d_kx = nullptr;      // byte -> value in units of 2^-60 (SCALED)
+    double *d_kc_cent = nullptr, *d_kc_split = nullptr;   // Kahan centroids [K/2][D], their split [K][D]
+    uint32_t kc_kcap = 0;
+    std::vector<double> h_kc_split;   // host copy of the split for the tree build
+    uint64_t pub_seq = 0;          // per-level tie-count publications (h_ready[1] = seq, h_ready[2] = ties)
+    double tie_abs = 0;            // the recheck's absolute tie band: centroid bits may differ by this much
     unsigned *d_counters = nullptr;   // per level: [2l] flagged rows, [2l+1] kd-tree ties; [66], [67] block counters;
                                       // [68], [69] the pruned wide search's task counters (SCHED_COUNTERS)
     uint64_t *d_hist = nullptr;       // byte histogram [256] | its all-reduced copy [256]
@@ -250,7 +260,34 @@ bool use_prune(const qvq_ctx *ctx, uint32_t K) {
     return wmink && K >= wmink && use_wide(ctx, K) && wide_prune_fits(ctx->Dp, K);
 }
 
+void free_kahan(qvq_ctx *ctx) {
+    KahanWork &w = ctx->kw;
+    dfree(w.keys);
+    dfree(w.iota);
+    dfree(w.order);
+    if (w.temp) (void)hipFree(w.temp);
+    w.temp = nullptr;
+    w.temp_bytes = 0;
+    dfree(w.koff);
+    dfree(w.off);
+    dfree(w.planes);
+    if (w.fn0) (void)hipFree(w.fn0);
+    if (w.fn1) (void)hipFree(w.fn1);
+    if (w.fn2) (void)hipFree(w.fn2);
+    if (w.P0) (void)hipFree(w.P0);
+    if (w.Etr) (void)hipFree(w.Etr);
+    w.fn0 = w.fn1 = w.fn2 = w.P0 = w.Etr = nullptr;
+    dfree(w.stats);
+    w.n_cap = 0;
+    w.k_cap = w.d_cap = 0;
+    dfree(ctx->d_kc_cent);
+    dfree(ctx->d_kc_split);
+    ctx->kc_kcap = 0;
+}
+
 void free_training(qvq_ctx *ctx) {
+    free_kahan(ctx);
+    dfree(ctx->d_A_alt);
     dfree(ctx->d_X64);
     dfree(ctx->d_ex_keys);
     dfree(ctx->d_ex_iota);
@@ -388,6 +425,16 @@ qvq_status alloc_training(qvq_ctx *ctx, uint64_t N, uint32_t D, int cs) {
     HIPCHK(hipMemcpy(ctx->d_w, ctx->terms.w, sizeof(ctx->terms.w), hipMemcpyHostToDevice));
     HIPCHK(hipMemcpy(ctx->d_lut64, ctx->terms.v64, sizeof(ctx->terms.v64), hipMemcpyHostToDevice));
     HIPCHK(hipMemcpy(ctx->d_plut, plut, sizeof(plut), hipMemcpyHostToDevice));
+    // SCALED values in units of 2^-60 for the Kahan chains; NORMAL values are integers, whose
+    // Kahan sums are exact (the centroids' bits are the exact sums' already)
+    uint64_t kx[256];
+    for (int b = 0; b < 256; b++) kx[b] = cs == QVQ_CS_SCALED ? (uint64_t)std::ldexp(ctx->terms.v64[b], 60) : 0;
+    HIPCHK(hipMemcpy(ctx->d_kx, kx, sizeof(kx), hipMemcpyHostToDevice));
+    // the band of rows whose answer can depend on the centroids' last bits:
+    // |c_kahan - c_exact| <= delta per component, so a distance moves by at most
+    // 2 delta sqrt(D) sqrt(d) + D delta^2
+    const double delta = cs == QVQ_CS_SCALED ? std::ldexp(1.0, -49) : 0.0;
+    ctx->tie_abs = 2 * delta * std::sqrt((double)D);
     return QVQ_OK;
 }
 
@@ -511,6 +558,66 @@ qvq_status run_update(qvq_ctx *ctx, const uint32_t *d_A, uint32_t K) {
     qvq_status st = run_update_slabs(ctx, d_A, K);
     if (st != QVQ_OK) return st;
     if (ctx->nslabs) HIPCHK(launch_reduce(ctx->stream, ctx->d_part, ctx->d_part_cnt, ctx->nslabs, 0, K, ctx->D, ctx->d_sums));
+    return QVQ_OK;
+}
+
+// Reference-bit ties on one rank: each level publishes its tie count, and a
+// level with ties recomputes the previous level's centroids with the reference's Kahan sums
+// before the kd-tree answers them.  QVQ_KAHAN=0: the exact-sum codebook answers them (A/B).
+bool kahan_mode(const qvq_ctx *ctx) {
+    static const bool off = env_is("QVQ_KAHAN", "0");
+    return !off && !ctx->comm && !ctx->host_ar && !ctx->exact;
+}
+
+qvq_status ensure_kahan(qvq_ctx *ctx, uint32_t Kc) {
+    KahanWork &w = ctx->kw;
+    const uint64_t N = ctx->N;
+    const uint32_t D = ctx->D;
+    if (ctx->kc_kcap < Kc) {
+        dfree(ctx->d_kc_cent);
+        dfree(ctx->d_kc_split);
+        HIPCHK(hipMalloc(&ctx->d_kc_cent, (uint64_t)Kc * D * 8));
+        HIPCHK(hipMalloc(&ctx->d_kc_split, 2ull * Kc * D * 8));
+        ctx->kc_kcap = Kc;
+    }
+    if (w.n_cap == N && w.k_cap >= Kc && w.d_cap == D) return QVQ_OK;
+    const uint32_t kcap = std::max(Kc, w.k_cap);
+    const uint32_t L = w.L, S = w.S;
+    {   // keep the sizes, free the buffers
+        dfree(w.keys);
+        dfree(w.iota);
+        dfree(w.order);
+        if (w.temp) (void)hipFree(w.temp);
+        dfree(w.koff);
+        dfree(w.off);
+        dfree(w.planes);
+        for (void **p : {&w.fn0, &w.fn1, &w.fn2, &w.P0, &w.Etr})
+            if (*p) (void)hipFree(*p), *p = nullptr;
+        dfree(w.stats);
+        w.temp = nullptr;
+    }
+    uint32_t NS, NG, NU;
+    KahanWork::caps(N, kcap, L, S, NS, NG, NU);
+    w.temp_bytes = std::max<size_t>(kahan_sort_temp_bytes(N), 16);
+    HIPCHK(hipMalloc(&w.keys, N * 4));
+    HIPCHK(hipMalloc(&w.iota, N * 4));
+    HIPCHK(hipMalloc(&w.order, N * 4));
+    HIPCHK(hipMalloc(&w.temp, w.temp_bytes));
+    HIPCHK(hipMalloc(&w.koff, ((uint64_t)kcap + 1) * 4));
+    HIPCHK(hipMalloc(&w.off, 3 * ((uint64_t)kcap + 1) * 4));
+    HIPCHK(hipMalloc(&w.planes, N * D));
+    const size_t fb = KahanWork::fn_bytes();
+    HIPCHK(hipMalloc(&w.fn0, (uint64_t)D * NS * fb));
+    HIPCHK(hipMalloc(&w.fn1, (uint64_t)D * NG * fb));
+    HIPCHK(hipMalloc(&w.fn2, (uint64_t)D * NU * fb));
+    HIPCHK(hipMalloc(&w.P0, (uint64_t)D * NS * 16));
+    HIPCHK(hipMalloc(&w.Etr, (uint64_t)D * NS * 16));
+    HIPCHK(hipMalloc(&w.stats, 4 * sizeof(unsigned)));
+    HIPCHK(hipMemset(w.stats, 0, 4 * sizeof(unsigned)));
+    HIPCHK(launch_exact_iota(ctx->stream, w.iota, N));
+    w.n_cap = N;
+    w.k_cap = kcap;
+    w.d_cap = D;
     return QVQ_OK;
 }
 
@@ -698,7 +805,8 @@ bool kd_merge(const qvq_ctx *ctx) {
     return on && !ctx->comm && !ctx->host_ar && !(abl_skip() & 4);
 }
 
-qvq_status run_level(qvq_ctx *ctx, uint32_t K, int slot, bool sums_out, const double *hC, uint64_t wait_seq) {
+qvq_status run_level(qvq_ctx *ctx, uint32_t K, int slot, bool sums_out, const double *hC, uint64_t wait_seq,
+                     bool defer_ties = false) {
     const bool fused = sums_out && use_fused(ctx, K);
     ctx->kd_pend = false;
     ctx->sums_copies = 1;
@@ -749,24 +857,34 @@ qvq_status run_level(qvq_ctx *ctx, uint32_t K, int slot, bool sums_out, const do
     if (abl_skip() & 1) {
     } else if (rc_mf32 && K >= rc_min_k && use_mfma(ctx, K) && recheck_mf32_fits(K)) {
         HIPCHK(launch_recheck_mf32(ctx->stream, ctx->num_cu, ctx->d_codes, ctx->d_flags, &cnt[0], ctx->d_rows,
-                                   ctx->d_C64_split, K, ctx->d_lut64, ctx->mf_th, 1e-12, ctx->d_A, ctx->d_ties,
+                                   ctx->d_C64_split, K, ctx->d_lut64, ctx->mf_th, 1e-12, ctx->tie_abs, ctx->d_A, ctx->d_ties,
                                    &cnt[1], xslab, xcnt, ctx->d_plut));
     } else {
         float alpha, beta, gamma;
         valu_coeffs(ctx, alpha, beta, gamma);
         const bool pruned = ctx->perm_k == K;   // the search's order is valid for the recheck too
         HIPCHK(launch_recheck(ctx->stream, ctx->num_cu, ctx->d_codes, ctx->Dp, ctx->D, ctx->d_flags, &cnt[0],
-                              ctx->d_C64_split, ctx->d_C32, K, ctx->d_lut64, alpha, beta, gamma, 1e-12, ctx->d_A,
+                              ctx->d_C64_split, ctx->d_C32, K, ctx->d_lut64, alpha, beta, gamma, 1e-12, ctx->tie_abs, ctx->d_A,
                               ctx->d_ties, &cnt[1], xslab, xcnt, ctx->d_plut, pruned ? ctx->d_perm : nullptr,
                               pruned ? ctx->d_tint : nullptr,
                               (float)((double)ctx->D / (ctx->terms.sx * ctx->terms.sx))));
     }
     qvq_status st;
+    if (defer_ties) {   // the level's tie count to the host, before the rest of the level runs
+        ctx->pub_seq++;
+        HIPCHK(launch_copy_out(ctx->stream, &cnt[1], reinterpret_cast<uint8_t *>(ctx->dh_ready) + 16, 4, nullptr,
+                               nullptr, 0, nullptr, nullptr, 0, ctx->dh_ready + 1, ctx->pub_seq,
+                               ctx->d_counters + 2 * 33 + 1));
+    }
     if (early_upd) {
         HIPCHK(hipEventRecord(ctx->ev[slot][2], ctx->stream));
         if ((st = run_update(ctx, ctx->d_A, K)) != QVQ_OK) return st;
         ctx->nslabs = 0;   // reduced already
         HIPCHK(hipEventRecord(ctx->ev[slot][3], ctx->stream));
+    }
+    if (defer_ties) {   // qvq_lbg answers the ties after the finalize, if there are any
+        ctx->upd[slot] = false;
+        return QVQ_OK;
     }
     // the tree build overlaps the search just enqueued
     const auto tw0 = std::chrono::steady_clock::now();
@@ -797,6 +915,38 @@ qvq_status run_level(qvq_ctx *ctx, uint32_t K, int slot, bool sums_out, const do
         HIPCHK(hipEventRecord(ctx->ev[slot][3], ctx->stream));
     }
     return QVQ_OK;
+}
+
+// The ties of a level run with defer_ties (nt > 0 of them in d_ties): the reference's split
+// codebook -- the previous level's centroids as Kahan sums in row order (k_kahan.hip; for the
+// NORMAL colour space the exact sums are those bits already), split -- its kd-tree, and the
+// ties answered against both (every distance recomputed from the reference's code vectors).
+// The moves go to sums copy 1 (fused: the finalize adds it) or straight into copy 0.
+qvq_status resolve_kahan_ties(qvq_ctx *ctx, uint32_t K, int slot, unsigned nt, bool fused) {
+    const uint32_t D = ctx->D, Kc = K / 2;
+    const double *S_ref = ctx->d_C64_split;
+    qvq_status st;
+    if (ctx->cs == QVQ_CS_SCALED) {
+        if ((st = ensure_kahan(ctx, Kc)) != QVQ_OK) return st;
+        static const int passes = std::getenv("QVQ_KAHAN_PASSES") ? std::atoi(std::getenv("QVQ_KAHAN_PASSES")) : 2;
+        HIPCHK(launch_kahan_centroids(ctx->stream, ctx->kw, ctx->d_codes, ctx->Dp, D, ctx->N,
+                                      K == 2 ? nullptr : ctx->d_A_alt, Kc, ctx->d_kx, ctx->d_kc_cent,
+                                      ctx->d_kc_split, passes));
+        S_ref = ctx->d_kc_split;
+    }
+    ctx->h_kc_split.resize((size_t)K * D);
+    HIPCHK(hipMemcpyAsync(ctx->h_kc_split.data(), S_ref, (size_t)K * D * 8, hipMemcpyDeviceToHost, ctx->stream));
+    if ((st = wait_stream(ctx)) != QVQ_OK) return st;
+    KdView kd;
+    build_tree(ctx, ctx->h_kc_split.data(), K, slot & 1, kd);
+    unsigned *cnt = ctx->d_counters + 2 * slot;
+    uint64_t *target = fused ? ctx->d_sums + sums_cap_stride(ctx) : ctx->d_sums;
+    if (kd.depth > 0) {
+        HIPCHK(launch_kd_resolve(ctx->stream, ctx->d_codes, ctx->Dp, D, ctx->d_ties, &cnt[1], S_ref, K, ctx->d_lut64,
+                                 kd, ctx->d_A, nullptr, nullptr, ctx->d_plut, target));
+        return QVQ_OK;
+    }
+    return resolve_host_ties(ctx, ctx->h_kc_split.data(), K, nt, false, target);
 }
 
 // The byte histogram of the resident rows (kept on the device: qvq_lbg derives sum ||x||^2 and
@@ -863,6 +1013,7 @@ QVQ_API qvq_status qvq_create(int hip_device, qvq_ctx **out) {
     if ((e = hipMalloc(&ctx->d_w, 256 * 4)) != hipSuccess) return bail(e, "hipMalloc");
     if ((e = hipMalloc(&ctx->d_lut64, 256 * 8)) != hipSuccess) return bail(e, "hipMalloc");
     if ((e = hipMalloc(&ctx->d_plut, 256 * 8)) != hipSuccess) return bail(e, "hipMalloc");
+    if ((e = hipMalloc(&ctx->d_kx, 256 * 8)) != hipSuccess) return bail(e, "hipMalloc");
     // mapped: [0, 64) the codebook ready number, [64, 1024) a quantize's small results
     if ((e = hipHostMalloc(&ctx->h_ready, 1024, hipHostMallocMapped | hipHostMallocCoherent)) != hipSuccess)
         return bail(e, "hipHostMalloc");
@@ -900,6 +1051,7 @@ QVQ_API void qvq_destroy(qvq_ctx *ctx) {
     dfree(ctx->d_w);
     dfree(ctx->d_lut64);
     dfree(ctx->d_plut);
+    dfree(ctx->d_kx);
     dfree(ctx->d_counters);
     dfree(ctx->d_hist);
     if (ctx->h_ready) (void)hipHostFree(ctx->h_ready);
@@ -1228,10 +1380,13 @@ QVQ_API qvq_status qvq_lbg(qvq_ctx *ctx, uint32_t bits, double eps, double *code
     // with bits >= 1 the first search writes every row's index
     if (bits == 0) HIPCHK(hipMemsetAsync(ctx->d_A, 0, ctx->N * 4, ctx->stream));
 
+    const bool kahan = kahan_mode(ctx);
+    if (kahan && !ctx->d_A_alt) HIPCHK(hipMalloc(&ctx->d_A_alt, ctx->N * 4));
     for (uint32_t lvl = 1; lvl <= bits; lvl++) {
         const uint32_t K = 1u << lvl;
         const int slot = (int)lvl - 1;
-        if ((st = run_level(ctx, K, slot, true, ctx->h_cb, ctx->seq)) != QVQ_OK) return st;
+        if (kahan) std::swap(ctx->d_A, ctx->d_A_alt);   // d_A_alt: the previous level's assignment
+        if ((st = run_level(ctx, K, slot, true, ctx->h_cb, ctx->seq, kahan)) != QVQ_OK) return st;
         const bool split = lvl < bits;
         {
             const uint32_t copies = ctx->sums_copies;
@@ -1250,6 +1405,18 @@ QVQ_API qvq_status qvq_lbg(qvq_ctx *ctx, uint32_t bits, double eps, double *code
             if ((st = all_reduce_sums(ctx, K)) != QVQ_OK) return st;
             HIPCHK(finalize(K, split, copies, copies > 1 ? tcnt : nullptr));
             if (copies > 1) ctx->sums1_dirty = false;
+            if (kahan) {   // the level's ties (published after its recheck)
+                if ((st = wait_flag(ctx, ctx->h_ready + 1, ctx->pub_seq)) != QVQ_OK) return st;
+                const unsigned nt = (unsigned)(uint32_t)ctx->h_ready[2];
+                if (nt) {
+                    const bool fused = use_fused(ctx, K);
+                    if (fused) ctx->sums1_dirty = true;
+                    if ((st = resolve_kahan_ties(ctx, K, slot, nt, fused)) != QVQ_OK) return st;
+                    if (split) ctx->seq--;   // the same codebook number again
+                    HIPCHK(finalize(K, split, fused ? 2 : 1, fused ? tcnt : nullptr));
+                    ctx->sums1_dirty = false;
+                }
+            }
         }
     }
     // Returned distortion: updateDistortion after the last fix (src/Quantizer.cpp:9-22,103),

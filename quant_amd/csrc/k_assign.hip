@@ -957,7 +957,7 @@ template <bool STAGED, int DT>
 __global__ __launch_bounds__(RECHECK_THREADS) void recheck_kernel(
     const uint8_t *__restrict__ codes, uint32_t Dp, uint32_t D, const uint32_t *__restrict__ flags,
     const unsigned int *__restrict__ flag_cnt, const double *__restrict__ C64, const float *__restrict__ g_C32,
-    uint32_t K, const double *__restrict__ lut64, float alpha, float beta, float gamma, double tie_rel,
+    uint32_t K, const double *__restrict__ lut64, float alpha, float beta, float gamma, double tie_rel, double tie_abs,
     uint32_t *__restrict__ A, uint32_t *__restrict__ ties, unsigned int *__restrict__ tie_cnt,
     uint64_t *__restrict__ xslab, uint32_t *__restrict__ xcnt, const uint64_t *__restrict__ plut) {
     extern __shared__ __attribute__((aligned(16))) double rsm[];
@@ -1063,7 +1063,7 @@ __global__ __launch_bounds__(RECHECK_THREADS) void recheck_kernel(
             d1 = m1;
             k1 = mk;
         }
-        if (d2 - d1 <= tie_rel * d1) {   // exact tie for the reference: the kd-tree decides
+        if (in_tie_band(d1, d2, tie_rel, tie_abs)) {   // a tie for the reference: the kd-tree decides
             if (lane == 0) ties[atomicAdd(tie_cnt, 1u)] = crow;   // A keeps the provisional index
         } else {
             // the search's index (its terms are in the slabs when fused); mostly unchanged
@@ -1088,7 +1088,7 @@ template <int DT>
 __global__ __launch_bounds__(RECHECK_THREADS) void recheck_chunked_kernel(
     const uint8_t *__restrict__ codes, uint32_t Dp, uint32_t D, const uint32_t *__restrict__ flags,
     const unsigned int *__restrict__ flag_cnt, const double *__restrict__ C64, const float *__restrict__ g_C32,
-    uint32_t K, const double *__restrict__ lut64, float alpha, float beta, float gamma, double tie_rel,
+    uint32_t K, const double *__restrict__ lut64, float alpha, float beta, float gamma, double tie_rel, double tie_abs,
     uint32_t *__restrict__ A, uint32_t *__restrict__ ties, unsigned int *__restrict__ tie_cnt,
     uint64_t *__restrict__ xslab, uint32_t *__restrict__ xcnt, const uint64_t *__restrict__ plut,
     const uint32_t *__restrict__ perm, const int32_t *__restrict__ tint, float qscale) {
@@ -1233,7 +1233,7 @@ __global__ __launch_bounds__(RECHECK_THREADS) void recheck_chunked_kernel(
             d1 = m1;
             k1 = mk;
         }
-        if (d2 - d1 <= tie_rel * d1) {   // exact tie for the reference: the kd-tree decides
+        if (in_tie_band(d1, d2, tie_rel, tie_abs)) {   // a tie for the reference: the kd-tree decides
             if (lane == 0) ties[atomicAdd(tie_cnt, 1u)] = crow;
         } else {
             const uint32_t from = __builtin_amdgcn_readfirstlane(carow);
@@ -1249,15 +1249,15 @@ template <bool S, int DT>
 static void launch_recheck_variant(hipStream_t s, int grid, size_t lds, const uint8_t *codes, uint32_t Dp, uint32_t D,
                                    const uint32_t *flags, const unsigned *flag_cnt, const double *C64,
                                    const float *C32, uint32_t K, const double *lut64, float alpha, float beta,
-                                   float gamma, double tie_rel, uint32_t *A, uint32_t *ties, unsigned *tie_cnt,
+                                   float gamma, double tie_rel, double tie_abs, uint32_t *A, uint32_t *ties, unsigned *tie_cnt,
                                    uint64_t *xslab, uint32_t *xcnt, const uint64_t *plut) {
     hipLaunchKernelGGL((recheck_kernel<S, DT>), dim3(grid), dim3(RECHECK_THREADS), lds, s, codes, Dp, D, flags,
-                       flag_cnt, C64, C32, K, lut64, alpha, beta, gamma, tie_rel, A, ties, tie_cnt, xslab, xcnt, plut);
+                       flag_cnt, C64, C32, K, lut64, alpha, beta, gamma, tie_rel, tie_abs, A, ties, tie_cnt, xslab, xcnt, plut);
 }
 
 hipError_t launch_recheck(hipStream_t s, int num_cu, const uint8_t *codes, uint32_t Dp, uint32_t D,
                           const uint32_t *flags, const unsigned *flag_cnt, const double *C64, const float *C32,
-                          uint32_t K, const double *lut64, float alpha, float beta, float gamma, double tie_rel,
+                          uint32_t K, const double *lut64, float alpha, float beta, float gamma, double tie_rel, double tie_abs,
                           uint32_t *A, uint32_t *ties, unsigned *tie_cnt, uint64_t *xslab, uint32_t *xcnt,
                           const uint64_t *plut, const uint32_t *perm, const int32_t *tint, float qscale) {
     if (Dp % 4 || Dp > 64) return hipErrorInvalidValue;
@@ -1271,17 +1271,17 @@ hipError_t launch_recheck(hipStream_t s, int num_cu, const uint8_t *codes, uint3
         const size_t clds = base + (size_t)RC_CHUNK * recheck_c32_stride(Dp) * 4;
         if (Dp == 12)
             hipLaunchKernelGGL(recheck_chunked_kernel<12>, dim3(num_cu), dim3(RECHECK_THREADS), clds, s, codes, Dp, D,
-                               flags, flag_cnt, C64, C32, K, lut64, alpha, beta, gamma, tie_rel, A, ties, tie_cnt,
+                               flags, flag_cnt, C64, C32, K, lut64, alpha, beta, gamma, tie_rel, tie_abs, A, ties, tie_cnt,
                                xslab, xcnt, plut, perm, tint, qscale);
         else
             hipLaunchKernelGGL(recheck_chunked_kernel<48>, dim3(num_cu), dim3(RECHECK_THREADS), clds, s, codes, Dp, D,
-                               flags, flag_cnt, C64, C32, K, lut64, alpha, beta, gamma, tie_rel, A, ties, tie_cnt,
+                               flags, flag_cnt, C64, C32, K, lut64, alpha, beta, gamma, tie_rel, tie_abs, A, ties, tie_cnt,
                                xslab, xcnt, plut, perm, tint, qscale);
         return hipGetLastError();
     }
 #define QVQ_RC(SS, DT)                                                                                             \
     launch_recheck_variant<SS, DT>(s, num_cu, lds, codes, Dp, D, flags, flag_cnt, C64, C32, K, lut64, alpha, beta, \
-                                   gamma, tie_rel, A, ties, tie_cnt, xslab, xcnt, plut)
+                                   gamma, tie_rel, tie_abs, A, ties, tie_cnt, xslab, xcnt, plut)
     if (Dp == 12) {
         if (staged) QVQ_RC(true, 12); else QVQ_RC(false, 12);
     } else if (Dp == 48) {

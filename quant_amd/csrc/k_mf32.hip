@@ -535,7 +535,7 @@ bool recheck_mf32_fits(uint32_t K) { return rc_lds_layout(K).total <= M32_LDS_MA
 __global__ __launch_bounds__(M32_THREADS) void recheck_mf32_kernel(
     const uint8_t *__restrict__ codes, const uint32_t *__restrict__ flags, const unsigned *__restrict__ flag_cnt,
     const _Float16 *__restrict__ g_rows, const double *__restrict__ C64, uint32_t K,
-    const double *__restrict__ g_lut64, MfThresholds th, double tie_rel, uint32_t *__restrict__ A,
+    const double *__restrict__ g_lut64, MfThresholds th, double tie_rel, double tie_abs, uint32_t *__restrict__ A,
     uint32_t *__restrict__ ties, unsigned *__restrict__ tie_cnt, uint64_t *__restrict__ xslab,
     uint32_t *__restrict__ xcnt, const uint64_t *__restrict__ plut) {
     extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
@@ -669,7 +669,7 @@ __global__ __launch_bounds__(M32_THREADS) void recheck_mf32_kernel(
                 take(ka, ref_l2_n<MF_D>(x, ra));
                 if (two) take(kb, ref_l2_n<MF_D>(x, rb));
             }
-            if (d2 - d1 <= tie_rel * d1) {   // exact tie for the reference: the kd-tree decides
+            if (in_tie_band(d1, d2, tie_rel, tie_abs)) {   // a tie for the reference: the kd-tree decides
                 ties[atomicAdd(tie_cnt, 1u)] = row;   // A keeps the provisional index
             } else {
                 const uint32_t from = A[row];   // the search's index (its terms are in the slabs when fused)
@@ -697,12 +697,12 @@ __global__ __launch_bounds__(M32_THREADS) void recheck_mf32_kernel(
 
 hipError_t launch_recheck_mf32(hipStream_t s, int num_cu, const uint8_t *codes, const uint32_t *flags,
                                const unsigned *flag_cnt, const _Float16 *cb_rows, const double *C64, uint32_t K,
-                               const double *lut64, const MfThresholds &th, double tie_rel, uint32_t *A,
+                               const double *lut64, const MfThresholds &th, double tie_rel, double tie_abs, uint32_t *A,
                                uint32_t *ties, unsigned *tie_cnt, uint64_t *xslab, uint32_t *xcnt,
                                const uint64_t *plut) {
     if (!recheck_mf32_fits(K)) return hipErrorInvalidValue;
     hipLaunchKernelGGL(recheck_mf32_kernel, dim3(num_cu), dim3(M32_THREADS), rc_lds_layout(K).total, s, codes, flags,
-                       flag_cnt, cb_rows, C64, K, lut64, th, tie_rel, A, ties, tie_cnt, xslab, xcnt, plut);
+                       flag_cnt, cb_rows, C64, K, lut64, th, tie_rel, tie_abs, A, ties, tie_cnt, xslab, xcnt, plut);
     return hipGetLastError();
 }
 
