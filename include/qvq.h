@@ -129,6 +129,10 @@ QVQ_API const uint32_t *qvq_assign_device(const qvq_ctx *ctx);
  *   (K x dim fp64) and counts (K u64), the engine's exact-sum rule. */
 QVQ_API qvq_status qvq_assign(qvq_ctx *ctx, const double *C, uint32_t K, uint32_t *assign);
 QVQ_API qvq_status qvq_update(qvq_ctx *ctx, const uint32_t *assign, uint32_t K, double *C_out, uint64_t *counts);
+/* The reference's own centroid bits (Solution::fixCodeVectors, reference src/Quantizer.cpp:59-87:
+ * Kahan sums in ascending row order times fl(1/n), empty cells 0) of the resident rows under
+ * assignment A, into C_out (K x dim fp64).  One rank (QVQ_EUNSUPPORTED with a communicator). */
+QVQ_API qvq_status qvq_update_kahan(qvq_ctx *ctx, const uint32_t *assign, uint32_t K, double *C_out);
 
 /* Decode (replaces CompressedImage::decompress, reference src/Compressor.cpp:156-165, and the
  * getImageFromVectors it calls, src/Compressor.cpp:64-85): raster[x*ySize+y] = the code-vector bytes

@@ -39,7 +39,7 @@ class _Timings(ctypes.Structure):
 _lib = None
 EXPORTED = ["qvq_create", "qvq_destroy", "qvq_last_error", "qvq_version", "qvq_set_images",
             "qvq_set_images_device", "qvq_set_synthetic", "qvq_set_vectors", "qvq_num_vectors",
-            "qvq_dim", "qvq_lbg", "qvq_assign_device", "qvq_assign", "qvq_update",
+            "qvq_dim", "qvq_lbg", "qvq_assign_device", "qvq_assign", "qvq_update", "qvq_update_kahan",
             "qvq_comm_unique_id", "qvq_comm_init", "qvq_set_timing", "qvq_get_timings", "qvq_host_kdtree_nn",
             "qvq_host_finalize", "qvq_host_row_terms", "qvq_decode", "qvq_decode_mse", "qvq_decode_device",
             "qvq_set_timeout", "qvq_host_wait_probe", "qvq_comm_init_host", "qvq_comm_info", "qvq_set_vectors_exact"]
@@ -73,6 +73,7 @@ def lib():
             "qvq_assign_device": ([P], P),
             "qvq_assign": ([P, P, u32, P], i),
             "qvq_update": ([P, P, u32, P, P], i),
+            "qvq_update_kahan": ([P, P, u32, P], i),
             "qvq_comm_unique_id": ([P], i),
             "qvq_comm_init": ([P, i, i, P], i),
             "qvq_set_timing": ([P, i], i),
@@ -200,6 +201,13 @@ class Engine:
         cnt = np.empty(K, np.uint64)
         _check(lib().qvq_update(self._h, _p(A), K, _p(C), _p(cnt)), self._h)
         return C, cnt
+
+    def update_kahan(self, A, K):
+        """The reference's centroid bits (Kahan sums in row order, src/Quantizer.cpp:59-87)."""
+        A = np.ascontiguousarray(A, np.uint32)
+        C = np.empty((K, self.dim), np.float64)
+        _check(lib().qvq_update_kahan(self._h, _p(A), K, _p(C)), self._h)
+        return C
 
     def assign_device_ptr(self):
         return lib().qvq_assign_device(self._h)

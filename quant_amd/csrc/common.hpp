@@ -202,8 +202,9 @@ __device__ inline void reduce_columns_block(const uint64_t *__restrict__ part, c
 // may differ from the exact sums' by tie_abs / (2 sqrt(D)) per component -- can decide them
 // (DESIGN.md 3.8): |d' - d| <= tie_abs sqrt(d) + tie_abs^2 / 2 for each distance.
 __host__ __device__ inline bool in_tie_band(double d1, double d2, double tie_rel, double tie_abs) {
-    const double band = tie_abs * (sqrt(d1) + sqrt(d2)) + tie_abs * tie_abs;
-    return d2 - d1 <= tie_rel * d1 || d2 - d1 <= band;
+    const double gap = d2 - d1;   // d2 = inf: one candidate only, never a tie
+    const double band = tie_abs * (sqrt(d1) + sqrt(fmin(d2, 1e300))) + tie_abs * tie_abs;
+    return gap <= tie_rel * d1 || gap <= band;
 }
 
 struct MfThresholds {
@@ -361,29 +362,32 @@ hipError_t launch_exact_gather(hipStream_t s, const double *X, uint32_t D, const
                                double *out);
 hipError_t launch_exact_fix(hipStream_t s, uint32_t *A, const uint32_t *rows, const uint32_t *vals, uint32_t n);
 // The reference's Kahan centroids on the device (k_kahan.hip, kahan_par.hpp): scratch for one
-// computation over N rows and K cells (KahanWork::caps sizes the function tables).
+// computation over N rows and up to k_cap cells (sizes from KahanWork::caps).
 struct KahanWork {
-    uint32_t L = 128, S = 32;          // steps per segment, segments per group (groups per supergroup)
-    uint32_t *keys = nullptr, *iota = nullptr, *order = nullptr;   // [N] each (sort)
-    void *temp = nullptr;
-    size_t temp_bytes = 0;
-    uint32_t *koff = nullptr;          // [K + 1]
-    uint32_t *off = nullptr;           // [3][K + 1]
-    uint8_t *planes = nullptr;         // [D][N]
-    void *fn0 = nullptr, *fn1 = nullptr, *fn2 = nullptr;   // [D][NS], [D][NG], [D][NU] functions
-    void *P0 = nullptr, *Etr = nullptr;                    // [D][NS] 128-bit states
-    unsigned *stats = nullptr;         // [3] table misses (segments, groups, supergroups)
-    uint64_t n_cap = 0;
+    uint32_t *hist = nullptr;          // [G][K] sort histograms (G = sort_blocks(N))
+    uint32_t *tot = nullptr;           // [K] rows per cell
+    uint32_t *koff = nullptr, *segoff = nullptr, *blkoff = nullptr;   // [K + 1] each
+    uint32_t *order = nullptr;         // [N] rows in cell order (stable)
+    uint8_t *planes = nullptr;         // [D][plane_len(N)]: the chains' bytes, component-major
+    void *meta = nullptr;              // [D][seg_cap] segment metadata
+    void *bsum = nullptr;              // [D][blk_cap] 128-bit block totals, then prefixes
+    void *bfn = nullptr;               // [D][blk_cap] block functions
+    void *tab = nullptr;               // the byte table (kahan::ByteTab)
+    unsigned *stats = nullptr;         // [4] blocks not composable, block misses, segment replays
+    uint32_t n_one = 0;                // K = 1: N (the mean's single cell)
+    uint64_t seg_cap = 0, blk_cap = 0, n_cap = 0;
     uint32_t k_cap = 0, d_cap = 0;
+    static size_t tab_bytes();
+    static void make_tab(const uint64_t *X, void *out);
+    static void caps(uint64_t N, uint32_t K, uint64_t &segs, uint64_t &blks);
+    static uint64_t plane_len(uint64_t N);
+    static size_t meta_bytes();
     static size_t fn_bytes();
-    static void caps(uint64_t N, uint32_t K, uint32_t L, uint32_t S, uint32_t &NS, uint32_t &NG, uint32_t &NU);
+    static uint32_t sort_blocks(uint64_t N);
 };
-size_t kahan_sort_temp_bytes(uint64_t N);
 // C [K][D] = the reference's centroids of assignment A (nullptr: K = 1, the mean of every row):
-// Kahan sums in ascending row order times fl(1/n), empty cells 0.  Xt[b] = value of byte b in
-// units of 2^-60 (SCALED).  With split_out also the split [2K][D] (x1.2 | x0.8).  passes 2: a
-// trusted walk re-estimates the segment tables' states first (fewer table misses).
+// Kahan sums in ascending row order times fl(1/n), empty cells 0, bit for bit (SCALED byte
+// values; w.tab from KahanWork::make_tab).  With split_out also the split [2K][D] (x1.2 | x0.8).
 hipError_t launch_kahan_centroids(hipStream_t s, const KahanWork &w, const uint8_t *codes, uint32_t Dp, uint32_t D,
-                                  uint64_t N, const uint32_t *A, uint32_t K, const uint64_t *Xt, double *C,
-                                  double *split_out, int passes);
+                                  uint64_t N, const uint32_t *A, uint32_t K, double *C, double *split_out);
 }  // namespace qvq

@@ -104,7 +104,6 @@ struct qvq_ctx {
     // the reference-bit (Kahan) centroids a level with kd-tree ties needs
     uint32_t *d_A_alt = nullptr;
     KahanWork kw;
-    uint64_t *d_kx = nullptr;      // byte -> value in units of 2^-60 (SCALED)
     double *d_kc_cent = nullptr, *d_kc_split = nullptr;   // Kahan centroids [K/2][D], their split [K][D]
     uint32_t kc_kcap = 0;
     std::vector<double> h_kc_split;   // host copy of the split for the tree build
@@ -118,6 +117,7 @@ struct qvq_ctx {
     uint32_t Kcap = 0;
     uint32_t G = 0;   // workgroup slabs
     double *d_C64_cent = nullptr, *d_C64_split = nullptr;
+    double *d_C64_split_alt = nullptr;   // qvq_lbg's next split while d_C64_split may still be needed
     float *d_C32 = nullptr;
     float *d_E32 = nullptr;   // D = 12: expanded fp32 terms for the small-K scan
     _Float16 *d_rows = nullptr;   // MFMA code-vector rows
@@ -260,26 +260,18 @@ bool use_prune(const qvq_ctx *ctx, uint32_t K) {
     return wmink && K >= wmink && use_wide(ctx, K) && wide_prune_fits(ctx->Dp, K);
 }
 
-void free_kahan(qvq_ctx *ctx) {
-    KahanWork &w = ctx->kw;
-    dfree(w.keys);
-    dfree(w.iota);
-    dfree(w.order);
-    if (w.temp) (void)hipFree(w.temp);
-    w.temp = nullptr;
-    w.temp_bytes = 0;
-    dfree(w.koff);
-    dfree(w.off);
+void free_kahan_work(KahanWork &w) {
+    for (uint32_t **p : {&w.hist, &w.tot, &w.koff, &w.segoff, &w.blkoff, &w.order}) dfree(*p);
     dfree(w.planes);
-    if (w.fn0) (void)hipFree(w.fn0);
-    if (w.fn1) (void)hipFree(w.fn1);
-    if (w.fn2) (void)hipFree(w.fn2);
-    if (w.P0) (void)hipFree(w.P0);
-    if (w.Etr) (void)hipFree(w.Etr);
-    w.fn0 = w.fn1 = w.fn2 = w.P0 = w.Etr = nullptr;
     dfree(w.stats);
-    w.n_cap = 0;
+    for (void **p : {&w.meta, &w.bsum, &w.bfn, &w.tab})
+        if (*p) (void)hipFree(*p), *p = nullptr;
+    w.seg_cap = w.blk_cap = w.n_cap = 0;
     w.k_cap = w.d_cap = 0;
+}
+
+void free_kahan(qvq_ctx *ctx) {
+    free_kahan_work(ctx->kw);
     dfree(ctx->d_kc_cent);
     dfree(ctx->d_kc_split);
     ctx->kc_kcap = 0;
@@ -310,6 +302,7 @@ void free_training(qvq_ctx *ctx) {
 void free_levels(qvq_ctx *ctx) {
     dfree(ctx->d_C64_cent);
     dfree(ctx->d_C64_split);
+    dfree(ctx->d_C64_split_alt);
     dfree(ctx->d_C32);
     dfree(ctx->d_E32);
     dfree(ctx->d_rows);
@@ -425,11 +418,6 @@ qvq_status alloc_training(qvq_ctx *ctx, uint64_t N, uint32_t D, int cs) {
     HIPCHK(hipMemcpy(ctx->d_w, ctx->terms.w, sizeof(ctx->terms.w), hipMemcpyHostToDevice));
     HIPCHK(hipMemcpy(ctx->d_lut64, ctx->terms.v64, sizeof(ctx->terms.v64), hipMemcpyHostToDevice));
     HIPCHK(hipMemcpy(ctx->d_plut, plut, sizeof(plut), hipMemcpyHostToDevice));
-    // SCALED values in units of 2^-60 for the Kahan chains; NORMAL values are integers, whose
-    // Kahan sums are exact (the centroids' bits are the exact sums' already)
-    uint64_t kx[256];
-    for (int b = 0; b < 256; b++) kx[b] = cs == QVQ_CS_SCALED ? (uint64_t)std::ldexp(ctx->terms.v64[b], 60) : 0;
-    HIPCHK(hipMemcpy(ctx->d_kx, kx, sizeof(kx), hipMemcpyHostToDevice));
     // the band of rows whose answer can depend on the centroids' last bits:
     // |c_kahan - c_exact| <= delta per component, so a distance moves by at most
     // 2 delta sqrt(D) sqrt(d) + D delta^2
@@ -445,6 +433,7 @@ qvq_status ensure_levels(qvq_ctx *ctx, uint32_t Kmax) {
     const uint64_t Kp = pad32(Kmax);
     HIPCHK(hipMalloc(&ctx->d_C64_cent, KD * 8));
     HIPCHK(hipMalloc(&ctx->d_C64_split, KD * 8));
+    HIPCHK(hipMalloc(&ctx->d_C64_split_alt, KD * 8));
     HIPCHK(hipMalloc(&ctx->d_C32, Kp * ctx->Dp * 4));
     if (ctx->D == MF_D) HIPCHK(hipMalloc(&ctx->d_E32, Kp * 16 * 4));
     HIPCHK(hipMalloc(&ctx->d_rows, Kp * 2 * cb_row_f16(ctx->D, ctx->Dp)));
@@ -582,39 +571,31 @@ qvq_status ensure_kahan(qvq_ctx *ctx, uint32_t Kc) {
     }
     if (w.n_cap == N && w.k_cap >= Kc && w.d_cap == D) return QVQ_OK;
     const uint32_t kcap = std::max(Kc, w.k_cap);
-    const uint32_t L = w.L, S = w.S;
-    {   // keep the sizes, free the buffers
-        dfree(w.keys);
-        dfree(w.iota);
-        dfree(w.order);
-        if (w.temp) (void)hipFree(w.temp);
-        dfree(w.koff);
-        dfree(w.off);
-        dfree(w.planes);
-        for (void **p : {&w.fn0, &w.fn1, &w.fn2, &w.P0, &w.Etr})
-            if (*p) (void)hipFree(*p), *p = nullptr;
-        dfree(w.stats);
-        w.temp = nullptr;
-    }
-    uint32_t NS, NG, NU;
-    KahanWork::caps(N, kcap, L, S, NS, NG, NU);
-    w.temp_bytes = std::max<size_t>(kahan_sort_temp_bytes(N), 16);
-    HIPCHK(hipMalloc(&w.keys, N * 4));
-    HIPCHK(hipMalloc(&w.iota, N * 4));
+    free_kahan_work(w);
+    uint64_t segs, blks;
+    KahanWork::caps(N, kcap, segs, blks);
+    HIPCHK(hipMalloc(&w.hist, (uint64_t)KahanWork::sort_blocks(N) * kcap * 4));
+    HIPCHK(hipMalloc(&w.tot, (uint64_t)kcap * 4));
+    for (uint32_t **p : {&w.koff, &w.segoff, &w.blkoff}) HIPCHK(hipMalloc(p, ((uint64_t)kcap + 1) * 4));
     HIPCHK(hipMalloc(&w.order, N * 4));
-    HIPCHK(hipMalloc(&w.temp, w.temp_bytes));
-    HIPCHK(hipMalloc(&w.koff, ((uint64_t)kcap + 1) * 4));
-    HIPCHK(hipMalloc(&w.off, 3 * ((uint64_t)kcap + 1) * 4));
-    HIPCHK(hipMalloc(&w.planes, N * D));
-    const size_t fb = KahanWork::fn_bytes();
-    HIPCHK(hipMalloc(&w.fn0, (uint64_t)D * NS * fb));
-    HIPCHK(hipMalloc(&w.fn1, (uint64_t)D * NG * fb));
-    HIPCHK(hipMalloc(&w.fn2, (uint64_t)D * NU * fb));
-    HIPCHK(hipMalloc(&w.P0, (uint64_t)D * NS * 16));
-    HIPCHK(hipMalloc(&w.Etr, (uint64_t)D * NS * 16));
+    HIPCHK(hipMalloc(&w.planes, (uint64_t)D * KahanWork::plane_len(N)));
+    HIPCHK(hipMemset(w.planes, 0, (uint64_t)D * KahanWork::plane_len(N)));
+    HIPCHK(hipMalloc(&w.meta, (uint64_t)D * segs * KahanWork::meta_bytes()));
+    HIPCHK(hipMalloc(&w.bsum, (uint64_t)D * blks * 16));
+    HIPCHK(hipMalloc(&w.bfn, (uint64_t)D * blks * KahanWork::fn_bytes()));
     HIPCHK(hipMalloc(&w.stats, 4 * sizeof(unsigned)));
     HIPCHK(hipMemset(w.stats, 0, 4 * sizeof(unsigned)));
-    HIPCHK(launch_exact_iota(ctx->stream, w.iota, N));
+    {   // the byte table: SCALED values in units of 2^-60
+        uint64_t kx[256];
+        for (int b = 0; b < 256; b++) kx[b] = (uint64_t)std::ldexp(ctx->terms.v64[b], 60);
+        std::vector<uint8_t> tab(KahanWork::tab_bytes());
+        KahanWork::make_tab(kx, tab.data());
+        HIPCHK(hipMalloc(&w.tab, tab.size()));
+        HIPCHK(hipMemcpy(w.tab, tab.data(), tab.size(), hipMemcpyHostToDevice));
+    }
+    w.n_one = (uint32_t)N;
+    w.seg_cap = segs;
+    w.blk_cap = blks;
     w.n_cap = N;
     w.k_cap = kcap;
     w.d_cap = D;
@@ -928,11 +909,17 @@ qvq_status resolve_kahan_ties(qvq_ctx *ctx, uint32_t K, int slot, unsigned nt, b
     qvq_status st;
     if (ctx->cs == QVQ_CS_SCALED) {
         if ((st = ensure_kahan(ctx, Kc)) != QVQ_OK) return st;
-        static const int passes = std::getenv("QVQ_KAHAN_PASSES") ? std::atoi(std::getenv("QVQ_KAHAN_PASSES")) : 2;
         HIPCHK(launch_kahan_centroids(ctx->stream, ctx->kw, ctx->d_codes, ctx->Dp, D, ctx->N,
-                                      K == 2 ? nullptr : ctx->d_A_alt, Kc, ctx->d_kx, ctx->d_kc_cent,
-                                      ctx->d_kc_split, passes));
+                                      K == 2 ? nullptr : ctx->d_A_alt, Kc, ctx->d_kc_cent, ctx->d_kc_split));
         S_ref = ctx->d_kc_split;
+        if (env_is("QVQ_KAHAN_DEBUG", "1")) {   // blocks not composable, block misses, segment replays
+            unsigned ms[4];
+            HIPCHK(hipMemcpyAsync(ms, ctx->kw.stats, sizeof(ms), hipMemcpyDeviceToHost, ctx->stream));
+            HIPCHK(hipMemsetAsync(ctx->kw.stats, 0, sizeof(ms), ctx->stream));
+            HIPCHK(hipStreamSynchronize(ctx->stream));
+            std::fprintf(stderr, "qvq kahan: K %u level ties %u blocks not composable %u block misses %u replays %u\n",
+                         K, nt, ms[0], ms[1], ms[2]);
+        }
     }
     ctx->h_kc_split.resize((size_t)K * D);
     HIPCHK(hipMemcpyAsync(ctx->h_kc_split.data(), S_ref, (size_t)K * D * 8, hipMemcpyDeviceToHost, ctx->stream));
@@ -1013,7 +1000,6 @@ QVQ_API qvq_status qvq_create(int hip_device, qvq_ctx **out) {
     if ((e = hipMalloc(&ctx->d_w, 256 * 4)) != hipSuccess) return bail(e, "hipMalloc");
     if ((e = hipMalloc(&ctx->d_lut64, 256 * 8)) != hipSuccess) return bail(e, "hipMalloc");
     if ((e = hipMalloc(&ctx->d_plut, 256 * 8)) != hipSuccess) return bail(e, "hipMalloc");
-    if ((e = hipMalloc(&ctx->d_kx, 256 * 8)) != hipSuccess) return bail(e, "hipMalloc");
     // mapped: [0, 64) the codebook ready number, [64, 1024) a quantize's small results
     if ((e = hipHostMalloc(&ctx->h_ready, 1024, hipHostMallocMapped | hipHostMallocCoherent)) != hipSuccess)
         return bail(e, "hipHostMalloc");
@@ -1051,7 +1037,6 @@ QVQ_API void qvq_destroy(qvq_ctx *ctx) {
     dfree(ctx->d_w);
     dfree(ctx->d_lut64);
     dfree(ctx->d_plut);
-    dfree(ctx->d_kx);
     dfree(ctx->d_counters);
     dfree(ctx->d_hist);
     if (ctx->h_ready) (void)hipHostFree(ctx->h_ready);
@@ -1361,13 +1346,16 @@ QVQ_API qvq_status qvq_lbg(qvq_ctx *ctx, uint32_t bits, double eps, double *code
         ctx->sums1_dirty = false;
     }
     // copies 2: copy 1 holds the ties' moves (added here; the next level's search clears it)
+    // the split a finalize writes: with deferred ties the level's own split must survive its
+    // (speculative) finalize, so the next one goes to the other buffer and the two swap
+    double *split_out = ctx->d_C64_split;
     auto finalize = [&](uint32_t K, bool split, uint32_t copies = 1, const unsigned *gate = nullptr) {
         if (split) ctx->seq++;
         const bool prune = split && use_prune(ctx, 2 * K);   // the next search's tile order
         ctx->perm_k = prune ? 2 * K : 0;
         return launch_finalize_prep(ctx->stream, K == 1 ? ctx->d_mean : ctx->d_sums, K, ctx->D, ctx->Dp, T.R, T.bias,
                                     T.scale,
-                                    ctx->d_C64_cent, split, ctx->d_C64_split, pad32(2 * K), T.mu, T.sx, ctx->mf_t,
+                                    ctx->d_C64_cent, split, split_out, pad32(2 * K), T.mu, T.sx, ctx->mf_t,
                                     ctx->d_C32, ctx->d_rows, ctx->d_E32, split ? ctx->dh_cb : nullptr, d_dist + 8,
                                     dist_done,
                                     split ? nullptr : d_dist + 2, split ? ctx->dh_ready : nullptr, ctx->seq,
@@ -1382,6 +1370,7 @@ QVQ_API qvq_status qvq_lbg(qvq_ctx *ctx, uint32_t bits, double eps, double *code
 
     const bool kahan = kahan_mode(ctx);
     if (kahan && !ctx->d_A_alt) HIPCHK(hipMalloc(&ctx->d_A_alt, ctx->N * 4));
+    if (kahan) split_out = ctx->d_C64_split_alt;
     for (uint32_t lvl = 1; lvl <= bits; lvl++) {
         const uint32_t K = 1u << lvl;
         const int slot = (int)lvl - 1;
@@ -1416,6 +1405,10 @@ QVQ_API qvq_status qvq_lbg(qvq_ctx *ctx, uint32_t bits, double eps, double *code
                     HIPCHK(finalize(K, split, fused ? 2 : 1, fused ? tcnt : nullptr));
                     ctx->sums1_dirty = false;
                 }
+                if (split) {
+                    std::swap(ctx->d_C64_split, ctx->d_C64_split_alt);
+                    split_out = ctx->d_C64_split_alt;
+                }
             }
         }
     }
@@ -1447,7 +1440,9 @@ QVQ_API qvq_status qvq_lbg(qvq_ctx *ctx, uint32_t bits, double eps, double *code
         std::memcpy(stats, h_small + sizeof(dres), sizeof(stats));
         if (codebook) std::memcpy(codebook, ctx->h_cb, cb_bytes);
     }
-    if (distortion) *distortion = (dres[0] - dres[2]) / (dres[1] * (double)ctx->D);
+    // closed form: sum ||x||^2 - sum_k (2 c_k.S_k - n_k ||c_k||^2) cancels to a few ulps of
+    // sum ||x||^2 when the cells are (nearly) exact; a distortion is never negative
+    if (distortion) *distortion = std::max(0.0, (dres[0] - dres[2]) / (dres[1] * (double)ctx->D));
     for (uint32_t lvl = 1; lvl <= bits; lvl++) {
         // assign: the search kernel; update: the non-fused update; other: the rest of the
         // level up to the next level's search (recheck, kd-tree, reduce, finalize, tables)
@@ -1540,6 +1535,40 @@ QVQ_API qvq_status qvq_update(qvq_ctx *ctx, const uint32_t *assign, uint32_t K, 
     if ((st = wait_stream(ctx)) != QVQ_OK) return st;   // bounded: the all-reduce may wait on peer ranks
     if (C_out) std::memcpy(C_out, stage, cB);
     if (counts) std::memcpy(counts, stage + cB, nB);
+    return QVQ_OK;
+}
+
+// The reference's centroids bit for bit (Solution::fixCodeVectors, src/Quantizer.cpp:59-87):
+// Kahan sums in ascending row order times fl(1/n) (k_kahan.hip).  One rank; byte rows.
+QVQ_API qvq_status qvq_update_kahan(qvq_ctx *ctx, const uint32_t *assign, uint32_t K, double *C_out) {
+    if (!ctx) return QVQ_EINVAL;
+    GUARD(ctx);
+    if (ctx->N == 0) return fail(ctx, QVQ_ESTATE, "no training set");
+    if (!assign || K == 0) return fail(ctx, QVQ_EINVAL, "empty assignment");
+    if (ctx->comm || ctx->host_ar) return fail(ctx, QVQ_EUNSUPPORTED, "Kahan centroids run on one rank");
+    if (ctx->exact) return qvq_update(ctx, assign, K, C_out, nullptr);   // exact mode: the Kahan chain already
+    if (ctx->cs != QVQ_CS_SCALED) return qvq_update(ctx, assign, K, C_out, nullptr);   // integers: exact = Kahan
+    for (uint64_t i = 0; i < ctx->N; i++)
+        if (assign[i] >= K) return fail(ctx, QVQ_EINVAL, "assignment index out of range");
+    HIPCHK(hipSetDevice(ctx->dev));
+    qvq_status st = ensure_levels(ctx, K);
+    if (st != QVQ_OK) return st;
+    if ((st = ensure_kahan(ctx, K)) != QVQ_OK) return st;
+    HIPCHK(hipMemcpy(ctx->d_A, assign, ctx->N * 4, hipMemcpyHostToDevice));
+    HIPCHK(launch_kahan_centroids(ctx->stream, ctx->kw, ctx->d_codes, ctx->Dp, ctx->D, ctx->N,
+                                  K == 1 ? nullptr : ctx->d_A, K, ctx->d_kc_cent, nullptr));
+    const uint64_t cB = (uint64_t)K * ctx->D * 8;
+    if ((st = ensure_pinned(ctx, ctx->h_stage, ctx->stage_bytes, cB)) != QVQ_OK) return st;
+    HIPCHK(hipMemcpyAsync(ctx->h_stage, ctx->d_kc_cent, cB, hipMemcpyDeviceToHost, ctx->stream));
+    if ((st = wait_stream(ctx)) != QVQ_OK) return st;
+    if (C_out) std::memcpy(C_out, ctx->h_stage, cB);
+    if (env_is("QVQ_KAHAN_DEBUG", "1")) {
+        unsigned ms[4];
+        HIPCHK(hipMemcpy(ms, ctx->kw.stats, sizeof(ms), hipMemcpyDeviceToHost));
+        HIPCHK(hipMemset(ctx->kw.stats, 0, sizeof(ms)));
+        std::fprintf(stderr, "qvq kahan: K %u blocks not composable %u block misses %u replays %u\n", K, ms[0], ms[1],
+                     ms[2]);
+    }
     return QVQ_OK;
 }
 

@@ -1,299 +1,580 @@
 // k_kahan.hip -- the reference's Kahan centroids (sumInArea, src/Quantizer.cpp:59-87) on the
-// device, exactly, for the byte engine's SCALED values: the rows sorted stably by their index,
-// one chain per (code vector, component), each chain cut into segments whose tables compose
-// (kahan_par.hpp).  Used on the levels whose tie band is not empty.
+// device, exactly, for the byte engine's SCALED values (kahan_par.hpp has the arithmetic).
+// Used on the levels whose tie band is not empty.
+//
+// Pipeline (one stream):
+//   1. stable counting sort of the rows by cell: per-4096-row histograms, column scan, cell
+//      offsets, then a wave per 4096 rows writes each row's sorted position in row order;
+//   2. gather: planes[d][p] = component d of the p-th sorted row (16 positions per thread);
+//   3. meta: a wave per block of 64 segments (64 steps each) of one chain and component:
+//      each lane's SegMeta, the block's total;
+//   4. block prefix: per chain and component, the exact sums before each block;
+//   5. build: a wave per block: each lane builds its segment's function (estimate D = 0), the
+//      wave composes the 64 into the block's function;
+//   6. eval: a wave per chain and component: the transient, block functions checked, blocks
+//      whose function does not answer re-walked segment by segment with the exact state
+//      (segments that do not answer replayed step by step); C = sum * fl(1/n), and the split.
 #include <hip/hip_runtime.h>
-#include <hipcub/hipcub.hpp>
 
 #include "common.hpp"
 #include "kahan_par.hpp"
 
+#define QVQ_FOR_EACH_DP(X) X(4) X(8) X(12) X(16) X(20) X(24) X(28) X(32) X(36) X(40) X(44) X(48) X(52) X(56) X(60) X(64)
+
 namespace qvq {
 
-using kahan::Chain;
+using kahan::ByteTab;
 using kahan::Fn;
 using kahan::i128;
+using kahan::SegMeta;
 using kahan::u128;
+using kahan::L;
+using kahan::SPB;
 
 namespace {
 
-constexpr int KT = 256;   // threads per block
+constexpr uint32_t SROWS = 4096;   // rows per sort block (one wave)
+constexpr uint32_t BLK_STEPS = L * SPB;
 
-__device__ inline uint32_t find_cell(const uint32_t *off, uint32_t K, uint32_t s) {   // off[k] <= s < off[k+1]
-    uint32_t lo = 0, hi = K;
-    while (hi - lo > 1) {
-        const uint32_t mid = (lo + hi) / 2;
-        if (off[mid] <= s) lo = mid;
-        else hi = mid;
-    }
-    return lo;
+__device__ inline uint32_t lane_id() { return threadIdx.x & 63; }
+// LDS written by other lanes of the same wave becomes visible to this lane (waves of one
+// workgroup work on independent chains here, so no workgroup barrier after the table staging)
+__device__ inline void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+    __builtin_amdgcn_wave_barrier();
 }
 
-// koff[k] = first sorted position with key >= k (keys sorted ascending)
-__global__ void kc_koff_kernel(const uint32_t *__restrict__ keys, uint64_t N, uint32_t K, uint32_t *__restrict__ koff) {
-    const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
-    if (k > K) return;
-    uint64_t lo = 0, hi = N;
-    while (lo < hi) {
-        const uint64_t mid = (lo + hi) / 2;
-        if (keys[mid] < k) lo = mid + 1;
-        else hi = mid;
-    }
-    koff[k] = (uint32_t)lo;
+// ---- 1. stable counting sort --------------------------------------------------------------------
+__global__ __launch_bounds__(64) void ks_hist_kernel(const uint32_t *__restrict__ A, uint64_t N, uint32_t K,
+                                                    uint32_t *__restrict__ hist) {
+    extern __shared__ uint32_t h[];
+    for (uint32_t i = threadIdx.x; i < K; i += 64) h[i] = 0;
+    __syncthreads();
+    const uint64_t r0 = (uint64_t)blockIdx.x * SROWS, r1 = min(N, r0 + SROWS);
+    for (uint64_t r = r0 + threadIdx.x; r < r1; r += 64) atomicAdd(&h[A[r]], 1u);
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < K; i += 64) hist[(uint64_t)blockIdx.x * K + i] = h[i];
 }
 
-// Per cell: segments (L), groups (L*S), supergroups (L*S*S); exclusive scans into off[3][K+1].
-// One block, each thread a contiguous run of cells.
-__global__ __launch_bounds__(1024) void kc_offsets_kernel(const uint32_t *__restrict__ koff, uint32_t K, uint32_t L,
-                                                          uint32_t S, uint32_t *__restrict__ off) {
+// hist[g][k] <- rows of blocks before g with index k (exclusive, in place); tot[k]
+__global__ __launch_bounds__(256) void ks_colscan_kernel(uint32_t *__restrict__ hist, uint32_t G, uint32_t K,
+                                                        uint32_t *__restrict__ tot) {
+    const uint32_t k = blockIdx.x * 256 + threadIdx.x;
+    if (k >= K) return;
+    uint32_t s = 0;
+    constexpr uint32_t CU = 16;
+    for (uint32_t g0 = 0; g0 < G; g0 += CU) {
+        uint32_t v[CU];
+#pragma unroll
+        for (uint32_t u = 0; u < CU; u++) v[u] = hist[(uint64_t)min(g0 + u, G - 1) * K + k];
+#pragma unroll
+        for (uint32_t u = 0; u < CU; u++)
+            if (g0 + u < G) {
+                hist[(uint64_t)(g0 + u) * K + k] = s;
+                s += v[u];
+            }
+    }
+    tot[k] = s;
+}
+
+// koff[k] = rows with index < k, koff[K] = N; seg/blk offsets of the chains (64-step segments,
+// 64-segment blocks).  One block of 1024 threads.
+__global__ __launch_bounds__(1024) void ks_offsets_kernel(const uint32_t *__restrict__ tot, uint32_t K,
+                                                         uint32_t *__restrict__ koff, uint32_t *__restrict__ segoff,
+                                                         uint32_t *__restrict__ blkoff) {
     __shared__ uint32_t part[3][1024];
     const uint32_t per = (K + 1023) / 1024, b = min(K, threadIdx.x * per), e = min(K, b + per);
-    const uint64_t span[3] = {L, (uint64_t)L * S, (uint64_t)L * S * S};
     uint32_t s[3] = {0, 0, 0};
-    for (uint32_t k = b; k < e; k++) {
-        const uint64_t n = koff[k + 1] - koff[k];
-        for (int l = 0; l < 3; l++) s[l] += (uint32_t)((n + span[l] - 1) / span[l]);
+    for (uint32_t i = b; i < e; i++) {
+        const uint32_t n = tot[i], ns = (n + L - 1) / L;
+        s[0] += n;
+        s[1] += ns;
+        s[2] += (ns + SPB - 1) / SPB;
     }
     for (int l = 0; l < 3; l++) part[l][threadIdx.x] = s[l];
     __syncthreads();
-    for (int o = 1; o < 1024; o <<= 1) {
+    for (uint32_t o = 1; o < 1024; o <<= 1) {
         uint32_t v[3];
-        for (int l = 0; l < 3; l++) v[l] = threadIdx.x >= (uint32_t)o ? part[l][threadIdx.x - o] : 0u;
+        for (int l = 0; l < 3; l++) v[l] = threadIdx.x >= o ? part[l][threadIdx.x - o] : 0u;
         __syncthreads();
         for (int l = 0; l < 3; l++) part[l][threadIdx.x] += v[l];
         __syncthreads();
     }
     uint32_t base[3];
     for (int l = 0; l < 3; l++) base[l] = part[l][threadIdx.x] - s[l];
-    for (uint32_t k = b; k < e; k++) {
-        const uint64_t n = koff[k + 1] - koff[k];
-        for (int l = 0; l < 3; l++) {
-            off[(uint64_t)l * (K + 1) + k] = base[l];
-            base[l] += (uint32_t)((n + span[l] - 1) / span[l]);
+    for (uint32_t i = b; i < e; i++) {
+        const uint32_t n = tot[i], ns = (n + L - 1) / L;
+        koff[i] = base[0];
+        segoff[i] = base[1];
+        blkoff[i] = base[2];
+        base[0] += n;
+        base[1] += ns;
+        base[2] += (ns + SPB - 1) / SPB;
+    }
+    if (threadIdx.x == 1023) {
+        koff[K] = part[0][1023];
+        segoff[K] = part[1][1023];
+        blkoff[K] = part[2][1023];
+    }
+}
+
+// order[koff[k] + rank] = row, rank in row order within cell k (stable).  A wave per 4096 rows,
+// 64-row chunks in order; the lanes of one index in a chunk are ranked by a ballot.
+__global__ __launch_bounds__(64) void ks_scatter_kernel(const uint32_t *__restrict__ A, uint64_t N, uint32_t K,
+                                                       const uint32_t *__restrict__ hist,
+                                                       const uint32_t *__restrict__ koff, uint32_t *__restrict__ order) {
+    extern __shared__ uint32_t cur[];
+    for (uint32_t i = threadIdx.x; i < K; i += 64) cur[i] = koff[i] + hist[(uint64_t)blockIdx.x * K + i];
+    __syncthreads();
+    const uint32_t lane = lane_id();
+    const uint64_t lt = (1ull << lane) - 1;
+    const uint64_t r0 = (uint64_t)blockIdx.x * SROWS, r1 = min(N, r0 + SROWS);
+    for (uint64_t base = r0; base < r1; base += 64) {
+        const uint64_t r = base + lane;
+        const bool in = r < r1;
+        const uint32_t key = in ? A[r] : 0xFFFFFFFFu;
+        uint64_t active = __ballot(in);
+        while (active) {
+            const int leader = __ffsll((long long)active) - 1;
+            const uint32_t kl = __shfl(key, leader, 64);
+            const uint64_t m = __ballot(key == kl) & active;
+            const uint32_t c = cur[kl];
+            if (key == kl && in) order[c + __popcll(m & lt)] = (uint32_t)r;
+            __syncthreads();   // one wave: orders the LDS read before the update
+            if (lane == (uint32_t)leader) cur[kl] = c + (uint32_t)__popcll(m);
+            __syncthreads();
+            active &= ~m;
         }
     }
-    if (threadIdx.x == 1023)
-        for (int l = 0; l < 3; l++) off[(uint64_t)l * (K + 1) + K] = part[l][1023];
 }
 
-// planes[d][p] = codes[order[p]][d] (order null: row p)
-__global__ void kc_gather_kernel(const uint8_t *__restrict__ codes, uint32_t Dp, uint32_t D, uint64_t N,
-                                 const uint32_t *__restrict__ order, uint8_t *__restrict__ planes) {
-    for (uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; p < N; p += (uint64_t)gridDim.x * blockDim.x) {
+// ---- 2. gather ------------------------------------------------------------------------------
+// planes[d][p] = component d of row order[p] (order null: row p).  16 positions per thread.
+template <int DP>
+constexpr int gather_pos() { return DP <= 16 ? 16 : 4; }
+template <int DP>
+__global__ __launch_bounds__(256) void ks_gather_kernel(const uint8_t *__restrict__ codes, uint64_t N, uint32_t D,
+                                                       const uint32_t *__restrict__ order, uint64_t PL,
+                                                       uint8_t *__restrict__ planes) {
+    constexpr int W = DP / 4, NP = gather_pos<DP>();
+    const uint64_t p0 = ((uint64_t)blockIdx.x * 256 + threadIdx.x) * NP;
+    if (p0 >= N) return;
+    uint32_t w[NP][W];
+#pragma unroll
+    for (int i = 0; i < NP; i++) {
+        const uint64_t p = min(p0 + i, N - 1);
         const uint64_t row = order ? order[p] : p;
-        const uint8_t *src = codes + row * Dp;
-        for (uint32_t d = 0; d < D; d++) planes[(uint64_t)d * N + p] = src[d];
+        const uint32_t *src = reinterpret_cast<const uint32_t *>(codes + row * DP);
+#pragma unroll
+        for (int u = 0; u < W; u++) w[i][u] = src[u];
+    }
+#pragma unroll
+    for (int d = 0; d < DP; d++) {
+        if ((uint32_t)d >= D) continue;
+        uint32_t o[NP / 4];
+#pragma unroll
+        for (int q = 0; q < NP / 4; q++) {
+            uint32_t v = 0;
+#pragma unroll
+            for (int t = 0; t < 4; t++) v |= ((w[4 * q + t][d >> 2] >> (8 * (d & 3))) & 0xFFu) << (8 * t);
+            o[q] = v;
+        }
+        if constexpr (NP == 16)
+            *reinterpret_cast<uint4 *>(planes + (uint64_t)d * PL + p0) = make_uint4(o[0], o[1], o[2], o[3]);
+        else
+            *reinterpret_cast<uint32_t *>(planes + (uint64_t)d * PL + p0) = o[0];
     }
 }
 
-struct Geo {   // where the chains live
+// ---- shared: blocks of a chain ---------------------------------------------------------------
+struct Geo {
     const uint8_t *planes;
-    uint64_t N;
-    const uint32_t *koff, *off;   // off: [3][K+1] segment / group / supergroup offsets
-    uint32_t K, D, L, S;
-    Fn *fn0, *fn1, *fn2;
-    uint32_t NS, NG, NU;          // capacities per component
-    __device__ Chain chain(uint32_t k, uint32_t d, const uint64_t *Xt) const {
-        Chain c;
-        c.b = planes + (uint64_t)d * N + koff[k];
-        c.Xt = Xt;
-        c.n = koff[k + 1] - koff[k];
-        c.f0 = fn0 + (uint64_t)d * NS + off[k];
-        c.f1 = fn1 + (uint64_t)d * NG + off[(K + 1) + k];
-        c.f2 = fn2 + (uint64_t)d * NU + off[2 * (K + 1) + k];
-        c.L = L;
-        c.S = S;
-        return c;
-    }
+    uint64_t PL;                              // plane stride (N rounded up, plus padding)
+    const uint32_t *koff, *segoff, *blkoff;   // [K + 1] each
+    uint32_t K, D;
+    SegMeta *meta;                            // [D][segoff[K]]
+    u128 *bsum;                               // [D][blkoff[K]]: block totals, then (scan) block prefixes
+    Fn *bfn;                                  // [D][blkoff[K]]
+    unsigned *stats;                          // [4]: blocks not composable, block misses, segment replays, chains
 };
 
-__device__ inline void stage_xt(const uint64_t *__restrict__ g, uint64_t *s) {
-    for (int i = threadIdx.x; i < 256; i += blockDim.x) s[i] = g[i];
+__device__ inline void stage_tab(const ByteTab *__restrict__ g, ByteTab *t) {
+    const uint32_t *src = reinterpret_cast<const uint32_t *>(g);
+    uint32_t *dst = reinterpret_cast<uint32_t *>(t);
+    for (uint32_t i = threadIdx.x; i < sizeof(ByteTab) / 4; i += blockDim.x) dst[i] = src[i];
+}
+
+// cell of flat block index fb (blkoff in LDS)
+__device__ inline uint32_t find_cell(const uint32_t *off, uint32_t K, uint32_t v) {   // off[k] <= v < off[k+1]
+    uint32_t lo = 0, hi = K;
+    while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) / 2;
+        if (off[mid] <= v) lo = mid;
+        else hi = mid;
+    }
+    return lo;
+}
+
+// The wave stages the bytes [src, src + n) (n <= BLK_STEPS) into dst (4-byte aligned).
+__device__ inline void stage_bytes(const uint8_t *__restrict__ src, uint32_t n, uint8_t *dst) {
+    const uint32_t lane = lane_id();
+    const uintptr_t a = (uintptr_t)src, a0 = a & ~(uintptr_t)3;
+    const uint32_t m = (uint32_t)(a - a0);
+    const uint32_t *s32 = reinterpret_cast<const uint32_t *>(a0);
+    uint32_t *d32 = reinterpret_cast<uint32_t *>(dst);
+    const uint32_t nw = (n + 3) / 4;
+    for (uint32_t i = lane; i < nw; i += 64) {
+        const uint32_t lo = s32[i], hi = m ? s32[i + 1] : 0u;   // planes are padded past the end
+        d32[i] = m ? (uint32_t)(((uint64_t)hi << 32 | lo) >> (8 * m)) : lo;
+    }
+}
+
+// ---- 3. meta ---------------------------------------------------------------------------------
+constexpr int WPB = 4;   // waves per workgroup (meta, build)
+
+__global__ __launch_bounds__(64 * WPB) void ks_meta_kernel(Geo g, const ByteTab *__restrict__ gtab) {
+    __shared__ ByteTab tab;
+    __shared__ __attribute__((aligned(16))) uint8_t bytes[WPB][BLK_STEPS];
+    stage_tab(gtab, &tab);
     __syncthreads();
-}
-
-// Exact sum of X over each segment: P0[d][seg] (then scanned per chain into the prefixes).
-__global__ __launch_bounds__(KT) void kc_segsum_kernel(Geo g, const uint64_t *__restrict__ gXt, i128 *__restrict__ P0) {
-    __shared__ uint64_t Xt[256];
-    stage_xt(gXt, Xt);
-    const uint32_t tot = g.off[g.K];
-    for (uint64_t t = (uint64_t)blockIdx.x * KT + threadIdx.x; t < (uint64_t)tot * g.D; t += (uint64_t)gridDim.x * KT) {
-        const uint32_t d = (uint32_t)(t / tot), seg = (uint32_t)(t - (uint64_t)d * tot);
-        const uint32_t k = find_cell(g.off, g.K, seg);
-        const uint64_t a = g.koff[k] + (uint64_t)(seg - g.off[k]) * g.L;
-        const uint64_t e = min((uint64_t)g.koff[k + 1], a + g.L);
-        const uint8_t *b = g.planes + (uint64_t)d * g.N;
-        u128 s = 0;
-        for (uint64_t p = a; p < e; p++) s += Xt[b[p]];
-        P0[(uint64_t)d * g.NS + seg] = (i128)s;
+    const uint32_t w = threadIdx.x >> 6, lane = lane_id();
+    const uint32_t TB = g.blkoff[g.K];
+    const uint64_t fb = (uint64_t)blockIdx.x * WPB + w;
+    if (fb >= (uint64_t)TB * g.D) return;
+    const uint32_t d = (uint32_t)(fb / TB), bb = (uint32_t)(fb - (uint64_t)d * TB);
+    const uint32_t k = find_cell(g.blkoff, g.K, bb), b = bb - g.blkoff[k];
+    const uint32_t n = g.koff[k + 1] - g.koff[k];
+    const uint32_t s0 = b * SPB, first = s0 * L, nb = min(BLK_STEPS, n - first);
+    stage_bytes(g.planes + (uint64_t)d * g.PL + g.koff[k] + first, nb, bytes[w]);
+    wave_sync();
+    const uint32_t s = s0 + lane, nseg = (n + L - 1) / L;
+    u128 tot = 0;
+    if (s < nseg) {
+        const uint32_t len = min(L, n - s * L);
+        const SegMeta m = kahan::seg_meta(tab, bytes[w] + lane * L, len);
+        g.meta[(uint64_t)d * g.segoff[g.K] + g.segoff[k] + s] = m;
+        tot = kahan::meta_sum(m);
     }
+    uint64_t lo = (uint64_t)tot, hi = (uint64_t)(tot >> 64);
+    for (int o = 32; o >= 1; o >>= 1) {   // wave sum of the block's segments (128-bit)
+        const uint64_t l2 = __shfl_xor((unsigned long long)lo, o, 64), h2 = __shfl_xor((unsigned long long)hi, o, 64);
+        const uint64_t t = lo + l2;
+        hi = hi + h2 + (t < lo);
+        lo = t;
+    }
+    if (lane == 0) g.bsum[(uint64_t)d * TB + bb] = ((u128)hi << 64) | lo;
 }
 
-// Exclusive scan of the segment sums along every chain: a wave per (cell, component).
-__global__ __launch_bounds__(KT) void kc_prefix_kernel(Geo g, i128 *__restrict__ P0) {
-    const uint32_t lane = threadIdx.x & 63;
-    const uint64_t w = ((uint64_t)blockIdx.x * KT + threadIdx.x) >> 6;
-    if (w >= (uint64_t)g.K * g.D) return;
-    const uint32_t k = (uint32_t)(w / g.D), d = (uint32_t)(w - (uint64_t)k * g.D);
-    const uint32_t s0 = g.off[k], s1 = g.off[k + 1];
-    i128 *p = P0 + (uint64_t)d * g.NS;
+// ---- 4. block prefixes: exclusive scan of the block totals along every chain --------------------
+__global__ __launch_bounds__(256) void ks_bscan_kernel(Geo g) {
+    const uint32_t lane = lane_id();
+    const uint64_t wv = ((uint64_t)blockIdx.x * 256 + threadIdx.x) >> 6;
+    if (wv >= (uint64_t)g.K * g.D) return;
+    const uint32_t k = (uint32_t)(wv / g.D), d = (uint32_t)(wv - (uint64_t)k * g.D);
+    const uint32_t TB = g.blkoff[g.K];
+    u128 *p = g.bsum + (uint64_t)d * TB;
+    const uint32_t b0 = g.blkoff[k], b1 = g.blkoff[k + 1];
     u128 carry = 0;
-    for (uint32_t base = s0; base < s1; base += 64) {
-        const uint32_t s = base + lane;
-        u128 v = s < s1 ? (u128)p[s] : 0, inc = v;
+    for (uint32_t base = b0; base < b1; base += 64) {
+        const uint32_t i = base + lane;
+        const u128 v = i < b1 ? p[i] : 0;
+        u128 inc = v;
         for (int o = 1; o < 64; o <<= 1) {
-            const uint64_t lo = __shfl_up((unsigned long long)(uint64_t)inc, o, 64);
-            const uint64_t hi = __shfl_up((unsigned long long)(uint64_t)(inc >> 64), o, 64);
-            if (lane >= (uint32_t)o) inc += ((u128)hi << 64) | lo;
+            const uint64_t l = __shfl_up((unsigned long long)(uint64_t)inc, o, 64);
+            const uint64_t h = __shfl_up((unsigned long long)(uint64_t)(inc >> 64), o, 64);
+            if (lane >= (uint32_t)o) inc += ((u128)h << 64) | l;
         }
-        if (s < s1) p[s] = (i128)(carry + inc - v);
-        const uint64_t tlo = __shfl((unsigned long long)(uint64_t)inc, 63, 64);
-        const uint64_t thi = __shfl((unsigned long long)(uint64_t)(inc >> 64), 63, 64);
-        carry += ((u128)thi << 64) | tlo;
+        if (i < b1) p[i] = carry + inc - v;
+        const uint64_t tl = __shfl((unsigned long long)(uint64_t)inc, 63, 64);
+        const uint64_t th = __shfl((unsigned long long)(uint64_t)(inc >> 64), 63, 64);
+        carry += ((u128)th << 64) | tl;
     }
 }
 
-// Segment tables: P0 holds each segment's exact prefix; Etr (pass 2, may be null) the trusted
-// walk's state at each segment start, the better estimate.
-__global__ __launch_bounds__(KT) void kc_build_kernel(Geo g, const uint64_t *__restrict__ gXt,
-                                                      const i128 *__restrict__ P0, const i128 *__restrict__ Etr) {
-    __shared__ uint64_t Xt[256];
-    stage_xt(gXt, Xt);
-    const uint32_t tot = g.off[g.K];
-    for (uint64_t t = (uint64_t)blockIdx.x * KT + threadIdx.x; t < (uint64_t)tot * g.D; t += (uint64_t)gridDim.x * KT) {
-        const uint32_t d = (uint32_t)(t / tot), seg = (uint32_t)(t - (uint64_t)d * tot);
-        const uint32_t k = find_cell(g.off, g.K, seg);
-        const uint64_t a = g.koff[k] + (uint64_t)(seg - g.off[k]) * g.L;
-        const uint32_t len = (uint32_t)min((uint64_t)g.L, (uint64_t)g.koff[k + 1] - a);
-        const uint64_t idx = (uint64_t)d * g.NS + seg;
-        const i128 P = P0[idx];
-        const int64_t dest = Etr ? (int64_t)(Etr[idx] - P) : 0;
-        g.fn0[idx] = kahan::build_segment(g.planes + (uint64_t)d * g.N + a, Xt, len, P, dest);
+// Exclusive wave scan of 128-bit values.
+__device__ inline u128 wave_excl_scan(u128 v) {
+    const uint32_t lane = lane_id();
+    u128 inc = v;
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint64_t l = __shfl_up((unsigned long long)(uint64_t)inc, o, 64);
+        const uint64_t h = __shfl_up((unsigned long long)(uint64_t)(inc >> 64), o, 64);
+        if (lane >= (uint32_t)o) inc += ((u128)h << 64) | l;
+    }
+    return inc - v;
+}
+
+// Each lane's function for segment b * SPB + lane of chain (k, d) (the block's bytes already in
+// `bytes`), estimate D_est, into fns[lane]; returns the exact prefix sum at the segment's start.
+// Lanes past the chain's end get an empty translation.
+__device__ inline u128 build_block_fns(const Geo &g, const ByteTab &tab, const uint8_t *bytes, uint32_t k, uint32_t d,
+                                       uint32_t b, int64_t D_est, Fn *fns) {
+    const uint32_t lane = lane_id();
+    const uint32_t n = g.koff[k + 1] - g.koff[k], nseg = (n + L - 1) / L;
+    const uint32_t s = b * SPB + lane;
+    const uint64_t mbase = (uint64_t)d * g.segoff[g.K] + g.segoff[k];
+    SegMeta self{};
+    if (s < nseg) self = g.meta[mbase + s];
+    const u128 P = g.bsum[(uint64_t)d * g.blkoff[g.K] + g.blkoff[k] + b] +
+                   wave_excl_scan(s < nseg ? kahan::meta_sum(self) : (u128)0);
+    Fn f;
+    if (s < nseg) {
+        SegMeta prev[8];
+        int np = 0;
+        for (int i = 1; i <= 8 && (int64_t)s - i >= 0; i++) {
+            prev[np++] = g.meta[mbase + s - i];
+            if (prev[np - 1].cmax >= 0) break;
+        }
+        kahan::build_fn(tab, bytes + lane * L, min(L, n - s * L), P, self, prev, np, s + 1 == nseg, D_est, f);
+    } else {
+        f.kind = kahan::FK_TRANS;
+        f.c_in = f.lne = f.c_out = 0;
+        f.off_in = f.off_out = f.sx9 = f.pad = 0;
+        f.lo = f.hi = 0;
+        for (int e = 0; e < kahan::NE; e++) f.dlt[e] = 0;
+    }
+    fns[lane] = f;
+    return P;
+}
+
+// ---- 5. build: block functions ------------------------------------------------------------------
+__global__ __launch_bounds__(64 * WPB) void ks_build_kernel(Geo g, const ByteTab *__restrict__ gtab) {
+    __shared__ ByteTab tab;
+    __shared__ __attribute__((aligned(16))) uint8_t bytes[WPB][BLK_STEPS];
+    __shared__ Fn fns[WPB][SPB];
+    __shared__ uint8_t ok[WPB][SPB];
+    stage_tab(gtab, &tab);
+    __syncthreads();
+    const uint32_t w = threadIdx.x >> 6, lane = lane_id();
+    const uint32_t TB = g.blkoff[g.K];
+    const uint64_t fb = (uint64_t)blockIdx.x * WPB + w;
+    if (fb >= (uint64_t)TB * g.D) return;
+    const uint32_t d = (uint32_t)(fb / TB), bb = (uint32_t)(fb - (uint64_t)d * TB);
+    const uint32_t k = find_cell(g.blkoff, g.K, bb), b = bb - g.blkoff[k];
+    const uint32_t n = g.koff[k + 1] - g.koff[k];
+    const uint32_t first = b * BLK_STEPS;
+    stage_bytes(g.planes + (uint64_t)d * g.PL + g.koff[k] + first, min(BLK_STEPS, n - first), bytes[w]);
+    wave_sync();
+    build_block_fns(g, tab, bytes[w], k, d, b, 0, fns[w]);
+    const uint32_t nseg = (n + L - 1) / L, cnt = min(SPB, nseg - b * SPB);
+    ok[w][lane] = kahan::fkind(fns[w][lane]) != kahan::FK_RAW;
+    wave_sync();
+    for (uint32_t st = 1; st < SPB; st <<= 1) {   // tree: fns[i] <- fns[i] then fns[i + st]
+        if ((lane & (2 * st - 1)) == 0 && lane + st < cnt) {
+            Fn h;
+            const bool c = ok[w][lane] && ok[w][lane + st] && kahan::compose(fns[w][lane], fns[w][lane + st], h);
+            ok[w][lane] = c;
+            if (c) fns[w][lane] = h;
+        }
+        wave_sync();
+    }
+    if (lane == 0) {
+        Fn r = fns[w][0];
+        if (!ok[w][0]) {
+            kahan::set_raw(r);
+            if (g.stats) atomicAdd(&g.stats[0], 1u);
+        }
+        g.bfn[(uint64_t)d * TB + bb] = r;
     }
 }
 
-// Groups (level 1) or supergroups (level 2): a thread per (function, component).
-template <int LEVEL>
-__global__ __launch_bounds__(KT) void kc_compose_kernel(Geo g, const uint64_t *__restrict__ gXt) {
-    __shared__ uint64_t Xt[256];
-    stage_xt(gXt, Xt);
-    const uint32_t *off = g.off + (uint64_t)LEVEL * (g.K + 1);
-    const uint32_t tot = off[g.K];
-    for (uint64_t t = (uint64_t)blockIdx.x * KT + threadIdx.x; t < (uint64_t)tot * g.D; t += (uint64_t)gridDim.x * KT) {
-        const uint32_t d = (uint32_t)(t / tot), f = (uint32_t)(t - (uint64_t)d * tot);
-        const uint32_t k = find_cell(off, g.K, f);
-        const Chain c = g.chain(k, d, Xt);
-        if (LEVEL == 1) g.fn1[(uint64_t)d * g.NG + f] = kahan::compose1(c, f - off[k]);
-        else g.fn2[(uint64_t)d * g.NU + f] = kahan::compose2(c, f - off[k]);
-    }
+// ---- 6. eval ----------------------------------------------------------------------------------
+constexpr int EPB = 4;   // chains per workgroup (a wave each)
+
+__device__ inline u128 bcast_u128(u128 v) {
+    return ((u128)(uint64_t)__shfl((unsigned long long)(uint64_t)(v >> 64), 0, 64) << 64) |
+           (uint64_t)__shfl((unsigned long long)(uint64_t)v, 0, 64);
 }
 
-// Trusted walk over a chain's pass-1 tables: the estimated state at every segment start.
-__global__ __launch_bounds__(KT) void kc_trust_kernel(Geo g, const uint64_t *__restrict__ gXt, const i128 *__restrict__ P0,
-                                                      i128 *__restrict__ Etr) {
-    __shared__ uint64_t Xt[256];
-    stage_xt(gXt, Xt);
-    for (uint64_t t = (uint64_t)blockIdx.x * KT + threadIdx.x; t < (uint64_t)g.K * g.D; t += (uint64_t)gridDim.x * KT) {
-        const uint32_t k = (uint32_t)(t / g.D), d = (uint32_t)(t - (uint64_t)k * g.D);
-        const Chain c = g.chain(k, d, Xt);
-        const uint64_t base = (uint64_t)d * g.NS + g.off[k];
-        const uint64_t nseg = (c.n + c.L - 1) / c.L;
-        // estimate_dest writes E - P; keep E itself (pass 2 adds back nothing)
-        int64_t *dest = reinterpret_cast<int64_t *>(Etr + base);   // scratch: one int64 per segment first
-        kahan::estimate_dest(c, P0 + base, dest);
-        for (uint64_t s = nseg; s-- > 0;) Etr[base + s] = P0[base + s] + (i128)dest[s];
+__global__ __launch_bounds__(64 * EPB) void ks_eval_kernel(Geo g, const ByteTab *__restrict__ gtab,
+                                                          double *__restrict__ C, double *__restrict__ split_out) {
+    __shared__ ByteTab tab;
+    __shared__ __attribute__((aligned(16))) uint8_t bytes[EPB][BLK_STEPS];
+    __shared__ Fn fns[EPB][SPB];
+    __shared__ u128 pseg[EPB][SPB];
+    stage_tab(gtab, &tab);
+    __syncthreads();
+    const uint32_t w = threadIdx.x >> 6, lane = lane_id();
+    const uint64_t wv = (uint64_t)blockIdx.x * EPB + w;
+    if (wv >= (uint64_t)g.K * g.D) return;
+    const uint32_t k = (uint32_t)(wv / g.D), d = (uint32_t)(wv - (uint64_t)k * g.D);
+    const uint32_t n = g.koff[k + 1] - g.koff[k], nseg = (n + L - 1) / L;
+    const uint8_t *src = g.planes + (uint64_t)d * g.PL + g.koff[k];
+    const uint32_t TB = g.blkoff[g.K];
+    const u128 *bpre = g.bsum + (uint64_t)d * TB + g.blkoff[k];
+    const uint64_t mbase = (uint64_t)d * g.segoff[g.K] + g.segoff[k];
+    double result = 0.0;
+    if (n) {
+        // the transient: the reference's doubles until sum >= 2 (lane 0; bytes staged per block)
+        uint32_t i = 0, staged = 0xFFFFFFFFu;
+        double sum = 0, c = 0;
+        u128 P = 0;
+        while (i < n && !(sum >= 2.0)) {
+            const uint32_t b = i / BLK_STEPS;
+            if (b != staged) {
+                stage_bytes(src + b * BLK_STEPS, min(BLK_STEPS, n - b * BLK_STEPS), bytes[w]);
+                wave_sync();
+                staged = b;
+            }
+            const uint32_t e = min(n, (b + 1) * BLK_STEPS);
+            if (lane == 0)
+                while (i < e && !(sum >= 2.0)) {
+                    const uint64_t X = tab.X[bytes[w][i - b * BLK_STEPS]];
+                    kahan::fstep(sum, c, ldexp((double)X, -60));
+                    P += X;
+                    i++;
+                }
+            i = __shfl(i, 0, 64);
+            sum = __shfl(sum, 0, 64);
+            c = __shfl(c, 0, 64);
+            P = bcast_u128(P);
+        }
+        if (!(sum >= 2.0)) {
+            result = sum;
+        } else {
+            const u128 E = (u128)(kahan::to_units(sum) - kahan::to_units(c));
+            int64_t D = (int64_t)(E - P);
+            uint32_t F = (uint32_t)E & 511;
+            uint32_t j = (i + L - 1) / L;
+            if (i % L) {   // exactly to the next segment boundary (inside the staged block)
+                const uint32_t e = min(n, j * L);
+                if (lane == 0) {
+                    int32_t ds;
+                    int64_t lo = -kahan::DLIM, hi = kahan::DLIM;
+                    kahan::sim<true>(tab, bytes[w] + (i - staged * BLK_STEPS), e - i, P, 0, F, D, ds, lo, hi);
+                    D += ds;
+                }
+                D = __shfl((long long)D, 0, 64);
+                F = __shfl(F, 0, 64);
+            }
+            unsigned nmiss = 0, nrep = 0;
+            while (j < nseg) {
+                const uint32_t b = j / SPB;
+                if (j % SPB == 0) {
+                    const Fn f = g.bfn[(uint64_t)d * TB + g.blkoff[k] + b];   // every lane: uniform
+                    if (kahan::apply(f, F, D)) {
+                        j = min(nseg, j + SPB);
+                        continue;
+                    }
+                    nmiss++;
+                }
+                // segment by segment: the block's functions built from the exact D
+                if (staged != b) {
+                    stage_bytes(src + b * BLK_STEPS, min(BLK_STEPS, n - b * BLK_STEPS), bytes[w]);
+                    wave_sync();
+                    staged = b;
+                }
+                pseg[w][lane] = build_block_fns(g, tab, bytes[w], k, d, b, D, fns[w]);
+                wave_sync();
+                const uint32_t end = min(nseg, (b + 1) * SPB);
+                for (; j < end; j++) {
+                    const Fn f = fns[w][j - b * SPB];
+                    if (kahan::apply(f, F, D)) continue;
+                    nrep++;
+                    if (lane == 0) {
+                        int32_t ds;
+                        int64_t lo = -kahan::DLIM, hi = kahan::DLIM;
+                        kahan::sim<true>(tab, bytes[w] + (j - b * SPB) * L, min(L, n - j * L), pseg[w][j - b * SPB], 0,
+                                         F, D, ds, lo, hi);
+                        D += ds;
+                    }
+                    D = __shfl((long long)D, 0, 64);
+                    F = __shfl(F, 0, 64);
+                }
+                wave_sync();
+            }
+            // the exact total: the last block's prefix and its segments' sums
+            const uint32_t lb = (nseg - 1) / SPB, s = lb * SPB + lane;
+            u128 v = s < nseg ? kahan::meta_sum(g.meta[mbase + s]) : (u128)0;
+            uint64_t lo = (uint64_t)v, hi = (uint64_t)(v >> 64);
+            for (int o = 32; o >= 1; o >>= 1) {
+                const uint64_t l2 = __shfl_xor((unsigned long long)lo, o, 64), h2 = __shfl_xor((unsigned long long)hi, o, 64);
+                const uint64_t t = lo + l2;
+                hi = hi + h2 + (t < lo);
+                lo = t;
+            }
+            const u128 Pn = bpre[lb] + (((u128)hi << 64) | lo);
+            result = kahan::to_double(Pn + (u128)(i128)D);
+            if (g.stats && lane == 0 && (nmiss | nrep)) {
+                atomicAdd(&g.stats[1], nmiss);
+                atomicAdd(&g.stats[2], nrep);
+            }
+        }
+        result = __dmul_rn(result, 1.0 / (double)n);   // operator/= by a scalar under -freciprocal-math
     }
-}
-
-// Every chain evaluated exactly: C[k][d] = Kahan sum * fl(1/n) (empty cell: 0).
-__global__ __launch_bounds__(KT) void kc_eval_kernel(Geo g, const uint64_t *__restrict__ gXt, double *__restrict__ C,
-                                                     unsigned *__restrict__ stats) {
-    __shared__ uint64_t Xt[256];
-    stage_xt(gXt, Xt);
-    for (uint64_t t = (uint64_t)blockIdx.x * KT + threadIdx.x; t < (uint64_t)g.K * g.D; t += (uint64_t)gridDim.x * KT) {
-        const uint32_t k = (uint32_t)(t / g.D), d = (uint32_t)(t - (uint64_t)k * g.D);
-        const Chain c = g.chain(k, d, Xt);
-        uint32_t miss[3] = {0, 0, 0};
-        double s = c.n ? kahan::eval_chain(c, miss) : 0.0;
-        if (c.n) s = __dmul_rn(s, 1.0 / (double)c.n);   // operator/= by a scalar under -freciprocal-math
-        C[t] = s;
-        if (stats && (miss[0] | miss[1] | miss[2])) {
-            atomicAdd(&stats[0], miss[0]);
-            atomicAdd(&stats[1], miss[1]);
-            atomicAdd(&stats[2], miss[2]);
+    if (lane == 0) {
+        const uint64_t t = (uint64_t)k * g.D + d;
+        C[t] = result;
+        if (split_out) {   // src/Quantizer.cpp:134-138: C * (1 + 0.2), then C * (1 - 0.2)
+            split_out[t] = __dmul_rn(result, (double)(1 + 0.2));
+            split_out[(uint64_t)g.K * g.D + t] = __dmul_rn(result, (double)(1 - 0.2));
         }
     }
 }
-
-// The split (src/Quantizer.cpp:134-138): S[k] = C[k] * (1 + 0.2), S[K + k] = C[k] * (1 - 0.2).
-__global__ void kc_split_kernel(const double *__restrict__ C, uint32_t K, uint32_t D, double *__restrict__ Sp) {
-    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= (uint64_t)K * D) return;
-    Sp[t] = __dmul_rn(C[t], (double)(1 + 0.2));
-    Sp[(uint64_t)K * D + t] = __dmul_rn(C[t], (double)(1 - 0.2));
-}
-
-int grid_of(uint64_t items) { return (int)std::max<uint64_t>(1, std::min<uint64_t>((items + KT - 1) / KT, 16384)); }
 
 }  // namespace
 
+// ---- host side -------------------------------------------------------------------------------
+size_t KahanWork::tab_bytes() { return sizeof(ByteTab); }
+
+void KahanWork::make_tab(const uint64_t *X, void *out) { kahan::make_tab(X, *reinterpret_cast<ByteTab *>(out)); }
+
+void KahanWork::caps(uint64_t N, uint32_t K, uint64_t &segs, uint64_t &blks) {
+    segs = (N + L - 1) / L + K;
+    blks = segs / SPB + K + 1;
+}
+uint64_t KahanWork::plane_len(uint64_t N) { return (N + 63) / 64 * 64 + 64; }
+size_t KahanWork::meta_bytes() { return sizeof(SegMeta); }
 size_t KahanWork::fn_bytes() { return sizeof(Fn); }
-
-// Capacity per component: every cell's last segment may be partial.
-void KahanWork::caps(uint64_t N, uint32_t K, uint32_t L, uint32_t S, uint32_t &NS, uint32_t &NG, uint32_t &NU) {
-    NS = (uint32_t)((N + L - 1) / L + K);
-    NG = (uint32_t)((N + (uint64_t)L * S - 1) / ((uint64_t)L * S) + K);
-    NU = (uint32_t)((N + (uint64_t)L * S * S - 1) / ((uint64_t)L * S * S) + K);
-}
-
-size_t kahan_sort_temp_bytes(uint64_t N) {
-    size_t bytes = 0;
-    (void)hipcub::DeviceRadixSort::SortPairs(nullptr, bytes, (const uint32_t *)nullptr, (uint32_t *)nullptr,
-                                             (const uint32_t *)nullptr, (uint32_t *)nullptr, (int)N);
-    return bytes;
-}
+uint32_t KahanWork::sort_blocks(uint64_t N) { return (uint32_t)((N + SROWS - 1) / SROWS); }
 
 hipError_t launch_kahan_centroids(hipStream_t s, const KahanWork &w, const uint8_t *codes, uint32_t Dp, uint32_t D,
-                                  uint64_t N, const uint32_t *A, uint32_t K, const uint64_t *Xt, double *C,
-                                  double *split_out, int passes) {
-    if (N == 0 || N > 0xFFFFFFFFull || D == 0 || K == 0) return hipErrorInvalidValue;
-    const uint32_t *order = nullptr;
+                                  uint64_t N, const uint32_t *A, uint32_t K, double *C, double *split_out) {
+    if (N == 0 || N > 0xFFFFFFFFull || D == 0 || K == 0 || D > Dp || Dp > 64 || (Dp & 3)) return hipErrorInvalidValue;
+    const uint32_t G = KahanWork::sort_blocks(N);
     if (A) {
-        int bits = 1;
-        while (bits < 32 && (1ull << bits) < K) bits++;
-        size_t tb = w.temp_bytes;
-        hipError_t e = hipcub::DeviceRadixSort::SortPairs(w.temp, tb, A, w.keys, (const uint32_t *)w.iota, w.order,
-                                                          (int)N, 0, bits, s);
-        if (e != hipSuccess) return e;
-        hipLaunchKernelGGL(kc_koff_kernel, dim3((K + 1 + 255) / 256), dim3(256), 0, s, w.keys, N, K, w.koff);
-        order = w.order;
+        hipLaunchKernelGGL(ks_hist_kernel, dim3(G), dim3(64), K * 4, s, A, N, K, w.hist);
+        hipLaunchKernelGGL(ks_colscan_kernel, dim3((K + 255) / 256), dim3(256), 0, s, w.hist, G, K, w.tot);
     } else {
         if (K != 1) return hipErrorInvalidValue;
-        const uint32_t ko[2] = {0, (uint32_t)N};
-        hipError_t e = hipMemcpyAsync(w.koff, ko, sizeof(ko), hipMemcpyHostToDevice, s);
+        hipError_t e = hipMemcpyAsync(w.tot, &w.n_one, 4, hipMemcpyHostToDevice, s);
         if (e != hipSuccess) return e;
     }
-    hipLaunchKernelGGL(kc_offsets_kernel, dim3(1), dim3(1024), 0, s, w.koff, K, w.L, w.S, w.off);
-    hipLaunchKernelGGL(kc_gather_kernel, dim3(grid_of(N)), dim3(KT), 0, s, codes, Dp, D, N, order, w.planes);
-    uint32_t NS, NG, NU;
-    KahanWork::caps(N, K, w.L, w.S, NS, NG, NU);
-    Geo g{w.planes, N, w.koff, w.off, K, D, w.L, w.S, reinterpret_cast<Fn *>(w.fn0), reinterpret_cast<Fn *>(w.fn1),
-          reinterpret_cast<Fn *>(w.fn2), NS, NG, NU};
-    i128 *P0 = reinterpret_cast<i128 *>(w.P0), *Etr = reinterpret_cast<i128 *>(w.Etr);
-    hipLaunchKernelGGL(kc_segsum_kernel, dim3(grid_of((uint64_t)NS * D)), dim3(KT), 0, s, g, Xt, P0);
-    hipLaunchKernelGGL(kc_prefix_kernel, dim3((unsigned)(((uint64_t)K * D * 64 + KT - 1) / KT)), dim3(KT), 0, s, g, P0);
-    hipLaunchKernelGGL(kc_build_kernel, dim3(grid_of((uint64_t)NS * D)), dim3(KT), 0, s, g, Xt, P0, (const i128 *)nullptr);
-    if (passes > 1) {
-        hipLaunchKernelGGL(kc_trust_kernel, dim3(grid_of((uint64_t)K * D)), dim3(KT), 0, s, g, Xt, P0, Etr);
-        hipLaunchKernelGGL(kc_build_kernel, dim3(grid_of((uint64_t)NS * D)), dim3(KT), 0, s, g, Xt, P0,
-                           (const i128 *)Etr);
+    hipLaunchKernelGGL(ks_offsets_kernel, dim3(1), dim3(1024), 0, s, w.tot, K, w.koff, w.segoff, w.blkoff);
+    if (A) hipLaunchKernelGGL(ks_scatter_kernel, dim3(G), dim3(64), K * 4, s, A, N, K, w.hist, w.koff, w.order);
+    const uint64_t PL = KahanWork::plane_len(N);
+    switch (Dp) {
+#define X(DPV)                                                                                                     \
+    case DPV:                                                                                                      \
+        hipLaunchKernelGGL(ks_gather_kernel<DPV>, dim3((uint32_t)((N + 256 * gather_pos<DPV>() - 1) /               \
+                                                                  (256 * gather_pos<DPV>()))),                       \
+                           dim3(256), 0, s, codes, N, D, A ? w.order : nullptr, PL, w.planes);                     \
+        break;
+        QVQ_FOR_EACH_DP(X)
+#undef X
+    default:
+        return hipErrorInvalidValue;
     }
-    hipLaunchKernelGGL(kc_compose_kernel<1>, dim3(grid_of((uint64_t)NG * D)), dim3(KT), 0, s, g, Xt);
-    hipLaunchKernelGGL(kc_compose_kernel<2>, dim3(grid_of((uint64_t)NU * D)), dim3(KT), 0, s, g, Xt);
-    hipLaunchKernelGGL(kc_eval_kernel, dim3(grid_of((uint64_t)K * D)), dim3(KT), 0, s, g, Xt, C, w.stats);
-    if (split_out)
-        hipLaunchKernelGGL(kc_split_kernel, dim3((unsigned)(((uint64_t)K * D + 255) / 256)), dim3(256), 0, s, C, K, D,
-                           split_out);
+    Geo g{};
+    g.planes = w.planes;
+    g.PL = PL;
+    g.koff = w.koff;
+    g.segoff = w.segoff;
+    g.blkoff = w.blkoff;
+    g.K = K;
+    g.D = D;
+    g.meta = reinterpret_cast<SegMeta *>(w.meta);
+    g.bsum = reinterpret_cast<u128 *>(w.bsum);
+    g.bfn = reinterpret_cast<Fn *>(w.bfn);
+    g.stats = w.stats;
+    const ByteTab *tab = reinterpret_cast<const ByteTab *>(w.tab);
+    // grids sized by the capacities; waves past the actual block count return at once
+    const uint64_t blk_waves = (uint64_t)w.blk_cap * D;
+    const uint32_t bgrid = (uint32_t)((blk_waves + WPB - 1) / WPB);
+    hipLaunchKernelGGL(ks_meta_kernel, dim3(bgrid), dim3(64 * WPB), 0, s, g, tab);
+    hipLaunchKernelGGL(ks_bscan_kernel, dim3((uint32_t)(((uint64_t)K * D * 64 + 255) / 256)), dim3(256), 0, s, g);
+    hipLaunchKernelGGL(ks_build_kernel, dim3(bgrid), dim3(64 * WPB), 0, s, g, tab);
+    hipLaunchKernelGGL(ks_eval_kernel, dim3((uint32_t)(((uint64_t)K * D + EPB - 1) / EPB)), dim3(64 * EPB), 0, s, g,
+                       tab, C, split_out);
     return hipGetLastError();
 }
 

@@ -1,7 +1,10 @@
-// CPU check of the segment-parallel Kahan evaluator (quant_amd/csrc/kahan_par.hpp): for
-// random SCALED chains of many kinds, eval_chain must return the bits of the reference's
-// sequential sumInArea (src/Quantizer.cpp:59-70), and the builder/composer are exercised at
-// several segment and group sizes.  Prints one line per case; exit status 1 on any mismatch.
+// CPU check of the segment-parallel Kahan evaluator (quant_amd/csrc/kahan_par.hpp): for chains of
+// many kinds, the pipeline the device runs (segment metadata, prefix sums, segment functions,
+// 64-segment block composites, the checked evaluation with replays) must return the bits of the
+// reference's sequential sumInArea (src/Quantizer.cpp:59-70).  Prints one summary line; exit
+// status 1 on any mismatch.
+//   test_kahan_chain [reps]            random chains
+//   test_kahan_chain /path/chains.bin  chains from a file ([u32 count] then per chain [u32 n][n bytes])
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -15,10 +18,10 @@ using namespace qvq::kahan;
 
 static double scaled(int b) { return ((double)(signed char)(unsigned char)b + 128.0) * (1.0 / 255); }
 
-static double kahan_ref(const std::vector<double> &x) {
+static double kahan_ref(const std::vector<uint8_t> &b, const ByteTab &tb) {
     double sum = 0, c = 0;
-    for (double v : x) {
-        double y = v - c;
+    for (uint8_t v : b) {
+        double y = ldexp((double)tb.X[v], -60) - c;
         double t = sum + y;
         c = (t - sum) - y;
         sum = t;
@@ -26,58 +29,163 @@ static double kahan_ref(const std::vector<double> &x) {
     return sum;
 }
 
-struct Result {
-    double v;
-    uint32_t stats[3];
+struct Stats {
+    uint64_t segs = 0, raw = 0, blocks = 0, blk_bad = 0, blk_miss = 0, seg_miss = 0, replays = 0;
 };
 
-// The engine's two passes over one chain: tables from dest 0, a trusted walk for the
-// estimates, tables again, composition, exact evaluation.
-static Result run_chain(const std::vector<uint8_t> &b, const uint64_t *Xt, uint32_t L, uint32_t S, int passes) {
-    const uint64_t n = b.size();
-    const uint64_t nseg = (n + L - 1) / L, GL = (uint64_t)L * S, ngrp = (n + GL - 1) / GL;
-    const uint64_t SL = GL * S, nsup = (n + SL - 1) / SL;
-    std::vector<Fn> f0(nseg), f1(ngrp), f2(nsup);
-    std::vector<i128> P0(nseg + 1);
-    std::vector<int64_t> dest(nseg, 0);
-    Chain c{b.data(), Xt, n, f0.data(), f1.data(), f2.data(), L, S};
-    for (int pass = 0; pass < passes; pass++) {
-        i128 P = 0;
-        for (uint64_t s = 0; s < nseg; s++) {
-            const uint64_t a = s * L;
-            const uint32_t len = (uint32_t)c.len0(s);
-            P0[s] = P;
-            f0[s] = build_segment(b.data() + a, Xt, len, P, dest[s]);
-            for (uint32_t j = 0; j < len; j++) P += (i128)Xt[b[a + j]];
-        }
-        if (pass + 1 < passes) estimate_dest(c, P0.data(), dest.data());
+// The device pipeline on one chain, serially.
+static double run_chain(const std::vector<uint8_t> &b, const ByteTab &tb, Stats &st) {
+    const uint32_t n = (uint32_t)b.size();
+    if (n == 0) return 0.0;
+    const uint32_t nseg = (n + L - 1) / L;
+    std::vector<SegMeta> meta(nseg);
+    std::vector<u128> P(nseg + 1);
+    P[0] = 0;
+    for (uint32_t j = 0; j < nseg; j++) {
+        const uint32_t len = std::min(L, n - j * L);
+        meta[j] = seg_meta(tb, b.data() + j * L, len);
+        P[j + 1] = P[j] + meta_sum(meta[j]);
     }
-    for (uint64_t g = 0; g < ngrp; g++) f1[g] = compose1(c, g);
-    for (uint64_t g = 0; g < nsup; g++) f2[g] = compose2(c, g);
-    Result r{};
-    r.v = eval_chain(c, r.stats);
-    return r;
+    auto build = [&](uint32_t j, int64_t D_est, Fn &f) {
+        SegMeta prev[8];
+        int np = 0;
+        for (int i = 1; i <= 8 && (int64_t)j - i >= 0; i++) prev[np++] = meta[j - i];
+        build_fn(tb, b.data() + j * L, std::min(L, n - j * L), P[j], meta[j], prev, np, j + 1 == nseg, D_est, f);
+    };
+    // block composites (estimates 0), a tree as on the device
+    const uint32_t nblk = (nseg + SPB - 1) / SPB;
+    std::vector<Fn> blk(nblk);
+    std::vector<bool> blk_ok(nblk);
+    for (uint32_t bi = 0; bi < nblk; bi++) {
+        const uint32_t s0 = bi * SPB, s1 = std::min(nseg, s0 + SPB);
+        std::vector<Fn> f(SPB);
+        std::vector<bool> ok(SPB, false);
+        for (uint32_t s = s0; s < s1; s++) {
+            build(s, 0, f[s - s0]);
+            ok[s - s0] = fkind(f[s - s0]) != FK_RAW;
+            st.segs++;
+            st.raw += !ok[s - s0];
+        }
+        for (uint32_t w = 1; w < SPB; w <<= 1)
+            for (uint32_t i = 0; i + w < SPB; i += 2 * w) {
+                if (s0 + i + w >= s1) continue;
+                Fn h;
+                const bool c = ok[i] && ok[i + w] && compose(f[i], f[i + w], h);
+                ok[i] = c;
+                if (c) f[i] = h;
+            }
+        blk[bi] = f[0];
+        blk_ok[bi] = ok[0];
+        st.blocks++;
+        st.blk_bad += !ok[0];
+    }
+    // evaluation
+    double sum;
+    u128 Pt, E;
+    const uint32_t tau = transient(tb, b.data(), n, sum, Pt, E);
+    if (!(sum >= 2.0)) return sum;
+    int64_t D = (int64_t)(E - Pt);
+    uint32_t F = (uint32_t)E & 511;
+    uint32_t j = (tau + L - 1) / L;
+    if (tau % L) {   // to the next boundary, exactly
+        const uint32_t end = std::min(n, j * L);
+        int32_t ds;
+        int64_t lo = -DLIM, hi = DLIM;
+        sim<true>(tb, b.data() + tau, end - tau, Pt, 0, F, D, ds, lo, hi);
+        D += ds;
+        st.replays++;
+    }
+    while (j < nseg) {
+        if ((uint32_t)((P[j] + (u128)(i128)D) & 511) != F) abort();   // state consistency
+        const uint32_t bi = j / SPB;
+        if (j % SPB == 0 && blk_ok[bi]) {
+            uint32_t F2 = F;
+            int64_t D2 = D;
+            if (apply(blk[bi], F2, D2)) {
+                F = F2;
+                D = D2;
+                j = std::min(nseg, j + SPB);
+                continue;
+            }
+            st.blk_miss++;
+        }
+        const uint32_t end = std::min(nseg, (bi + 1) * SPB);
+        for (; j < end; j++) {
+            Fn f;
+            build(j, D, f);
+            uint32_t F2 = F;
+            int64_t D2 = D;
+            if (apply(f, F2, D2)) {
+                F = F2;
+                D = D2;
+                continue;
+            }
+            st.seg_miss += fkind(f) != FK_RAW;
+            st.replays++;
+            int32_t ds;
+            int64_t lo = -DLIM, hi = DLIM;
+            sim<true>(tb, b.data() + j * L, std::min(L, n - j * L), P[j], 0, F, D, ds, lo, hi);
+            D += ds;
+        }
+    }
+    return to_double(P[nseg] + (u128)(i128)D);
+}
+
+static int check(const std::vector<uint8_t> &b, const ByteTab &tb, Stats &st, const char *what) {
+    const double ref = kahan_ref(b, tb);
+    const double got = run_chain(b, tb, st);
+    if (memcmp(&ref, &got, 8) != 0) {
+        printf("MISMATCH %s n %zu: ref %.17g got %.17g\n", what, b.size(), ref, got);
+        return 1;
+    }
+    return 0;
+}
+
+static void report(const char *what, int cases, int bad, const Stats &st) {
+    printf("%s: cases %d mismatches %d | segments %llu raw %llu | blocks %llu not composable %llu missed %llu | "
+           "segment misses %llu replays %llu\n",
+           what, cases, bad, (unsigned long long)st.segs, (unsigned long long)st.raw, (unsigned long long)st.blocks,
+           (unsigned long long)st.blk_bad, (unsigned long long)st.blk_miss, (unsigned long long)st.seg_miss,
+           (unsigned long long)st.replays);
 }
 
 int main(int argc, char **argv) {
-    const int reps = argc > 1 ? atoi(argv[1]) : 200;
     uint64_t Xt[256];
     for (int b = 0; b < 256; b++) Xt[b] = (uint64_t)ldexp(scaled(b), 60);
-    std::mt19937_64 rng(12345);
+    static ByteTab tb;
+    make_tab(Xt, tb);
+    Stats st;
     int bad = 0, cases = 0;
-    uint64_t tot_seg = 0, fail_seg = 0, tot_grp = 0, fail_grp = 0, tot_sup = 0, fail_sup = 0;
+    if (argc > 1 && argv[1][0] == '/') {
+        FILE *fp = fopen(argv[1], "rb");
+        if (!fp) return 2;
+        uint32_t nc = 0;
+        if (fread(&nc, 4, 1, fp) != 1) return 2;
+        for (uint32_t i = 0; i < nc; i++) {
+            uint32_t n = 0;
+            if (fread(&n, 4, 1, fp) != 1) return 2;
+            std::vector<uint8_t> b(n);
+            if (n && fread(b.data(), 1, n, fp) != n) return 2;
+            bad += check(b, tb, st, "file");
+            cases++;
+        }
+        report(argv[1], cases, bad, st);
+        return bad ? 1 : 0;
+    }
+    const int reps = argc > 1 ? atoi(argv[1]) : 200;
+    std::mt19937_64 rng(12345);
     // byte codes: code b has value (int8(b) + 128)/255, so u = b ^ 0x80 is the value index
     auto code = [](int u) { return (uint8_t)(u ^ 0x80); };
     for (int rep = 0; rep < reps; rep++) {
-        const int kind = rep % 8;
+        const int kind = rep % 10;
         uint64_t n;
         if (rep % 5 == 0) n = 1 + rng() % 50;
         else if (rep % 5 == 1) n = 1 + rng() % 5000;
         else if (rep % 5 == 2) n = 1 + rng() % 200000;
-        else n = 1 + rng() % 1000000;
+        else n = 1 + rng() % 600000;
         std::vector<uint8_t> b(n);
-        std::vector<double> x(n);
         const int lo = (int)(rng() % 256), span = 1 + (int)(rng() % 40);
+        const uint64_t period = 50 + rng() % 20000;
         for (uint64_t i = 0; i < n; i++) {
             int u;
             switch (kind) {
@@ -88,36 +196,17 @@ int main(int argc, char **argv) {
             case 4: u = (rng() % 3 == 0) ? 0 : (int)(rng() % 256); break;            // zeros
             case 5: u = 255; break;                                                  // flat 1.0
             case 6: u = (rng() % 2) ? 255 : 128 + (int)(rng() % 8); break;           // 1.0 and mid
-            default: u = (int)(64 + rng() % 64); break;                              // [0.25, 0.5)
+            case 7: u = (int)(64 + rng() % 64); break;                               // [0.25, 0.5)
+            case 8: u = ((i / period) % 2) ? (int)(rng() % 4) : (int)(128 + rng() % 128); break;   // dark/bright regions
+            default: u = ((i / period) % 3 == 0) ? 0 : ((i / period) % 3 == 1) ? (int)(rng() % 6) : 255; break;
             }
             b[i] = code(u);
-            x[i] = scaled(b[i]);
         }
-        const double ref = kahan_ref(x);
-        static const uint32_t Ls[] = {16, 64, 128, 256};
-        static const uint32_t Ss[] = {4, 16, 32};
-        const uint32_t L = Ls[rep % 4], S = Ss[rep % 3];
-        const int mode = argc > 2 ? atoi(argv[2]) : 2;
-        Result r = run_chain(b, Xt, L, S, mode);
+        char what[64];
+        snprintf(what, sizeof(what), "rep %d kind %d", rep, kind);
+        bad += check(b, tb, st, what);
         cases++;
-        const uint64_t nseg = (n + L - 1) / L, ngrp = (nseg + S - 1) / S, nsup = (ngrp + S - 1) / S;
-        tot_seg += nseg;
-        tot_grp += ngrp;
-        tot_sup += nsup;
-        fail_seg += r.stats[0];
-        fail_grp += r.stats[1];
-        fail_sup += r.stats[2];
-        if (getenv("KVERBOSE")) printf("kind %d n %llu L %u S %u misses %u/%llu %u/%llu %u/%llu\n", kind, (unsigned long long)n, L, S,
-                                       r.stats[0], (unsigned long long)nseg, r.stats[1], (unsigned long long)ngrp,
-                                       r.stats[2], (unsigned long long)nsup);
-        if (memcmp(&ref, &r.v, 8) != 0) {
-            bad++;
-            printf("MISMATCH rep %d kind %d n %llu L %u S %u: ref %.17g got %.17g\n", rep, kind,
-                   (unsigned long long)n, L, S, ref, r.v);
-        }
     }
-    printf("cases %d mismatches %d | table misses: segments %llu/%llu groups %llu/%llu super %llu/%llu\n", cases, bad,
-           (unsigned long long)fail_seg, (unsigned long long)tot_seg, (unsigned long long)fail_grp,
-           (unsigned long long)tot_grp, (unsigned long long)fail_sup, (unsigned long long)tot_sup);
+    report("random", cases, bad, st);
     return bad ? 1 : 0;
 }

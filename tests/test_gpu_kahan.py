@@ -45,7 +45,8 @@ def _check(engine, case, cs=oracle.SCALED):
     # the engine's codebook is the exact-sum centroid of its (the reference's) final cells
     np.testing.assert_array_equal(C, oracle.centroids(X, A_k, 1 << bits, sum_mode=1))
     assert np.max(np.abs(C - C_k) / np.maximum(np.abs(C_k), 1e-300)) <= 1e-12
-    assert abs(d - d_k) <= 1e-9 * abs(d_k)
+    # the closed-form distortion is exact to ~1e-16 of the mean square value (cancellation)
+    assert abs(d - d_k) <= 1e-9 * abs(d_k) + 1e-14 * float(np.mean(X * X))
     return int((A_k != A_x).sum())
 
 
@@ -64,3 +65,59 @@ def test_normal_colour_space_needs_no_kahan(engine):
     # NORMAL values are integers: the Kahan sums are exact, both rules agree
     case = dict(kind="noise96", seed=26, side=96, bw=2, bh=2, bits=10)
     assert _check(engine, case, cs=oracle.NORMAL) == 0
+
+
+# ---- the Kahan centroid evaluator itself (qvq_update_kahan, k_kahan.hip) -------------------------
+def _spatial_assign(n, K, seed, run=5000):
+    """Cells in runs along the row order (as a real assignment: image regions), some cells empty."""
+    rng = np.random.default_rng(seed)
+    runs = rng.integers(0, max(1, K - K // 8), (n + run - 1) // run)
+    A = np.repeat(runs, run)[:n].astype(np.uint32)
+    flip = rng.random(n) < 0.2
+    A[flip] = rng.integers(0, K, int(flip.sum()))
+    return A
+
+
+KAHAN_CASES = [
+    # (image, side, bw, bh, K, assignment)
+    ("noise", 96, 2, 2, 37, "random"),
+    ("noise", 96, 1, 1, 1, "mean"),
+    ("synthetic", 512, 2, 2, 32, "lbg5"),
+    ("synthetic", 512, 2, 2, 512, "lbg9"),
+    ("dark", 256, 2, 2, 8, "spatial"),     # values near 0 (tiny grids) and 1.0 (decisions)
+    ("synthetic", 4096, 2, 2, 32, "spatial"),
+    ("synthetic", 4096, 2, 2, 512, "spatial"),
+    ("synthetic", 4096, 2, 2, 1, "mean"),
+    ("synthetic", 1024, 4, 4, 64, "spatial"),
+]
+
+
+@pytest.mark.parametrize("case", KAHAN_CASES, ids=lambda c: "-".join(str(x) for x in c))
+def test_kahan_centroids_are_the_reference_bits(engine, case):
+    img, side, bw, bh, K, how = case
+    if img == "noise":
+        rgb = np.random.default_rng(7).integers(0, 256, side * side * 3, dtype=np.uint8)
+    elif img == "dark":
+        rng = np.random.default_rng(3)
+        # raw bytes 127 (value 1.0), 128..131 (values 0..3/255) and a few others, in regions
+        base = np.where((np.arange(side * side * 3) // 5000) % 2, 127, 128).astype(np.int64)
+        rgb = (base + rng.integers(0, 4, side * side * 3) * (base == 128)).astype(np.uint8)
+        mask = rng.random(rgb.size) < 0.01
+        rgb[mask] = rng.integers(0, 256, int(mask.sum()))
+    else:
+        rgb = oracle.gen_image(side)
+    X, _ = oracle.tile(rgb, side, side, bw, bh)
+    n = X.shape[0]
+    if how == "random":
+        A = np.random.default_rng(1).integers(0, K - 3, n).astype(np.uint32)   # the last cells empty
+    elif how == "mean":
+        A = np.zeros(n, np.uint32)
+    elif how.startswith("lbg"):
+        _, _, _, _, assigns = oracle.lbg(X, int(how[3:]), sum_mode=0, threads=8, dump=True)
+        A = assigns[-1].astype(np.uint32)
+    else:
+        A = _spatial_assign(n, K, seed=side + K)
+    engine.set_images(rgb, 1, side, side, bw, bh, oracle.SCALED)
+    C = engine.update_kahan(A, K)
+    C_ref = oracle.centroids(X, A, K, sum_mode=0)
+    np.testing.assert_array_equal(C.view(np.uint64), C_ref.view(np.uint64))
