@@ -147,8 +147,8 @@ QVQ_API qvq_status qvq_update_kahan(qvq_ctx *ctx, const uint32_t *assign, uint32
  * device pointers and a hipStream_t on which it launches (NULL = the legacy null stream, so
  * work the caller queued on blocking streams is ordered before it; the engine's own queued work
  * is ordered before it on any stream) and synchronises that stream before returning.  d_assign
- * must be 4-byte aligned; other alignments are accepted (unaligned rasters and index arrays take
- * a per-pixel kernel). */
+ * must be 4-byte aligned (QVQ_EINVAL otherwise); an unaligned raster takes a per-pixel kernel,
+ * as does the host qvq_decode path for any alignment of its staging. */
 QVQ_API qvq_status qvq_decode(qvq_ctx *ctx, const uint8_t *codebook, uint32_t K, const uint32_t *assign,
                               uint64_t nblocks, uint32_t xSize, uint32_t ySize, uint32_t bw, uint32_t bh, uint8_t *rgb);
 QVQ_API qvq_status qvq_decode_mse(qvq_ctx *ctx, const uint8_t *codebook, uint32_t K, const uint32_t *assign,

@@ -40,8 +40,9 @@ void EngineHandle::check(qvq_status st, const char *what) {
 namespace {
 
 // LBGQuantizer::quantize (src/Quantizer.cpp:119-144) on the engine.  The training set is
-// copied into one flat fp64 array; every value must be a NORMAL or SCALED colour value
-// (the engine sums exactly), otherwise std::runtime_error.
+// copied into one flat fp64 array.  Byte images of the NORMAL or SCALED colour space take the
+// byte engine; any other finite data (CIE1931 values, arbitrary doubles) the engine's exact
+// mode, the reference's arithmetic; non-finite values: std::runtime_error.
 class HipLBGQuantizer : public AbstractQuantizer {
 public:
     std::tuple<std::vector<Vector>, std::vector<size_t>, VectorType> quantize(const std::vector<Vector> &trainingSet,

@@ -250,6 +250,8 @@ inline size_t tint_bytes(uint32_t Kp) { return (size_t)2 * (PRUNE_MAXK_HOST / 32
 // 64-row chunks per image column of blocks (the workgroup's chunks stack across it; 1 = none).
 bool wide_can_search(uint32_t Dp);
 bool wide_prune_fits(uint32_t Dp, uint32_t K);
+// the whole codebook sits in one workgroup's LDS (the search is not streamed)
+bool wide_codebook_resident(uint32_t Dp, uint32_t K);
 hipError_t launch_assign_wide(hipStream_t s, int num_cu, uint32_t Dp, uint32_t D, const uint8_t *codes, uint64_t N,
                               const _Float16 *cb_rows, uint32_t K, const float *C32, const MfThresholds &th,
                               uint32_t *A, uint32_t *flags, unsigned *flag_cnt, const uint32_t *perm = nullptr,

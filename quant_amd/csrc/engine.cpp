@@ -249,14 +249,17 @@ bool use_fused(const qvq_ctx *ctx, uint32_t K) {
 // stopped by a provable bound) for D = 12 from K = QVQ_PRUNE_MINK (default 512; 0 = off) up to
 // prune_order's capacity.  Its order is computed by the previous level's finalize.
 // Other D (assign_wide_kernel, streamed codebooks): from K = QVQ_WPRUNE_MINK (default 1024).
+// A codebook resident in LDS (small D) is searched unpruned unless QVQ_WPRUNE_MINK is set:
+// its per-wave windows measured no faster.
 // The D = 12 kernel keeps one tile envelope per lane: at most 64 tiles (K <= 2048).
 bool use_prune(const qvq_ctx *ctx, uint32_t K) {
     static const uint32_t mink = std::getenv("QVQ_PRUNE_MINK") ? (uint32_t)std::atoi(std::getenv("QVQ_PRUNE_MINK")) : 512u;
-    static const uint32_t wmink =
-        std::getenv("QVQ_WPRUNE_MINK") ? (uint32_t)std::atoi(std::getenv("QVQ_WPRUNE_MINK")) : 1024u;
+    static const bool wset = std::getenv("QVQ_WPRUNE_MINK") != nullptr;
+    static const uint32_t wmink = wset ? (uint32_t)std::atoi(std::getenv("QVQ_WPRUNE_MINK")) : 1024u;
     if (K > PRUNE_MAXK_HOST) return false;
     if (ctx->D == MF_D)
         return mink && K >= mink && K <= 2048 && use_mfma(ctx, K) && mf32_prune_fits(K, use_fused(ctx, K));
+    if (!wset && wide_codebook_resident(ctx->Dp, K)) return false;
     return wmink && K >= wmink && use_wide(ctx, K) && wide_prune_fits(ctx->Dp, K);
 }
 
@@ -1157,8 +1160,14 @@ QVQ_API qvq_status qvq_set_vectors(qvq_ctx *ctx, const double *X, uint64_t n, ui
             break;
         }
     }
-    // other values (arbitrary fp64 data, CIE1931): the reference's own arithmetic (exact mode)
-    if (cs_found < 0) return qvq_set_vectors_exact(ctx, X, n, dim);
+    // other values (arbitrary fp64 data, CIE1931): the reference's own arithmetic (exact mode),
+    // one rank only -- with a communicator the ranks would disagree on the mode: fail fast here
+    // instead of at qvq_lbg, where peers would wait in the first all-reduce
+    if (cs_found < 0) {
+        if (ctx->comm || ctx->host_ar)
+            return fail(ctx, QVQ_EUNSUPPORTED, "values are not byte images (exact mode runs on one rank)");
+        return qvq_set_vectors_exact(ctx, X, n, dim);
+    }
     HIPCHK(hipSetDevice(ctx->dev));
     qvq_status st = alloc_training(ctx, n, dim, cs_found);
     if (st != QVQ_OK) return st;
@@ -1221,12 +1230,13 @@ qvq_status exact_koff(qvq_ctx *ctx, uint32_t K) {
 // fp64 argmin, exact ties answered by the host kd-tree over hC.  Returns the tie count.
 qvq_status exact_assign(qvq_ctx *ctx, const double *hC, uint32_t K, unsigned &nties) {
     const uint32_t D = ctx->D;
+    qvq_status st;
     unsigned *cnt = ctx->d_counters + 1;
     HIPCHK(hipMemsetAsync(cnt, 0, sizeof(unsigned), ctx->stream));
     HIPCHK(launch_exact_assign(ctx->stream, ctx->d_X64, ctx->N, D, ctx->d_C64_split, K, 1e-12, ctx->d_A, ctx->d_ties,
                                cnt));
     HIPCHK(hipMemcpyAsync(&nties, cnt, sizeof(unsigned), hipMemcpyDeviceToHost, ctx->stream));
-    HIPCHK(hipStreamSynchronize(ctx->stream));
+    if ((st = wait_stream(ctx)) != QVQ_OK) return st;
     if (nties == 0) return QVQ_OK;
     const uint64_t need = (uint64_t)nties * (8 + 8ull * D);
     if (ctx->scatter_bytes < need) {
@@ -1241,12 +1251,12 @@ qvq_status exact_assign(qvq_ctx *ctx, const double *hC, uint32_t K, unsigned &nt
     HIPCHK(launch_exact_gather(ctx->stream, ctx->d_X64, D, ctx->d_ties, nties, d_rows));
     HIPCHK(hipMemcpyAsync(rows.data(), ctx->d_ties, nties * 4, hipMemcpyDeviceToHost, ctx->stream));
     HIPCHK(hipMemcpyAsync(q.data(), d_rows, q.size() * 8, hipMemcpyDeviceToHost, ctx->stream));
-    HIPCHK(hipStreamSynchronize(ctx->stream));
+    if ((st = wait_stream(ctx)) != QVQ_OK) return st;
     RefKDTree tree(hC, K, (int)D);
     for (unsigned i = 0; i < nties; i++) vals[i] = tree.nearest(q.data() + (size_t)i * D);
     HIPCHK(hipMemcpyAsync(d_vals, vals.data(), nties * 4, hipMemcpyHostToDevice, ctx->stream));
     HIPCHK(launch_exact_fix(ctx->stream, ctx->d_A, ctx->d_ties, d_vals, nties));
-    HIPCHK(hipStreamSynchronize(ctx->stream));   // the host vectors must outlive the copies
+    if ((st = wait_stream(ctx)) != QVQ_OK) return st;   // the host vectors must outlive the copies
     return QVQ_OK;
 }
 
@@ -1272,7 +1282,7 @@ qvq_status lbg_exact(qvq_ctx *ctx, uint32_t bits, double *codebook, uint32_t *as
     std::vector<double> hC((size_t)Kmax * D), hS((size_t)Kmax * D);
     if ((st = exact_centroids(ctx, true, 1, nullptr)) != QVQ_OK) return st;
     HIPCHK(hipMemcpyAsync(hC.data(), ctx->d_C64_cent, (size_t)D * 8, hipMemcpyDeviceToHost, ctx->stream));
-    HIPCHK(hipStreamSynchronize(ctx->stream));
+    if ((st = wait_stream(ctx)) != QVQ_OK) return st;
     if (bits == 0) HIPCHK(hipMemsetAsync(ctx->d_A, 0, ctx->N * 4, ctx->stream));
     for (uint32_t lvl = 1; lvl <= bits; lvl++) {
         const uint32_t K = 1u << lvl, H = K / 2;
@@ -1287,15 +1297,20 @@ qvq_status lbg_exact(qvq_ctx *ctx, uint32_t bits, double *codebook, uint32_t *as
         ctx->tm.host_ties[lvl - 1] = nt;
         if ((st = exact_centroids(ctx, false, K, nullptr)) != QVQ_OK) return st;
         HIPCHK(hipMemcpyAsync(hC.data(), ctx->d_C64_cent, (size_t)K * D * 8, hipMemcpyDeviceToHost, ctx->stream));
-        HIPCHK(hipStreamSynchronize(ctx->stream));
+        if ((st = wait_stream(ctx)) != QVQ_OK) return st;
     }
     // updateDistortion after the last fix (src/Quantizer.cpp:9-22)
     double dist = 0;
     HIPCHK(launch_exact_distortion(ctx->stream, ctx->d_X64, ctx->N, D, ctx->d_C64_cent, ctx->d_A, ctx->d_dist_part,
                                    ctx->d_dist_part + 4096));
-    HIPCHK(hipMemcpyAsync(&dist, ctx->d_dist_part + 4096, 8, hipMemcpyDeviceToHost, ctx->stream));
-    if (assign) HIPCHK(hipMemcpyAsync(assign, ctx->d_A, ctx->N * 4, hipMemcpyDeviceToHost, ctx->stream));
-    HIPCHK(hipStreamSynchronize(ctx->stream));
+    // results reach the caller only after the bounded wait succeeds (staged in pinned memory)
+    if ((st = ensure_pinned(ctx, ctx->h_stage, ctx->stage_bytes, 8 + (assign ? ctx->N * 4 : 0))) != QVQ_OK) return st;
+    uint8_t *stage = static_cast<uint8_t *>(ctx->h_stage);
+    HIPCHK(hipMemcpyAsync(stage, ctx->d_dist_part + 4096, 8, hipMemcpyDeviceToHost, ctx->stream));
+    if (assign) HIPCHK(hipMemcpyAsync(stage + 8, ctx->d_A, ctx->N * 4, hipMemcpyDeviceToHost, ctx->stream));
+    if ((st = wait_stream(ctx)) != QVQ_OK) return st;
+    std::memcpy(&dist, stage, 8);
+    if (assign) std::memcpy(assign, stage + 8, ctx->N * 4);
     if (codebook) std::memcpy(codebook, hC.data(), (size_t)Kmax * D * 8);
     if (distortion) *distortion = dist;
     ctx->tm.total_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();

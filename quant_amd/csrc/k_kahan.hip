@@ -3,9 +3,9 @@
 // Used on the levels whose tie band is not empty.
 //
 // Pipeline (one stream):
-//   1. stable counting sort of the rows by cell: per-4096-row histograms, column scan, cell
-//      offsets, then a wave per 4096 rows writes each row's sorted position in row order;
-//   2. gather: planes[d][p] = component d of the p-th sorted row (16 positions per thread);
+//   1. stable counting sort of the rows by cell: per-4096-row histograms, a scan per cell, cell
+//      offsets, then a wave per 4096 rows writes each row's bytes at its sorted position into
+//      the component planes (planes[d][p] = component d of the p-th row in cell order);
 //   3. meta: a wave per block of 64 segments (64 steps each) of one chain and component:
 //      each lane's SegMeta, the block's total;
 //   4. block prefix: per chain and component, the exact sums before each block;
@@ -44,37 +44,44 @@ __device__ inline void wave_sync() {
     __builtin_amdgcn_wave_barrier();
 }
 
-// ---- 1. stable counting sort --------------------------------------------------------------------
+// ---- 1. stable counting sort, writing the planes ----------------------------------------------
+// hist[k][g]: rows of 4096-row block g with index k (transposed: a key's column is contiguous)
 __global__ __launch_bounds__(64) void ks_hist_kernel(const uint32_t *__restrict__ A, uint64_t N, uint32_t K,
-                                                    uint32_t *__restrict__ hist) {
+                                                    uint32_t G, uint32_t *__restrict__ hist) {
     extern __shared__ uint32_t h[];
     for (uint32_t i = threadIdx.x; i < K; i += 64) h[i] = 0;
     __syncthreads();
     const uint64_t r0 = (uint64_t)blockIdx.x * SROWS, r1 = min(N, r0 + SROWS);
     for (uint64_t r = r0 + threadIdx.x; r < r1; r += 64) atomicAdd(&h[A[r]], 1u);
     __syncthreads();
-    for (uint32_t i = threadIdx.x; i < K; i += 64) hist[(uint64_t)blockIdx.x * K + i] = h[i];
+    for (uint32_t i = threadIdx.x; i < K; i += 64) hist[(uint64_t)i * G + blockIdx.x] = h[i];
 }
 
-// hist[g][k] <- rows of blocks before g with index k (exclusive, in place); tot[k]
-__global__ __launch_bounds__(256) void ks_colscan_kernel(uint32_t *__restrict__ hist, uint32_t G, uint32_t K,
+// Per key (a block each): hist[k][g] <- rows of blocks before g with index k; tot[k].
+__global__ __launch_bounds__(256) void ks_colscan_kernel(uint32_t *__restrict__ hist, uint32_t G,
                                                         uint32_t *__restrict__ tot) {
-    const uint32_t k = blockIdx.x * 256 + threadIdx.x;
-    if (k >= K) return;
+    __shared__ uint32_t wsum[4];
+    uint32_t *col = hist + (uint64_t)blockIdx.x * G;
+    const uint32_t per = (G + 255) / 256, g0 = min(G, threadIdx.x * per), g1 = min(G, g0 + per);
     uint32_t s = 0;
-    constexpr uint32_t CU = 16;
-    for (uint32_t g0 = 0; g0 < G; g0 += CU) {
-        uint32_t v[CU];
-#pragma unroll
-        for (uint32_t u = 0; u < CU; u++) v[u] = hist[(uint64_t)min(g0 + u, G - 1) * K + k];
-#pragma unroll
-        for (uint32_t u = 0; u < CU; u++)
-            if (g0 + u < G) {
-                hist[(uint64_t)(g0 + u) * K + k] = s;
-                s += v[u];
-            }
+    for (uint32_t g = g0; g < g1; g++) s += col[g];
+    // block exclusive scan of the threads' sums
+    const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    uint32_t inc = s;
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t v = __shfl_up(inc, o, 64);
+        if (lane >= (uint32_t)o) inc += v;
     }
-    tot[k] = s;
+    if (lane == 63) wsum[w] = inc;
+    __syncthreads();
+    uint32_t base = inc - s;
+    for (uint32_t i = 0; i < w; i++) base += wsum[i];
+    for (uint32_t g = g0; g < g1; g++) {
+        const uint32_t v = col[g];
+        col[g] = base;
+        base += v;
+    }
+    if (threadIdx.x == 255) tot[blockIdx.x] = base;
 }
 
 // koff[k] = rows with index < k, koff[K] = N; seg/blk offsets of the chains (64-step segments,
@@ -118,72 +125,82 @@ __global__ __launch_bounds__(1024) void ks_offsets_kernel(const uint32_t *__rest
     }
 }
 
-// order[koff[k] + rank] = row, rank in row order within cell k (stable).  A wave per 4096 rows,
-// 64-row chunks in order; the lanes of one index in a chunk are ranked by a ballot.
-__global__ __launch_bounds__(64) void ks_scatter_kernel(const uint32_t *__restrict__ A, uint64_t N, uint32_t K,
+// planes[d][p] = component d of the p-th row in (cell, row) order: a wave per 4096 rows, 64-row
+// chunks in order.  Each chunk's (cell, lane) pairs are sorted across the wave (bitonic, by
+// shuffles), so a row's rank among the chunk's rows of its cell is its distance from its run's
+// start; the sorted lanes write the rows (each run's bytes contiguous) and each run's last lane
+// advances its cell's position.
+template <int DP>
+__global__ __launch_bounds__(64) void ks_scatter_kernel(const uint8_t *__restrict__ codes, const uint32_t *__restrict__ A,
+                                                       uint64_t N, uint32_t K, uint32_t D, uint32_t G,
                                                        const uint32_t *__restrict__ hist,
-                                                       const uint32_t *__restrict__ koff, uint32_t *__restrict__ order) {
+                                                       const uint32_t *__restrict__ koff, uint64_t PL,
+                                                       uint8_t *__restrict__ planes) {
+    constexpr int W = DP / 4;
     extern __shared__ uint32_t cur[];
-    for (uint32_t i = threadIdx.x; i < K; i += 64) cur[i] = koff[i] + hist[(uint64_t)blockIdx.x * K + i];
+    for (uint32_t i = threadIdx.x; i < K; i += 64) cur[i] = koff[i] + hist[(uint64_t)i * G + blockIdx.x];
     __syncthreads();
     const uint32_t lane = lane_id();
-    const uint64_t lt = (1ull << lane) - 1;
+    constexpr uint32_t NOKEY = (1u << 26) - 1;
     const uint64_t r0 = (uint64_t)blockIdx.x * SROWS, r1 = min(N, r0 + SROWS);
     for (uint64_t base = r0; base < r1; base += 64) {
         const uint64_t r = base + lane;
         const bool in = r < r1;
-        const uint32_t key = in ? A[r] : 0xFFFFFFFFu;
-        uint64_t active = __ballot(in);
-        while (active) {
-            const int leader = __ffsll((long long)active) - 1;
-            const uint32_t kl = __shfl(key, leader, 64);
-            const uint64_t m = __ballot(key == kl) & active;
-            const uint32_t c = cur[kl];
-            if (key == kl && in) order[c + __popcll(m & lt)] = (uint32_t)r;
-            __syncthreads();   // one wave: orders the LDS read before the update
-            if (lane == (uint32_t)leader) cur[kl] = c + (uint32_t)__popcll(m);
-            __syncthreads();
-            active &= ~m;
+        uint32_t w[W];
+        const uint32_t *src = reinterpret_cast<const uint32_t *>(codes + (in ? r : r0) * DP);
+#pragma unroll
+        for (int u = 0; u < W; u++) w[u] = src[u];
+        uint32_t v = ((in ? A[r] : NOKEY) << 6) | lane;
+        for (uint32_t k = 2; k <= 64; k <<= 1)
+            for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+                const uint32_t o = __shfl_xor(v, j, 64);
+                const bool lo_half = (lane & j) == 0, up = (lane & k) == 0;
+                v = (lo_half == up) ? min(v, o) : max(v, o);
+            }
+        const uint32_t key = v >> 6, from = v & 63;
+        const uint32_t kprev = __shfl_up(key, 1, 64), knext = __shfl_down(key, 1, 64);
+        const bool start = lane == 0 || kprev != key, end = lane == 63 || knext != key;
+        uint32_t rs = start ? lane : 0;
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t t = __shfl_up(rs, o, 64);
+            if (lane >= (uint32_t)o) rs = max(rs, t);
         }
+        uint32_t row[W];
+#pragma unroll
+        for (int u = 0; u < W; u++) row[u] = __shfl(w[u], from, 64);
+        if (key != NOKEY) {
+            const uint32_t dst = cur[key] + (lane - rs);
+#pragma unroll
+            for (int d = 0; d < DP; d++)
+                if ((uint32_t)d < D) planes[(uint64_t)d * PL + dst] = (uint8_t)(row[d >> 2] >> (8 * (d & 3)));
+            if (end) cur[key] = dst + 1;
+        }
+        wave_sync();
     }
 }
 
-// ---- 2. gather ------------------------------------------------------------------------------
-// planes[d][p] = component d of row order[p] (order null: row p).  16 positions per thread.
+// The mean's single cell (no sort): planes[d][p] = component d of row p.
 template <int DP>
-constexpr int gather_pos() { return DP <= 16 ? 16 : 4; }
-template <int DP>
-__global__ __launch_bounds__(256) void ks_gather_kernel(const uint8_t *__restrict__ codes, uint64_t N, uint32_t D,
-                                                       const uint32_t *__restrict__ order, uint64_t PL,
-                                                       uint8_t *__restrict__ planes) {
-    constexpr int W = DP / 4, NP = gather_pos<DP>();
-    const uint64_t p0 = ((uint64_t)blockIdx.x * 256 + threadIdx.x) * NP;
+__global__ __launch_bounds__(256) void ks_transpose_kernel(const uint8_t *__restrict__ codes, uint64_t N, uint32_t D,
+                                                          uint64_t PL, uint8_t *__restrict__ planes) {
+    constexpr int W = DP / 4;
+    const uint64_t p0 = ((uint64_t)blockIdx.x * 256 + threadIdx.x) * 4;
     if (p0 >= N) return;
-    uint32_t w[NP][W];
+    uint32_t w[4][W];
 #pragma unroll
-    for (int i = 0; i < NP; i++) {
-        const uint64_t p = min(p0 + i, N - 1);
-        const uint64_t row = order ? order[p] : p;
-        const uint32_t *src = reinterpret_cast<const uint32_t *>(codes + row * DP);
+    for (int i = 0; i < 4; i++) {
+        const uint32_t *src = reinterpret_cast<const uint32_t *>(codes + min(p0 + i, N - 1) * DP);
 #pragma unroll
         for (int u = 0; u < W; u++) w[i][u] = src[u];
     }
 #pragma unroll
-    for (int d = 0; d < DP; d++) {
-        if ((uint32_t)d >= D) continue;
-        uint32_t o[NP / 4];
-#pragma unroll
-        for (int q = 0; q < NP / 4; q++) {
+    for (int d = 0; d < DP; d++)
+        if ((uint32_t)d < D) {
             uint32_t v = 0;
 #pragma unroll
-            for (int t = 0; t < 4; t++) v |= ((w[4 * q + t][d >> 2] >> (8 * (d & 3))) & 0xFFu) << (8 * t);
-            o[q] = v;
+            for (int t = 0; t < 4; t++) v |= ((w[t][d >> 2] >> (8 * (d & 3))) & 0xFFu) << (8 * t);
+            *reinterpret_cast<uint32_t *>(planes + (uint64_t)d * PL + p0) = v;
         }
-        if constexpr (NP == 16)
-            *reinterpret_cast<uint4 *>(planes + (uint64_t)d * PL + p0) = make_uint4(o[0], o[1], o[2], o[3]);
-        else
-            *reinterpret_cast<uint32_t *>(planes + (uint64_t)d * PL + p0) = o[0];
-    }
 }
 
 // ---- shared: blocks of a chain ---------------------------------------------------------------
@@ -318,13 +335,10 @@ __device__ inline u128 build_block_fns(const Geo &g, const ByteTab &tab, const u
                    wave_excl_scan(s < nseg ? kahan::meta_sum(self) : (u128)0);
     Fn f;
     if (s < nseg) {
-        SegMeta prev[8];
-        int np = 0;
-        for (int i = 1; i <= 8 && (int64_t)s - i >= 0; i++) {
-            prev[np++] = g.meta[mbase + s - i];
-            if (prev[np - 1].cmax >= 0) break;
-        }
-        kahan::build_fn(tab, bytes + lane * L, min(L, n - s * L), P, self, prev, np, s + 1 == nseg, D_est, f);
+        int c_in;
+        uint32_t off_in;
+        kahan::input_structure([&](int i) { return g.meta[mbase + s - i]; }, (int)min(8u, s), c_in, off_in);
+        kahan::build_fn(tab, bytes + lane * L, min(L, n - s * L), P, self, c_in, off_in, s + 1 == nseg, D_est, f);
     } else {
         f.kind = kahan::FK_TRANS;
         f.c_in = f.lne = f.c_out = 0;
@@ -403,19 +417,44 @@ __global__ __launch_bounds__(64 * EPB) void ks_eval_kernel(Geo g, const ByteTab 
     const u128 *bpre = g.bsum + (uint64_t)d * TB + g.blkoff[k];
     const uint64_t mbase = (uint64_t)d * g.segoff[g.K] + g.segoff[k];
     double result = 0.0;
+    // the exact total: the last block's prefix and its segments' sums
+    u128 Pn = 0;
     if (n) {
-        // the transient: the reference's doubles until sum >= 2 (lane 0; bytes staged per block)
+        const uint32_t lb = (nseg - 1) / SPB, s = lb * SPB + lane;
+        const u128 v = s < nseg ? kahan::meta_sum(g.meta[mbase + s]) : (u128)0;
+        uint64_t lo = (uint64_t)v, hi = (uint64_t)(v >> 64);
+        for (int o = 32; o >= 1; o >>= 1) {
+            const uint64_t l2 = __shfl_xor((unsigned long long)lo, o, 64), h2 = __shfl_xor((unsigned long long)hi, o, 64);
+            const uint64_t t = lo + l2;
+            hi = hi + h2 + (t < lo);
+            lo = t;
+        }
+        Pn = bpre[lb] + (((u128)hi << 64) | lo);
+    }
+    if (n && Pn) {   // (every value 0: the sum is 0)
+        // the transient: the reference's doubles until sum >= 2 (lane 0; bytes staged per block;
+        // segments of zeros skipped while c = 0, where a zero step changes nothing)
         uint32_t i = 0, staged = 0xFFFFFFFFu;
         double sum = 0, c = 0;
         u128 P = 0;
         while (i < n && !(sum >= 2.0)) {
             const uint32_t b = i / BLK_STEPS;
+            if (c == 0 && i % L == 0) {
+                const uint32_t s = b * SPB + lane;
+                const bool nz = s >= i / L && s < nseg && kahan::meta_sum(g.meta[mbase + s]) != 0;
+                const uint64_t mask = __ballot(nz);
+                if (!mask) {
+                    i = min(n, (b + 1) * BLK_STEPS);
+                    continue;
+                }
+                i = max(i, (b * SPB + (uint32_t)(__ffsll((long long)mask) - 1)) * L);
+            }
             if (b != staged) {
                 stage_bytes(src + b * BLK_STEPS, min(BLK_STEPS, n - b * BLK_STEPS), bytes[w]);
                 wave_sync();
                 staged = b;
             }
-            const uint32_t e = min(n, (b + 1) * BLK_STEPS);
+            const uint32_t e = min(n, (i / L + 1) * L);   // to the end of the segment
             if (lane == 0)
                 while (i < e && !(sum >= 2.0)) {
                     const uint64_t X = tab.X[bytes[w][i - b * BLK_STEPS]];
@@ -437,20 +476,20 @@ __global__ __launch_bounds__(64 * EPB) void ks_eval_kernel(Geo g, const ByteTab 
             uint32_t j = (i + L - 1) / L;
             if (i % L) {   // exactly to the next segment boundary (inside the staged block)
                 const uint32_t e = min(n, j * L);
-                if (lane == 0) {
-                    int32_t ds;
-                    int64_t lo = -kahan::DLIM, hi = kahan::DLIM;
-                    kahan::sim<true>(tab, bytes[w] + (i - staged * BLK_STEPS), e - i, P, 0, F, D, ds, lo, hi);
-                    D += ds;
-                }
+                if (lane == 0) D += kahan::replay(tab, bytes[w] + (i - staged * BLK_STEPS), e - i, P, F, D);
                 D = __shfl((long long)D, 0, 64);
                 F = __shfl(F, 0, 64);
             }
             unsigned nmiss = 0, nrep = 0;
+            const Fn *bf = g.bfn + (uint64_t)d * TB + g.blkoff[k];
+            const uint32_t nblk = (nseg + SPB - 1) / SPB;
+            Fn fnext;
+            if (j % SPB == 0 && j < nseg) fnext = bf[j / SPB];
             while (j < nseg) {
                 const uint32_t b = j / SPB;
                 if (j % SPB == 0) {
-                    const Fn f = g.bfn[(uint64_t)d * TB + g.blkoff[k] + b];   // every lane: uniform
+                    const Fn f = fnext;   // every lane: uniform
+                    if (b + 1 < nblk) fnext = bf[b + 1];
                     if (kahan::apply(f, F, D)) {
                         j = min(nseg, j + SPB);
                         continue;
@@ -467,32 +506,17 @@ __global__ __launch_bounds__(64 * EPB) void ks_eval_kernel(Geo g, const ByteTab 
                 wave_sync();
                 const uint32_t end = min(nseg, (b + 1) * SPB);
                 for (; j < end; j++) {
-                    const Fn f = fns[w][j - b * SPB];
-                    if (kahan::apply(f, F, D)) continue;
+                    if (kahan::apply(fns[w][j - b * SPB], F, D)) continue;
                     nrep++;
-                    if (lane == 0) {
-                        int32_t ds;
-                        int64_t lo = -kahan::DLIM, hi = kahan::DLIM;
-                        kahan::sim<true>(tab, bytes[w] + (j - b * SPB) * L, min(L, n - j * L), pseg[w][j - b * SPB], 0,
-                                         F, D, ds, lo, hi);
-                        D += ds;
-                    }
+                    if (lane == 0)
+                        D += kahan::replay(tab, bytes[w] + (j - b * SPB) * L, min(L, n - j * L), pseg[w][j - b * SPB],
+                                           F, D);
                     D = __shfl((long long)D, 0, 64);
                     F = __shfl(F, 0, 64);
                 }
+                if (end < nseg && end % SPB == 0) fnext = bf[end / SPB];
                 wave_sync();
             }
-            // the exact total: the last block's prefix and its segments' sums
-            const uint32_t lb = (nseg - 1) / SPB, s = lb * SPB + lane;
-            u128 v = s < nseg ? kahan::meta_sum(g.meta[mbase + s]) : (u128)0;
-            uint64_t lo = (uint64_t)v, hi = (uint64_t)(v >> 64);
-            for (int o = 32; o >= 1; o >>= 1) {
-                const uint64_t l2 = __shfl_xor((unsigned long long)lo, o, 64), h2 = __shfl_xor((unsigned long long)hi, o, 64);
-                const uint64_t t = lo + l2;
-                hi = hi + h2 + (t < lo);
-                lo = t;
-            }
-            const u128 Pn = bpre[lb] + (((u128)hi << 64) | lo);
             result = kahan::to_double(Pn + (u128)(i128)D);
             if (g.stats && lane == 0 && (nmiss | nrep)) {
                 atomicAdd(&g.stats[1], nmiss);
@@ -531,23 +555,25 @@ hipError_t launch_kahan_centroids(hipStream_t s, const KahanWork &w, const uint8
                                   uint64_t N, const uint32_t *A, uint32_t K, double *C, double *split_out) {
     if (N == 0 || N > 0xFFFFFFFFull || D == 0 || K == 0 || D > Dp || Dp > 64 || (Dp & 3)) return hipErrorInvalidValue;
     const uint32_t G = KahanWork::sort_blocks(N);
+    const uint64_t PL = KahanWork::plane_len(N);
     if (A) {
-        hipLaunchKernelGGL(ks_hist_kernel, dim3(G), dim3(64), K * 4, s, A, N, K, w.hist);
-        hipLaunchKernelGGL(ks_colscan_kernel, dim3((K + 255) / 256), dim3(256), 0, s, w.hist, G, K, w.tot);
+        hipLaunchKernelGGL(ks_hist_kernel, dim3(G), dim3(64), K * 4, s, A, N, K, G, w.hist);
+        hipLaunchKernelGGL(ks_colscan_kernel, dim3(K), dim3(256), 0, s, w.hist, G, w.tot);
     } else {
         if (K != 1) return hipErrorInvalidValue;
         hipError_t e = hipMemcpyAsync(w.tot, &w.n_one, 4, hipMemcpyHostToDevice, s);
         if (e != hipSuccess) return e;
     }
     hipLaunchKernelGGL(ks_offsets_kernel, dim3(1), dim3(1024), 0, s, w.tot, K, w.koff, w.segoff, w.blkoff);
-    if (A) hipLaunchKernelGGL(ks_scatter_kernel, dim3(G), dim3(64), K * 4, s, A, N, K, w.hist, w.koff, w.order);
-    const uint64_t PL = KahanWork::plane_len(N);
     switch (Dp) {
 #define X(DPV)                                                                                                     \
     case DPV:                                                                                                      \
-        hipLaunchKernelGGL(ks_gather_kernel<DPV>, dim3((uint32_t)((N + 256 * gather_pos<DPV>() - 1) /               \
-                                                                  (256 * gather_pos<DPV>()))),                       \
-                           dim3(256), 0, s, codes, N, D, A ? w.order : nullptr, PL, w.planes);                     \
+        if (A)                                                                                                     \
+            hipLaunchKernelGGL(ks_scatter_kernel<DPV>, dim3(G), dim3(64), K * 4, s, codes, A, N, K, D, G, w.hist,  \
+                               w.koff, PL, w.planes);                                                              \
+        else                                                                                                       \
+            hipLaunchKernelGGL(ks_transpose_kernel<DPV>, dim3((uint32_t)((N + 1023) / 1024)), dim3(256), 0, s,     \
+                               codes, N, D, PL, w.planes);                                                         \
         break;
         QVQ_FOR_EACH_DP(X)
 #undef X

@@ -552,6 +552,16 @@ static hipError_t launch_wide_dp(hipStream_t s, int num_cu, uint32_t D, const ui
     return hipGetLastError();
 }
 
+bool wide_codebook_resident(uint32_t Dp, uint32_t K) {
+    switch (Dp) {
+#define X(DPV) \
+    case DPV: return wide_resident<DPV>(K);
+        X(4) X(8) X(12) X(16) X(20) X(24) X(28) X(32) X(36) X(40) X(44) X(48) X(52) X(56) X(60) X(64)
+#undef X
+    }
+    return false;
+}
+
 bool wide_prune_fits(uint32_t Dp, uint32_t K) {
     switch (Dp) {
 #define X(DPV) \

@@ -90,59 +90,87 @@ QVQ_HD inline uint32_t rnd(uint32_t t, uint32_t lg) {
     return (t + ((1u << (lg - 1)) - 1) + ((t >> lg) & 1)) & ~((1u << lg) - 1);
 }
 
-// ---- one trajectory ------------------------------------------------------------------------
-// Steps b[0..n) from E = P + D0 with E mod 512 = F (the caller's class representative).  bl0:
-// the binade of every E on the way (0: compute it at each decision from the exact E).  Out: the
-// final F, the sum of deltas, and [lo, hi] narrowed to the input D for which every decision
-// would be the same.
-template <bool EXACT_BL>
-QVQ_HD inline void sim(const ByteTab &tb, const uint8_t *b, uint32_t n, u128 P, int bl0, uint32_t &F, int64_t D0,
-                       int32_t &dsum, int64_t &lo, int64_t &hi) {
-    uint64_t q = (uint64_t)P;
+// ---- trajectories ------------------------------------------------------------------------------
+// NEN trajectories over steps b[0..n), all from the prefix P: entry e starts at E = P + D0[e]
+// with E mod 512 = F[e] (the caller's class representatives).  bl0: the binade of every E on
+// the way (0: computed at each decision from the exact E).  Out: the final F[e], the sums of
+// deltas ds[e], and [lo, hi] narrowed to the input D for which every decision of every entry
+// would be the same (absolute D of each entry's own input).
+template <int NEN, bool EXACT_BL>
+QVQ_HD inline void sim_n(const ByteTab &tb, const uint8_t *b, uint32_t n, u128 P, int bl0, uint32_t *F,
+                         const int64_t *D0, int32_t *ds, int64_t &lo, int64_t &hi) {
+    uint64_t q = (uint64_t)P;   // the prefix mod 2^64 (only bits < 41 are read)
     u128 Pj = P;
-    int32_t d = 0;
-    for (uint32_t i = 0; i < n; i++) {
-        const uint8_t c = b[i];
-        const uint64_t pk = tb.pk[c];
-        if (pk >> 62) {   // x = 1.0: a decision
-            const uint64_t E64 = q + (uint64_t)(D0 + d);
-            int bl = bl0;
-            if (EXACT_BL) bl = bitlen(Pj + (u128)(i128)(D0 + d));
-            const int su = bl - 53;
-            const uint64_t U = 1ull << su, h = U >> 1, e = E64 & (U - 1);
-            const bool pos = e < h || (e == h && !((E64 >> su) & 1));
-            const uint32_t r8 = rnd(F, 8), r7 = rnd(F, 7), r = pos ? r8 : r7;
-            if (r8 != r7) {
-                int64_t l, u;
-                if (e == h) l = u = 0;
-                else if (pos) l = -(int64_t)e, u = (int64_t)(h - 1 - e);
-                else l = (int64_t)(h + 1 - e), u = (int64_t)(U - 1 - e);
-                if (EXACT_BL) {   // the shift must also keep E in its binade
-                    const i128 E = (i128)(Pj + (u128)(i128)(D0 + d));
-                    const i128 bl_lo = ((i128)1 << (bl - 1)) - E, bl_hi = ((i128)1 << bl) - 1 - E;
-                    if (bl_lo > (i128)l) l = bl_lo > (i128)DLIM ? DLIM : (int64_t)bl_lo;
-                    if (bl_hi < (i128)u) u = bl_hi < -(i128)DLIM ? -DLIM : (int64_t)bl_hi;
-                }
-                if (D0 + l > lo) lo = D0 + l;
-                if (D0 + u < hi) hi = D0 + u;
-            }
-            d += (int32_t)r - (int32_t)F;
-            F = r & 511;
-        } else {
-            const uint32_t t = F + (uint32_t)((pk >> 41) & 511), sh = (uint32_t)((pk >> 50) & 31);
-            const uint32_t hm1 = (uint32_t)((pk >> 55) & 127);
-            const uint32_t m = ~(2 * hm1 + 1);   // exact steps: hm1 = 0 -> ~1, but the parity bit is 0 and t & ~1 ...
-            uint32_t r;
-            if (sh == 31) r = t;   // exact step
-            else r = (t + hm1 + ((t >> sh) & 1)) & ~((1u << sh) - 1);
-            (void)m;
-            d += (int32_t)r - (int32_t)t;
-            F = r & 511;
+    int32_t d[NEN];
+#pragma unroll
+    for (int e = 0; e < NEN; e++) d[e] = 0;
+    const bool aligned = ((uintptr_t)b & 3) == 0;
+    for (uint32_t i0 = 0; i0 < n; i0 += 4) {
+        uint32_t word;
+        if (aligned && i0 + 4 <= n) word = *reinterpret_cast<const uint32_t *>(b + i0);
+        else {
+            word = 0;
+            for (uint32_t u = 0; u < 4 && i0 + u < n; u++) word |= (uint32_t)b[i0 + u] << (8 * u);
         }
-        q += tb.X[c];
-        if (EXACT_BL) Pj += tb.X[c];
+        const uint32_t m = n - i0 < 4 ? n - i0 : 4;
+#pragma unroll
+        for (uint32_t u = 0; u < 4; u++) {
+            if (u >= m) break;
+            const uint32_t c = (word >> (8 * u)) & 0xFF;
+            const uint64_t pk = tb.pk[c];
+            if (pk >> 62) {   // x = 1.0: a decision per entry
+#pragma unroll
+                for (int e = 0; e < NEN; e++) {
+                    const uint64_t E64 = q + (uint64_t)(D0[e] + d[e]);
+                    int bl = bl0;
+                    if (EXACT_BL) bl = bitlen(Pj + (u128)(i128)(D0[e] + d[e]));
+                    const int su = bl - 53;
+                    const uint64_t U = 1ull << su, h = U >> 1, ee = E64 & (U - 1);
+                    const bool pos = ee < h || (ee == h && !((E64 >> su) & 1));
+                    const uint32_t r8 = rnd(F[e], 8), r7 = rnd(F[e], 7), r = pos ? r8 : r7;
+                    if (r8 != r7) {
+                        int64_t l, u2;
+                        if (ee == h) l = u2 = 0;
+                        else if (pos) l = -(int64_t)ee, u2 = (int64_t)(h - 1 - ee);
+                        else l = (int64_t)(h + 1 - ee), u2 = (int64_t)(U - 1 - ee);
+                        if (EXACT_BL) {   // the shift must also keep E in its binade
+                            const i128 E = (i128)(Pj + (u128)(i128)(D0[e] + d[e]));
+                            const i128 bl_lo = ((i128)1 << (bl - 1)) - E, bl_hi = ((i128)1 << bl) - 1 - E;
+                            if (bl_lo > (i128)l) l = bl_lo > (i128)DLIM ? DLIM : (int64_t)bl_lo;
+                            if (bl_hi < (i128)u2) u2 = bl_hi < -(i128)DLIM ? -DLIM : (int64_t)bl_hi;
+                        }
+                        if (D0[e] + l > lo) lo = D0[e] + l;
+                        if (D0[e] + u2 < hi) hi = D0[e] + u2;
+                    }
+                    d[e] += (int32_t)r - (int32_t)F[e];
+                    F[e] = r & 511;
+                }
+            } else {
+                const uint32_t xm = (uint32_t)(pk >> 41) & 511, sh = (uint32_t)(pk >> 50) & 31;
+                const uint32_t hm1 = (uint32_t)(pk >> 55) & 127;
+                const uint32_t mask = sh == 31 ? 0xFFFFFFFFu : ~((1u << sh) - 1);
+#pragma unroll
+                for (int e = 0; e < NEN; e++) {
+                    const uint32_t t = F[e] + xm;
+                    const uint32_t r = (t + hm1 + ((t >> (sh & 31)) & (sh != 31))) & mask;
+                    d[e] += (int32_t)r - (int32_t)t;
+                    F[e] = r & 511;
+                }
+            }
+            q += pk & ((1ull << 41) - 1);
+            if (EXACT_BL) Pj += tb.X[c];
+        }
     }
-    dsum = d;
+#pragma unroll
+    for (int e = 0; e < NEN; e++) ds[e] = d[e];
+}
+
+// One trajectory (the exact replay: D0 is the true input D, so every decision is the true one).
+QVQ_HD inline int32_t replay(const ByteTab &tb, const uint8_t *b, uint32_t n, u128 P, uint32_t &F, int64_t D0) {
+    int32_t ds;
+    int64_t lo = -DLIM, hi = DLIM;
+    sim_n<1, true>(tb, b, n, P, 0, &F, &D0, &ds, lo, hi);
+    return ds;
 }
 
 // The binade of every state E in [P - DLIM, P + S + DLIM] (S: the steps' sum), or 0 when they
@@ -188,8 +216,11 @@ QVQ_HD inline bool apply(const Fn &f, uint32_t &F, int64_t &D) {
     if (rel & ((1u << f.c_in) - 1)) return false;
     if (D < (int64_t)f.lo || D > (int64_t)f.hi) return false;
     const int e = (int)((rel >> f.c_in) & ((1u << f.lne) - 1));
-    D += f.dlt[e];
-    F = (F + f.sx9 + (uint32_t)f.dlt[e]) & 511;
+    int32_t dl = 0;
+#pragma unroll
+    for (int i = 0; i < NE; i++) dl = i == e ? f.dlt[i] : dl;   // (a select chain: f may be in registers)
+    D += dl;
+    F = (F + f.sx9 + (uint32_t)dl) & 511;
     return true;
 }
 
@@ -263,43 +294,93 @@ struct SegMeta {
 };
 QVQ_HD inline SegMeta seg_meta(const ByteTab &tb, const uint8_t *b, uint32_t n) {
     SegMeta m;
-    int cmax = -1, G = -1;
-    uint32_t apos = 0;
-    u128 s = 0;
-    for (uint32_t i = 0; i < n; i++) {
-        const uint8_t c = b[i];
-        if (tb.cg[c] >= cmax && tb.cg[c] >= 0) cmax = tb.cg[c], apos = i;
-        if (tb.dg[c] > G) G = tb.dg[c];
-        s += tb.X[c];
+    int key = -1, G = -1;   // key = cg << 8 | position: its maximum is the last step of the top grade
+    uint64_t slo = 0, shi = 0;
+    const bool aligned = ((uintptr_t)b & 3) == 0;
+    for (uint32_t i0 = 0; i0 < n; i0 += 4) {
+        uint32_t word;
+        if (aligned && i0 + 4 <= n) word = *reinterpret_cast<const uint32_t *>(b + i0);
+        else {
+            word = 0;
+            for (uint32_t u = 0; u < 4 && i0 + u < n; u++) word |= (uint32_t)b[i0 + u] << (8 * u);
+        }
+#pragma unroll
+        for (uint32_t u = 0; u < 4; u++) {
+            if (i0 + u >= n) break;
+            const uint32_t c = (word >> (8 * u)) & 0xFF;
+            const int cg = tb.cg[c], dg = tb.dg[c];
+            if (cg >= 0) key = key > (cg << 8 | (int)(i0 + u)) ? key : (cg << 8 | (int)(i0 + u));
+            G = G > dg ? G : dg;
+            const uint64_t x = tb.X[c], t = slo + x;
+            shi += t < slo;
+            slo = t;
+        }
     }
+    const int cmax = key < 0 ? -1 : key >> 8;
     uint32_t F = 0;
     if (cmax >= 0)
-        for (uint32_t i = apos + 1; i < n; i++) {   // grades below cmax: no decisions, no class reads
+        for (uint32_t i = (uint32_t)(key & 0xFF) + 1; i < n; i++) {   // grades below cmax: no decisions, no class reads
             const uint64_t pk = tb.pk[b[i]];
             const uint32_t t = F + (uint32_t)((pk >> 41) & 511), sh = (uint32_t)((pk >> 50) & 31);
             const uint32_t hm1 = (uint32_t)((pk >> 55) & 127);
             F = sh == 31 ? t : (t + hm1 + ((t >> sh) & 1)) & ~((1u << sh) - 1);
             F &= (1u << cmax) - 1;
         }
-    m.s_lo = (uint64_t)s;
-    m.s_hi = (uint8_t)(s >> 64);
+    m.s_lo = slo;
+    m.s_hi = (uint8_t)shi;
     m.cmax = (int8_t)cmax;
     m.G = (int8_t)G;
     m.pad = 0;
     m.off = (uint16_t)F;
-    m.sx9 = (uint16_t)(s & 511);
+    m.sx9 = (uint16_t)(slo & 511);
     return m;
 }
 QVQ_HD inline u128 meta_sum(const SegMeta &m) { return ((u128)m.s_hi << 64) | m.s_lo; }
 
 // ---- building a segment's function -------------------------------------------------------------
-// Segment j of a chain (n_j steps at b, exact prefix P at its start).  prev[-i] (i = 1..nprev) are
-// the metadata of the preceding segments (nearest first); final: the chain's last segment.
-// D_est: the estimate of the input D that decides the x = 1.0 steps (any value is safe).
-QVQ_HD inline void build_fn(const ByteTab &tb, const uint8_t *b, uint32_t n, u128 P, const SegMeta &self,
-                            const SegMeta *prev, int nprev, bool final, int64_t D_est, Fn &f) {
+// The input class structure of a segment: the nearest preceding segment with an anchor (its
+// cmax and tail offset), translated by the exact segments in between.  prev(i) (i = 1..np) gives
+// the metadata of the i-th preceding segment.  c_in = -1: none within np segments.
+template <class PrevFn>
+QVQ_HD inline void input_structure(PrevFn prev, int np, int &c_in, uint32_t &off_in) {
+    c_in = -1;
+    off_in = 0;
+    uint32_t trans = 0;
+    for (int i = 1; i <= np; i++) {
+        const SegMeta m = prev(i);
+        if (m.cmax >= 0) {
+            c_in = m.cmax;
+            off_in = (m.off + trans) & ((1u << c_in) - 1);
+            return;
+        }
+        trans += m.sx9;
+    }
+}
+
+// Entries [e0, e0 + NEN) of f through sim_n (f's header already set); [lo, hi] narrowed.
+template <int NEN, bool EXACT_BL>
+QVQ_HD inline void build_group(const ByteTab &tb, const uint8_t *b, uint32_t n, u128 P, int bl0, int64_t D_est,
+                               int e0, Fn &f, int64_t &lo, int64_t &hi) {
+    uint32_t F[NEN];
+    int64_t D0[NEN];
+    int32_t ds[NEN];
+#pragma unroll
+    for (int e = 0; e < NEN; e++) {
+        F[e] = (f.off_in + ((uint32_t)(e0 + e) << f.c_in)) & 511;
+        // the representative input D: D == F - P (mod 512), next to D_est
+        D0[e] = D_est + (int64_t)((F[e] - (uint32_t)(uint64_t)P - (uint32_t)D_est + 256) & 511) - 256;
+    }
+    sim_n<NEN, EXACT_BL>(tb, b, n, P, bl0, F, D0, ds, lo, hi);
+#pragma unroll
+    for (int e = 0; e < NEN; e++) f.dlt[e0 + e] = ds[e];
+}
+
+// Segment j of a chain (n steps at b, exact prefix P at its start, metadata self, input class
+// structure (c_in, off_in) from input_structure); final: the chain's last segment.  D_est: the
+// estimate of the input D that decides the x = 1.0 steps (any value is safe).
+QVQ_HD inline void build_fn(const ByteTab &tb, const uint8_t *b, uint32_t n, u128 P, const SegMeta &self, int c_in,
+                            uint32_t off_in, bool final, int64_t D_est, Fn &f) {
     f.pad = 0;
-    for (int e = 0; e < NE; e++) f.dlt[e] = 0;
     if (self.G < 0) {   // every step exact: a translation
         f.kind = (uint8_t)(FK_TRANS | (final ? FK_FINAL : 0));
         f.c_in = f.lne = f.c_out = 0;
@@ -307,51 +388,32 @@ QVQ_HD inline void build_fn(const ByteTab &tb, const uint8_t *b, uint32_t n, u12
         f.sx9 = self.sx9;
         f.lo = -(int32_t)DLIM;
         f.hi = (int32_t)DLIM;
-        return;
-    }
-    // the input class structure: the nearest preceding segment with an anchor, translated by the
-    // exact segments in between
-    int c_in = -1;
-    uint32_t off_in = 0, trans = 0;
-    for (int i = 0; i < nprev; i++) {
-        const SegMeta &m = prev[i];
-        if (m.cmax >= 0) {
-            c_in = m.cmax;
-            off_in = (m.off + trans) & 511;
-            break;
-        }
-        trans += m.sx9;
-    }
-    const int bl0 = fixed_binade(P, meta_sum(self));
-    if (c_in < 0 || P < MIN_STATE + (u128)DLIM) {
-        set_raw(f);
+        for (int e = 0; e < NE; e++) f.dlt[e] = 0;
         return;
     }
     const int lne = self.G + 1 - c_in > 0 ? self.G + 1 - c_in : 0;
-    if (lne > 4) {
+    if (c_in < 0 || P < MIN_STATE + (u128)DLIM || lne > 4) {
         set_raw(f);
         return;
     }
     f.kind = (uint8_t)(FK_TABLE | (final ? FK_FINAL : 0));
     f.c_in = (uint8_t)c_in;
     f.lne = (uint8_t)lne;
-    f.c_out = (uint8_t)(self.cmax >= 0 ? self.cmax : c_in);
-    f.off_in = (uint16_t)(off_in & ((1u << c_in) - 1));
+    f.c_out = (uint8_t)self.cmax;   // G >= 0 means some step rounds: an anchor exists
+    f.off_in = (uint16_t)off_in;
+    f.off_out = self.off;
     f.sx9 = self.sx9;
+    for (int e = 0; e < NE; e++) f.dlt[e] = 0;
     int64_t lo = -DLIM, hi = DLIM;
-    for (int e = 0; e < (1 << lne); e++) {
-        uint32_t F = (f.off_in + ((uint32_t)e << c_in)) & 511;
-        // the representative input D: D == F - P (mod 512), next to D_est
-        const int64_t D0 = D_est + (int64_t)(((F - (uint32_t)(uint64_t)P - (uint32_t)D_est + 256) & 511)) - 256;
-        int32_t ds;
-        if (bl0) sim<false>(tb, b, n, P, bl0, F, D0, ds, lo, hi);
-        else sim<true>(tb, b, n, P, 0, F, D0, ds, lo, hi);
-        f.dlt[e] = ds;
-        if (e == 0) f.off_out = (uint16_t)(F & (f.c_out < 9 ? (1u << f.c_out) - 1 : 511));
+    const int bl0 = fixed_binade(P, meta_sum(self));
+    if (bl0) {   // the binade is fixed: entries in groups of up to 4
+        if (lne == 0) build_group<1, false>(tb, b, n, P, bl0, D_est, 0, f, lo, hi);
+        else if (lne == 1) build_group<2, false>(tb, b, n, P, bl0, D_est, 0, f, lo, hi);
+        else
+            for (int e0 = 0; e0 < (1 << lne); e0 += 4) build_group<4, false>(tb, b, n, P, bl0, D_est, e0, f, lo, hi);
+    } else {     // a power of two inside the segment's range: each entry with the exact binade
+        for (int e0 = 0; e0 < (1 << lne); e0++) build_group<1, true>(tb, b, n, P, 0, D_est, e0, f, lo, hi);
     }
-    // the output structure: the segment's own anchor, or (no anchor) the input's, carried
-    if (self.cmax >= 0) f.off_out = self.off;
-    else f.off_out = (uint16_t)((f.off_in + self.sx9 + (uint32_t)f.dlt[0]) & ((1u << c_in) - 1));
     f.lo = (int32_t)lo;
     f.hi = (int32_t)hi;
     if (f.lo > f.hi) f.lo = 1, f.hi = 0;

@@ -1,5 +1,5 @@
-// kd_walk.hpp -- device code shared by the kd-tree tie kernels (k_assign.hip: kd_resolve_kernel,
-// k_tail.hip: the level tail's kd phase) and the rechecks: the reference-order fp64 distance
+// kd_walk.hpp -- device code shared by the kd-tree tie kernels (k_assign.hip: kd_resolve_kernel
+// and kd_reduce_kernel) and the rechecks: the reference-order fp64 distance
 // (nanoflann.hpp:320-345 as the reference build computes it) and the wave-parallel walk of the
 // reference kd-tree (nanoflann.hpp:1212-1270).
 #pragma once

@@ -47,10 +47,10 @@ static double run_chain(const std::vector<uint8_t> &b, const ByteTab &tb, Stats 
         P[j + 1] = P[j] + meta_sum(meta[j]);
     }
     auto build = [&](uint32_t j, int64_t D_est, Fn &f) {
-        SegMeta prev[8];
-        int np = 0;
-        for (int i = 1; i <= 8 && (int64_t)j - i >= 0; i++) prev[np++] = meta[j - i];
-        build_fn(tb, b.data() + j * L, std::min(L, n - j * L), P[j], meta[j], prev, np, j + 1 == nseg, D_est, f);
+        int c_in;
+        uint32_t off_in;
+        input_structure([&](int i) { return meta[j - i]; }, (int)std::min<uint32_t>(8, j), c_in, off_in);
+        build_fn(tb, b.data() + j * L, std::min(L, n - j * L), P[j], meta[j], c_in, off_in, j + 1 == nseg, D_est, f);
     };
     // block composites (estimates 0), a tree as on the device
     const uint32_t nblk = (nseg + SPB - 1) / SPB;
@@ -89,10 +89,7 @@ static double run_chain(const std::vector<uint8_t> &b, const ByteTab &tb, Stats 
     uint32_t j = (tau + L - 1) / L;
     if (tau % L) {   // to the next boundary, exactly
         const uint32_t end = std::min(n, j * L);
-        int32_t ds;
-        int64_t lo = -DLIM, hi = DLIM;
-        sim<true>(tb, b.data() + tau, end - tau, Pt, 0, F, D, ds, lo, hi);
-        D += ds;
+        D += replay(tb, b.data() + tau, end - tau, Pt, F, D);
         st.replays++;
     }
     while (j < nseg) {
@@ -110,9 +107,10 @@ static double run_chain(const std::vector<uint8_t> &b, const ByteTab &tb, Stats 
             st.blk_miss++;
         }
         const uint32_t end = std::min(nseg, (bi + 1) * SPB);
+        std::vector<Fn> fb(SPB);
+        for (uint32_t t = j; t < end; t++) build(t, D, fb[t - bi * SPB]);
         for (; j < end; j++) {
-            Fn f;
-            build(j, D, f);
+            const Fn &f = fb[j - bi * SPB];
             uint32_t F2 = F;
             int64_t D2 = D;
             if (apply(f, F2, D2)) {
@@ -122,10 +120,7 @@ static double run_chain(const std::vector<uint8_t> &b, const ByteTab &tb, Stats 
             }
             st.seg_miss += fkind(f) != FK_RAW;
             st.replays++;
-            int32_t ds;
-            int64_t lo = -DLIM, hi = DLIM;
-            sim<true>(tb, b.data() + j * L, std::min(L, n - j * L), P[j], 0, F, D, ds, lo, hi);
-            D += ds;
+            D += replay(tb, b.data() + j * L, std::min(L, n - j * L), P[j], F, D);
         }
     }
     return to_double(P[nseg] + (u128)(i128)D);
