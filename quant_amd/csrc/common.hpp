@@ -300,10 +300,18 @@ bool sorted_sums_fits(uint32_t K);
 hipError_t launch_sorted_sums(hipStream_t s, uint32_t Dp, uint32_t G, const uint8_t *codes, uint64_t N,
                               const uint32_t *A, uint32_t K, uint32_t D, const uint64_t *plut, uint32_t *hist,
                               uint32_t *scratch, uint32_t *idx, uint32_t *ks, uint64_t *sums);
+// A counter published to mapped host memory by a kernel: *dst = *cnt, then *flag = seq
+// (flag null: nothing).
+struct PubArgs {
+    const unsigned *cnt = nullptr;
+    uint32_t *dst = nullptr;
+    uint64_t *flag = nullptr;
+    uint64_t seq = 0;
+};
 // Sums of G slabs, the last nsub of them subtracted (fused path: slab G + 1 holds the terms
-// of re-assigned rows at their provisional index).
+// of re-assigned rows at their provisional index).  pub: a tie count to publish first.
 hipError_t launch_reduce(hipStream_t s, const uint64_t *part, const uint32_t *part_cnt, uint32_t G, uint32_t nsub,
-                         uint32_t K, uint32_t D, uint64_t *sums);
+                         uint32_t K, uint32_t D, uint64_t *sums, PubArgs pub = PubArgs());
 // Up to three device ranges (sizes multiples of 4 bytes, 0 = unused) copied in one launch,
 // e.g. into mapped pinned host memory; with flag (mapped) the copy then publishes *flag = seq
 // (done: a block counter at 0, left at 0).

@@ -23,6 +23,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <string>
+#include <memory>
 #include <vector>
 
 #include "common.hpp"
@@ -146,10 +147,13 @@ struct qvq_ctx {
     uint8_t *h_tree[2] = {nullptr, nullptr}, *dh_tree[2] = {nullptr, nullptr};
     uint8_t *d_tree = nullptr;   // device copy of the level's tree image (one DMA per level)
     std::vector<double> cb_local;   // host copy of the published codebook for the tree build
+    std::unique_ptr<RefKDTree> tree;   // the last level's tree over cb_local
+    KdView tree_kd;                    // and its device image (depth 0: none)
     uint64_t tree_cap = 0;
     uint32_t nslabs = 0;   // slabs holding the last run_level's sums
     uint32_t col_blocks = 0;   // blocks per image column (consecutive rows run down a column); 0: no image
     bool kd_pend = false;      // run_level left its kd-tree ties to kd_reduce_kernel (pend_kd)
+    PubArgs pub;               // run_level left its tie-count publication to the next reduce
     uint32_t sums_copies = 1;  // 2: run_level's tie moves are in copy 1 of d_sums (the finalize adds it)
     KdView pend_kd{};
     bool sums1_dirty = false;  // copy 1 of d_sums may hold moves (a quantize that stopped early)
@@ -613,8 +617,10 @@ void build_tree(qvq_ctx *ctx, const double *hC, uint32_t K, int buf, KdView &kd)
     if (env_is("QVQ_KDTREE", "host")) return;
     // the build reads the codebook many times; mapped memory the GPU just wrote is read
     // once, sequentially, into ordinary memory first
+    ctx->tree_kd = KdView{};
     ctx->cb_local.assign(hC, hC + (size_t)K * ctx->D);
-    RefKDTree tree(ctx->cb_local.data(), K, (int)ctx->D);
+    ctx->tree.reset(new RefKDTree(ctx->cb_local.data(), K, (int)ctx->D));
+    const RefKDTree &tree = *ctx->tree;
     const uint32_t D = ctx->D;
     const size_t nn = tree.num_nodes();
     KdView v;
@@ -644,6 +650,7 @@ void build_tree(qvq_ctx *ctx, const double *hC, uint32_t K, int buf, KdView &kd)
     v.nodes = reinterpret_cast<const KdNodeDev *>(dlo + 2 * D);
     v.vind = reinterpret_cast<const uint32_t *>(v.nodes + nn);
     kd = v;
+    ctx->tree_kd = v;
 }
 
 // Copy between a caller's host buffer and device memory at DMA speed: the host range is pinned
@@ -856,19 +863,22 @@ qvq_status run_level(qvq_ctx *ctx, uint32_t K, int slot, bool sums_out, const do
     qvq_status st;
     if (defer_ties) {   // the level's tie count to the host, before the rest of the level runs
         ctx->pub_seq++;
-        HIPCHK(launch_copy_out(ctx->stream, &cnt[1], reinterpret_cast<uint8_t *>(ctx->dh_ready) + 16, 4, nullptr,
-                               nullptr, 0, nullptr, nullptr, 0, ctx->dh_ready + 1, ctx->pub_seq,
-                               ctx->d_counters + 2 * 33 + 1));
+        if (fused) {   // published by the slab reduce that follows (qvq_lbg): no launch of its own
+            ctx->pub.cnt = &cnt[1];
+            ctx->pub.dst = reinterpret_cast<uint32_t *>(reinterpret_cast<uint8_t *>(ctx->dh_ready) + 16);
+            ctx->pub.flag = ctx->dh_ready + 1;
+            ctx->pub.seq = ctx->pub_seq;
+        } else {
+            HIPCHK(launch_copy_out(ctx->stream, &cnt[1], reinterpret_cast<uint8_t *>(ctx->dh_ready) + 16, 4, nullptr,
+                                   nullptr, 0, nullptr, nullptr, 0, ctx->dh_ready + 1, ctx->pub_seq,
+                                   ctx->d_counters + 2 * 33 + 1));
+        }
     }
     if (early_upd) {
         HIPCHK(hipEventRecord(ctx->ev[slot][2], ctx->stream));
         if ((st = run_update(ctx, ctx->d_A, K)) != QVQ_OK) return st;
         ctx->nslabs = 0;   // reduced already
         HIPCHK(hipEventRecord(ctx->ev[slot][3], ctx->stream));
-    }
-    if (defer_ties) {   // qvq_lbg answers the ties after the finalize, if there are any
-        ctx->upd[slot] = false;
-        return QVQ_OK;
     }
     // the tree build overlaps the search just enqueued
     const auto tw0 = std::chrono::steady_clock::now();
@@ -878,6 +888,10 @@ qvq_status run_level(qvq_ctx *ctx, uint32_t K, int slot, bool sums_out, const do
     build_tree(ctx, hC, K, slot & 1, kd);
     ctx->tm.wait_ms[slot] = std::chrono::duration<double, std::milli>(tw1 - tw0).count();
     ctx->tm.tree_ms[slot] = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tw1).count();
+    if (defer_ties) {   // qvq_lbg answers the ties after the finalize, if there are any (the tree kept)
+        ctx->upd[slot] = false;
+        return QVQ_OK;
+    }
     if (abl_skip() & 2) {
     } else if (kd.depth > 0 && fused && kd_merge(ctx) && kd_reduce_fits(kd, K)) {
         ctx->kd_pend = true;   // with the reduce (qvq_lbg)
@@ -928,7 +942,16 @@ qvq_status resolve_kahan_ties(qvq_ctx *ctx, uint32_t K, int slot, unsigned nt, b
     HIPCHK(hipMemcpyAsync(ctx->h_kc_split.data(), S_ref, (size_t)K * D * 8, hipMemcpyDeviceToHost, ctx->stream));
     if ((st = wait_stream(ctx)) != QVQ_OK) return st;
     KdView kd;
-    build_tree(ctx, ctx->h_kc_split.data(), K, slot & 1, kd);
+    // the level's tree (over the exact-sum split, built during the search) is the reference's
+    // tree too when no differing coordinate can move a box, cut or partition (kdtree.cpp)
+    static const bool reuse = !env_is("QVQ_KAHAN_TREE", "rebuild");
+    if (reuse && ctx->tree && ctx->tree_kd.depth > 0 && ctx->cb_local.size() == (size_t)K * D &&
+        ctx->tree->unchanged_under(ctx->h_kc_split.data())) {
+        kd = ctx->tree_kd;
+        if (env_is("QVQ_KAHAN_DEBUG", "1")) std::fprintf(stderr, "qvq kahan: K %u the level's tree reused\n", K);
+    } else {
+        build_tree(ctx, ctx->h_kc_split.data(), K, slot & 1, kd);
+    }
     unsigned *cnt = ctx->d_counters + 2 * slot;
     uint64_t *target = fused ? ctx->d_sums + sums_cap_stride(ctx) : ctx->d_sums;
     if (kd.depth > 0) {
@@ -1404,7 +1427,13 @@ QVQ_API qvq_status qvq_lbg(qvq_ctx *ctx, uint32_t bits, double eps, double *code
                 ctx->kd_pend = false;
             } else if (!(abl_skip() & 4) && ctx->nslabs) {   // nslabs 0: the sorted sums are in d_sums already
                 HIPCHK(launch_reduce(ctx->stream, ctx->d_part, ctx->d_part_cnt, ctx->nslabs, ctx->nsub, K, ctx->D,
-                                     ctx->d_sums));
+                                     ctx->d_sums, ctx->pub));
+            }
+            if (ctx->pub.flag) {   // run_level left the tie count to the reduce, which did not run
+                if (!ctx->nslabs || (abl_skip() & 4) || ctx->kd_pend)
+                    HIPCHK(launch_copy_out(ctx->stream, ctx->pub.cnt, ctx->pub.dst, 4, nullptr, nullptr, 0, nullptr,
+                                           nullptr, 0, ctx->pub.flag, ctx->pub.seq, ctx->d_counters + 2 * 33 + 1));
+                ctx->pub = PubArgs();
             }
             if ((st = all_reduce_sums(ctx, K)) != QVQ_OK) return st;
             HIPCHK(finalize(K, split, copies, copies > 1 ? tcnt : nullptr));

@@ -630,17 +630,22 @@ constexpr int REDUCE_THREADS = 1024;
 __global__ __launch_bounds__(REDUCE_THREADS) void reduce_kernel(const uint64_t *__restrict__ part,
                                                                 const uint32_t *__restrict__ part_cnt, uint32_t G,
                                                                 uint32_t nsub, uint32_t K, uint32_t D,
-                                                                uint64_t *__restrict__ sums) {
+                                                                uint64_t *__restrict__ sums, PubArgs pub) {
+    if (pub.flag && blockIdx.x == 0 && threadIdx.x == 0) {   // the count (final: the recheck ran before)
+        *reinterpret_cast<volatile uint32_t *>(pub.dst) = *pub.cnt;
+        __threadfence_system();
+        *reinterpret_cast<volatile uint64_t *>(pub.flag) = pub.seq;
+    }
     __shared__ uint64_t red[2 * 16 * 64];
     reduce_columns_block(part, part_cnt, G, nsub, K, D, sums, blockIdx.x, red);
 }
 
 hipError_t launch_reduce(hipStream_t s, const uint64_t *part, const uint32_t *part_cnt, uint32_t G, uint32_t nsub,
-                         uint32_t K, uint32_t D, uint64_t *sums) {
+                         uint32_t K, uint32_t D, uint64_t *sums, PubArgs pub) {
     if (nsub > G) return hipErrorInvalidValue;
     const uint64_t cols = (uint64_t)K * D + K;
     hipLaunchKernelGGL(reduce_kernel, dim3((int)((cols + 63) / 64)), dim3(REDUCE_THREADS), 0, s, part, part_cnt, G,
-                       nsub, K, D, sums);
+                       nsub, K, D, sums, pub);
     return hipGetLastError();
 }
 

@@ -6,6 +6,7 @@
 #include "kdtree.hpp"
 
 #include <algorithm>
+#include <cmath>
 #include <limits>
 #include <memory>
 
@@ -76,6 +77,8 @@ RefKDTree::RefKDTree(const double *pts, size_t K, int dim) : pts_(pts), dim_(dim
         }
     }
     nodes_.reserve(2 * (K / 5 + 1));
+    node_box_.clear();
+    node_box_.reserve(2 * (K / 5 + 1) * (size_t)dim);
     std::vector<Box> box(root_bbox_);
     divide(0, K, box.data(), 1, nodes_, depth_);
     flat_nodes_.resize(nodes_.size());
@@ -125,7 +128,7 @@ void RefKDTree::plane_split(size_t *ind, size_t count, int cutfeat, double cutva
 }
 
 void RefKDTree::middle_split(size_t *ind, size_t count, size_t &index, int &cutfeat, double &cutval,
-                             const Box *bbox) {
+                             const Box *bbox, Node *info) {
     const double EPS = 0.00001;
     double max_span = bbox[0].high - bbox[0].low;
     for (int i = 1; i < dim_; i++) max_span = std::max(max_span, bbox[i].high - bbox[i].low);
@@ -163,6 +166,17 @@ void RefKDTree::middle_split(size_t *ind, size_t count, size_t &index, int &cutf
     if (!have) min_max(ind, count, cutfeat, mn, mx);
     const double split_val = (bbox[cutfeat].low + bbox[cutfeat].high) / 2;
     cutval = split_val < mn ? mn : (split_val > mx ? mx : split_val);
+    {   // what a later change of one coordinate can move (unchanged_under)
+        double second = -std::numeric_limits<double>::infinity();
+        uint64_t cand = 0;
+        for (int j = 0; j < nq; j++) {
+            cand |= 1ull << q[j];
+            if (q[j] != cutfeat) second = std::max(second, qmx[j] - qmn[j]);
+        }
+        info->cand = cand;
+        info->spread_gap = have ? max_spread - second : -1.0;
+        info->split_val = split_val;
+    }
     size_t lim1, lim2;
     plane_split(ind, count, cutfeat, cutval, lim1, lim2);
     if (lim1 > count / 2) index = lim1;
@@ -175,24 +189,28 @@ int RefKDTree::divide(size_t left, size_t right, Box *bbox, int level, std::vect
     const int me = (int)nodes.size();
     depth = std::max(depth, level);
     nodes.push_back(Node());
+    node_box_.resize(node_box_.size() + dim_);
     if (right - left <= 10) {   // leaf_max_size (KDTreeVectorOfVectorsAdaptor.hpp:59)
         Node &n = nodes[me];
         n.leaf = true;
         n.left = left;
         n.right = right;
         n.child1 = n.child2 = -1;
+        n.cutval = 0;
         double mn[64], mx[64];
         rows_min_max(pts_, vind_.data() + left, right - left, dim_, mn, mx);   // row-major: a point's coordinates are contiguous
         for (int d = 0; d < dim_; d++) {
             bbox[d].low = mn[d];
             bbox[d].high = mx[d];
         }
+        std::copy(bbox, bbox + dim_, node_box_.begin() + (size_t)me * dim_);
         return me;
     }
     size_t idx;
     int cutfeat;
     double cutval;
-    middle_split(vind_.data() + left, right - left, idx, cutfeat, cutval, bbox);
+    Node info;
+    middle_split(vind_.data() + left, right - left, idx, cutfeat, cutval, bbox, &info);
     // children's boxes (a vector per node cost two heap allocations each)
     Box *lb = level_boxes(level), *rb = lb + dim_;
     std::copy(bbox, bbox + dim_, lb);
@@ -210,11 +228,59 @@ int RefKDTree::divide(size_t left, size_t right, Box *bbox, int level, std::vect
     n.child2 = c2;
     n.divlow = lb[cutfeat].high;
     n.divhigh = rb[cutfeat].low;
+    n.cutval = cutval;
+    n.split_val = info.split_val;
+    n.spread_gap = info.spread_gap;
+    n.cand = info.cand;
     for (int d = 0; d < dim_; d++) {
         bbox[d].low = std::min(lb[d].low, rb[d].low);
         bbox[d].high = std::max(lb[d].high, rb[d].high);
     }
+    std::copy(bbox, bbox + dim_, node_box_.begin() + (size_t)me * dim_);
     return me;
+}
+
+bool RefKDTree::unchanged_under(const double *pts2) const {
+    std::vector<uint32_t> pos;   // point -> its place in vind (built on the first changed coordinate)
+    for (size_t p = 0; p < K_; p++)
+        for (int d = 0; d < dim_; d++) {
+            const double x = pts_[p * (size_t)dim_ + d], y = pts2[p * (size_t)dim_ + d];
+            if (x == y && std::signbit(x) == std::signbit(y)) continue;
+            if (pos.empty()) {
+                pos.resize(K_);
+                for (size_t i = 0; i < K_; i++) pos[vind_[i]] = (uint32_t)i;
+            }
+            const double dev = std::fabs(x - y);
+            // the root box is every cell box's origin
+            if (!(x > root_bbox_[d].low && x < root_bbox_[d].high && y > root_bbox_[d].low && y < root_bbox_[d].high))
+                return false;
+            const size_t at = pos[p];
+            int node = 0;
+            while (!nodes_[node].leaf) {
+                const Node &n = nodes_[node];
+                const Box &b = node_box_[(size_t)node * dim_ + d];
+                const bool extreme = !(x > b.low && x < b.high && y > b.low && y < b.high);
+                if (extreme && ((n.cand >> d) & 1)) {
+                    // the spread of a candidate moves by at most dev: the choice must keep its margin
+                    if (!(n.spread_gap > 2 * dev)) return false;
+                    // and the cut dimension's clamp must stay inactive on both sides
+                    if (d == n.divfeat && (n.cutval != n.split_val || !((x < n.cutval) == (y < n.cutval))))
+                        return false;
+                }
+                if (n.divfeat == d) {   // the partition compares against the cut: same side, never equal
+                    const double c = n.cutval;
+                    if ((x < c) != (y < c) || x == c || y == c) return false;
+                }
+                const Node &c1 = nodes_[n.child1];
+                const bool left = at < c1.right;
+                if (n.divfeat == d) {   // the children's boxes give divlow / divhigh
+                    const Box &cb = node_box_[(size_t)(left ? n.child1 : n.child2) * dim_ + d];
+                    if (left ? !(x < cb.high && y < cb.high) : !(x > cb.low && y > cb.low)) return false;
+                }
+                node = left ? n.child1 : n.child2;
+            }
+        }
+    return true;
 }
 
 void RefKDTree::flatten(KdNodeDev *nodes, uint32_t *vind, double *lo, double *hi) const {

@@ -32,6 +32,11 @@ public:
     size_t num_nodes() const { return nodes_.size(); }
     int depth() const { return depth_; }
     void flatten(KdNodeDev *nodes, uint32_t *vind, double *lo, double *hi) const;
+    // True when the tree the reference would build over pts2 (K x dim, the same shape; e.g. the
+    // Kahan-bit codebook next to the exact-sum one) is this tree bit for bit: structure, cut
+    // values, boxes (a sufficient test, per differing coordinate along its point's path: the
+    // root box, the cut choices, cut values, partitions and children's boxes it can reach stay).
+    bool unchanged_under(const double *pts2) const;
 
 private:
     struct Node {
@@ -39,6 +44,9 @@ private:
         size_t left, right;      // the node's points: vind[left, right)
         int divfeat;
         double divlow, divhigh;
+        double cutval, split_val;   // the cut and the cell-box midpoint it was clamped from
+        double spread_gap;          // the cut dimension's spread minus the next candidate's
+        uint64_t cand;              // dimensions that were split candidates
         int child1, child2;
     };
     // the build reads one coordinate of many points at a time: a column-major copy keeps
@@ -47,7 +55,8 @@ private:
     double ptr(size_t i, int d) const { return pts_[i * (size_t)dim_ + d]; }   // row-major
     // bbox: the node's cell box (dim entries); children's boxes live in boxes_ at their level
     int divide(size_t left, size_t right, Box *bbox, int level, std::vector<Node> &nodes, int &depth);
-    void middle_split(size_t *ind, size_t count, size_t &index, int &cutfeat, double &cutval, const Box *bbox);
+    void middle_split(size_t *ind, size_t count, size_t &index, int &cutfeat, double &cutval, const Box *bbox,
+                      Node *info);
     void plane_split(size_t *ind, size_t count, int cutfeat, double cutval, size_t &lim1, size_t &lim2);
     void min_max(const size_t *ind, size_t count, int e, double &mn, double &mx) const;
     const double *pts_;
@@ -57,6 +66,7 @@ private:
     std::vector<size_t> vind_;
     std::vector<Node> nodes_;
     std::vector<Box> root_bbox_;
+    std::vector<Box> node_box_;   // [node][dim]: the node's actual point box (the build's in/out bbox)
     int depth_ = 0;
     std::vector<KdNodeDev> flat_nodes_;
     std::vector<uint32_t> flat_vind_;
