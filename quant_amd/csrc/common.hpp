@@ -377,11 +377,11 @@ struct KahanWork {
     uint32_t *hist = nullptr;          // [G][K] sort histograms (G = sort_blocks(N))
     uint32_t *tot = nullptr;           // [K] rows per cell
     uint32_t *koff = nullptr, *segoff = nullptr, *blkoff = nullptr;   // [K + 1] each
-    uint32_t *order = nullptr;         // [N] rows in cell order (stable)
     uint8_t *planes = nullptr;         // [D][plane_len(N)]: the chains' bytes, component-major
     void *meta = nullptr;              // [D][seg_cap] segment metadata
     void *bsum = nullptr;              // [D][blk_cap] 128-bit block totals, then prefixes
     void *bfn = nullptr;               // [D][blk_cap] block functions
+    void *sfn = nullptr;               // [D][seg_cap] segment functions
     void *tab = nullptr;               // the byte table (kahan::ByteTab)
     unsigned *stats = nullptr;         // [4] blocks not composable, block misses, segment replays
     uint32_t n_one = 0;                // K = 1: N (the mean's single cell)
@@ -393,6 +393,7 @@ struct KahanWork {
     static uint64_t plane_len(uint64_t N);
     static size_t meta_bytes();
     static size_t fn_bytes();
+    static size_t segfn_bytes();
     static uint32_t sort_blocks(uint64_t N);
 };
 // C [K][D] = the reference's centroids of assignment A (nullptr: K = 1, the mean of every row):

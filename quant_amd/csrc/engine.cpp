@@ -268,10 +268,10 @@ bool use_prune(const qvq_ctx *ctx, uint32_t K) {
 }
 
 void free_kahan_work(KahanWork &w) {
-    for (uint32_t **p : {&w.hist, &w.tot, &w.koff, &w.segoff, &w.blkoff, &w.order}) dfree(*p);
+    for (uint32_t **p : {&w.hist, &w.tot, &w.koff, &w.segoff, &w.blkoff}) dfree(*p);
     dfree(w.planes);
     dfree(w.stats);
-    for (void **p : {&w.meta, &w.bsum, &w.bfn, &w.tab})
+    for (void **p : {&w.meta, &w.bsum, &w.bfn, &w.sfn, &w.tab})
         if (*p) (void)hipFree(*p), *p = nullptr;
     w.seg_cap = w.blk_cap = w.n_cap = 0;
     w.k_cap = w.d_cap = 0;
@@ -584,12 +584,12 @@ qvq_status ensure_kahan(qvq_ctx *ctx, uint32_t Kc) {
     HIPCHK(hipMalloc(&w.hist, (uint64_t)KahanWork::sort_blocks(N) * kcap * 4));
     HIPCHK(hipMalloc(&w.tot, (uint64_t)kcap * 4));
     for (uint32_t **p : {&w.koff, &w.segoff, &w.blkoff}) HIPCHK(hipMalloc(p, ((uint64_t)kcap + 1) * 4));
-    HIPCHK(hipMalloc(&w.order, N * 4));
     HIPCHK(hipMalloc(&w.planes, (uint64_t)D * KahanWork::plane_len(N)));
     HIPCHK(hipMemset(w.planes, 0, (uint64_t)D * KahanWork::plane_len(N)));
     HIPCHK(hipMalloc(&w.meta, (uint64_t)D * segs * KahanWork::meta_bytes()));
     HIPCHK(hipMalloc(&w.bsum, (uint64_t)D * blks * 16));
     HIPCHK(hipMalloc(&w.bfn, (uint64_t)D * blks * KahanWork::fn_bytes()));
+    HIPCHK(hipMalloc(&w.sfn, (uint64_t)D * segs * KahanWork::segfn_bytes()));
     HIPCHK(hipMalloc(&w.stats, 4 * sizeof(unsigned)));
     HIPCHK(hipMemset(w.stats, 0, 4 * sizeof(unsigned)));
     {   // the byte table: SCALED values in units of 2^-60

@@ -33,7 +33,7 @@ using kahan::SPB;
 
 namespace {
 
-constexpr uint32_t SROWS = 4096;   // rows per sort block (one wave)
+constexpr uint32_t SROWS = 1024;   // rows per sort block (one wave)
 constexpr uint32_t BLK_STEPS = L * SPB;
 
 __device__ inline uint32_t lane_id() { return threadIdx.x & 63; }
@@ -212,6 +212,7 @@ struct Geo {
     SegMeta *meta;                            // [D][segoff[K]]
     u128 *bsum;                               // [D][blkoff[K]]: block totals, then (scan) block prefixes
     Fn *bfn;                                  // [D][blkoff[K]]
+    kahan::SegFn *sfn;                        // [D][segoff[K]]: the segment functions (estimates 0)
     unsigned *stats;                          // [4]: blocks not composable, block misses, segment replays, chains
 };
 
@@ -370,6 +371,11 @@ __global__ __launch_bounds__(64 * WPB) void ks_build_kernel(Geo g, const ByteTab
     wave_sync();
     build_block_fns(g, tab, bytes[w], k, d, b, 0, fns[w]);
     const uint32_t nseg = (n + L - 1) / L, cnt = min(SPB, nseg - b * SPB);
+    if (lane < cnt) {   // for the evaluation's re-walks of blocks that do not answer
+        kahan::SegFn sf;
+        kahan::pack_seg(fns[w][lane], sf);
+        g.sfn[(uint64_t)d * g.segoff[g.K] + g.segoff[k] + b * SPB + lane] = sf;
+    }
     ok[w][lane] = kahan::fkind(fns[w][lane]) != kahan::FK_RAW;
     wave_sync();
     for (uint32_t st = 1; st < SPB; st <<= 1) {   // tree: fns[i] <- fns[i] then fns[i + st]
@@ -496,13 +502,17 @@ __global__ __launch_bounds__(64 * EPB) void ks_eval_kernel(Geo g, const ByteTab 
                     }
                     nmiss++;
                 }
-                // segment by segment: the block's functions built from the exact D
+                // segment by segment: the block's stored segment functions, each checked
                 if (staged != b) {
                     stage_bytes(src + b * BLK_STEPS, min(BLK_STEPS, n - b * BLK_STEPS), bytes[w]);
-                    wave_sync();
                     staged = b;
                 }
-                pseg[w][lane] = build_block_fns(g, tab, bytes[w], k, d, b, D, fns[w]);
+                {
+                    const uint32_t s = b * SPB + lane;
+                    const u128 v = s < nseg ? kahan::meta_sum(g.meta[mbase + s]) : (u128)0;
+                    pseg[w][lane] = bpre[b] + wave_excl_scan(v);
+                    if (s < nseg) kahan::unpack_seg(g.sfn[mbase + s], fns[w][lane]);
+                }
                 wave_sync();
                 const uint32_t end = min(nseg, (b + 1) * SPB);
                 for (; j < end; j++) {
@@ -549,6 +559,7 @@ void KahanWork::caps(uint64_t N, uint32_t K, uint64_t &segs, uint64_t &blks) {
 uint64_t KahanWork::plane_len(uint64_t N) { return (N + 63) / 64 * 64 + 64; }
 size_t KahanWork::meta_bytes() { return sizeof(SegMeta); }
 size_t KahanWork::fn_bytes() { return sizeof(Fn); }
+size_t KahanWork::segfn_bytes() { return sizeof(kahan::SegFn); }
 uint32_t KahanWork::sort_blocks(uint64_t N) { return (uint32_t)((N + SROWS - 1) / SROWS); }
 
 hipError_t launch_kahan_centroids(hipStream_t s, const KahanWork &w, const uint8_t *codes, uint32_t Dp, uint32_t D,
@@ -591,6 +602,7 @@ hipError_t launch_kahan_centroids(hipStream_t s, const KahanWork &w, const uint8
     g.meta = reinterpret_cast<SegMeta *>(w.meta);
     g.bsum = reinterpret_cast<u128 *>(w.bsum);
     g.bfn = reinterpret_cast<Fn *>(w.bfn);
+    g.sfn = reinterpret_cast<kahan::SegFn *>(w.sfn);
     g.stats = w.stats;
     const ByteTab *tab = reinterpret_cast<const ByteTab *>(w.tab);
     // grids sized by the capacities; waves past the actual block count return at once

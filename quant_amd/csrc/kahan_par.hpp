@@ -96,6 +96,58 @@ QVQ_HD inline uint32_t rnd(uint32_t t, uint32_t lg) {
 // the way (0: computed at each decision from the exact E).  Out: the final F[e], the sums of
 // deltas ds[e], and [lo, hi] narrowed to the input D for which every decision of every entry
 // would be the same (absolute D of each entry's own input).
+// One step of NEN trajectories (byte c, its packed parameters pk).
+template <int NEN, bool EXACT_BL>
+QVQ_HD inline void step_n(const ByteTab &tb, uint32_t c, uint64_t pk, uint64_t &q, u128 &Pj, int bl0, uint32_t *F,
+                          const int64_t *D0, int32_t *d, int64_t &lo, int64_t &hi) {
+    if (pk >> 62) {   // x = 1.0: a decision per entry
+#pragma unroll
+        for (int e = 0; e < NEN; e++) {
+            const uint64_t E64 = q + (uint64_t)(D0[e] + d[e]);
+            int bl = bl0;
+            if (EXACT_BL) bl = bitlen(Pj + (u128)(i128)(D0[e] + d[e]));
+            const int su = bl - 53;
+            const uint64_t U = 1ull << su, h = U >> 1, ee = E64 & (U - 1);
+            const bool pos = ee < h || (ee == h && !((E64 >> su) & 1));
+            const uint32_t r8 = rnd(F[e], 8), r7 = rnd(F[e], 7), r = pos ? r8 : r7;
+            if (r8 != r7) {
+                int64_t l, u2;
+                if (ee == h) l = u2 = 0;
+                else if (pos) l = -(int64_t)ee, u2 = (int64_t)(h - 1 - ee);
+                else l = (int64_t)(h + 1 - ee), u2 = (int64_t)(U - 1 - ee);
+                if (EXACT_BL) {   // the shift must also keep E in its binade
+                    const i128 E = (i128)(Pj + (u128)(i128)(D0[e] + d[e]));
+                    const i128 bl_lo = ((i128)1 << (bl - 1)) - E, bl_hi = ((i128)1 << bl) - 1 - E;
+                    if (bl_lo > (i128)l) l = bl_lo > (i128)DLIM ? DLIM : (int64_t)bl_lo;
+                    if (bl_hi < (i128)u2) u2 = bl_hi < -(i128)DLIM ? -DLIM : (int64_t)bl_hi;
+                }
+                if (D0[e] + l > lo) lo = D0[e] + l;
+                if (D0[e] + u2 < hi) hi = D0[e] + u2;
+            }
+            d[e] += (int32_t)r - (int32_t)F[e];
+            F[e] = r & 511;
+        }
+    } else {
+        const uint32_t xm = (uint32_t)(pk >> 41) & 511, sh = (uint32_t)(pk >> 50) & 31;
+        const uint32_t hm1 = (uint32_t)(pk >> 55) & 127;
+        const uint32_t mask = sh == 31 ? 0xFFFFFFFFu : ~((1u << sh) - 1);
+#pragma unroll
+        for (int e = 0; e < NEN; e++) {
+            const uint32_t t = F[e] + xm;
+            const uint32_t r = (t + hm1 + ((t >> (sh & 31)) & (sh != 31))) & mask;
+            d[e] += (int32_t)r - (int32_t)t;
+            F[e] = r & 511;
+        }
+    }
+    q += pk & ((1ull << 41) - 1);
+    if (EXACT_BL) Pj += tb.X[c];
+}
+
+// NEN trajectories over steps b[0..n), all from the prefix P: entry e starts at E = P + D0[e]
+// with E mod 512 = F[e] (the caller's class representatives).  bl0: the binade of every E on
+// the way (0: computed at each decision from the exact E).  Out: the final F[e], the sums of
+// deltas ds[e], and [lo, hi] narrowed to the input D for which every decision of every entry
+// would be the same (absolute D of each entry's own input).
 template <int NEN, bool EXACT_BL>
 QVQ_HD inline void sim_n(const ByteTab &tb, const uint8_t *b, uint32_t n, u128 P, int bl0, uint32_t *F,
                          const int64_t *D0, int32_t *ds, int64_t &lo, int64_t &hi) {
@@ -104,62 +156,20 @@ QVQ_HD inline void sim_n(const ByteTab &tb, const uint8_t *b, uint32_t n, u128 P
     int32_t d[NEN];
 #pragma unroll
     for (int e = 0; e < NEN; e++) d[e] = 0;
-    const bool aligned = ((uintptr_t)b & 3) == 0;
-    for (uint32_t i0 = 0; i0 < n; i0 += 4) {
-        uint32_t word;
-        if (aligned && i0 + 4 <= n) word = *reinterpret_cast<const uint32_t *>(b + i0);
-        else {
-            word = 0;
-            for (uint32_t u = 0; u < 4 && i0 + u < n; u++) word |= (uint32_t)b[i0 + u] << (8 * u);
+    if (((uintptr_t)b & 3) == 0) {   // whole words: the four table reads of a word issued together
+        const uint32_t nw = n / 4;
+        for (uint32_t w = 0; w < nw; w++) {
+            const uint32_t word = reinterpret_cast<const uint32_t *>(b)[w];
+            uint64_t pk[4];
+#pragma unroll
+            for (int u = 0; u < 4; u++) pk[u] = tb.pk[(word >> (8 * u)) & 0xFF];
+#pragma unroll
+            for (int u = 0; u < 4; u++)
+                step_n<NEN, EXACT_BL>(tb, (word >> (8 * u)) & 0xFF, pk[u], q, Pj, bl0, F, D0, d, lo, hi);
         }
-        const uint32_t m = n - i0 < 4 ? n - i0 : 4;
-#pragma unroll
-        for (uint32_t u = 0; u < 4; u++) {
-            if (u >= m) break;
-            const uint32_t c = (word >> (8 * u)) & 0xFF;
-            const uint64_t pk = tb.pk[c];
-            if (pk >> 62) {   // x = 1.0: a decision per entry
-#pragma unroll
-                for (int e = 0; e < NEN; e++) {
-                    const uint64_t E64 = q + (uint64_t)(D0[e] + d[e]);
-                    int bl = bl0;
-                    if (EXACT_BL) bl = bitlen(Pj + (u128)(i128)(D0[e] + d[e]));
-                    const int su = bl - 53;
-                    const uint64_t U = 1ull << su, h = U >> 1, ee = E64 & (U - 1);
-                    const bool pos = ee < h || (ee == h && !((E64 >> su) & 1));
-                    const uint32_t r8 = rnd(F[e], 8), r7 = rnd(F[e], 7), r = pos ? r8 : r7;
-                    if (r8 != r7) {
-                        int64_t l, u2;
-                        if (ee == h) l = u2 = 0;
-                        else if (pos) l = -(int64_t)ee, u2 = (int64_t)(h - 1 - ee);
-                        else l = (int64_t)(h + 1 - ee), u2 = (int64_t)(U - 1 - ee);
-                        if (EXACT_BL) {   // the shift must also keep E in its binade
-                            const i128 E = (i128)(Pj + (u128)(i128)(D0[e] + d[e]));
-                            const i128 bl_lo = ((i128)1 << (bl - 1)) - E, bl_hi = ((i128)1 << bl) - 1 - E;
-                            if (bl_lo > (i128)l) l = bl_lo > (i128)DLIM ? DLIM : (int64_t)bl_lo;
-                            if (bl_hi < (i128)u2) u2 = bl_hi < -(i128)DLIM ? -DLIM : (int64_t)bl_hi;
-                        }
-                        if (D0[e] + l > lo) lo = D0[e] + l;
-                        if (D0[e] + u2 < hi) hi = D0[e] + u2;
-                    }
-                    d[e] += (int32_t)r - (int32_t)F[e];
-                    F[e] = r & 511;
-                }
-            } else {
-                const uint32_t xm = (uint32_t)(pk >> 41) & 511, sh = (uint32_t)(pk >> 50) & 31;
-                const uint32_t hm1 = (uint32_t)(pk >> 55) & 127;
-                const uint32_t mask = sh == 31 ? 0xFFFFFFFFu : ~((1u << sh) - 1);
-#pragma unroll
-                for (int e = 0; e < NEN; e++) {
-                    const uint32_t t = F[e] + xm;
-                    const uint32_t r = (t + hm1 + ((t >> (sh & 31)) & (sh != 31))) & mask;
-                    d[e] += (int32_t)r - (int32_t)t;
-                    F[e] = r & 511;
-                }
-            }
-            q += pk & ((1ull << 41) - 1);
-            if (EXACT_BL) Pj += tb.X[c];
-        }
+        for (uint32_t i = nw * 4; i < n; i++) step_n<NEN, EXACT_BL>(tb, b[i], tb.pk[b[i]], q, Pj, bl0, F, D0, d, lo, hi);
+    } else {
+        for (uint32_t i = 0; i < n; i++) step_n<NEN, EXACT_BL>(tb, b[i], tb.pk[b[i]], q, Pj, bl0, F, D0, d, lo, hi);
     }
 #pragma unroll
     for (int e = 0; e < NEN; e++) ds[e] = d[e];
@@ -196,6 +206,43 @@ struct Fn {
 };
 
 QVQ_HD inline uint8_t fkind(const Fn &f) { return f.kind & 0x7F; }
+
+// A segment's function as stored for the evaluation's re-walks (a segment's sums of deltas fit
+// 16 bits: 64 steps of at most 128 units).
+struct SegFn {
+    uint8_t kind, c_in, lne, c_out;
+    uint16_t off_in, off_out, sx9, pad;
+    int32_t lo, hi;
+    int16_t dlt[NE];
+};
+QVQ_HD inline void pack_seg(const Fn &f, SegFn &s) {
+    s.kind = f.kind;
+    s.c_in = f.c_in;
+    s.lne = f.lne;
+    s.c_out = f.c_out;
+    s.off_in = f.off_in;
+    s.off_out = f.off_out;
+    s.sx9 = f.sx9;
+    s.pad = 0;
+    s.lo = f.lo;
+    s.hi = f.hi;
+#pragma unroll
+    for (int e = 0; e < NE; e++) s.dlt[e] = (int16_t)f.dlt[e];
+}
+QVQ_HD inline void unpack_seg(const SegFn &s, Fn &f) {
+    f.kind = s.kind;
+    f.c_in = s.c_in;
+    f.lne = s.lne;
+    f.c_out = s.c_out;
+    f.off_in = s.off_in;
+    f.off_out = s.off_out;
+    f.sx9 = s.sx9;
+    f.pad = 0;
+    f.lo = s.lo;
+    f.hi = s.hi;
+#pragma unroll
+    for (int e = 0; e < NE; e++) f.dlt[e] = s.dlt[e];
+}
 QVQ_HD inline void set_raw(Fn &f) {
     f.kind = FK_RAW;
     f.c_in = f.lne = f.c_out = 0;
@@ -265,16 +312,17 @@ QVQ_HD inline bool compose(const Fn &f, const Fn &g, Fn &h) {
     h.pad = 0;
     int64_t lo = f.lo, hi = f.hi;
     const uint32_t mf = (1u << f.lne) - 1, mg = (1u << g.lne) - 1;
-    for (int e = 0; e < (1 << lne); e++) {
+#pragma unroll
+    for (int e = 0; e < NE; e++) {   // (a fixed trip count: h stays in registers)
         const uint32_t F0 = (f.off_in + ((uint32_t)e << f.c_in)) & 511;
         const int32_t d1 = f.dlt[e & mf];
         const uint32_t F1 = (F0 + f.sx9 + (uint32_t)d1) & 511;
         const int32_t d2 = g.dlt[(((F1 - g.off_in) & 511) >> g.c_in) & mg];
-        h.dlt[e] = d1 + d2;
-        if ((int64_t)g.lo - d1 > lo) lo = (int64_t)g.lo - d1;
-        if ((int64_t)g.hi - d1 < hi) hi = (int64_t)g.hi - d1;
+        const bool live = e < (1 << lne);
+        h.dlt[e] = live ? d1 + d2 : 0;
+        if (live && (int64_t)g.lo - d1 > lo) lo = (int64_t)g.lo - d1;
+        if (live && (int64_t)g.hi - d1 < hi) hi = (int64_t)g.hi - d1;
     }
-    for (int e = 1 << lne; e < NE; e++) h.dlt[e] = 0;
     h.lo = (int32_t)(lo < -DLIM ? -DLIM : lo);
     h.hi = (int32_t)(hi > DLIM ? DLIM : hi);
     if (h.lo > h.hi) h.lo = 1, h.hi = 0;   // never answers (every input re-walked)
@@ -372,7 +420,8 @@ QVQ_HD inline void build_group(const ByteTab &tb, const uint8_t *b, uint32_t n, 
     }
     sim_n<NEN, EXACT_BL>(tb, b, n, P, bl0, F, D0, ds, lo, hi);
 #pragma unroll
-    for (int e = 0; e < NEN; e++) f.dlt[e0 + e] = ds[e];
+    for (int e = 0; e < NE; e++)   // (a fixed trip count: f stays in registers)
+        if (e >= e0 && e < e0 + NEN) f.dlt[e] = ds[(e - e0) & (NEN - 1)];
 }
 
 // Segment j of a chain (n steps at b, exact prefix P at its start, metadata self, input class

@@ -22,6 +22,16 @@ def load_png_rgb(name):
     return np.frombuffer(im.tobytes(), np.uint8).copy(), w, h
 
 
+def reference_lbg(X, bits):
+    """The oracle's reference rule (Kahan centroids, sum_mode 0): its indices A_k, codebook C_k,
+    distortion d_k, and C_e, the engine's codebook for those indices (the exact-sum centroids
+    of the final cells, its documented centroid rule: within 1e-12 of C_k)."""
+    from oracle import oracle
+    C_k, A_k, d_k = oracle.lbg(X, bits, sum_mode=0)
+    C_e = oracle.centroids(X, A_k, 1 << bits, sum_mode=1)
+    return C_e, A_k, d_k, C_k
+
+
 @pytest.fixture(scope="session")
 def engine():
     import torch   # noqa: F401  (torch's bundled HIP runtime opens the device first: quant_amd.Engine)

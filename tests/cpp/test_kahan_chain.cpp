@@ -56,12 +56,14 @@ static double run_chain(const std::vector<uint8_t> &b, const ByteTab &tb, Stats 
     const uint32_t nblk = (nseg + SPB - 1) / SPB;
     std::vector<Fn> blk(nblk);
     std::vector<bool> blk_ok(nblk);
+    std::vector<SegFn> segfn(nseg);   // stored for the evaluation's re-walks (estimates 0)
     for (uint32_t bi = 0; bi < nblk; bi++) {
         const uint32_t s0 = bi * SPB, s1 = std::min(nseg, s0 + SPB);
         std::vector<Fn> f(SPB);
         std::vector<bool> ok(SPB, false);
         for (uint32_t s = s0; s < s1; s++) {
             build(s, 0, f[s - s0]);
+            pack_seg(f[s - s0], segfn[s]);
             ok[s - s0] = fkind(f[s - s0]) != FK_RAW;
             st.segs++;
             st.raw += !ok[s - s0];
@@ -107,10 +109,9 @@ static double run_chain(const std::vector<uint8_t> &b, const ByteTab &tb, Stats 
             st.blk_miss++;
         }
         const uint32_t end = std::min(nseg, (bi + 1) * SPB);
-        std::vector<Fn> fb(SPB);
-        for (uint32_t t = j; t < end; t++) build(t, D, fb[t - bi * SPB]);
         for (; j < end; j++) {
-            const Fn &f = fb[j - bi * SPB];
+            Fn f;
+            unpack_seg(segfn[j], f);
             uint32_t F2 = F;
             int64_t D2 = D;
             if (apply(f, F2, D2)) {

@@ -107,12 +107,15 @@ def test_sharded_ranks_bit_identical_c2(engine, tmp_path, world):
     """The N>1 schedule executed: C2's rows split over `world` processes (contiguous ranges,
     one shared GPU, the per-level exchange through gloo).  Every rank gets the 1-rank codebook
     and distortion bit for bit, the ranks' indices concatenate to the 1-rank indices, and all
-    equal the oracle (exact-sum rule; the Kahan rule's indices too)."""
+    equal the oracle (on one rank the reference's Kahan rule; with a communicator the engine
+    keeps the exact-sum rule, DESIGN.md 5 -- the two agree on this input)."""
     X, _ = oracle.tile(oracle.gen_image(512, 0x5EED), 512, 512, 2, 2)
     engine.set_vectors(X)
     C0, A0, d0 = engine.lbg(10)
     C_x, A_x, d_x = oracle.lbg(X, 10, sum_mode=1)
-    np.testing.assert_array_equal(A0, A_x)
+    _, A_k, _ = oracle.lbg(X, 10, sum_mode=0)
+    np.testing.assert_array_equal(A0, A_k)
+    np.testing.assert_array_equal(A_k, A_x)
     np.testing.assert_array_equal(C0, C_x)
     res = _run_ranks(world, "c2", tmp_path)
     for r in res:
@@ -133,7 +136,9 @@ def test_sharded_ranks_bit_identical_c5_slice(engine, tmp_path):
     imgs = [oracle.gen_image(512, 0x5EED + b) for b in range(4)]
     X = np.concatenate([oracle.tile(im, 512, 512, 2, 2)[0] for im in imgs])
     C_x, A_x, _ = oracle.lbg(X, 10, sum_mode=1)
-    np.testing.assert_array_equal(A0, A_x)
+    _, A_k, _ = oracle.lbg(X, 10, sum_mode=0)
+    np.testing.assert_array_equal(A0, A_k)   # one rank: the reference rule
+    np.testing.assert_array_equal(A_k, A_x)  # (the ranks' exact-sum rule agrees here)
     np.testing.assert_array_equal(C0, C_x)
     res = _run_ranks(2, "c5", tmp_path)
     for r in res:

@@ -6,7 +6,7 @@ Kahan mode (the reference's own rule; north-star tolerance is 1e-5)."""
 import numpy as np
 import pytest
 
-from conftest import load_png_rgb
+from conftest import load_png_rgb, reference_lbg
 from oracle import oracle
 
 pytestmark = pytest.mark.gpu
@@ -17,14 +17,12 @@ KAHAN_RTOL = 1e-12
 def _check_against_oracle(engine, rgb, xs, ys, bw, bh, bits, cs=oracle.SCALED):
     import quant_amd
     X, _ = oracle.tile(rgb, xs, ys, bw, bh, cs=cs, pad_code=128 if cs == oracle.SCALED else 0)
-    C_k, A_k, d_k = oracle.lbg(X, bits, sum_mode=0)
-    C_x, A_x, d_x = oracle.lbg(X, bits, sum_mode=1)
+    C_e, A_k, d_k, C_k = reference_lbg(X, bits)
     engine.set_images(rgb, 1, xs, ys, bw, bh, cs)
     C, A, d = engine.lbg(bits)
     assert A.shape == A_k.shape
-    np.testing.assert_array_equal(A, A_k)          # reference rule
-    np.testing.assert_array_equal(A, A_x)
-    np.testing.assert_array_equal(C, C_x)          # engine rule, bit-exact
+    np.testing.assert_array_equal(A, A_k)          # reference rule (Kahan centroid bits)
+    np.testing.assert_array_equal(C, C_e)          # engine centroid rule on those cells, bit-exact
     scale = np.maximum(np.abs(C_k), 1e-300)
     assert np.max(np.abs(C - C_k) / scale) <= KAHAN_RTOL
     assert abs(d - d_k) <= 1e-9 * abs(d_k)
@@ -83,20 +81,20 @@ def test_multi_image_batch(engine):
     # image-major concatenation (SURVEY.md 8(d) C5 definition) on a small batch
     imgs = [oracle.gen_image(64, 0x5EED + b) for b in range(3)]
     X = np.concatenate([oracle.tile(im, 64, 64, 2, 2)[0] for im in imgs])
-    C_x, A_x, _ = oracle.lbg(X, 6, sum_mode=1)
+    C_e, A_k, _, _ = reference_lbg(X, 6)
     engine.set_synthetic(64, 0x5EED, 3, 2, 2)
     C, A, _ = engine.lbg(6)
-    np.testing.assert_array_equal(A, A_x)
-    np.testing.assert_array_equal(C, C_x)
+    np.testing.assert_array_equal(A, A_k)
+    np.testing.assert_array_equal(C, C_e)
 
 
 def test_set_vectors_path(engine):
     X, _ = oracle.tile(oracle.gen_image(64), 64, 64, 2, 2)
-    C_x, A_x, _ = oracle.lbg(X, 5, sum_mode=1)
+    C_e, A_k, _, _ = reference_lbg(X, 5)
     engine.set_vectors(X)
     C, A, _ = engine.lbg(5)
-    np.testing.assert_array_equal(A, A_x)
-    np.testing.assert_array_equal(C, C_x)
+    np.testing.assert_array_equal(A, A_k)
+    np.testing.assert_array_equal(C, C_e)
 
 
 def test_set_vectors_rejects_bad_data(engine):
@@ -175,12 +173,11 @@ def test_lbg_zero_rows_and_empty_cells(engine, kdmode):
     X, _ = oracle.tile(oracle.gen_image(64), 64, 64, 2, 2)
     X = X[:300].copy()
     X[rng.choice(300, 120, replace=False)] = 0.0
-    C_k, A_k, d_k = oracle.lbg(X, 9, sum_mode=0)
-    C_x, A_x, _ = oracle.lbg(X, 9, sum_mode=1)
+    C_e, A_k, d_k, _ = reference_lbg(X, 9)
     engine.set_vectors(X)
     C, A, d = engine.lbg(9)
     np.testing.assert_array_equal(A, A_k)
-    np.testing.assert_array_equal(C, C_x)
+    np.testing.assert_array_equal(C, C_e)
     assert abs(d - d_k) <= 1e-9 * abs(d_k)
     assert sum(engine.timings()["host_ties"]) > 0
 

@@ -8,6 +8,7 @@ and NORMAL values.  Reference: src/Quantizer.cpp:24-32 (assign), nanoflann.hpp:3
 import numpy as np
 import pytest
 
+from conftest import reference_lbg
 from oracle import oracle
 
 pytestmark = pytest.mark.gpu
@@ -36,12 +37,12 @@ def test_pruned_search_matches_reference(engine, kind, cs):
     S = 256
     rgb = _image(kind, S)
     X, _ = oracle.tile(rgb, S, S, 2, 2, cs=cs, pad_code=128 if cs == oracle.SCALED else 0)
-    C_x, A_x, d_x = oracle.lbg(X, 10, sum_mode=1)
+    C_e, A_k, d_k, _ = reference_lbg(X, 10)
     engine.set_images(rgb, 1, S, S, 2, 2, quant_amd.SCALED if cs == oracle.SCALED else quant_amd.NORMAL)
     C, A, d = engine.lbg(10)
-    np.testing.assert_array_equal(A, A_x)
-    np.testing.assert_array_equal(C, C_x)
-    assert abs(d - d_x) <= 1e-9 * abs(d_x)
+    np.testing.assert_array_equal(A, A_k)
+    np.testing.assert_array_equal(C, C_e)
+    assert abs(d - d_k) <= 1e-9 * abs(d_k)
 
 
 # The wide search (D = 48, 4x4 blocks) prunes from K = 1024 with streamed codebook slices: a
@@ -53,12 +54,12 @@ def test_wide_pruned_search_matches_reference(engine, kind, S, bits, vectors):
     import quant_amd
     rgb = _image(kind, S, seed=3)
     X, _ = oracle.tile(rgb, S, S, 4, 4)
-    C_x, A_x, d_x = oracle.lbg(X, bits, sum_mode=1)
+    C_e, A_k, d_k, _ = reference_lbg(X, bits)
     if vectors:
         engine.set_vectors(X)
     else:
         engine.set_images(rgb, 1, S, S, 4, 4, quant_amd.SCALED)
     C, A, d = engine.lbg(bits)
-    np.testing.assert_array_equal(A, A_x)
-    np.testing.assert_array_equal(C, C_x)
-    assert abs(d - d_x) <= 1e-9 * abs(d_x)
+    np.testing.assert_array_equal(A, A_k)   # the reference rule (this case's exact-sum rule differs)
+    np.testing.assert_array_equal(C, C_e)
+    assert abs(d - d_k) <= 1e-9 * abs(d_k)
