@@ -382,6 +382,7 @@ struct KahanWork {
     void *bsum = nullptr;              // [D][blk_cap] 128-bit block totals, then prefixes
     void *bfn = nullptr;               // [D][blk_cap] block functions
     void *sfn = nullptr;               // [D][seg_cap] segment functions
+    void *bfn8 = nullptr;              // [D][blk_cap][8] 8-segment sub-block functions
     void *tab = nullptr;               // the byte table (kahan::ByteTab)
     unsigned *stats = nullptr;         // [4] blocks not composable, block misses, segment replays
     uint32_t n_one = 0;                // K = 1: N (the mean's single cell)

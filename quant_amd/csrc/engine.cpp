@@ -271,7 +271,7 @@ void free_kahan_work(KahanWork &w) {
     for (uint32_t **p : {&w.hist, &w.tot, &w.koff, &w.segoff, &w.blkoff}) dfree(*p);
     dfree(w.planes);
     dfree(w.stats);
-    for (void **p : {&w.meta, &w.bsum, &w.bfn, &w.sfn, &w.tab})
+    for (void **p : {&w.meta, &w.bsum, &w.bfn, &w.sfn, &w.bfn8, &w.tab})
         if (*p) (void)hipFree(*p), *p = nullptr;
     w.seg_cap = w.blk_cap = w.n_cap = 0;
     w.k_cap = w.d_cap = 0;
@@ -590,6 +590,7 @@ qvq_status ensure_kahan(qvq_ctx *ctx, uint32_t Kc) {
     HIPCHK(hipMalloc(&w.bsum, (uint64_t)D * blks * 16));
     HIPCHK(hipMalloc(&w.bfn, (uint64_t)D * blks * KahanWork::fn_bytes()));
     HIPCHK(hipMalloc(&w.sfn, (uint64_t)D * segs * KahanWork::segfn_bytes()));
+    HIPCHK(hipMalloc(&w.bfn8, (uint64_t)D * blks * 8 * KahanWork::fn_bytes()));
     HIPCHK(hipMalloc(&w.stats, 4 * sizeof(unsigned)));
     HIPCHK(hipMemset(w.stats, 0, 4 * sizeof(unsigned)));
     {   // the byte table: SCALED values in units of 2^-60

@@ -213,6 +213,7 @@ struct Geo {
     u128 *bsum;                               // [D][blkoff[K]]: block totals, then (scan) block prefixes
     Fn *bfn;                                  // [D][blkoff[K]]
     kahan::SegFn *sfn;                        // [D][segoff[K]]: the segment functions (estimates 0)
+    Fn *bfn8;                                 // [D][blkoff[K]][8]: 8-segment sub-block functions
     unsigned *stats;                          // [4]: blocks not composable, block misses, segment replays, chains
 };
 
@@ -335,11 +336,14 @@ __device__ inline u128 build_block_fns(const Geo &g, const ByteTab &tab, const u
     const u128 P = g.bsum[(uint64_t)d * g.blkoff[g.K] + g.blkoff[k] + b] +
                    wave_excl_scan(s < nseg ? kahan::meta_sum(self) : (u128)0);
     Fn f;
+    int ne = 0, bl0 = 0;
+    const uint8_t *bs = bytes + lane * L;
+    const uint32_t len = s < nseg ? min(L, n - s * L) : L;
     if (s < nseg) {
         int c_in;
         uint32_t off_in;
         kahan::input_structure([&](int i) { return g.meta[mbase + s - i]; }, (int)min(8u, s), c_in, off_in);
-        kahan::build_fn(tab, bytes + lane * L, min(L, n - s * L), P, self, c_in, off_in, s + 1 == nseg, D_est, f);
+        ne = kahan::build_header(bs, len, P, self, c_in, off_in, s + 1 == nseg, f, bl0);
     } else {
         f.kind = kahan::FK_TRANS;
         f.c_in = f.lne = f.c_out = 0;
@@ -347,6 +351,17 @@ __device__ inline u128 build_block_fns(const Geo &g, const ByteTab &tab, const u
         f.lo = f.hi = 0;
         for (int e = 0; e < kahan::NE; e++) f.dlt[e] = 0;
     }
+    // the entries, wave-uniform (lanes of one wave otherwise run every template variant in turn)
+    const bool fast = ne && bl0, slow = ne && !bl0;
+    int nf = fast ? ne : 0, nx = slow ? ne : 0;
+    for (int o = 32; o >= 1; o >>= 1) {
+        nf = max(nf, __shfl_xor(nf, o, 64));
+        nx = max(nx, __shfl_xor(nx, o, 64));
+    }
+    if (nf == 1 || nf == 2) kahan::build_entries<2, false>(tab, bs, len, P, bl0, D_est, 0, f, fast);
+    else
+        for (int e0 = 0; e0 < nf; e0 += 4) kahan::build_entries<4, false>(tab, bs, len, P, bl0, D_est, e0, f, fast && e0 < ne);
+    for (int e0 = 0; e0 < nx; e0++) kahan::build_entries<1, true>(tab, bs, len, P, 0, D_est, e0, f, slow && e0 < ne);
     fns[lane] = f;
     return P;
 }
@@ -386,6 +401,11 @@ __global__ __launch_bounds__(64 * WPB) void ks_build_kernel(Geo g, const ByteTab
             if (c) fns[w][lane] = h;
         }
         wave_sync();
+        if (st == 4 && (lane & 7) == 0 && lane < cnt) {   // the 8-segment sub-blocks, for the evaluation
+            Fn r = fns[w][lane];
+            if (!ok[w][lane]) kahan::set_raw(r);
+            g.bfn8[((uint64_t)d * TB + bb) * 8 + lane / 8] = r;
+        }
     }
     if (lane == 0) {
         Fn r = fns[w][0];
@@ -488,7 +508,9 @@ __global__ __launch_bounds__(64 * EPB) void ks_eval_kernel(Geo g, const ByteTab 
             }
             unsigned nmiss = 0, nrep = 0;
             const Fn *bf = g.bfn + (uint64_t)d * TB + g.blkoff[k];
+            const Fn *bf8 = g.bfn8 + ((uint64_t)d * TB + g.blkoff[k]) * 8;
             const uint32_t nblk = (nseg + SPB - 1) / SPB;
+            uint32_t loaded = 0xFFFFFFFFu;   // the block whose segment functions sit in fns[w]
             Fn fnext;
             if (j % SPB == 0 && j < nseg) fnext = bf[j / SPB];
             while (j < nseg) {
@@ -502,19 +524,28 @@ __global__ __launch_bounds__(64 * EPB) void ks_eval_kernel(Geo g, const ByteTab 
                     }
                     nmiss++;
                 }
-                // segment by segment: the block's stored segment functions, each checked
-                if (staged != b) {
-                    stage_bytes(src + b * BLK_STEPS, min(BLK_STEPS, n - b * BLK_STEPS), bytes[w]);
-                    staged = b;
+                if (j % 8 == 0) {   // the 8-segment sub-block
+                    const Fn f = bf8[j / 8];
+                    if (kahan::apply(f, F, D)) {
+                        j = min(nseg, j + 8);
+                        if (j % SPB == 0 && j < nseg) fnext = bf[j / SPB];
+                        continue;
+                    }
                 }
-                {
+                // segment by segment: the block's stored segment functions, each checked
+                if (loaded != b) {
+                    if (staged != b) {
+                        stage_bytes(src + b * BLK_STEPS, min(BLK_STEPS, n - b * BLK_STEPS), bytes[w]);
+                        staged = b;
+                    }
                     const uint32_t s = b * SPB + lane;
                     const u128 v = s < nseg ? kahan::meta_sum(g.meta[mbase + s]) : (u128)0;
                     pseg[w][lane] = bpre[b] + wave_excl_scan(v);
                     if (s < nseg) kahan::unpack_seg(g.sfn[mbase + s], fns[w][lane]);
+                    loaded = b;
+                    wave_sync();
                 }
-                wave_sync();
-                const uint32_t end = min(nseg, (b + 1) * SPB);
+                const uint32_t end = min(nseg, (j / 8 + 1) * 8);
                 for (; j < end; j++) {
                     if (kahan::apply(fns[w][j - b * SPB], F, D)) continue;
                     nrep++;
@@ -524,8 +555,7 @@ __global__ __launch_bounds__(64 * EPB) void ks_eval_kernel(Geo g, const ByteTab 
                     D = __shfl((long long)D, 0, 64);
                     F = __shfl(F, 0, 64);
                 }
-                if (end < nseg && end % SPB == 0) fnext = bf[end / SPB];
-                wave_sync();
+                if (j % SPB == 0 && j < nseg) fnext = bf[j / SPB];
             }
             result = kahan::to_double(Pn + (u128)(i128)D);
             if (g.stats && lane == 0 && (nmiss | nrep)) {
@@ -603,6 +633,7 @@ hipError_t launch_kahan_centroids(hipStream_t s, const KahanWork &w, const uint8
     g.bsum = reinterpret_cast<u128 *>(w.bsum);
     g.bfn = reinterpret_cast<Fn *>(w.bfn);
     g.sfn = reinterpret_cast<kahan::SegFn *>(w.sfn);
+    g.bfn8 = reinterpret_cast<Fn *>(w.bfn8);
     g.stats = w.stats;
     const ByteTab *tab = reinterpret_cast<const ByteTab *>(w.tab);
     // grids sized by the capacities; waves past the actual block count return at once

@@ -59,6 +59,7 @@ constexpr uint64_t ONE = 1ull << 60;      // x = 1.0
 struct ByteTab {
     uint64_t X[256];
     uint64_t pk[256];
+    uint64_t op[256];   // lo: X mod 512 | hm1 << 9 | parity shift << 16 (31: exact); hi: rounding mask
     int8_t cg[256], dg[256];
 };
 QVQ_HD inline int bitlen(u128 v) {
@@ -80,6 +81,8 @@ QVQ_HD inline void make_tab(const uint64_t *X, ByteTab &t) {
         const uint64_t hm1 = lg > 0 && lg < 8 ? (1ull << (lg - 1)) - 1 : 0;
         t.X[b] = x;
         t.pk[b] = (x & ((1ull << 41) - 1)) | ((x & 511) << 41) | (sh << 50) | (hm1 << 55) | ((uint64_t)(lg == 8) << 62);
+        const uint32_t mask = lg <= 0 || lg == 8 ? 0xFFFFFFFFu : ~((1u << lg) - 1);
+        t.op[b] = (x & 511) | (hm1 << 9) | (sh << 16) | ((uint64_t)mask << 32);
         t.cg[b] = (int8_t)(lg == 8 ? 7 : lg);
         t.dg[b] = (int8_t)lg;
     }
@@ -96,27 +99,32 @@ QVQ_HD inline uint32_t rnd(uint32_t t, uint32_t lg) {
 // the way (0: computed at each decision from the exact E).  Out: the final F[e], the sums of
 // deltas ds[e], and [lo, hi] narrowed to the input D for which every decision of every entry
 // would be the same (absolute D of each entry's own input).
-// One step of NEN trajectories (byte c, its packed parameters pk).
+// One step of NEN trajectories (byte c).  R[e] is the trajectory's fine state without the mod
+// 512 (only bits below 9 are ever read), so a step is four VALU per entry; Sxm accumulates X mod
+// 512 for the deltas: sum(delta) = R_end - R_start - Sxm (mod 2^32).
 template <int NEN, bool EXACT_BL>
-QVQ_HD inline void step_n(const ByteTab &tb, uint32_t c, uint64_t pk, uint64_t &q, u128 &Pj, int bl0, uint32_t *F,
-                          const int64_t *D0, int32_t *d, int64_t &lo, int64_t &hi) {
+QVQ_HD inline void step_n(const ByteTab &tb, uint32_t c, uint64_t &q, u128 &Pj, uint32_t &Sxm, int bl0, uint32_t *R,
+                          const int64_t *D0, const uint32_t *R0, int64_t &lo, int64_t &hi) {
+    const uint64_t pk = tb.pk[c];
     if (pk >> 62) {   // x = 1.0: a decision per entry
 #pragma unroll
         for (int e = 0; e < NEN; e++) {
-            const uint64_t E64 = q + (uint64_t)(D0[e] + d[e]);
+            const int64_t d = (int64_t)(int32_t)(R[e] - R0[e] - Sxm);   // deltas so far
+            const uint64_t E64 = q + (uint64_t)(D0[e] + d);
             int bl = bl0;
-            if (EXACT_BL) bl = bitlen(Pj + (u128)(i128)(D0[e] + d[e]));
+            if (EXACT_BL) bl = bitlen(Pj + (u128)(i128)(D0[e] + d));
             const int su = bl - 53;
             const uint64_t U = 1ull << su, h = U >> 1, ee = E64 & (U - 1);
             const bool pos = ee < h || (ee == h && !((E64 >> su) & 1));
-            const uint32_t r8 = rnd(F[e], 8), r7 = rnd(F[e], 7), r = pos ? r8 : r7;
+            const uint32_t F = R[e] & 511;
+            const uint32_t r8 = rnd(F, 8), r7 = rnd(F, 7), r = pos ? r8 : r7;
             if (r8 != r7) {
                 int64_t l, u2;
                 if (ee == h) l = u2 = 0;
                 else if (pos) l = -(int64_t)ee, u2 = (int64_t)(h - 1 - ee);
                 else l = (int64_t)(h + 1 - ee), u2 = (int64_t)(U - 1 - ee);
                 if (EXACT_BL) {   // the shift must also keep E in its binade
-                    const i128 E = (i128)(Pj + (u128)(i128)(D0[e] + d[e]));
+                    const i128 E = (i128)(Pj + (u128)(i128)(D0[e] + d));
                     const i128 bl_lo = ((i128)1 << (bl - 1)) - E, bl_hi = ((i128)1 << bl) - 1 - E;
                     if (bl_lo > (i128)l) l = bl_lo > (i128)DLIM ? DLIM : (int64_t)bl_lo;
                     if (bl_hi < (i128)u2) u2 = bl_hi < -(i128)DLIM ? -DLIM : (int64_t)bl_hi;
@@ -124,20 +132,18 @@ QVQ_HD inline void step_n(const ByteTab &tb, uint32_t c, uint64_t pk, uint64_t &
                 if (D0[e] + l > lo) lo = D0[e] + l;
                 if (D0[e] + u2 < hi) hi = D0[e] + u2;
             }
-            d[e] += (int32_t)r - (int32_t)F[e];
-            F[e] = r & 511;
+            R[e] += r - F;   // (X mod 512 = 0 for x = 1.0)
         }
     } else {
-        const uint32_t xm = (uint32_t)(pk >> 41) & 511, sh = (uint32_t)(pk >> 50) & 31;
-        const uint32_t hm1 = (uint32_t)(pk >> 55) & 127;
-        const uint32_t mask = sh == 31 ? 0xFFFFFFFFu : ~((1u << sh) - 1);
+        const uint64_t op = tb.op[c];
+        const uint32_t xm = (uint32_t)op & 511, hm1 = ((uint32_t)op >> 9) & 127, sh = ((uint32_t)op >> 16) & 31;
+        const uint32_t mask = (uint32_t)(op >> 32);
 #pragma unroll
         for (int e = 0; e < NEN; e++) {
-            const uint32_t t = F[e] + xm;
-            const uint32_t r = (t + hm1 + ((t >> (sh & 31)) & (sh != 31))) & mask;
-            d[e] += (int32_t)r - (int32_t)t;
-            F[e] = r & 511;
+            const uint32_t t = R[e] + xm;
+            R[e] = (t + hm1 + ((t >> sh) & 1)) & mask;   // sh = 31 (exact): t < 2^31 reads 0
         }
+        Sxm += xm;
     }
     q += pk & ((1ull << 41) - 1);
     if (EXACT_BL) Pj += tb.X[c];
@@ -153,26 +159,25 @@ QVQ_HD inline void sim_n(const ByteTab &tb, const uint8_t *b, uint32_t n, u128 P
                          const int64_t *D0, int32_t *ds, int64_t &lo, int64_t &hi) {
     uint64_t q = (uint64_t)P;   // the prefix mod 2^64 (only bits < 41 are read)
     u128 Pj = P;
-    int32_t d[NEN];
+    uint32_t Sxm = 0, R[NEN], R0[NEN];
 #pragma unroll
-    for (int e = 0; e < NEN; e++) d[e] = 0;
-    if (((uintptr_t)b & 3) == 0) {   // whole words: the four table reads of a word issued together
+    for (int e = 0; e < NEN; e++) R[e] = R0[e] = F[e];
+    if (((uintptr_t)b & 3) == 0) {   // whole words
         const uint32_t nw = n / 4;
         for (uint32_t w = 0; w < nw; w++) {
             const uint32_t word = reinterpret_cast<const uint32_t *>(b)[w];
-            uint64_t pk[4];
 #pragma unroll
-            for (int u = 0; u < 4; u++) pk[u] = tb.pk[(word >> (8 * u)) & 0xFF];
-#pragma unroll
-            for (int u = 0; u < 4; u++)
-                step_n<NEN, EXACT_BL>(tb, (word >> (8 * u)) & 0xFF, pk[u], q, Pj, bl0, F, D0, d, lo, hi);
+            for (int u = 0; u < 4; u++) step_n<NEN, EXACT_BL>(tb, (word >> (8 * u)) & 0xFF, q, Pj, Sxm, bl0, R, D0, R0, lo, hi);
         }
-        for (uint32_t i = nw * 4; i < n; i++) step_n<NEN, EXACT_BL>(tb, b[i], tb.pk[b[i]], q, Pj, bl0, F, D0, d, lo, hi);
+        for (uint32_t i = nw * 4; i < n; i++) step_n<NEN, EXACT_BL>(tb, b[i], q, Pj, Sxm, bl0, R, D0, R0, lo, hi);
     } else {
-        for (uint32_t i = 0; i < n; i++) step_n<NEN, EXACT_BL>(tb, b[i], tb.pk[b[i]], q, Pj, bl0, F, D0, d, lo, hi);
+        for (uint32_t i = 0; i < n; i++) step_n<NEN, EXACT_BL>(tb, b[i], q, Pj, Sxm, bl0, R, D0, R0, lo, hi);
     }
 #pragma unroll
-    for (int e = 0; e < NEN; e++) ds[e] = d[e];
+    for (int e = 0; e < NEN; e++) {
+        ds[e] = (int32_t)(R[e] - R0[e] - Sxm);
+        F[e] = R[e] & 511;
+    }
 }
 
 // One trajectory (the exact replay: D0 is the true input D, so every decision is the true one).
@@ -352,28 +357,30 @@ QVQ_HD inline SegMeta seg_meta(const ByteTab &tb, const uint8_t *b, uint32_t n) 
             word = 0;
             for (uint32_t u = 0; u < 4 && i0 + u < n; u++) word |= (uint32_t)b[i0 + u] << (8 * u);
         }
+        const uint32_t m4 = n - i0 < 4 ? n - i0 : 4;
 #pragma unroll
         for (uint32_t u = 0; u < 4; u++) {
-            if (i0 + u >= n) break;
             const uint32_t c = (word >> (8 * u)) & 0xFF;
-            const int cg = tb.cg[c], dg = tb.dg[c];
-            if (cg >= 0) key = key > (cg << 8 | (int)(i0 + u)) ? key : (cg << 8 | (int)(i0 + u));
+            const int cg = u < m4 ? tb.cg[c] : -1, dg = u < m4 ? tb.dg[c] : -1;
+            const int kk = cg << 8 | (int)(i0 + u);
+            key = cg >= 0 && kk > key ? kk : key;
             G = G > dg ? G : dg;
-            const uint64_t x = tb.X[c], t = slo + x;
+            const uint64_t x = u < m4 ? tb.X[c] : 0, t = slo + x;
             shi += t < slo;
             slo = t;
         }
     }
     const int cmax = key < 0 ? -1 : key >> 8;
     uint32_t F = 0;
-    if (cmax >= 0)
-        for (uint32_t i = (uint32_t)(key & 0xFF) + 1; i < n; i++) {   // grades below cmax: no decisions, no class reads
-            const uint64_t pk = tb.pk[b[i]];
-            const uint32_t t = F + (uint32_t)((pk >> 41) & 511), sh = (uint32_t)((pk >> 50) & 31);
-            const uint32_t hm1 = (uint32_t)((pk >> 55) & 127);
-            F = sh == 31 ? t : (t + hm1 + ((t >> sh) & 1)) & ~((1u << sh) - 1);
-            F &= (1u << cmax) - 1;
+    if (cmax >= 0) {   // the tail after the anchor: grades below cmax, no decisions, no class reads
+        const uint32_t mk = (1u << cmax) - 1;
+        for (uint32_t i = (uint32_t)(key & 0xFF) + 1; i < n; i++) {
+            const uint64_t op = tb.op[b[i]];
+            const uint32_t xm = (uint32_t)op & 511, hm1 = ((uint32_t)op >> 9) & 127, sh = ((uint32_t)op >> 16) & 31;
+            const uint32_t t = F + xm;
+            F = ((t + hm1 + ((t >> sh) & 1)) & (uint32_t)(op >> 32)) & mk;
         }
+    }
     m.s_lo = slo;
     m.s_hi = (uint8_t)shi;
     m.cmax = (int8_t)cmax;
@@ -408,7 +415,7 @@ QVQ_HD inline void input_structure(PrevFn prev, int np, int &c_in, uint32_t &off
 // Entries [e0, e0 + NEN) of f through sim_n (f's header already set); [lo, hi] narrowed.
 template <int NEN, bool EXACT_BL>
 QVQ_HD inline void build_group(const ByteTab &tb, const uint8_t *b, uint32_t n, u128 P, int bl0, int64_t D_est,
-                               int e0, Fn &f, int64_t &lo, int64_t &hi) {
+                               int e0, Fn &f, int64_t &lo, int64_t &hi, bool active = true) {
     uint32_t F[NEN];
     int64_t D0[NEN];
     int32_t ds[NEN];
@@ -418,18 +425,28 @@ QVQ_HD inline void build_group(const ByteTab &tb, const uint8_t *b, uint32_t n, 
         // the representative input D: D == F - P (mod 512), next to D_est
         D0[e] = D_est + (int64_t)((F[e] - (uint32_t)(uint64_t)P - (uint32_t)D_est + 256) & 511) - 256;
     }
-    sim_n<NEN, EXACT_BL>(tb, b, n, P, bl0, F, D0, ds, lo, hi);
+    int64_t l2 = lo, h2 = hi;
+    sim_n<NEN, EXACT_BL>(tb, b, n, P, bl0, F, D0, ds, l2, h2);
+    if (!active) return;   // (a lane that ran along with its wave)
+    lo = l2;
+    hi = h2;
 #pragma unroll
     for (int e = 0; e < NE; e++)   // (a fixed trip count: f stays in registers)
         if (e >= e0 && e < e0 + NEN) f.dlt[e] = ds[(e - e0) & (NEN - 1)];
 }
 
 // Segment j of a chain (n steps at b, exact prefix P at its start, metadata self, input class
-// structure (c_in, off_in) from input_structure); final: the chain's last segment.  D_est: the
-// estimate of the input D that decides the x = 1.0 steps (any value is safe).
-QVQ_HD inline void build_fn(const ByteTab &tb, const uint8_t *b, uint32_t n, u128 P, const SegMeta &self, int c_in,
-                            uint32_t off_in, bool final, int64_t D_est, Fn &f) {
+// structure (c_in, off_in) from input_structure); final: the chain's last segment.  The header
+// of its function (kind, classes, output structure); returns the entries to simulate (0: none,
+// the function is complete) and in bl0 the binade of the segment's states (0: a power of two
+// inside its range, each decision then takes the exact binade).
+QVQ_HD inline int build_header(const uint8_t *b, uint32_t n, u128 P, const SegMeta &self, int c_in, uint32_t off_in,
+                               bool final, Fn &f, int &bl0) {
+    (void)b;
+    (void)n;
     f.pad = 0;
+    bl0 = 0;
+    for (int e = 0; e < NE; e++) f.dlt[e] = 0;
     if (self.G < 0) {   // every step exact: a translation
         f.kind = (uint8_t)(FK_TRANS | (final ? FK_FINAL : 0));
         f.c_in = f.lne = f.c_out = 0;
@@ -437,13 +454,12 @@ QVQ_HD inline void build_fn(const ByteTab &tb, const uint8_t *b, uint32_t n, u12
         f.sx9 = self.sx9;
         f.lo = -(int32_t)DLIM;
         f.hi = (int32_t)DLIM;
-        for (int e = 0; e < NE; e++) f.dlt[e] = 0;
-        return;
+        return 0;
     }
     const int lne = self.G + 1 - c_in > 0 ? self.G + 1 - c_in : 0;
     if (c_in < 0 || P < MIN_STATE + (u128)DLIM || lne > 4) {
         set_raw(f);
-        return;
+        return 0;
     }
     f.kind = (uint8_t)(FK_TABLE | (final ? FK_FINAL : 0));
     f.c_in = (uint8_t)c_in;
@@ -452,20 +468,37 @@ QVQ_HD inline void build_fn(const ByteTab &tb, const uint8_t *b, uint32_t n, u12
     f.off_in = (uint16_t)off_in;
     f.off_out = self.off;
     f.sx9 = self.sx9;
-    for (int e = 0; e < NE; e++) f.dlt[e] = 0;
-    int64_t lo = -DLIM, hi = DLIM;
-    const int bl0 = fixed_binade(P, meta_sum(self));
-    if (bl0) {   // the binade is fixed: entries in groups of up to 4
-        if (lne == 0) build_group<1, false>(tb, b, n, P, bl0, D_est, 0, f, lo, hi);
-        else if (lne == 1) build_group<2, false>(tb, b, n, P, bl0, D_est, 0, f, lo, hi);
-        else
-            for (int e0 = 0; e0 < (1 << lne); e0 += 4) build_group<4, false>(tb, b, n, P, bl0, D_est, e0, f, lo, hi);
-    } else {     // a power of two inside the segment's range: each entry with the exact binade
-        for (int e0 = 0; e0 < (1 << lne); e0++) build_group<1, true>(tb, b, n, P, 0, D_est, e0, f, lo, hi);
-    }
+    f.lo = -(int32_t)DLIM;
+    f.hi = (int32_t)DLIM;
+    bl0 = fixed_binade(P, meta_sum(self));
+    return 1 << lne;
+}
+
+// Entries [e0, e0 + NEN) of f (header set by build_header), f's interval narrowed.
+template <int NEN, bool EXACT_BL>
+QVQ_HD inline void build_entries(const ByteTab &tb, const uint8_t *b, uint32_t n, u128 P, int bl0, int64_t D_est,
+                                 int e0, Fn &f, bool active = true) {
+    int64_t lo = f.lo, hi = f.hi;
+    build_group<NEN, EXACT_BL>(tb, b, n, P, bl0, D_est, e0, f, lo, hi, active);
+    if (!active) return;
     f.lo = (int32_t)lo;
     f.hi = (int32_t)hi;
     if (f.lo > f.hi) f.lo = 1, f.hi = 0;
+}
+
+// The whole function (host; the device runs the entries wave-uniformly, k_kahan.hip).
+QVQ_HD inline void build_fn(const ByteTab &tb, const uint8_t *b, uint32_t n, u128 P, const SegMeta &self, int c_in,
+                            uint32_t off_in, bool final, int64_t D_est, Fn &f) {
+    int bl0;
+    const int ne = build_header(b, n, P, self, c_in, off_in, final, f, bl0);
+    if (!ne) return;
+    if (bl0) {
+        if (ne <= 2) build_entries<2, false>(tb, b, n, P, bl0, D_est, 0, f);
+        else
+            for (int e0 = 0; e0 < ne; e0 += 4) build_entries<4, false>(tb, b, n, P, bl0, D_est, e0, f);
+    } else {
+        for (int e0 = 0; e0 < ne; e0++) build_entries<1, true>(tb, b, n, P, 0, D_est, e0, f);
+    }
 }
 
 // ---- the transient and the final rounding -------------------------------------------------------

@@ -129,7 +129,12 @@ static double run_chain(const std::vector<uint8_t> &b, const ByteTab &tb, Stats 
 
 static int check(const std::vector<uint8_t> &b, const ByteTab &tb, Stats &st, const char *what) {
     const double ref = kahan_ref(b, tb);
+    const Stats before = st;
     const double got = run_chain(b, tb, st);
+    if (getenv("KCHAIN"))   // per chain: blocks, re-walked blocks, replays
+        printf("chain n %zu blocks %llu bad %llu miss %llu replays %llu\n", b.size(),
+               (unsigned long long)(st.blocks - before.blocks), (unsigned long long)(st.blk_bad - before.blk_bad),
+               (unsigned long long)(st.blk_miss - before.blk_miss), (unsigned long long)(st.replays - before.replays));
     if (memcmp(&ref, &got, 8) != 0) {
         printf("MISMATCH %s n %zu: ref %.17g got %.17g\n", what, b.size(), ref, got);
         return 1;
