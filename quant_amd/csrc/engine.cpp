@@ -24,6 +24,7 @@
 #include <cstring>
 #include <string>
 #include <memory>
+#include <unordered_map>
 #include <vector>
 
 #include "common.hpp"
@@ -108,6 +109,9 @@ struct qvq_ctx {
     double *d_kc_cent = nullptr, *d_kc_split = nullptr;   // Kahan centroids [K/2][D], their split [K][D]
     uint32_t kc_kcap = 0;
     std::vector<double> h_kc_split;   // host copy of the split for the tree build
+    uint8_t *d_kc_sel = nullptr;      // [K/2] the cells a tie certificate needs the reference's sums of
+    std::vector<double> cert_kp;      // the reference's split where known (tie certificate)
+    std::vector<uint8_t> cert_known;
     uint64_t pub_seq = 0;          // per-level tie-count publications (h_ready[1] = seq, h_ready[2] = ties)
     double tie_abs = 0;            // the recheck's absolute tie band: centroid bits may differ by this much
     unsigned *d_counters = nullptr;   // per level: [2l] flagged rows, [2l+1] kd-tree ties; [66], [67] block counters;
@@ -281,6 +285,7 @@ void free_kahan(qvq_ctx *ctx) {
     free_kahan_work(ctx->kw);
     dfree(ctx->d_kc_cent);
     dfree(ctx->d_kc_split);
+    dfree(ctx->d_kc_sel);
     ctx->kc_kcap = 0;
 }
 
@@ -572,8 +577,10 @@ qvq_status ensure_kahan(qvq_ctx *ctx, uint32_t Kc) {
     if (ctx->kc_kcap < Kc) {
         dfree(ctx->d_kc_cent);
         dfree(ctx->d_kc_split);
+        dfree(ctx->d_kc_sel);
         HIPCHK(hipMalloc(&ctx->d_kc_cent, (uint64_t)Kc * D * 8));
         HIPCHK(hipMalloc(&ctx->d_kc_split, 2ull * Kc * D * 8));
+        HIPCHK(hipMalloc(&ctx->d_kc_sel, Kc));
         ctx->kc_kcap = Kc;
     }
     if (w.n_cap == N && w.k_cap >= Kc && w.d_cap == D) return QVQ_OK;
@@ -916,6 +923,110 @@ qvq_status run_level(qvq_ctx *ctx, uint32_t K, int slot, bool sums_out, const do
     return QVQ_OK;
 }
 
+// |c_kahan - c_exact| per split component for SCALED values (the tie band's delta)
+constexpr double KAHAN_DELTA = 0x1p-49;
+
+// The ties of a Kahan level answered from the level's own tree (over the exact-sum split) and
+// the reference's sums of the few cells that can matter: each tie row's
+// candidates (every code vector within a slack of its nearest that covers the reference's
+// bits), the reference's Kahan centroids of the candidates' parent cells (the selected cells
+// only), then the reference's search replayed over every split the certificate allows
+// (RefKDTree::certified_search).  done = false, nothing changed, when a row is not decided:
+// the caller then computes the whole split and its tree.
+qvq_status certify_kahan_ties(qvq_ctx *ctx, uint32_t K, unsigned nt, uint64_t *target, bool &done) {
+    done = false;
+    static const bool on = !env_is("QVQ_TIE_CERT", "0");
+    if (!on || !ctx->tree || ctx->cb_local.size() != (size_t)K * ctx->D || K < 4) return QVQ_OK;
+    const uint32_t D = ctx->D, Dp = ctx->Dp, Kc = K / 2;
+    const RefKDTree &tree = *ctx->tree;
+    const uint64_t need = (uint64_t)nt * (4 + Dp);
+    if (ctx->scatter_bytes < need) {
+        dfree(ctx->d_scatter);
+        HIPCHK(hipMalloc(&ctx->d_scatter, need));
+        ctx->scatter_bytes = need;
+    }
+    uint32_t *d_vals = ctx->d_scatter;
+    uint8_t *d_gath = reinterpret_cast<uint8_t *>(ctx->d_scatter + nt);
+    std::vector<uint8_t> code((uint64_t)nt * Dp);
+    HIPCHK(launch_gather_codes(ctx->stream, ctx->d_codes, Dp, ctx->d_ties, nt, d_gath));
+    HIPCHK(hipMemcpyAsync(code.data(), d_gath, code.size(), hipMemcpyDeviceToHost, ctx->stream));
+    qvq_status st;
+    if ((st = wait_stream(ctx)) != QVQ_OK) return st;
+    // coordinates whose reference bits are the exact sums' without computing them: a cell's
+    // exact mean is 0 or 1 only when all its values are (SCALED values lie in [0, 1], at least
+    // 1/(255 n) from 1 otherwise; Kahan sums of 0s and 1s are exact), split by 1.2 or 0.8
+    std::vector<double> &kp = ctx->cert_kp;
+    std::vector<uint8_t> &known = ctx->cert_known;
+    kp.assign(ctx->cb_local.begin(), ctx->cb_local.end());
+    known.resize((size_t)K * D);
+    for (size_t i = 0; i < known.size(); i++) {
+        const double u = i / D < Kc ? 1 + 0.2 : 1 - 0.2, v = kp[i];
+        known[i] = v == 0 || std::fabs(v - u) <= 1e-14;
+    }
+    // distinct rows, their candidates, the cells to sum
+    std::unordered_map<std::string, uint32_t> uniq;
+    std::vector<uint32_t> of(nt);
+    std::vector<double> qs;
+    for (uint32_t i = 0; i < nt; i++) {
+        const auto it = uniq.emplace(std::string(reinterpret_cast<const char *>(&code[(size_t)i * Dp]), D),
+                                     (uint32_t)uniq.size());
+        of[i] = it.first->second;
+        if (it.second)
+            for (uint32_t d = 0; d < D; d++) qs.push_back(ctx->terms.v64[code[(size_t)i * Dp + d]]);
+    }
+    const uint32_t nu = (uint32_t)uniq.size();
+    std::vector<std::vector<uint32_t>> cand(nu);
+    std::vector<uint8_t> sel(Kc, 0);
+    uint32_t cells = 0;
+    for (uint32_t u = 0; u < nu; u++) {
+        double dmin;
+        tree.near_set(&qs[(size_t)u * D], 1e-9, 1e-9, cand[u], dmin);
+        for (uint32_t j : cand[u])
+            for (uint32_t d = 0; d < D; d++)
+                if (!known[(size_t)j * D + d]) {
+                    cells += !sel[j % Kc];
+                    sel[j % Kc] = 1;
+                    break;
+                }
+    }
+    if (cells) {   // the reference's centroids of those cells (of the previous level's assignment)
+        if ((st = ensure_kahan(ctx, Kc)) != QVQ_OK) return st;
+        HIPCHK(hipMemcpyAsync(ctx->d_kc_sel, sel.data(), Kc, hipMemcpyHostToDevice, ctx->stream));
+        HIPCHK(launch_kahan_centroids(ctx->stream, ctx->kw, ctx->d_codes, ctx->Dp, D, ctx->N, ctx->d_A_alt, Kc,
+                                      ctx->d_kc_cent, ctx->d_kc_split, ctx->d_kc_sel));
+        ctx->h_kc_split.resize((size_t)K * D);
+        HIPCHK(hipMemcpyAsync(ctx->h_kc_split.data(), ctx->d_kc_split, (size_t)K * D * 8, hipMemcpyDeviceToHost,
+                              ctx->stream));
+        if ((st = wait_stream(ctx)) != QVQ_OK) return st;
+        for (uint32_t c = 0; c < Kc; c++)
+            if (sel[c])
+                for (uint32_t r : {c, c + Kc}) {
+                    std::memcpy(&kp[(size_t)r * D], &ctx->h_kc_split[(size_t)r * D], D * 8);
+                    std::memset(&known[(size_t)r * D], 1, D);
+                }
+    }
+    std::vector<uint32_t> ans(nu), vals(nt);
+    for (uint32_t u = 0; u < nu; u++) {
+        const int64_t a = certify_tie(tree, &qs[(size_t)u * D], cand[u], kp.data(), known.data(), (int)D, KAHAN_DELTA);
+        if (a < 0) {
+            if (env_is("QVQ_KAHAN_DEBUG", "1"))
+                std::fprintf(stderr, "qvq kahan: K %u ties %u (%u distinct) cells %u: row not certified\n", K, nt, nu,
+                             cells);
+            return QVQ_OK;
+        }
+        ans[u] = (uint32_t)a;
+    }
+    for (uint32_t i = 0; i < nt; i++) vals[i] = ans[of[i]];
+    HIPCHK(hipMemcpyAsync(d_vals, vals.data(), nt * 4, hipMemcpyHostToDevice, ctx->stream));
+    HIPCHK(launch_fix_rows(ctx->stream, ctx->d_codes, Dp, D, ctx->d_A, ctx->d_ties, d_vals, nt, K, nullptr, nullptr,
+                           ctx->d_plut, target));
+    if ((st = wait_stream(ctx)) != QVQ_OK) return st;   // vals must outlive the copy
+    if (env_is("QVQ_KAHAN_DEBUG", "1"))
+        std::fprintf(stderr, "qvq kahan: K %u ties %u (%u distinct) certified, cells summed %u\n", K, nt, nu, cells);
+    done = true;
+    return QVQ_OK;
+}
+
 // The ties of a level run with defer_ties (nt > 0 of them in d_ties): the reference's split
 // codebook -- the previous level's centroids as Kahan sums in row order (k_kahan.hip; for the
 // NORMAL colour space the exact sums are those bits already), split -- its kd-tree, and the
@@ -925,7 +1036,10 @@ qvq_status resolve_kahan_ties(qvq_ctx *ctx, uint32_t K, int slot, unsigned nt, b
     const uint32_t D = ctx->D, Kc = K / 2;
     const double *S_ref = ctx->d_C64_split;
     qvq_status st;
+    uint64_t *target = fused ? ctx->d_sums + sums_cap_stride(ctx) : ctx->d_sums;
     if (ctx->cs == QVQ_CS_SCALED) {
+        bool done;
+        if ((st = certify_kahan_ties(ctx, K, nt, target, done)) != QVQ_OK || done) return st;
         if ((st = ensure_kahan(ctx, Kc)) != QVQ_OK) return st;
         HIPCHK(launch_kahan_centroids(ctx->stream, ctx->kw, ctx->d_codes, ctx->Dp, D, ctx->N,
                                       K == 2 ? nullptr : ctx->d_A_alt, Kc, ctx->d_kc_cent, ctx->d_kc_split));
@@ -954,7 +1068,6 @@ qvq_status resolve_kahan_ties(qvq_ctx *ctx, uint32_t K, int slot, unsigned nt, b
         build_tree(ctx, ctx->h_kc_split.data(), K, slot & 1, kd);
     }
     unsigned *cnt = ctx->d_counters + 2 * slot;
-    uint64_t *target = fused ? ctx->d_sums + sums_cap_stride(ctx) : ctx->d_sums;
     if (kd.depth > 0) {
         HIPCHK(launch_kd_resolve(ctx->stream, ctx->d_codes, ctx->Dp, D, ctx->d_ties, &cnt[1], S_ref, K, ctx->d_lut64,
                                  kd, ctx->d_A, nullptr, nullptr, ctx->d_plut, target));

@@ -7,6 +7,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <functional>
 #include <limits>
 #include <memory>
 
@@ -281,6 +282,297 @@ bool RefKDTree::unchanged_under(const double *pts2) const {
             }
         }
     return true;
+}
+
+void RefKDTree::near_set(const double *q, double slack_rel, double slack_abs, std::vector<uint32_t> &out,
+                         double &dmin) const {
+    static thread_local std::vector<std::pair<double, uint32_t>> seen;
+    static thread_local std::vector<int> stack;
+    seen.clear();
+    stack.assign(1, 0);
+    double best = std::numeric_limits<double>::infinity();
+    // a box's squared distance is rounded a few ulps at most: the bound keeps a relative margin
+    auto limit = [&] { return (best * (1 + slack_rel) + slack_abs) * (1 + 1e-12); };
+    auto box_dist = [&](int node) {
+        const Box *b = &node_box_[(size_t)node * dim_];
+        double s = 0;
+        for (int d = 0; d < dim_; d++) {
+            const double x = q[d], e = x < b[d].low ? b[d].low - x : (x > b[d].high ? x - b[d].high : 0.0);
+            s += e * e;
+        }
+        return s;
+    };
+    while (!stack.empty()) {
+        const int node = stack.back();
+        stack.pop_back();
+        if (box_dist(node) > limit()) continue;
+        const Node &n = nodes_[node];
+        if (n.leaf) {
+            for (size_t i = n.left; i < n.right; i++) {
+                const uint32_t p = (uint32_t)vind_[i];
+                const double d = ref_l2(q, pts_ + (size_t)p * dim_, dim_);
+                seen.emplace_back(d, p);
+                best = std::min(best, d);
+            }
+            continue;
+        }
+        const double d1 = box_dist(n.child1), d2 = box_dist(n.child2);
+        stack.push_back(d1 <= d2 ? n.child2 : n.child1);   // the closer child pops first
+        stack.push_back(d1 <= d2 ? n.child1 : n.child2);
+    }
+    dmin = best;
+    out.clear();
+    const double lim = best * (1 + slack_rel) + slack_abs;
+    for (const auto &s : seen)
+        if (s.first <= lim) out.push_back(s.second);
+}
+
+// One node of the build replayed over every codebook within delta of this one (interval
+// endpoints: each build quantity is a monotone function of the coordinates it reads, so the
+// endpoints' values bound it).  True when the candidate dimensions, the cut dimension, the cut's
+// clamp and every point's side of the cut are the same for all of them; then the children's
+// cell boxes and divlow / divhigh get their intervals.
+bool RefKDTree::cert_split(int node) const {
+    const Node &n = nodes_[node];
+    CertNode &cn = cert_[node];
+    cn.state = 2;
+    const int D = dim_;
+    const Iv *cb = &cert_box_[(size_t)node * D * 2];
+    const size_t *ind = vind_.data() + n.left;
+    const size_t count = n.right - n.left;
+    const double EPS = 0.00001;
+    double sp_lo[64], sp_hi[64], ms_lo = 0, ms_hi = 0;
+    for (int d = 0; d < D; d++) {
+        sp_lo[d] = cb[2 * d + 1].lo - cb[2 * d].hi;
+        sp_hi[d] = cb[2 * d + 1].hi - cb[2 * d].lo;
+        ms_lo = d ? std::max(ms_lo, sp_lo[d]) : sp_lo[d];
+        ms_hi = d ? std::max(ms_hi, sp_hi[d]) : sp_hi[d];
+    }
+    const double th_lo = (1 - EPS) * ms_lo, th_hi = (1 - EPS) * ms_hi;
+    uint64_t cand = 0;
+    for (int d = 0; d < D; d++) {
+        if (sp_lo[d] > th_hi) cand |= 1ull << d;
+        else if (!(sp_hi[d] <= th_lo)) return false;
+    }
+    if (cand != n.cand) return false;
+    auto col = [&](int d, size_t b, size_t e, Iv &mn, Iv &mx) {
+        const Iv v0 = piv(vind_[b], d);
+        mn = mx = v0;
+        for (size_t i = b + 1; i < e; i++) {
+            const Iv v = piv(vind_[i], d);
+            mn.lo = std::min(mn.lo, v.lo);
+            mn.hi = std::min(mn.hi, v.hi);
+            mx.lo = std::max(mx.lo, v.lo);
+            mx.hi = std::max(mx.hi, v.hi);
+        }
+    };
+    const int c = n.divfeat;
+    Iv mn, mx;
+    col(c, n.left, n.right, mn, mx);
+    if (cand) {   // the first candidate of greatest spread, strictly ahead of the others
+        if (!((cand >> c) & 1)) return false;
+        const double sc_lo = mx.lo - mn.hi;
+        for (int j = 0; j < D; j++) {
+            if (j == c || !((cand >> j) & 1)) continue;
+            Iv jm, jx;
+            col(j, n.left, n.right, jm, jx);
+            const double sj_hi = jx.hi - jm.lo;
+            if (j < c ? !(sj_hi < sc_lo) : !(sj_hi <= sc_lo)) return false;
+        }
+    } else if (c != 0) {
+        return false;
+    }
+    const Iv sv{(cb[2 * c].lo + cb[2 * c + 1].lo) / 2, (cb[2 * c].hi + cb[2 * c + 1].hi) / 2};
+    Iv cut;
+    if (n.cutval == n.split_val) {   // not clamped, for all; no point meets the cut unless both are exact
+        if (!(sv.lo >= mn.hi && sv.hi <= mx.lo)) return false;
+        cut = sv;
+        for (size_t i = 0; i < count; i++) {   // and on the exact split's side of it
+            const double e = ptr(ind[i], c);
+            const int side_e = e < n.cutval ? 0 : (e == n.cutval ? 1 : 2);
+            const Iv v = piv(ind[i], c);
+            int side;
+            if (v.hi < cut.lo) side = 0;
+            else if (v.lo > cut.hi) side = 2;
+            else if (v.lo == v.hi && cut.lo == cut.hi && v.lo == cut.lo) side = 1;
+            else return false;
+            if (side != side_e) return false;
+        }
+    } else {   // clamped to the points' minimum (maximum): the points at it stay the extreme ones
+        const bool low = n.cutval > n.split_val;
+        if (low ? !(sv.hi < mn.lo) : !(sv.lo > mx.hi)) return false;
+        cut = low ? mn : mx;
+        size_t nat = 0;
+        bool exact = true;   // every one of them known, all at one value
+        Iv at{0, 0};
+        for (size_t i = 0; i < count; i++)
+            if (ptr(ind[i], c) == n.cutval) {
+                const Iv v = piv(ind[i], c);
+                exact = exact && v.lo == v.hi && (nat == 0 || v.lo == at.lo);
+                at = v;
+                nat++;
+            }
+        if (!exact && nat != 1) return false;
+        const double lim = exact ? at.lo : (low ? at.hi : at.lo);
+        for (size_t i = 0; i < count; i++) {
+            if (ptr(ind[i], c) == n.cutval) continue;
+            const Iv v = piv(ind[i], c);
+            if (low ? !(v.lo > lim) : !(v.hi < lim)) return false;
+        }
+    }
+    Iv *lb = &cert_box_[(size_t)n.child1 * D * 2], *rb = &cert_box_[(size_t)n.child2 * D * 2];
+    std::copy(cb, cb + 2 * D, lb);
+    std::copy(cb, cb + 2 * D, rb);
+    lb[2 * c + 1] = cut;
+    rb[2 * c] = cut;
+    cert_box_set_[n.child1] = cert_box_set_[n.child2] = 1;
+    const Node &c1 = nodes_[n.child1], &c2 = nodes_[n.child2];
+    Iv t0, t1;
+    col(c, c1.left, c1.right, t0, cn.dl);
+    col(c, c2.left, c2.right, cn.dh, t1);
+    cn.state = 1;
+    return true;
+}
+
+void RefKDTree::cert_reset(double delta, const double *kpts, const uint8_t *known) const {
+    if (cert_delta_ == delta && cert_k_ == kpts && cert_known_ == known) return;
+    const int D = dim_;
+    cert_delta_ = delta;
+    cert_k_ = kpts;
+    cert_known_ = known;
+    cert_.assign(nodes_.size(), CertNode());
+    cert_box_.assign(nodes_.size() * D * 2, Iv{0, 0});
+    cert_box_set_.assign(nodes_.size(), 0);
+    for (int d = 0; d < D; d++) {   // the root's cell box: the points' box
+        Iv lo = piv(0, d), hi = lo;
+        for (size_t p = 1; p < K_; p++) {
+            const Iv v = piv(p, d);
+            lo.lo = std::min(lo.lo, v.lo);
+            lo.hi = std::min(lo.hi, v.hi);
+            hi.lo = std::max(hi.lo, v.lo);
+            hi.hi = std::max(hi.hi, v.hi);
+        }
+        cert_box_[2 * d] = lo;
+        cert_box_[2 * d + 1] = hi;
+    }
+    cert_box_set_[0] = 1;
+}
+
+namespace {
+// x * x over x in [e.lo, e.hi] (a product of a value with itself rounds monotonically in |x|)
+inline void sq_iv(double elo, double ehi, double &lo, double &hi) {
+    if (elo >= 0) lo = elo * elo, hi = ehi * ehi;
+    else if (ehi <= 0) lo = ehi * ehi, hi = elo * elo;
+    else lo = 0, hi = std::max(elo * elo, ehi * ehi);
+}
+}  // namespace
+
+// kd_nearest_flat (the reference's search) replayed over every codebook the certificate allows:
+// each quantity an interval, each decision taken only when all of them take it.
+int64_t RefKDTree::certified_search(const double *q, double delta, const double *kpts, const uint8_t *known) const {
+    if (dim_ > 64) return -1;
+    cert_reset(delta, kpts, known);
+    const int D = dim_;
+    constexpr double U = 1.1102230246251565e-16;   // unit roundoff
+    double dlo[64], dhi[64];
+    double mlo = 0, mhi = 0;
+    for (int d = 0; d < D; d++) {   // the initial distances against the root box
+        const double x = q[d];
+        const Iv lo = cert_box_[2 * d], hi = cert_box_[2 * d + 1];
+        dlo[d] = dhi[d] = 0;
+        if (!(x < lo.lo) && x < lo.hi) return -1;
+        if (x < lo.lo) {
+            sq_iv(x - lo.hi, x - lo.lo, dlo[d], dhi[d]);
+            mlo += dlo[d];
+            mhi += dhi[d];
+        }
+        if (!(x > hi.hi) && x > hi.lo) return -1;
+        if (x > hi.hi) {
+            sq_iv(x - hi.hi, x - hi.lo, dlo[d], dhi[d]);
+            mlo += dlo[d];
+            mhi += dhi[d];
+        }
+    }
+    const double MAXD = 1.7976931348623157e308;
+    double blo = MAXD, bhi = MAXD;   // the best distance so far
+    int64_t idx = 0;
+    bool amb = false, ok = true;
+    // a point's distance: exact when all its coordinates are known, else around the exact-sum
+    // split's by the coordinates' slack (and both evaluations' rounding)
+    auto pdist = [&](uint32_t p, double &lo, double &hi) {
+        const size_t r = (size_t)p * D;
+        bool all = true;
+        for (int d = 0; d < D; d++) all = all && known[r + d];
+        if (all) {
+            lo = hi = ref_l2(q, kpts + r, D);
+            return;
+        }
+        const double de = ref_l2(q, pts_ + r, D);
+        double lin = 0;
+        for (int d = 0; d < D; d++)
+            if (!known[r + d]) lin += 2 * std::fabs(q[d] - pts_[r + d]) * delta + delta * delta;
+        const double pert = (lin + (D + 4) * U * (2 * de + lin)) * (1 + 1e-9) + 1e-300;
+        lo = de - pert;
+        hi = de + pert;
+    };
+    std::function<void(int, double, double)> search = [&](int node, double slo, double shi) {
+        if (!ok) return;
+        const Node &n = nodes_[node];
+        if (n.leaf) {
+            const double wlo = blo, whi = bhi;   // the leaf's worst, captured at entry
+            for (size_t i = n.left; i < n.right; i++) {
+                const uint32_t p = (uint32_t)vind_[i];
+                double lo, hi;
+                pdist(p, lo, hi);
+                // kept iff dist < worst and best > dist: with best <= worst, iff dist < best
+                const bool yes = hi < wlo && hi < blo, no = lo >= whi || lo >= bhi;
+                if (yes) {
+                    blo = lo, bhi = hi, idx = p, amb = false;
+                } else if (!no) {
+                    blo = std::min(blo, lo), bhi = std::min(bhi, hi), amb = true;
+                }
+            }
+            return;
+        }
+        if (cert_[node].state == 0 && cert_box_set_[node]) cert_split(node);
+        if (cert_[node].state != 1) {
+            ok = false;
+            return;
+        }
+        const int f = n.divfeat;
+        const double val = q[f];
+        const CertNode &cn = cert_[node];
+        const double s_hi = (val - cn.dl.lo) + (val - cn.dh.lo), s_lo = (val - cn.dl.hi) + (val - cn.dh.hi);
+        if (!(s_hi < 0) && !(s_lo >= 0)) {
+            ok = false;
+            return;
+        }
+        const bool left_first = s_hi < 0;
+        search(left_first ? n.child1 : n.child2, slo, shi);
+        if (!ok) return;
+        double clo, chi;
+        if (left_first) sq_iv(val - cn.dh.hi, val - cn.dh.lo, clo, chi);
+        else sq_iv(val - cn.dl.hi, val - cn.dl.lo, clo, chi);
+        const double tlo = dlo[f], thi = dhi[f];
+        const double m2lo = (slo - thi) + clo, m2hi = (shi - tlo) + chi;
+        dlo[f] = clo;
+        dhi[f] = chi;
+        if (m2hi <= blo) search(left_first ? n.child2 : n.child1, m2lo, m2hi);
+        else if (!(m2lo > bhi)) ok = false;
+        dlo[f] = tlo;
+        dhi[f] = thi;
+    };
+    search(0, mlo, mhi);
+    return ok && !amb && blo < MAXD ? idx : -1;
+}
+
+int64_t certify_tie(const RefKDTree &t, const double *q, const std::vector<uint32_t> &cand, const double *kpts,
+                    const uint8_t *known, int dim, double delta) {
+    if (cand.empty()) return -1;
+    for (uint32_t j : cand)
+        for (int d = 0; d < dim; d++)
+            if (!known[(size_t)j * dim + d]) return -1;
+    return t.certified_search(q, delta, kpts, known);
 }
 
 void RefKDTree::flatten(KdNodeDev *nodes, uint32_t *vind, double *lo, double *hi) const {

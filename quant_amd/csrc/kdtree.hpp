@@ -38,6 +38,22 @@ public:
     // root box, the cut choices, cut values, partitions and children's boxes it can reach stay).
     bool unchanged_under(const double *pts2) const;
 
+    // ---- the reference's answer without the reference's whole split ----------
+    // This tree is built over the exact-sum split; the reference's (Kahan-bit) split differs
+    // from it by at most delta per coordinate.
+    // Every point whose ref_l2 distance to q is at most dmin (1 + slack_rel) + slack_abs, dmin
+    // the least distance; the points' own box per node prunes the walk.
+    void near_set(const double *q, double slack_rel, double slack_abs, std::vector<uint32_t> &out,
+                  double &dmin) const;
+    // The index the reference's search over its own (Kahan-bit) split returns for q, from this
+    // tree: the search replayed over every split within delta of this one that equals kpts on
+    // the coordinates known marks (K x dim bytes), each build and search quantity an interval
+    // (each is a monotone function of what it reads), each decision taken only when all of them
+    // take it; the build's decisions per node are cached for one (delta, kpts, known).  -1 when
+    // a decision is not the same for all: the caller then computes the reference's split and
+    // its tree.
+    int64_t certified_search(const double *q, double delta, const double *kpts, const uint8_t *known) const;
+
 private:
     struct Node {
         bool leaf;
@@ -71,6 +87,31 @@ private:
     std::vector<KdNodeDev> flat_nodes_;
     std::vector<uint32_t> flat_vind_;
     std::vector<double> flat_box_;
+
+    // certified_search's replay: the values each build quantity takes over all splits allowed
+    struct Iv { double lo, hi; };
+    struct CertNode {
+        int8_t state = 0;   // 0 not replayed, 1 the same split for every such codebook, 2 not shown
+        Iv dl{0, 0}, dh{0, 0};   // divlow, divhigh
+    };
+    Iv piv(size_t p, int d) const {
+        const size_t i = p * (size_t)dim_ + d;
+        if (cert_known_[i]) return {cert_k_[i], cert_k_[i]};
+        return {pts_[i] - cert_delta_, pts_[i] + cert_delta_};
+    }
+    bool cert_split(int node) const;
+    void cert_reset(double delta, const double *kpts, const uint8_t *known) const;
+    mutable double cert_delta_ = -1;
+    mutable const double *cert_k_ = nullptr;
+    mutable const uint8_t *cert_known_ = nullptr;
+    mutable std::vector<CertNode> cert_;
+    mutable std::vector<Iv> cert_box_;   // [node][dim][lo, hi]: the node's cell box, once its parent replayed
+    mutable std::vector<uint8_t> cert_box_set_;
 };
+
+// The reference's index for tie row q: certified_search, once the candidates cand (near_set
+// over the exact-sum split, slack covering the reference's bits) are all known; else -1.
+int64_t certify_tie(const RefKDTree &t, const double *q, const std::vector<uint32_t> &cand, const double *kpts,
+                    const uint8_t *known, int dim, double delta);
 
 }  // namespace qvq

@@ -74,3 +74,30 @@ def test_kdtree_reuse_is_sound(tmp_path, s512):
     exe = _build(tmp_path, "test_kdtree_reuse", [os.path.join(CSRC, "kdtree.cpp")])
     r = subprocess.run([exe, str(path)], capture_output=True, text=True, timeout=600)
     assert r.returncode == 0 and "wrong claims 0" in r.stdout, r.stdout + r.stderr
+
+
+def test_tie_certificate_is_sound(tmp_path):
+    """quant_amd/csrc/kdtree.cpp certified_search: answering tie rows from the
+    exact-sum split's tree, with the reference's bits computed only for the candidates' cells,
+    never gives an index other than the reference's (the synthetic image's levels with extra
+    ordinary rows, and the four noise seeds of the Kahan corpus)."""
+    import sys
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    import json
+    from tie_cert_data import write_levels
+    rng = np.random.default_rng(5)
+    path = tmp_path / "levels.bin"
+    with open(path, "wb") as f:
+        X, _ = oracle.tile(oracle.gen_image(512), 512, 512, 2, 2)
+        write_levels(f, X, 9, 100, rng)
+        corpus = json.load(open(os.path.join(ROOT, "tests", "golden", "kahan_divergent.json")))
+        for case in corpus["noise_seeds"]:
+            rgb = np.random.default_rng(case["seed"]).integers(0, 256, 96 * 96 * 3, dtype=np.uint8)
+            X, _ = oracle.tile(rgb, 96, 96, 2, 2)
+            write_levels(f, X, case["bits"], 20, rng)
+    exe = _build(tmp_path, "test_tie_cert", [os.path.join(CSRC, "kdtree.cpp")])
+    r = subprocess.run([exe, str(path)], capture_output=True, text=True, timeout=600)
+    last = r.stdout.strip().splitlines()[-1]
+    assert r.returncode == 0 and " wrong 0 " in last and "delta 0" in last, r.stdout[-3000:] + r.stderr
+    certified = int(last.split("certified ")[1].split()[0])
+    assert certified > 0, last
