@@ -977,17 +977,24 @@ qvq_status certify_kahan_ties(qvq_ctx *ctx, uint32_t K, unsigned nt, uint64_t *t
     const uint32_t nu = (uint32_t)uniq.size();
     std::vector<std::vector<uint32_t>> cand(nu);
     std::vector<uint8_t> sel(Kc, 0);
+    std::vector<uint32_t> blame;
     uint32_t cells = 0;
+    auto want = [&](uint32_t j) {
+        for (uint32_t d = 0; d < D; d++)
+            if (!known[(size_t)j * D + d]) {
+                cells += !sel[j % Kc];
+                sel[j % Kc] = 1;
+                return;
+            }
+    };
     for (uint32_t u = 0; u < nu; u++) {
         double dmin;
         tree.near_set(&qs[(size_t)u * D], 1e-9, 1e-9, cand[u], dmin);
-        for (uint32_t j : cand[u])
-            for (uint32_t d = 0; d < D; d++)
-                if (!known[(size_t)j * D + d]) {
-                    cells += !sel[j % Kc];
-                    sel[j % Kc] = 1;
-                    break;
-                }
+        for (uint32_t j : cand[u]) want(j);
+        // and the points whose bits settle the replay's open decisions
+        blame.clear();
+        tree.certify_blame(&qs[(size_t)u * D], KAHAN_DELTA, kp.data(), known.data(), blame);
+        for (uint32_t j : blame) want(j);
     }
     if (cells) {   // the reference's centroids of those cells (of the previous level's assignment)
         if ((st = ensure_kahan(ctx, Kc)) != QVQ_OK) return st;

@@ -327,15 +327,44 @@ void RefKDTree::near_set(const double *q, double slack_rel, double slack_abs, st
         if (s.first <= lim) out.push_back(s.second);
 }
 
+// Blame (the collecting run): the points holding node's least and greatest value in dimension
+// d, unless known already.
+void RefKDTree::blame_extremes(int node, int d) const {
+    const Node &n = nodes_[node];
+    double mn = ptr(vind_[n.left], d), mx = mn;
+    for (size_t i = n.left + 1; i < n.right; i++) {
+        const double v = ptr(vind_[i], d);
+        mn = std::min(mn, v);
+        mx = std::max(mx, v);
+    }
+    for (size_t i = n.left; i < n.right; i++) {
+        const size_t p = vind_[i];
+        const double v = ptr(p, d);
+        if ((v == mn || v == mx) && !cert_known_[p * (size_t)dim_ + d]) cert_blame_->push_back((uint32_t)p);
+    }
+}
+
+// ... and with_cell those of the node's cell box's origin in d too (the root's box and every
+// ancestor that cut along d).
+void RefKDTree::blame_dim(int node, int d, bool with_cell) const {
+    blame_extremes(node, d);
+    if (!with_cell) return;
+    for (int a = cert_parent_[node]; a >= 0; a = cert_parent_[a])
+        if (nodes_[a].divfeat == d) blame_extremes(a, d);
+    if (node != 0) blame_extremes(0, d);
+}
+
 // One node of the build replayed over every codebook within delta of this one (interval
 // endpoints: each build quantity is a monotone function of the coordinates it reads, so the
 // endpoints' values bound it).  True when the candidate dimensions, the cut dimension, the cut's
 // clamp and every point's side of the cut are the same for all of them; then the children's
-// cell boxes and divlow / divhigh get their intervals.
+// cell boxes and divlow / divhigh get their intervals.  Collecting, an open decision blames the
+// points it reads and the replay goes on with the exact split's decision.
 bool RefKDTree::cert_split(int node) const {
     const Node &n = nodes_[node];
     CertNode &cn = cert_[node];
     cn.state = 2;
+    const bool collect = cert_blame_ != nullptr;
     const int D = dim_;
     const Iv *cb = &cert_box_[(size_t)node * D * 2];
     const size_t *ind = vind_.data() + n.left;
@@ -351,10 +380,17 @@ bool RefKDTree::cert_split(int node) const {
     const double th_lo = (1 - EPS) * ms_lo, th_hi = (1 - EPS) * ms_hi;
     uint64_t cand = 0;
     for (int d = 0; d < D; d++) {
-        if (sp_lo[d] > th_hi) cand |= 1ull << d;
-        else if (!(sp_hi[d] <= th_lo)) return false;
+        if (sp_lo[d] > th_hi) {
+            cand |= 1ull << d;
+        } else if (!(sp_hi[d] <= th_lo)) {   // open: the dimension's span and the widest's
+            if (!collect) return false;
+            blame_dim(node, d, true);
+            for (int e = 0; e < D; e++)
+                if (sp_hi[e] >= ms_lo) blame_dim(node, e, true);
+        }
     }
-    if (cand != n.cand) return false;
+    if (!collect && cand != n.cand) return false;
+    cand = n.cand;
     auto col = [&](int d, size_t b, size_t e, Iv &mn, Iv &mx) {
         const Iv v0 = piv(vind_[b], d);
         mn = mx = v0;
@@ -370,14 +406,17 @@ bool RefKDTree::cert_split(int node) const {
     Iv mn, mx;
     col(c, n.left, n.right, mn, mx);
     if (cand) {   // the first candidate of greatest spread, strictly ahead of the others
-        if (!((cand >> c) & 1)) return false;
         const double sc_lo = mx.lo - mn.hi;
         for (int j = 0; j < D; j++) {
             if (j == c || !((cand >> j) & 1)) continue;
             Iv jm, jx;
             col(j, n.left, n.right, jm, jx);
             const double sj_hi = jx.hi - jm.lo;
-            if (j < c ? !(sj_hi < sc_lo) : !(sj_hi <= sc_lo)) return false;
+            if (j < c ? !(sj_hi < sc_lo) : !(sj_hi <= sc_lo)) {
+                if (!collect) return false;
+                blame_dim(node, j, false);
+                blame_dim(node, c, false);
+            }
         }
     } else if (c != 0) {
         return false;
@@ -385,8 +424,12 @@ bool RefKDTree::cert_split(int node) const {
     const Iv sv{(cb[2 * c].lo + cb[2 * c + 1].lo) / 2, (cb[2 * c].hi + cb[2 * c + 1].hi) / 2};
     Iv cut;
     if (n.cutval == n.split_val) {   // not clamped, for all; no point meets the cut unless both are exact
-        if (!(sv.lo >= mn.hi && sv.hi <= mx.lo)) return false;
+        if (!(sv.lo >= mn.hi && sv.hi <= mx.lo)) {
+            if (!collect) return false;
+            blame_dim(node, c, true);
+        }
         cut = sv;
+        bool blamed = false;
         for (size_t i = 0; i < count; i++) {   // and on the exact split's side of it
             const double e = ptr(ind[i], c);
             const int side_e = e < n.cutval ? 0 : (e == n.cutval ? 1 : 2);
@@ -395,12 +438,20 @@ bool RefKDTree::cert_split(int node) const {
             if (v.hi < cut.lo) side = 0;
             else if (v.lo > cut.hi) side = 2;
             else if (v.lo == v.hi && cut.lo == cut.hi && v.lo == cut.lo) side = 1;
-            else return false;
-            if (side != side_e) return false;
+            else side = -1;
+            if (side != side_e) {
+                if (!collect) return false;
+                if (!cert_known_[ind[i] * (size_t)D + c]) cert_blame_->push_back((uint32_t)ind[i]);
+                if (!blamed) blame_dim(node, c, true);
+                blamed = true;
+            }
         }
     } else {   // clamped to the points' minimum (maximum): the points at it stay the extreme ones
         const bool low = n.cutval > n.split_val;
-        if (low ? !(sv.hi < mn.lo) : !(sv.lo > mx.hi)) return false;
+        if (low ? !(sv.hi < mn.lo) : !(sv.lo > mx.hi)) {
+            if (!collect) return false;
+            blame_dim(node, c, true);
+        }
         cut = low ? mn : mx;
         size_t nat = 0;
         bool exact = true;   // every one of them known, all at one value
@@ -412,12 +463,21 @@ bool RefKDTree::cert_split(int node) const {
                 at = v;
                 nat++;
             }
-        if (!exact && nat != 1) return false;
+        bool open = !exact && nat != 1;
         const double lim = exact ? at.lo : (low ? at.hi : at.lo);
-        for (size_t i = 0; i < count; i++) {
+        for (size_t i = 0; i < count && !open; i++) {
             if (ptr(ind[i], c) == n.cutval) continue;
             const Iv v = piv(ind[i], c);
-            if (low ? !(v.lo > lim) : !(v.hi < lim)) return false;
+            open = low ? !(v.lo > lim) : !(v.hi < lim);
+        }
+        if (open) {
+            if (!collect) return false;
+            blame_dim(node, c, false);
+            for (size_t i = 0; i < count; i++) {   // and every point that may reach the extreme
+                const Iv v = piv(ind[i], c);
+                if ((low ? v.lo <= cut.hi : v.hi >= cut.lo) && !cert_known_[ind[i] * (size_t)D + c])
+                    cert_blame_->push_back((uint32_t)ind[i]);
+            }
         }
     }
     Iv *lb = &cert_box_[(size_t)n.child1 * D * 2], *rb = &cert_box_[(size_t)n.child2 * D * 2];
@@ -443,6 +503,11 @@ void RefKDTree::cert_reset(double delta, const double *kpts, const uint8_t *know
     cert_.assign(nodes_.size(), CertNode());
     cert_box_.assign(nodes_.size() * D * 2, Iv{0, 0});
     cert_box_set_.assign(nodes_.size(), 0);
+    if (cert_parent_.size() != nodes_.size()) {
+        cert_parent_.assign(nodes_.size(), -1);
+        for (size_t i = 0; i < nodes_.size(); i++)
+            if (!nodes_[i].leaf) cert_parent_[nodes_[i].child1] = cert_parent_[nodes_[i].child2] = (int)i;
+    }
     for (int d = 0; d < D; d++) {   // the root's cell box: the points' box
         Iv lo = piv(0, d), hi = lo;
         for (size_t p = 1; p < K_; p++) {
@@ -467,10 +532,22 @@ inline void sq_iv(double elo, double ehi, double &lo, double &hi) {
 }
 }  // namespace
 
+void RefKDTree::certify_blame(const double *q, double delta, const double *kpts, const uint8_t *known,
+                              std::vector<uint32_t> &blame) const {
+    cert_delta_ = -1;   // a fresh replay, kept apart from the strict one's cache
+    cert_blame_ = &blame;
+    certified_search(q, delta, kpts, known);
+    cert_blame_ = nullptr;
+    cert_delta_ = -1;
+}
+
 // kd_nearest_flat (the reference's search) replayed over every codebook the certificate allows:
-// each quantity an interval, each decision taken only when all of them take it.
+// each quantity an interval, each decision taken only when all of them take it (collecting:
+// an open decision blames the points it reads and the exact split's decision is taken).
 int64_t RefKDTree::certified_search(const double *q, double delta, const double *kpts, const uint8_t *known) const {
     if (dim_ > 64) return -1;
+    const bool collect = cert_blame_ != nullptr;
+    if (collect && cert_delta_ != -1) cert_delta_ = -1;
     cert_reset(delta, kpts, known);
     const int D = dim_;
     constexpr double U = 1.1102230246251565e-16;   // unit roundoff
@@ -480,13 +557,15 @@ int64_t RefKDTree::certified_search(const double *q, double delta, const double 
         const double x = q[d];
         const Iv lo = cert_box_[2 * d], hi = cert_box_[2 * d + 1];
         dlo[d] = dhi[d] = 0;
-        if (!(x < lo.lo) && x < lo.hi) return -1;
+        if ((!(x < lo.lo) && x < lo.hi) || (!(x > hi.hi) && x > hi.lo)) {
+            if (!collect) return -1;
+            blame_extremes(0, d);
+        }
         if (x < lo.lo) {
             sq_iv(x - lo.hi, x - lo.lo, dlo[d], dhi[d]);
             mlo += dlo[d];
             mhi += dhi[d];
         }
-        if (!(x > hi.hi) && x > hi.lo) return -1;
         if (x > hi.hi) {
             sq_iv(x - hi.hi, x - hi.lo, dlo[d], dhi[d]);
             mlo += dlo[d];
@@ -497,6 +576,7 @@ int64_t RefKDTree::certified_search(const double *q, double delta, const double 
     double blo = MAXD, bhi = MAXD;   // the best distance so far
     int64_t idx = 0;
     bool amb = false, ok = true;
+    std::vector<int> path;
     // a point's distance: exact when all its coordinates are known, else around the exact-sum
     // split's by the coordinates' slack (and both evaluations' rounding)
     auto pdist = [&](uint32_t p, double &lo, double &hi) {
@@ -515,6 +595,13 @@ int64_t RefKDTree::certified_search(const double *q, double delta, const double 
         lo = de - pert;
         hi = de + pert;
     };
+    auto blame_pt = [&](uint32_t p) {
+        for (int d = 0; d < D; d++)
+            if (!known[(size_t)p * D + d]) {
+                cert_blame_->push_back(p);
+                return;
+            }
+    };
     std::function<void(int, double, double)> search = [&](int node, double slo, double shi) {
         if (!ok) return;
         const Node &n = nodes_[node];
@@ -529,6 +616,10 @@ int64_t RefKDTree::certified_search(const double *q, double delta, const double 
                 if (yes) {
                     blo = lo, bhi = hi, idx = p, amb = false;
                 } else if (!no) {
+                    if (collect) {
+                        blame_pt(p);
+                        blame_pt((uint32_t)idx);
+                    }
                     blo = std::min(blo, lo), bhi = std::min(bhi, hi), amb = true;
                 }
             }
@@ -543,12 +634,19 @@ int64_t RefKDTree::certified_search(const double *q, double delta, const double 
         const double val = q[f];
         const CertNode &cn = cert_[node];
         const double s_hi = (val - cn.dl.lo) + (val - cn.dh.lo), s_lo = (val - cn.dl.hi) + (val - cn.dh.hi);
+        bool left_first = s_hi < 0;
         if (!(s_hi < 0) && !(s_lo >= 0)) {
-            ok = false;
-            return;
+            if (!collect) {
+                ok = false;
+                return;
+            }
+            blame_extremes(n.child1, f);
+            blame_extremes(n.child2, f);
+            left_first = (val - n.divlow) + (val - n.divhigh) < 0;
         }
-        const bool left_first = s_hi < 0;
+        path.push_back(node);
         search(left_first ? n.child1 : n.child2, slo, shi);
+        path.pop_back();
         if (!ok) return;
         double clo, chi;
         if (left_first) sq_iv(val - cn.dh.hi, val - cn.dh.lo, clo, chi);
@@ -557,8 +655,26 @@ int64_t RefKDTree::certified_search(const double *q, double delta, const double 
         const double m2lo = (slo - thi) + clo, m2hi = (shi - tlo) + chi;
         dlo[f] = clo;
         dhi[f] = chi;
-        if (m2hi <= blo) search(left_first ? n.child2 : n.child1, m2lo, m2hi);
-        else if (!(m2lo > bhi)) ok = false;
+        bool visit = m2hi <= blo;
+        if (!visit && !(m2lo > bhi)) {
+            if (!collect) {
+                ok = false;
+                return;
+            }
+            blame_pt((uint32_t)idx);
+            for (int a : path) {
+                blame_extremes(nodes_[a].child1, nodes_[a].divfeat);
+                blame_extremes(nodes_[a].child2, nodes_[a].divfeat);
+            }
+            blame_extremes(n.child1, f);
+            blame_extremes(n.child2, f);
+            visit = true;
+        }
+        if (visit) {
+            path.push_back(node);
+            search(left_first ? n.child2 : n.child1, m2lo, m2hi);
+            path.pop_back();
+        }
         dlo[f] = tlo;
         dhi[f] = thi;
     };

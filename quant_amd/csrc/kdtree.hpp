@@ -53,6 +53,11 @@ public:
     // a decision is not the same for all: the caller then computes the reference's split and
     // its tree.
     int64_t certified_search(const double *q, double delta, const double *kpts, const uint8_t *known) const;
+    // The same replay collecting instead of deciding: every point whose reference bits would
+    // settle a decision the intervals leave open is appended to blame (then the exact split's
+    // decision is taken), so that one round of Kahan sums can make the strict replay succeed.
+    void certify_blame(const double *q, double delta, const double *kpts, const uint8_t *known,
+                       std::vector<uint32_t> &blame) const;
 
 private:
     struct Node {
@@ -101,6 +106,10 @@ private:
     }
     bool cert_split(int node) const;
     void cert_reset(double delta, const double *kpts, const uint8_t *known) const;
+    void blame_extremes(int node, int d) const;
+    void blame_dim(int node, int d, bool with_cell) const;
+    mutable std::vector<uint32_t> *cert_blame_ = nullptr;   // collecting (certify_blame)
+    mutable std::vector<int> cert_parent_;
     mutable double cert_delta_ = -1;
     mutable const double *cert_k_ = nullptr;
     mutable const uint8_t *cert_known_ = nullptr;

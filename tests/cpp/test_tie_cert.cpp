@@ -46,9 +46,16 @@ int main(int argc, char **argv) {
         long cert = 0, wrong = 0, multi = 0, cells = 0;
         // the engine's order: every row's candidates first, then the parent cells of the
         // nonzero ones (both split rows of each) from the reference's sums, then the answers
+        std::vector<uint32_t> blame;
+        const bool use_blame = !getenv("TIE_CERT_NO_BLAME");
         for (uint32_t r = 0; r < n; r++) {
             double dmin;
             tree.near_set(q.data() + (size_t)r * D, 1e-9, 1e-9, cand, dmin);
+            if (use_blame) {   // and the points the replay's open decisions read
+                blame.clear();
+                tree.certify_blame(q.data() + (size_t)r * D, delta, kp.data(), known.data(), blame);
+                cand.insert(cand.end(), blame.begin(), blame.end());
+            }
             for (uint32_t j : cand) {
                 bool all = true;
                 for (uint32_t d = 0; d < D; d++) all = all && known[(size_t)j * D + d];
