@@ -67,6 +67,8 @@ def parse():
     ap.add_argument("--c5-images", type=int, default=64)
     ap.add_argument("--c5-steps", type=int, default=3, help="0 disables the c5 sub-object")
     ap.add_argument("--c4-steps", type=int, default=5, help="0 disables the c4 sub-object")
+    ap.add_argument("--share-steps", type=int, default=3,
+                    help="0 disables the c5_rank_share sub-object (N=8 per-rank share through a 1-rank RCCL communicator)")
     ap.add_argument("--e2e-reps", type=int, default=7, help="0 disables the end_to_end sub-object (the first rep after a reconfiguration is not timed; the second still pays first-use costs, hence the median of 7)")
     ap.add_argument("--dry-run", action="store_true", help="CPU only: start the ranks, join gloo, print the plan")
     return ap.parse_args()
@@ -316,6 +318,9 @@ def main():
                      "launches": len(launches), "flop_per_block": "3*K*D",
                      "timing": "HIP events around one level's search per quantize, levels in rotation, in quantizes after the timed steps",
                      "per_level": per_level,
+                     # the single dominant launch: the largest K's search (the headline frac above
+                     # averages every level's launches)
+                     "dominant": dict(K=max(by_k), **per_level[str(max(by_k))]),
                      "hbm_view": {"algorithmic_bytes_per_launch": assign_bytes,
                                   "achieved_GBps": round(assign_bytes / avg_launch_s / 1e9, 1),
                                   "peak_GBps": PEAK_HBM_GBS}},
@@ -368,6 +373,33 @@ def main():
         result["c4"] = {"workload": "C4: %dx%d synthetic, 4x4 blocks (D=48), 4096 code vectors" % (args.size, args.size),
                         "value": round(eng.n * 12 * args.c4_steps / el / 1e6, 3), "unit": "Mblocks/s",
                         "ms_per_step": round(el * 1e3 / args.c4_steps, 3), "steps": args.c4_steps, "warmup": 1}
+    if world == 1 and args.share_steps > 0:
+        # one rank's share of C5 at N=8, under the communicator schedule (a 1-rank RCCL
+        # communicator: the all-reduce per level, kd ties and reduce as with N ranks) and under
+        # the one-rank schedule: the per-rank workload of the 8-GPU run, not a scaling curve
+        n_share = max(1, args.c5_images // 8)
+        share_res = {}
+        for label, with_comm in (("one_rank_schedule", False), ("rccl_schedule", True)):
+            e2 = quant_amd.Engine(local)
+            try:
+                if with_comm:
+                    e2.comm_init(1, 0, quant_amd.Engine.comm_unique_id())
+                e2.set_synthetic(args.size, 0x5EED, n_share, 2, 2, quant_amd.SCALED)
+                e2.set_timing(-2)
+                o2 = (np.empty((1 << args.bits, e2.dim), np.float64), np.zeros(1, np.float64))
+                el = timed(lambda: e2.lbg(args.bits, want_assign=False, out=o2), args.share_steps, 1)
+                kind = e2.comm_info()[2]
+                share_res[label] = {"ms_per_step": round(el * 1e3 / args.share_steps, 3),
+                                    "Mblocks_per_s": round(e2.n * args.bits * args.share_steps / el / 1e6, 3),
+                                    "communicator": "RCCL, 1 rank" if kind == quant_amd.COMM_RCCL else "none"}
+            finally:
+                e2.close()
+        r1, rc = share_res["one_rank_schedule"]["ms_per_step"], share_res["rccl_schedule"]["ms_per_step"]
+        result["c5_rank_share"] = {"workload": "the N=8 per-rank share of C5: %d x %dx%d synthetic images, 2x2 blocks, "
+                                               "%d code vectors on one GPU (per-rank workload, not a scaling curve)"
+                                               % (n_share, args.size, args.size, 1 << args.bits),
+                                   "steps": args.share_steps, "warmup": 1, **share_res,
+                                   "rccl_over_one_rank": round(rc / r1, 4)}
     if world == 1 and args.e2e_reps > 0:
         # the drop-in's compress region from a host raster: H2D + tiling + quantize + indices D2H
         rgb = synthetic_raster(args.size, 0x5EED)
