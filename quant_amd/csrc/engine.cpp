@@ -19,6 +19,10 @@
 #include <algorithm>
 #include <atomic>
 #include <chrono>
+#include <condition_variable>
+#include <functional>
+#include <mutex>
+#include <thread>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -153,6 +157,19 @@ struct qvq_ctx {
     std::vector<double> cb_local;   // host copy of the published codebook for the tree build
     std::unique_ptr<RefKDTree> tree;   // the last level's tree over cb_local
     KdView tree_kd;                    // and its device image (depth 0: none)
+    // deferred-tie levels build their tree on this worker, off the launch path (start_tree_job)
+    struct Worker {
+        std::thread th;
+        std::mutex m;
+        std::condition_variable cv;
+        std::function<void()> job;
+        bool stop = false;
+        std::atomic<bool> busy{false};
+    } worker;
+    std::atomic<bool> tree_cancel{false};
+    bool tree_job = false, job_ok = false;
+    int job_buf = 0;
+    KdView job_kd;
     uint64_t tree_cap = 0;
     uint32_t nslabs = 0;   // slabs holding the last run_level's sums
     uint32_t col_blocks = 0;   // blocks per image column (consecutive rows run down a column); 0: no image
@@ -617,48 +634,136 @@ qvq_status ensure_kahan(qvq_ctx *ctx, uint32_t Kc) {
     return QVQ_OK;
 }
 
+bool join_tree_job(qvq_ctx *ctx, bool cancel);
+
 // Build the reference kd-tree over the host copy hC of the K code vectors being searched
 // into tree image buffer buf (pinned host memory, DMA-copied to d_tree for kd_resolve_kernel).  An empty
 // view means host resolution (tree too deep/large for the kernel's LDS, or QVQ_KDTREE=host).
-void build_tree(qvq_ctx *ctx, const double *hC, uint32_t K, int buf, KdView &kd) {
-    kd = KdView{};
-    if (env_is("QVQ_KDTREE", "host")) return;
+// The host part: the tree (ctx->tree over ctx->cb_local) and its flattened image in h_tree[buf];
+// v.bytes = 0 when there is no device image (too large, or too deep for the kernel's LDS).
+// No HIP call: the tree worker runs it.
+void build_tree_host(qvq_ctx *ctx, const double *hC, uint32_t K, int buf, KdView &v,
+                     const std::atomic<bool> *cancel = nullptr) {
+    v = KdView{};
     // the build reads the codebook many times; mapped memory the GPU just wrote is read
     // once, sequentially, into ordinary memory first
-    ctx->tree_kd = KdView{};
     ctx->cb_local.assign(hC, hC + (size_t)K * ctx->D);
-    ctx->tree.reset(new RefKDTree(ctx->cb_local.data(), K, (int)ctx->D));
+    ctx->tree.reset(new RefKDTree(ctx->cb_local.data(), K, (int)ctx->D, cancel));
     const RefKDTree &tree = *ctx->tree;
+    if (tree.cancelled()) return;
     const uint32_t D = ctx->D;
     const size_t nn = tree.num_nodes();
-    KdView v;
-    v.depth = tree.depth();
-    v.n_nodes = (uint32_t)nn;
+    KdView t;
+    t.depth = tree.depth();
+    t.n_nodes = (uint32_t)nn;
     const uint64_t bytes = 16ull * D + nn * sizeof(KdNodeDev) + 4ull * K;
     if (bytes > ctx->tree_cap) return;
-    v.bytes = (uint32_t)bytes;
-    if (!kd_resolve_fits(v, K)) return;
+    t.bytes = (uint32_t)bytes;
+    if (!kd_resolve_fits(t, K)) return;
     double *lo = reinterpret_cast<double *>(ctx->h_tree[buf]), *hi = lo + D;
     KdNodeDev *nodes = reinterpret_cast<KdNodeDev *>(hi + D);
     uint32_t *vind = reinterpret_cast<uint32_t *>(nodes + nn);
     tree.flatten(nodes, vind, lo, hi);
-    // Every kd_resolve workgroup stages the image.  Big images (C4: 150+ KB) go to device
-    // memory with one DMA first (mapped reads from 16 workgroups cost up to ~70 us); small
-    // ones are read in place (the DMA itself costs ~5 us of stream time per level).
+    v = t;
+}
+
+// The device view of image buf (v from build_tree_host).  Every kd_resolve workgroup stages the
+// image.  Big images (C4: 150+ KB) go to device memory with one DMA first (mapped reads from 16
+// workgroups cost up to ~70 us); small ones are read in place (the DMA itself costs ~5 us of
+// stream time per level).
+void tree_view(qvq_ctx *ctx, int buf, KdView &v) {
+    if (!v.bytes) {
+        v = KdView{};
+        return;
+    }
+    const uint32_t D = ctx->D;
     const double *dlo = reinterpret_cast<const double *>(ctx->dh_tree[buf]);
     static const uint64_t dma_min = std::getenv("QVQ_TREE_DMA_MIN") ? std::atoll(std::getenv("QVQ_TREE_DMA_MIN"))
                                                                       : 32768;   // ablation
-    if (bytes > dma_min) {
-        if (hipMemcpyAsync(ctx->d_tree, ctx->h_tree[buf], bytes, hipMemcpyHostToDevice, ctx->stream) != hipSuccess)
+    if (v.bytes > dma_min) {
+        if (hipMemcpyAsync(ctx->d_tree, ctx->h_tree[buf], v.bytes, hipMemcpyHostToDevice, ctx->stream) != hipSuccess) {
+            v = KdView{};
             return;
+        }
         dlo = reinterpret_cast<const double *>(ctx->d_tree);
     }
     v.lo = dlo;
     v.hi = dlo + D;
     v.nodes = reinterpret_cast<const KdNodeDev *>(dlo + 2 * D);
-    v.vind = reinterpret_cast<const uint32_t *>(v.nodes + nn);
-    kd = v;
+    v.vind = reinterpret_cast<const uint32_t *>(v.nodes + v.n_nodes);
+}
+
+void build_tree(qvq_ctx *ctx, const double *hC, uint32_t K, int buf, KdView &kd) {
+    kd = KdView{};
+    ctx->tree_kd = KdView{};
+    if (env_is("QVQ_KDTREE", "host")) return;
+    build_tree_host(ctx, hC, K, buf, kd);
+    tree_view(ctx, buf, kd);
+    ctx->tree_kd = kd;
+}
+
+// A deferred-tie level (qvq_lbg's Kahan path) needs its tree only when it has ties, which the
+// host learns after the search: the worker awaits the codebook's publication and builds the
+// tree while this thread enqueues the rest of the level; join_tree_job waits for it (ties)
+// or cancels it (none).
+void start_tree_job(qvq_ctx *ctx, const double *hC, uint32_t K, int buf, uint64_t wait_seq) {
+    join_tree_job(ctx, true);
+    if (env_is("QVQ_KDTREE", "host")) return;
+    qvq_ctx::Worker &w = ctx->worker;
+    if (!w.th.joinable())
+        w.th = std::thread([&w] {
+            std::unique_lock<std::mutex> lk(w.m);
+            for (;;) {
+                w.cv.wait(lk, [&w] { return w.stop || w.job; });
+                if (w.stop) return;
+                std::function<void()> job = std::move(w.job);
+                w.job = nullptr;
+                lk.unlock();
+                job();
+                w.busy.store(false, std::memory_order_release);
+                lk.lock();
+            }
+        });
+    ctx->tree_cancel.store(false);
+    ctx->tree_job = true;
+    ctx->job_ok = false;
+    ctx->job_buf = buf;
+    ctx->tree_kd = KdView{};
+    const int slot = (int)__builtin_ctz(K) - 1;
+    w.busy.store(true, std::memory_order_relaxed);
+    {
+        std::lock_guard<std::mutex> g(w.m);
+        w.job = [ctx, hC, K, buf, wait_seq, slot] {
+            const auto t0 = std::chrono::steady_clock::now();
+            volatile uint64_t *flag = ctx->h_ready;
+            while (wait_seq && *flag < wait_seq)   // the codebook's publication (bounded by cancel)
+                if (ctx->tree_cancel.load(std::memory_order_relaxed)) return;
+            std::atomic_thread_fence(std::memory_order_acquire);
+            const auto t1 = std::chrono::steady_clock::now();
+            build_tree_host(ctx, hC, K, buf, ctx->job_kd, &ctx->tree_cancel);
+            ctx->job_ok = !ctx->tree->cancelled();
+            ctx->tm.wait_ms[slot] = std::chrono::duration<double, std::milli>(t1 - t0).count();
+            ctx->tm.tree_ms[slot] =
+                std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t1).count();
+        };
+    }
+    w.cv.notify_one();
+}
+
+bool join_tree_job(qvq_ctx *ctx, bool cancel) {
+    if (!ctx->tree_job) return false;
+    if (cancel) ctx->tree_cancel.store(true);
+    while (ctx->worker.busy.load(std::memory_order_acquire)) std::this_thread::yield();
+    ctx->tree_job = false;
+    if (!ctx->job_ok) {
+        ctx->tree.reset();
+        ctx->tree_kd = KdView{};
+        return false;
+    }
+    KdView v = ctx->job_kd;
+    tree_view(ctx, ctx->job_buf, v);
     ctx->tree_kd = v;
+    return true;
 }
 
 // Copy between a caller's host buffer and device memory at DMA speed: the host range is pinned
@@ -888,6 +993,11 @@ qvq_status run_level(qvq_ctx *ctx, uint32_t K, int slot, bool sums_out, const do
         ctx->nslabs = 0;   // reduced already
         HIPCHK(hipEventRecord(ctx->ev[slot][3], ctx->stream));
     }
+    if (defer_ties) {   // qvq_lbg answers the ties after the finalize, if there are any (tree on the worker)
+        start_tree_job(ctx, hC, K, slot & 1, wait_seq);
+        ctx->upd[slot] = false;
+        return QVQ_OK;
+    }
     // the tree build overlaps the search just enqueued
     const auto tw0 = std::chrono::steady_clock::now();
     if (wait_seq && (st = wait_codebook(ctx, wait_seq)) != QVQ_OK) return st;
@@ -896,10 +1006,6 @@ qvq_status run_level(qvq_ctx *ctx, uint32_t K, int slot, bool sums_out, const do
     build_tree(ctx, hC, K, slot & 1, kd);
     ctx->tm.wait_ms[slot] = std::chrono::duration<double, std::milli>(tw1 - tw0).count();
     ctx->tm.tree_ms[slot] = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tw1).count();
-    if (defer_ties) {   // qvq_lbg answers the ties after the finalize, if there are any (the tree kept)
-        ctx->upd[slot] = false;
-        return QVQ_OK;
-    }
     if (abl_skip() & 2) {
     } else if (kd.depth > 0 && fused && kd_merge(ctx) && kd_reduce_fits(kd, K)) {
         ctx->kd_pend = true;   // with the reduce (qvq_lbg)
@@ -1175,6 +1281,15 @@ QVQ_API qvq_status qvq_create(int hip_device, qvq_ctx **out) {
 
 QVQ_API void qvq_destroy(qvq_ctx *ctx) {
     if (!ctx) return;
+    join_tree_job(ctx, true);
+    if (ctx->worker.th.joinable()) {
+        {
+            std::lock_guard<std::mutex> g(ctx->worker.m);
+            ctx->worker.stop = true;
+        }
+        ctx->worker.cv.notify_one();
+        ctx->worker.th.join();
+    }
     (void)hipSetDevice(ctx->dev);
     if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
     if (ctx->comm) ncclCommDestroy(ctx->comm);
@@ -1529,6 +1644,10 @@ QVQ_API qvq_status qvq_lbg(qvq_ctx *ctx, uint32_t bits, double eps, double *code
 
     const bool kahan = kahan_mode(ctx);
     if (kahan && !ctx->d_A_alt) HIPCHK(hipMalloc(&ctx->d_A_alt, ctx->N * 4));
+    struct JobGuard {   // no tree build outlives the call (an error return included)
+        qvq_ctx *c;
+        ~JobGuard() { join_tree_job(c, true); }
+    } job_guard{ctx};
     if (kahan) split_out = ctx->d_C64_split_alt;
     for (uint32_t lvl = 1; lvl <= bits; lvl++) {
         const uint32_t K = 1u << lvl;
@@ -1562,11 +1681,11 @@ QVQ_API qvq_status qvq_lbg(qvq_ctx *ctx, uint32_t bits, double eps, double *code
             if (kahan) {   // the level's ties (published after its recheck)
                 if ((st = wait_flag(ctx, ctx->h_ready + 1, ctx->pub_seq)) != QVQ_OK) return st;
                 const unsigned nt = (unsigned)(uint32_t)ctx->h_ready[2];
+                join_tree_job(ctx, nt == 0);   // the level's tree: needed for ties only
                 if (nt) {
                     const bool fused = use_fused(ctx, K);
                     if (fused) ctx->sums1_dirty = true;
                     if ((st = resolve_kahan_ties(ctx, K, slot, nt, fused)) != QVQ_OK) return st;
-                    if (split) ctx->seq--;   // the same codebook number again
                     HIPCHK(finalize(K, split, fused ? 2 : 1, fused ? tcnt : nullptr));
                     ctx->sums1_dirty = false;
                 }

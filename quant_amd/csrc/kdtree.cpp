@@ -51,7 +51,8 @@ __attribute__((target_clones("avx2", "default"))) void rows_min_max(const double
 }
 }  // namespace
 
-RefKDTree::RefKDTree(const double *pts, size_t K, int dim) : pts_(pts), dim_(dim), K_(K) {
+RefKDTree::RefKDTree(const double *pts, size_t K, int dim, const std::atomic<bool> *cancel)
+    : pts_(pts), dim_(dim), K_(K), cancel_(cancel) {
     static thread_local std::vector<double> cols;   // reused: a fresh 1.5 MB buffer per level page-faults
     if (cols.size() < K * (size_t)dim) cols.resize(K * (size_t)dim);
     double *const cbuf = cols.data();
@@ -191,7 +192,8 @@ int RefKDTree::divide(size_t left, size_t right, Box *bbox, int level, std::vect
     depth = std::max(depth, level);
     nodes.push_back(Node());
     node_box_.resize(node_box_.size() + dim_);
-    if (right - left <= 10) {   // leaf_max_size (KDTreeVectorOfVectorsAdaptor.hpp:59)
+    if (cancel_ && !cancelled_ && cancel_->load(std::memory_order_relaxed)) cancelled_ = true;
+    if (right - left <= 10 || cancelled_) {   // leaf_max_size (KDTreeVectorOfVectorsAdaptor.hpp:59)
         Node &n = nodes[me];
         n.leaf = true;
         n.left = left;

@@ -8,6 +8,7 @@
 // the C-ABI engine builds it per level while the GPU searches, and either uploads it for
 // the device traversal (k_assign.hip, kd_nearest_dev) or answers handed-back rows here.
 #pragma once
+#include <atomic>
 #include <cstddef>
 #include <cstdint>
 #include <vector>
@@ -23,8 +24,10 @@ struct Box { double low, high; };
 
 class RefKDTree {
 public:
-    // pts: K x dim, row-major, borrowed for the lifetime of the tree.
-    RefKDTree(const double *pts, size_t K, int dim);
+    // pts: K x dim, row-major, borrowed for the lifetime of the tree.  cancel (optional): the
+    // build stops early once it reads true, leaving a tree to be discarded (cancelled()).
+    RefKDTree(const double *pts, size_t K, int dim, const std::atomic<bool> *cancel = nullptr);
+    bool cancelled() const { return cancelled_; }
     // Index the reference's kd-tree search returns for query q (dim values).
     uint32_t nearest(const double *q) const;
     // Flattened copy for the device search (kdtree_dev.hpp); depth = longest root-to-leaf
@@ -83,6 +86,8 @@ private:
     const double *pts_;
     int dim_;
     size_t K_;
+    const std::atomic<bool> *cancel_ = nullptr;
+    bool cancelled_ = false;
     const double *cols_ = nullptr;   // [dim][K], thread-local scratch valid during the build
     std::vector<size_t> vind_;
     std::vector<Node> nodes_;
