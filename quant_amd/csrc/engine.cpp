@@ -116,6 +116,7 @@ struct qvq_ctx {
     uint8_t *d_kc_sel = nullptr;      // [K/2] the cells a tie certificate needs the reference's sums of
     std::vector<double> cert_kp;      // the reference's split where known (tie certificate)
     std::vector<uint8_t> cert_known;
+    std::vector<uint32_t> cert_vals;  // the certified answers (host side of their upload)
     uint64_t pub_seq = 0;          // per-level tie-count publications (h_ready[1] = seq, h_ready[2] = ties)
     double tie_abs = 0;            // the recheck's absolute tie band: centroid bits may differ by this much
     unsigned *d_counters = nullptr;   // per level: [2l] flagged rows, [2l+1] kd-tree ties; [66], [67] block counters;
@@ -1033,12 +1034,13 @@ qvq_status run_level(qvq_ctx *ctx, uint32_t K, int slot, bool sums_out, const do
 constexpr double KAHAN_DELTA = 0x1p-49;
 
 // The ties of a Kahan level answered from the level's own tree (over the exact-sum split) and
-// the reference's sums of the few cells that can matter: each tie row's
-// candidates (every code vector within a slack of its nearest that covers the reference's
-// bits), the reference's Kahan centroids of the candidates' parent cells (the selected cells
-// only), then the reference's search replayed over every split the certificate allows
-// (RefKDTree::certified_search).  done = false, nothing changed, when a row is not decided:
-// the caller then computes the whole split and its tree.
+// the reference's sums of the few cells that can matter: the reference's search
+// replayed over every split the certificate allows (RefKDTree::certified_search), first with
+// what is known without sums; for the rows it leaves open, the reference's Kahan centroids of
+// their candidates' parent cells (every code vector within a slack of the nearest that covers
+// the reference's bits; the selected cells only), the replay again; for rows still open, the
+// cells of the points a collecting replay blames, and once more.  done = false, nothing
+// changed, when a row stays open: the caller then computes the whole split and its tree.
 qvq_status certify_kahan_ties(qvq_ctx *ctx, uint32_t K, unsigned nt, uint64_t *target, bool &done) {
     done = false;
     static const bool on = !env_is("QVQ_TIE_CERT", "0");
@@ -1069,7 +1071,7 @@ qvq_status certify_kahan_ties(qvq_ctx *ctx, uint32_t K, unsigned nt, uint64_t *t
         const double u = i / D < Kc ? 1 + 0.2 : 1 - 0.2, v = kp[i];
         known[i] = v == 0 || std::fabs(v - u) <= 1e-14;
     }
-    // distinct rows, their candidates, the cells to sum
+    // distinct rows
     std::unordered_map<std::string, uint32_t> uniq;
     std::vector<uint32_t> of(nt);
     std::vector<double> qs;
@@ -1081,61 +1083,90 @@ qvq_status certify_kahan_ties(qvq_ctx *ctx, uint32_t K, unsigned nt, uint64_t *t
             for (uint32_t d = 0; d < D; d++) qs.push_back(ctx->terms.v64[code[(size_t)i * Dp + d]]);
     }
     const uint32_t nu = (uint32_t)uniq.size();
-    std::vector<std::vector<uint32_t>> cand(nu);
+    std::vector<int64_t> ans(nu, -1);
+    std::vector<uint32_t> open;
+    auto replay = [&](const std::vector<uint32_t> &rows, std::vector<uint32_t> &left) {
+        left.clear();
+        tree.cert_clear();   // kp / known may have changed in place
+        for (uint32_t u : rows)
+            if ((ans[u] = tree.certified_search(&qs[(size_t)u * D], KAHAN_DELTA, kp.data(), known.data())) < 0)
+                left.push_back(u);
+    };
+    std::vector<uint32_t> all(nu);
+    for (uint32_t u = 0; u < nu; u++) all[u] = u;
+    replay(all, open);
     std::vector<uint8_t> sel(Kc, 0);
-    std::vector<uint32_t> blame;
-    uint32_t cells = 0;
-    auto want = [&](uint32_t j) {
+    uint32_t cells = 0, rounds = 0;
+    auto want = [&](uint32_t j, bool &any) {
         for (uint32_t d = 0; d < D; d++)
             if (!known[(size_t)j * D + d]) {
-                cells += !sel[j % Kc];
+                if (!sel[j % Kc]) cells++, any = true;
                 sel[j % Kc] = 1;
                 return;
             }
     };
-    for (uint32_t u = 0; u < nu; u++) {
-        double dmin;
-        tree.near_set(&qs[(size_t)u * D], 1e-9, 1e-9, cand[u], dmin);
-        for (uint32_t j : cand[u]) want(j);
-        // and the points whose bits settle the replay's open decisions
-        blame.clear();
-        tree.certify_blame(&qs[(size_t)u * D], KAHAN_DELTA, kp.data(), known.data(), blame);
-        for (uint32_t j : blame) want(j);
-    }
-    if (cells) {   // the reference's centroids of those cells (of the previous level's assignment)
-        if ((st = ensure_kahan(ctx, Kc)) != QVQ_OK) return st;
+    // the reference's centroids of the selected cells (of the previous level's assignment)
+    auto sum_cells = [&]() -> qvq_status {
+        qvq_status s2;
+        if ((s2 = ensure_kahan(ctx, Kc)) != QVQ_OK) return s2;
         HIPCHK(hipMemcpyAsync(ctx->d_kc_sel, sel.data(), Kc, hipMemcpyHostToDevice, ctx->stream));
         HIPCHK(launch_kahan_centroids(ctx->stream, ctx->kw, ctx->d_codes, ctx->Dp, D, ctx->N, ctx->d_A_alt, Kc,
                                       ctx->d_kc_cent, ctx->d_kc_split, ctx->d_kc_sel));
         ctx->h_kc_split.resize((size_t)K * D);
         HIPCHK(hipMemcpyAsync(ctx->h_kc_split.data(), ctx->d_kc_split, (size_t)K * D * 8, hipMemcpyDeviceToHost,
                               ctx->stream));
-        if ((st = wait_stream(ctx)) != QVQ_OK) return st;
+        if ((s2 = wait_stream(ctx)) != QVQ_OK) return s2;
         for (uint32_t c = 0; c < Kc; c++)
             if (sel[c])
                 for (uint32_t r : {c, c + Kc}) {
                     std::memcpy(&kp[(size_t)r * D], &ctx->h_kc_split[(size_t)r * D], D * 8);
                     std::memset(&known[(size_t)r * D], 1, D);
                 }
-    }
-    std::vector<uint32_t> ans(nu), vals(nt);
-    for (uint32_t u = 0; u < nu; u++) {
-        const int64_t a = certify_tie(tree, &qs[(size_t)u * D], cand[u], kp.data(), known.data(), (int)D, KAHAN_DELTA);
-        if (a < 0) {
-            if (env_is("QVQ_KAHAN_DEBUG", "1"))
-                std::fprintf(stderr, "qvq kahan: K %u ties %u (%u distinct) cells %u: row not certified\n", K, nt, nu,
-                             cells);
-            return QVQ_OK;
+        rounds++;
+        return QVQ_OK;
+    };
+    std::vector<uint32_t> cand, blame, left;
+    if (!open.empty()) {   // the candidates' cells
+        bool any = false;
+        for (uint32_t u : open) {
+            double dmin;
+            tree.near_set(&qs[(size_t)u * D], 1e-9, 1e-9, cand, dmin);
+            for (uint32_t j : cand) want(j, any);
         }
-        ans[u] = (uint32_t)a;
+        if (any) {
+            if ((st = sum_cells()) != QVQ_OK) return st;
+            replay(open, left);
+            open.swap(left);
+        }
     }
-    for (uint32_t i = 0; i < nt; i++) vals[i] = ans[of[i]];
+    if (!open.empty()) {   // the cells of the points whose bits settle the open decisions
+        bool any = false;
+        for (uint32_t u : open) {
+            blame.clear();
+            tree.certify_blame(&qs[(size_t)u * D], KAHAN_DELTA, kp.data(), known.data(), blame);
+            for (uint32_t j : blame) want(j, any);
+        }
+        if (any) {
+            if ((st = sum_cells()) != QVQ_OK) return st;
+            replay(open, left);
+            open.swap(left);
+        }
+    }
+    if (!open.empty()) {
+        if (env_is("QVQ_KAHAN_DEBUG", "1"))
+            std::fprintf(stderr, "qvq kahan: K %u ties %u (%u distinct) cells %u: %zu rows not certified\n", K, nt, nu,
+                         cells, open.size());
+        return QVQ_OK;
+    }
+    std::vector<uint32_t> &vals = ctx->cert_vals;   // outlives the copy (no wait)
+    vals.resize(nt);
+    for (uint32_t i = 0; i < nt; i++) vals[i] = (uint32_t)ans[of[i]];
     HIPCHK(hipMemcpyAsync(d_vals, vals.data(), nt * 4, hipMemcpyHostToDevice, ctx->stream));
     HIPCHK(launch_fix_rows(ctx->stream, ctx->d_codes, Dp, D, ctx->d_A, ctx->d_ties, d_vals, nt, K, nullptr, nullptr,
                            ctx->d_plut, target));
-    if ((st = wait_stream(ctx)) != QVQ_OK) return st;   // vals must outlive the copy
     if (env_is("QVQ_KAHAN_DEBUG", "1"))
-        std::fprintf(stderr, "qvq kahan: K %u ties %u (%u distinct) certified, cells summed %u\n", K, nt, nu, cells);
+        std::fprintf(stderr, "qvq kahan: K %u ties %u (%u distinct) certified, cells summed %u in %u rounds\n", K, nt,
+                     nu, cells, rounds);
     done = true;
     return QVQ_OK;
 }

@@ -7,7 +7,6 @@
 
 #include <algorithm>
 #include <cmath>
-#include <functional>
 #include <limits>
 #include <memory>
 
@@ -53,6 +52,8 @@ __attribute__((target_clones("avx2", "default"))) void rows_min_max(const double
 
 RefKDTree::RefKDTree(const double *pts, size_t K, int dim, const std::atomic<bool> *cancel)
     : pts_(pts), dim_(dim), K_(K), cancel_(cancel) {
+    static std::atomic<uint64_t> next_id{1};
+    id_ = next_id.fetch_add(1);
     static thread_local std::vector<double> cols;   // reused: a fresh 1.5 MB buffer per level page-faults
     if (cols.size() < K * (size_t)dim) cols.resize(K * (size_t)dim);
     double *const cbuf = cols.data();
@@ -332,6 +333,7 @@ void RefKDTree::near_set(const double *q, double slack_rel, double slack_abs, st
 // Blame (the collecting run): the points holding node's least and greatest value in dimension
 // d, unless known already.
 void RefKDTree::blame_extremes(int node, int d) const {
+    CertScratch &S = cert_scratch();
     const Node &n = nodes_[node];
     double mn = ptr(vind_[n.left], d), mx = mn;
     for (size_t i = n.left + 1; i < n.right; i++) {
@@ -342,16 +344,17 @@ void RefKDTree::blame_extremes(int node, int d) const {
     for (size_t i = n.left; i < n.right; i++) {
         const size_t p = vind_[i];
         const double v = ptr(p, d);
-        if ((v == mn || v == mx) && !cert_known_[p * (size_t)dim_ + d]) cert_blame_->push_back((uint32_t)p);
+        if ((v == mn || v == mx) && !S.known[p * (size_t)dim_ + d]) S.blame->push_back((uint32_t)p);
     }
 }
 
 // ... and with_cell those of the node's cell box's origin in d too (the root's box and every
 // ancestor that cut along d).
 void RefKDTree::blame_dim(int node, int d, bool with_cell) const {
+    CertScratch &S = cert_scratch();
     blame_extremes(node, d);
     if (!with_cell) return;
-    for (int a = cert_parent_[node]; a >= 0; a = cert_parent_[a])
+    for (int a = S.parent[node]; a >= 0; a = S.parent[a])
         if (nodes_[a].divfeat == d) blame_extremes(a, d);
     if (node != 0) blame_extremes(0, d);
 }
@@ -363,12 +366,13 @@ void RefKDTree::blame_dim(int node, int d, bool with_cell) const {
 // cell boxes and divlow / divhigh get their intervals.  Collecting, an open decision blames the
 // points it reads and the replay goes on with the exact split's decision.
 bool RefKDTree::cert_split(int node) const {
+    CertScratch &S = cert_scratch();
     const Node &n = nodes_[node];
-    CertNode &cn = cert_[node];
+    CertNode &cn = S.node[node];
     cn.state = 2;
-    const bool collect = cert_blame_ != nullptr;
+    const bool collect = S.blame != nullptr;
     const int D = dim_;
-    const Iv *cb = &cert_box_[(size_t)node * D * 2];
+    const Iv *cb = &S.box[(size_t)node * D * 2];
     const size_t *ind = vind_.data() + n.left;
     const size_t count = n.right - n.left;
     const double EPS = 0.00001;
@@ -393,27 +397,13 @@ bool RefKDTree::cert_split(int node) const {
     }
     if (!collect && cand != n.cand) return false;
     cand = n.cand;
-    auto col = [&](int d, size_t b, size_t e, Iv &mn, Iv &mx) {
-        const Iv v0 = piv(vind_[b], d);
-        mn = mx = v0;
-        for (size_t i = b + 1; i < e; i++) {
-            const Iv v = piv(vind_[i], d);
-            mn.lo = std::min(mn.lo, v.lo);
-            mn.hi = std::min(mn.hi, v.hi);
-            mx.lo = std::max(mx.lo, v.lo);
-            mx.hi = std::max(mx.hi, v.hi);
-        }
-    };
     const int c = n.divfeat;
-    Iv mn, mx;
-    col(c, n.left, n.right, mn, mx);
+    const Iv mn = iv_min(node, c), mx = iv_max(node, c);
     if (cand) {   // the first candidate of greatest spread, strictly ahead of the others
         const double sc_lo = mx.lo - mn.hi;
         for (int j = 0; j < D; j++) {
             if (j == c || !((cand >> j) & 1)) continue;
-            Iv jm, jx;
-            col(j, n.left, n.right, jm, jx);
-            const double sj_hi = jx.hi - jm.lo;
+            const double sj_hi = iv_max(node, j).hi - iv_min(node, j).lo;
             if (j < c ? !(sj_hi < sc_lo) : !(sj_hi <= sc_lo)) {
                 if (!collect) return false;
                 blame_dim(node, j, false);
@@ -423,6 +413,9 @@ bool RefKDTree::cert_split(int node) const {
     } else if (c != 0) {
         return false;
     }
+    // the exact split's children: their exact boxes along c tell whether a point sits on the cut
+    const Node &c1 = nodes_[n.child1], &c2 = nodes_[n.child2];
+    const double e1 = node_box_[(size_t)n.child1 * D + c].high, e2 = node_box_[(size_t)n.child2 * D + c].low;
     const Iv sv{(cb[2 * c].lo + cb[2 * c + 1].lo) / 2, (cb[2 * c].hi + cb[2 * c + 1].hi) / 2};
     Iv cut;
     if (n.cutval == n.split_val) {   // not clamped, for all; no point meets the cut unless both are exact
@@ -432,7 +425,10 @@ bool RefKDTree::cert_split(int node) const {
         }
         cut = sv;
         bool blamed = false;
-        for (size_t i = 0; i < count; i++) {   // and on the exact split's side of it
+        // no point on the cut: each child strictly on its side (O(1)); else point by point
+        const bool plain = e1 < n.cutval && e2 > n.cutval;
+        if (plain && iv_max(n.child1, c).hi < cut.lo && iv_min(n.child2, c).lo > cut.hi) {
+        } else for (size_t i = 0; i < count; i++) {   // and on the exact split's side of it
             const double e = ptr(ind[i], c);
             const int side_e = e < n.cutval ? 0 : (e == n.cutval ? 1 : 2);
             const Iv v = piv(ind[i], c);
@@ -443,7 +439,7 @@ bool RefKDTree::cert_split(int node) const {
             else side = -1;
             if (side != side_e) {
                 if (!collect) return false;
-                if (!cert_known_[ind[i] * (size_t)D + c]) cert_blame_->push_back((uint32_t)ind[i]);
+                if (!S.known[ind[i] * (size_t)D + c]) S.blame->push_back((uint32_t)ind[i]);
                 if (!blamed) blame_dim(node, c, true);
                 blamed = true;
             }
@@ -455,6 +451,19 @@ bool RefKDTree::cert_split(int node) const {
             blame_dim(node, c, true);
         }
         cut = low ? mn : mx;
+        // the usual shape: one child is exactly the points at the clamp value (O(1) then)
+        const int at_child = low ? n.child1 : n.child2, rest = low ? n.child2 : n.child1;
+        const bool shaped = low ? (e1 == n.cutval && e2 > n.cutval) : (e2 == n.cutval && e1 < n.cutval);
+        bool quick = false;
+        if (shaped) {
+            const Iv am = iv_min(at_child, c), ax = iv_max(at_child, c);
+            const bool one = nodes_[at_child].right - nodes_[at_child].left == 1;
+            const bool ex = am.lo == ax.hi;   // all known, one value
+            if (ex || one) {
+                const double lim = ex ? am.lo : (low ? ax.hi : am.lo);
+                quick = low ? iv_min(rest, c).lo > lim : iv_max(rest, c).hi < lim;
+            }
+        }
         size_t nat = 0;
         bool exact = true;   // every one of them known, all at one value
         Iv at{0, 0};
@@ -465,9 +474,9 @@ bool RefKDTree::cert_split(int node) const {
                 at = v;
                 nat++;
             }
-        bool open = !exact && nat != 1;
+        bool open = !quick && !exact && nat != 1;
         const double lim = exact ? at.lo : (low ? at.hi : at.lo);
-        for (size_t i = 0; i < count && !open; i++) {
+        for (size_t i = 0; i < count && !open && !quick; i++) {
             if (ptr(ind[i], c) == n.cutval) continue;
             const Iv v = piv(ind[i], c);
             open = low ? !(v.lo > lim) : !(v.hi < lim);
@@ -477,52 +486,97 @@ bool RefKDTree::cert_split(int node) const {
             blame_dim(node, c, false);
             for (size_t i = 0; i < count; i++) {   // and every point that may reach the extreme
                 const Iv v = piv(ind[i], c);
-                if ((low ? v.lo <= cut.hi : v.hi >= cut.lo) && !cert_known_[ind[i] * (size_t)D + c])
-                    cert_blame_->push_back((uint32_t)ind[i]);
+                if ((low ? v.lo <= cut.hi : v.hi >= cut.lo) && !S.known[ind[i] * (size_t)D + c])
+                    S.blame->push_back((uint32_t)ind[i]);
             }
         }
     }
-    Iv *lb = &cert_box_[(size_t)n.child1 * D * 2], *rb = &cert_box_[(size_t)n.child2 * D * 2];
+    Iv *lb = &S.box[(size_t)n.child1 * D * 2], *rb = &S.box[(size_t)n.child2 * D * 2];
     std::copy(cb, cb + 2 * D, lb);
     std::copy(cb, cb + 2 * D, rb);
     lb[2 * c + 1] = cut;
     rb[2 * c] = cut;
-    cert_box_set_[n.child1] = cert_box_set_[n.child2] = 1;
-    const Node &c1 = nodes_[n.child1], &c2 = nodes_[n.child2];
-    Iv t0, t1;
-    col(c, c1.left, c1.right, t0, cn.dl);
-    col(c, c2.left, c2.right, cn.dh, t1);
+    S.box_set[n.child1] = S.box_set[n.child2] = 1;
+    cn.dl = iv_max(n.child1, c);
+    cn.dh = iv_min(n.child2, c);
+    (void)c1;
+    (void)c2;
     cn.state = 1;
     return true;
 }
 
+RefKDTree::CertScratch &RefKDTree::cert_scratch() {
+    static thread_local CertScratch s;
+    return s;
+}
+
 void RefKDTree::cert_reset(double delta, const double *kpts, const uint8_t *known) const {
-    if (cert_delta_ == delta && cert_k_ == kpts && cert_known_ == known) return;
+    CertScratch &S = cert_scratch();
+    const bool collect = S.blame != nullptr;
+    if (S.owner == id_ && S.delta == delta && S.k == kpts && S.known == known && S.collect == collect)
+        return;
     const int D = dim_;
-    cert_delta_ = delta;
-    cert_k_ = kpts;
-    cert_known_ = known;
-    cert_.assign(nodes_.size(), CertNode());
-    cert_box_.assign(nodes_.size() * D * 2, Iv{0, 0});
-    cert_box_set_.assign(nodes_.size(), 0);
-    if (cert_parent_.size() != nodes_.size()) {
-        cert_parent_.assign(nodes_.size(), -1);
-        for (size_t i = 0; i < nodes_.size(); i++)
-            if (!nodes_[i].leaf) cert_parent_[nodes_[i].child1] = cert_parent_[nodes_[i].child2] = (int)i;
+    const size_t nn = nodes_.size();
+    if (S.owner != id_) {
+        S.parent.assign(nn, -1);
+        for (size_t i = 0; i < nn; i++)
+            if (!nodes_[i].leaf) S.parent[nodes_[i].child1] = S.parent[nodes_[i].child2] = (int)i;
+    }
+    S.owner = id_;
+    S.collect = collect;
+    S.delta = delta;
+    S.k = kpts;
+    S.known = known;
+    S.node.assign(nn, CertNode());
+    S.box.resize(nn * D * 2);
+    S.box_set.assign(nn, 0);
+    S.agg.resize(nn * D * 4);
+    // per node and dimension: min / max over its points whose bits are not known (exact-sum
+    // values) and over those known (the reference's values), children before parents
+    constexpr double INF = std::numeric_limits<double>::infinity();
+    for (size_t i = nodes_.size(); i-- > 0;) {
+        double *a = &S.agg[i * D * 4];
+        const Node &n = nodes_[i];
+        for (int d = 0; d < D; d++) {
+            a[4 * d] = a[4 * d + 2] = INF;
+            a[4 * d + 1] = a[4 * d + 3] = -INF;
+        }
+        if (n.leaf) {
+            for (size_t j = n.left; j < n.right; j++) {
+                const size_t p = vind_[j];
+                for (int d = 0; d < D; d++) {
+                    const size_t e = p * (size_t)D + d;
+                    const int o = known[e] ? 2 : 0;
+                    const double v = known[e] ? kpts[e] : pts_[e];
+                    a[4 * d + o] = std::min(a[4 * d + o], v);
+                    a[4 * d + o + 1] = std::max(a[4 * d + o + 1], v);
+                }
+            }
+        } else {
+            const double *b = &S.agg[(size_t)n.child1 * D * 4], *c = &S.agg[(size_t)n.child2 * D * 4];
+            for (int k = 0; k < 4 * D; k += 2) {
+                a[k] = std::min(b[k], c[k]);
+                a[k + 1] = std::max(b[k + 1], c[k + 1]);
+            }
+        }
     }
     for (int d = 0; d < D; d++) {   // the root's cell box: the points' box
-        Iv lo = piv(0, d), hi = lo;
-        for (size_t p = 1; p < K_; p++) {
-            const Iv v = piv(p, d);
-            lo.lo = std::min(lo.lo, v.lo);
-            lo.hi = std::min(lo.hi, v.hi);
-            hi.lo = std::max(hi.lo, v.lo);
-            hi.hi = std::max(hi.hi, v.hi);
-        }
-        cert_box_[2 * d] = lo;
-        cert_box_[2 * d + 1] = hi;
+        S.box[2 * d] = iv_min(0, d);
+        S.box[2 * d + 1] = iv_max(0, d);
     }
-    cert_box_set_[0] = 1;
+    S.box_set[0] = 1;
+}
+
+// The least (greatest) value of dimension d over node's points, over every allowed codebook.
+RefKDTree::Iv RefKDTree::iv_min(int node, int d) const {
+    CertScratch &S = cert_scratch();
+    const double *a = &S.agg[((size_t)node * dim_ + d) * 4];
+    return {std::min(a[0] - S.delta, a[2]), std::min(a[0] + S.delta, a[2])};
+}
+RefKDTree::Iv RefKDTree::iv_max(int node, int d) const {
+    CertScratch &S = cert_scratch();
+    const double *a = &S.agg[((size_t)node * dim_ + d) * 4];
+    return {std::max(a[1] - S.delta, a[3]), std::max(a[1] + S.delta, a[3])};
 }
 
 namespace {
@@ -536,20 +590,26 @@ inline void sq_iv(double elo, double ehi, double &lo, double &hi) {
 
 void RefKDTree::certify_blame(const double *q, double delta, const double *kpts, const uint8_t *known,
                               std::vector<uint32_t> &blame) const {
-    cert_delta_ = -1;   // a fresh replay, kept apart from the strict one's cache
-    cert_blame_ = &blame;
+    CertScratch &S = cert_scratch();
+    // the collecting replay keeps a cache of its own (a node it replayed has blamed already)
+    S.blame = &blame;
     certified_search(q, delta, kpts, known);
-    cert_blame_ = nullptr;
-    cert_delta_ = -1;
+    S.blame = nullptr;
+}
+
+void RefKDTree::cert_clear() const {
+    CertScratch &S = cert_scratch();
+    S.delta = -1;
+    if (S.owner == id_) S.owner = 0;
 }
 
 // kd_nearest_flat (the reference's search) replayed over every codebook the certificate allows:
 // each quantity an interval, each decision taken only when all of them take it (collecting:
 // an open decision blames the points it reads and the exact split's decision is taken).
 int64_t RefKDTree::certified_search(const double *q, double delta, const double *kpts, const uint8_t *known) const {
+    CertScratch &S = cert_scratch();
     if (dim_ > 64) return -1;
-    const bool collect = cert_blame_ != nullptr;
-    if (collect && cert_delta_ != -1) cert_delta_ = -1;
+    const bool collect = S.blame != nullptr;
     cert_reset(delta, kpts, known);
     const int D = dim_;
     constexpr double U = 1.1102230246251565e-16;   // unit roundoff
@@ -557,7 +617,7 @@ int64_t RefKDTree::certified_search(const double *q, double delta, const double 
     double mlo = 0, mhi = 0;
     for (int d = 0; d < D; d++) {   // the initial distances against the root box
         const double x = q[d];
-        const Iv lo = cert_box_[2 * d], hi = cert_box_[2 * d + 1];
+        const Iv lo = S.box[2 * d], hi = S.box[2 * d + 1];
         dlo[d] = dhi[d] = 0;
         if ((!(x < lo.lo) && x < lo.hi) || (!(x > hi.hi) && x > hi.lo)) {
             if (!collect) return -1;
@@ -600,11 +660,11 @@ int64_t RefKDTree::certified_search(const double *q, double delta, const double 
     auto blame_pt = [&](uint32_t p) {
         for (int d = 0; d < D; d++)
             if (!known[(size_t)p * D + d]) {
-                cert_blame_->push_back(p);
+                S.blame->push_back(p);
                 return;
             }
     };
-    std::function<void(int, double, double)> search = [&](int node, double slo, double shi) {
+    auto search = [&](auto &&self, int node, double slo, double shi) -> void {
         if (!ok) return;
         const Node &n = nodes_[node];
         if (n.leaf) {
@@ -627,14 +687,14 @@ int64_t RefKDTree::certified_search(const double *q, double delta, const double 
             }
             return;
         }
-        if (cert_[node].state == 0 && cert_box_set_[node]) cert_split(node);
-        if (cert_[node].state != 1) {
+        if (S.node[node].state == 0 && S.box_set[node]) cert_split(node);
+        if (S.node[node].state != 1) {
             ok = false;
             return;
         }
         const int f = n.divfeat;
         const double val = q[f];
-        const CertNode &cn = cert_[node];
+        const CertNode &cn = S.node[node];
         const double s_hi = (val - cn.dl.lo) + (val - cn.dh.lo), s_lo = (val - cn.dl.hi) + (val - cn.dh.hi);
         bool left_first = s_hi < 0;
         if (!(s_hi < 0) && !(s_lo >= 0)) {
@@ -647,7 +707,7 @@ int64_t RefKDTree::certified_search(const double *q, double delta, const double 
             left_first = (val - n.divlow) + (val - n.divhigh) < 0;
         }
         path.push_back(node);
-        search(left_first ? n.child1 : n.child2, slo, shi);
+        self(self, left_first ? n.child1 : n.child2, slo, shi);
         path.pop_back();
         if (!ok) return;
         double clo, chi;
@@ -674,13 +734,13 @@ int64_t RefKDTree::certified_search(const double *q, double delta, const double 
         }
         if (visit) {
             path.push_back(node);
-            search(left_first ? n.child2 : n.child1, m2lo, m2hi);
+            self(self, left_first ? n.child2 : n.child1, m2lo, m2hi);
             path.pop_back();
         }
         dlo[f] = tlo;
         dhi[f] = thi;
     };
-    search(0, mlo, mhi);
+    search(search, 0, mlo, mhi);
     return ok && !amb && blo < MAXD ? idx : -1;
 }
 

@@ -61,6 +61,8 @@ public:
     // decision is taken), so that one round of Kahan sums can make the strict replay succeed.
     void certify_blame(const double *q, double delta, const double *kpts, const uint8_t *known,
                        std::vector<uint32_t> &blame) const;
+    // Forget the replays' caches (kpts or known changed in place).
+    void cert_clear() const;
 
 private:
     struct Node {
@@ -104,23 +106,37 @@ private:
         int8_t state = 0;   // 0 not replayed, 1 the same split for every such codebook, 2 not shown
         Iv dl{0, 0}, dh{0, 0};   // divlow, divhigh
     };
+    // the replay's state, per thread (replays of one tree may run on several threads) and
+    // reused from tree to tree (no fresh pages per level); owned by the tree that reset it last
+    struct CertScratch {
+        uint64_t owner = 0;   // the owning tree's id_
+        double delta = -1;
+        const double *k = nullptr;       // the reference's split where known
+        const uint8_t *known = nullptr;
+        bool collect = false;            // the cache's mode
+        std::vector<uint32_t> *blame = nullptr;   // collecting (certify_blame)
+        std::vector<CertNode> node;
+        std::vector<Iv> box;          // [node][dim][lo, hi]: the node's cell box, once its parent replayed
+        std::vector<uint8_t> box_set;
+        std::vector<double> agg;      // [node][dim][min, max unknown | min, max known]
+        std::vector<int> parent;
+    };
+    static CertScratch &cert_scratch();
     Iv piv(size_t p, int d) const {
+        const CertScratch &S = cert_scratch();
         const size_t i = p * (size_t)dim_ + d;
-        if (cert_known_[i]) return {cert_k_[i], cert_k_[i]};
-        return {pts_[i] - cert_delta_, pts_[i] + cert_delta_};
+        if (S.known[i]) return {S.k[i], S.k[i]};
+        return {pts_[i] - S.delta, pts_[i] + S.delta};
     }
     bool cert_split(int node) const;
     void cert_reset(double delta, const double *kpts, const uint8_t *known) const;
     void blame_extremes(int node, int d) const;
+    Iv iv_min(int node, int d) const;
+    Iv iv_max(int node, int d) const;
+
     void blame_dim(int node, int d, bool with_cell) const;
-    mutable std::vector<uint32_t> *cert_blame_ = nullptr;   // collecting (certify_blame)
-    mutable std::vector<int> cert_parent_;
-    mutable double cert_delta_ = -1;
-    mutable const double *cert_k_ = nullptr;
-    mutable const uint8_t *cert_known_ = nullptr;
-    mutable std::vector<CertNode> cert_;
-    mutable std::vector<Iv> cert_box_;   // [node][dim][lo, hi]: the node's cell box, once its parent replayed
-    mutable std::vector<uint8_t> cert_box_set_;
+
+    uint64_t id_;   // unique per tree (a later tree may reuse this one's address)
 };
 
 // The reference's index for tie row q: certified_search, once the candidates cand (near_set

@@ -6,6 +6,7 @@
 //   test_tie_cert levels.bin
 // file: per level [u32 K][u32 D][u32 n] exact split (K x D f64) | Kahan split (K x D f64) |
 //       rows (n x D f64) | the reference's indices (n u32)
+#include <chrono>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -44,49 +45,61 @@ int main(int argc, char **argv) {
         RefKDTree tree(ex.data(), K, (int)D);
         std::vector<uint32_t> cand;
         long cert = 0, wrong = 0, multi = 0, cells = 0;
-        // the engine's order: every row's candidates first, then the parent cells of the
-        // nonzero ones (both split rows of each) from the reference's sums, then the answers
-        std::vector<uint32_t> blame;
-        const bool use_blame = !getenv("TIE_CERT_NO_BLAME");
-        for (uint32_t r = 0; r < n; r++) {
+        // the engine's order (engine.cpp certify_kahan_ties): each row's replay with what is
+        // known without sums; for the rows left open, the parent cells of their candidates
+        // (both split rows of each) from the reference's sums and the replay again; for rows
+        // still open, the cells of the points a collecting replay blames, and once more
+        const auto t0 = std::chrono::steady_clock::now();
+        std::vector<uint32_t> blame, open, left;
+        std::vector<int64_t> got(n, -1);
+        auto replay = [&](std::vector<uint32_t> &rows) {
+            tree.cert_clear();   // kp / known changed in place
+            left.clear();
+            for (uint32_t r : rows)
+                if ((got[r] = tree.certified_search(q.data() + (size_t)r * D, delta, kp.data(), known.data())) < 0)
+                    left.push_back(r);
+            rows.swap(left);
+        };
+        auto need = [&](uint32_t j) {
+            bool all = true;
+            for (uint32_t d = 0; d < D; d++) all = all && known[(size_t)j * D + d];
+            if (all) return;
+            const uint32_t par = j % (K / 2);
+            for (uint32_t s : {par, par + K / 2}) {
+                std::memcpy(&kp[(size_t)s * D], &ka[(size_t)s * D], D * 8);
+                std::memset(&known[(size_t)s * D], 1, D);
+            }
+            cells++;
+        };
+        for (uint32_t r = 0; r < n; r++) open.push_back(r);
+        replay(open);
+        for (uint32_t r : open) {
             double dmin;
             tree.near_set(q.data() + (size_t)r * D, 1e-9, 1e-9, cand, dmin);
-            if (use_blame) {   // and the points the replay's open decisions read
+            for (uint32_t j : cand) need(j);
+        }
+        if (!open.empty()) replay(open);
+        if (!getenv("TIE_CERT_NO_BLAME")) {
+            for (uint32_t r : open) {
                 blame.clear();
                 tree.certify_blame(q.data() + (size_t)r * D, delta, kp.data(), known.data(), blame);
-                cand.insert(cand.end(), blame.begin(), blame.end());
+                for (uint32_t j : blame) need(j);
             }
-            for (uint32_t j : cand) {
-                bool all = true;
-                for (uint32_t d = 0; d < D; d++) all = all && known[(size_t)j * D + d];
-                if (all) continue;
-                const uint32_t par = j % (K / 2);
-                for (uint32_t s : {par, par + K / 2}) {
-                    std::memcpy(&kp[(size_t)s * D], &ka[(size_t)s * D], D * 8);
-                    std::memset(&known[(size_t)s * D], 1, D);
-                }
-                cells++;
-            }
+            if (!open.empty()) replay(open);
         }
+        const auto t1 = std::chrono::steady_clock::now();
         for (uint32_t r = 0; r < n; r++) {
-            const double *x = q.data() + (size_t)r * D;
-            double dmin;
-            tree.near_set(x, 1e-9, 1e-9, cand, dmin);
-            const int64_t a = certify_tie(tree, x, cand, kp.data(), known.data(), (int)D, delta);
-            if (a < 0 && getenv("TIE_CERT_VERBOSE")) {
-                printf("undecided level %d row %u want %u:", level, r, want[r]);
-                for (uint32_t j : cand)
-                    printf(" %u(ex %.17g ka %.17g)", j, ref_l2(x, ex.data() + (size_t)j * D, (int)D),
-                           ref_l2(x, kp.data() + (size_t)j * D, (int)D));
-                printf("\n");
+            if (got[r] < 0) {
+                if (getenv("TIE_CERT_VERBOSE")) printf("undecided level %d row %u want %u\n", level, r, want[r]);
+                continue;
             }
-            if (a < 0) continue;
             cert++;
-            if ((uint32_t)a != want[r]) {
+            if ((uint32_t)got[r] != want[r]) {
                 wrong++;
-                if (wrong <= 5) printf("WRONG level %d row %u: got %lld want %u\n", level, r, (long long)a, want[r]);
+                if (wrong <= 5) printf("WRONG level %d row %u: got %lld want %u\n", level, r, (long long)got[r], want[r]);
             }
         }
+        const auto t2 = std::chrono::steady_clock::now();
         // rows whose candidates tie exactly under the reference's bits
         for (uint32_t r = 0; r < n; r++) {
             const double *x = q.data() + (size_t)r * D;
@@ -101,8 +114,9 @@ int main(int argc, char **argv) {
             }
             multi += at > 1;
         }
-        printf("level K %u: rows %u certified %ld wrong %ld exact ties %ld cells computed %ld\n", K, n, cert, wrong,
-               multi, cells);
+        printf("level K %u: rows %u certified %ld wrong %ld exact ties %ld cells computed %ld (host %.3f + %.3f ms)\n",
+               K, n, cert, wrong, multi, cells, std::chrono::duration<double, std::milli>(t1 - t0).count(),
+               std::chrono::duration<double, std::milli>(t2 - t1).count());
         tot_rows += n;
         tot_cert += cert;
         tot_wrong += wrong;
