@@ -62,6 +62,8 @@ typedef struct {
                                    traversal (device kernel; host only for trees too deep) */
     double wait_ms[32];         /* host wall waiting for the level's codebook (previous finalize) */
     double tree_ms[32];         /* host wall building the level's kd-tree image (overlaps the search) */
+    int kahan_redo;             /* 1: a level's ties failed the speculative reference-rule check, and the
+                                   quantize ran again with synchronous reference-bit levels */
 } qvq_timings;
 
 /* Context: one per GPU per host thread.  Owns device memory and one HIP stream. */

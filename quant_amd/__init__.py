@@ -33,7 +33,7 @@ class _Timings(ctypes.Structure):
                 ("assign_ms", ctypes.c_double * 32), ("update_ms", ctypes.c_double * 32),
                 ("other_ms", ctypes.c_double * 32), ("flagged", ctypes.c_uint64 * 32),
                 ("host_ties", ctypes.c_uint64 * 32), ("wait_ms", ctypes.c_double * 32),
-                ("tree_ms", ctypes.c_double * 32)]
+                ("tree_ms", ctypes.c_double * 32), ("kahan_redo", ctypes.c_int)]
 
 
 _lib = None
@@ -233,7 +233,8 @@ class Engine:
                 "assign_ms": list(t.assign_ms[:max(L, 1)]), "update_ms": list(t.update_ms[:max(L, 1)]),
                 "other_ms": list(t.other_ms[:max(L, 1)]),
                 "flagged": list(t.flagged[:max(L, 1)]), "host_ties": list(t.host_ties[:max(L, 1)]),
-                "wait_ms": list(t.wait_ms[:max(L, 1)]), "tree_ms": list(t.tree_ms[:max(L, 1)])}
+                "wait_ms": list(t.wait_ms[:max(L, 1)]), "tree_ms": list(t.tree_ms[:max(L, 1)]),
+                "kahan_redo": t.kahan_redo}
 
     # -- multi-GPU -----------------------------------------------------------------------
     def decode(self, cb_bytes, A, xSize, ySize, bw, bh):

@@ -332,12 +332,24 @@ hipError_t launch_mean_sums(hipStream_t s, uint32_t Dp, const uint8_t *codes, ui
 // sum_k (2 c_k.S_k - n_k ||c_k||^2) (closed-form distortion).  With done (a counter at 0,
 // left at 0) the last block also publishes *ready = seq in mapped host memory; dist_part
 // holds the per-block partials (<= 8000).
+// The level's tie rows exported with the codebook (the speculative Kahan check, engine.cpp):
+// out (mapped host memory) = [u32 count][u32 pad] then per row [u32 row][u32 A[row]][Dp code
+// bytes], the first cap rows; released with the ready flag.
+struct TieExport {
+    const uint32_t *rows = nullptr;
+    const unsigned *cnt = nullptr;
+    const uint32_t *A = nullptr;
+    const uint8_t *codes = nullptr;
+    uint32_t cap = 0;
+    uint8_t *out = nullptr;
+};
 hipError_t launch_finalize_prep(hipStream_t s, const uint64_t *sums, uint32_t K, uint32_t D, uint32_t Dp, int64_t R,
                                 int64_t bias, int scale, double *C_cent, bool split, double *C64n, uint32_t Kpad_next,
                                 double mu, double sx, int t, float *C32, _Float16 *cb_rows, float *E32,
                                 double *host_cb, double *dist_part, unsigned *done, double *dist_out, uint64_t *ready, uint64_t seq,
                                 bool zero_sums, uint32_t ncopy = 1, uint32_t *perm = nullptr, int32_t *tint = nullptr,
-                                uint32_t zero_skip = 0, uint64_t copy_stride = 0, const unsigned *copy_gate = nullptr);
+                                uint32_t zero_skip = 0, uint64_t copy_stride = 0, const unsigned *copy_gate = nullptr,
+                                const TieExport &ties = TieExport());
 // (zero_sums: clears copies zero_skip .. ncopy - 1; copy_stride 0: the copies follow each other,
 // 2KD + K apart; copy_gate: copies past the first are read and cleared only if *copy_gate != 0)
 hipError_t launch_finalize(hipStream_t s, const uint64_t *sums, uint32_t K, uint32_t D, int64_t R, int64_t bias,

@@ -20,6 +20,7 @@
 #include <atomic>
 #include <chrono>
 #include <condition_variable>
+#include <deque>
 #include <functional>
 #include <mutex>
 #include <thread>
@@ -159,14 +160,32 @@ struct qvq_ctx {
     std::unique_ptr<RefKDTree> tree;   // the last level's tree over cb_local
     KdView tree_kd;                    // and its device image (depth 0: none)
     // deferred-tie levels build their tree on this worker, off the launch path (start_tree_job)
-    struct Worker {
+    struct Worker {   // one host thread, jobs in order
         std::thread th;
         std::mutex m;
         std::condition_variable cv;
-        std::function<void()> job;
+        std::deque<std::function<void()>> q;
         bool stop = false;
-        std::atomic<bool> busy{false};
+        std::atomic<int> pending{0};
     } worker;
+    // the speculative Kahan check (qvq_lbg): level L's ties verified on the worker while the GPU
+    // runs level L + 1; three assignment buffers keep A_{L-1} (the check's cells) until L + 2
+    uint32_t *d_A3 = nullptr;
+    uint8_t *h_tx[2] = {nullptr, nullptr}, *dh_tx[2] = {nullptr, nullptr};   // TieExport, per level parity
+    uint32_t tx_cap = 0;
+    hipStream_t vstream = nullptr;   // the check's selected Kahan sums
+    struct Verify {
+        bool posted = false;
+        std::atomic<bool> done{true}, cancel{false};
+        int status = 0;   // 0: the reference's indices are the speculative ones; 1: not shown
+        uint32_t K = 0;
+        uint64_t seq = 0;
+        int par = 0;
+        const uint32_t *A_prev = nullptr;
+        std::unique_ptr<RefKDTree> tree;
+        std::vector<double> cb;
+        hipEvent_t ev = nullptr;
+    } ver[2];
     std::atomic<bool> tree_cancel{false};
     bool tree_job = false, job_ok = false;
     int job_buf = 0;
@@ -310,6 +329,7 @@ void free_kahan(qvq_ctx *ctx) {
 void free_training(qvq_ctx *ctx) {
     free_kahan(ctx);
     dfree(ctx->d_A_alt);
+    dfree(ctx->d_A3);
     dfree(ctx->d_X64);
     dfree(ctx->d_ex_keys);
     dfree(ctx->d_ex_iota);
@@ -707,54 +727,57 @@ void build_tree(qvq_ctx *ctx, const double *hC, uint32_t K, int buf, KdView &kd)
 // host learns after the search: the worker awaits the codebook's publication and builds the
 // tree while this thread enqueues the rest of the level; join_tree_job waits for it (ties)
 // or cancels it (none).
-void start_tree_job(qvq_ctx *ctx, const double *hC, uint32_t K, int buf, uint64_t wait_seq) {
-    join_tree_job(ctx, true);
-    if (env_is("QVQ_KDTREE", "host")) return;
+void post_job(qvq_ctx *ctx, std::function<void()> job) {
     qvq_ctx::Worker &w = ctx->worker;
     if (!w.th.joinable())
         w.th = std::thread([&w] {
             std::unique_lock<std::mutex> lk(w.m);
             for (;;) {
-                w.cv.wait(lk, [&w] { return w.stop || w.job; });
+                w.cv.wait(lk, [&w] { return w.stop || !w.q.empty(); });
                 if (w.stop) return;
-                std::function<void()> job = std::move(w.job);
-                w.job = nullptr;
+                std::function<void()> job = std::move(w.q.front());
+                w.q.pop_front();
                 lk.unlock();
                 job();
-                w.busy.store(false, std::memory_order_release);
+                w.pending.fetch_sub(1, std::memory_order_release);
                 lk.lock();
             }
         });
+    w.pending.fetch_add(1, std::memory_order_relaxed);
+    {
+        std::lock_guard<std::mutex> g(w.m);
+        w.q.push_back(std::move(job));
+    }
+    w.cv.notify_one();
+}
+
+void start_tree_job(qvq_ctx *ctx, const double *hC, uint32_t K, int buf, uint64_t wait_seq) {
+    join_tree_job(ctx, true);
+    if (env_is("QVQ_KDTREE", "host")) return;
     ctx->tree_cancel.store(false);
     ctx->tree_job = true;
     ctx->job_ok = false;
     ctx->job_buf = buf;
     ctx->tree_kd = KdView{};
     const int slot = (int)__builtin_ctz(K) - 1;
-    w.busy.store(true, std::memory_order_relaxed);
-    {
-        std::lock_guard<std::mutex> g(w.m);
-        w.job = [ctx, hC, K, buf, wait_seq, slot] {
-            const auto t0 = std::chrono::steady_clock::now();
-            volatile uint64_t *flag = ctx->h_ready;
-            while (wait_seq && *flag < wait_seq)   // the codebook's publication (bounded by cancel)
-                if (ctx->tree_cancel.load(std::memory_order_relaxed)) return;
-            std::atomic_thread_fence(std::memory_order_acquire);
-            const auto t1 = std::chrono::steady_clock::now();
-            build_tree_host(ctx, hC, K, buf, ctx->job_kd, &ctx->tree_cancel);
-            ctx->job_ok = !ctx->tree->cancelled();
-            ctx->tm.wait_ms[slot] = std::chrono::duration<double, std::milli>(t1 - t0).count();
-            ctx->tm.tree_ms[slot] =
-                std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t1).count();
-        };
-    }
-    w.cv.notify_one();
+    post_job(ctx, [ctx, hC, K, buf, wait_seq, slot] {
+        const auto t0 = std::chrono::steady_clock::now();
+        volatile uint64_t *flag = ctx->h_ready;
+        while (wait_seq && *flag < wait_seq)   // the codebook's publication (bounded by cancel)
+            if (ctx->tree_cancel.load(std::memory_order_relaxed)) return;
+        std::atomic_thread_fence(std::memory_order_acquire);
+        const auto t1 = std::chrono::steady_clock::now();
+        build_tree_host(ctx, hC, K, buf, ctx->job_kd, &ctx->tree_cancel);
+        ctx->job_ok = !ctx->tree->cancelled();
+        ctx->tm.wait_ms[slot] = std::chrono::duration<double, std::milli>(t1 - t0).count();
+        ctx->tm.tree_ms[slot] = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t1).count();
+    });
 }
 
 bool join_tree_job(qvq_ctx *ctx, bool cancel) {
     if (!ctx->tree_job) return false;
     if (cancel) ctx->tree_cancel.store(true);
-    while (ctx->worker.busy.load(std::memory_order_acquire)) std::this_thread::yield();
+    while (ctx->worker.pending.load(std::memory_order_acquire)) std::this_thread::yield();
     ctx->tree_job = false;
     if (!ctx->job_ok) {
         ctx->tree.reset();
@@ -1041,12 +1064,119 @@ constexpr double KAHAN_DELTA = 0x1p-49;
 // the reference's bits; the selected cells only), the replay again; for rows still open, the
 // cells of the points a collecting replay blames, and once more.  done = false, nothing
 // changed, when a row stays open: the caller then computes the whole split and its tree.
+// The certificate over nu distinct rows qs (nu x D values): ans[u] the reference's index, or -1
+// for a row it leaves open.  tree: the level's tree over the exact-sum split (K code vectors);
+// A_prev: the previous level's assignment (the cells summed on stream; sync waits for it).
+template <class Sync>
+qvq_status certify_rows(qvq_ctx *ctx, const RefKDTree &tree, const double *cb, uint32_t K, const uint32_t *A_prev,
+                        hipStream_t stream, Sync sync, const std::vector<double> &qs, uint32_t nu,
+                        std::vector<int64_t> &ans, uint32_t &open_rows, uint32_t &cells, uint32_t &rounds) {
+    const uint32_t D = ctx->D, Kc = K / 2;
+    // coordinates whose reference bits are the exact sums' without computing them: a cell's
+    // exact mean is 0 or 1 only when all its values are (SCALED values lie in [0, 1], at least
+    // 1/(255 n) from 1 otherwise; Kahan sums of 0s and 1s are exact), split by 1.2 or 0.8
+    std::vector<double> &kp = ctx->cert_kp;
+    std::vector<uint8_t> &known = ctx->cert_known;
+    kp.assign(cb, cb + (size_t)K * D);
+    known.resize((size_t)K * D);
+    for (size_t i = 0; i < known.size(); i++) {
+        const double u = i / D < Kc ? 1 + 0.2 : 1 - 0.2, v = kp[i];
+        known[i] = v == 0 || std::fabs(v - u) <= 1e-14;
+    }
+    ans.assign(nu, -1);
+    std::vector<uint32_t> open, left;
+    auto replay = [&](const std::vector<uint32_t> &rows) {
+        left.clear();
+        tree.cert_clear();   // kp / known may have changed in place
+        for (uint32_t u : rows)
+            if ((ans[u] = tree.certified_search(&qs[(size_t)u * D], KAHAN_DELTA, kp.data(), known.data())) < 0)
+                left.push_back(u);
+        open.swap(left);
+    };
+    std::vector<uint32_t> all(nu);
+    for (uint32_t u = 0; u < nu; u++) all[u] = u;
+    replay(all);
+    std::vector<uint8_t> sel(Kc, 0);
+    cells = rounds = 0;
+    auto want = [&](uint32_t j, bool &any) {
+        for (uint32_t d = 0; d < D; d++)
+            if (!known[(size_t)j * D + d]) {
+                if (!sel[j % Kc]) cells++, any = true;
+                sel[j % Kc] = 1;
+                return;
+            }
+    };
+    // the reference's centroids of the selected cells (of the previous level's assignment)
+    auto sum_cells = [&]() -> qvq_status {
+        qvq_status s2;
+        if ((s2 = ensure_kahan(ctx, Kc)) != QVQ_OK) return s2;
+        HIPCHK(hipMemcpyAsync(ctx->d_kc_sel, sel.data(), Kc, hipMemcpyHostToDevice, stream));
+        HIPCHK(launch_kahan_centroids(stream, ctx->kw, ctx->d_codes, ctx->Dp, D, ctx->N, A_prev, Kc, ctx->d_kc_cent,
+                                      ctx->d_kc_split, ctx->d_kc_sel));
+        ctx->h_kc_split.resize((size_t)K * D);
+        HIPCHK(hipMemcpyAsync(ctx->h_kc_split.data(), ctx->d_kc_split, (size_t)K * D * 8, hipMemcpyDeviceToHost, stream));
+        if ((s2 = sync()) != QVQ_OK) return s2;
+        for (uint32_t c = 0; c < Kc; c++)
+            if (sel[c])
+                for (uint32_t r : {c, c + Kc}) {
+                    std::memcpy(&kp[(size_t)r * D], &ctx->h_kc_split[(size_t)r * D], D * 8);
+                    std::memset(&known[(size_t)r * D], 1, D);
+                }
+        rounds++;
+        return QVQ_OK;
+    };
+    qvq_status st;
+    std::vector<uint32_t> cand, blame;
+    if (!open.empty() && K >= 4) {   // the candidates' cells
+        bool any = false;
+        for (uint32_t u : open) {
+            double dmin;
+            tree.near_set(&qs[(size_t)u * D], 1e-9, 1e-9, cand, dmin);
+            for (uint32_t j : cand) want(j, any);
+        }
+        if (any) {
+            if ((st = sum_cells()) != QVQ_OK) return st;
+            replay(std::vector<uint32_t>(open));
+        }
+    }
+    if (!open.empty() && K >= 4) {   // the cells of the points whose bits settle the open decisions
+        bool any = false;
+        for (uint32_t u : open) {
+            blame.clear();
+            tree.certify_blame(&qs[(size_t)u * D], KAHAN_DELTA, kp.data(), known.data(), blame);
+            for (uint32_t j : blame) want(j, any);
+        }
+        if (any) {
+            if ((st = sum_cells()) != QVQ_OK) return st;
+            replay(std::vector<uint32_t>(open));
+        }
+    }
+    open_rows = (uint32_t)open.size();
+    return QVQ_OK;
+}
+
+// Distinct rows of n row records (code bytes at code + i * stride, D of them): their values qs,
+// and of[i] = the distinct row of record i.
+uint32_t distinct_rows(const qvq_ctx *ctx, const uint8_t *code, size_t stride, uint32_t n, std::vector<double> &qs,
+                       std::vector<uint32_t> &of) {
+    std::unordered_map<std::string, uint32_t> uniq;
+    of.resize(n);
+    qs.clear();
+    for (uint32_t i = 0; i < n; i++) {
+        const uint8_t *c = code + (size_t)i * stride;
+        const auto it = uniq.emplace(std::string(reinterpret_cast<const char *>(c), ctx->D), (uint32_t)uniq.size());
+        of[i] = it.first->second;
+        if (it.second)
+            for (uint32_t d = 0; d < ctx->D; d++) qs.push_back(ctx->terms.v64[c[d]]);
+    }
+    return (uint32_t)uniq.size();
+}
+
 qvq_status certify_kahan_ties(qvq_ctx *ctx, uint32_t K, unsigned nt, uint64_t *target, bool &done) {
     done = false;
     static const bool on = !env_is("QVQ_TIE_CERT", "0");
     if (!on || !ctx->tree || ctx->cb_local.size() != (size_t)K * ctx->D || K < 4) return QVQ_OK;
-    const uint32_t D = ctx->D, Dp = ctx->Dp, Kc = K / 2;
-    const RefKDTree &tree = *ctx->tree;
+    const uint32_t D = ctx->D, Dp = ctx->Dp;
     const uint64_t need = (uint64_t)nt * (4 + Dp);
     if (ctx->scatter_bytes < need) {
         dfree(ctx->d_scatter);
@@ -1060,102 +1190,18 @@ qvq_status certify_kahan_ties(qvq_ctx *ctx, uint32_t K, unsigned nt, uint64_t *t
     HIPCHK(hipMemcpyAsync(code.data(), d_gath, code.size(), hipMemcpyDeviceToHost, ctx->stream));
     qvq_status st;
     if ((st = wait_stream(ctx)) != QVQ_OK) return st;
-    // coordinates whose reference bits are the exact sums' without computing them: a cell's
-    // exact mean is 0 or 1 only when all its values are (SCALED values lie in [0, 1], at least
-    // 1/(255 n) from 1 otherwise; Kahan sums of 0s and 1s are exact), split by 1.2 or 0.8
-    std::vector<double> &kp = ctx->cert_kp;
-    std::vector<uint8_t> &known = ctx->cert_known;
-    kp.assign(ctx->cb_local.begin(), ctx->cb_local.end());
-    known.resize((size_t)K * D);
-    for (size_t i = 0; i < known.size(); i++) {
-        const double u = i / D < Kc ? 1 + 0.2 : 1 - 0.2, v = kp[i];
-        known[i] = v == 0 || std::fabs(v - u) <= 1e-14;
-    }
-    // distinct rows
-    std::unordered_map<std::string, uint32_t> uniq;
-    std::vector<uint32_t> of(nt);
     std::vector<double> qs;
-    for (uint32_t i = 0; i < nt; i++) {
-        const auto it = uniq.emplace(std::string(reinterpret_cast<const char *>(&code[(size_t)i * Dp]), D),
-                                     (uint32_t)uniq.size());
-        of[i] = it.first->second;
-        if (it.second)
-            for (uint32_t d = 0; d < D; d++) qs.push_back(ctx->terms.v64[code[(size_t)i * Dp + d]]);
-    }
-    const uint32_t nu = (uint32_t)uniq.size();
-    std::vector<int64_t> ans(nu, -1);
-    std::vector<uint32_t> open;
-    auto replay = [&](const std::vector<uint32_t> &rows, std::vector<uint32_t> &left) {
-        left.clear();
-        tree.cert_clear();   // kp / known may have changed in place
-        for (uint32_t u : rows)
-            if ((ans[u] = tree.certified_search(&qs[(size_t)u * D], KAHAN_DELTA, kp.data(), known.data())) < 0)
-                left.push_back(u);
-    };
-    std::vector<uint32_t> all(nu);
-    for (uint32_t u = 0; u < nu; u++) all[u] = u;
-    replay(all, open);
-    std::vector<uint8_t> sel(Kc, 0);
-    uint32_t cells = 0, rounds = 0;
-    auto want = [&](uint32_t j, bool &any) {
-        for (uint32_t d = 0; d < D; d++)
-            if (!known[(size_t)j * D + d]) {
-                if (!sel[j % Kc]) cells++, any = true;
-                sel[j % Kc] = 1;
-                return;
-            }
-    };
-    // the reference's centroids of the selected cells (of the previous level's assignment)
-    auto sum_cells = [&]() -> qvq_status {
-        qvq_status s2;
-        if ((s2 = ensure_kahan(ctx, Kc)) != QVQ_OK) return s2;
-        HIPCHK(hipMemcpyAsync(ctx->d_kc_sel, sel.data(), Kc, hipMemcpyHostToDevice, ctx->stream));
-        HIPCHK(launch_kahan_centroids(ctx->stream, ctx->kw, ctx->d_codes, ctx->Dp, D, ctx->N, ctx->d_A_alt, Kc,
-                                      ctx->d_kc_cent, ctx->d_kc_split, ctx->d_kc_sel));
-        ctx->h_kc_split.resize((size_t)K * D);
-        HIPCHK(hipMemcpyAsync(ctx->h_kc_split.data(), ctx->d_kc_split, (size_t)K * D * 8, hipMemcpyDeviceToHost,
-                              ctx->stream));
-        if ((s2 = wait_stream(ctx)) != QVQ_OK) return s2;
-        for (uint32_t c = 0; c < Kc; c++)
-            if (sel[c])
-                for (uint32_t r : {c, c + Kc}) {
-                    std::memcpy(&kp[(size_t)r * D], &ctx->h_kc_split[(size_t)r * D], D * 8);
-                    std::memset(&known[(size_t)r * D], 1, D);
-                }
-        rounds++;
-        return QVQ_OK;
-    };
-    std::vector<uint32_t> cand, blame, left;
-    if (!open.empty()) {   // the candidates' cells
-        bool any = false;
-        for (uint32_t u : open) {
-            double dmin;
-            tree.near_set(&qs[(size_t)u * D], 1e-9, 1e-9, cand, dmin);
-            for (uint32_t j : cand) want(j, any);
-        }
-        if (any) {
-            if ((st = sum_cells()) != QVQ_OK) return st;
-            replay(open, left);
-            open.swap(left);
-        }
-    }
-    if (!open.empty()) {   // the cells of the points whose bits settle the open decisions
-        bool any = false;
-        for (uint32_t u : open) {
-            blame.clear();
-            tree.certify_blame(&qs[(size_t)u * D], KAHAN_DELTA, kp.data(), known.data(), blame);
-            for (uint32_t j : blame) want(j, any);
-        }
-        if (any) {
-            if ((st = sum_cells()) != QVQ_OK) return st;
-            replay(open, left);
-            open.swap(left);
-        }
-    }
-    if (!open.empty()) {
+    std::vector<uint32_t> of;
+    const uint32_t nu = distinct_rows(ctx, code.data(), Dp, nt, qs, of);
+    std::vector<int64_t> ans;
+    uint32_t open = 0, cells = 0, rounds = 0;
+    if ((st = certify_rows(ctx, *ctx->tree, ctx->cb_local.data(), K, ctx->d_A_alt, ctx->stream,
+                           [ctx] { return wait_stream(ctx); }, qs, nu, ans, open, cells, rounds)) != QVQ_OK)
+        return st;
+    if (open) {
         if (env_is("QVQ_KAHAN_DEBUG", "1"))
-            std::fprintf(stderr, "qvq kahan: K %u ties %u (%u distinct) cells %u: %zu rows not certified\n", K, nt, nu,
-                         cells, open.size());
+            std::fprintf(stderr, "qvq kahan: K %u ties %u (%u distinct) cells %u: %u rows not certified\n", K, nt, nu,
+                         cells, open);
         return QVQ_OK;
     }
     std::vector<uint32_t> &vals = ctx->cert_vals;   // outlives the copy (no wait)
@@ -1169,6 +1215,80 @@ qvq_status certify_kahan_ties(qvq_ctx *ctx, uint32_t K, unsigned nt, uint64_t *t
                      nu, cells, rounds);
     done = true;
     return QVQ_OK;
+}
+
+// The speculative check of one level (on the worker): the level's tie rows and their
+// speculative indices (exported with its codebook) against the reference's, by the certificate
+// over the level's tree.  status 0: all equal; 1: a row differs or stays open (qvq_lbg then
+// redoes the quantize with the synchronous Kahan levels).
+void verify_level(qvq_ctx *ctx, qvq_ctx::Verify &v) {
+    v.status = 1;
+    (void)hipSetDevice(ctx->dev);
+    volatile uint64_t *flag = ctx->h_ready;
+    while (*flag < v.seq)   // the export is released with the codebook's ready number
+        if (v.cancel.load(std::memory_order_relaxed)) return;
+    std::atomic_thread_fence(std::memory_order_acquire);
+    const uint32_t *tx = reinterpret_cast<const uint32_t *>(ctx->h_tx[v.par]);
+    const uint32_t nt = tx[0];
+    if (nt == 0) {
+        v.status = 0;
+        return;
+    }
+    if (nt > ctx->tx_cap || !v.tree || v.tree->cancelled() || v.K < 4) return;
+    const uint32_t Dp = ctx->Dp, words = 2 + Dp / 4;
+    std::vector<uint32_t> rec(tx + 2, tx + 2 + (size_t)nt * words);   // out of the mapped buffer at once
+    std::vector<double> qs;
+    std::vector<uint32_t> of;
+    const uint32_t nu =
+        distinct_rows(ctx, reinterpret_cast<const uint8_t *>(rec.data() + 2), (size_t)words * 4, nt, qs, of);
+    std::vector<int64_t> ans;
+    uint32_t open = 0, cells = 0, rounds = 0;
+    auto sync = [ctx]() -> qvq_status {
+        HIPCHK(hipStreamSynchronize(ctx->vstream));
+        return QVQ_OK;
+    };
+    if (hipStreamWaitEvent(ctx->vstream, v.ev, 0) != hipSuccess) return;
+    if (certify_rows(ctx, *v.tree, v.cb.data(), v.K, v.A_prev, ctx->vstream, sync, qs, nu, ans, open, cells,
+                     rounds) != QVQ_OK || open)
+        return;
+    for (uint32_t i = 0; i < nt; i++)
+        if ((uint32_t)ans[of[i]] != rec[(size_t)i * words + 1]) {
+            if (env_is("QVQ_KAHAN_DEBUG", "1"))
+                std::fprintf(stderr, "qvq kahan: K %u row %u: speculative %u, the reference %lld\n", v.K,
+                             rec[(size_t)i * words], rec[(size_t)i * words + 1], (long long)ans[of[i]]);
+            return;
+        }
+    if (env_is("QVQ_KAHAN_DEBUG", "1"))
+        std::fprintf(stderr, "qvq kahan: K %u ties %u (%u distinct) verified, cells summed %u in %u rounds\n", v.K,
+                     nt, nu, cells, rounds);
+    v.status = 0;
+}
+
+bool join_verify(qvq_ctx::Verify &v) {
+    if (!v.posted) return true;
+    while (!v.done.load(std::memory_order_acquire)) std::this_thread::yield();
+    v.posted = false;
+    v.tree.reset();
+    return v.status == 0;
+}
+
+// The speculative check's buffers (once per context): the third assignment buffer, the mapped
+// tie exports, the check's stream and events, and the Kahan work for the largest level.
+qvq_status ensure_speculation(qvq_ctx *ctx, uint32_t Kmax) {
+    if (!ctx->d_A_alt) HIPCHK(hipMalloc(&ctx->d_A_alt, ctx->N * 4));
+    if (!ctx->d_A3) HIPCHK(hipMalloc(&ctx->d_A3, ctx->N * 4));
+    if (!ctx->h_tx[0]) {
+        ctx->tx_cap = 65536;
+        const size_t bytes = 8 + (size_t)ctx->tx_cap * (8 + 64);
+        for (int i = 0; i < 2; i++) {
+            HIPCHK(hipHostMalloc(reinterpret_cast<void **>(&ctx->h_tx[i]), bytes, hipHostMallocMapped));
+            HIPCHK(hipHostGetDevicePointer(reinterpret_cast<void **>(&ctx->dh_tx[i]), ctx->h_tx[i], 0));
+        }
+    }
+    if (!ctx->vstream) HIPCHK(hipStreamCreateWithFlags(&ctx->vstream, hipStreamNonBlocking));
+    for (auto &v : ctx->ver)
+        if (!v.ev) HIPCHK(hipEventCreateWithFlags(&v.ev, hipEventDisableTiming));
+    return Kmax >= 4 ? ensure_kahan(ctx, Kmax / 2) : QVQ_OK;
 }
 
 // The ties of a level run with defer_ties (nt > 0 of them in d_ties): the reference's split
@@ -1313,6 +1433,8 @@ QVQ_API qvq_status qvq_create(int hip_device, qvq_ctx **out) {
 QVQ_API void qvq_destroy(qvq_ctx *ctx) {
     if (!ctx) return;
     join_tree_job(ctx, true);
+    for (auto &v : ctx->ver) v.cancel.store(true);
+    while (ctx->worker.pending.load(std::memory_order_acquire)) std::this_thread::yield();
     if (ctx->worker.th.joinable()) {
         {
             std::lock_guard<std::mutex> g(ctx->worker.m);
@@ -1347,6 +1469,11 @@ QVQ_API void qvq_destroy(qvq_ctx *ctx) {
             for (int j = 0; j < 4; j++) (void)hipEventDestroy(ctx->ev[l][j]);
     if (ctx->ev_end) (void)hipEventDestroy(ctx->ev_end);
     if (ctx->ev_sync) (void)hipEventDestroy(ctx->ev_sync);
+    for (auto &v : ctx->ver)
+        if (v.ev) (void)hipEventDestroy(v.ev);
+    for (uint8_t *h : ctx->h_tx)
+        if (h) (void)hipHostFree(h);
+    if (ctx->vstream) (void)hipStreamDestroy(ctx->vstream);
     if (ctx->stream) (void)hipStreamDestroy(ctx->stream);
     delete ctx;
 }
@@ -1637,6 +1764,29 @@ QVQ_API qvq_status qvq_lbg(qvq_ctx *ctx, uint32_t bits, double eps, double *code
         if ((st = all_reduce(ctx, ctx->d_hist + 256, 256, false)) != QVQ_OK) return st;
         hist = ctx->d_hist + 256;
     }
+    // Reference-bit (Kahan) levels, SCALED values on one rank (NORMAL values are integers: the
+    // exact sums are the reference's bits).  Speculative (default): each level runs as with exact
+    // sums, its ties answered by the exact-sum tree on the device, and the worker checks them
+    // against the reference's rule (the certificate) while the GPU runs the next
+    // level; a level whose check fails makes the quantize run again with synchronous Kahan
+    // levels (each waits for its ties to be answered by the reference's rule).  QVQ_SPECULATE=0:
+    // synchronous from the start.
+    const bool kahan = kahan_mode(ctx) && ctx->cs == QVQ_CS_SCALED;
+    static const bool spec_off = env_is("QVQ_SPECULATE", "0");
+    bool spec = kahan && !spec_off;
+    if (spec && (st = ensure_speculation(ctx, Kmax)) != QVQ_OK) return st;
+    if (kahan && !ctx->d_A_alt) HIPCHK(hipMalloc(&ctx->d_A_alt, ctx->N * 4));
+    struct JobGuard {   // no tree build or check outlives the call (an error return included)
+        qvq_ctx *c;
+        ~JobGuard() {
+            join_tree_job(c, true);
+            for (auto &v : c->ver) {
+                v.cancel.store(true);
+                join_verify(v);
+            }
+        }
+    } job_guard{ctx};
+    for (int attempt = 0;; attempt++) {
     HIPCHK(launch_mean_sums(ctx->stream, ctx->Dp, ctx->d_codes, ctx->N, ctx->D, ctx->d_plut, ctx->d_mean,
                             ctx->d_counters, N_COUNTERS, d_dist, hist, ctx->d_lut64));
     if ((st = all_reduce_sums(ctx, 1, ctx->d_mean, MEAN_COPIES)) != QVQ_OK) {
@@ -1654,8 +1804,9 @@ QVQ_API qvq_status qvq_lbg(qvq_ctx *ctx, uint32_t bits, double eps, double *code
     // the split a finalize writes: with deferred ties the level's own split must survive its
     // (speculative) finalize, so the next one goes to the other buffer and the two swap
     double *split_out = ctx->d_C64_split;
-    auto finalize = [&](uint32_t K, bool split, uint32_t copies = 1, const unsigned *gate = nullptr) {
-        if (split) ctx->seq++;
+    auto finalize = [&](uint32_t K, bool split, uint32_t copies = 1, const unsigned *gate = nullptr,
+                        const TieExport &tx = TieExport()) {
+        if (split || tx.out) ctx->seq++;
         const bool prune = split && use_prune(ctx, 2 * K);   // the next search's tile order
         ctx->perm_k = prune ? 2 * K : 0;
         return launch_finalize_prep(ctx->stream, K == 1 ? ctx->d_mean : ctx->d_sums, K, ctx->D, ctx->Dp, T.R, T.bias,
@@ -1663,28 +1814,34 @@ QVQ_API qvq_status qvq_lbg(qvq_ctx *ctx, uint32_t bits, double eps, double *code
                                     ctx->d_C64_cent, split, split_out, pad32(2 * K), T.mu, T.sx, ctx->mf_t,
                                     ctx->d_C32, ctx->d_rows, ctx->d_E32, split ? ctx->dh_cb : nullptr, d_dist + 8,
                                     dist_done,
-                                    split ? nullptr : d_dist + 2, split ? ctx->dh_ready : nullptr, ctx->seq,
-                                    K == 1, K == 1 ? MEAN_COPIES : copies,
+                                    split ? nullptr : d_dist + 2, (split || tx.out) ? ctx->dh_ready : nullptr,
+                                    ctx->seq, K == 1, K == 1 ? MEAN_COPIES : copies,
                                     prune ? ctx->d_perm : nullptr, prune ? ctx->d_tint : nullptr, K == 1 ? 0 : 1,
                                     copies > 1 ? sums_cap_stride(ctx) : 0,
-                                    gate);
+                                    gate, tx);
     };
     HIPCHK(finalize(1, bits > 0));
     // with bits >= 1 the first search writes every row's index
     if (bits == 0) HIPCHK(hipMemsetAsync(ctx->d_A, 0, ctx->N * 4, ctx->stream));
 
-    const bool kahan = kahan_mode(ctx);
-    if (kahan && !ctx->d_A_alt) HIPCHK(hipMalloc(&ctx->d_A_alt, ctx->N * 4));
-    struct JobGuard {   // no tree build outlives the call (an error return included)
-        qvq_ctx *c;
-        ~JobGuard() { join_tree_job(c, true); }
-    } job_guard{ctx};
-    if (kahan) split_out = ctx->d_C64_split_alt;
+    const bool sync_kahan = kahan && !spec;
+    if (sync_kahan) split_out = ctx->d_C64_split_alt;
+    uint32_t *const abuf[3] = {ctx->d_A, ctx->d_A_alt, ctx->d_A3};
+    bool spec_failed = false;
     for (uint32_t lvl = 1; lvl <= bits; lvl++) {
         const uint32_t K = 1u << lvl;
         const int slot = (int)lvl - 1;
-        if (kahan) std::swap(ctx->d_A, ctx->d_A_alt);   // d_A_alt: the previous level's assignment
-        if ((st = run_level(ctx, K, slot, true, ctx->h_cb, ctx->seq, kahan)) != QVQ_OK) return st;
+        if (spec) {   // A_L in abuf[L % 3]: level L's check reads A_{L-1} until level L + 2 starts
+            if (lvl >= 3 && !join_verify(ctx->ver[lvl & 1])) {
+                spec_failed = true;
+                break;
+            }
+            ctx->d_A = abuf[lvl % 3];
+            ctx->d_A_alt = abuf[(lvl + 2) % 3];
+        } else if (kahan) {
+            std::swap(ctx->d_A, ctx->d_A_alt);   // d_A_alt: the previous level's assignment
+        }
+        if ((st = run_level(ctx, K, slot, true, ctx->h_cb, ctx->seq, sync_kahan)) != QVQ_OK) return st;
         const bool split = lvl < bits;
         {
             const uint32_t copies = ctx->sums_copies;
@@ -1707,9 +1864,38 @@ QVQ_API qvq_status qvq_lbg(qvq_ctx *ctx, uint32_t bits, double eps, double *code
                 ctx->pub = PubArgs();
             }
             if ((st = all_reduce_sums(ctx, K)) != QVQ_OK) return st;
-            HIPCHK(finalize(K, split, copies, copies > 1 ? tcnt : nullptr));
+            TieExport tx;
+            if (spec) {   // the level's tie rows and their indices go out with its codebook
+                tx.rows = ctx->d_ties;
+                tx.cnt = tcnt;
+                tx.A = ctx->d_A;
+                tx.codes = ctx->d_codes;
+                tx.cap = ctx->tx_cap;
+                tx.out = ctx->dh_tx[lvl & 1];
+            }
+            HIPCHK(finalize(K, split, copies, copies > 1 ? tcnt : nullptr, tx));
             if (copies > 1) ctx->sums1_dirty = false;
-            if (kahan) {   // the level's ties (published after its recheck)
+            if (spec) {   // the check of this level, on the worker
+                qvq_ctx::Verify &v = ctx->ver[lvl & 1];
+                v.posted = true;
+                v.done.store(false);
+                v.cancel.store(false);
+                v.status = 1;
+                v.K = K;
+                v.seq = ctx->seq;
+                v.par = (int)(lvl & 1);
+                v.A_prev = lvl >= 2 ? ctx->d_A_alt : nullptr;
+                v.tree = std::move(ctx->tree);
+                v.cb = std::move(ctx->cb_local);
+                ctx->cb_local.clear();
+                HIPCHK(hipEventRecord(v.ev, ctx->stream));
+                qvq_ctx::Verify *vp = &v;
+                post_job(ctx, [ctx, vp] {
+                    verify_level(ctx, *vp);
+                    vp->done.store(true, std::memory_order_release);
+                });
+            }
+            if (sync_kahan) {   // the level's ties (published after its recheck)
                 if ((st = wait_flag(ctx, ctx->h_ready + 1, ctx->pub_seq)) != QVQ_OK) return st;
                 const unsigned nt = (unsigned)(uint32_t)ctx->h_ready[2];
                 join_tree_job(ctx, nt == 0);   // the level's tree: needed for ties only
@@ -1726,6 +1912,26 @@ QVQ_API qvq_status qvq_lbg(qvq_ctx *ctx, uint32_t bits, double eps, double *code
                 }
             }
         }
+    }
+    if (spec && !spec_failed)
+        for (uint32_t l : {bits - 1, bits})
+            if (l >= 1 && !join_verify(ctx->ver[l & 1])) spec_failed = true;
+    if (!spec_failed) break;
+    // a check failed: every check joined, the stream drained, then the quantize again with
+    // synchronous Kahan levels
+    for (auto &v : ctx->ver) {
+        v.cancel.store(true);
+        join_verify(v);
+    }
+    if ((st = wait_stream(ctx)) != QVQ_OK) return st;
+    if (ctx->sums1_dirty) {
+        HIPCHK(hipMemsetAsync(ctx->d_sums, 0, ctx->sums_bytes, ctx->stream));
+        ctx->sums1_dirty = false;
+    }
+    ctx->kd_pend = false;
+    ctx->pub = PubArgs();
+    ctx->tm.kahan_redo++;
+    spec = false;
     }
     // Returned distortion: updateDistortion after the last fix (src/Quantizer.cpp:9-22,103),
     // from the sums of the final assignment (finalize_prep_kernel without split).

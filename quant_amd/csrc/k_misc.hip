@@ -975,6 +975,7 @@ struct FinArgs {
     uint32_t *perm;         // split: the next search's tile order (prune_order), or null
     int32_t *tint;
     float *qproj;           // with perm: the split code vectors' projections (finalize_split_item)
+    TieExport ties;         // out != null: the level's tie rows to mapped memory (TieExport)
 };
 
 // A split row j (< 2K: child of code vector j mod K, from that code vector's sums hs, ls, cnt of
@@ -1187,7 +1188,7 @@ __device__ void finalize_block_done(const FinArgs &a, double term, double *red, 
     // host_cb: every wave's mapped stores complete before the barrier, and thread 0's
     // system-scope fence below releases them with the block's count (MI355X guide's
     // producer pattern: one fence per block, not one per thread)
-    if (a.host_cb) __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (a.host_cb || a.ties.out) __asm__ volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (red)
         for (int w = (int)blockDim.x / 2; w > 0; w >>= 1) {
@@ -1196,7 +1197,7 @@ __device__ void finalize_block_done(const FinArgs &a, double term, double *red, 
         }
     if (threadIdx.x == 0) {
         if (red) dist_part[blockIdx.x] = red[0];
-        if (a.host_cb) __threadfence_system();
+        if (a.host_cb || a.ties.out) __threadfence_system();
         else __threadfence();
         last = atomicAdd(done, 1u) == gridDim.x - 1;
     }
@@ -1234,6 +1235,18 @@ __global__ __launch_bounds__(256) void finalize_prep_kernel(FinArgs a, double *_
     const uint32_t per = 256 / L, n = fin_rows(a);
     double term = 0.0;
     for (uint32_t j0 = blockIdx.x * per; j0 < n; j0 += gridDim.x * per) term += finalize_item(a, j0 + r, d, L);
+    if (a.ties.out) {   // the tie rows, a thread per 4 bytes of a row record
+        const TieExport &t = a.ties;
+        const uint32_t nt = *t.cnt, m = min(nt, t.cap), words = 2 + a.Dp / 4;
+        uint32_t *o = reinterpret_cast<uint32_t *>(t.out);
+        if (blockIdx.x == 0 && threadIdx.x == 0) o[0] = nt;
+        for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < (uint64_t)m * words;
+             i += (uint64_t)gridDim.x * blockDim.x) {
+            const uint32_t k = (uint32_t)(i / words), w = (uint32_t)(i % words), row = t.rows[k];
+            o[2 + i] = w == 0 ? row
+                              : (w == 1 ? t.A[row] : reinterpret_cast<const uint32_t *>(t.codes + (uint64_t)row * a.Dp)[w - 2]);
+        }
+    }
     if (!done) return;
     __shared__ double red[256];
     // (the distortion's block tree only on the level that returns it: 8 barriers fewer elsewhere)
@@ -1271,6 +1284,7 @@ static FinArgs fin_args(const uint64_t *sums, uint32_t K, uint32_t D, uint32_t D
     a.perm = nullptr;
     a.tint = nullptr;
     a.qproj = nullptr;
+    a.ties = TieExport();
     return a;
 }
 
@@ -1279,8 +1293,11 @@ hipError_t launch_finalize_prep(hipStream_t s, const uint64_t *sums, uint32_t K,
                                 double mu, double sx, int t, float *C32, _Float16 *cb_rows, float *E32,
                                 double *host_cb, double *dist_part, unsigned *done, double *dist_out, uint64_t *ready,
                                 uint64_t seq, bool zero_sums, uint32_t ncopy, uint32_t *perm, int32_t *tint,
-                                uint32_t zero_skip, uint64_t copy_stride, const unsigned *copy_gate) {
+                                uint32_t zero_skip, uint64_t copy_stride, const unsigned *copy_gate,
+                                const TieExport &ties) {
     if (D == 0 || D > 64) return hipErrorInvalidValue;
+    if (ties.out && (!done || !ready || !ties.rows || !ties.cnt || !ties.A || !ties.codes || (Dp & 3)))
+        return hipErrorInvalidValue;   // released with the ready flag
     if (zero_sums && !done) return hipErrorInvalidValue;   // the clearing is the last block's
     const uint32_t L = D <= 16 ? 16 : (D <= 32 ? 32 : 64);
     const uint32_t n = split ? std::max(2 * K, Kpad_next) : K;
@@ -1289,6 +1306,7 @@ hipError_t launch_finalize_prep(hipStream_t s, const uint64_t *sums, uint32_t K,
                          E32, host_cb, dist_out != nullptr);
     a.ncopy = ncopy ? ncopy : 1;
     a.gate = copy_gate;
+    a.ties = ties;
     if (copy_stride) {
         if (copy_stride < 2 * (uint64_t)K * D + K) return hipErrorInvalidValue;
         a.cstride = copy_stride;
