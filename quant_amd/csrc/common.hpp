@@ -341,6 +341,7 @@ struct TieExport {
     const uint32_t *A = nullptr;
     const uint8_t *codes = nullptr;
     uint32_t cap = 0;
+    uint64_t n_rows = 0;   // rows in codes / A (a row index past it is written as ~0, nothing read)
     uint8_t *out = nullptr;
 };
 hipError_t launch_finalize_prep(hipStream_t s, const uint64_t *sums, uint32_t K, uint32_t D, uint32_t Dp, int64_t R,

@@ -1237,6 +1237,8 @@ void verify_level(qvq_ctx *ctx, qvq_ctx::Verify &v) {
     if (nt > ctx->tx_cap || !v.tree || v.tree->cancelled() || v.K < 4) return;
     const uint32_t Dp = ctx->Dp, words = 2 + Dp / 4;
     std::vector<uint32_t> rec(tx + 2, tx + 2 + (size_t)nt * words);   // out of the mapped buffer at once
+    for (uint32_t i = 0; i < nt; i++)
+        if (rec[(size_t)i * words] >= ctx->N || rec[(size_t)i * words + 1] >= v.K) return;
     std::vector<double> qs;
     std::vector<uint32_t> of;
     const uint32_t nu =
@@ -1838,6 +1840,7 @@ QVQ_API qvq_status qvq_lbg(qvq_ctx *ctx, uint32_t bits, double eps, double *code
             }
             ctx->d_A = abuf[lvl % 3];
             ctx->d_A_alt = abuf[(lvl + 2) % 3];
+            ctx->d_A3 = abuf[(lvl + 1) % 3];   // the three stay distinct across calls
         } else if (kahan) {
             std::swap(ctx->d_A, ctx->d_A_alt);   // d_A_alt: the previous level's assignment
         }
@@ -1871,6 +1874,7 @@ QVQ_API qvq_status qvq_lbg(qvq_ctx *ctx, uint32_t bits, double eps, double *code
                 tx.A = ctx->d_A;
                 tx.codes = ctx->d_codes;
                 tx.cap = ctx->tx_cap;
+                tx.n_rows = ctx->N;
                 tx.out = ctx->dh_tx[lvl & 1];
             }
             HIPCHK(finalize(K, split, copies, copies > 1 ? tcnt : nullptr, tx));

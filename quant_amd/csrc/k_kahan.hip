@@ -55,7 +55,7 @@ __global__ __launch_bounds__(64) void ks_hist_kernel(const uint32_t *__restrict_
     const uint64_t r0 = (uint64_t)blockIdx.x * SROWS, r1 = min(N, r0 + SROWS);
     for (uint64_t r = r0 + threadIdx.x; r < r1; r += 64) {
         const uint32_t a = A[r];
-        if (!sel || sel[a]) atomicAdd(&h[a], 1u);
+        if (a < K && (!sel || sel[a])) atomicAdd(&h[a], 1u);
     }
     __syncthreads();
     for (uint32_t i = threadIdx.x; i < K; i += 64) hist[(uint64_t)i * G + blockIdx.x] = h[i];
@@ -150,7 +150,7 @@ __global__ __launch_bounds__(64) void ks_scatter_kernel(const uint8_t *__restric
     for (uint64_t base = r0; base < r1; base += 64) {
         const uint64_t r = base + lane;
         uint32_t a = r < r1 ? A[r] : NOKEY;
-        if (sel && a != NOKEY && !sel[a]) a = NOKEY;   // a row of a cell not asked for
+        if (a >= K || (sel && !sel[a])) a = NOKEY;   // a row of a cell not asked for
         if (__ballot(a != NOKEY) == 0) continue;      // (wave-uniform)
         uint32_t w[W];
         const uint32_t *src = reinterpret_cast<const uint32_t *>(codes + (a != NOKEY ? r : r0) * DP);

@@ -1243,6 +1243,10 @@ __global__ __launch_bounds__(256) void finalize_prep_kernel(FinArgs a, double *_
         for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < (uint64_t)m * words;
              i += (uint64_t)gridDim.x * blockDim.x) {
             const uint32_t k = (uint32_t)(i / words), w = (uint32_t)(i % words), row = t.rows[k];
+            if (row >= t.n_rows) {   // (never: the recheck lists rows)
+                o[2 + i] = ~0u;
+                continue;
+            }
             o[2 + i] = w == 0 ? row
                               : (w == 1 ? t.A[row] : reinterpret_cast<const uint32_t *>(t.codes + (uint64_t)row * a.Dp)[w - 2]);
         }
@@ -1296,7 +1300,7 @@ hipError_t launch_finalize_prep(hipStream_t s, const uint64_t *sums, uint32_t K,
                                 uint32_t zero_skip, uint64_t copy_stride, const unsigned *copy_gate,
                                 const TieExport &ties) {
     if (D == 0 || D > 64) return hipErrorInvalidValue;
-    if (ties.out && (!done || !ready || !ties.rows || !ties.cnt || !ties.A || !ties.codes || (Dp & 3)))
+    if (ties.out && (!done || !ready || !ties.rows || !ties.cnt || !ties.A || !ties.codes || (Dp & 3) || !ties.n_rows))
         return hipErrorInvalidValue;   // released with the ready flag
     if (zero_sums && !done) return hipErrorInvalidValue;   // the clearing is the last block's
     const uint32_t L = D <= 16 ? 16 : (D <= 32 ? 32 : 64);
