@@ -413,9 +413,10 @@ struct KahanWork {
 // C [K][D] = the reference's centroids of assignment A (nullptr: K = 1, the mean of every row):
 // Kahan sums in ascending row order times fl(1/n), empty cells 0, bit for bit (SCALED byte
 // values; w.tab from KahanWork::make_tab).  With split_out also the split [2K][D] (x1.2 | x0.8).
-// sel (K bytes, device; nullptr: every cell): only the cells it marks are summed (the others
-// come out 0), and the sort skips the other rows' bytes.
+// sel (n_sel entries, device; nullptr: every cell): the selected cells only, compacted: sel[a] =
+// slot + 1 for a selected cell a, 0 otherwise; K is then the number of slots, and C / split_out
+// rows are slots (split_out: slot | K + slot).  The sort skips the other rows' bytes.
 hipError_t launch_kahan_centroids(hipStream_t s, const KahanWork &w, const uint8_t *codes, uint32_t Dp, uint32_t D,
                                   uint64_t N, const uint32_t *A, uint32_t K, double *C, double *split_out,
-                                  const uint8_t *sel = nullptr);
+                                  const uint32_t *sel = nullptr, uint32_t n_sel = 0);
 }  // namespace qvq

@@ -114,7 +114,7 @@ struct qvq_ctx {
     double *d_kc_cent = nullptr, *d_kc_split = nullptr;   // Kahan centroids [K/2][D], their split [K][D]
     uint32_t kc_kcap = 0;
     std::vector<double> h_kc_split;   // host copy of the split for the tree build
-    uint8_t *d_kc_sel = nullptr;      // [K/2] the cells a tie certificate needs the reference's sums of
+    uint32_t *d_kc_sel = nullptr;     // [K/2] slot + 1 of the cells a tie certificate sums (0: not summed)
     std::vector<double> cert_kp;      // the reference's split where known (tie certificate)
     std::vector<uint8_t> cert_known;
     std::vector<uint32_t> cert_vals;  // the certified answers (host side of their upload)
@@ -618,7 +618,7 @@ qvq_status ensure_kahan(qvq_ctx *ctx, uint32_t Kc) {
         dfree(ctx->d_kc_sel);
         HIPCHK(hipMalloc(&ctx->d_kc_cent, (uint64_t)Kc * D * 8));
         HIPCHK(hipMalloc(&ctx->d_kc_split, 2ull * Kc * D * 8));
-        HIPCHK(hipMalloc(&ctx->d_kc_sel, Kc));
+        HIPCHK(hipMalloc(&ctx->d_kc_sel, (uint64_t)Kc * 4));
         ctx->kc_kcap = Kc;
     }
     if (w.n_cap == N && w.k_cap >= Kc && w.d_cap == D) return QVQ_OK;
@@ -1106,22 +1106,33 @@ qvq_status certify_rows(qvq_ctx *ctx, const RefKDTree &tree, const double *cb, u
                 return;
             }
     };
-    // the reference's centroids of the selected cells (of the previous level's assignment)
+    // the reference's centroids of the selected cells (of the previous level's assignment),
+    // compacted to slots: the split rows come back as slot | S + slot
+    std::vector<uint32_t> slot_of, cell_of;
     auto sum_cells = [&]() -> qvq_status {
         qvq_status s2;
         if ((s2 = ensure_kahan(ctx, Kc)) != QVQ_OK) return s2;
-        HIPCHK(hipMemcpyAsync(ctx->d_kc_sel, sel.data(), Kc, hipMemcpyHostToDevice, stream));
-        HIPCHK(launch_kahan_centroids(stream, ctx->kw, ctx->d_codes, ctx->Dp, D, ctx->N, A_prev, Kc, ctx->d_kc_cent,
-                                      ctx->d_kc_split, ctx->d_kc_sel));
-        ctx->h_kc_split.resize((size_t)K * D);
-        HIPCHK(hipMemcpyAsync(ctx->h_kc_split.data(), ctx->d_kc_split, (size_t)K * D * 8, hipMemcpyDeviceToHost, stream));
-        if ((s2 = sync()) != QVQ_OK) return s2;
+        slot_of.assign(Kc, 0);
+        cell_of.clear();
         for (uint32_t c = 0; c < Kc; c++)
-            if (sel[c])
-                for (uint32_t r : {c, c + Kc}) {
-                    std::memcpy(&kp[(size_t)r * D], &ctx->h_kc_split[(size_t)r * D], D * 8);
-                    std::memset(&known[(size_t)r * D], 1, D);
-                }
+            if (sel[c]) {
+                cell_of.push_back(c);
+                slot_of[c] = (uint32_t)cell_of.size();
+            }
+        const uint32_t S = (uint32_t)cell_of.size();
+        HIPCHK(hipMemcpyAsync(ctx->d_kc_sel, slot_of.data(), (size_t)Kc * 4, hipMemcpyHostToDevice, stream));
+        HIPCHK(launch_kahan_centroids(stream, ctx->kw, ctx->d_codes, ctx->Dp, D, ctx->N, A_prev, S, ctx->d_kc_cent,
+                                      ctx->d_kc_split, ctx->d_kc_sel, Kc));
+        ctx->h_kc_split.resize((size_t)2 * S * D);
+        HIPCHK(hipMemcpyAsync(ctx->h_kc_split.data(), ctx->d_kc_split, (size_t)2 * S * D * 8, hipMemcpyDeviceToHost,
+                              stream));
+        if ((s2 = sync()) != QVQ_OK) return s2;
+        for (uint32_t t = 0; t < S; t++)
+            for (uint32_t h = 0; h < 2; h++) {
+                const uint32_t r = cell_of[t] + h * Kc;
+                std::memcpy(&kp[(size_t)r * D], &ctx->h_kc_split[((size_t)h * S + t) * D], D * 8);
+                std::memset(&known[(size_t)r * D], 1, D);
+            }
         rounds++;
         return QVQ_OK;
     };
@@ -1249,7 +1260,7 @@ void verify_level(qvq_ctx *ctx, qvq_ctx::Verify &v) {
         HIPCHK(hipStreamSynchronize(ctx->vstream));
         return QVQ_OK;
     };
-    if (hipStreamWaitEvent(ctx->vstream, v.ev, 0) != hipSuccess) return;
+    // (A_prev is complete: the GPU wrote the flag seen above after the levels that made it)
     if (certify_rows(ctx, *v.tree, v.cb.data(), v.K, v.A_prev, ctx->vstream, sync, qs, nu, ans, open, cells,
                      rounds) != QVQ_OK || open)
         return;
@@ -1788,7 +1799,28 @@ QVQ_API qvq_status qvq_lbg(qvq_ctx *ctx, uint32_t bits, double eps, double *code
             }
         }
     } job_guard{ctx};
+    // distortion inputs, per-level counters and the codebook go to mapped pinned memory in one
+    // launch (the mapped split-codebook buffer is free once the last tree is built); the copy's
+    // own flag ends the wait: polling it wakes the host at once (a stream synchronize costs tens
+    // of us of wake-up), and the wait is bounded (wait.hpp), so a peer rank that dies inside a
+    // level's all-reduce ends this call with QVQ_ECOMM
+    bool out_enqueued = false;
+    uint64_t out_seq = 0;
+    auto enqueue_out = [&]() -> qvq_status {
+        if (ctx->timing_level == -1) HIPCHK(hipEventRecord(ctx->ev_end, ctx->stream));   // each record idles the GPU ~6 us
+        uint8_t *dh_small = reinterpret_cast<uint8_t *>(ctx->dh_ready) + 64;
+        static_assert(3 * sizeof(double) + 2 * 33 * sizeof(unsigned) <= 1024 - 64, "small results exceed the mapped area");
+        const uint64_t cb_bytes = codebook ? (uint64_t)Kmax * ctx->D * 8 : 0;
+        uint64_t *done = reinterpret_cast<uint64_t *>(dh_small + (1024 - 64 - 8));
+        out_seq = ++ctx->out_seq;
+        HIPCHK(launch_copy_out(ctx->stream, ctx->d_dist_part, dh_small, 3 * sizeof(double), ctx->d_counters,
+                               dh_small + 3 * sizeof(double), 2 * 33 * sizeof(unsigned), ctx->d_C64_cent, ctx->dh_cb,
+                               cb_bytes, done, out_seq, ctx->d_counters + 2 * 33 + 1));
+        out_enqueued = true;
+        return QVQ_OK;
+    };
     for (int attempt = 0;; attempt++) {
+    out_enqueued = false;
     HIPCHK(launch_mean_sums(ctx->stream, ctx->Dp, ctx->d_codes, ctx->N, ctx->D, ctx->d_plut, ctx->d_mean,
                             ctx->d_counters, N_COUNTERS, d_dist, hist, ctx->d_lut64));
     if ((st = all_reduce_sums(ctx, 1, ctx->d_mean, MEAN_COPIES)) != QVQ_OK) {
@@ -1892,7 +1924,6 @@ QVQ_API qvq_status qvq_lbg(qvq_ctx *ctx, uint32_t bits, double eps, double *code
                 v.tree = std::move(ctx->tree);
                 v.cb = std::move(ctx->cb_local);
                 ctx->cb_local.clear();
-                HIPCHK(hipEventRecord(v.ev, ctx->stream));
                 qvq_ctx::Verify *vp = &v;
                 post_job(ctx, [ctx, vp] {
                     verify_level(ctx, *vp);
@@ -1917,9 +1948,11 @@ QVQ_API qvq_status qvq_lbg(qvq_ctx *ctx, uint32_t bits, double eps, double *code
             }
         }
     }
-    if (spec && !spec_failed)
+    if (spec && !spec_failed) {   // the results' copy overlaps the last checks
+        if ((st = enqueue_out()) != QVQ_OK) return st;
         for (uint32_t l : {bits - 1, bits})
             if (l >= 1 && !join_verify(ctx->ver[l & 1])) spec_failed = true;
+    }
     if (!spec_failed) break;
     // a check failed: every check joined, the stream drained, then the quantize again with
     // synchronous Kahan levels
@@ -1939,25 +1972,14 @@ QVQ_API qvq_status qvq_lbg(qvq_ctx *ctx, uint32_t bits, double eps, double *code
     }
     // Returned distortion: updateDistortion after the last fix (src/Quantizer.cpp:9-22,103),
     // from the sums of the final assignment (finalize_prep_kernel without split).
-    if (ctx->timing_level == -1) HIPCHK(hipEventRecord(ctx->ev_end, ctx->stream));   // each record idles the GPU ~6 us
-    // distortion inputs, per-level counters and the codebook go to mapped pinned memory in one
-    // launch (the mapped split-codebook buffer is free once the last tree is built)
+    // (enqueue_out: before the last checks are joined when speculating)
+    if (!out_enqueued && (st = enqueue_out()) != QVQ_OK) return st;
     double dres[3];
     unsigned stats[2 * 33];
     {
         uint8_t *h_small = reinterpret_cast<uint8_t *>(ctx->h_ready) + 64;
-        uint8_t *dh_small = reinterpret_cast<uint8_t *>(ctx->dh_ready) + 64;
-        static_assert(sizeof(dres) + sizeof(stats) <= 1024 - 64, "small results exceed the mapped area");
         const uint64_t cb_bytes = codebook ? (uint64_t)Kmax * ctx->D * 8 : 0;
-        // the copy's own flag ends the wait: polling it wakes the host at once (a stream
-        // synchronize costs tens of us of wake-up), and the wait is bounded (wait.hpp), so a
-        // peer rank that dies inside a level's all-reduce ends this call with QVQ_ECOMM
-        uint64_t *done = reinterpret_cast<uint64_t *>(dh_small + (1024 - 64 - 8));
-        const uint64_t seq = ++ctx->out_seq;
-        HIPCHK(launch_copy_out(ctx->stream, d_dist, dh_small, sizeof(dres), ctx->d_counters, dh_small + sizeof(dres),
-                               sizeof(stats), ctx->d_C64_cent, ctx->dh_cb, cb_bytes, done, seq,
-                               ctx->d_counters + 2 * 33 + 1));
-        qvq_status ws = wait_flag(ctx, reinterpret_cast<volatile uint64_t *>(h_small + (1024 - 64 - 8)), seq);
+        qvq_status ws = wait_flag(ctx, reinterpret_cast<volatile uint64_t *>(h_small + (1024 - 64 - 8)), out_seq);
         if (ws != QVQ_OK) return ws;
         if (assign)   // every collective of this call is complete: a plain copy
             HIPCHK(host_copy(ctx, assign, ctx->d_A, ctx->N * 4, hipMemcpyDeviceToHost));

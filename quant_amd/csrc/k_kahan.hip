@@ -46,16 +46,23 @@ __device__ inline void wave_sync() {
 
 // ---- 1. stable counting sort, writing the planes ----------------------------------------------
 // hist[k][g]: rows of 4096-row block g with index k (transposed: a key's column is contiguous)
+// a row's key: its cell, or with sel its cell's slot; ~0u for a row not summed
+__device__ inline uint32_t ks_key(uint32_t a, uint32_t K, const uint32_t *__restrict__ sel, uint32_t n_sel) {
+    if (!sel) return a < K ? a : ~0u;
+    const uint32_t s = a < n_sel ? sel[a] : 0u;
+    return s ? s - 1 : ~0u;
+}
+
 __global__ __launch_bounds__(64) void ks_hist_kernel(const uint32_t *__restrict__ A, uint64_t N, uint32_t K,
                                                     uint32_t G, uint32_t *__restrict__ hist,
-                                                    const uint8_t *__restrict__ sel) {
+                                                    const uint32_t *__restrict__ sel, uint32_t n_sel) {
     extern __shared__ uint32_t h[];
     for (uint32_t i = threadIdx.x; i < K; i += 64) h[i] = 0;
     __syncthreads();
     const uint64_t r0 = (uint64_t)blockIdx.x * SROWS, r1 = min(N, r0 + SROWS);
     for (uint64_t r = r0 + threadIdx.x; r < r1; r += 64) {
-        const uint32_t a = A[r];
-        if (a < K && (!sel || sel[a])) atomicAdd(&h[a], 1u);
+        const uint32_t a = ks_key(A[r], K, sel, n_sel);
+        if (a != ~0u) atomicAdd(&h[a], 1u);
     }
     __syncthreads();
     for (uint32_t i = threadIdx.x; i < K; i += 64) hist[(uint64_t)i * G + blockIdx.x] = h[i];
@@ -139,7 +146,8 @@ __global__ __launch_bounds__(64) void ks_scatter_kernel(const uint8_t *__restric
                                                        uint64_t N, uint32_t K, uint32_t D, uint32_t G,
                                                        const uint32_t *__restrict__ hist,
                                                        const uint32_t *__restrict__ koff, uint64_t PL,
-                                                       uint8_t *__restrict__ planes, const uint8_t *__restrict__ sel) {
+                                                       uint8_t *__restrict__ planes, const uint32_t *__restrict__ sel,
+                                                       uint32_t n_sel) {
     constexpr int W = DP / 4;
     extern __shared__ uint32_t cur[];
     for (uint32_t i = threadIdx.x; i < K; i += 64) cur[i] = koff[i] + hist[(uint64_t)i * G + blockIdx.x];
@@ -149,8 +157,8 @@ __global__ __launch_bounds__(64) void ks_scatter_kernel(const uint8_t *__restric
     const uint64_t r0 = (uint64_t)blockIdx.x * SROWS, r1 = min(N, r0 + SROWS);
     for (uint64_t base = r0; base < r1; base += 64) {
         const uint64_t r = base + lane;
-        uint32_t a = r < r1 ? A[r] : NOKEY;
-        if (a >= K || (sel && !sel[a])) a = NOKEY;   // a row of a cell not asked for
+        uint32_t a = r < r1 ? ks_key(A[r], K, sel, n_sel) : ~0u;
+        if (a == ~0u) a = NOKEY;   // a row of a cell not asked for
         if (__ballot(a != NOKEY) == 0) continue;      // (wave-uniform)
         uint32_t w[W];
         const uint32_t *src = reinterpret_cast<const uint32_t *>(codes + (a != NOKEY ? r : r0) * DP);
@@ -600,12 +608,12 @@ uint32_t KahanWork::sort_blocks(uint64_t N) { return (uint32_t)((N + SROWS - 1) 
 
 hipError_t launch_kahan_centroids(hipStream_t s, const KahanWork &w, const uint8_t *codes, uint32_t Dp, uint32_t D,
                                   uint64_t N, const uint32_t *A, uint32_t K, double *C, double *split_out,
-                                  const uint8_t *sel) {
+                                  const uint32_t *sel, uint32_t n_sel) {
     if (N == 0 || N > 0xFFFFFFFFull || D == 0 || K == 0 || D > Dp || Dp > 64 || (Dp & 3)) return hipErrorInvalidValue;
     const uint32_t G = KahanWork::sort_blocks(N);
     const uint64_t PL = KahanWork::plane_len(N);
     if (A) {
-        hipLaunchKernelGGL(ks_hist_kernel, dim3(G), dim3(64), K * 4, s, A, N, K, G, w.hist, sel);
+        hipLaunchKernelGGL(ks_hist_kernel, dim3(G), dim3(64), K * 4, s, A, N, K, G, w.hist, sel, n_sel);
         hipLaunchKernelGGL(ks_colscan_kernel, dim3(K), dim3(256), 0, s, w.hist, G, w.tot);
     } else {
         if (K != 1) return hipErrorInvalidValue;
@@ -618,7 +626,7 @@ hipError_t launch_kahan_centroids(hipStream_t s, const KahanWork &w, const uint8
     case DPV:                                                                                                      \
         if (A)                                                                                                     \
             hipLaunchKernelGGL(ks_scatter_kernel<DPV>, dim3(G), dim3(64), K * 4, s, codes, A, N, K, D, G, w.hist,  \
-                               w.koff, PL, w.planes, sel);                                                         \
+                               w.koff, PL, w.planes, sel, n_sel);                                                  \
         else                                                                                                       \
             hipLaunchKernelGGL(ks_transpose_kernel<DPV>, dim3((uint32_t)((N + 1023) / 1024)), dim3(256), 0, s,     \
                                codes, N, D, PL, w.planes);                                                         \
