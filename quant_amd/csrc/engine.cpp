@@ -168,6 +168,17 @@ struct qvq_ctx {
         bool stop = false;
         std::atomic<int> pending{0};
     } worker;
+    // helpers of the worker for the certificate's replays (persistent: their per-thread replay
+    // caches stay warm); pool_run forks fn over them and the calling thread
+    struct Pool {
+        std::vector<std::thread> th;
+        std::mutex m;
+        std::condition_variable cv, idle;
+        std::function<void(uint32_t)> fn;
+        uint64_t epoch = 0;
+        uint32_t want = 0, busy = 0;
+        bool stop = false;
+    } pool;
     // the speculative Kahan check (qvq_lbg): level L's ties verified on the worker while the GPU
     // runs level L + 1; three assignment buffers keep A_{L-1} (the check's cells) until L + 2
     uint32_t *d_A3 = nullptr;
@@ -1064,6 +1075,45 @@ constexpr double KAHAN_DELTA = 0x1p-49;
 // the reference's bits; the selected cells only), the replay again; for rows still open, the
 // cells of the points a collecting replay blames, and once more.  done = false, nothing
 // changed, when a row stays open: the caller then computes the whole split and its tree.
+uint32_t cert_threads();
+
+// fn(t) for t = 0 .. n - 1: t = 0 on the calling thread, the others on the pool's threads.
+void pool_run(qvq_ctx *ctx, uint32_t n, const std::function<void(uint32_t)> &fn) {
+    qvq_ctx::Pool &P = ctx->pool;
+    if (n <= 1) {
+        fn(0);
+        return;
+    }
+    while (P.th.size() + 1 < n) {
+        const uint32_t t = (uint32_t)P.th.size() + 1;
+        P.th.emplace_back([&P, t, dev = ctx->dev] {
+            (void)hipSetDevice(dev);
+            uint64_t seen = 0;
+            std::unique_lock<std::mutex> lk(P.m);
+            for (;;) {
+                P.cv.wait(lk, [&] { return P.stop || (P.epoch != seen && t < P.want); });
+                if (P.stop) return;
+                seen = P.epoch;
+                lk.unlock();
+                P.fn(t);
+                lk.lock();
+                if (--P.busy == 0) P.idle.notify_all();
+            }
+        });
+    }
+    {
+        std::lock_guard<std::mutex> g(P.m);
+        P.fn = fn;
+        P.want = n;
+        P.busy = n - 1;
+        P.epoch++;
+    }
+    P.cv.notify_all();
+    fn(0);
+    std::unique_lock<std::mutex> lk(P.m);
+    P.idle.wait(lk, [&] { return P.busy == 0; });
+}
+
 // The certificate over nu distinct rows qs (nu x D values): ans[u] the reference's index, or -1
 // for a row it leaves open.  tree: the level's tree over the exact-sum split (K code vectors);
 // A_prev: the previous level's assignment (the cells summed on stream; sync waits for it).
@@ -1084,27 +1134,59 @@ qvq_status certify_rows(qvq_ctx *ctx, const RefKDTree &tree, const double *cb, u
         known[i] = v == 0 || std::fabs(v - u) <= 1e-14;
     }
     ans.assign(nu, -1);
+    // rows over host threads when the replays are long (48-D: the search visits most leaves)
+    const uint32_t nthr = (uint64_t)nu * K * D >= (1u << 18) ? std::min<uint32_t>(nu, cert_threads()) : 1;
+    auto each = [&](const std::vector<uint32_t> &rows, auto &&fn) {   // fn(u, thread slot)
+        if (nthr <= 1 || rows.size() < 2) {
+            for (uint32_t u : rows) fn(u, 0u);
+            return;
+        }
+        std::atomic<size_t> next{0};
+        pool_run(ctx, std::min<uint32_t>(nthr, (uint32_t)rows.size()), [&](uint32_t t) {
+            for (size_t i = next++; i < rows.size(); i = next++) fn(rows[i], t);
+        });
+    };
     std::vector<uint32_t> open, left;
     auto replay = [&](const std::vector<uint32_t> &rows) {
-        left.clear();
         tree.cert_clear();   // kp / known may have changed in place
+        each(rows, [&](uint32_t u, uint32_t) {
+            ans[u] = tree.certified_search(&qs[(size_t)u * D], KAHAN_DELTA, kp.data(), known.data());
+        });
+        left.clear();
         for (uint32_t u : rows)
-            if ((ans[u] = tree.certified_search(&qs[(size_t)u * D], KAHAN_DELTA, kp.data(), known.data())) < 0)
-                left.push_back(u);
+            if (ans[u] < 0) left.push_back(u);
         open.swap(left);
     };
+    // each row's candidates (every code vector within a slack of the nearest that covers the
+    // reference's bits): rows whose candidates are all known replay at once
+    std::vector<std::vector<uint32_t>> cand(nu);
     std::vector<uint32_t> all(nu);
     for (uint32_t u = 0; u < nu; u++) all[u] = u;
-    replay(all);
+    each(all, [&](uint32_t u, uint32_t) {
+        double dmin;
+        tree.near_set(&qs[(size_t)u * D], 1e-9, 1e-9, cand[u], dmin);
+    });
+    auto all_known = [&](uint32_t j) {
+        for (uint32_t d = 0; d < D; d++)
+            if (!known[(size_t)j * D + d]) return false;
+        return true;
+    };
+    std::vector<uint32_t> ready, pend;
+    for (uint32_t u = 0; u < nu; u++) {
+        bool k = true;
+        for (uint32_t j : cand[u]) k = k && all_known(j);
+        (k ? ready : pend).push_back(u);
+    }
+    if (!ready.empty()) {
+        replay(ready);
+        pend.insert(pend.end(), open.begin(), open.end());
+    }
     std::vector<uint8_t> sel(Kc, 0);
     cells = rounds = 0;
-    auto want = [&](uint32_t j, bool &any) {
-        for (uint32_t d = 0; d < D; d++)
-            if (!known[(size_t)j * D + d]) {
-                if (!sel[j % Kc]) cells++, any = true;
-                sel[j % Kc] = 1;
-                return;
-            }
+    auto want = [&](uint32_t j) {
+        if (all_known(j)) return;
+        cells += !sel[j % Kc];
+        sel[j % Kc] = 1;
     };
     // the reference's centroids of the selected cells (of the previous level's assignment),
     // compacted to slots: the split rows come back as slot | S + slot
@@ -1136,34 +1218,36 @@ qvq_status certify_rows(qvq_ctx *ctx, const RefKDTree &tree, const double *cb, u
         rounds++;
         return QVQ_OK;
     };
-    qvq_status st;
-    std::vector<uint32_t> cand, blame;
-    if (!open.empty() && K >= 4) {   // the candidates' cells
-        bool any = false;
-        for (uint32_t u : open) {
-            double dmin;
-            tree.near_set(&qs[(size_t)u * D], 1e-9, 1e-9, cand, dmin);
-            for (uint32_t j : cand) want(j, any);
-        }
-        if (any) {
-            if ((st = sum_cells()) != QVQ_OK) return st;
-            replay(std::vector<uint32_t>(open));
-        }
-    }
-    if (!open.empty() && K >= 4) {   // the cells of the points whose bits settle the open decisions
-        bool any = false;
-        for (uint32_t u : open) {
-            blame.clear();
-            tree.certify_blame(&qs[(size_t)u * D], KAHAN_DELTA, kp.data(), known.data(), blame);
-            for (uint32_t j : blame) want(j, any);
-        }
-        if (any) {
-            if ((st = sum_cells()) != QVQ_OK) return st;
-            replay(std::vector<uint32_t>(open));
-        }
+    open.clear();
+    if (!pend.empty() && K >= 4 && A_prev) {
+        // one round of sums: the rows' candidates and the points whose bits settle the decisions
+        // a collecting replay leaves open (with the candidates unknown, it blames them too)
+        std::vector<std::vector<uint32_t>> blame(std::max<uint32_t>(nthr, 1));
+        each(pend, [&](uint32_t u, uint32_t t) {
+            tree.certify_blame(&qs[(size_t)u * D], KAHAN_DELTA, kp.data(), known.data(), blame[t]);
+        });
+        for (uint32_t u : pend)
+            for (uint32_t j : cand[u]) want(j);
+        for (const auto &b : blame)
+            for (uint32_t j : b) want(j);
+        qvq_status st;
+        if (cells && (st = sum_cells()) != QVQ_OK) return st;
+        replay(pend);
+    } else {
+        open = pend;
     }
     open_rows = (uint32_t)open.size();
     return QVQ_OK;
+}
+
+// Host threads for the certificate's replays (at most 8, half the machine's).
+uint32_t cert_threads() {
+    static const uint32_t n = [] {
+        const char *e = std::getenv("QVQ_CERT_THREADS");
+        if (e) return (uint32_t)std::max(1, std::atoi(e));
+        return std::max<uint32_t>(1, std::min<uint32_t>(8, std::thread::hardware_concurrency() / 2));
+    }();
+    return n;
 }
 
 // Distinct rows of n row records (code bytes at code + i * stride, D of them): their values qs,
@@ -1448,6 +1532,12 @@ QVQ_API void qvq_destroy(qvq_ctx *ctx) {
     join_tree_job(ctx, true);
     for (auto &v : ctx->ver) v.cancel.store(true);
     while (ctx->worker.pending.load(std::memory_order_acquire)) std::this_thread::yield();
+    {
+        std::lock_guard<std::mutex> g(ctx->pool.m);
+        ctx->pool.stop = true;
+    }
+    ctx->pool.cv.notify_all();
+    for (auto &t : ctx->pool.th) t.join();
     if (ctx->worker.th.joinable()) {
         {
             std::lock_guard<std::mutex> g(ctx->worker.m);

@@ -513,7 +513,8 @@ RefKDTree::CertScratch &RefKDTree::cert_scratch() {
 void RefKDTree::cert_reset(double delta, const double *kpts, const uint8_t *known) const {
     CertScratch &S = cert_scratch();
     const bool collect = S.blame != nullptr;
-    if (S.owner == id_ && S.delta == delta && S.k == kpts && S.known == known && S.collect == collect)
+    const uint64_t gen = cert_gen_.load(std::memory_order_acquire);
+    if (S.owner == id_ && S.gen == gen && S.delta == delta && S.k == kpts && S.known == known && S.collect == collect)
         return;
     const int D = dim_;
     const size_t nn = nodes_.size();
@@ -523,6 +524,7 @@ void RefKDTree::cert_reset(double delta, const double *kpts, const uint8_t *know
             if (!nodes_[i].leaf) S.parent[nodes_[i].child1] = S.parent[nodes_[i].child2] = (int)i;
     }
     S.owner = id_;
+    S.gen = gen;
     S.collect = collect;
     S.delta = delta;
     S.k = kpts;
@@ -597,11 +599,7 @@ void RefKDTree::certify_blame(const double *q, double delta, const double *kpts,
     S.blame = nullptr;
 }
 
-void RefKDTree::cert_clear() const {
-    CertScratch &S = cert_scratch();
-    S.delta = -1;
-    if (S.owner == id_) S.owner = 0;
-}
+void RefKDTree::cert_clear() const { cert_gen_.fetch_add(1, std::memory_order_acq_rel); }
 
 // kd_nearest_flat (the reference's search) replayed over every codebook the certificate allows:
 // each quantity an interval, each decision taken only when all of them take it (collecting:
@@ -650,9 +648,9 @@ int64_t RefKDTree::certified_search(const double *q, double delta, const double 
             return;
         }
         const double de = ref_l2(q, pts_ + r, D);
-        double lin = 0;
-        for (int d = 0; d < D; d++)
-            if (!known[r + d]) lin += 2 * std::fabs(q[d] - pts_[r + d]) * delta + delta * delta;
+        // sum_d 2 |q_d - c_d| delta + delta^2 over the coordinates, at most (Cauchy-Schwarz,
+        // with sum_d (q_d - c_d)^2 <= de (1 + D u))
+        const double lin = 2 * delta * std::sqrt(D * de * (1 + (D + 4) * U)) + D * delta * delta;
         const double pert = (lin + (D + 4) * U * (2 * de + lin)) * (1 + 1e-9) + 1e-300;
         lo = de - pert;
         hi = de + pert;

@@ -61,7 +61,7 @@ public:
     // decision is taken), so that one round of Kahan sums can make the strict replay succeed.
     void certify_blame(const double *q, double delta, const double *kpts, const uint8_t *known,
                        std::vector<uint32_t> &blame) const;
-    // Forget the replays' caches (kpts or known changed in place).
+    // Forget the replays' caches, on every thread (kpts or known changed in place).
     void cert_clear() const;
 
 private:
@@ -110,6 +110,7 @@ private:
     // reused from tree to tree (no fresh pages per level); owned by the tree that reset it last
     struct CertScratch {
         uint64_t owner = 0;   // the owning tree's id_
+        uint64_t gen = 0;     // and its cert_gen_ then
         double delta = -1;
         const double *k = nullptr;       // the reference's split where known
         const uint8_t *known = nullptr;
@@ -137,6 +138,7 @@ private:
     void blame_dim(int node, int d, bool with_cell) const;
 
     uint64_t id_;   // unique per tree (a later tree may reuse this one's address)
+    mutable std::atomic<uint64_t> cert_gen_{0};   // cert_clear: every thread's cache is stale
 };
 
 // The reference's index for tie row q: certified_search, once the candidates cand (near_set

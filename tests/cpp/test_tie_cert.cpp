@@ -45,25 +45,31 @@ int main(int argc, char **argv) {
         RefKDTree tree(ex.data(), K, (int)D);
         std::vector<uint32_t> cand;
         long cert = 0, wrong = 0, multi = 0, cells = 0;
-        // the engine's order (engine.cpp certify_kahan_ties): each row's replay with what is
-        // known without sums; for the rows left open, the parent cells of their candidates
-        // (both split rows of each) from the reference's sums and the replay again; for rows
-        // still open, the cells of the points a collecting replay blames, and once more
+        // the engine's order (engine.cpp certify_rows): each row's candidates; rows whose
+        // candidates are all known replay at once; for the others (and those left open), one
+        // round: the parent cells (both split rows of each) of the candidates and of the points
+        // a collecting replay blames, from the reference's sums, then the replay again
         const auto t0 = std::chrono::steady_clock::now();
-        std::vector<uint32_t> blame, open, left;
+        std::vector<uint32_t> blame, ready, pend, left;
         std::vector<int64_t> got(n, -1);
-        auto replay = [&](std::vector<uint32_t> &rows) {
-            tree.cert_clear();   // kp / known changed in place
-            left.clear();
-            for (uint32_t r : rows)
-                if ((got[r] = tree.certified_search(q.data() + (size_t)r * D, delta, kp.data(), known.data())) < 0)
-                    left.push_back(r);
-            rows.swap(left);
+        std::vector<std::vector<uint32_t>> cands(n);
+        auto all_known = [&](uint32_t j) {
+            for (uint32_t d = 0; d < D; d++)
+                if (!known[(size_t)j * D + d]) return false;
+            return true;
         };
+        for (uint32_t r = 0; r < n; r++) {
+            double dmin;
+            tree.near_set(q.data() + (size_t)r * D, 1e-9, 1e-9, cands[r], dmin);
+            bool k = true;
+            for (uint32_t j : cands[r]) k = k && all_known(j);
+            (k ? ready : pend).push_back(r);
+        }
+        for (uint32_t r : ready)
+            if ((got[r] = tree.certified_search(q.data() + (size_t)r * D, delta, kp.data(), known.data())) < 0)
+                pend.push_back(r);
         auto need = [&](uint32_t j) {
-            bool all = true;
-            for (uint32_t d = 0; d < D; d++) all = all && known[(size_t)j * D + d];
-            if (all) return;
+            if (all_known(j)) return;
             const uint32_t par = j % (K / 2);
             for (uint32_t s : {par, par + K / 2}) {
                 std::memcpy(&kp[(size_t)s * D], &ka[(size_t)s * D], D * 8);
@@ -71,22 +77,13 @@ int main(int argc, char **argv) {
             }
             cells++;
         };
-        for (uint32_t r = 0; r < n; r++) open.push_back(r);
-        replay(open);
-        for (uint32_t r : open) {
-            double dmin;
-            tree.near_set(q.data() + (size_t)r * D, 1e-9, 1e-9, cand, dmin);
-            for (uint32_t j : cand) need(j);
-        }
-        if (!open.empty()) replay(open);
-        if (!getenv("TIE_CERT_NO_BLAME")) {
-            for (uint32_t r : open) {
-                blame.clear();
-                tree.certify_blame(q.data() + (size_t)r * D, delta, kp.data(), known.data(), blame);
-                for (uint32_t j : blame) need(j);
-            }
-            if (!open.empty()) replay(open);
-        }
+        if (!getenv("TIE_CERT_NO_BLAME"))
+            for (uint32_t r : pend) tree.certify_blame(q.data() + (size_t)r * D, delta, kp.data(), known.data(), blame);
+        for (uint32_t r : pend)
+            for (uint32_t j : cands[r]) need(j);
+        for (uint32_t j : blame) need(j);
+        tree.cert_clear();   // kp / known changed in place
+        for (uint32_t r : pend) got[r] = tree.certified_search(q.data() + (size_t)r * D, delta, kp.data(), known.data());
         const auto t1 = std::chrono::steady_clock::now();
         for (uint32_t r = 0; r < n; r++) {
             if (got[r] < 0) {
