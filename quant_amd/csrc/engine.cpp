@@ -180,9 +180,10 @@ struct qvq_ctx {
         bool stop = false;
     } pool;
     // the speculative Kahan check (qvq_lbg): level L's ties verified on the worker while the GPU
-    // runs level L + 1; three assignment buffers keep A_{L-1} (the check's cells) until L + 2
-    uint32_t *d_A3 = nullptr;
-    uint8_t *h_tx[2] = {nullptr, nullptr}, *dh_tx[2] = {nullptr, nullptr};   // TieExport, per level parity
+    // runs levels L + 1 and L + 2; four assignment buffers keep A_{L-1} (the check's cells)
+    // until level L + 3, when the check is joined
+    uint32_t *d_A3 = nullptr, *d_A4 = nullptr;
+    uint8_t *h_tx[3] = {nullptr, nullptr, nullptr}, *dh_tx[3] = {nullptr, nullptr, nullptr};   // TieExport, level % 3
     uint32_t tx_cap = 0;
     hipStream_t vstream = nullptr;   // the check's selected Kahan sums
     struct Verify {
@@ -196,7 +197,7 @@ struct qvq_ctx {
         std::unique_ptr<RefKDTree> tree;
         std::vector<double> cb;
         hipEvent_t ev = nullptr;
-    } ver[2];
+    } ver[3];   // level % 3
     std::atomic<bool> tree_cancel{false};
     bool tree_job = false, job_ok = false;
     int job_buf = 0;
@@ -341,6 +342,7 @@ void free_training(qvq_ctx *ctx) {
     free_kahan(ctx);
     dfree(ctx->d_A_alt);
     dfree(ctx->d_A3);
+    dfree(ctx->d_A4);
     dfree(ctx->d_X64);
     dfree(ctx->d_ex_keys);
     dfree(ctx->d_ex_iota);
@@ -1135,7 +1137,8 @@ qvq_status certify_rows(qvq_ctx *ctx, const RefKDTree &tree, const double *cb, u
     }
     ans.assign(nu, -1);
     // rows over host threads when the replays are long (48-D: the search visits most leaves)
-    const uint32_t nthr = (uint64_t)nu * K * D >= (1u << 18) ? std::min<uint32_t>(nu, cert_threads()) : 1;
+    const uint32_t nthr =
+        (nu >= 32 || (uint64_t)nu * K * D >= (1u << 18)) ? std::min<uint32_t>(nu, cert_threads()) : 1;
     auto each = [&](const std::vector<uint32_t> &rows, auto &&fn) {   // fn(u, thread slot)
         if (nthr <= 1 || rows.size() < 2) {
             for (uint32_t u : rows) fn(u, 0u);
@@ -1369,15 +1372,33 @@ bool join_verify(qvq_ctx::Verify &v) {
     return v.status == 0;
 }
 
+// join_verify within the context's wait bounds (the check waits for the GPU): a timeout fails
+// the call as any other wait does (wait_failed); ok = the check's verdict.
+qvq_status join_verify_bounded(qvq_ctx *ctx, qvq_ctx::Verify &v, bool &ok) {
+    ok = true;
+    if (!v.posted) return QVQ_OK;
+    std::string err;
+    const qvq_status st = wait_until([&] { return v.done.load(std::memory_order_acquire); },
+                                     [&](std::string &m) { return probe_stream(ctx, m); },
+                                     [&](std::string &m) { return probe_comm(ctx, m); }, ctx->timeout_s, err);
+    if (st != QVQ_OK) {
+        for (auto &u : ctx->ver) u.cancel.store(true);
+        return wait_failed(ctx, fail(ctx, st, err));
+    }
+    ok = join_verify(v);
+    return QVQ_OK;
+}
+
 // The speculative check's buffers (once per context): the third assignment buffer, the mapped
 // tie exports, the check's stream and events, and the Kahan work for the largest level.
 qvq_status ensure_speculation(qvq_ctx *ctx, uint32_t Kmax) {
     if (!ctx->d_A_alt) HIPCHK(hipMalloc(&ctx->d_A_alt, ctx->N * 4));
     if (!ctx->d_A3) HIPCHK(hipMalloc(&ctx->d_A3, ctx->N * 4));
+    if (!ctx->d_A4) HIPCHK(hipMalloc(&ctx->d_A4, ctx->N * 4));
     if (!ctx->h_tx[0]) {
         ctx->tx_cap = 65536;
         const size_t bytes = 8 + (size_t)ctx->tx_cap * (8 + 64);
-        for (int i = 0; i < 2; i++) {
+        for (int i = 0; i < 3; i++) {
             HIPCHK(hipHostMalloc(reinterpret_cast<void **>(&ctx->h_tx[i]), bytes, hipHostMallocMapped));
             HIPCHK(hipHostGetDevicePointer(reinterpret_cast<void **>(&ctx->dh_tx[i]), ctx->h_tx[i], 0));
         }
@@ -1950,19 +1971,24 @@ QVQ_API qvq_status qvq_lbg(qvq_ctx *ctx, uint32_t bits, double eps, double *code
 
     const bool sync_kahan = kahan && !spec;
     if (sync_kahan) split_out = ctx->d_C64_split_alt;
-    uint32_t *const abuf[3] = {ctx->d_A, ctx->d_A_alt, ctx->d_A3};
+    uint32_t *const abuf[4] = {ctx->d_A, ctx->d_A_alt, ctx->d_A3, ctx->d_A4};
     bool spec_failed = false;
     for (uint32_t lvl = 1; lvl <= bits; lvl++) {
         const uint32_t K = 1u << lvl;
         const int slot = (int)lvl - 1;
-        if (spec) {   // A_L in abuf[L % 3]: level L's check reads A_{L-1} until level L + 2 starts
-            if (lvl >= 3 && !join_verify(ctx->ver[lvl & 1])) {
-                spec_failed = true;
-                break;
+        if (spec) {   // A_L in abuf[L % 4]: level L's check reads A_{L-1} until level L + 3 starts
+            if (lvl >= 4) {
+                bool ok;
+                if ((st = join_verify_bounded(ctx, ctx->ver[lvl % 3], ok)) != QVQ_OK) return st;
+                if (!ok) {
+                    spec_failed = true;
+                    break;
+                }
             }
-            ctx->d_A = abuf[lvl % 3];
-            ctx->d_A_alt = abuf[(lvl + 2) % 3];
-            ctx->d_A3 = abuf[(lvl + 1) % 3];   // the three stay distinct across calls
+            ctx->d_A = abuf[lvl % 4];
+            ctx->d_A_alt = abuf[(lvl + 3) % 4];
+            ctx->d_A3 = abuf[(lvl + 1) % 4];   // the four stay distinct across calls
+            ctx->d_A4 = abuf[(lvl + 2) % 4];
         } else if (kahan) {
             std::swap(ctx->d_A, ctx->d_A_alt);   // d_A_alt: the previous level's assignment
         }
@@ -1997,19 +2023,19 @@ QVQ_API qvq_status qvq_lbg(qvq_ctx *ctx, uint32_t bits, double eps, double *code
                 tx.codes = ctx->d_codes;
                 tx.cap = ctx->tx_cap;
                 tx.n_rows = ctx->N;
-                tx.out = ctx->dh_tx[lvl & 1];
+                tx.out = ctx->dh_tx[lvl % 3];
             }
             HIPCHK(finalize(K, split, copies, copies > 1 ? tcnt : nullptr, tx));
             if (copies > 1) ctx->sums1_dirty = false;
             if (spec) {   // the check of this level, on the worker
-                qvq_ctx::Verify &v = ctx->ver[lvl & 1];
+                qvq_ctx::Verify &v = ctx->ver[lvl % 3];
                 v.posted = true;
                 v.done.store(false);
                 v.cancel.store(false);
                 v.status = 1;
                 v.K = K;
                 v.seq = ctx->seq;
-                v.par = (int)(lvl & 1);
+                v.par = (int)(lvl % 3);
                 v.A_prev = lvl >= 2 ? ctx->d_A_alt : nullptr;
                 v.tree = std::move(ctx->tree);
                 v.cb = std::move(ctx->cb_local);
@@ -2040,8 +2066,11 @@ QVQ_API qvq_status qvq_lbg(qvq_ctx *ctx, uint32_t bits, double eps, double *code
     }
     if (spec && !spec_failed) {   // the results' copy overlaps the last checks
         if ((st = enqueue_out()) != QVQ_OK) return st;
-        for (uint32_t l : {bits - 1, bits})
-            if (l >= 1 && !join_verify(ctx->ver[l & 1])) spec_failed = true;
+        for (uint32_t l = bits >= 3 ? bits - 2 : 1; l <= bits; l++) {
+            bool ok;
+            if ((st = join_verify_bounded(ctx, ctx->ver[l % 3], ok)) != QVQ_OK) return st;
+            if (!ok) spec_failed = true;
+        }
     }
     if (!spec_failed) break;
     // a check failed: every check joined, the stream drained, then the quantize again with
