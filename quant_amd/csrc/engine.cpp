@@ -115,6 +115,8 @@ struct qvq_ctx {
     uint32_t kc_kcap = 0;
     std::vector<double> h_kc_split;   // host copy of the split for the tree build
     uint32_t *d_kc_sel = nullptr;     // [K/2] slot + 1 of the cells a tie certificate sums (0: not summed)
+    uint32_t *h_kc_sel = nullptr;     // its pinned host side
+    double *h_kc_out = nullptr, *dh_kc_out = nullptr;   // [K][D] mapped: the selected cells' split rows
     std::vector<double> cert_kp;      // the reference's split where known (tie certificate)
     std::vector<uint8_t> cert_known;
     std::vector<uint32_t> cert_vals;  // the certified answers (host side of their upload)
@@ -173,11 +175,11 @@ struct qvq_ctx {
     struct Pool {
         std::vector<std::thread> th;
         std::mutex m;
-        std::condition_variable cv, idle;
+        std::condition_variable cv;
         std::function<void(uint32_t)> fn;
-        uint64_t epoch = 0;
-        uint32_t want = 0, busy = 0;
-        bool stop = false;
+        std::atomic<uint64_t> epoch{0};
+        std::atomic<uint32_t> want{0}, busy{0};
+        std::atomic<bool> stop{false};
     } pool;
     // the speculative Kahan check (qvq_lbg): level L's ties verified on the worker while the GPU
     // runs levels L + 1 and L + 2; four assignment buffers keep A_{L-1} (the check's cells)
@@ -335,6 +337,10 @@ void free_kahan(qvq_ctx *ctx) {
     dfree(ctx->d_kc_cent);
     dfree(ctx->d_kc_split);
     dfree(ctx->d_kc_sel);
+    if (ctx->h_kc_sel) (void)hipHostFree(ctx->h_kc_sel);
+    if (ctx->h_kc_out) (void)hipHostFree(ctx->h_kc_out);
+    ctx->h_kc_sel = nullptr;
+    ctx->h_kc_out = ctx->dh_kc_out = nullptr;
     ctx->kc_kcap = 0;
 }
 
@@ -629,9 +635,14 @@ qvq_status ensure_kahan(qvq_ctx *ctx, uint32_t Kc) {
         dfree(ctx->d_kc_cent);
         dfree(ctx->d_kc_split);
         dfree(ctx->d_kc_sel);
+        if (ctx->h_kc_sel) (void)hipHostFree(ctx->h_kc_sel);
+        if (ctx->h_kc_out) (void)hipHostFree(ctx->h_kc_out);
         HIPCHK(hipMalloc(&ctx->d_kc_cent, (uint64_t)Kc * D * 8));
         HIPCHK(hipMalloc(&ctx->d_kc_split, 2ull * Kc * D * 8));
         HIPCHK(hipMalloc(&ctx->d_kc_sel, (uint64_t)Kc * 4));
+        HIPCHK(hipHostMalloc(reinterpret_cast<void **>(&ctx->h_kc_sel), (uint64_t)Kc * 4, hipHostMallocDefault));
+        HIPCHK(hipHostMalloc(reinterpret_cast<void **>(&ctx->h_kc_out), 2ull * Kc * D * 8, hipHostMallocMapped));
+        HIPCHK(hipHostGetDevicePointer(reinterpret_cast<void **>(&ctx->dh_kc_out), ctx->h_kc_out, 0));
         ctx->kc_kcap = Kc;
     }
     if (w.n_cap == N && w.k_cap >= Kc && w.d_cap == D) return QVQ_OK;
@@ -1079,7 +1090,24 @@ constexpr double KAHAN_DELTA = 0x1p-49;
 // changed, when a row stays open: the caller then computes the whole split and its tree.
 uint32_t cert_threads();
 
+// QVQ_CERT_TRACE=1: the certificate's phases, us since the check saw its level's export
+struct CertTrace {
+    bool on = false;
+    std::chrono::steady_clock::time_point t0;
+    std::string s;
+    void mark(const char *what) {
+        if (!on) return;
+        char b[64];
+        std::snprintf(b, sizeof(b), " %s %.0f", what,
+                      std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count());
+        s += b;
+    }
+};
+thread_local CertTrace cert_trace;
+
 // fn(t) for t = 0 .. n - 1: t = 0 on the calling thread, the others on the pool's threads.
+// The helpers poll for work for a while before they sleep (a futex wake-up costs tens of us,
+// as long as the replays themselves on a tie level of C3).
 void pool_run(qvq_ctx *ctx, uint32_t n, const std::function<void(uint32_t)> &fn) {
     qvq_ctx::Pool &P = ctx->pool;
     if (n <= 1) {
@@ -1091,29 +1119,37 @@ void pool_run(qvq_ctx *ctx, uint32_t n, const std::function<void(uint32_t)> &fn)
         P.th.emplace_back([&P, t, dev = ctx->dev] {
             (void)hipSetDevice(dev);
             uint64_t seen = 0;
-            std::unique_lock<std::mutex> lk(P.m);
             for (;;) {
-                P.cv.wait(lk, [&] { return P.stop || (P.epoch != seen && t < P.want); });
-                if (P.stop) return;
-                seen = P.epoch;
-                lk.unlock();
-                P.fn(t);
-                lk.lock();
-                if (--P.busy == 0) P.idle.notify_all();
+                uint64_t e = P.epoch.load(std::memory_order_acquire);
+                const auto until = std::chrono::steady_clock::now() + std::chrono::milliseconds(20);
+                while (e == seen && !P.stop.load(std::memory_order_relaxed) && std::chrono::steady_clock::now() < until) {
+                    std::this_thread::yield();
+                    e = P.epoch.load(std::memory_order_acquire);
+                }
+                if (e == seen && !P.stop.load()) {   // idle: sleep until the next run
+                    std::unique_lock<std::mutex> lk(P.m);
+                    P.cv.wait(lk, [&] { return P.stop.load() || P.epoch.load() != seen; });
+                    e = P.epoch.load(std::memory_order_acquire);
+                }
+                if (P.stop.load()) return;
+                seen = e;
+                if (t < P.want.load(std::memory_order_acquire)) {
+                    P.fn(t);
+                    P.busy.fetch_sub(1, std::memory_order_acq_rel);
+                }
             }
         });
     }
+    P.fn = fn;
+    P.want.store(n, std::memory_order_release);
+    P.busy.store(n - 1, std::memory_order_release);
     {
         std::lock_guard<std::mutex> g(P.m);
-        P.fn = fn;
-        P.want = n;
-        P.busy = n - 1;
-        P.epoch++;
+        P.epoch.fetch_add(1, std::memory_order_acq_rel);
     }
     P.cv.notify_all();
     fn(0);
-    std::unique_lock<std::mutex> lk(P.m);
-    P.idle.wait(lk, [&] { return P.busy == 0; });
+    while (P.busy.load(std::memory_order_acquire)) std::this_thread::yield();
 }
 
 // The certificate over nu distinct rows qs (nu x D values): ans[u] the reference's index, or -1
@@ -1169,6 +1205,7 @@ qvq_status certify_rows(qvq_ctx *ctx, const RefKDTree &tree, const double *cb, u
         double dmin;
         tree.near_set(&qs[(size_t)u * D], 1e-9, 1e-9, cand[u], dmin);
     });
+    cert_trace.mark("near");
     auto all_known = [&](uint32_t j) {
         for (uint32_t d = 0; d < D; d++)
             if (!known[(size_t)j * D + d]) return false;
@@ -1183,6 +1220,7 @@ qvq_status certify_rows(qvq_ctx *ctx, const RefKDTree &tree, const double *cb, u
     if (!ready.empty()) {
         replay(ready);
         pend.insert(pend.end(), open.begin(), open.end());
+        cert_trace.mark("replay");
     }
     std::vector<uint8_t> sel(Kc, 0);
     cells = rounds = 0;
@@ -1192,30 +1230,31 @@ qvq_status certify_rows(qvq_ctx *ctx, const RefKDTree &tree, const double *cb, u
         sel[j % Kc] = 1;
     };
     // the reference's centroids of the selected cells (of the previous level's assignment),
-    // compacted to slots: the split rows come back as slot | S + slot
-    std::vector<uint32_t> slot_of, cell_of;
-    auto sum_cells = [&]() -> qvq_status {
+    // compacted to slots; the split rows (slot | S + slot) land in mapped host memory
+    std::vector<uint32_t> cell_of;
+    auto launch_cells = [&](const std::vector<uint8_t> &pick) -> qvq_status {
         qvq_status s2;
         if ((s2 = ensure_kahan(ctx, Kc)) != QVQ_OK) return s2;
-        slot_of.assign(Kc, 0);
         cell_of.clear();
-        for (uint32_t c = 0; c < Kc; c++)
-            if (sel[c]) {
-                cell_of.push_back(c);
-                slot_of[c] = (uint32_t)cell_of.size();
-            }
-        const uint32_t S = (uint32_t)cell_of.size();
-        HIPCHK(hipMemcpyAsync(ctx->d_kc_sel, slot_of.data(), (size_t)Kc * 4, hipMemcpyHostToDevice, stream));
-        HIPCHK(launch_kahan_centroids(stream, ctx->kw, ctx->d_codes, ctx->Dp, D, ctx->N, A_prev, S, ctx->d_kc_cent,
-                                      ctx->d_kc_split, ctx->d_kc_sel, Kc));
-        ctx->h_kc_split.resize((size_t)2 * S * D);
-        HIPCHK(hipMemcpyAsync(ctx->h_kc_split.data(), ctx->d_kc_split, (size_t)2 * S * D * 8, hipMemcpyDeviceToHost,
-                              stream));
+        for (uint32_t c = 0; c < Kc; c++) {
+            ctx->h_kc_sel[c] = pick[c] ? (uint32_t)cell_of.size() + 1 : 0u;
+            if (pick[c]) cell_of.push_back(c);
+        }
+        HIPCHK(hipMemcpyAsync(ctx->d_kc_sel, ctx->h_kc_sel, (size_t)Kc * 4, hipMemcpyHostToDevice, stream));
+        HIPCHK(launch_kahan_centroids(stream, ctx->kw, ctx->d_codes, ctx->Dp, D, ctx->N, A_prev,
+                                      (uint32_t)cell_of.size(), ctx->d_kc_cent, ctx->dh_kc_out, ctx->d_kc_sel, Kc));
+        cert_trace.mark("launched");
+        return QVQ_OK;
+    };
+    auto finish_cells = [&]() -> qvq_status {
+        qvq_status s2;
         if ((s2 = sync()) != QVQ_OK) return s2;
+        cert_trace.mark("sums");
+        const uint32_t S = (uint32_t)cell_of.size();
         for (uint32_t t = 0; t < S; t++)
             for (uint32_t h = 0; h < 2; h++) {
                 const uint32_t r = cell_of[t] + h * Kc;
-                std::memcpy(&kp[(size_t)r * D], &ctx->h_kc_split[((size_t)h * S + t) * D], D * 8);
+                std::memcpy(&kp[(size_t)r * D], &ctx->h_kc_out[((size_t)h * S + t) * D], D * 8);
                 std::memset(&known[(size_t)r * D], 1, D);
             }
         rounds++;
@@ -1223,19 +1262,30 @@ qvq_status certify_rows(qvq_ctx *ctx, const RefKDTree &tree, const double *cb, u
     };
     open.clear();
     if (!pend.empty() && K >= 4 && A_prev) {
-        // one round of sums: the rows' candidates and the points whose bits settle the decisions
-        // a collecting replay leaves open (with the candidates unknown, it blames them too)
+        // the candidates' cells on the GPU while a collecting replay finds the points whose bits
+        // settle the decisions the intervals leave open (with the candidates unknown, it blames
+        // them too); their cells, if new, in a second round
+        qvq_status st;
+        for (uint32_t u : pend)
+            for (uint32_t j : cand[u]) want(j);
+        std::vector<uint8_t> first = sel;
+        if (cells && (st = launch_cells(first)) != QVQ_OK) return st;
         std::vector<std::vector<uint32_t>> blame(std::max<uint32_t>(nthr, 1));
         each(pend, [&](uint32_t u, uint32_t t) {
             tree.certify_blame(&qs[(size_t)u * D], KAHAN_DELTA, kp.data(), known.data(), blame[t]);
         });
-        for (uint32_t u : pend)
-            for (uint32_t j : cand[u]) want(j);
+        const uint32_t c0 = cells;
         for (const auto &b : blame)
             for (uint32_t j : b) want(j);
-        qvq_status st;
-        if (cells && (st = sum_cells()) != QVQ_OK) return st;
+        cert_trace.mark("blame");
+        if (c0 && (st = finish_cells()) != QVQ_OK) return st;
+        if (cells > c0) {
+            std::vector<uint8_t> more(Kc, 0);
+            for (uint32_t c = 0; c < Kc; c++) more[c] = sel[c] && !first[c];
+            if ((st = launch_cells(more)) != QVQ_OK || (st = finish_cells()) != QVQ_OK) return st;
+        }
         replay(pend);
+        cert_trace.mark("replay");
     } else {
         open = pend;
     }
@@ -1326,6 +1376,10 @@ void verify_level(qvq_ctx *ctx, qvq_ctx::Verify &v) {
     while (*flag < v.seq)   // the export is released with the codebook's ready number
         if (v.cancel.load(std::memory_order_relaxed)) return;
     std::atomic_thread_fence(std::memory_order_acquire);
+    static const bool trace = env_is("QVQ_CERT_TRACE", "1");
+    cert_trace.on = trace;
+    cert_trace.t0 = std::chrono::steady_clock::now();
+    cert_trace.s.clear();
     const uint32_t *tx = reinterpret_cast<const uint32_t *>(ctx->h_tx[v.par]);
     const uint32_t nt = tx[0];
     if (nt == 0) {
@@ -1358,9 +1412,10 @@ void verify_level(qvq_ctx *ctx, qvq_ctx::Verify &v) {
                              rec[(size_t)i * words], rec[(size_t)i * words + 1], (long long)ans[of[i]]);
             return;
         }
-    if (env_is("QVQ_KAHAN_DEBUG", "1"))
-        std::fprintf(stderr, "qvq kahan: K %u ties %u (%u distinct) verified, cells summed %u in %u rounds\n", v.K,
-                     nt, nu, cells, rounds);
+    cert_trace.mark("done");
+    if (env_is("QVQ_KAHAN_DEBUG", "1") || trace)
+        std::fprintf(stderr, "qvq kahan: K %u ties %u (%u distinct) verified, cells summed %u in %u rounds%s%s\n", v.K,
+                     nt, nu, cells, rounds, trace ? " | us:" : "", cert_trace.s.c_str());
     v.status = 0;
 }
 
@@ -1555,7 +1610,7 @@ QVQ_API void qvq_destroy(qvq_ctx *ctx) {
     while (ctx->worker.pending.load(std::memory_order_acquire)) std::this_thread::yield();
     {
         std::lock_guard<std::mutex> g(ctx->pool.m);
-        ctx->pool.stop = true;
+        ctx->pool.stop.store(true);
     }
     ctx->pool.cv.notify_all();
     for (auto &t : ctx->pool.th) t.join();
