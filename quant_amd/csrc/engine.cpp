@@ -1105,9 +1105,8 @@ struct CertTrace {
 };
 thread_local CertTrace cert_trace;
 
-// fn(t) for t = 0 .. n - 1: t = 0 on the calling thread, the others on the pool's threads.
-// The helpers poll for work for a while before they sleep (a futex wake-up costs tens of us,
-// as long as the replays themselves on a tie level of C3).
+// fn(t) for t = 0 .. n - 1: t = 0 on the calling thread, the others on the pool's threads
+// (for replays of tens of us and more: a helper's wake-up costs about that).
 void pool_run(qvq_ctx *ctx, uint32_t n, const std::function<void(uint32_t)> &fn) {
     qvq_ctx::Pool &P = ctx->pool;
     if (n <= 1) {
@@ -1120,19 +1119,12 @@ void pool_run(qvq_ctx *ctx, uint32_t n, const std::function<void(uint32_t)> &fn)
             (void)hipSetDevice(dev);
             uint64_t seen = 0;
             for (;;) {
-                uint64_t e = P.epoch.load(std::memory_order_acquire);
-                const auto until = std::chrono::steady_clock::now() + std::chrono::milliseconds(20);
-                while (e == seen && !P.stop.load(std::memory_order_relaxed) && std::chrono::steady_clock::now() < until) {
-                    std::this_thread::yield();
-                    e = P.epoch.load(std::memory_order_acquire);
-                }
-                if (e == seen && !P.stop.load()) {   // idle: sleep until the next run
+                {
                     std::unique_lock<std::mutex> lk(P.m);
                     P.cv.wait(lk, [&] { return P.stop.load() || P.epoch.load() != seen; });
-                    e = P.epoch.load(std::memory_order_acquire);
+                    if (P.stop.load()) return;
+                    seen = P.epoch.load();
                 }
-                if (P.stop.load()) return;
-                seen = e;
                 if (t < P.want.load(std::memory_order_acquire)) {
                     P.fn(t);
                     P.busy.fetch_sub(1, std::memory_order_acq_rel);
@@ -1140,12 +1132,12 @@ void pool_run(qvq_ctx *ctx, uint32_t n, const std::function<void(uint32_t)> &fn)
             }
         });
     }
-    P.fn = fn;
-    P.want.store(n, std::memory_order_release);
-    P.busy.store(n - 1, std::memory_order_release);
     {
         std::lock_guard<std::mutex> g(P.m);
-        P.epoch.fetch_add(1, std::memory_order_acq_rel);
+        P.fn = fn;
+        P.want.store(n);
+        P.busy.store(n - 1);
+        P.epoch.fetch_add(1);
     }
     P.cv.notify_all();
     fn(0);
@@ -1173,8 +1165,8 @@ qvq_status certify_rows(qvq_ctx *ctx, const RefKDTree &tree, const double *cb, u
     }
     ans.assign(nu, -1);
     // rows over host threads when the replays are long (48-D: the search visits most leaves)
-    const uint32_t nthr =
-        (nu >= 32 || (uint64_t)nu * K * D >= (1u << 18)) ? std::min<uint32_t>(nu, cert_threads()) : 1;
+    const bool long_search = (uint64_t)K * D >= 65536;   // 48-D: a search visits most leaves
+    const uint32_t nthr = long_search ? std::min<uint32_t>(nu, cert_threads()) : 1;
     auto each = [&](const std::vector<uint32_t> &rows, auto &&fn) {   // fn(u, thread slot)
         if (nthr <= 1 || rows.size() < 2) {
             for (uint32_t u : rows) fn(u, 0u);
@@ -1197,30 +1189,39 @@ qvq_status certify_rows(qvq_ctx *ctx, const RefKDTree &tree, const double *cb, u
         open.swap(left);
     };
     // each row's candidates (every code vector within a slack of the nearest that covers the
-    // reference's bits): rows whose candidates are all known replay at once
+    // reference's bits); short searches replay every row at once and list candidates for the
+    // rows left open only, long ones (48-D) replay at once only rows whose candidates are known
     std::vector<std::vector<uint32_t>> cand(nu);
     std::vector<uint32_t> all(nu);
     for (uint32_t u = 0; u < nu; u++) all[u] = u;
-    each(all, [&](uint32_t u, uint32_t) {
-        double dmin;
-        tree.near_set(&qs[(size_t)u * D], 1e-9, 1e-9, cand[u], dmin);
-    });
-    cert_trace.mark("near");
+    auto near = [&](const std::vector<uint32_t> &rows) {
+        each(rows, [&](uint32_t u, uint32_t) {
+            double dmin;
+            tree.near_set(&qs[(size_t)u * D], 1e-9, 1e-9, cand[u], dmin);
+        });
+        cert_trace.mark("near");
+    };
     auto all_known = [&](uint32_t j) {
         for (uint32_t d = 0; d < D; d++)
             if (!known[(size_t)j * D + d]) return false;
         return true;
     };
     std::vector<uint32_t> ready, pend;
-    for (uint32_t u = 0; u < nu; u++) {
-        bool k = true;
-        for (uint32_t j : cand[u]) k = k && all_known(j);
-        (k ? ready : pend).push_back(u);
+    if (long_search) {
+        near(all);
+        for (uint32_t u = 0; u < nu; u++) {
+            bool k = true;
+            for (uint32_t j : cand[u]) k = k && all_known(j);
+            (k ? ready : pend).push_back(u);
+        }
+    } else {
+        ready = all;
     }
     if (!ready.empty()) {
         replay(ready);
         pend.insert(pend.end(), open.begin(), open.end());
         cert_trace.mark("replay");
+        if (!long_search) near(pend);
     }
     std::vector<uint8_t> sel(Kc, 0);
     cells = rounds = 0;

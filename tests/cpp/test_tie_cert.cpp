@@ -45,8 +45,9 @@ int main(int argc, char **argv) {
         RefKDTree tree(ex.data(), K, (int)D);
         std::vector<uint32_t> cand;
         long cert = 0, wrong = 0, multi = 0, cells = 0;
-        // the engine's order (engine.cpp certify_rows): each row's candidates; rows whose
-        // candidates are all known replay at once; for the others (and those left open), one
+        // the engine's order (engine.cpp certify_rows): short searches replay every row at once,
+        // long ones (48-D) first list each row's candidates and replay at once only rows whose
+        // candidates are all known; for the others (and those left open), one
         // round: the parent cells (both split rows of each) of the candidates and of the points
         // a collecting replay blames, from the reference's sums, then the replay again
         const auto t0 = std::chrono::steady_clock::now();
@@ -58,16 +59,24 @@ int main(int argc, char **argv) {
                 if (!known[(size_t)j * D + d]) return false;
             return true;
         };
+        const bool long_search = (uint64_t)K * D >= 65536;   // (48-D: near_set first)
         for (uint32_t r = 0; r < n; r++) {
-            double dmin;
-            tree.near_set(q.data() + (size_t)r * D, 1e-9, 1e-9, cands[r], dmin);
             bool k = true;
-            for (uint32_t j : cands[r]) k = k && all_known(j);
+            if (long_search) {
+                double dmin;
+                tree.near_set(q.data() + (size_t)r * D, 1e-9, 1e-9, cands[r], dmin);
+                for (uint32_t j : cands[r]) k = k && all_known(j);
+            }
             (k ? ready : pend).push_back(r);
         }
         for (uint32_t r : ready)
-            if ((got[r] = tree.certified_search(q.data() + (size_t)r * D, delta, kp.data(), known.data())) < 0)
+            if ((got[r] = tree.certified_search(q.data() + (size_t)r * D, delta, kp.data(), known.data())) < 0) {
                 pend.push_back(r);
+                if (!long_search) {
+                    double dmin;
+                    tree.near_set(q.data() + (size_t)r * D, 1e-9, 1e-9, cands[r], dmin);
+                }
+            }
         auto need = [&](uint32_t j) {
             if (all_known(j)) return;
             const uint32_t par = j % (K / 2);
