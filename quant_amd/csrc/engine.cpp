@@ -1207,7 +1207,8 @@ qvq_status certify_rows(qvq_ctx *ctx, const RefKDTree &tree, const double *cb, u
         return true;
     };
     std::vector<uint32_t> ready, pend;
-    if (long_search) {
+    const bool near_first = long_search || nu <= 16;   // few rows: skip replays doomed by unknown candidates
+    if (near_first) {
         near(all);
         for (uint32_t u = 0; u < nu; u++) {
             bool k = true;
@@ -1221,7 +1222,7 @@ qvq_status certify_rows(qvq_ctx *ctx, const RefKDTree &tree, const double *cb, u
         replay(ready);
         pend.insert(pend.end(), open.begin(), open.end());
         cert_trace.mark("replay");
-        if (!long_search) near(pend);
+        if (!near_first) near(pend);
     }
     std::vector<uint8_t> sel(Kc, 0);
     cells = rounds = 0;

@@ -514,8 +514,8 @@ void RefKDTree::cert_reset(double delta, const double *kpts, const uint8_t *know
     CertScratch &S = cert_scratch();
     const bool collect = S.blame != nullptr;
     const uint64_t gen = cert_gen_.load(std::memory_order_acquire);
-    if (S.owner == id_ && S.gen == gen && S.delta == delta && S.k == kpts && S.known == known && S.collect == collect)
-        return;
+    const bool same_agg = S.owner == id_ && S.gen == gen && S.k == kpts && S.known == known;
+    if (same_agg && S.delta == delta && S.collect == collect) return;
     const int D = dim_;
     const size_t nn = nodes_.size();
     if (S.owner != id_) {
@@ -523,42 +523,44 @@ void RefKDTree::cert_reset(double delta, const double *kpts, const uint8_t *know
         for (size_t i = 0; i < nn; i++)
             if (!nodes_[i].leaf) S.parent[nodes_[i].child1] = S.parent[nodes_[i].child2] = (int)i;
     }
-    S.owner = id_;
-    S.gen = gen;
+    // the replay's node states: per mode (a collecting replay's are not a strict one's)
     S.collect = collect;
     S.delta = delta;
-    S.k = kpts;
-    S.known = known;
     S.node.assign(nn, CertNode());
     S.box.resize(nn * D * 2);
     S.box_set.assign(nn, 0);
-    S.agg.resize(nn * D * 4);
-    // per node and dimension: min / max over its points whose bits are not known (exact-sum
-    // values) and over those known (the reference's values), children before parents
-    constexpr double INF = std::numeric_limits<double>::infinity();
-    for (size_t i = nodes_.size(); i-- > 0;) {
-        double *a = &S.agg[i * D * 4];
-        const Node &n = nodes_[i];
-        for (int d = 0; d < D; d++) {
-            a[4 * d] = a[4 * d + 2] = INF;
-            a[4 * d + 1] = a[4 * d + 3] = -INF;
-        }
-        if (n.leaf) {
-            for (size_t j = n.left; j < n.right; j++) {
-                const size_t p = vind_[j];
+    if (!same_agg) {
+        S.owner = id_;
+        S.gen = gen;
+        S.k = kpts;
+        S.known = known;
+        S.agg.resize(nn * D * 4);
+        // per node and dimension: min / max over its points whose bits are not known (exact-sum
+        // values) and over those known (the reference's values), children before parents
+        constexpr double INF = std::numeric_limits<double>::infinity();
+        for (size_t i = nn; i-- > 0;) {
+            double *a = &S.agg[i * D * 4];
+            const Node &n = nodes_[i];
+            if (n.leaf) {
                 for (int d = 0; d < D; d++) {
-                    const size_t e = p * (size_t)D + d;
-                    const int o = known[e] ? 2 : 0;
-                    const double v = known[e] ? kpts[e] : pts_[e];
-                    a[4 * d + o] = std::min(a[4 * d + o], v);
-                    a[4 * d + o + 1] = std::max(a[4 * d + o + 1], v);
+                    a[4 * d] = a[4 * d + 2] = INF;
+                    a[4 * d + 1] = a[4 * d + 3] = -INF;
                 }
-            }
-        } else {
-            const double *b = &S.agg[(size_t)n.child1 * D * 4], *c = &S.agg[(size_t)n.child2 * D * 4];
-            for (int k = 0; k < 4 * D; k += 2) {
-                a[k] = std::min(b[k], c[k]);
-                a[k + 1] = std::max(b[k + 1], c[k + 1]);
+                for (size_t j = n.left; j < n.right; j++) {
+                    const size_t r = vind_[j] * (size_t)D;
+                    for (int d = 0; d < D; d++) {
+                        const int o = known[r + d] ? 2 : 0;
+                        const double v = o ? kpts[r + d] : pts_[r + d];
+                        a[4 * d + o] = std::min(a[4 * d + o], v);
+                        a[4 * d + o + 1] = std::max(a[4 * d + o + 1], v);
+                    }
+                }
+            } else {
+                const double *b = &S.agg[(size_t)n.child1 * D * 4], *c = &S.agg[(size_t)n.child2 * D * 4];
+                for (int k = 0; k < 4 * D; k += 2) {
+                    a[k] = std::min(b[k], c[k]);
+                    a[k + 1] = std::max(b[k + 1], c[k + 1]);
+                }
             }
         }
     }
