@@ -1159,9 +1159,11 @@ qvq_status certify_rows(qvq_ctx *ctx, const RefKDTree &tree, const double *cb, u
     std::vector<uint8_t> &known = ctx->cert_known;
     kp.assign(cb, cb + (size_t)K * D);
     known.resize((size_t)K * D);
-    for (size_t i = 0; i < known.size(); i++) {
-        const double u = i / D < Kc ? 1 + 0.2 : 1 - 0.2, v = kp[i];
-        known[i] = v == 0 || std::fabs(v - u) <= 1e-14;
+    for (uint32_t j = 0; j < K; j++) {
+        const double u = j < Kc ? 1 + 0.2 : 1 - 0.2;
+        const double *v = &kp[(size_t)j * D];
+        uint8_t *k = &known[(size_t)j * D];
+        for (uint32_t d = 0; d < D; d++) k[d] = v[d] == 0 || std::fabs(v[d] - u) <= 1e-14;
     }
     ans.assign(nu, -1);
     // rows over host threads when the replays are long (48-D: the search visits most leaves)
@@ -1178,8 +1180,8 @@ qvq_status certify_rows(qvq_ctx *ctx, const RefKDTree &tree, const double *cb, u
         });
     };
     std::vector<uint32_t> open, left;
+    tree.cert_clear();   // kp / known: this level's (the vectors are reused)
     auto replay = [&](const std::vector<uint32_t> &rows) {
-        tree.cert_clear();   // kp / known may have changed in place
         each(rows, [&](uint32_t u, uint32_t) {
             ans[u] = tree.certified_search(&qs[(size_t)u * D], KAHAN_DELTA, kp.data(), known.data());
         });
@@ -1253,12 +1255,15 @@ qvq_status certify_rows(qvq_ctx *ctx, const RefKDTree &tree, const double *cb, u
         if ((s2 = sync()) != QVQ_OK) return s2;
         cert_trace.mark("sums");
         const uint32_t S = (uint32_t)cell_of.size();
+        std::vector<uint32_t> changed;
         for (uint32_t t = 0; t < S; t++)
             for (uint32_t h = 0; h < 2; h++) {
                 const uint32_t r = cell_of[t] + h * Kc;
                 std::memcpy(&kp[(size_t)r * D], &ctx->h_kc_out[((size_t)h * S + t) * D], D * 8);
                 std::memset(&known[(size_t)r * D], 1, D);
+                changed.push_back(r);
             }
+        tree.cert_update(changed.data(), changed.size());   // kp / known changed on these rows
         rounds++;
         return QVQ_OK;
     };

@@ -520,8 +520,13 @@ void RefKDTree::cert_reset(double delta, const double *kpts, const uint8_t *know
     const size_t nn = nodes_.size();
     if (S.owner != id_) {
         S.parent.assign(nn, -1);
-        for (size_t i = 0; i < nn; i++)
-            if (!nodes_[i].leaf) S.parent[nodes_[i].child1] = S.parent[nodes_[i].child2] = (int)i;
+        S.leaf_of.resize(K_);
+        for (size_t i = 0; i < nn; i++) {
+            const Node &n = nodes_[i];
+            if (!n.leaf) S.parent[n.child1] = S.parent[n.child2] = (int)i;
+            else
+                for (size_t j = n.left; j < n.right; j++) S.leaf_of[vind_[j]] = (int)i;
+        }
     }
     // the replay's node states: per mode (a collecting replay's are not a strict one's)
     S.collect = collect;
@@ -602,6 +607,46 @@ void RefKDTree::certify_blame(const double *q, double delta, const double *kpts,
 }
 
 void RefKDTree::cert_clear() const { cert_gen_.fetch_add(1, std::memory_order_acq_rel); }
+
+void RefKDTree::cert_update(const uint32_t *pts, size_t n) const {
+    const uint64_t gen = cert_gen_.fetch_add(1, std::memory_order_acq_rel) + 1;   // other threads: all anew
+    CertScratch &S = cert_scratch();
+    if (S.owner != id_ || !S.known || S.gen + 1 != gen) return;   // the next reset recomputes all
+    const int D = dim_;
+    const size_t nn = nodes_.size();
+    constexpr double INF = std::numeric_limits<double>::infinity();
+    S.dirty.assign(nn, 0);
+    for (size_t i = 0; i < n; i++)
+        for (int a = S.leaf_of[pts[i]]; a >= 0 && !S.dirty[a]; a = S.parent[a]) S.dirty[a] = 1;
+    for (size_t i = nn; i-- > 0;) {   // children before parents
+        if (!S.dirty[i]) continue;
+        double *a = &S.agg[i * D * 4];
+        const Node &nd = nodes_[i];
+        if (nd.leaf) {
+            for (int d = 0; d < D; d++) {
+                a[4 * d] = a[4 * d + 2] = INF;
+                a[4 * d + 1] = a[4 * d + 3] = -INF;
+            }
+            for (size_t j = nd.left; j < nd.right; j++) {
+                const size_t r = vind_[j] * (size_t)D;
+                for (int d = 0; d < D; d++) {
+                    const int o = S.known[r + d] ? 2 : 0;
+                    const double v = o ? S.k[r + d] : pts_[r + d];
+                    a[4 * d + o] = std::min(a[4 * d + o], v);
+                    a[4 * d + o + 1] = std::max(a[4 * d + o + 1], v);
+                }
+            }
+        } else {
+            const double *b = &S.agg[(size_t)nd.child1 * D * 4], *c = &S.agg[(size_t)nd.child2 * D * 4];
+            for (int k = 0; k < 4 * D; k += 2) {
+                a[k] = std::min(b[k], c[k]);
+                a[k + 1] = std::max(b[k + 1], c[k + 1]);
+            }
+        }
+    }
+    S.gen = gen;
+    S.delta = -1;   // node states anew at the next replay, aggregates kept
+}
 
 // kd_nearest_flat (the reference's search) replayed over every codebook the certificate allows:
 // each quantity an interval, each decision taken only when all of them take it (collecting:

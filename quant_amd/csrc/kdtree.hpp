@@ -63,6 +63,9 @@ public:
                        std::vector<uint32_t> &blame) const;
     // Forget the replays' caches, on every thread (kpts or known changed in place).
     void cert_clear() const;
+    // The same after kpts / known changed on the rows pts[0..n) only: the calling thread's
+    // cache keeps its per-node values but those of these points' leaves and their ancestors.
+    void cert_update(const uint32_t *pts, size_t n) const;
 
 private:
     struct Node {
@@ -121,6 +124,8 @@ private:
         std::vector<uint8_t> box_set;
         std::vector<double> agg;      // [node][dim][min, max unknown | min, max known]
         std::vector<int> parent;
+        std::vector<int> leaf_of;     // point -> its leaf
+        std::vector<uint8_t> dirty;   // cert_update's marks
     };
     static CertScratch &cert_scratch();
     Iv piv(size_t p, int d) const {

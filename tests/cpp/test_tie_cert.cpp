@@ -77,12 +77,14 @@ int main(int argc, char **argv) {
                     tree.near_set(q.data() + (size_t)r * D, 1e-9, 1e-9, cands[r], dmin);
                 }
             }
+        std::vector<uint32_t> changed;
         auto need = [&](uint32_t j) {
             if (all_known(j)) return;
             const uint32_t par = j % (K / 2);
             for (uint32_t s : {par, par + K / 2}) {
                 std::memcpy(&kp[(size_t)s * D], &ka[(size_t)s * D], D * 8);
                 std::memset(&known[(size_t)s * D], 1, D);
+                changed.push_back(s);
             }
             cells++;
         };
@@ -91,7 +93,7 @@ int main(int argc, char **argv) {
         for (uint32_t r : pend)
             for (uint32_t j : cands[r]) need(j);
         for (uint32_t j : blame) need(j);
-        tree.cert_clear();   // kp / known changed in place
+        tree.cert_update(changed.data(), changed.size());   // kp / known changed on these rows
         for (uint32_t r : pend) got[r] = tree.certified_search(q.data() + (size_t)r * D, delta, kp.data(), known.data());
         const auto t1 = std::chrono::steady_clock::now();
         for (uint32_t r = 0; r < n; r++) {
