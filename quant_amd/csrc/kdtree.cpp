@@ -16,6 +16,26 @@ namespace qvq {
 double ref_l2(const double *a, const double *b, int dim) { return ref_l2_hd(a, b, dim); }
 
 namespace {
+// ref_l2_hd's sum with an early exit: once a prefix exceeds cap it is returned (the terms are
+// nonnegative and rounding is monotone, so the whole sum, in the same order, exceeds cap too).
+inline double ref_l2_cap(const double *a, const double *b, int dim, double cap) {
+    double r = 0;
+    int d = 0;
+    for (; d + 3 < dim; d += 4) {
+        const double e0 = a[d] - b[d], e1 = a[d + 1] - b[d + 1];
+        const double e2 = a[d + 2] - b[d + 2], e3 = a[d + 3] - b[d + 3];
+        r += (e1 * e1 + e2 * e2) + (e0 * e0 + e3 * e3);
+        if (r > cap) return r;
+    }
+    for (; d < dim; d++) {
+        const double e = a[d] - b[d];
+        r += e * e;
+    }
+    return r;
+}
+}  // namespace
+
+namespace {
 constexpr int KD_MAX_DIM = 64;
 
 // children's boxes per tree level, [2][KD_MAX_DIM] each: allocated on first use and kept
@@ -313,7 +333,9 @@ void RefKDTree::near_set(const double *q, double slack_rel, double slack_abs, st
         if (n.leaf) {
             for (size_t i = n.left; i < n.right; i++) {
                 const uint32_t p = (uint32_t)vind_[i];
-                const double d = ref_l2(q, pts_ + (size_t)p * dim_, dim_);
+                const double cap = best * (1 + slack_rel) + slack_abs;   // beyond it: no candidate
+                const double d = ref_l2_cap(q, pts_ + (size_t)p * dim_, dim_, cap);
+                if (d > cap) continue;
                 seen.emplace_back(d, p);
                 best = std::min(best, d);
             }
@@ -684,23 +706,27 @@ int64_t RefKDTree::certified_search(const double *q, double delta, const double 
     int64_t idx = 0;
     bool amb = false, ok = true;
     std::vector<int> path;
+    // sum_d 2 |q_d - c_d| delta + delta^2 over the coordinates, at most (Cauchy-Schwarz, with
+    // sum_d (q_d - c_d)^2 <= de (1 + D u)), and both evaluations' rounding; de - pert(de) grows
+    // with de
+    auto pert = [&](double de) {
+        const double lin = 2 * delta * std::sqrt(D * de * (1 + (D + 4) * U)) + D * delta * delta;
+        return (lin + (D + 4) * U * (2 * de + lin)) * (1 + 1e-9) + 1e-300;
+    };
     // a point's distance: exact when all its coordinates are known, else around the exact-sum
-    // split's by the coordinates' slack (and both evaluations' rounding)
-    auto pdist = [&](uint32_t p, double &lo, double &hi) {
+    // split's; a prefix past the best so far (bhi) settles a rejection early
+    auto pdist = [&](uint32_t p, double bound, double &lo, double &hi) {
         const size_t r = (size_t)p * D;
         bool all = true;
         for (int d = 0; d < D; d++) all = all && known[r + d];
         if (all) {
-            lo = hi = ref_l2(q, kpts + r, D);
+            lo = hi = ref_l2_cap(q, kpts + r, D, bound);
             return;
         }
-        const double de = ref_l2(q, pts_ + r, D);
-        // sum_d 2 |q_d - c_d| delta + delta^2 over the coordinates, at most (Cauchy-Schwarz,
-        // with sum_d (q_d - c_d)^2 <= de (1 + D u))
-        const double lin = 2 * delta * std::sqrt(D * de * (1 + (D + 4) * U)) + D * delta * delta;
-        const double pert = (lin + (D + 4) * U * (2 * de + lin)) * (1 + 1e-9) + 1e-300;
-        lo = de - pert;
-        hi = de + pert;
+        double de = ref_l2_cap(q, pts_ + r, D, bound);
+        if (de > bound && !(de - pert(de) >= bound)) de = ref_l2(q, pts_ + r, D);
+        lo = de - pert(de);
+        hi = de + pert(de);
     };
     auto blame_pt = [&](uint32_t p) {
         for (int d = 0; d < D; d++)
@@ -717,7 +743,7 @@ int64_t RefKDTree::certified_search(const double *q, double delta, const double 
             for (size_t i = n.left; i < n.right; i++) {
                 const uint32_t p = (uint32_t)vind_[i];
                 double lo, hi;
-                pdist(p, lo, hi);
+                pdist(p, bhi, lo, hi);
                 // kept iff dist < worst and best > dist: with best <= worst, iff dist < best
                 const bool yes = hi < wlo && hi < blo, no = lo >= whi || lo >= bhi;
                 if (yes) {
