@@ -352,21 +352,25 @@ void RefKDTree::near_set(const double *q, double slack_rel, double slack_abs, st
         if (s.first <= lim) out.push_back(s.second);
 }
 
-// Blame (the collecting run): the points holding node's least and greatest value in dimension
-// d, unless known already.
+// Blame (the collecting run): the points holding the least and greatest value in dimension d
+// among node's points whose bits are not known (the aggregates keep them).
+// Small nodes: every such point at the extreme value (duplicated code vectors).
 void RefKDTree::blame_extremes(int node, int d) const {
     CertScratch &S = cert_scratch();
+    const uint32_t *g = &S.arg[((size_t)node * dim_ + d) * 2];
     const Node &n = nodes_[node];
-    double mn = ptr(vind_[n.left], d), mx = mn;
-    for (size_t i = n.left + 1; i < n.right; i++) {
-        const double v = ptr(vind_[i], d);
-        mn = std::min(mn, v);
-        mx = std::max(mx, v);
+    if (n.right - n.left > 256) {
+        for (int k = 0; k < 2; k++)
+            if (g[k] != ~0u) S.blame->push_back(g[k]);
+        return;
     }
-    for (size_t i = n.left; i < n.right; i++) {
-        const size_t p = vind_[i];
-        const double v = ptr(p, d);
-        if ((v == mn || v == mx) && !S.known[p * (size_t)dim_ + d]) S.blame->push_back((uint32_t)p);
+    for (int k = 0; k < 2; k++) {
+        if (g[k] == ~0u) continue;
+        const double v = ptr(g[k], d);
+        for (size_t i = n.left; i < n.right; i++) {
+            const size_t p = vind_[i];
+            if (ptr(p, d) == v && !S.known[p * (size_t)dim_ + d]) S.blame->push_back((uint32_t)p);
+        }
     }
 }
 
@@ -562,40 +566,61 @@ void RefKDTree::cert_reset(double delta, const double *kpts, const uint8_t *know
         S.k = kpts;
         S.known = known;
         S.agg.resize(nn * D * 4);
+        S.arg.resize(nn * D * 2);
         // per node and dimension: min / max over its points whose bits are not known (exact-sum
         // values) and over those known (the reference's values), children before parents
-        constexpr double INF = std::numeric_limits<double>::infinity();
-        for (size_t i = nn; i-- > 0;) {
-            double *a = &S.agg[i * D * 4];
-            const Node &n = nodes_[i];
-            if (n.leaf) {
-                for (int d = 0; d < D; d++) {
-                    a[4 * d] = a[4 * d + 2] = INF;
-                    a[4 * d + 1] = a[4 * d + 3] = -INF;
-                }
-                for (size_t j = n.left; j < n.right; j++) {
-                    const size_t r = vind_[j] * (size_t)D;
-                    for (int d = 0; d < D; d++) {
-                        const int o = known[r + d] ? 2 : 0;
-                        const double v = o ? kpts[r + d] : pts_[r + d];
-                        a[4 * d + o] = std::min(a[4 * d + o], v);
-                        a[4 * d + o + 1] = std::max(a[4 * d + o + 1], v);
-                    }
-                }
-            } else {
-                const double *b = &S.agg[(size_t)n.child1 * D * 4], *c = &S.agg[(size_t)n.child2 * D * 4];
-                for (int k = 0; k < 4 * D; k += 2) {
-                    a[k] = std::min(b[k], c[k]);
-                    a[k + 1] = std::max(b[k + 1], c[k + 1]);
-                }
-            }
-        }
+        for (size_t i = nn; i-- > 0;) cert_agg_node(i);
     }
     for (int d = 0; d < D; d++) {   // the root's cell box: the points' box
         S.box[2 * d] = iv_min(0, d);
         S.box[2 * d + 1] = iv_max(0, d);
     }
     S.box_set[0] = 1;
+}
+
+// One node's aggregates (children's first): min / max over the unknown points (and which ones)
+// and over the known points.
+void RefKDTree::cert_agg_node(size_t i) const {
+    CertScratch &S = cert_scratch();
+    constexpr double INF = std::numeric_limits<double>::infinity();
+    const int D = dim_;
+    double *a = &S.agg[i * D * 4];
+    uint32_t *g = &S.arg[i * D * 2];
+    const Node &n = nodes_[i];
+    if (n.leaf) {
+        for (int d = 0; d < D; d++) {
+            a[4 * d] = a[4 * d + 2] = INF;
+            a[4 * d + 1] = a[4 * d + 3] = -INF;
+            g[2 * d] = g[2 * d + 1] = ~0u;
+        }
+        for (size_t j = n.left; j < n.right; j++) {
+            const uint32_t p = (uint32_t)vind_[j];
+            const size_t r = p * (size_t)D;
+            for (int d = 0; d < D; d++) {
+                if (S.known[r + d]) {
+                    const double v = S.k[r + d];
+                    a[4 * d + 2] = std::min(a[4 * d + 2], v);
+                    a[4 * d + 3] = std::max(a[4 * d + 3], v);
+                } else {
+                    const double v = pts_[r + d];
+                    if (v < a[4 * d]) a[4 * d] = v, g[2 * d] = p;
+                    if (v > a[4 * d + 1]) a[4 * d + 1] = v, g[2 * d + 1] = p;
+                }
+            }
+        }
+        return;
+    }
+    const double *b = &S.agg[(size_t)n.child1 * D * 4], *c = &S.agg[(size_t)n.child2 * D * 4];
+    const uint32_t *gb = &S.arg[(size_t)n.child1 * D * 2], *gc = &S.arg[(size_t)n.child2 * D * 2];
+    for (int d = 0; d < D; d++) {
+        const bool lo1 = b[4 * d] <= c[4 * d], hi1 = b[4 * d + 1] >= c[4 * d + 1];
+        a[4 * d] = lo1 ? b[4 * d] : c[4 * d];
+        g[2 * d] = lo1 ? gb[2 * d] : gc[2 * d];
+        a[4 * d + 1] = hi1 ? b[4 * d + 1] : c[4 * d + 1];
+        g[2 * d + 1] = hi1 ? gb[2 * d + 1] : gc[2 * d + 1];
+        a[4 * d + 2] = std::min(b[4 * d + 2], c[4 * d + 2]);
+        a[4 * d + 3] = std::max(b[4 * d + 3], c[4 * d + 3]);
+    }
 }
 
 // The least (greatest) value of dimension d over node's points, over every allowed codebook.
@@ -634,38 +659,12 @@ void RefKDTree::cert_update(const uint32_t *pts, size_t n) const {
     const uint64_t gen = cert_gen_.fetch_add(1, std::memory_order_acq_rel) + 1;   // other threads: all anew
     CertScratch &S = cert_scratch();
     if (S.owner != id_ || !S.known || S.gen + 1 != gen) return;   // the next reset recomputes all
-    const int D = dim_;
     const size_t nn = nodes_.size();
-    constexpr double INF = std::numeric_limits<double>::infinity();
     S.dirty.assign(nn, 0);
     for (size_t i = 0; i < n; i++)
         for (int a = S.leaf_of[pts[i]]; a >= 0 && !S.dirty[a]; a = S.parent[a]) S.dirty[a] = 1;
-    for (size_t i = nn; i-- > 0;) {   // children before parents
-        if (!S.dirty[i]) continue;
-        double *a = &S.agg[i * D * 4];
-        const Node &nd = nodes_[i];
-        if (nd.leaf) {
-            for (int d = 0; d < D; d++) {
-                a[4 * d] = a[4 * d + 2] = INF;
-                a[4 * d + 1] = a[4 * d + 3] = -INF;
-            }
-            for (size_t j = nd.left; j < nd.right; j++) {
-                const size_t r = vind_[j] * (size_t)D;
-                for (int d = 0; d < D; d++) {
-                    const int o = S.known[r + d] ? 2 : 0;
-                    const double v = o ? S.k[r + d] : pts_[r + d];
-                    a[4 * d + o] = std::min(a[4 * d + o], v);
-                    a[4 * d + o + 1] = std::max(a[4 * d + o + 1], v);
-                }
-            }
-        } else {
-            const double *b = &S.agg[(size_t)nd.child1 * D * 4], *c = &S.agg[(size_t)nd.child2 * D * 4];
-            for (int k = 0; k < 4 * D; k += 2) {
-                a[k] = std::min(b[k], c[k]);
-                a[k + 1] = std::max(b[k + 1], c[k + 1]);
-            }
-        }
-    }
+    for (size_t i = nn; i-- > 0;)   // children before parents
+        if (S.dirty[i]) cert_agg_node(i);
     S.gen = gen;
     S.delta = -1;   // node states anew at the next replay, aggregates kept
 }

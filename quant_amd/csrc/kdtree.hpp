@@ -123,6 +123,7 @@ private:
         std::vector<Iv> box;          // [node][dim][lo, hi]: the node's cell box, once its parent replayed
         std::vector<uint8_t> box_set;
         std::vector<double> agg;      // [node][dim][min, max unknown | min, max known]
+        std::vector<uint32_t> arg;    // [node][dim][point at the unknown min, at the unknown max]
         std::vector<int> parent;
         std::vector<int> leaf_of;     // point -> its leaf
         std::vector<uint8_t> dirty;   // cert_update's marks
@@ -137,6 +138,7 @@ private:
     bool cert_split(int node) const;
     void cert_reset(double delta, const double *kpts, const uint8_t *known) const;
     void blame_extremes(int node, int d) const;
+    void cert_agg_node(size_t i) const;
     Iv iv_min(int node, int d) const;
     Iv iv_max(int node, int d) const;
 
