@@ -357,7 +357,7 @@ void RefKDTree::near_set(const double *q, double slack_rel, double slack_abs, st
 // Small nodes: every such point at the extreme value (duplicated code vectors).
 void RefKDTree::blame_extremes(int node, int d) const {
     CertScratch &S = cert_scratch();
-    const uint32_t *g = &S.arg[((size_t)node * dim_ + d) * 2];
+    const uint32_t *g = &arg_[((size_t)node * dim_ + d) * 2];
     const Node &n = nodes_[node];
     if (n.right - n.left > 256) {
         for (int k = 0; k < 2; k++)
@@ -377,10 +377,9 @@ void RefKDTree::blame_extremes(int node, int d) const {
 // ... and with_cell those of the node's cell box's origin in d too (the root's box and every
 // ancestor that cut along d).
 void RefKDTree::blame_dim(int node, int d, bool with_cell) const {
-    CertScratch &S = cert_scratch();
     blame_extremes(node, d);
     if (!with_cell) return;
-    for (int a = S.parent[node]; a >= 0; a = S.parent[a])
+    for (int a = parent_[node]; a >= 0; a = parent_[a])
         if (nodes_[a].divfeat == d) blame_extremes(a, d);
     if (node != 0) blame_extremes(0, d);
 }
@@ -536,41 +535,51 @@ RefKDTree::CertScratch &RefKDTree::cert_scratch() {
     return s;
 }
 
+void RefKDTree::cert_ensure_agg(uint64_t gen, const double *kpts, const uint8_t *known) const {
+    if (agg_gen_.load(std::memory_order_acquire) == gen && agg_k_ == kpts && agg_known_ == known) return;
+    std::lock_guard<std::mutex> g(agg_mu_);
+    if (agg_gen_.load(std::memory_order_acquire) == gen && agg_k_ == kpts && agg_known_ == known) return;
+    const size_t nn = nodes_.size();
+    if (parent_.size() != nn) {
+        parent_.assign(nn, -1);
+        leaf_of_.resize(K_);
+        for (size_t i = 0; i < nn; i++) {
+            const Node &n = nodes_[i];
+            if (!n.leaf) parent_[n.child1] = parent_[n.child2] = (int)i;
+            else
+                for (size_t j = n.left; j < n.right; j++) leaf_of_[vind_[j]] = (int)i;
+        }
+    }
+    agg_k_ = kpts;
+    agg_known_ = known;
+    agg_.resize(nn * dim_ * 4);
+    arg_.resize(nn * dim_ * 2);
+    // per node and dimension: min / max over its points whose bits are not known (exact-sum
+    // values) and over those known (the reference's values), children before parents
+    for (size_t i = nn; i-- > 0;) cert_agg_node(i);
+    agg_gen_.store(gen, std::memory_order_release);
+}
+
 void RefKDTree::cert_reset(double delta, const double *kpts, const uint8_t *known) const {
     CertScratch &S = cert_scratch();
     const bool collect = S.blame != nullptr;
     const uint64_t gen = cert_gen_.load(std::memory_order_acquire);
-    const bool same_agg = S.owner == id_ && S.gen == gen && S.k == kpts && S.known == known;
-    if (same_agg && S.delta == delta && S.collect == collect) return;
+    cert_ensure_agg(gen, kpts, known);
+    if (S.owner == id_ && S.gen == gen && S.k == kpts && S.known == known && S.delta == delta &&
+        S.collect == collect)
+        return;
     const int D = dim_;
     const size_t nn = nodes_.size();
-    if (S.owner != id_) {
-        S.parent.assign(nn, -1);
-        S.leaf_of.resize(K_);
-        for (size_t i = 0; i < nn; i++) {
-            const Node &n = nodes_[i];
-            if (!n.leaf) S.parent[n.child1] = S.parent[n.child2] = (int)i;
-            else
-                for (size_t j = n.left; j < n.right; j++) S.leaf_of[vind_[j]] = (int)i;
-        }
-    }
-    // the replay's node states: per mode (a collecting replay's are not a strict one's)
+    // the replay's node states: per thread and mode (a collecting replay's are not a strict one's)
+    S.owner = id_;
+    S.gen = gen;
+    S.k = kpts;
+    S.known = known;
     S.collect = collect;
     S.delta = delta;
     S.node.assign(nn, CertNode());
     S.box.resize(nn * D * 2);
     S.box_set.assign(nn, 0);
-    if (!same_agg) {
-        S.owner = id_;
-        S.gen = gen;
-        S.k = kpts;
-        S.known = known;
-        S.agg.resize(nn * D * 4);
-        S.arg.resize(nn * D * 2);
-        // per node and dimension: min / max over its points whose bits are not known (exact-sum
-        // values) and over those known (the reference's values), children before parents
-        for (size_t i = nn; i-- > 0;) cert_agg_node(i);
-    }
     for (int d = 0; d < D; d++) {   // the root's cell box: the points' box
         S.box[2 * d] = iv_min(0, d);
         S.box[2 * d + 1] = iv_max(0, d);
@@ -581,11 +590,12 @@ void RefKDTree::cert_reset(double delta, const double *kpts, const uint8_t *know
 // One node's aggregates (children's first): min / max over the unknown points (and which ones)
 // and over the known points.
 void RefKDTree::cert_agg_node(size_t i) const {
-    CertScratch &S = cert_scratch();
     constexpr double INF = std::numeric_limits<double>::infinity();
     const int D = dim_;
-    double *a = &S.agg[i * D * 4];
-    uint32_t *g = &S.arg[i * D * 2];
+    const double *kp = agg_k_;
+    const uint8_t *known = agg_known_;
+    double *a = &agg_[i * D * 4];
+    uint32_t *g = &arg_[i * D * 2];
     const Node &n = nodes_[i];
     if (n.leaf) {
         for (int d = 0; d < D; d++) {
@@ -597,8 +607,8 @@ void RefKDTree::cert_agg_node(size_t i) const {
             const uint32_t p = (uint32_t)vind_[j];
             const size_t r = p * (size_t)D;
             for (int d = 0; d < D; d++) {
-                if (S.known[r + d]) {
-                    const double v = S.k[r + d];
+                if (known[r + d]) {
+                    const double v = kp[r + d];
                     a[4 * d + 2] = std::min(a[4 * d + 2], v);
                     a[4 * d + 3] = std::max(a[4 * d + 3], v);
                 } else {
@@ -610,8 +620,8 @@ void RefKDTree::cert_agg_node(size_t i) const {
         }
         return;
     }
-    const double *b = &S.agg[(size_t)n.child1 * D * 4], *c = &S.agg[(size_t)n.child2 * D * 4];
-    const uint32_t *gb = &S.arg[(size_t)n.child1 * D * 2], *gc = &S.arg[(size_t)n.child2 * D * 2];
+    const double *b = &agg_[(size_t)n.child1 * D * 4], *c = &agg_[(size_t)n.child2 * D * 4];
+    const uint32_t *gb = &arg_[(size_t)n.child1 * D * 2], *gc = &arg_[(size_t)n.child2 * D * 2];
     for (int d = 0; d < D; d++) {
         const bool lo1 = b[4 * d] <= c[4 * d], hi1 = b[4 * d + 1] >= c[4 * d + 1];
         a[4 * d] = lo1 ? b[4 * d] : c[4 * d];
@@ -626,12 +636,12 @@ void RefKDTree::cert_agg_node(size_t i) const {
 // The least (greatest) value of dimension d over node's points, over every allowed codebook.
 RefKDTree::Iv RefKDTree::iv_min(int node, int d) const {
     CertScratch &S = cert_scratch();
-    const double *a = &S.agg[((size_t)node * dim_ + d) * 4];
+    const double *a = &agg_[((size_t)node * dim_ + d) * 4];
     return {std::min(a[0] - S.delta, a[2]), std::min(a[0] + S.delta, a[2])};
 }
 RefKDTree::Iv RefKDTree::iv_max(int node, int d) const {
     CertScratch &S = cert_scratch();
-    const double *a = &S.agg[((size_t)node * dim_ + d) * 4];
+    const double *a = &agg_[((size_t)node * dim_ + d) * 4];
     return {std::max(a[1] - S.delta, a[3]), std::max(a[1] + S.delta, a[3])};
 }
 
@@ -656,17 +666,17 @@ void RefKDTree::certify_blame(const double *q, double delta, const double *kpts,
 void RefKDTree::cert_clear() const { cert_gen_.fetch_add(1, std::memory_order_acq_rel); }
 
 void RefKDTree::cert_update(const uint32_t *pts, size_t n) const {
-    const uint64_t gen = cert_gen_.fetch_add(1, std::memory_order_acq_rel) + 1;   // other threads: all anew
-    CertScratch &S = cert_scratch();
-    if (S.owner != id_ || !S.known || S.gen + 1 != gen) return;   // the next reset recomputes all
+    std::lock_guard<std::mutex> g(agg_mu_);
+    const uint64_t gen = cert_gen_.fetch_add(1, std::memory_order_acq_rel) + 1;   // the node states: all anew
+    if (agg_gen_.load(std::memory_order_acquire) + 1 != gen || parent_.size() != nodes_.size())
+        return;   // the next replay recomputes every aggregate
     const size_t nn = nodes_.size();
-    S.dirty.assign(nn, 0);
+    std::vector<uint8_t> dirty(nn, 0);
     for (size_t i = 0; i < n; i++)
-        for (int a = S.leaf_of[pts[i]]; a >= 0 && !S.dirty[a]; a = S.parent[a]) S.dirty[a] = 1;
+        for (int a = leaf_of_[pts[i]]; a >= 0 && !dirty[a]; a = parent_[a]) dirty[a] = 1;
     for (size_t i = nn; i-- > 0;)   // children before parents
-        if (S.dirty[i]) cert_agg_node(i);
-    S.gen = gen;
-    S.delta = -1;   // node states anew at the next replay, aggregates kept
+        if (dirty[i]) cert_agg_node(i);
+    agg_gen_.store(gen, std::memory_order_release);
 }
 
 // kd_nearest_flat (the reference's search) replayed over every codebook the certificate allows:

@@ -10,6 +10,7 @@
 #pragma once
 #include <atomic>
 #include <cstddef>
+#include <mutex>
 #include <cstdint>
 #include <vector>
 
@@ -122,12 +123,18 @@ private:
         std::vector<CertNode> node;
         std::vector<Iv> box;          // [node][dim][lo, hi]: the node's cell box, once its parent replayed
         std::vector<uint8_t> box_set;
-        std::vector<double> agg;      // [node][dim][min, max unknown | min, max known]
-        std::vector<uint32_t> arg;    // [node][dim][point at the unknown min, at the unknown max]
-        std::vector<int> parent;
-        std::vector<int> leaf_of;     // point -> its leaf
-        std::vector<uint8_t> dirty;   // cert_update's marks
     };
+    // the per-node aggregates, shared by the threads that replay (computed by the first of them
+    // for one (cert_gen_, kpts, known), then read only)
+    mutable std::mutex agg_mu_;
+    mutable std::atomic<uint64_t> agg_gen_{~0ull};
+    mutable const double *agg_k_ = nullptr;
+    mutable const uint8_t *agg_known_ = nullptr;
+    mutable std::vector<double> agg_;      // [node][dim][min, max unknown | min, max known]
+    mutable std::vector<uint32_t> arg_;    // [node][dim][point at the unknown min, at the unknown max]
+    mutable std::vector<int> parent_;
+    mutable std::vector<int> leaf_of_;     // point -> its leaf
+    void cert_ensure_agg(uint64_t gen, const double *kpts, const uint8_t *known) const;
     static CertScratch &cert_scratch();
     Iv piv(size_t p, int d) const {
         const CertScratch &S = cert_scratch();
