@@ -9,6 +9,7 @@
 #include <cmath>
 #include <limits>
 #include <memory>
+#include <thread>
 
 namespace qvq {
 
@@ -393,11 +394,10 @@ void RefKDTree::blame_dim(int node, int d, bool with_cell) const {
 bool RefKDTree::cert_split(int node) const {
     CertScratch &S = cert_scratch();
     const Node &n = nodes_[node];
-    CertNode &cn = S.node[node];
-    cn.state = 2;
+    CertNode &cn = cnode_[node];
     const bool collect = S.blame != nullptr;
     const int D = dim_;
-    const Iv *cb = &S.box[(size_t)node * D * 2];
+    const Iv *cb = &cbox_[(size_t)node * D * 2];
     const size_t *ind = vind_.data() + n.left;
     const size_t count = n.right - n.left;
     const double EPS = 0.00001;
@@ -516,17 +516,15 @@ bool RefKDTree::cert_split(int node) const {
             }
         }
     }
-    Iv *lb = &S.box[(size_t)n.child1 * D * 2], *rb = &S.box[(size_t)n.child2 * D * 2];
+    Iv *lb = &cbox_[(size_t)n.child1 * D * 2], *rb = &cbox_[(size_t)n.child2 * D * 2];
     std::copy(cb, cb + 2 * D, lb);
     std::copy(cb, cb + 2 * D, rb);
     lb[2 * c + 1] = cut;
     rb[2 * c] = cut;
-    S.box_set[n.child1] = S.box_set[n.child2] = 1;
     cn.dl = iv_max(n.child1, c);
     cn.dh = iv_min(n.child2, c);
     (void)c1;
     (void)c2;
-    cn.state = 1;
     return true;
 }
 
@@ -565,26 +563,38 @@ void RefKDTree::cert_reset(double delta, const double *kpts, const uint8_t *know
     const bool collect = S.blame != nullptr;
     const uint64_t gen = cert_gen_.load(std::memory_order_acquire);
     cert_ensure_agg(gen, kpts, known);
-    if (S.owner == id_ && S.gen == gen && S.k == kpts && S.known == known && S.delta == delta &&
-        S.collect == collect)
-        return;
-    const int D = dim_;
-    const size_t nn = nodes_.size();
-    // the replay's node states: per thread and mode (a collecting replay's are not a strict one's)
     S.owner = id_;
     S.gen = gen;
     S.k = kpts;
     S.known = known;
     S.collect = collect;
     S.delta = delta;
-    S.node.assign(nn, CertNode());
-    S.box.resize(nn * D * 2);
-    S.box_set.assign(nn, 0);
-    for (int d = 0; d < D; d++) {   // the root's cell box: the points' box
-        S.box[2 * d] = iv_min(0, d);
-        S.box[2 * d + 1] = iv_max(0, d);
+    // the shared node states for this key: reset by the first thread that brings a new key
+    // (the replays of one key start after it; a phase's threads share its key)
+    if (ckey_gen_.load(std::memory_order_acquire) == gen && ckey_delta_ == delta && ckey_k_ == kpts &&
+        ckey_known_ == known && ckey_collect_ == collect)
+        return;
+    std::lock_guard<std::mutex> g(agg_mu_);
+    if (ckey_gen_.load(std::memory_order_acquire) == gen && ckey_delta_ == delta && ckey_k_ == kpts &&
+        ckey_known_ == known && ckey_collect_ == collect)
+        return;
+    const int D = dim_;
+    const size_t nn = nodes_.size();
+    if (!cstate_ || cnode_.size() != nn) {
+        cstate_.reset(new std::atomic<int8_t>[nn]);
+        cnode_.assign(nn, CertNode());
+        cbox_.resize(nn * D * 2);
     }
-    S.box_set[0] = 1;
+    for (size_t i = 0; i < nn; i++) cstate_[i].store(0, std::memory_order_relaxed);
+    for (int d = 0; d < D; d++) {   // the root's cell box: the points' box
+        cbox_[2 * d] = iv_min(0, d);
+        cbox_[2 * d + 1] = iv_max(0, d);
+    }
+    ckey_delta_ = delta;
+    ckey_k_ = kpts;
+    ckey_known_ = known;
+    ckey_collect_ = collect;
+    ckey_gen_.store(gen, std::memory_order_release);
 }
 
 // One node's aggregates (children's first): min / max over the unknown points (and which ones)
@@ -693,7 +703,7 @@ int64_t RefKDTree::certified_search(const double *q, double delta, const double 
     double mlo = 0, mhi = 0;
     for (int d = 0; d < D; d++) {   // the initial distances against the root box
         const double x = q[d];
-        const Iv lo = S.box[2 * d], hi = S.box[2 * d + 1];
+        const Iv lo = cbox_[2 * d], hi = cbox_[2 * d + 1];
         dlo[d] = dhi[d] = 0;
         if ((!(x < lo.lo) && x < lo.hi) || (!(x > hi.hi) && x > hi.lo)) {
             if (!collect) return -1;
@@ -767,14 +777,27 @@ int64_t RefKDTree::certified_search(const double *q, double delta, const double 
             }
             return;
         }
-        if (S.node[node].state == 0 && S.box_set[node]) cert_split(node);
-        if (S.node[node].state != 1) {
+        int8_t st = cstate_[node].load(std::memory_order_acquire);
+        if (st == 0) {   // replayed once, by whichever thread gets here first
+            int8_t z = 0;
+            if (cstate_[node].compare_exchange_strong(z, 3, std::memory_order_acq_rel)) {
+                st = cert_split(node) ? 1 : 2;
+                cstate_[node].store(st, std::memory_order_release);
+            } else {
+                st = z;
+            }
+        }
+        while (st == 3) {
+            std::this_thread::yield();
+            st = cstate_[node].load(std::memory_order_acquire);
+        }
+        if (st != 1) {
             ok = false;
             return;
         }
         const int f = n.divfeat;
         const double val = q[f];
-        const CertNode &cn = S.node[node];
+        const CertNode &cn = cnode_[node];
         const double s_hi = (val - cn.dl.lo) + (val - cn.dh.lo), s_lo = (val - cn.dl.hi) + (val - cn.dh.hi);
         bool left_first = s_hi < 0;
         if (!(s_hi < 0) && !(s_lo >= 0)) {

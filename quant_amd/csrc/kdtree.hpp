@@ -10,6 +10,7 @@
 #pragma once
 #include <atomic>
 #include <cstddef>
+#include <memory>
 #include <mutex>
 #include <cstdint>
 #include <vector>
@@ -107,7 +108,6 @@ private:
     // certified_search's replay: the values each build quantity takes over all splits allowed
     struct Iv { double lo, hi; };
     struct CertNode {
-        int8_t state = 0;   // 0 not replayed, 1 the same split for every such codebook, 2 not shown
         Iv dl{0, 0}, dh{0, 0};   // divlow, divhigh
     };
     // the replay's state, per thread (replays of one tree may run on several threads) and
@@ -120,10 +120,19 @@ private:
         const uint8_t *known = nullptr;
         bool collect = false;            // the cache's mode
         std::vector<uint32_t> *blame = nullptr;   // collecting (certify_blame)
-        std::vector<CertNode> node;
-        std::vector<Iv> box;          // [node][dim][lo, hi]: the node's cell box, once its parent replayed
-        std::vector<uint8_t> box_set;
     };
+    // the replayed nodes, shared by the threads that replay with one key (cert_gen_, delta,
+    // kpts, known, mode): a node's state goes 0 -> 3 (being replayed by one thread) -> 1 (the
+    // same split for every allowed codebook; its children's cell boxes and its divlow /
+    // divhigh set) or 2 (not shown)
+    mutable std::unique_ptr<std::atomic<int8_t>[]> cstate_;
+    mutable std::vector<CertNode> cnode_;   // dl, dh
+    mutable std::vector<Iv> cbox_;          // [node][dim][lo, hi]: the node's cell box
+    mutable std::atomic<uint64_t> ckey_gen_{~0ull};
+    mutable double ckey_delta_ = -1;
+    mutable const double *ckey_k_ = nullptr;
+    mutable const uint8_t *ckey_known_ = nullptr;
+    mutable bool ckey_collect_ = false;
     // the per-node aggregates, shared by the threads that replay (computed by the first of them
     // for one (cert_gen_, kpts, known), then read only)
     mutable std::mutex agg_mu_;
