@@ -354,20 +354,21 @@ void RefKDTree::near_set(const double *q, double slack_rel, double slack_abs, st
 }
 
 // Blame (the collecting run): the points holding the least and greatest value in dimension d
-// among node's points whose bits are not known (the aggregates keep them).
-// Small nodes: every such point at the extreme value (duplicated code vectors).
+// among node's points whose bits are not known, every one at that value (duplicated code
+// vectors).  A large node finds them by descending to a leaf through the children whose
+// aggregate holds the value (O(depth), not a scan).
 void RefKDTree::blame_extremes(int node, int d) const {
     CertScratch &S = cert_scratch();
-    const uint32_t *g = &arg_[((size_t)node * dim_ + d) * 2];
-    const Node &n = nodes_[node];
-    if (n.right - n.left > 256) {
-        for (int k = 0; k < 2; k++)
-            if (g[k] != ~0u) S.blame->push_back(g[k]);
-        return;
-    }
-    for (int k = 0; k < 2; k++) {
-        if (g[k] == ~0u) continue;
-        const double v = ptr(g[k], d);
+    for (int s = 0; s < 2; s++) {
+        const size_t off = (size_t)s * dim_ + d;
+        const double v = agg_[(size_t)node * dim_ * 4 + off];
+        if (std::isinf(v)) continue;   // no unknown point
+        int m = node;
+        while (nodes_[m].right - nodes_[m].left > 256 && !nodes_[m].leaf) {
+            const Node &n = nodes_[m];
+            m = agg_[(size_t)n.child1 * dim_ * 4 + off] == v ? n.child1 : n.child2;
+        }
+        const Node &n = nodes_[m];
         for (size_t i = n.left; i < n.right; i++) {
             const size_t p = vind_[i];
             if (ptr(p, d) == v && !S.known[p * (size_t)dim_ + d]) S.blame->push_back((uint32_t)p);
@@ -551,7 +552,6 @@ void RefKDTree::cert_ensure_agg(uint64_t gen, const double *kpts, const uint8_t 
     agg_k_ = kpts;
     agg_known_ = known;
     agg_.resize(nn * dim_ * 4);
-    arg_.resize(nn * dim_ * 2);
     // per node and dimension: min / max over its points whose bits are not known (exact-sum
     // values) and over those known (the reference's values), children before parents
     for (size_t i = nn; i-- > 0;) cert_agg_node(i);
@@ -597,62 +597,49 @@ void RefKDTree::cert_reset(double delta, const double *kpts, const uint8_t *know
     ckey_gen_.store(gen, std::memory_order_release);
 }
 
-// One node's aggregates (children's first): min / max over the unknown points (and which ones)
-// and over the known points.
+// One node's aggregates (children's first): min / max over the unknown points and over the known
+// points, stored [min unknown | max unknown | min known | max known][dim] so that the loops
+// below are plain element-wise min / max (vectorised; a branch per value mispredicted on the
+// irregular known pattern).
 void RefKDTree::cert_agg_node(size_t i) const {
     constexpr double INF = std::numeric_limits<double>::infinity();
     const int D = dim_;
-    const double *kp = agg_k_;
-    const uint8_t *known = agg_known_;
-    double *a = &agg_[i * D * 4];
-    uint32_t *g = &arg_[i * D * 2];
+    double *__restrict mnu = &agg_[i * D * 4], *__restrict mxu = mnu + D, *__restrict mnk = mxu + D,
+                       *__restrict mxk = mnk + D;
     const Node &n = nodes_[i];
     if (n.leaf) {
-        for (int d = 0; d < D; d++) {
-            a[4 * d] = a[4 * d + 2] = INF;
-            a[4 * d + 1] = a[4 * d + 3] = -INF;
-            g[2 * d] = g[2 * d + 1] = ~0u;
-        }
+        for (int d = 0; d < D; d++) mnu[d] = mnk[d] = INF, mxu[d] = mxk[d] = -INF;
         for (size_t j = n.left; j < n.right; j++) {
-            const uint32_t p = (uint32_t)vind_[j];
-            const size_t r = p * (size_t)D;
+            const size_t r = vind_[j] * (size_t)D;
+            const double *__restrict x = pts_ + r, *__restrict kv = agg_k_ + r;
+            const uint8_t *__restrict k = agg_known_ + r;
             for (int d = 0; d < D; d++) {
-                if (known[r + d]) {
-                    const double v = kp[r + d];
-                    a[4 * d + 2] = std::min(a[4 * d + 2], v);
-                    a[4 * d + 3] = std::max(a[4 * d + 3], v);
-                } else {
-                    const double v = pts_[r + d];
-                    if (v < a[4 * d]) a[4 * d] = v, g[2 * d] = p;
-                    if (v > a[4 * d + 1]) a[4 * d + 1] = v, g[2 * d + 1] = p;
-                }
+                const bool kk = k[d] != 0;
+                mnu[d] = std::min(mnu[d], kk ? INF : x[d]);
+                mxu[d] = std::max(mxu[d], kk ? -INF : x[d]);
+                mnk[d] = std::min(mnk[d], kk ? kv[d] : INF);
+                mxk[d] = std::max(mxk[d], kk ? kv[d] : -INF);
             }
         }
         return;
     }
-    const double *b = &agg_[(size_t)n.child1 * D * 4], *c = &agg_[(size_t)n.child2 * D * 4];
-    const uint32_t *gb = &arg_[(size_t)n.child1 * D * 2], *gc = &arg_[(size_t)n.child2 * D * 2];
-    for (int d = 0; d < D; d++) {
-        const bool lo1 = b[4 * d] <= c[4 * d], hi1 = b[4 * d + 1] >= c[4 * d + 1];
-        a[4 * d] = lo1 ? b[4 * d] : c[4 * d];
-        g[2 * d] = lo1 ? gb[2 * d] : gc[2 * d];
-        a[4 * d + 1] = hi1 ? b[4 * d + 1] : c[4 * d + 1];
-        g[2 * d + 1] = hi1 ? gb[2 * d + 1] : gc[2 * d + 1];
-        a[4 * d + 2] = std::min(b[4 * d + 2], c[4 * d + 2]);
-        a[4 * d + 3] = std::max(b[4 * d + 3], c[4 * d + 3]);
-    }
+    const double *__restrict b = &agg_[(size_t)n.child1 * D * 4], *__restrict c = &agg_[(size_t)n.child2 * D * 4];
+    for (int d = 0; d < D; d++) mnu[d] = std::min(b[d], c[d]);
+    for (int d = D; d < 2 * D; d++) mxu[d - D] = std::max(b[d], c[d]);
+    for (int d = 2 * D; d < 3 * D; d++) mnk[d - 2 * D] = std::min(b[d], c[d]);
+    for (int d = 3 * D; d < 4 * D; d++) mxk[d - 3 * D] = std::max(b[d], c[d]);
 }
 
 // The least (greatest) value of dimension d over node's points, over every allowed codebook.
 RefKDTree::Iv RefKDTree::iv_min(int node, int d) const {
     CertScratch &S = cert_scratch();
-    const double *a = &agg_[((size_t)node * dim_ + d) * 4];
-    return {std::min(a[0] - S.delta, a[2]), std::min(a[0] + S.delta, a[2])};
+    const double *a = &agg_[(size_t)node * dim_ * 4 + d];
+    return {std::min(a[0] - S.delta, a[2 * dim_]), std::min(a[0] + S.delta, a[2 * dim_])};
 }
 RefKDTree::Iv RefKDTree::iv_max(int node, int d) const {
     CertScratch &S = cert_scratch();
-    const double *a = &agg_[((size_t)node * dim_ + d) * 4];
-    return {std::max(a[1] - S.delta, a[3]), std::max(a[1] + S.delta, a[3])};
+    const double *a = &agg_[(size_t)node * dim_ * 4 + d];
+    return {std::max(a[dim_] - S.delta, a[3 * dim_]), std::max(a[dim_] + S.delta, a[3 * dim_])};
 }
 
 namespace {

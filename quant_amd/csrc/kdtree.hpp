@@ -139,8 +139,7 @@ private:
     mutable std::atomic<uint64_t> agg_gen_{~0ull};
     mutable const double *agg_k_ = nullptr;
     mutable const uint8_t *agg_known_ = nullptr;
-    mutable std::vector<double> agg_;      // [node][dim][min, max unknown | min, max known]
-    mutable std::vector<uint32_t> arg_;    // [node][dim][point at the unknown min, at the unknown max]
+    mutable std::vector<double> agg_;      // [node][min unknown | max unknown | min known | max known][dim]
     mutable std::vector<int> parent_;
     mutable std::vector<int> leaf_of_;     // point -> its leaf
     void cert_ensure_agg(uint64_t gen, const double *kpts, const uint8_t *known) const;
