@@ -70,6 +70,8 @@ def parse():
     ap.add_argument("--share-steps", type=int, default=3,
                     help="0 disables the c5_rank_share sub-object (N=8 per-rank share through a 1-rank RCCL communicator)")
     ap.add_argument("--e2e-reps", type=int, default=7, help="0 disables the end_to_end sub-object (the first rep after a reconfiguration is not timed; the second still pays first-use costs, hence the median of 7)")
+    ap.add_argument("--exact-reps", type=int, default=2,
+                    help="0 disables the exact_cie1931 sub-object (exact mode on the C3 raster's CIE1931 blocks)")
     ap.add_argument("--dry-run", action="store_true", help="CPU only: start the ranks, join gloo, print the plan")
     return ap.parse_args()
 
@@ -179,6 +181,53 @@ def synthetic_raster(S, seed):
             v = sm[ch].astype(np.int64) + (z % np.uint64(33)).astype(np.int64) - 16
             out[:, ch] = np.clip(v, 0, 255)
     return out.ravel()
+
+
+def cie_blocks(rgb, S):
+    """The 2x2 blocks (getBlocksAsVectorsFromImage: x-major blocks and pixels, src/Compressor.cpp:31-62)
+    of an S x S raster's signed-char values, each pixel mapped through CIE1931 (src/ColorSpace.cpp:30-38):
+    values off the byte grid, which only the exact mode (k_exact.hip) takes."""
+    p = rgb.reshape(S * S, 3).view(np.int8).astype(np.float64)
+    xyz = np.empty_like(p)
+    xyz[:, 0] = (p[:, 0] * 0.490 + p[:, 1] * 0.310 + p[:, 2] * 0.200) / 0.17697
+    xyz[:, 1] = (p[:, 0] * 0.17697 + p[:, 1] * 0.81240 + p[:, 2] * 0.01063) / 0.17697
+    xyz[:, 2] = (p[:, 0] * 0 + p[:, 1] * 0.01 + p[:, 2] * 0.99) / 0.17697
+    return np.ascontiguousarray(xyz.reshape(S // 2, 2, S // 2, 2, 3).transpose(0, 2, 1, 3, 4).reshape(-1, 12))
+
+
+def exact_cie(args, eng, cpu):
+    """Exact mode measured: qvq_lbg on the C3 raster's CIE1931 blocks (wall per quantize, inputs
+    resident), and with cpu the oracle's Kahan rule on a bounded sample (512 x 512) beside it."""
+    X = cie_blocks(synthetic_raster(args.size, 0x5EED), args.size)
+    eng.set_vectors(X, exact=True)
+    eng.lbg(args.bits, want_assign=False)   # warm-up (allocations)
+    ms = []
+    for _ in range(args.exact_reps):
+        t = time.perf_counter()
+        eng.lbg(args.bits, want_assign=False)
+        ms.append((time.perf_counter() - t) * 1e3)
+    tm = eng.timings()
+    best = min(ms)
+    out = {"workload": "C3 raster (%dx%d, 2x2 blocks) mapped through CIE1931, %d code vectors, exact mode "
+                       "(fp64 search in nanoflann order + Kahan chains, the reference's arithmetic bit for bit)"
+                       % (args.size, args.size, 1 << args.bits),
+           "rows": int(X.shape[0]), "ms_per_quantize": round(best, 2), "reps": args.exact_reps,
+           "Mblocks_per_s": round(X.shape[0] * args.bits / best / 1e3, 3),
+           "assign_ms": [round(v, 2) for v in tm["assign_ms"]], "update_ms": [round(v, 2) for v in tm["update_ms"]],
+           "phases": "per level, wall: assign = fp64 search + tie answers; update = stable sort + Kahan chains"}
+    if cpu:
+        from oracle import oracle
+        s = 512
+        Xs = cie_blocks(synthetic_raster(s, 0x5EED), s)
+        threads = args.cpu_threads or min(16, os.cpu_count() or 1)
+        t = time.perf_counter()
+        oracle.lbg(Xs, args.bits, sum_mode=0, threads=threads)
+        cs = time.perf_counter() - t
+        out["cpu_baseline"] = {"kind": "port", "sample": "%dx%d CIE1931 blocks (%d rows), %d levels, oracle Kahan rule"
+                                                        % (s, s, Xs.shape[0], args.bits),
+                               "cores": threads, "Mblocks_per_s": round(Xs.shape[0] * args.bits / cs / 1e6, 3)}
+    del X
+    return out
 
 
 def main():
@@ -418,6 +467,12 @@ def main():
                                 "ms": round(med * 1e3, 3), "Mblocks_per_s": round(n_local * args.bits / med / 1e6, 3),
                                 "reps": args.e2e_reps}
         result["end_to_end_ms"] = round(med * 1e3, 3)
+    if world == 1 and args.exact_reps > 0:
+        e3 = quant_amd.Engine(local)
+        try:
+            result["exact_cie1931"] = exact_cie(args, e3, not args.no_cpu_baseline)
+        finally:
+            e3.close()
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         try:
             cb = cpu_baseline(args)

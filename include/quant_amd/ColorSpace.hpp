@@ -1,7 +1,7 @@
 // quant_amd C++ API -- colour spaces (reference: include/ColorSpace.hpp, src/ColorSpace.cpp).
 // NORMAL: the signed byte as a double.  SCALED: (byte + 128) / 255.  CIE1931: the
-// reference's linear maps (host conversions only; the engine sums NORMAL/SCALED exactly
-// and rejects CIE1931 training sets).
+// reference's linear maps (host conversions; the engine sums NORMAL/SCALED byte images exactly,
+// and CIE1931 training sets go through its exact mode, the reference's Kahan arithmetic).
 #pragma once
 #include <memory>
 

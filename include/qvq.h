@@ -54,8 +54,8 @@ enum { QVQ_CS_NORMAL = 0, QVQ_CS_SCALED = 1, QVQ_CS_CIE1931 = 2 };
 typedef struct {
     int levels;                 /* split levels run by the last qvq_lbg */
     double total_ms;            /* whole qvq_lbg, host wall */
-    double assign_ms[32];       /* device time of the assignment kernel per level */
-    double update_ms[32];       /* device time of the centroid-sum kernel per level */
+    double assign_ms[32];       /* device time of the assignment kernel per level (exact mode: wall time) */
+    double update_ms[32];       /* device time of the centroid-sum kernel per level (exact mode: wall time) */
     double other_ms[32];        /* rest of the level: recheck, kd-tree ties, reduce, finalize + tables */
     uint64_t flagged[32];       /* rows re-checked in fp64 per level */
     uint64_t host_ties[32];     /* exact fp64 ties per level, answered by the reference kd-tree

@@ -1896,11 +1896,17 @@ qvq_status lbg_exact(qvq_ctx *ctx, uint32_t bits, double *codebook, uint32_t *as
         }
         HIPCHK(hipMemcpyAsync(ctx->d_C64_split, hS.data(), (size_t)K * D * 8, hipMemcpyHostToDevice, ctx->stream));
         unsigned nt = 0;
-        if ((st = exact_assign(ctx, hS.data(), K, nt)) != QVQ_OK) return st;
+        const auto ta = std::chrono::steady_clock::now();
+        if ((st = exact_assign(ctx, hS.data(), K, nt)) != QVQ_OK) return st;   // synchronous
+        const auto tb = std::chrono::steady_clock::now();
         ctx->tm.host_ties[lvl - 1] = nt;
         if ((st = exact_centroids(ctx, false, K, nullptr)) != QVQ_OK) return st;
         HIPCHK(hipMemcpyAsync(hC.data(), ctx->d_C64_cent, (size_t)K * D * 8, hipMemcpyDeviceToHost, ctx->stream));
         if ((st = wait_stream(ctx)) != QVQ_OK) return st;
+        // wall times: assign (search + ties) and update (sort + Kahan chains + codebook copy)
+        ctx->tm.assign_ms[lvl - 1] = std::chrono::duration<float, std::milli>(tb - ta).count();
+        ctx->tm.update_ms[lvl - 1] =
+            std::chrono::duration<float, std::milli>(std::chrono::steady_clock::now() - tb).count();
     }
     // updateDistortion after the last fix (src/Quantizer.cpp:9-22)
     double dist = 0;
