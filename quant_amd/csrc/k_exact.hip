@@ -12,6 +12,9 @@
 // Kahan is sequential by definition: one thread per (code vector, component) chain, the row
 // loads prefetched ahead of the dependent adds.  Built with -ffp-contract=off (no FMA
 // contraction inside the compensation).
+#include <cstdlib>
+#include <cstring>
+
 #include <hipcub/hipcub.hpp>
 
 #include "common.hpp"
@@ -20,36 +23,70 @@ namespace qvq {
 
 constexpr int EX_THREADS = 256;
 
-// A[row] = the lexicographic (fp64 distance, index) minimum over the K code vectors of C
-// ([K][D], staged in LDS when lds); rows whose best two distances are within tie_rel go to ties.
+// A[row] = the lexicographic (fp64 distance, index) minimum over the K code vectors of C ([K][D]);
+// rows whose best two distances are within tie_rel go to ties.  The codebook is staged in LDS
+// in chunks of kc code vectors (kc * D * 8 <= EX_LDS_BYTES; one chunk when it fits), ascending,
+// so every row still scans k in ascending order; each lane keeps its row's best two across chunks.
+constexpr uint32_t EX_LDS_BYTES = 64 * 1024;
+
 __global__ __launch_bounds__(EX_THREADS) void exact_assign_kernel(const double *__restrict__ X, uint64_t N, uint32_t D,
-                                                                  const double *__restrict__ C, uint32_t K, bool lds,
+                                                                  const double *__restrict__ C, uint32_t K, uint32_t kc,
                                                                   double tie_rel, uint32_t *__restrict__ A,
                                                                   uint32_t *__restrict__ ties,
                                                                   unsigned *__restrict__ tie_cnt) {
     extern __shared__ double cs[];
-    if (lds) {
+    const uint64_t stride = (uint64_t)gridDim.x * EX_THREADS;
+    const uint64_t first = (uint64_t)blockIdx.x * EX_THREADS + threadIdx.x;
+    if (kc >= K) {   // the whole codebook in LDS: grid-stride over rows
         for (uint32_t i = threadIdx.x; i < K * D; i += EX_THREADS) cs[i] = C[i];
         __syncthreads();
+        for (uint64_t row = first; row < N; row += stride) {
+            const double *x = X + row * D;
+            double d1 = INFINITY, d2 = INFINITY;
+            uint32_t k1 = 0;
+            for (uint32_t k = 0; k < K; k++) {
+                const double d = ref_l2_hd(x, cs + (size_t)k * D, (int)D);
+                if (d < d1) {   // ascending k: the first minimum is the lowest index
+                    d2 = d1;
+                    d1 = d;
+                    k1 = k;
+                } else if (d < d2) {
+                    d2 = d;
+                }
+            }
+            A[row] = k1;
+            if (d2 - d1 <= tie_rel * d1) ties[atomicAdd(tie_cnt, 1u)] = (uint32_t)row;
+        }
+        return;
     }
-    const double *cb = lds ? cs : C;
-    for (uint64_t row = (uint64_t)blockIdx.x * EX_THREADS + threadIdx.x; row < N;
-         row += (uint64_t)gridDim.x * EX_THREADS) {
-        const double *x = X + row * D;
+    // chunked: one row per lane per pass (the grid covers N), the chunks staged in turn
+    for (uint64_t base = (uint64_t)blockIdx.x * EX_THREADS; base < N; base += stride) {
+        const uint64_t row = base + threadIdx.x;
+        const bool live = row < N;
+        const double *x = X + (live ? row : 0) * D;
         double d1 = INFINITY, d2 = INFINITY;
         uint32_t k1 = 0;
-        for (uint32_t k = 0; k < K; k++) {
-            const double d = ref_l2_hd(x, cb + (size_t)k * D, (int)D);
-            if (d < d1) {   // ascending k: the first minimum is the lowest index
-                d2 = d1;
-                d1 = d;
-                k1 = k;
-            } else if (d < d2) {
-                d2 = d;
+        for (uint32_t k0 = 0; k0 < K; k0 += kc) {
+            const uint32_t n = min(kc, K - k0);
+            __syncthreads();   // the previous chunk is read by every lane
+            for (uint32_t i = threadIdx.x; i < n * D; i += EX_THREADS) cs[i] = C[(size_t)k0 * D + i];
+            __syncthreads();
+            if (!live) continue;
+            for (uint32_t k = 0; k < n; k++) {
+                const double d = ref_l2_hd(x, cs + (size_t)k * D, (int)D);
+                if (d < d1) {
+                    d2 = d1;
+                    d1 = d;
+                    k1 = k0 + k;
+                } else if (d < d2) {
+                    d2 = d;
+                }
             }
         }
-        A[row] = k1;
-        if (d2 - d1 <= tie_rel * d1) ties[atomicAdd(tie_cnt, 1u)] = (uint32_t)row;
+        if (live) {
+            A[row] = k1;
+            if (d2 - d1 <= tie_rel * d1) ties[atomicAdd(tie_cnt, 1u)] = (uint32_t)row;
+        }
     }
 }
 
@@ -104,6 +141,75 @@ __global__ __launch_bounds__(EX_THREADS) void kahan_centroids_kernel(const doubl
     if (cnt && d == 0) cnt[k] = n;
 }
 
+// The same chains for few, long cells (K <= KC_MAX_K, D <= 64: the mean and the first levels, a
+// chain of up to N steps): one workgroup per code vector; waves 1-3 stage the cell's rows, tile
+// by tile (KC_TILE_BYTES, double-buffered), from HBM into LDS while wave 0's lanes run the D
+// chains over the previous tile from LDS.  The per-thread kernel above waits on two dependent
+// global loads (order, then the row) per 16 steps; here the chain only waits on LDS reads issued
+// 16 ahead of the dependent adds.
+constexpr int KC_THREADS = 256;
+constexpr uint32_t KC_TILE_BYTES = 32 * 1024;   // two buffers: the 64 KB dynamic LDS default
+constexpr uint32_t KC_MAX_K = 64;
+
+__global__ __launch_bounds__(KC_THREADS) void kahan_chains_lds_kernel(const double *__restrict__ X, uint64_t N,
+                                                                      uint32_t D, const uint32_t *__restrict__ order,
+                                                                      const uint32_t *__restrict__ koff, double *__restrict__ C,
+                                                                      uint64_t *__restrict__ cnt) {
+    extern __shared__ double tiles[];   // [2][T * D]
+    const uint32_t k = blockIdx.x;
+    const uint32_t T = KC_TILE_BYTES / 8 / D;
+    const uint64_t b = order ? koff[k] : 0, e = order ? koff[k + 1] : N;
+    const uint64_t n = e - b, ntiles = (n + T - 1) / T;
+    const uint32_t wave = threadIdx.x / 64, lane = threadIdx.x % 64;
+    auto stage = [&](uint64_t t) {   // waves 1..3: tile t of the cell into buffer t & 1
+        double *buf = tiles + (t & 1) * (size_t)T * D;
+        const uint64_t r0 = b + t * T;
+        const uint32_t cnt_el = (uint32_t)min<uint64_t>(T, e - r0) * D;
+        for (uint32_t i = threadIdx.x - 64; i < cnt_el; i += KC_THREADS - 64) {
+            const uint32_t r = i / D, d = i - r * D;
+            const uint64_t row = order ? order[r0 + r] : r0 + r;
+            buf[i] = X[row * D + d];
+        }
+    };
+    double sum = 0.0, c = 0.0;
+    if (wave != 0 && ntiles) stage(0);
+    __syncthreads();
+    for (uint64_t t = 0; t < ntiles; t++) {
+        if (wave != 0) {
+            if (t + 1 < ntiles) stage(t + 1);
+        } else if (lane < D) {
+            const double *cur = tiles + (t & 1) * (size_t)T * D + lane;
+            const uint32_t rows = (uint32_t)min<uint64_t>(T, e - (b + t * T));
+            uint32_t r = 0;
+            constexpr int U = 16;
+            for (; r + U <= rows; r += U) {
+                double v[U];
+#pragma unroll
+                for (int u = 0; u < U; u++) v[u] = cur[(size_t)(r + u) * D];
+#pragma unroll
+                for (int u = 0; u < U; u++) {
+                    const double y = v[u] - c;
+                    const double s = sum + y;
+                    c = (s - sum) - y;
+                    sum = s;
+                }
+            }
+            for (; r < rows; r++) {
+                const double y = cur[(size_t)r * D] - c;
+                const double s = sum + y;
+                c = (s - sum) - y;
+                sum = s;
+            }
+        }
+        __syncthreads();
+    }
+    if (wave == 0 && lane < D) {
+        if (n) sum *= 1.0 / (double)n;   // operator/= by a scalar under -freciprocal-math
+        C[(size_t)k * D + lane] = sum;
+        if (cnt && lane == 0) cnt[k] = n;
+    }
+}
+
 // Per-block partials of sum_rows ||x - C[A[row]]||^2 (norm of the difference: squares added in
 // component order, include/VectorOperations.hpp:107-111); exact_sum_kernel adds them in order.
 __global__ __launch_bounds__(EX_THREADS) void exact_dist_kernel(const double *__restrict__ X, uint64_t N, uint32_t D,
@@ -154,9 +260,10 @@ static int grid_for(uint64_t items, int cap = 4096) {
 
 hipError_t launch_exact_assign(hipStream_t s, const double *X, uint64_t N, uint32_t D, const double *C, uint32_t K,
                                double tie_rel, uint32_t *A, uint32_t *ties, unsigned *tie_cnt) {
-    const bool lds = (size_t)K * D * 8 <= 64 * 1024;
-    hipLaunchKernelGGL(exact_assign_kernel, dim3(grid_for(N, 8192)), dim3(EX_THREADS), lds ? (size_t)K * D * 8 : 0, s, X,
-                       N, D, C, K, lds, tie_rel, A, ties, tie_cnt);
+    const uint32_t kc = (uint32_t)std::max<size_t>(1, EX_LDS_BYTES / (8 * (size_t)D));   // code vectors per chunk
+    const size_t lds = (size_t)std::min(kc, K) * D * 8;
+    hipLaunchKernelGGL(exact_assign_kernel, dim3(grid_for(N, 8192)), dim3(EX_THREADS), lds, s, X, N, D, C, K, kc,
+                       tie_rel, A, ties, tie_cnt);
     return hipGetLastError();
 }
 
@@ -170,9 +277,16 @@ size_t exact_sort_temp_bytes(uint64_t N) {
 hipError_t launch_exact_centroids(hipStream_t s, const double *X, uint64_t N, uint32_t D, const uint32_t *A, uint32_t K,
                                   uint32_t *keys_out, uint32_t *iota, uint32_t *order, uint32_t *koff, void *temp,
                                   size_t temp_bytes, double *C, uint64_t *cnt) {
+    static const bool thread_chains = std::getenv("QVQ_EXACT_CHAINS") && !std::strcmp(std::getenv("QVQ_EXACT_CHAINS"), "thread");   // A/B
+    const bool lds_chains = !thread_chains && D <= 64 && (!A || K <= KC_MAX_K);
+    const size_t lds_bytes = lds_chains ? 2 * (size_t)(KC_TILE_BYTES / 8 / D) * D * 8 : 0;
     if (!A) {   // the mean: every row, in order
-        hipLaunchKernelGGL(kahan_centroids_kernel, dim3(grid_for((uint64_t)D)), dim3(EX_THREADS), 0, s, X, N, D,
-                           (const uint32_t *)nullptr, (const uint32_t *)nullptr, 1u, C, cnt);
+        if (lds_chains)
+            hipLaunchKernelGGL(kahan_chains_lds_kernel, dim3(1), dim3(KC_THREADS), lds_bytes, s, X, N, D,
+                               (const uint32_t *)nullptr, (const uint32_t *)nullptr, C, cnt);
+        else
+            hipLaunchKernelGGL(kahan_centroids_kernel, dim3(grid_for((uint64_t)D)), dim3(EX_THREADS), 0, s, X, N, D,
+                               (const uint32_t *)nullptr, (const uint32_t *)nullptr, 1u, C, cnt);
         return hipGetLastError();
     }
     int bits = 1;
@@ -181,8 +295,12 @@ hipError_t launch_exact_centroids(hipStream_t s, const double *X, uint64_t N, ui
     hipError_t e = hipcub::DeviceRadixSort::SortPairs(temp, temp_bytes, A, keys_out, iota, order, (int)N, 0, bits, s);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(exact_koff_kernel, dim3((K + 1 + 255) / 256), dim3(256), 0, s, keys_out, N, K, koff);
-    hipLaunchKernelGGL(kahan_centroids_kernel, dim3(grid_for((uint64_t)K * D, 1u << 30)), dim3(EX_THREADS), 0, s, X, N,
-                       D, order, koff, K, C, cnt);
+    if (lds_chains)
+        hipLaunchKernelGGL(kahan_chains_lds_kernel, dim3(K), dim3(KC_THREADS), lds_bytes, s, X, N, D, order, koff, C,
+                           cnt);
+    else
+        hipLaunchKernelGGL(kahan_centroids_kernel, dim3(grid_for((uint64_t)K * D, 1u << 30)), dim3(EX_THREADS), 0, s, X,
+                           N, D, order, koff, K, C, cnt);
     return hipGetLastError();
 }
 
