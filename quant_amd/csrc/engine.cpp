@@ -1465,7 +1465,14 @@ qvq_status ensure_speculation(qvq_ctx *ctx, uint32_t Kmax) {
             HIPCHK(hipHostGetDevicePointer(reinterpret_cast<void **>(&ctx->dh_tx[i]), ctx->h_tx[i], 0));
         }
     }
-    if (!ctx->vstream) HIPCHK(hipStreamCreateWithFlags(&ctx->vstream, hipStreamNonBlocking));
+    if (!ctx->vstream) {   // high priority: the check's few short kernels go ahead of the next search's queued blocks
+        int lo = 0, hi = 0;
+        static const bool prio = !env_is("QVQ_VSTREAM_PRIO", "0");   // A/B
+        if (prio && hipDeviceGetStreamPriorityRange(&lo, &hi) == hipSuccess && hi != lo)
+            HIPCHK(hipStreamCreateWithPriority(&ctx->vstream, hipStreamNonBlocking, hi));
+        else
+            HIPCHK(hipStreamCreateWithFlags(&ctx->vstream, hipStreamNonBlocking));
+    }
     for (auto &v : ctx->ver)
         if (!v.ev) HIPCHK(hipEventCreateWithFlags(&v.ev, hipEventDisableTiming));
     return Kmax >= 4 ? ensure_kahan(ctx, Kmax / 2) : QVQ_OK;
@@ -1998,7 +2005,7 @@ QVQ_API qvq_status qvq_lbg(qvq_ctx *ctx, uint32_t bits, double eps, double *code
         out_enqueued = true;
         return QVQ_OK;
     };
-    for (int attempt = 0;; attempt++) {
+    for (;;) {   // once, or twice when a speculative check fails
     out_enqueued = false;
     HIPCHK(launch_mean_sums(ctx->stream, ctx->Dp, ctx->d_codes, ctx->N, ctx->D, ctx->d_plut, ctx->d_mean,
                             ctx->d_counters, N_COUNTERS, d_dist, hist, ctx->d_lut64));

@@ -10,3 +10,10 @@ QVQ_EXACT_CHAINS=thread timeout -k 10 400 python3 tools/exact_c3.py --reps 1 > g
 cat gpurun_out/exact_c3_thread.log
 echo
 bash tools/gpu_r04d.sh
+echo "== A/B check stream priority"
+for p in 1 0; do
+QVQ_VSTREAM_PRIO=$p timeout -k 10 120 python3 tools/c4_trace.py > gpurun_out/c4t_p$p.log 2>&1 || exit 1
+echo "prio=$p c4: $(grep -h 'quantize' gpurun_out/c4t_p$p.log | tr '\n' ' ')"
+QVQ_VSTREAM_PRIO=$p timeout -k 10 120 python3 tools/quick_timing.py 4096,2,10 > gpurun_out/c3q_p$p.log 2>&1 || exit 1
+echo "prio=$p c3: $(grep -o '"wall_ms": [0-9.]*' gpurun_out/c3q_p$p.log | tr '\n' ' ')"
+done
