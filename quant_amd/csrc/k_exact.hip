@@ -141,15 +141,15 @@ __global__ __launch_bounds__(EX_THREADS) void kahan_centroids_kernel(const doubl
     if (cnt && d == 0) cnt[k] = n;
 }
 
-// The same chains for few, long cells (K <= KC_MAX_K, D <= 64: the mean and the first levels, a
-// chain of up to N steps): one workgroup per code vector; waves 1-3 stage the cell's rows, tile
-// by tile (KC_TILE_BYTES, double-buffered), from HBM into LDS while wave 0's lanes run the D
-// chains over the previous tile from LDS.  The per-thread kernel above waits on two dependent
+// The same chains, staged (D <= 64; the mean's chain is N steps, and a level's time is its
+// largest cell's chain, which on skewed data stays long at every K): one workgroup per code
+// vector; waves 1-3 stage the cell's rows, tile by tile (KC_TILE_BYTES, double-buffered), from
+// HBM into LDS while wave 0's lanes run the D chains over the previous tile from LDS.  The per-thread kernel above waits on two dependent
 // global loads (order, then the row) per 16 steps; here the chain only waits on LDS reads issued
 // 16 ahead of the dependent adds.
 constexpr int KC_THREADS = 256;
 constexpr uint32_t KC_TILE_BYTES = 32 * 1024;   // two buffers: the 64 KB dynamic LDS default
-constexpr uint32_t KC_MAX_K = 64;
+constexpr uint32_t KC_MAX_K = 1u << 20;   // every level (the largest cell sets a level's time)
 
 __global__ __launch_bounds__(KC_THREADS) void kahan_chains_lds_kernel(const double *__restrict__ X, uint64_t N,
                                                                       uint32_t D, const uint32_t *__restrict__ order,
@@ -161,15 +161,30 @@ __global__ __launch_bounds__(KC_THREADS) void kahan_chains_lds_kernel(const doub
     const uint64_t b = order ? koff[k] : 0, e = order ? koff[k + 1] : N;
     const uint64_t n = e - b, ntiles = (n + T - 1) / T;
     const uint32_t wave = threadIdx.x / 64, lane = threadIdx.x % 64;
-    auto stage = [&](uint64_t t) {   // waves 1..3: tile t of the cell into buffer t & 1
+    // waves 1..3: tile t of the cell into buffer t & 1.  Every load of a lane's share is issued
+    // before the first is used (order entries, then the values, then the LDS stores): a loop
+    // that waits on each element's two dependent loads in turn took ~100 ns per row.
+    constexpr uint32_t LOADERS = KC_THREADS - 64;
+    constexpr uint32_t EPL = (KC_TILE_BYTES / 8 + LOADERS - 1) / LOADERS;   // elements per loader lane
+    auto stage = [&](uint64_t t) {
         double *buf = tiles + (t & 1) * (size_t)T * D;
         const uint64_t r0 = b + t * T;
         const uint32_t cnt_el = (uint32_t)min<uint64_t>(T, e - r0) * D;
-        for (uint32_t i = threadIdx.x - 64; i < cnt_el; i += KC_THREADS - 64) {
+        const uint32_t i0 = threadIdx.x - 64;
+        uint64_t src[EPL];
+#pragma unroll
+        for (uint32_t j = 0; j < EPL; j++) {
+            const uint32_t i = i0 + j * LOADERS;
             const uint32_t r = i / D, d = i - r * D;
-            const uint64_t row = order ? order[r0 + r] : r0 + r;
-            buf[i] = X[row * D + d];
+            src[j] = i < cnt_el ? (uint64_t)(order ? order[r0 + r] : r0 + r) * D + d : 0;
         }
+        double v[EPL];
+#pragma unroll
+        for (uint32_t j = 0; j < EPL; j++)
+            if (i0 + j * LOADERS < cnt_el) v[j] = X[src[j]];
+#pragma unroll
+        for (uint32_t j = 0; j < EPL; j++)
+            if (i0 + j * LOADERS < cnt_el) buf[i0 + j * LOADERS] = v[j];
     };
     double sum = 0.0, c = 0.0;
     if (wave != 0 && ntiles) stage(0);
@@ -278,7 +293,9 @@ hipError_t launch_exact_centroids(hipStream_t s, const double *X, uint64_t N, ui
                                   uint32_t *keys_out, uint32_t *iota, uint32_t *order, uint32_t *koff, void *temp,
                                   size_t temp_bytes, double *C, uint64_t *cnt) {
     static const bool thread_chains = std::getenv("QVQ_EXACT_CHAINS") && !std::strcmp(std::getenv("QVQ_EXACT_CHAINS"), "thread");   // A/B
-    const bool lds_chains = !thread_chains && D <= 64 && (!A || K <= KC_MAX_K);
+    static const uint32_t lds_max_k = std::getenv("QVQ_EXACT_LDS_MAXK") ? (uint32_t)std::atoi(std::getenv("QVQ_EXACT_LDS_MAXK"))
+                                                                        : KC_MAX_K;   // A/B
+    const bool lds_chains = !thread_chains && D <= 64 && (!A || K <= lds_max_k);
     const size_t lds_bytes = lds_chains ? 2 * (size_t)(KC_TILE_BYTES / 8 / D) * D * 8 : 0;
     if (!A) {   // the mean: every row, in order
         if (lds_chains)
