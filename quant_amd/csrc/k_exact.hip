@@ -29,6 +29,60 @@ constexpr int EX_THREADS = 256;
 // so every row still scans k in ascending order; each lane keeps its row's best two across chunks.
 constexpr uint32_t EX_LDS_BYTES = 64 * 1024;
 
+// ref_l2_hd (kdtree_dev.hpp) with the dimension known at compile time: the same operations in
+// the same order, the row held in registers (with a run-time dimension every code vector re-read
+// the row's D values from memory: 96 B per lane per code vector at D = 12).
+template <int DT>
+__device__ inline double ref_l2_fixed(const double (&x)[DT], const double *__restrict__ c) {
+    double r = 0;
+    int d = 0;
+#pragma unroll
+    for (; d + 3 < DT; d += 4) {
+        const double e0 = x[d] - c[d], e1 = x[d + 1] - c[d + 1];
+        const double e2 = x[d + 2] - c[d + 2], e3 = x[d + 3] - c[d + 3];
+        r += (e1 * e1 + e2 * e2) + (e0 * e0 + e3 * e3);
+    }
+#pragma unroll
+    for (; d < DT; d++) {
+        const double e = x[d] - c[d];
+        r += e * e;
+    }
+    return r;
+}
+
+// One row against code vectors [k0, k0 + n) of cb (LDS), updating its best two (ascending k).
+template <int DT>
+__device__ inline void scan_codes(const double *__restrict__ xg, uint32_t D, const double *cb, uint32_t k0, uint32_t n,
+                                  double &d1, double &d2, uint32_t &k1) {
+    if constexpr (DT > 0) {
+        double x[DT];
+#pragma unroll
+        for (int d = 0; d < DT; d++) x[d] = xg[d];
+        for (uint32_t k = 0; k < n; k++) {
+            const double d = ref_l2_fixed<DT>(x, cb + (size_t)k * DT);
+            if (d < d1) {   // ascending k: the first minimum is the lowest index
+                d2 = d1;
+                d1 = d;
+                k1 = k0 + k;
+            } else if (d < d2) {
+                d2 = d;
+            }
+        }
+    } else {
+        for (uint32_t k = 0; k < n; k++) {
+            const double d = ref_l2_hd(xg, cb + (size_t)k * D, (int)D);
+            if (d < d1) {
+                d2 = d1;
+                d1 = d;
+                k1 = k0 + k;
+            } else if (d < d2) {
+                d2 = d;
+            }
+        }
+    }
+}
+
+template <int DT>
 __global__ __launch_bounds__(EX_THREADS) void exact_assign_kernel(const double *__restrict__ X, uint64_t N, uint32_t D,
                                                                   const double *__restrict__ C, uint32_t K, uint32_t kc,
                                                                   double tie_rel, uint32_t *__restrict__ A,
@@ -41,19 +95,9 @@ __global__ __launch_bounds__(EX_THREADS) void exact_assign_kernel(const double *
         for (uint32_t i = threadIdx.x; i < K * D; i += EX_THREADS) cs[i] = C[i];
         __syncthreads();
         for (uint64_t row = first; row < N; row += stride) {
-            const double *x = X + row * D;
             double d1 = INFINITY, d2 = INFINITY;
             uint32_t k1 = 0;
-            for (uint32_t k = 0; k < K; k++) {
-                const double d = ref_l2_hd(x, cs + (size_t)k * D, (int)D);
-                if (d < d1) {   // ascending k: the first minimum is the lowest index
-                    d2 = d1;
-                    d1 = d;
-                    k1 = k;
-                } else if (d < d2) {
-                    d2 = d;
-                }
-            }
+            scan_codes<DT>(X + row * D, D, cs, 0, K, d1, d2, k1);
             A[row] = k1;
             if (d2 - d1 <= tie_rel * d1) ties[atomicAdd(tie_cnt, 1u)] = (uint32_t)row;
         }
@@ -63,7 +107,6 @@ __global__ __launch_bounds__(EX_THREADS) void exact_assign_kernel(const double *
     for (uint64_t base = (uint64_t)blockIdx.x * EX_THREADS; base < N; base += stride) {
         const uint64_t row = base + threadIdx.x;
         const bool live = row < N;
-        const double *x = X + (live ? row : 0) * D;
         double d1 = INFINITY, d2 = INFINITY;
         uint32_t k1 = 0;
         for (uint32_t k0 = 0; k0 < K; k0 += kc) {
@@ -71,17 +114,7 @@ __global__ __launch_bounds__(EX_THREADS) void exact_assign_kernel(const double *
             __syncthreads();   // the previous chunk is read by every lane
             for (uint32_t i = threadIdx.x; i < n * D; i += EX_THREADS) cs[i] = C[(size_t)k0 * D + i];
             __syncthreads();
-            if (!live) continue;
-            for (uint32_t k = 0; k < n; k++) {
-                const double d = ref_l2_hd(x, cs + (size_t)k * D, (int)D);
-                if (d < d1) {
-                    d2 = d1;
-                    d1 = d;
-                    k1 = k0 + k;
-                } else if (d < d2) {
-                    d2 = d;
-                }
-            }
+            if (live) scan_codes<DT>(X + row * D, D, cs, k0, n, d1, d2, k1);
         }
         if (live) {
             A[row] = k1;
@@ -277,8 +310,14 @@ hipError_t launch_exact_assign(hipStream_t s, const double *X, uint64_t N, uint3
                                double tie_rel, uint32_t *A, uint32_t *ties, unsigned *tie_cnt) {
     const uint32_t kc = (uint32_t)std::max<size_t>(1, EX_LDS_BYTES / (8 * (size_t)D));   // code vectors per chunk
     const size_t lds = (size_t)std::min(kc, K) * D * 8;
-    hipLaunchKernelGGL(exact_assign_kernel, dim3(grid_for(N, 8192)), dim3(EX_THREADS), lds, s, X, N, D, C, K, kc,
-                       tie_rel, A, ties, tie_cnt);
+    const dim3 grid(grid_for(N, 8192)), block(EX_THREADS);
+    switch (D) {   // the dimensions of the reference's block shapes held in registers
+    case 3: hipLaunchKernelGGL(exact_assign_kernel<3>, grid, block, lds, s, X, N, D, C, K, kc, tie_rel, A, ties, tie_cnt); break;
+    case 6: hipLaunchKernelGGL(exact_assign_kernel<6>, grid, block, lds, s, X, N, D, C, K, kc, tie_rel, A, ties, tie_cnt); break;
+    case 12: hipLaunchKernelGGL(exact_assign_kernel<12>, grid, block, lds, s, X, N, D, C, K, kc, tie_rel, A, ties, tie_cnt); break;
+    case 48: hipLaunchKernelGGL(exact_assign_kernel<48>, grid, block, lds, s, X, N, D, C, K, kc, tie_rel, A, ties, tie_cnt); break;
+    default: hipLaunchKernelGGL(exact_assign_kernel<0>, grid, block, lds, s, X, N, D, C, K, kc, tie_rel, A, ties, tie_cnt);
+    }
     return hipGetLastError();
 }
 
