@@ -87,3 +87,21 @@ def test_bounded_wait_policy(scenario, status, max_s):
     if scenario in (1, 2):
         assert el >= 0.25
 
+
+
+def test_bench_cie_blocks_follow_the_reference_tiling():
+    """bench.py's exact_cie1931 input: getBlocksAsVectorsFromImage (the oracle's NORMAL tiling,
+    src/Compressor.cpp:31-62) of the synthetic raster, each pixel through CIE1931
+    (src/ColorSpace.cpp:30-38)."""
+    import sys
+    sys.path.insert(0, ROOT)
+    import bench
+    S = 64
+    rgb = bench.synthetic_raster(S, 0x5EED)
+    X = bench.cie_blocks(rgb, S)
+    Xr, _ = oracle.tile(rgb, S, S, 2, 2, cs=oracle.NORMAL)
+    p = Xr.reshape(-1, 3)
+    ref = np.stack([(p[:, 0] * 0.490 + p[:, 1] * 0.310 + p[:, 2] * 0.200) / 0.17697,
+                    (p[:, 0] * 0.17697 + p[:, 1] * 0.81240 + p[:, 2] * 0.01063) / 0.17697,
+                    (p[:, 0] * 0 + p[:, 1] * 0.01 + p[:, 2] * 0.99) / 0.17697], axis=1).reshape(-1, 12)
+    np.testing.assert_array_equal(X, ref)
