@@ -204,17 +204,29 @@ __global__ __launch_bounds__(KC_THREADS) void kahan_chains_lds_kernel(const doub
         const uint64_t r0 = b + t * T;
         const uint32_t cnt_el = (uint32_t)min<uint64_t>(T, e - r0) * D;
         const uint32_t i0 = threadIdx.x - 64;
+        // past the tile's end a lane loads the tile's last element again (no branch around the
+        // loads, so they all issue back to back) and does not store it
         uint64_t src[EPL];
+        uint32_t dd[EPL];
 #pragma unroll
         for (uint32_t j = 0; j < EPL; j++) {
-            const uint32_t i = i0 + j * LOADERS;
-            const uint32_t r = i / D, d = i - r * D;
-            src[j] = i < cnt_el ? (uint64_t)(order ? order[r0 + r] : r0 + r) * D + d : 0;
+            const uint32_t i = min(i0 + j * LOADERS, cnt_el - 1);
+            const uint32_t r = i / D;
+            dd[j] = i - r * D;
+            src[j] = r0 + r;
         }
+        if (order) {   // one uniform branch around all the order loads (they issue together)
+            uint32_t o[EPL];
+#pragma unroll
+            for (uint32_t j = 0; j < EPL; j++) o[j] = order[src[j]];
+#pragma unroll
+            for (uint32_t j = 0; j < EPL; j++) src[j] = o[j];
+        }
+#pragma unroll
+        for (uint32_t j = 0; j < EPL; j++) src[j] = src[j] * D + dd[j];
         double v[EPL];
 #pragma unroll
-        for (uint32_t j = 0; j < EPL; j++)
-            if (i0 + j * LOADERS < cnt_el) v[j] = X[src[j]];
+        for (uint32_t j = 0; j < EPL; j++) v[j] = X[src[j]];
 #pragma unroll
         for (uint32_t j = 0; j < EPL; j++)
             if (i0 + j * LOADERS < cnt_el) buf[i0 + j * LOADERS] = v[j];
