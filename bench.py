@@ -331,7 +331,9 @@ def main():
     traffic, traffic_src = None, None
     try:
         pmc = json.load(open(PMC_SUMMARY))
-        ks = [v for k, v in pmc["kernels"].items() if k.startswith("assign_")]
+        # every search launch (assign_mf32_kernel<...> and assign_small_kernel<...>, whatever
+        # the name's prefix), weighted by launches
+        ks = [v for k, v in pmc["kernels"].items() if "assign_" in k]
         if ks and pmc.get("workload") == workload_key(args):
             tot = sum(v["hbm_bytes"] * v["launches"] for v in ks)
             traffic = round(tot / sum(v["launches"] for v in ks))

@@ -15,10 +15,11 @@
  * interface on top of these entry points; INTEGRATION.md shows the binding.  Everything
  * here is plain C: pointers, sizes, status codes; no exceptions cross this boundary.
  *
- * Results: code-vector indices are bit-identical to the reference's kd-tree assignment
- * (src/Quantizer.cpp:24-32), centroids equal the exact sum of the members rounded once
- * and multiplied by fl(1/count) (the reference's Kahan sum agrees to <= 1 ulp,
- * src/Quantizer.cpp:59-87).
+ * Results: code-vector indices are bit-identical to the reference's (src/Quantizer.cpp:24-32:
+ * nanoflann's kd-tree answer over the codebook the reference computes, whose centroids are Kahan
+ * sums in ascending row order, src/Quantizer.cpp:59-87) on any rank count; the returned codebook
+ * is the exact sum of each final cell's members rounded once and multiplied by fl(1/count) (the
+ * reference's Kahan sum agrees to <= 1 ulp).
  */
 #ifndef QVQ_H
 #define QVQ_H
@@ -64,6 +65,9 @@ typedef struct {
     double tree_ms[32];         /* host wall building the level's kd-tree image (overlaps the search) */
     int kahan_redo;             /* 1: a level's ties failed the speculative reference-rule check, and the
                                    quantize ran again with synchronous reference-bit levels */
+    int tie_overflow;           /* levels whose tie rows exceeded the check's export (each forces the redo) */
+    int kahan_relays;           /* several ranks: levels whose tie rows needed cells summed over every
+                                   rank's rows (the chained Kahan sums at the end of the call) */
 } qvq_timings;
 
 /* Context: one per GPU per host thread.  Owns device memory and one HIP stream. */
@@ -116,8 +120,10 @@ QVQ_API uint32_t qvq_dim(const qvq_ctx *ctx);
  *   codebook   : K x dim fp64
  *   assign     : n u32 (this rank's rows)
  *   distortion : mean squared error of the final codebook, as updateDistortion
- * With a communicator (qvq_comm_init) every rank runs this on its own rows and all ranks
- * get the same codebook.
+ * With a communicator (qvq_comm_init) every rank runs this on its own rows -- consecutive ranges
+ * of the global rows, rank 0 first -- and all ranks get the same codebook, distortion and indices
+ * as one rank over all the rows (the reference's Kahan rule included: cells whose reference bits
+ * decide a tie are summed across the ranks in row order).
  */
 QVQ_API qvq_status qvq_lbg(qvq_ctx *ctx, uint32_t bits, double eps, double *codebook, uint32_t *assign,
                            double *distortion);
@@ -133,8 +139,16 @@ QVQ_API qvq_status qvq_assign(qvq_ctx *ctx, const double *C, uint32_t K, uint32_
 QVQ_API qvq_status qvq_update(qvq_ctx *ctx, const uint32_t *assign, uint32_t K, double *C_out, uint64_t *counts);
 /* The reference's own centroid bits (Solution::fixCodeVectors, reference src/Quantizer.cpp:59-87:
  * Kahan sums in ascending row order times fl(1/n), empty cells 0) of the resident rows under
- * assignment A, into C_out (K x dim fp64).  One rank (QVQ_EUNSUPPORTED with a communicator). */
+ * assignment A, into C_out (K x dim fp64).  With a communicator of several ranks every rank passes
+ * its own rows' assignment and gets the centroids of all ranks' rows, each cell's chain running
+ * over the ranks' rows in rank order (the ranks must hold consecutive ranges of the global rows,
+ * rank 0 first, as qvq_lbg's sharding does). */
 QVQ_API qvq_status qvq_update_kahan(qvq_ctx *ctx, const uint32_t *assign, uint32_t K, double *C_out);
+/* Test entry: qvq_update_kahan with this context's rows cut into nsplits virtual ranks at
+ * splits[0..nsplits] (0 = splits[0] <= ... <= splits[nsplits] = N), the several-rank chained
+ * evaluation run rank after rank on one device; equals qvq_update_kahan for any cuts. */
+QVQ_API qvq_status qvq_update_kahan_split(qvq_ctx *ctx, const uint32_t *assign, uint32_t K, const uint64_t *splits,
+                                          uint32_t nsplits, double *C_out);
 
 /* Decode (replaces CompressedImage::decompress, reference src/Compressor.cpp:156-165, and the
  * getImageFromVectors it calls, src/Compressor.cpp:64-85): raster[x*ySize+y] = the code-vector bytes
@@ -210,6 +224,10 @@ QVQ_API qvq_status qvq_host_row_terms(const uint8_t *codes, uint32_t dim, int co
  * stream fails; 5 the stream drains without publishing.  Returns the wait's status and its
  * duration in *elapsed_s. */
 QVQ_API qvq_status qvq_host_wait_probe(int scenario, double timeout_s, double *elapsed_s);
+/* The certificate's helper-thread pool (engine.cpp pool_run) over `rounds` jobs of 1..maxn (<= 64)
+ * threads, the count changing from job to job: *errors = job slots that ran other than exactly
+ * once.  Host only, for tests. */
+QVQ_API qvq_status qvq_host_pool_stress(uint32_t rounds, uint32_t maxn, uint64_t *errors);
 
 #ifdef __cplusplus
 }

@@ -33,7 +33,8 @@ class _Timings(ctypes.Structure):
                 ("assign_ms", ctypes.c_double * 32), ("update_ms", ctypes.c_double * 32),
                 ("other_ms", ctypes.c_double * 32), ("flagged", ctypes.c_uint64 * 32),
                 ("host_ties", ctypes.c_uint64 * 32), ("wait_ms", ctypes.c_double * 32),
-                ("tree_ms", ctypes.c_double * 32), ("kahan_redo", ctypes.c_int)]
+                ("tree_ms", ctypes.c_double * 32), ("kahan_redo", ctypes.c_int), ("tie_overflow", ctypes.c_int),
+                ("kahan_relays", ctypes.c_int)]
 
 
 _lib = None
@@ -42,7 +43,8 @@ EXPORTED = ["qvq_create", "qvq_destroy", "qvq_last_error", "qvq_version", "qvq_s
             "qvq_dim", "qvq_lbg", "qvq_assign_device", "qvq_assign", "qvq_update", "qvq_update_kahan",
             "qvq_comm_unique_id", "qvq_comm_init", "qvq_set_timing", "qvq_get_timings", "qvq_host_kdtree_nn",
             "qvq_host_finalize", "qvq_host_row_terms", "qvq_decode", "qvq_decode_mse", "qvq_decode_device",
-            "qvq_set_timeout", "qvq_host_wait_probe", "qvq_comm_init_host", "qvq_comm_info", "qvq_set_vectors_exact"]
+            "qvq_set_timeout", "qvq_host_wait_probe", "qvq_comm_init_host", "qvq_comm_info", "qvq_set_vectors_exact",
+            "qvq_update_kahan_split", "qvq_host_pool_stress"]
 
 COMM_NONE, COMM_RCCL, COMM_HOST = 0, 1, 2
 # int fn(void *buf, uint64_t count, int dtype, void *user) (qvq.h, qvq_comm_init_host)
@@ -74,6 +76,8 @@ def lib():
             "qvq_assign": ([P, P, u32, P], i),
             "qvq_update": ([P, P, u32, P, P], i),
             "qvq_update_kahan": ([P, P, u32, P], i),
+            "qvq_update_kahan_split": ([P, P, u32, P, u32, P], i),
+            "qvq_host_pool_stress": ([u32, u32, P], i),
             "qvq_comm_unique_id": ([P], i),
             "qvq_comm_init": ([P, i, i, P], i),
             "qvq_set_timing": ([P, i], i),
@@ -129,15 +133,22 @@ class Engine:
     def __init__(self, device=0):
         _torch_runtime_first()
         h = ctypes.c_void_p()
-        _check(lib().qvq_create(device, ctypes.byref(h)))
+        L = lib()
+        _check(L.qvq_create(device, ctypes.byref(h)))
         self._h = h
+        self._L = L   # held by the engine: at interpreter shutdown the module globals may be gone
 
     def close(self):
-        if getattr(self, "_h", None):
-            lib().qvq_destroy(self._h)
+        h = getattr(self, "_h", None)
+        if h:
             self._h = None
+            self._L.qvq_destroy(h)
 
-    __del__ = close
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:   # noqa: BLE001  (interpreter shutdown: nothing left to report to)
+            pass
 
     def __enter__(self):
         return self
@@ -209,6 +220,15 @@ class Engine:
         _check(lib().qvq_update_kahan(self._h, _p(A), K, _p(C)), self._h)
         return C
 
+    def update_kahan_split(self, A, K, splits):
+        """update_kahan with the rows cut into virtual ranks at splits (0 .. n): the several-rank
+        chained evaluation run rank after rank on this device (test entry)."""
+        A = np.ascontiguousarray(A, np.uint32)
+        sp = np.ascontiguousarray(splits, np.uint64)
+        C = np.empty((K, self.dim), np.float64)
+        _check(lib().qvq_update_kahan_split(self._h, _p(A), K, _p(sp), sp.size - 1, _p(C)), self._h)
+        return C
+
     def assign_device_ptr(self):
         return lib().qvq_assign_device(self._h)
 
@@ -234,7 +254,7 @@ class Engine:
                 "other_ms": list(t.other_ms[:max(L, 1)]),
                 "flagged": list(t.flagged[:max(L, 1)]), "host_ties": list(t.host_ties[:max(L, 1)]),
                 "wait_ms": list(t.wait_ms[:max(L, 1)]), "tree_ms": list(t.tree_ms[:max(L, 1)]),
-                "kahan_redo": t.kahan_redo}
+                "kahan_redo": t.kahan_redo, "tie_overflow": t.tie_overflow, "kahan_relays": t.kahan_relays}
 
     # -- multi-GPU -----------------------------------------------------------------------
     def decode(self, cb_bytes, A, xSize, ySize, bw, bh):
@@ -318,6 +338,13 @@ def host_wait_probe(scenario, timeout_s):
     el = ctypes.c_double()
     st = lib().qvq_host_wait_probe(int(scenario), float(timeout_s), ctypes.byref(el))
     return st, el.value
+
+
+def host_pool_stress(rounds, maxn):
+    """The certificate's thread pool under jobs of changing width (qvq.h): slots run != once."""
+    bad = ctypes.c_uint64()
+    _check(lib().qvq_host_pool_stress(int(rounds), int(maxn), ctypes.byref(bad)))
+    return bad.value
 
 
 def host_finalize(hi, lo, cnt, colorspace=SCALED):

@@ -419,4 +419,21 @@ struct KahanWork {
 hipError_t launch_kahan_centroids(hipStream_t s, const KahanWork &w, const uint8_t *codes, uint32_t Dp, uint32_t D,
                                   uint64_t N, const uint32_t *A, uint32_t K, double *C, double *split_out,
                                   const uint32_t *sel = nullptr, uint32_t n_sel = 0);
+// The same centroids when a cell's rows are split over ranks (each rank holds a contiguous
+// range of the global rows, ranks in row order; engine.cpp kahan_chained).  gather: u64
+// [nranks][K * D][2] chain totals | [nranks][K] row counts, zeroed by the caller; each rank
+// writes its slice (chain_local) and the caller sums gather over the ranks (an all-gather);
+// chain_build then takes each chain's exact prefix from the lower ranks' totals.  state: u64
+// [K * D][2], the reference's (sum, c) bits: chain_eval (once per rank, in rank order, each from
+// the previous rank's output; rank 0 from zeros) advances it over this rank's rows; chain_finish
+// divides by the global row count (C [K][D], split_out [2K][D] as launch_kahan_centroids).
+hipError_t launch_kahan_chain_local(hipStream_t s, const KahanWork &w, const uint8_t *codes, uint32_t Dp, uint32_t D,
+                                    uint64_t N, const uint32_t *A, uint32_t K, const uint32_t *sel, uint32_t n_sel,
+                                    uint64_t *gather, uint32_t rank, uint32_t nranks);
+hipError_t launch_kahan_chain_build(hipStream_t s, const KahanWork &w, uint32_t D, uint64_t N, uint32_t K,
+                                    const uint64_t *gather, uint32_t rank);
+hipError_t launch_kahan_chain_eval(hipStream_t s, const KahanWork &w, uint32_t D, uint64_t N, uint32_t K,
+                                   uint64_t *state, const uint64_t *gather, uint32_t rank);
+hipError_t launch_kahan_chain_finish(hipStream_t s, uint32_t D, uint32_t K, const uint64_t *state,
+                                     const uint64_t *gather, uint32_t nranks, double *C, double *split_out);
 }  // namespace qvq

@@ -80,6 +80,24 @@ using namespace qvq;
 
 constexpr uint32_t SCHED_COUNTERS = 2 * 33 + 2, N_COUNTERS = SCHED_COUNTERS + 2;
 
+namespace qvq {
+// One level's tie certificate (engine.cpp certify_rows): the level's distinct tie
+// rows, the split as far as its reference bits are known, the answers; with several ranks the
+// rows left open and the cells they need wait for the end of the quantize (cert_finish).
+struct CertState {
+    std::vector<double> qs;           // distinct tie rows (nu x D values)
+    uint32_t nu = 0;
+    std::vector<uint32_t> of;         // tie record -> distinct row
+    std::vector<uint32_t> rows, spec; // the tie records: row, speculative index
+    std::vector<double> kp;           // the reference's split where known
+    std::vector<uint8_t> known;
+    std::vector<int64_t> ans;         // per distinct row: the reference's index, -1 open
+    std::vector<uint32_t> pend;       // distinct rows still open
+    std::vector<uint8_t> sel;         // [K/2] the parent cells those rows need
+    uint32_t cells = 0, rounds = 0;
+};
+}  // namespace qvq
+
 struct qvq_ctx {
     int dev = 0;
     int num_cu = 256;
@@ -191,15 +209,32 @@ struct qvq_ctx {
     struct Verify {
         bool posted = false;
         std::atomic<bool> done{true}, cancel{false};
-        int status = 0;   // 0: the reference's indices are the speculative ones; 1: not shown
-        uint32_t K = 0;
+        int status = 0;   // 0: the reference's indices are the speculative ones; 1: not shown; 2: deferred
+        uint32_t K = 0, level = 0;
         uint64_t seq = 0;
         int par = 0;
         const uint32_t *A_prev = nullptr;
         std::unique_ptr<RefKDTree> tree;
         std::vector<double> cb;
+        CertState cs;
         hipEvent_t ev = nullptr;
     } ver[3];   // level % 3
+    // several ranks: the checks whose rows wait for cells summed over every rank's rows (status
+    // 2), finished together at the end of qvq_lbg; A_prev stays valid (one assignment buffer per
+    // level, d_Aext)
+    struct Deferred {
+        uint32_t level = 0, K = 0;
+        const uint32_t *A_prev = nullptr;
+        std::unique_ptr<RefKDTree> tree;
+        std::vector<double> cb;
+        CertState cs;
+    };
+    std::vector<Deferred> deferred;
+    std::vector<uint32_t *> d_Aext;   // assignment buffers beyond the four (several ranks: one per level)
+    uint64_t *d_vote = nullptr, *h_vote = nullptr;   // the ranks' small all-reduced decisions (qvq_lbg)
+    uint64_t vote_cap = 0;
+    uint64_t *d_kc_chain = nullptr;   // chained Kahan sums: gather | state (k_kahan.hip)
+    uint64_t kc_chain_cap = 0;
     std::atomic<bool> tree_cancel{false};
     bool tree_job = false, job_ok = false;
     int job_buf = 0;
@@ -278,6 +313,8 @@ void dfree(T *&p) {
 }
 
 uint32_t pad32(uint32_t K) { return (K + 31) & ~31u; }   // MFMA tile pairs
+bool kahan_mode(const qvq_ctx *ctx);
+double tie_band(const qvq_ctx *ctx);
 // QVQ_SEARCH=valu, QVQ_FUSE=0 and QVQ_KDTREE=host select paths for ablations and tests.
 bool env_is(const char *name, const char *val) {
     const char *v = std::getenv(name);
@@ -334,6 +371,8 @@ void free_kahan_work(KahanWork &w) {
 
 void free_kahan(qvq_ctx *ctx) {
     free_kahan_work(ctx->kw);
+    dfree(ctx->d_kc_chain);
+    ctx->kc_chain_cap = 0;
     dfree(ctx->d_kc_cent);
     dfree(ctx->d_kc_split);
     dfree(ctx->d_kc_sel);
@@ -349,6 +388,9 @@ void free_training(qvq_ctx *ctx) {
     dfree(ctx->d_A_alt);
     dfree(ctx->d_A3);
     dfree(ctx->d_A4);
+    for (uint32_t *&p : ctx->d_Aext) dfree(p);
+    ctx->d_Aext.clear();
+    ctx->deferred.clear();
     dfree(ctx->d_X64);
     dfree(ctx->d_ex_keys);
     dfree(ctx->d_ex_iota);
@@ -619,13 +661,16 @@ qvq_status run_update(qvq_ctx *ctx, const uint32_t *d_A, uint32_t K) {
     return QVQ_OK;
 }
 
-// Reference-bit ties on one rank: each level publishes its tie count, and a
-// level with ties recomputes the previous level's centroids with the reference's Kahan sums
-// before the kd-tree answers them.  QVQ_KAHAN=0: the exact-sum codebook answers them (A/B).
+// Reference-bit ties: the indices of the rows whose answer can depend on
+// the centroids' last bits follow the reference's Kahan sums, on any rank count (several ranks:
+// the chains run across the ranks, kahan_chained).  QVQ_KAHAN=0: the exact-sum codebook answers
+// them (A/B).
 bool kahan_mode(const qvq_ctx *ctx) {
     static const bool off = env_is("QVQ_KAHAN", "0");
-    return !off && !ctx->comm && !ctx->host_ar && !ctx->exact;
+    return !off && !ctx->exact;
 }
+// The recheck's absolute tie band: only where a reference-bit step follows (kahan_mode)
+double tie_band(const qvq_ctx *ctx) { return kahan_mode(ctx) ? ctx->tie_abs : 0.0; }
 
 qvq_status ensure_kahan(qvq_ctx *ctx, uint32_t Kc) {
     KahanWork &w = ctx->kw;
@@ -676,6 +721,91 @@ qvq_status ensure_kahan(qvq_ctx *ctx, uint32_t Kc) {
     w.n_cap = N;
     w.k_cap = kcap;
     w.d_cap = D;
+    return QVQ_OK;
+}
+
+// Sum over the ranks of n small u64 values (host, in place) on the context's stream, waiting for
+// the result: the ranks' decisions at the end of qvq_lbg, so that every rank takes the same
+// branch.  One rank: nothing to do.
+qvq_status vote(qvq_ctx *ctx, uint64_t *vals, uint64_t n) {
+    if (ctx->nranks <= 1 || (!ctx->comm && !ctx->host_ar) || n == 0) return QVQ_OK;
+    if (ctx->vote_cap < n) {
+        dfree(ctx->d_vote);
+        if (ctx->h_vote) (void)hipHostFree(ctx->h_vote);
+        ctx->h_vote = nullptr;
+        ctx->vote_cap = 0;
+        HIPCHK(hipMalloc(&ctx->d_vote, n * 8));
+        HIPCHK(hipHostMalloc(reinterpret_cast<void **>(&ctx->h_vote), n * 8, hipHostMallocDefault));
+        ctx->vote_cap = n;
+    }
+    std::memcpy(ctx->h_vote, vals, n * 8);
+    HIPCHK(hipMemcpyAsync(ctx->d_vote, ctx->h_vote, n * 8, hipMemcpyHostToDevice, ctx->stream));
+    qvq_status st = all_reduce(ctx, ctx->d_vote, n, false);
+    if (st != QVQ_OK) return st;
+    HIPCHK(hipMemcpyAsync(ctx->h_vote, ctx->d_vote, n * 8, hipMemcpyDeviceToHost, ctx->stream));
+    if ((st = wait_stream(ctx)) != QVQ_OK) return st;
+    std::memcpy(vals, ctx->h_vote, n * 8);
+    return QVQ_OK;
+}
+
+// The reference's Kahan centroids (and their split) of S cells when the rows are split over the
+// ranks, each rank holding a contiguous range of the global rows, ranks in row order (DESIGN.md
+// 5; src/Quantizer.cpp:59-70 sums each cell's rows in ascending global order, so a chain runs
+// across the ranks).  A: this rank's rows' cells among K_in (nullptr: the mean, K_in = S = 1);
+// sel: the device slot map of launch_kahan_centroids (nullptr: every cell, S = K_in).  Every
+// rank calls it with the same cells and gets the same C_out [S][D] / split_out [2S][D] (device):
+//   1. each rank sorts its rows of the cells and sums each chain exactly (its totals and row
+//      counts into its slice of an all-gather, one collective): every chain's exact prefix at
+//      each rank's first row;
+//   2. each rank builds its segment functions at those global prefixes;
+//   3. the chains pass from rank to rank: rank q advances the reference's state (sum, c) over
+//      its rows and an all-reduce, the others contributing zeros, hands it on (nranks small
+//      collectives);
+//   4. C = sum * fl(1/n), n the cell's rows over every rank.
+// splits (qvq_update_kahan_split, tests): this context's rows as virtual ranks cut at the given
+// offsets, run one after another on the device (no collective).
+qvq_status kahan_chained(qvq_ctx *ctx, const uint32_t *A, uint32_t K_in, const uint32_t *sel, uint32_t S,
+                         double *C_out, double *split_out, const std::vector<uint64_t> *splits = nullptr) {
+    const uint32_t D = ctx->D, Dp = ctx->Dp;
+    const bool virt = splits != nullptr;
+    const uint32_t R = virt ? (uint32_t)splits->size() - 1 : (uint32_t)ctx->nranks;
+    const uint32_t rank = virt ? 0u : (uint32_t)ctx->rank;
+    const uint32_t Ks = sel ? S : K_in;   // the sort's keys: slots, or cells
+    if (!A && (K_in != 1 || S != 1 || sel)) return fail(ctx, QVQ_EINVAL, "kahan_chained: the mean is one cell");
+    qvq_status st = ensure_kahan(ctx, std::max(K_in, S));
+    if (st != QVQ_OK) return st;
+    const uint64_t gcount = 2ull * R * S * D + (uint64_t)R * S, scount = 2ull * S * D;
+    if (ctx->kc_chain_cap < gcount + scount) {
+        dfree(ctx->d_kc_chain);
+        ctx->kc_chain_cap = 0;
+        HIPCHK(hipMalloc(&ctx->d_kc_chain, (gcount + scount) * 8));
+        ctx->kc_chain_cap = gcount + scount;
+    }
+    uint64_t *gather = ctx->d_kc_chain, *state = gather + gcount;
+    hipStream_t s = ctx->stream;
+    HIPCHK(hipMemsetAsync(gather, 0, (gcount + scount) * 8, s));
+    const KahanWork &w = ctx->kw;
+    if (virt) {
+        for (uint32_t v = 0; v < R; v++) {
+            const uint64_t off = (*splits)[v], n = (*splits)[v + 1] - off;
+            if (!n) continue;
+            const uint8_t *codes = ctx->d_codes + off * Dp;
+            const uint32_t *Av = A ? A + off : nullptr;
+            HIPCHK(launch_kahan_chain_local(s, w, codes, Dp, D, n, Av, Ks, sel, K_in, gather, v, R));
+            HIPCHK(launch_kahan_chain_build(s, w, D, n, Ks, gather, v));
+            HIPCHK(launch_kahan_chain_eval(s, w, D, n, Ks, state, gather, v));
+        }
+    } else {
+        HIPCHK(launch_kahan_chain_local(s, w, ctx->d_codes, Dp, D, ctx->N, A, Ks, sel, K_in, gather, rank, R));
+        if (R > 1 && (st = all_reduce(ctx, gather, gcount, false)) != QVQ_OK) return st;
+        HIPCHK(launch_kahan_chain_build(s, w, D, ctx->N, Ks, gather, rank));
+        for (uint32_t q = 0; q < R; q++) {
+            if (q == rank) HIPCHK(launch_kahan_chain_eval(s, w, D, ctx->N, Ks, state, gather, rank));
+            else HIPCHK(hipMemsetAsync(state, 0, scount * 8, s));
+            if (R > 1 && (st = all_reduce(ctx, state, scount, false)) != QVQ_OK) return st;
+        }
+    }
+    HIPCHK(launch_kahan_chain_finish(s, D, Ks, state, gather, R, C_out, split_out));
     return QVQ_OK;
 }
 
@@ -965,7 +1095,7 @@ qvq_status run_level(qvq_ctx *ctx, uint32_t K, int slot, bool sums_out, const do
     // one rank, sums from a separate pass: that pass (and its reduce) runs before the tree is
     // built -- it overlaps the host build instead of waiting behind it -- and the ties' moves are
     // then applied to the finished sums (move_row_sums)
-    const bool early_upd = sums_out && !fused && kd_merge(ctx);
+    const bool early_upd = sums_out && !fused && (kd_merge(ctx) || defer_ties);
     uint64_t *sums1 = early_upd ? ctx->d_sums : nullptr;
     uint64_t *xslab = fused ? ctx->d_part + (uint64_t)ctx->G * K * ctx->D : nullptr;
     uint32_t *xcnt = fused ? ctx->d_part_cnt + (uint64_t)ctx->G * K : nullptr;
@@ -1009,14 +1139,14 @@ qvq_status run_level(qvq_ctx *ctx, uint32_t K, int slot, bool sums_out, const do
     if (abl_skip() & 1) {
     } else if (rc_mf32 && K >= rc_min_k && use_mfma(ctx, K) && recheck_mf32_fits(K)) {
         HIPCHK(launch_recheck_mf32(ctx->stream, ctx->num_cu, ctx->d_codes, ctx->d_flags, &cnt[0], ctx->d_rows,
-                                   ctx->d_C64_split, K, ctx->d_lut64, ctx->mf_th, 1e-12, ctx->tie_abs, ctx->d_A, ctx->d_ties,
+                                   ctx->d_C64_split, K, ctx->d_lut64, ctx->mf_th, 1e-12, tie_band(ctx), ctx->d_A, ctx->d_ties,
                                    &cnt[1], xslab, xcnt, ctx->d_plut));
     } else {
         float alpha, beta, gamma;
         valu_coeffs(ctx, alpha, beta, gamma);
         const bool pruned = ctx->perm_k == K;   // the search's order is valid for the recheck too
         HIPCHK(launch_recheck(ctx->stream, ctx->num_cu, ctx->d_codes, ctx->Dp, ctx->D, ctx->d_flags, &cnt[0],
-                              ctx->d_C64_split, ctx->d_C32, K, ctx->d_lut64, alpha, beta, gamma, 1e-12, ctx->tie_abs, ctx->d_A,
+                              ctx->d_C64_split, ctx->d_C32, K, ctx->d_lut64, alpha, beta, gamma, 1e-12, tie_band(ctx), ctx->d_A,
                               ctx->d_ties, &cnt[1], xslab, xcnt, ctx->d_plut, pruned ? ctx->d_perm : nullptr,
                               pruned ? ctx->d_tint : nullptr,
                               (float)((double)ctx->D / (ctx->terms.sx * ctx->terms.sx))));
@@ -1105,8 +1235,29 @@ struct CertTrace {
 };
 thread_local CertTrace cert_trace;
 
+// The split rows of the cells cell_of (their reference bits, [2][S][D]: slot | S + slot) into a
+// certificate's known split; the tree's replay caches updated for those points.
+void cert_apply_cells(const RefKDTree &tree, CertState &cs, uint32_t Kc, uint32_t D, const std::vector<uint32_t> &cell_of,
+                      const double *split) {
+    const uint32_t S = (uint32_t)cell_of.size();
+    std::vector<uint32_t> changed;
+    for (uint32_t t = 0; t < S; t++)
+        for (uint32_t h = 0; h < 2; h++) {
+            const uint32_t r = cell_of[t] + h * Kc;
+            std::memcpy(&cs.kp[(size_t)r * D], &split[((size_t)h * S + t) * D], D * 8);
+            std::memset(&cs.known[(size_t)r * D], 1, D);
+            changed.push_back(r);
+        }
+    tree.cert_update(changed.data(), changed.size());   // kp / known changed on these rows
+    cs.rounds++;
+}
+
 // fn(t) for t = 0 .. n - 1: t = 0 on the calling thread, the others on the pool's threads
-// (for replays of tens of us and more: a helper's wake-up costs about that).
+// (for replays of tens of us and more: a helper's wake-up costs about that).  A job is one
+// epoch: a helper reads the epoch, want and fn together under the lock, so it runs each epoch
+// at most once and never a stale fn; a helper spawned now starts from the current epoch (it
+// never sees a finished job as new).  The caller's fn(0) and the wait for busy == 0 keep every
+// helper's fn(t) inside this call.
 void pool_run(qvq_ctx *ctx, uint32_t n, const std::function<void(uint32_t)> &fn) {
     qvq_ctx::Pool &P = ctx->pool;
     if (n <= 1) {
@@ -1115,18 +1266,27 @@ void pool_run(qvq_ctx *ctx, uint32_t n, const std::function<void(uint32_t)> &fn)
     }
     while (P.th.size() + 1 < n) {
         const uint32_t t = (uint32_t)P.th.size() + 1;
-        P.th.emplace_back([&P, t, dev = ctx->dev] {
+        uint64_t start;
+        {
+            std::lock_guard<std::mutex> g(P.m);
+            start = P.epoch.load();
+        }
+        P.th.emplace_back([&P, t, start, dev = ctx->dev] {
             (void)hipSetDevice(dev);
-            uint64_t seen = 0;
+            uint64_t seen = start;
             for (;;) {
+                uint32_t want;
+                std::function<void(uint32_t)> job;
                 {
                     std::unique_lock<std::mutex> lk(P.m);
                     P.cv.wait(lk, [&] { return P.stop.load() || P.epoch.load() != seen; });
                     if (P.stop.load()) return;
                     seen = P.epoch.load();
+                    want = P.want.load();
+                    if (t < want) job = P.fn;
                 }
-                if (t < P.want.load(std::memory_order_acquire)) {
-                    P.fn(t);
+                if (t < want) {
+                    job(t);
                     P.busy.fetch_sub(1, std::memory_order_acq_rel);
                 }
             }
@@ -1144,19 +1304,25 @@ void pool_run(qvq_ctx *ctx, uint32_t n, const std::function<void(uint32_t)> &fn)
     while (P.busy.load(std::memory_order_acquire)) std::this_thread::yield();
 }
 
-// The certificate over nu distinct rows qs (nu x D values): ans[u] the reference's index, or -1
-// for a row it leaves open.  tree: the level's tree over the exact-sum split (K code vectors);
-// A_prev: the previous level's assignment (the cells summed on stream; sync waits for it).
+// The certificate over cs.nu distinct rows cs.qs (nu x D values): cs.ans[u] the reference's
+// index, or -1 for a row it leaves open.  tree: the level's tree over the exact-sum split cb (K
+// code vectors); A_prev: the previous level's assignment (nullptr at K = 2: the parent cell is the
+// mean of every row), whose selected cells are summed on stream (sync waits for them).
+// defer (several ranks): a cell's rows are split over the ranks, so no cell is
+// summed here: the rows the known coordinates leave open stay in cs.pend with every cell they
+// need in cs.sel (their candidates' and the blamed points'), and cert_finish completes them once
+// the ranks have summed those cells together (qvq_lbg).
 template <class Sync>
 qvq_status certify_rows(qvq_ctx *ctx, const RefKDTree &tree, const double *cb, uint32_t K, const uint32_t *A_prev,
-                        hipStream_t stream, Sync sync, const std::vector<double> &qs, uint32_t nu,
-                        std::vector<int64_t> &ans, uint32_t &open_rows, uint32_t &cells, uint32_t &rounds) {
-    const uint32_t D = ctx->D, Kc = K / 2;
+                        hipStream_t stream, Sync sync, CertState &cs, bool defer, uint32_t &open_rows) {
+    const uint32_t D = ctx->D, Kc = K / 2, nu = cs.nu;
+    const std::vector<double> &qs = cs.qs;
+    std::vector<int64_t> &ans = cs.ans;
     // coordinates whose reference bits are the exact sums' without computing them: a cell's
     // exact mean is 0 or 1 only when all its values are (SCALED values lie in [0, 1], at least
     // 1/(255 n) from 1 otherwise; Kahan sums of 0s and 1s are exact), split by 1.2 or 0.8
-    std::vector<double> &kp = ctx->cert_kp;
-    std::vector<uint8_t> &known = ctx->cert_known;
+    std::vector<double> &kp = cs.kp;
+    std::vector<uint8_t> &known = cs.known;
     kp.assign(cb, cb + (size_t)K * D);
     known.resize((size_t)K * D);
     for (uint32_t j = 0; j < K; j++) {
@@ -1166,6 +1332,8 @@ qvq_status certify_rows(qvq_ctx *ctx, const RefKDTree &tree, const double *cb, u
         for (uint32_t d = 0; d < D; d++) k[d] = v[d] == 0 || std::fabs(v[d] - u) <= 1e-14;
     }
     ans.assign(nu, -1);
+    cs.pend.clear();
+    cs.sel.assign(Kc, 0);
     // rows over host threads when the replays are long (48-D: the search visits most leaves)
     const bool long_search = (uint64_t)K * D >= 65536;   // 48-D: a search visits most leaves
     const uint32_t nthr = long_search ? std::min<uint32_t>(nu, cert_threads()) : 1;
@@ -1208,7 +1376,7 @@ qvq_status certify_rows(qvq_ctx *ctx, const RefKDTree &tree, const double *cb, u
             if (!known[(size_t)j * D + d]) return false;
         return true;
     };
-    std::vector<uint32_t> ready, pend;
+    std::vector<uint32_t> ready, &pend = cs.pend;
     const bool near_first = long_search || nu <= 16;   // few rows: skip replays doomed by unknown candidates
     if (near_first) {
         near(all);
@@ -1226,11 +1394,11 @@ qvq_status certify_rows(qvq_ctx *ctx, const RefKDTree &tree, const double *cb, u
         cert_trace.mark("replay");
         if (!near_first) near(pend);
     }
-    std::vector<uint8_t> sel(Kc, 0);
-    cells = rounds = 0;
+    std::vector<uint8_t> &sel = cs.sel;
+    cs.cells = cs.rounds = 0;
     auto want = [&](uint32_t j) {
         if (all_known(j)) return;
-        cells += !sel[j % Kc];
+        cs.cells += !sel[j % Kc];
         sel[j % Kc] = 1;
     };
     // the reference's centroids of the selected cells (of the previous level's assignment),
@@ -1244,9 +1412,14 @@ qvq_status certify_rows(qvq_ctx *ctx, const RefKDTree &tree, const double *cb, u
             ctx->h_kc_sel[c] = pick[c] ? (uint32_t)cell_of.size() + 1 : 0u;
             if (pick[c]) cell_of.push_back(c);
         }
-        HIPCHK(hipMemcpyAsync(ctx->d_kc_sel, ctx->h_kc_sel, (size_t)Kc * 4, hipMemcpyHostToDevice, stream));
-        HIPCHK(launch_kahan_centroids(stream, ctx->kw, ctx->d_codes, ctx->Dp, D, ctx->N, A_prev,
-                                      (uint32_t)cell_of.size(), ctx->d_kc_cent, ctx->dh_kc_out, ctx->d_kc_sel, Kc));
+        if (A_prev) {
+            HIPCHK(hipMemcpyAsync(ctx->d_kc_sel, ctx->h_kc_sel, (size_t)Kc * 4, hipMemcpyHostToDevice, stream));
+            HIPCHK(launch_kahan_centroids(stream, ctx->kw, ctx->d_codes, ctx->Dp, D, ctx->N, A_prev,
+                                          (uint32_t)cell_of.size(), ctx->d_kc_cent, ctx->dh_kc_out, ctx->d_kc_sel, Kc));
+        } else {   // K = 2: the one parent cell is the mean of every row
+            HIPCHK(launch_kahan_centroids(stream, ctx->kw, ctx->d_codes, ctx->Dp, D, ctx->N, nullptr, 1,
+                                          ctx->d_kc_cent, ctx->dh_kc_out));
+        }
         cert_trace.mark("launched");
         return QVQ_OK;
     };
@@ -1254,21 +1427,11 @@ qvq_status certify_rows(qvq_ctx *ctx, const RefKDTree &tree, const double *cb, u
         qvq_status s2;
         if ((s2 = sync()) != QVQ_OK) return s2;
         cert_trace.mark("sums");
-        const uint32_t S = (uint32_t)cell_of.size();
-        std::vector<uint32_t> changed;
-        for (uint32_t t = 0; t < S; t++)
-            for (uint32_t h = 0; h < 2; h++) {
-                const uint32_t r = cell_of[t] + h * Kc;
-                std::memcpy(&kp[(size_t)r * D], &ctx->h_kc_out[((size_t)h * S + t) * D], D * 8);
-                std::memset(&known[(size_t)r * D], 1, D);
-                changed.push_back(r);
-            }
-        tree.cert_update(changed.data(), changed.size());   // kp / known changed on these rows
-        rounds++;
+        cert_apply_cells(tree, cs, Kc, D, cell_of, ctx->h_kc_out);
         return QVQ_OK;
     };
     open.clear();
-    if (!pend.empty() && K >= 4 && A_prev) {
+    if (!pend.empty() && (K >= 4 ? A_prev != nullptr : K == 2)) {
         // the candidates' cells on the GPU while a collecting replay finds the points whose bits
         // settle the decisions the intervals leave open (with the candidates unknown, it blames
         // them too); their cells, if new, in a second round
@@ -1276,17 +1439,21 @@ qvq_status certify_rows(qvq_ctx *ctx, const RefKDTree &tree, const double *cb, u
         for (uint32_t u : pend)
             for (uint32_t j : cand[u]) want(j);
         std::vector<uint8_t> first = sel;
-        if (cells && (st = launch_cells(first)) != QVQ_OK) return st;
+        if (cs.cells && !defer && (st = launch_cells(first)) != QVQ_OK) return st;
         std::vector<std::vector<uint32_t>> blame(std::max<uint32_t>(nthr, 1));
         each(pend, [&](uint32_t u, uint32_t t) {
             tree.certify_blame(&qs[(size_t)u * D], KAHAN_DELTA, kp.data(), known.data(), blame[t]);
         });
-        const uint32_t c0 = cells;
+        const uint32_t c0 = cs.cells;
         for (const auto &b : blame)
             for (uint32_t j : b) want(j);
         cert_trace.mark("blame");
+        if (defer) {   // the cells come from every rank's rows (cert_finish)
+            open_rows = (uint32_t)pend.size();
+            return QVQ_OK;
+        }
         if (c0 && (st = finish_cells()) != QVQ_OK) return st;
-        if (cells > c0) {
+        if (cs.cells > c0) {
             std::vector<uint8_t> more(Kc, 0);
             for (uint32_t c = 0; c < Kc; c++) more[c] = sel[c] && !first[c];
             if ((st = launch_cells(more)) != QVQ_OK || (st = finish_cells()) != QVQ_OK) return st;
@@ -1296,8 +1463,38 @@ qvq_status certify_rows(qvq_ctx *ctx, const RefKDTree &tree, const double *cb, u
     } else {
         open = pend;
     }
+    pend = open;
     open_rows = (uint32_t)open.size();
     return QVQ_OK;
+}
+
+// The deferred rows (certify_rows with defer) once the cells cell_of have their reference bits:
+// split rows at split ([2][S][D]: slot | S + slot); returns the rows still open.
+uint32_t cert_finish(const RefKDTree &tree, CertState &cs, uint32_t K, uint32_t D, const std::vector<uint32_t> &cell_of,
+                     const double *split) {
+    cert_apply_cells(tree, cs, K / 2, D, cell_of, split);
+    tree.cert_clear();   // (every thread's cache: the replays run here, the defer's ran elsewhere)
+    std::vector<uint32_t> open;
+    for (uint32_t u : cs.pend) {
+        cs.ans[u] = tree.certified_search(&cs.qs[(size_t)u * D], KAHAN_DELTA, cs.kp.data(), cs.known.data());
+        if (cs.ans[u] < 0) open.push_back(u);
+    }
+    cs.pend.swap(open);
+    return (uint32_t)cs.pend.size();
+}
+
+// A settled row whose reference index is not its speculative one (the quantize must be redone).
+bool cert_mismatch(const CertState &cs, uint32_t K) {
+    for (size_t i = 0; i < cs.rows.size(); i++) {
+        const int64_t a = cs.ans[cs.of[i]];
+        if (a >= 0 && (uint32_t)a != cs.spec[i]) {
+            if (env_is("QVQ_KAHAN_DEBUG", "1"))
+                std::fprintf(stderr, "qvq kahan: K %u row %u: speculative %u, the reference %lld\n", K, cs.rows[i],
+                             cs.spec[i], (long long)a);
+            return true;
+        }
+    }
+    return false;
 }
 
 // Host threads for the certificate's replays (at most 8, half the machine's).
@@ -1330,7 +1527,7 @@ uint32_t distinct_rows(const qvq_ctx *ctx, const uint8_t *code, size_t stride, u
 qvq_status certify_kahan_ties(qvq_ctx *ctx, uint32_t K, unsigned nt, uint64_t *target, bool &done) {
     done = false;
     static const bool on = !env_is("QVQ_TIE_CERT", "0");
-    if (!on || !ctx->tree || ctx->cb_local.size() != (size_t)K * ctx->D || K < 4) return QVQ_OK;
+    if (!on || !ctx->tree || ctx->cb_local.size() != (size_t)K * ctx->D || K < 2) return QVQ_OK;
     const uint32_t D = ctx->D, Dp = ctx->Dp;
     const uint64_t need = (uint64_t)nt * (4 + Dp);
     if (ctx->scatter_bytes < need) {
@@ -1345,29 +1542,27 @@ qvq_status certify_kahan_ties(qvq_ctx *ctx, uint32_t K, unsigned nt, uint64_t *t
     HIPCHK(hipMemcpyAsync(code.data(), d_gath, code.size(), hipMemcpyDeviceToHost, ctx->stream));
     qvq_status st;
     if ((st = wait_stream(ctx)) != QVQ_OK) return st;
-    std::vector<double> qs;
-    std::vector<uint32_t> of;
-    const uint32_t nu = distinct_rows(ctx, code.data(), Dp, nt, qs, of);
-    std::vector<int64_t> ans;
-    uint32_t open = 0, cells = 0, rounds = 0;
-    if ((st = certify_rows(ctx, *ctx->tree, ctx->cb_local.data(), K, ctx->d_A_alt, ctx->stream,
-                           [ctx] { return wait_stream(ctx); }, qs, nu, ans, open, cells, rounds)) != QVQ_OK)
+    CertState cs;
+    cs.nu = distinct_rows(ctx, code.data(), Dp, nt, cs.qs, cs.of);
+    uint32_t open = 0;
+    if ((st = certify_rows(ctx, *ctx->tree, ctx->cb_local.data(), K, K == 2 ? nullptr : ctx->d_A_alt, ctx->stream,
+                           [ctx] { return wait_stream(ctx); }, cs, false, open)) != QVQ_OK)
         return st;
     if (open) {
         if (env_is("QVQ_KAHAN_DEBUG", "1"))
-            std::fprintf(stderr, "qvq kahan: K %u ties %u (%u distinct) cells %u: %u rows not certified\n", K, nt, nu,
-                         cells, open);
+            std::fprintf(stderr, "qvq kahan: K %u ties %u (%u distinct) cells %u: %u rows not certified\n", K, nt, cs.nu,
+                         cs.cells, open);
         return QVQ_OK;
     }
     std::vector<uint32_t> &vals = ctx->cert_vals;   // outlives the copy (no wait)
     vals.resize(nt);
-    for (uint32_t i = 0; i < nt; i++) vals[i] = (uint32_t)ans[of[i]];
+    for (uint32_t i = 0; i < nt; i++) vals[i] = (uint32_t)cs.ans[cs.of[i]];
     HIPCHK(hipMemcpyAsync(d_vals, vals.data(), nt * 4, hipMemcpyHostToDevice, ctx->stream));
     HIPCHK(launch_fix_rows(ctx->stream, ctx->d_codes, Dp, D, ctx->d_A, ctx->d_ties, d_vals, nt, K, nullptr, nullptr,
                            ctx->d_plut, target));
     if (env_is("QVQ_KAHAN_DEBUG", "1"))
         std::fprintf(stderr, "qvq kahan: K %u ties %u (%u distinct) certified, cells summed %u in %u rounds\n", K, nt,
-                     nu, cells, rounds);
+                     cs.nu, cs.cells, cs.rounds);
     done = true;
     return QVQ_OK;
 }
@@ -1375,7 +1570,10 @@ qvq_status certify_kahan_ties(qvq_ctx *ctx, uint32_t K, unsigned nt, uint64_t *t
 // The speculative check of one level (on the worker): the level's tie rows and their
 // speculative indices (exported with its codebook) against the reference's, by the certificate
 // over the level's tree.  status 0: all equal; 1: a row differs or stays open (qvq_lbg then
-// redoes the quantize with the synchronous Kahan levels).
+// redoes the quantize with the synchronous Kahan levels); 2 (several ranks): the rows settled
+// so far agree and the rest wait for cells summed over every rank's rows (v.cs, cert_finish).
+// QVQ_KAHAN_FAIL_LEVEL=L (tests): level L's check fails (on rank QVQ_KAHAN_FAIL_RANK, default
+// every rank), exercising the redo.
 void verify_level(qvq_ctx *ctx, qvq_ctx::Verify &v) {
     v.status = 1;
     (void)hipSetDevice(ctx->dev);
@@ -1383,6 +1581,9 @@ void verify_level(qvq_ctx *ctx, qvq_ctx::Verify &v) {
     while (*flag < v.seq)   // the export is released with the codebook's ready number
         if (v.cancel.load(std::memory_order_relaxed)) return;
     std::atomic_thread_fence(std::memory_order_acquire);
+    static const int fail_level = std::getenv("QVQ_KAHAN_FAIL_LEVEL") ? std::atoi(std::getenv("QVQ_KAHAN_FAIL_LEVEL")) : 0;
+    static const int fail_rank = std::getenv("QVQ_KAHAN_FAIL_RANK") ? std::atoi(std::getenv("QVQ_KAHAN_FAIL_RANK")) : -1;
+    if (fail_level && (int)v.level == fail_level && (fail_rank < 0 || fail_rank == ctx->rank)) return;
     static const bool trace = env_is("QVQ_CERT_TRACE", "1");
     cert_trace.on = trace;
     cert_trace.t0 = std::chrono::steady_clock::now();
@@ -1393,61 +1594,91 @@ void verify_level(qvq_ctx *ctx, qvq_ctx::Verify &v) {
         v.status = 0;
         return;
     }
-    if (nt > ctx->tx_cap || !v.tree || v.tree->cancelled() || v.K < 4) return;
+    if (nt > ctx->tx_cap) {
+        ctx->tm.tie_overflow++;
+        return;
+    }
+    if (!v.tree || v.tree->cancelled() || v.K < 2) return;
     const uint32_t Dp = ctx->Dp, words = 2 + Dp / 4;
     std::vector<uint32_t> rec(tx + 2, tx + 2 + (size_t)nt * words);   // out of the mapped buffer at once
-    for (uint32_t i = 0; i < nt; i++)
-        if (rec[(size_t)i * words] >= ctx->N || rec[(size_t)i * words + 1] >= v.K) return;
-    std::vector<double> qs;
-    std::vector<uint32_t> of;
-    const uint32_t nu =
-        distinct_rows(ctx, reinterpret_cast<const uint8_t *>(rec.data() + 2), (size_t)words * 4, nt, qs, of);
-    std::vector<int64_t> ans;
-    uint32_t open = 0, cells = 0, rounds = 0;
-    auto sync = [ctx]() -> qvq_status {
-        HIPCHK(hipStreamSynchronize(ctx->vstream));
-        return QVQ_OK;
-    };
-    // (A_prev is complete: the GPU wrote the flag seen above after the levels that made it)
-    if (certify_rows(ctx, *v.tree, v.cb.data(), v.K, v.A_prev, ctx->vstream, sync, qs, nu, ans, open, cells,
-                     rounds) != QVQ_OK || open)
-        return;
-    for (uint32_t i = 0; i < nt; i++)
-        if ((uint32_t)ans[of[i]] != rec[(size_t)i * words + 1]) {
-            if (env_is("QVQ_KAHAN_DEBUG", "1"))
-                std::fprintf(stderr, "qvq kahan: K %u row %u: speculative %u, the reference %lld\n", v.K,
-                             rec[(size_t)i * words], rec[(size_t)i * words + 1], (long long)ans[of[i]]);
-            return;
+    CertState &cs = v.cs;
+    cs.rows.resize(nt);
+    cs.spec.resize(nt);
+    for (uint32_t i = 0; i < nt; i++) {
+        cs.rows[i] = rec[(size_t)i * words];
+        cs.spec[i] = rec[(size_t)i * words + 1];
+        if (cs.rows[i] >= ctx->N || cs.spec[i] >= v.K) return;
+    }
+    cs.nu = distinct_rows(ctx, reinterpret_cast<const uint8_t *>(rec.data() + 2), (size_t)words * 4, nt, cs.qs, cs.of);
+    uint32_t open = 0;
+    // the selected cells' sums on the check's stream: a bounded poll that also ends when the
+    // call cancels the check (a failed wait in qvq_lbg), so joining a cancelled check is prompt
+    auto sync = [ctx, &v]() -> qvq_status {
+        const auto until = std::chrono::steady_clock::now() + std::chrono::duration<double>(ctx->timeout_s);
+        for (;;) {
+            const hipError_t q = hipStreamQuery(ctx->vstream);
+            if (q == hipSuccess) return QVQ_OK;
+            if (q != hipErrorNotReady) return QVQ_EDEVICE;
+            if (v.cancel.load(std::memory_order_relaxed) || std::chrono::steady_clock::now() > until)
+                return QVQ_EDEVICE;
+            std::this_thread::yield();
         }
+    };
+    const bool defer = ctx->nranks > 1;
+    // (A_prev is complete: the GPU wrote the flag seen above after the levels that made it)
+    if (certify_rows(ctx, *v.tree, v.cb.data(), v.K, v.A_prev, ctx->vstream, sync, cs, defer, open) != QVQ_OK ||
+        (open && !defer))
+        return;
+    if (cert_mismatch(cs, v.K)) return;
     cert_trace.mark("done");
     if (env_is("QVQ_KAHAN_DEBUG", "1") || trace)
-        std::fprintf(stderr, "qvq kahan: K %u ties %u (%u distinct) verified, cells summed %u in %u rounds%s%s\n", v.K,
-                     nt, nu, cells, rounds, trace ? " | us:" : "", cert_trace.s.c_str());
-    v.status = 0;
+        std::fprintf(stderr, "qvq kahan: K %u ties %u (%u distinct) %s, cells %s %u in %u rounds%s%s\n", v.K, nt, cs.nu,
+                     open ? "deferred" : "verified", open ? "wanted" : "summed", cs.cells, cs.rounds,
+                     trace ? " | us:" : "", cert_trace.s.c_str());
+    v.status = open ? 2 : 0;
 }
 
-bool join_verify(qvq_ctx::Verify &v) {
-    if (!v.posted) return true;
+// The check's verdict (status 0 / 1 / 2, -1: none posted); its tree and rows are released,
+// except a deferred check's (status 2, several ranks), which moves to ctx->deferred.
+int join_verify(qvq_ctx *ctx, qvq_ctx::Verify &v) {
+    if (!v.posted) return -1;
     while (!v.done.load(std::memory_order_acquire)) std::this_thread::yield();
     v.posted = false;
+    const int status = v.status;
+    if (status == 2) {
+        qvq_ctx::Deferred d;
+        d.level = v.level;
+        d.K = v.K;
+        d.A_prev = v.A_prev;
+        d.tree = std::move(v.tree);
+        d.cb = std::move(v.cb);
+        d.cs = std::move(v.cs);
+        ctx->deferred.push_back(std::move(d));
+    }
     v.tree.reset();
-    return v.status == 0;
+    v.cs = CertState();
+    return status;
 }
 
-// join_verify within the context's wait bounds (the check waits for the GPU): a timeout fails
-// the call as any other wait does (wait_failed); ok = the check's verdict.
+// join_verify within the context's wait bounds: a failed stream or communicator, or a timeout,
+// fails the call as any other wait does (wait_failed; a drained stream is no failure here: the
+// check's host replays may outlast the GPU's work).  ok = not failed (status 0, 2 or none).
 qvq_status join_verify_bounded(qvq_ctx *ctx, qvq_ctx::Verify &v, bool &ok) {
     ok = true;
     if (!v.posted) return QVQ_OK;
     std::string err;
-    const qvq_status st = wait_until([&] { return v.done.load(std::memory_order_acquire); },
-                                     [&](std::string &m) { return probe_stream(ctx, m); },
-                                     [&](std::string &m) { return probe_comm(ctx, m); }, ctx->timeout_s, err);
+    const qvq_status st = wait_until(
+        [&] { return v.done.load(std::memory_order_acquire); },
+        [&](std::string &m) {
+            const StreamState ss = probe_stream(ctx, m);
+            return ss == StreamState::Drained ? StreamState::Running : ss;
+        },
+        [&](std::string &m) { return probe_comm(ctx, m); }, ctx->timeout_s, err);
     if (st != QVQ_OK) {
         for (auto &u : ctx->ver) u.cancel.store(true);
         return wait_failed(ctx, fail(ctx, st, err));
     }
-    ok = join_verify(v);
+    ok = join_verify(ctx, v) != 1;
     return QVQ_OK;
 }
 
@@ -1525,6 +1756,101 @@ qvq_status resolve_kahan_ties(qvq_ctx *ctx, uint32_t K, int slot, unsigned nt, b
         return QVQ_OK;
     }
     return resolve_host_ties(ctx, ctx->h_kc_split.data(), K, nt, false, target);
+}
+
+// resolve_kahan_ties on several ranks (a level with ties on any rank, every rank calls it): the
+// reference's whole split from the chains over every rank's rows (kahan_chained), its kd-tree,
+// this rank's ties (nt) answered against both, and the ties' moves of every rank summed (sums
+// copy 1, added by the finalize that follows).
+qvq_status resolve_kahan_ties_multi(qvq_ctx *ctx, uint32_t K, int slot, unsigned nt) {
+    const uint32_t D = ctx->D, Kc = K / 2;
+    qvq_status st;
+    uint64_t *target = ctx->d_sums + sums_cap_stride(ctx);
+    if ((st = kahan_chained(ctx, K == 2 ? nullptr : ctx->d_A_alt, Kc, nullptr, Kc, ctx->d_kc_cent, ctx->d_kc_split)) !=
+        QVQ_OK)
+        return st;
+    ctx->h_kc_split.resize((size_t)K * D);
+    HIPCHK(hipMemcpyAsync(ctx->h_kc_split.data(), ctx->d_kc_split, (size_t)K * D * 8, hipMemcpyDeviceToHost, ctx->stream));
+    if ((st = wait_stream(ctx)) != QVQ_OK) return st;
+    if (nt) {
+        KdView kd;
+        static const bool reuse = !env_is("QVQ_KAHAN_TREE", "rebuild");
+        if (reuse && ctx->tree && ctx->tree_kd.depth > 0 && ctx->cb_local.size() == (size_t)K * D &&
+            ctx->tree->unchanged_under(ctx->h_kc_split.data()))
+            kd = ctx->tree_kd;
+        else
+            build_tree(ctx, ctx->h_kc_split.data(), K, slot & 1, kd);
+        unsigned *cnt = ctx->d_counters + 2 * slot;
+        if (kd.depth > 0)
+            HIPCHK(launch_kd_resolve(ctx->stream, ctx->d_codes, ctx->Dp, D, ctx->d_ties, &cnt[1], ctx->d_kc_split, K,
+                                     ctx->d_lut64, kd, ctx->d_A, nullptr, nullptr, ctx->d_plut, target));
+        else if ((st = resolve_host_ties(ctx, ctx->h_kc_split.data(), K, nt, false, target)) != QVQ_OK)
+            return st;
+    }
+    return all_reduce_sums(ctx, K, target);
+}
+
+// Several ranks, at the end of a speculative qvq_lbg: the checks whose rows wait
+// for cells summed over every rank's rows (ctx->deferred).  A vote of every rank's failure and,
+// per level, of the cells its open rows need; then for each level with cells wanted (ascending,
+// every rank the same), their reference bits from the chains over every rank's rows
+// (kahan_chained on the level's parent assignment, alev[L - 1]) and this rank's open rows
+// replayed with them (cert_finish); a second vote of the failures.  failed: in, this rank's
+// failure so far; out, any rank's (the quantize is then redone on every rank).
+qvq_status resolve_deferred(qvq_ctx *ctx, uint32_t bits, const std::vector<uint32_t *> &alev, bool &failed) {
+    const uint32_t D = ctx->D;
+    // [0] failures | per level L: its parent cells (2^(L-1)), four 16-bit counts per word
+    std::vector<uint64_t> off(bits + 2, 1);
+    for (uint32_t L = 1; L <= bits; L++) off[L + 1] = off[L] + ((1ull << (L - 1)) + 3) / 4;
+    std::vector<uint64_t> v(off[bits + 1], 0);
+    v[0] = failed ? 1 : 0;
+    for (const auto &d : ctx->deferred)
+        for (uint32_t c = 0; c < d.K / 2; c++)
+            if (d.cs.sel[c]) v[off[d.level] + c / 4] |= 1ull << (16 * (c % 4));
+    qvq_status st;
+    if ((st = vote(ctx, v.data(), v.size())) != QVQ_OK) return st;
+    if (v[0]) {
+        failed = true;
+        return QVQ_OK;
+    }
+    bool local_fail = false;
+    std::vector<uint32_t> cell_of;
+    std::vector<double> split;
+    for (uint32_t L = 1; L <= bits; L++) {
+        const uint32_t Kc = 1u << (L - 1);
+        cell_of.clear();
+        for (uint32_t c = 0; c < Kc; c++)
+            if ((v[off[L] + c / 4] >> (16 * (c % 4))) & 0xFFFF) cell_of.push_back(c);
+        if (cell_of.empty()) continue;
+        ctx->tm.kahan_relays++;
+        const uint32_t S = (uint32_t)cell_of.size();
+        if ((st = ensure_kahan(ctx, Kc)) != QVQ_OK) return st;
+        if (L >= 2) {
+            for (uint32_t c = 0; c < Kc; c++) ctx->h_kc_sel[c] = 0;
+            for (uint32_t t = 0; t < S; t++) ctx->h_kc_sel[cell_of[t]] = t + 1;
+            HIPCHK(hipMemcpyAsync(ctx->d_kc_sel, ctx->h_kc_sel, (size_t)Kc * 4, hipMemcpyHostToDevice, ctx->stream));
+            st = kahan_chained(ctx, alev[L - 1], Kc, ctx->d_kc_sel, S, ctx->d_kc_cent, ctx->d_kc_split);
+        } else {
+            st = kahan_chained(ctx, nullptr, 1, nullptr, 1, ctx->d_kc_cent, ctx->d_kc_split);
+        }
+        if (st != QVQ_OK) return st;
+        split.resize(2ull * S * D);
+        HIPCHK(hipMemcpyAsync(split.data(), ctx->d_kc_split, split.size() * 8, hipMemcpyDeviceToHost, ctx->stream));
+        if ((st = wait_stream(ctx)) != QVQ_OK) return st;
+        for (auto &d : ctx->deferred) {
+            if (d.level != L) continue;
+            const uint32_t open = cert_finish(*d.tree, d.cs, d.K, D, cell_of, split.data());
+            const bool bad = open || cert_mismatch(d.cs, d.K);
+            if (env_is("QVQ_KAHAN_DEBUG", "1"))
+                std::fprintf(stderr, "qvq kahan: rank %d K %u deferred rows finished over %u cells: %s\n", ctx->rank,
+                             d.K, S, open ? "rows left open" : bad ? "a row differs" : "verified");
+            local_fail = local_fail || bad;
+        }
+    }
+    uint64_t f = local_fail ? 1 : 0;
+    if ((st = vote(ctx, &f, 1)) != QVQ_OK) return st;
+    failed = f != 0;
+    return QVQ_OK;
 }
 
 // The byte histogram of the resident rows (kept on the device: qvq_lbg derives sum ||x||^2 and
@@ -1657,6 +1983,8 @@ QVQ_API void qvq_destroy(qvq_ctx *ctx) {
     if (ctx->h_decode_stat) (void)hipHostFree(ctx->h_decode_stat);
     if (ctx->h_stage) (void)hipHostFree(ctx->h_stage);
     if (ctx->h_ar_stage) (void)hipHostFree(ctx->h_ar_stage);
+    dfree(ctx->d_vote);
+    if (ctx->h_vote) (void)hipHostFree(ctx->h_vote);
     if (ctx->ev_ready)
         for (int l = 0; l < 32; l++)
             for (int j = 0; j < 4; j++) (void)hipEventDestroy(ctx->ev[l][j]);
@@ -1963,28 +2291,31 @@ QVQ_API qvq_status qvq_lbg(qvq_ctx *ctx, uint32_t bits, double eps, double *code
         if ((st = all_reduce(ctx, ctx->d_hist + 256, 256, false)) != QVQ_OK) return st;
         hist = ctx->d_hist + 256;
     }
-    // Reference-bit (Kahan) levels, SCALED values on one rank (NORMAL values are integers: the
-    // exact sums are the reference's bits).  Speculative (default): each level runs as with exact
-    // sums, its ties answered by the exact-sum tree on the device, and the worker checks them
-    // against the reference's rule (the certificate) while the GPU runs the next
-    // level; a level whose check fails makes the quantize run again with synchronous Kahan
-    // levels (each waits for its ties to be answered by the reference's rule).  QVQ_SPECULATE=0:
-    // synchronous from the start.
+    // Reference-bit (Kahan) levels, SCALED values (NORMAL values are integers: the exact sums are
+    // the reference's bits).  Speculative (default): each level runs as with exact sums, its ties
+    // answered by the exact-sum tree on the device, and the worker checks them against the
+    // reference's rule (the certificate) while the GPU runs the next level; a
+    // level whose check fails makes the quantize run again with synchronous Kahan levels (each
+    // waits for its ties to be answered by the reference's rule).  Several ranks:
+    // a check never sums a cell on its own (a cell's chain runs over every rank's rows); its open
+    // rows wait for the end of the call, where the ranks vote, sum the cells wanted together
+    // (kahan_chained) and vote again, so that every rank redoes the quantize or none does.
+    // QVQ_SPECULATE=0: synchronous from the start.
     const bool kahan = kahan_mode(ctx) && ctx->cs == QVQ_CS_SCALED;
+    const bool multi = ctx->nranks > 1 && (ctx->comm || ctx->host_ar);
     static const bool spec_off = env_is("QVQ_SPECULATE", "0");
     bool spec = kahan && !spec_off;
     if (spec && (st = ensure_speculation(ctx, Kmax)) != QVQ_OK) return st;
     if (kahan && !ctx->d_A_alt) HIPCHK(hipMalloc(&ctx->d_A_alt, ctx->N * 4));
-    struct JobGuard {   // no tree build or check outlives the call (an error return included)
-        qvq_ctx *c;
-        ~JobGuard() {
-            join_tree_job(c, true);
-            for (auto &v : c->ver) {
-                v.cancel.store(true);
-                join_verify(v);
-            }
-        }
-    } job_guard{ctx};
+    // several ranks, speculative: one assignment buffer per level, so that every level's parent
+    // assignment is still there when the deferred checks finish at the end of the call
+    const uint32_t npool = spec && multi ? std::max<uint32_t>(4, bits + 1) : 4;
+    while (spec && 4 + ctx->d_Aext.size() < npool) {
+        uint32_t *p = nullptr;
+        HIPCHK(hipMalloc(&p, ctx->N * 4));
+        ctx->d_Aext.push_back(p);
+    }
+    ctx->deferred.clear();
     // distortion inputs, per-level counters and the codebook go to mapped pinned memory in one
     // launch (the mapped split-codebook buffer is free once the last tree is built); the copy's
     // own flag ends the wait: polling it wakes the host at once (a stream synchronize costs tens
@@ -2046,27 +2377,38 @@ QVQ_API qvq_status qvq_lbg(qvq_ctx *ctx, uint32_t bits, double eps, double *code
 
     const bool sync_kahan = kahan && !spec;
     if (sync_kahan) split_out = ctx->d_C64_split_alt;
-    uint32_t *const abuf[4] = {ctx->d_A, ctx->d_A_alt, ctx->d_A3, ctx->d_A4};
-    bool spec_failed = false;
+    // the assignment buffers (d_A, d_A_alt, d_A3, d_A4 and d_Aext own them together): level L
+    // writes abuf[L % P]; a check of level L reads A_{L-1} until level L + 3 starts (one rank) or
+    // to the end of the call (several ranks, P > bits)
+    std::vector<uint32_t *> abuf = {ctx->d_A, ctx->d_A_alt, ctx->d_A3, ctx->d_A4};
+    abuf.insert(abuf.end(), ctx->d_Aext.begin(), ctx->d_Aext.end());
+    const uint32_t P = spec ? (uint32_t)std::min<size_t>(abuf.size(), npool) : 4;
+    std::vector<uint32_t *> alev(bits + 1, nullptr);   // A_L of this call
+    bool spec_failed = false, local_fail = false;
     for (uint32_t lvl = 1; lvl <= bits; lvl++) {
         const uint32_t K = 1u << lvl;
         const int slot = (int)lvl - 1;
-        if (spec) {   // A_L in abuf[L % 4]: level L's check reads A_{L-1} until level L + 3 starts
+        if (spec) {
             if (lvl >= 4) {
                 bool ok;
                 if ((st = join_verify_bounded(ctx, ctx->ver[lvl % 3], ok)) != QVQ_OK) return st;
-                if (!ok) {
+                if (!ok && !multi) {
                     spec_failed = true;
                     break;
                 }
+                local_fail = local_fail || !ok;   // several ranks: every rank runs on to the vote
             }
-            ctx->d_A = abuf[lvl % 4];
-            ctx->d_A_alt = abuf[(lvl + 3) % 4];
-            ctx->d_A3 = abuf[(lvl + 1) % 4];   // the four stay distinct across calls
-            ctx->d_A4 = abuf[(lvl + 2) % 4];
+            ctx->d_A = abuf[lvl % P];
+            ctx->d_A_alt = abuf[(lvl + P - 1) % P];
+            ctx->d_A3 = abuf[(lvl + 1) % P];   // the buffers stay distinct, and owned, across calls
+            ctx->d_A4 = abuf[(lvl + 2) % P];
+            ctx->d_Aext.clear();   // the rest of the pool
+            for (uint32_t *q : abuf)
+                if (q != ctx->d_A && q != ctx->d_A_alt && q != ctx->d_A3 && q != ctx->d_A4) ctx->d_Aext.push_back(q);
         } else if (kahan) {
             std::swap(ctx->d_A, ctx->d_A_alt);   // d_A_alt: the previous level's assignment
         }
+        alev[lvl] = ctx->d_A;
         if ((st = run_level(ctx, K, slot, true, ctx->h_cb, ctx->seq, sync_kahan)) != QVQ_OK) return st;
         const bool split = lvl < bits;
         {
@@ -2109,6 +2451,7 @@ QVQ_API qvq_status qvq_lbg(qvq_ctx *ctx, uint32_t bits, double eps, double *code
                 v.cancel.store(false);
                 v.status = 1;
                 v.K = K;
+                v.level = lvl;
                 v.seq = ctx->seq;
                 v.par = (int)(lvl % 3);
                 v.A_prev = lvl >= 2 ? ctx->d_A_alt : nullptr;
@@ -2124,12 +2467,20 @@ QVQ_API qvq_status qvq_lbg(qvq_ctx *ctx, uint32_t bits, double eps, double *code
             if (sync_kahan) {   // the level's ties (published after its recheck)
                 if ((st = wait_flag(ctx, ctx->h_ready + 1, ctx->pub_seq)) != QVQ_OK) return st;
                 const unsigned nt = (unsigned)(uint32_t)ctx->h_ready[2];
-                join_tree_job(ctx, nt == 0);   // the level's tree: needed for ties only
-                if (nt) {
+                uint64_t nt_all = nt;   // every rank's ties: the ranks resolve together
+                if (multi && (st = vote(ctx, &nt_all, 1)) != QVQ_OK) return st;
+                join_tree_job(ctx, nt_all == 0);   // the level's tree: needed for ties only
+                if (nt_all) {
                     const bool fused = use_fused(ctx, K);
-                    if (fused) ctx->sums1_dirty = true;
-                    if ((st = resolve_kahan_ties(ctx, K, slot, nt, fused)) != QVQ_OK) return st;
-                    HIPCHK(finalize(K, split, fused ? 2 : 1, fused ? tcnt : nullptr));
+                    if (multi) {   // every rank's moves in copy 1, all-reduced, added by the finalize
+                        ctx->sums1_dirty = true;
+                        if ((st = resolve_kahan_ties_multi(ctx, K, slot, nt)) != QVQ_OK) return st;
+                        HIPCHK(finalize(K, split, 2, nullptr));
+                    } else {
+                        if (fused) ctx->sums1_dirty = true;
+                        if ((st = resolve_kahan_ties(ctx, K, slot, nt, fused)) != QVQ_OK) return st;
+                        HIPCHK(finalize(K, split, fused ? 2 : 1, fused ? tcnt : nullptr));
+                    }
                     ctx->sums1_dirty = false;
                 }
                 if (split) {
@@ -2144,16 +2495,20 @@ QVQ_API qvq_status qvq_lbg(qvq_ctx *ctx, uint32_t bits, double eps, double *code
         for (uint32_t l = bits >= 3 ? bits - 2 : 1; l <= bits; l++) {
             bool ok;
             if ((st = join_verify_bounded(ctx, ctx->ver[l % 3], ok)) != QVQ_OK) return st;
-            if (!ok) spec_failed = true;
+            local_fail = local_fail || !ok;
         }
+        spec_failed = local_fail;
+        if (multi && (st = resolve_deferred(ctx, bits, alev, spec_failed)) != QVQ_OK) return st;
     }
+    ctx->deferred.clear();
     if (!spec_failed) break;
     // a check failed: every check joined, the stream drained, then the quantize again with
     // synchronous Kahan levels
     for (auto &v : ctx->ver) {
         v.cancel.store(true);
-        join_verify(v);
+        join_verify(ctx, v);
     }
+    ctx->deferred.clear();
     if ((st = wait_stream(ctx)) != QVQ_OK) return st;
     if (ctx->sums1_dirty) {
         HIPCHK(hipMemsetAsync(ctx->d_sums, 0, ctx->sums_bytes, ctx->stream));
@@ -2286,7 +2641,6 @@ QVQ_API qvq_status qvq_update_kahan(qvq_ctx *ctx, const uint32_t *assign, uint32
     GUARD(ctx);
     if (ctx->N == 0) return fail(ctx, QVQ_ESTATE, "no training set");
     if (!assign || K == 0) return fail(ctx, QVQ_EINVAL, "empty assignment");
-    if (ctx->comm || ctx->host_ar) return fail(ctx, QVQ_EUNSUPPORTED, "Kahan centroids run on one rank");
     if (ctx->exact) return qvq_update(ctx, assign, K, C_out, nullptr);   // exact mode: the Kahan chain already
     if (ctx->cs != QVQ_CS_SCALED) return qvq_update(ctx, assign, K, C_out, nullptr);   // integers: exact = Kahan
     for (uint64_t i = 0; i < ctx->N; i++)
@@ -2296,8 +2650,13 @@ QVQ_API qvq_status qvq_update_kahan(qvq_ctx *ctx, const uint32_t *assign, uint32
     if (st != QVQ_OK) return st;
     if ((st = ensure_kahan(ctx, K)) != QVQ_OK) return st;
     HIPCHK(hipMemcpy(ctx->d_A, assign, ctx->N * 4, hipMemcpyHostToDevice));
-    HIPCHK(launch_kahan_centroids(ctx->stream, ctx->kw, ctx->d_codes, ctx->Dp, ctx->D, ctx->N,
-                                  K == 1 ? nullptr : ctx->d_A, K, ctx->d_kc_cent, nullptr));
+    if (ctx->nranks > 1) {   // every rank's rows: the chains pass from rank to rank (kahan_chained)
+        if ((st = kahan_chained(ctx, K == 1 ? nullptr : ctx->d_A, K, nullptr, K, ctx->d_kc_cent, nullptr)) != QVQ_OK)
+            return st;
+    } else {
+        HIPCHK(launch_kahan_centroids(ctx->stream, ctx->kw, ctx->d_codes, ctx->Dp, ctx->D, ctx->N,
+                                      K == 1 ? nullptr : ctx->d_A, K, ctx->d_kc_cent, nullptr));
+    }
     const uint64_t cB = (uint64_t)K * ctx->D * 8;
     if ((st = ensure_pinned(ctx, ctx->h_stage, ctx->stage_bytes, cB)) != QVQ_OK) return st;
     HIPCHK(hipMemcpyAsync(ctx->h_stage, ctx->d_kc_cent, cB, hipMemcpyDeviceToHost, ctx->stream));
@@ -2310,6 +2669,36 @@ QVQ_API qvq_status qvq_update_kahan(qvq_ctx *ctx, const uint32_t *assign, uint32
         std::fprintf(stderr, "qvq kahan: K %u blocks not composable %u block misses %u replays %u\n", K, ms[0], ms[1],
                      ms[2]);
     }
+    return QVQ_OK;
+}
+
+// Test entry: qvq_update_kahan with this context's rows cut into virtual ranks at splits[0..n]
+// (0 = splits[0] <= ... <= splits[n] = N), the chained evaluation of several ranks run in turn on
+// one device (kahan_chained).  The result must equal qvq_update_kahan's for any cuts.
+QVQ_API qvq_status qvq_update_kahan_split(qvq_ctx *ctx, const uint32_t *assign, uint32_t K, const uint64_t *splits,
+                                          uint32_t nsplits, double *C_out) {
+    if (!ctx) return QVQ_EINVAL;
+    GUARD(ctx);
+    if (ctx->N == 0) return fail(ctx, QVQ_ESTATE, "no training set");
+    if (ctx->exact || ctx->cs != QVQ_CS_SCALED) return fail(ctx, QVQ_EUNSUPPORTED, "SCALED byte rows only");
+    if (!assign || K == 0 || !splits || nsplits == 0) return fail(ctx, QVQ_EINVAL, "empty assignment or splits");
+    if (splits[0] != 0 || splits[nsplits] != ctx->N) return fail(ctx, QVQ_EINVAL, "splits must run from 0 to N");
+    for (uint32_t i = 0; i < nsplits; i++)
+        if (splits[i] > splits[i + 1]) return fail(ctx, QVQ_EINVAL, "splits must not decrease");
+    for (uint64_t i = 0; i < ctx->N; i++)
+        if (assign[i] >= K) return fail(ctx, QVQ_EINVAL, "assignment index out of range");
+    HIPCHK(hipSetDevice(ctx->dev));
+    qvq_status st = ensure_levels(ctx, K);
+    if (st != QVQ_OK) return st;
+    HIPCHK(hipMemcpy(ctx->d_A, assign, ctx->N * 4, hipMemcpyHostToDevice));
+    const std::vector<uint64_t> cuts(splits, splits + nsplits + 1);
+    if ((st = kahan_chained(ctx, K == 1 ? nullptr : ctx->d_A, K, nullptr, K, ctx->d_kc_cent, nullptr, &cuts)) != QVQ_OK)
+        return st;
+    const uint64_t cB = (uint64_t)K * ctx->D * 8;
+    if ((st = ensure_pinned(ctx, ctx->h_stage, ctx->stage_bytes, cB)) != QVQ_OK) return st;
+    HIPCHK(hipMemcpyAsync(ctx->h_stage, ctx->d_kc_cent, cB, hipMemcpyDeviceToHost, ctx->stream));
+    if ((st = wait_stream(ctx)) != QVQ_OK) return st;
+    if (C_out) std::memcpy(C_out, ctx->h_stage, cB);
     return QVQ_OK;
 }
 
@@ -2520,6 +2909,31 @@ QVQ_API qvq_status qvq_host_wait_probe(int scenario, double timeout_s, double *e
     if (elapsed_s) *elapsed_s = std::chrono::duration<double>(clock::now() - t0).count();
     if (st != QVQ_OK) g_static_err = err;
     return st;
+}
+
+QVQ_API qvq_status qvq_host_pool_stress(uint32_t rounds, uint32_t maxn, uint64_t *errors) {
+    if (!errors || maxn < 1 || maxn > 64) return QVQ_EINVAL;
+    std::unique_ptr<qvq_ctx> ctx(new qvq_ctx());   // the pool only: no device work
+    std::atomic<uint32_t> hits[64];
+    uint64_t bad = 0;
+    for (uint32_t r = 0; r < rounds; r++) {
+        // n grows and shrinks (new helpers spawn while earlier epochs exist, idle ones wake late)
+        const uint32_t n = 1 + (uint32_t)(((uint64_t)r * 2654435761u) >> 7) % maxn;
+        for (auto &h : hits) h.store(0);
+        pool_run(ctx.get(), n, [&](uint32_t t) {
+            hits[t].fetch_add(1);
+            if ((t + r) % 5 == 0) std::this_thread::yield();
+        });
+        for (uint32_t t = 0; t < 64; t++) bad += hits[t].load() != (t < n ? 1u : 0u);
+    }
+    {
+        std::lock_guard<std::mutex> g(ctx->pool.m);
+        ctx->pool.stop.store(true);
+    }
+    ctx->pool.cv.notify_all();
+    for (auto &t : ctx->pool.th) t.join();
+    *errors = bad;
+    return QVQ_OK;
 }
 
 QVQ_API qvq_status qvq_host_row_terms(const uint8_t *codes, uint32_t dim, int colorspace, uint64_t *hi,

@@ -298,8 +298,51 @@ __global__ __launch_bounds__(64 * WPB) void ks_meta_kernel(Geo g, const ByteTab 
     if (lane == 0) g.bsum[(uint64_t)d * TB + bb] = ((u128)hi << 64) | lo;
 }
 
+// ---- 3b. chained: this rank's chain totals and row counts into its slice of gather ----------
+__global__ __launch_bounds__(256) void ks_totals_kernel(Geo g, uint64_t *__restrict__ gather, uint32_t rank,
+                                                       uint32_t nranks) {
+    const uint32_t lane = lane_id();
+    const uint64_t wv = ((uint64_t)blockIdx.x * 256 + threadIdx.x) >> 6;
+    if (wv >= (uint64_t)g.K * g.D) return;
+    const uint32_t k = (uint32_t)(wv / g.D), d = (uint32_t)(wv - (uint64_t)k * g.D);
+    const uint32_t TB = g.blkoff[g.K];
+    const u128 *p = g.bsum + (uint64_t)d * TB;
+    uint64_t lo = 0, hi = 0;
+    for (uint32_t i = g.blkoff[k] + lane; i < g.blkoff[k + 1]; i += 64) {
+        const u128 v = p[i];
+        const uint64_t t = lo + (uint64_t)v;
+        hi += (uint64_t)(v >> 64) + (t < lo);
+        lo = t;
+    }
+    for (int o = 32; o >= 1; o >>= 1) {
+        const uint64_t l2 = __shfl_xor((unsigned long long)lo, o, 64), h2 = __shfl_xor((unsigned long long)hi, o, 64);
+        const uint64_t t = lo + l2;
+        hi = hi + h2 + (t < lo);
+        lo = t;
+    }
+    if (lane == 0) {
+        const uint64_t KD = (uint64_t)g.K * g.D;
+        uint64_t *e = gather + 2 * (rank * KD + (uint64_t)k * g.D + d);
+        e[0] = lo;
+        e[1] = hi;
+        if (d == 0) gather[2 * nranks * KD + (uint64_t)rank * g.K + k] = g.koff[k + 1] - g.koff[k];
+    }
+}
+
 // ---- 4. block prefixes: exclusive scan of the block totals along every chain --------------------
-__global__ __launch_bounds__(256) void ks_bscan_kernel(Geo g) {
+// Chained chains (a cell's rows split over ranks): gather (u64) holds every rank's
+// chain totals [nranks][K * D][lo, hi] and row counts [nranks][K]; a rank's chains start at
+// the exact sum of the lower ranks' rows.
+__device__ inline u128 chain_prefix(const uint64_t *gather, uint32_t rank, uint64_t KD, uint64_t t) {
+    u128 p = 0;
+    for (uint32_t q = 0; q < rank; q++) {
+        const uint64_t *e = gather + 2 * (q * KD + t);
+        p += ((u128)e[1] << 64) | e[0];
+    }
+    return p;
+}
+
+__global__ __launch_bounds__(256) void ks_bscan_kernel(Geo g, const uint64_t *__restrict__ gather, uint32_t rank) {
     const uint32_t lane = lane_id();
     const uint64_t wv = ((uint64_t)blockIdx.x * 256 + threadIdx.x) >> 6;
     if (wv >= (uint64_t)g.K * g.D) return;
@@ -307,7 +350,7 @@ __global__ __launch_bounds__(256) void ks_bscan_kernel(Geo g) {
     const uint32_t TB = g.blkoff[g.K];
     u128 *p = g.bsum + (uint64_t)d * TB;
     const uint32_t b0 = g.blkoff[k], b1 = g.blkoff[k + 1];
-    u128 carry = 0;
+    u128 carry = gather ? chain_prefix(gather, rank, (uint64_t)g.K * g.D, (uint64_t)k * g.D + d) : (u128)0;
     for (uint32_t base = b0; base < b1; base += 64) {
         const uint32_t i = base + lane;
         const u128 v = i < b1 ? p[i] : 0;
@@ -439,8 +482,14 @@ __device__ inline u128 bcast_u128(u128 v) {
            (uint64_t)__shfl((unsigned long long)(uint64_t)v, 0, 64);
 }
 
+// state (chained, nullptr: one rank): per chain the reference's state (sum, c) as two doubles'
+// bits, read as the chain's input (the lower ranks' rows summed) and overwritten by its state
+// after this rank's rows; C and split_out are then not written (ks_finish_kernel divides).
+// gather / rank: the chains' exact prefix at this rank's first row (chain_prefix).
 __global__ __launch_bounds__(64 * EPB) void ks_eval_kernel(Geo g, const ByteTab *__restrict__ gtab,
-                                                          double *__restrict__ C, double *__restrict__ split_out) {
+                                                          double *__restrict__ C, double *__restrict__ split_out,
+                                                          uint64_t *__restrict__ state,
+                                                          const uint64_t *__restrict__ gather, uint32_t rank) {
     __shared__ ByteTab tab;
     __shared__ __attribute__((aligned(16))) uint8_t bytes[EPB][BLK_STEPS];
     __shared__ Fn fns[EPB][SPB];
@@ -456,9 +505,17 @@ __global__ __launch_bounds__(64 * EPB) void ks_eval_kernel(Geo g, const ByteTab 
     const uint32_t TB = g.blkoff[g.K];
     const u128 *bpre = g.bsum + (uint64_t)d * TB + g.blkoff[k];
     const uint64_t mbase = (uint64_t)d * g.segoff[g.K] + g.segoff[k];
-    double result = 0.0;
-    // the exact total: the last block's prefix and its segments' sums
-    u128 Pn = 0;
+    const uint64_t t_out = (uint64_t)k * g.D + d;
+    // the state entering this rank's rows, and their exact prefix (one rank: the chain's start)
+    double sum = 0, c = 0;
+    u128 P0 = 0;
+    if (state) {
+        sum = __longlong_as_double((long long)state[2 * t_out]);
+        c = __longlong_as_double((long long)state[2 * t_out + 1]);
+        if (gather) P0 = chain_prefix(gather, rank, (uint64_t)g.K * g.D, t_out);
+    }
+    // the exact total after this rank's rows: the last block's prefix and its segments' sums
+    u128 Pn = P0;
     if (n) {
         const uint32_t lb = (nseg - 1) / SPB, s = lb * SPB + lane;
         const u128 v = s < nseg ? kahan::meta_sum(g.meta[mbase + s]) : (u128)0;
@@ -471,12 +528,13 @@ __global__ __launch_bounds__(64 * EPB) void ks_eval_kernel(Geo g, const ByteTab 
         }
         Pn = bpre[lb] + (((u128)hi << 64) | lo);
     }
-    if (n && Pn) {   // (every value 0: the sum is 0)
+    // nothing to add: no rows, or every value 0 while c = 0 (a zero step then changes nothing;
+    // with sum >= 2 a zero step is exact for any c)
+    if (n && (Pn != P0 || (c != 0.0 && !(sum >= 2.0)))) {
         // the transient: the reference's doubles until sum >= 2 (lane 0; bytes staged per block;
         // segments of zeros skipped while c = 0, where a zero step changes nothing)
         uint32_t i = 0, staged = 0xFFFFFFFFu;
-        double sum = 0, c = 0;
-        u128 P = 0;
+        u128 P = P0;
         while (i < n && !(sum >= 2.0)) {
             const uint32_t b = i / BLK_STEPS;
             if (c == 0 && i % L == 0) {
@@ -507,9 +565,7 @@ __global__ __launch_bounds__(64 * EPB) void ks_eval_kernel(Geo g, const ByteTab 
             c = __shfl(c, 0, 64);
             P = bcast_u128(P);
         }
-        if (!(sum >= 2.0)) {
-            result = sum;
-        } else {
+        if (sum >= 2.0) {
             const u128 E = (u128)(kahan::to_units(sum) - kahan::to_units(c));
             int64_t D = (int64_t)(E - P);
             uint32_t F = (uint32_t)E & 511;
@@ -571,23 +627,53 @@ __global__ __launch_bounds__(64 * EPB) void ks_eval_kernel(Geo g, const ByteTab 
                 }
                 if (j % SPB == 0 && j < nseg) fnext = bf[j / SPB];
             }
-            result = kahan::to_double(Pn + (u128)(i128)D);
+            // the state is E = Pn + D exactly: sum = RN(E), c = sum - E (kahan_par.hpp)
+            const u128 Ef = Pn + (u128)(i128)D;
+            sum = kahan::to_double(Ef);
+            c = ldexp((double)(int64_t)(kahan::to_units(sum) - (i128)Ef), -60);
             if (g.stats && lane == 0 && (nmiss | nrep)) {
                 atomicAdd(&g.stats[1], nmiss);
                 atomicAdd(&g.stats[2], nrep);
             }
         }
-        result = __dmul_rn(result, 1.0 / (double)n);   // operator/= by a scalar under -freciprocal-math
     }
     if (lane == 0) {
-        const uint64_t t = (uint64_t)k * g.D + d;
-        C[t] = result;
-        if (split_out) {   // src/Quantizer.cpp:134-138: C * (1 + 0.2), then C * (1 - 0.2)
-            split_out[t] = __dmul_rn(result, (double)(1 + 0.2));
-            split_out[(uint64_t)g.K * g.D + t] = __dmul_rn(result, (double)(1 - 0.2));
+        if (state) {
+            state[2 * t_out] = (uint64_t)__double_as_longlong(sum);
+            state[2 * t_out + 1] = (uint64_t)__double_as_longlong(c);
+        } else {
+            // operator/= by a scalar under -freciprocal-math; an empty cell stays 0 (no divide)
+            const double result = n ? __dmul_rn(sum, 1.0 / (double)n) : 0.0;
+            C[t_out] = result;
+            if (split_out) {   // src/Quantizer.cpp:134-138: C * (1 + 0.2), then C * (1 - 0.2)
+                split_out[t_out] = __dmul_rn(result, (double)(1 + 0.2));
+                split_out[(uint64_t)g.K * g.D + t_out] = __dmul_rn(result, (double)(1 - 0.2));
+            }
         }
     }
 }
+
+// Chained: C = sum * fl(1/n) with n the cell's rows on every rank (an empty cell stays 0), and
+// the split, from the state after the last rank's rows.
+__global__ __launch_bounds__(256) void ks_finish_kernel(uint32_t K, uint32_t D, const uint64_t *__restrict__ state,
+                                                       const uint64_t *__restrict__ gather, uint32_t nranks,
+                                                       double *__restrict__ C, double *__restrict__ split_out) {
+    const uint64_t t = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    const uint64_t KD = (uint64_t)K * D;
+    if (t >= KD) return;
+    const uint32_t k = (uint32_t)(t / D);
+    uint64_t n = 0;
+    for (uint32_t q = 0; q < nranks; q++) n += gather[2 * nranks * KD + (uint64_t)q * K + k];
+    const double sum = __longlong_as_double((long long)state[2 * t]);
+    const double result = n ? __dmul_rn(sum, 1.0 / (double)n) : 0.0;
+    C[t] = result;
+    if (split_out) {
+        split_out[t] = __dmul_rn(result, (double)(1 + 0.2));
+        split_out[KD + t] = __dmul_rn(result, (double)(1 - 0.2));
+    }
+}
+
+__global__ void ks_set_u32_kernel(uint32_t *p, uint32_t v) { *p = v; }
 
 }  // namespace
 
@@ -606,10 +692,14 @@ size_t KahanWork::fn_bytes() { return sizeof(Fn); }
 size_t KahanWork::segfn_bytes() { return sizeof(kahan::SegFn); }
 uint32_t KahanWork::sort_blocks(uint64_t N) { return (uint32_t)((N + SROWS - 1) / SROWS); }
 
-hipError_t launch_kahan_centroids(hipStream_t s, const KahanWork &w, const uint8_t *codes, uint32_t Dp, uint32_t D,
-                                  uint64_t N, const uint32_t *A, uint32_t K, double *C, double *split_out,
-                                  const uint32_t *sel, uint32_t n_sel) {
-    if (N == 0 || N > 0xFFFFFFFFull || D == 0 || K == 0 || D > Dp || Dp > 64 || (Dp & 3)) return hipErrorInvalidValue;
+namespace {
+
+// The sort into component planes (the selected cells' rows, or every row for the mean).
+hipError_t kahan_sort(hipStream_t s, const KahanWork &w, const uint8_t *codes, uint32_t Dp, uint32_t D, uint64_t N,
+                      const uint32_t *A, uint32_t K, const uint32_t *sel, uint32_t n_sel) {
+    if (N == 0 || N > 0xFFFFFFFFull || D == 0 || K == 0 || D > Dp || Dp > 64 || (Dp & 3) || N > w.n_cap ||
+        K > w.k_cap || D > w.d_cap)
+        return hipErrorInvalidValue;
     const uint32_t G = KahanWork::sort_blocks(N);
     const uint64_t PL = KahanWork::plane_len(N);
     if (A) {
@@ -617,8 +707,7 @@ hipError_t launch_kahan_centroids(hipStream_t s, const KahanWork &w, const uint8
         hipLaunchKernelGGL(ks_colscan_kernel, dim3(K), dim3(256), 0, s, w.hist, G, w.tot);
     } else {
         if (K != 1) return hipErrorInvalidValue;
-        hipError_t e = hipMemcpyAsync(w.tot, &w.n_one, 4, hipMemcpyHostToDevice, s);
-        if (e != hipSuccess) return e;
+        hipLaunchKernelGGL(ks_set_u32_kernel, dim3(1), dim3(1), 0, s, w.tot, (uint32_t)N);
     }
     hipLaunchKernelGGL(ks_offsets_kernel, dim3(1), dim3(1024), 0, s, w.tot, K, w.koff, w.segoff, w.blkoff);
     switch (Dp) {
@@ -636,9 +725,13 @@ hipError_t launch_kahan_centroids(hipStream_t s, const KahanWork &w, const uint8
     default:
         return hipErrorInvalidValue;
     }
+    return hipSuccess;
+}
+
+Geo make_geo(const KahanWork &w, uint64_t N, uint32_t K, uint32_t D) {
     Geo g{};
     g.planes = w.planes;
-    g.PL = PL;
+    g.PL = KahanWork::plane_len(N);
     g.koff = w.koff;
     g.segoff = w.segoff;
     g.blkoff = w.blkoff;
@@ -650,15 +743,68 @@ hipError_t launch_kahan_centroids(hipStream_t s, const KahanWork &w, const uint8
     g.sfn = reinterpret_cast<kahan::SegFn *>(w.sfn);
     g.bfn8 = reinterpret_cast<Fn *>(w.bfn8);
     g.stats = w.stats;
+    return g;
+}
+
+// grids sized by the capacities; waves past the actual block count return at once
+uint32_t blk_grid(const KahanWork &w, uint32_t D) { return (uint32_t)(((uint64_t)w.blk_cap * D + WPB - 1) / WPB); }
+uint32_t chain_grid(uint32_t K, uint32_t D) { return (uint32_t)(((uint64_t)K * D * 64 + 255) / 256); }
+
+}  // namespace
+
+hipError_t launch_kahan_centroids(hipStream_t s, const KahanWork &w, const uint8_t *codes, uint32_t Dp, uint32_t D,
+                                  uint64_t N, const uint32_t *A, uint32_t K, double *C, double *split_out,
+                                  const uint32_t *sel, uint32_t n_sel) {
+    hipError_t e = kahan_sort(s, w, codes, Dp, D, N, A, K, sel, n_sel);
+    if (e != hipSuccess) return e;
+    const Geo g = make_geo(w, N, K, D);
     const ByteTab *tab = reinterpret_cast<const ByteTab *>(w.tab);
-    // grids sized by the capacities; waves past the actual block count return at once
-    const uint64_t blk_waves = (uint64_t)w.blk_cap * D;
-    const uint32_t bgrid = (uint32_t)((blk_waves + WPB - 1) / WPB);
-    hipLaunchKernelGGL(ks_meta_kernel, dim3(bgrid), dim3(64 * WPB), 0, s, g, tab);
-    hipLaunchKernelGGL(ks_bscan_kernel, dim3((uint32_t)(((uint64_t)K * D * 64 + 255) / 256)), dim3(256), 0, s, g);
-    hipLaunchKernelGGL(ks_build_kernel, dim3(bgrid), dim3(64 * WPB), 0, s, g, tab);
+    hipLaunchKernelGGL(ks_meta_kernel, dim3(blk_grid(w, D)), dim3(64 * WPB), 0, s, g, tab);
+    hipLaunchKernelGGL(ks_bscan_kernel, dim3(chain_grid(K, D)), dim3(256), 0, s, g, (const uint64_t *)nullptr, 0u);
+    hipLaunchKernelGGL(ks_build_kernel, dim3(blk_grid(w, D)), dim3(64 * WPB), 0, s, g, tab);
     hipLaunchKernelGGL(ks_eval_kernel, dim3((uint32_t)(((uint64_t)K * D + EPB - 1) / EPB)), dim3(64 * EPB), 0, s, g,
-                       tab, C, split_out);
+                       tab, C, split_out, (uint64_t *)nullptr, (const uint64_t *)nullptr, 0u);
+    return hipGetLastError();
+}
+
+hipError_t launch_kahan_chain_local(hipStream_t s, const KahanWork &w, const uint8_t *codes, uint32_t Dp, uint32_t D,
+                                    uint64_t N, const uint32_t *A, uint32_t K, const uint32_t *sel, uint32_t n_sel,
+                                    uint64_t *gather, uint32_t rank, uint32_t nranks) {
+    if (!gather || rank >= nranks) return hipErrorInvalidValue;
+    hipError_t e = kahan_sort(s, w, codes, Dp, D, N, A, K, sel, n_sel);
+    if (e != hipSuccess) return e;
+    const Geo g = make_geo(w, N, K, D);
+    hipLaunchKernelGGL(ks_meta_kernel, dim3(blk_grid(w, D)), dim3(64 * WPB), 0, s, g,
+                       reinterpret_cast<const ByteTab *>(w.tab));
+    hipLaunchKernelGGL(ks_totals_kernel, dim3(chain_grid(K, D)), dim3(256), 0, s, g, gather, rank, nranks);
+    return hipGetLastError();
+}
+
+hipError_t launch_kahan_chain_build(hipStream_t s, const KahanWork &w, uint32_t D, uint64_t N, uint32_t K,
+                                    const uint64_t *gather, uint32_t rank) {
+    const Geo g = make_geo(w, N, K, D);
+    hipLaunchKernelGGL(ks_bscan_kernel, dim3(chain_grid(K, D)), dim3(256), 0, s, g, gather, rank);
+    hipLaunchKernelGGL(ks_build_kernel, dim3(blk_grid(w, D)), dim3(64 * WPB), 0, s, g,
+                       reinterpret_cast<const ByteTab *>(w.tab));
+    return hipGetLastError();
+}
+
+hipError_t launch_kahan_chain_eval(hipStream_t s, const KahanWork &w, uint32_t D, uint64_t N, uint32_t K,
+                                   uint64_t *state, const uint64_t *gather, uint32_t rank) {
+    if (!state) return hipErrorInvalidValue;
+    const Geo g = make_geo(w, N, K, D);
+    hipLaunchKernelGGL(ks_eval_kernel, dim3((uint32_t)(((uint64_t)K * D + EPB - 1) / EPB)), dim3(64 * EPB), 0, s, g,
+                       reinterpret_cast<const ByteTab *>(w.tab), (double *)nullptr, (double *)nullptr, state, gather,
+                       rank);
+    return hipGetLastError();
+}
+
+hipError_t launch_kahan_chain_finish(hipStream_t s, uint32_t D, uint32_t K, const uint64_t *state,
+                                     const uint64_t *gather, uint32_t nranks, double *C, double *split_out) {
+    const uint64_t KD = (uint64_t)K * D;
+    if (KD == 0) return hipSuccess;
+    hipLaunchKernelGGL(ks_finish_kernel, dim3((uint32_t)((KD + 255) / 256)), dim3(256), 0, s, K, D, state, gather,
+                       nranks, C, split_out);
     return hipGetLastError();
 }
 

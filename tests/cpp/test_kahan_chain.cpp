@@ -10,6 +10,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <random>
+#include <algorithm>
 #include <vector>
 
 #include "kahan_par.hpp"
@@ -127,6 +128,72 @@ static double run_chain(const std::vector<uint8_t> &b, const ByteTab &tb, Stats 
     return to_double(P[nseg] + (u128)(i128)D);
 }
 
+// The chained evaluation (k_kahan.hip, several ranks): the chain split at cuts into pieces, each
+// piece's segment functions built with the global exact prefix, each piece evaluated from the
+// state (sum, c) the previous piece left -- rank by rank, as engine.cpp's relay runs it.
+static double run_chain_split(const std::vector<uint8_t> &b, const std::vector<uint32_t> &cuts, const ByteTab &tb,
+                              Stats &st) {
+    double sum = 0, c = 0;
+    u128 P0 = 0;
+    for (size_t r = 0; r + 1 < cuts.size(); r++) {
+        const uint8_t *pb = b.data() + cuts[r];
+        const uint32_t n = cuts[r + 1] - cuts[r];
+        if (n == 0) continue;
+        const uint32_t nseg = (n + L - 1) / L;
+        std::vector<SegMeta> meta(nseg);
+        std::vector<u128> P(nseg + 1);
+        P[0] = P0;
+        for (uint32_t j = 0; j < nseg; j++) {
+            meta[j] = seg_meta(tb, pb + j * L, std::min(L, n - j * L));
+            P[j + 1] = P[j] + meta_sum(meta[j]);
+        }
+        const u128 Pn = P[nseg];
+        const u128 Pin = P0;
+        P0 = Pn;   // the next piece's prefix
+        if (Pn == Pin && !(c != 0.0 && !(sum >= 2.0))) continue;   // nothing changes the state
+        std::vector<SegFn> segfn(nseg);
+        for (uint32_t j = 0; j < nseg; j++) {   // (the piece's own segments only: a new rank knows nothing before)
+            int c_in;
+            uint32_t off_in;
+            input_structure([&](int i) { return meta[j - i]; }, (int)std::min<uint32_t>(8, j), c_in, off_in);
+            Fn f;
+            build_fn(tb, pb + j * L, std::min(L, n - j * L), P[j], meta[j], c_in, off_in, j + 1 == nseg, 0, f);
+            pack_seg(f, segfn[j]);
+            st.segs++;
+            st.raw += fkind(f) == FK_RAW;
+        }
+        // the transient from the incoming state
+        uint32_t i = 0;
+        u128 Pt = Pin;
+        while (i < n && !(sum >= 2.0)) {
+            fstep(sum, c, ldexp((double)tb.X[pb[i]], -60));
+            Pt += tb.X[pb[i]];
+            i++;
+        }
+        if (!(sum >= 2.0)) continue;
+        const u128 E = (u128)(to_units(sum) - to_units(c));
+        int64_t D = (int64_t)(E - Pt);
+        uint32_t F = (uint32_t)E & 511;
+        uint32_t j = (i + L - 1) / L;
+        if (i % L) {
+            D += replay(tb, pb + i, std::min(n, j * L) - i, Pt, F, D);
+            st.replays++;
+        }
+        for (; j < nseg; j++) {
+            if ((uint32_t)((P[j] + (u128)(i128)D) & 511) != F) abort();
+            Fn f;
+            unpack_seg(segfn[j], f);
+            if (apply(f, F, D)) continue;
+            st.replays++;
+            D += replay(tb, pb + j * L, std::min(L, n - j * L), P[j], F, D);
+        }
+        const u128 Ef = Pn + (u128)(i128)D;
+        sum = to_double(Ef);
+        c = ldexp((double)(int64_t)(to_units(sum) - (i128)Ef), -60);
+    }
+    return sum;
+}
+
 static int check(const std::vector<uint8_t> &b, const ByteTab &tb, Stats &st, const char *what) {
     const double ref = kahan_ref(b, tb);
     const Stats before = st;
@@ -138,6 +205,24 @@ static int check(const std::vector<uint8_t> &b, const ByteTab &tb, Stats &st, co
     if (memcmp(&ref, &got, 8) != 0) {
         printf("MISMATCH %s n %zu: ref %.17g got %.17g\n", what, b.size(), ref, got);
         return 1;
+    }
+    // the same chain split over 2..9 "ranks" at random cuts (some early: inside the transient,
+    // some empty pieces), each piece evaluated from the state the previous one left
+    static std::mt19937_64 rng(777);
+    const uint32_t n = (uint32_t)b.size();
+    for (int rep = 0; rep < 3; rep++) {
+        const int pieces = 2 + (int)(rng() % 8);
+        std::vector<uint32_t> cuts = {0, n};
+        for (int p = 1; p < pieces; p++) {
+            const uint64_t r = rng();
+            cuts.push_back(r % 4 == 0 ? (uint32_t)(r % std::min<uint32_t>(n + 1, 300)) : (uint32_t)(r % (n + 1)));
+        }
+        std::sort(cuts.begin(), cuts.end());
+        const double got2 = run_chain_split(b, cuts, tb, st);
+        if (memcmp(&ref, &got2, 8) != 0) {
+            printf("MISMATCH (split %d) %s n %zu: ref %.17g got %.17g\n", pieces, what, b.size(), ref, got2);
+            return 1;
+        }
     }
     return 0;
 }

@@ -6,7 +6,11 @@ src/Quantizer.cpp:27-31 assign, :80-86 fix), executed for real.
 
     python rank_worker.py RANK WORLD PORT CASE OUT.npz
 CASE: c2 -- the C2 image (512^2, 2x2) split into contiguous row ranges (qvq_set_vectors);
-      c5 -- the reduced C5 batch (4 x 512^2 images, 2x2), whole images per rank (qvq_set_synthetic).
+      c5 -- the reduced C5 batch (4 x 512^2 images, 2x2), whole images per rank (qvq_set_synthetic);
+      corpus -- every case of tests/golden/kahan_divergent.json (inputs where the reference's
+      Kahan centroid bits decide an index), rows split into contiguous ranges: per case the
+      quantize (C{i}, A{i}, d{i}, redo{i}) and qvq_update_kahan of the local indices (K{i}: the
+      reference's centroids over every rank's rows).
 """
 import os
 import sys
@@ -43,6 +47,26 @@ def main():
     elif case == "c5":
         lo, hi = shard(4, world, rank)
         eng.set_synthetic(512, 0x5EED + lo, hi - lo, 2, 2)
+    elif case == "corpus":
+        import json
+        from oracle import oracle
+        sys.path.insert(0, os.path.join(ROOT, "tests", "helpers"))
+        from kahan_env_worker import make
+        corpus = json.load(open(os.path.join(ROOT, "tests", "golden", "kahan_divergent.json")))
+        res = {}
+        for i, c in enumerate(corpus["noise_seeds"] + corpus["found"]):
+            X, _ = oracle.tile(make(c), c["side"], c["side"], c["bw"], c["bh"])
+            lo, hi = shard(X.shape[0], world, rank)
+            eng.set_vectors(X[lo:hi])
+            C, A, d = eng.lbg(c["bits"])
+            tm = eng.timings()
+            res.update({"C%d" % i: C, "A%d" % i: A, "d%d" % i: np.array([d]), "redo%d" % i: np.array([tm["kahan_redo"]]),
+                        "relays%d" % i: np.array([tm["kahan_relays"]]),
+                        "K%d" % i: eng.update_kahan(A, 1 << c["bits"])})
+        np.savez(out, info=np.array(eng.comm_info()), **res)
+        eng.close()
+        dist.destroy_process_group()
+        return
     else:
         raise SystemExit("unknown case " + case)
     C, A, d = eng.lbg(10)

@@ -92,8 +92,7 @@ KAHAN_CASES = [
 ]
 
 
-@pytest.mark.parametrize("case", KAHAN_CASES, ids=lambda c: "-".join(str(x) for x in c))
-def test_kahan_centroids_are_the_reference_bits(engine, case):
+def _kahan_input(case):
     img, side, bw, bh, K, how = case
     if img == "noise":
         rgb = np.random.default_rng(7).integers(0, 256, side * side * 3, dtype=np.uint8)
@@ -117,7 +116,97 @@ def test_kahan_centroids_are_the_reference_bits(engine, case):
         A = assigns[-1].astype(np.uint32)
     else:
         A = _spatial_assign(n, K, seed=side + K)
+    return rgb, X, A
+
+
+@pytest.mark.parametrize("case", KAHAN_CASES, ids=lambda c: "-".join(str(x) for x in c))
+def test_kahan_centroids_are_the_reference_bits(engine, case):
+    img, side, bw, bh, K, how = case
+    rgb, X, A = _kahan_input(case)
     engine.set_images(rgb, 1, side, side, bw, bh, oracle.SCALED)
     C = engine.update_kahan(A, K)
     C_ref = oracle.centroids(X, A, K, sum_mode=0)
     np.testing.assert_array_equal(C.view(np.uint64), C_ref.view(np.uint64))
+
+
+def _cuts(n, rng, pieces):
+    """Row offsets cutting n rows into `pieces` ranks: some cuts early (inside the chains' double
+    transient), some repeated (a rank without rows), some at the end."""
+    c = [0, n]
+    for p in range(pieces - 1):
+        r = rng.random()
+        c.append(int(rng.integers(0, min(n, 40) + 1)) if r < 0.3 else n if r < 0.4 else int(rng.integers(0, n + 1)))
+    return np.array(sorted(c), np.uint64)
+
+
+@pytest.mark.parametrize("case", KAHAN_CASES, ids=lambda c: "-".join(str(x) for x in c))
+def test_chained_kahan_centroids_are_the_reference_bits(engine, case):
+    """a cell's Kahan chain split over ranks (k_kahan.hip chained evaluation: each
+    rank's functions built at the chain's global prefix, the state (sum, c) handed from rank to
+    rank), here as virtual ranks on one device at random cuts -- the reference's bits for every
+    cut (src/Quantizer.cpp:59-70 sums the cell's rows in ascending order over all of them)."""
+    img, side, bw, bh, K, how = case
+    rgb, X, A = _kahan_input(case)
+    engine.set_images(rgb, 1, side, side, bw, bh, oracle.SCALED)
+    C_ref = oracle.centroids(X, A, K, sum_mode=0).view(np.uint64)
+    rng = np.random.default_rng(side * 131 + K)
+    n = X.shape[0]
+    for pieces in (2, 3, 5, 8):
+        cuts = _cuts(n, rng, pieces)
+        C = engine.update_kahan_split(A, K, cuts)
+        np.testing.assert_array_equal(C.view(np.uint64), C_ref, err_msg="cuts %s" % cuts.tolist())
+
+
+CORPUS_SUBSET = CORPUS["noise_seeds"] + CORPUS["found"][::4]
+
+
+@pytest.mark.parametrize("case", CORPUS_SUBSET, ids=lambda c: "%s-%d-%d-%dx%d-n%d" % (
+    c["kind"], c["seed"], c["side"], c["bw"], c["bh"], c["bits"]))
+def test_corpus_through_one_rank_communicator(engine, case):
+    """The verdict's r04 gap: with a communicator the indices must follow the reference's rule
+    too.  A one-rank RCCL communicator runs the collective schedule; its codebook and indices
+    equal the communicator-free run's (and the oracle's Kahan rule)."""
+    import quant_amd
+    rgb = _make(case)
+    side, bw, bh, bits = case["side"], case["bw"], case["bh"], case["bits"]
+    engine.set_images(rgb, 1, side, side, bw, bh, oracle.SCALED)
+    C0, A0, d0 = engine.lbg(bits)
+    with quant_amd.Engine(0) as eng:
+        eng.comm_init(1, 0, quant_amd.Engine.comm_unique_id())
+        assert _check(eng, case) > 0
+        C1, A1, d1 = eng.lbg(bits)
+    np.testing.assert_array_equal(A1, A0)
+    np.testing.assert_array_equal(C1, C0)
+    assert d1 == d0
+
+
+def _env_worker(env, cases):
+    import subprocess
+    import sys
+    worker = os.path.join(os.path.dirname(os.path.abspath(__file__)), "helpers", "kahan_env_worker.py")
+    r = subprocess.run([sys.executable, worker, json.dumps(cases)], env=dict(os.environ, **env), capture_output=True,
+                       text=True, timeout=240)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-3000:]
+    return [json.loads(l) for l in r.stdout.splitlines() if l.startswith("{")]
+
+
+def test_synchronous_kahan_levels_follow_the_reference_rule():
+    """the synchronous Kahan path (QVQ_SPECULATE=0: every tie level's ties answered
+    by the certificate or the whole reference-bit split before the level finishes) on corpus
+    cases, in a process of its own (the switch is read once)."""
+    res = _env_worker({"QVQ_SPECULATE": "0"}, CORPUS["noise_seeds"][:2] + CORPUS["found"][:6])
+    assert len(res) == 8
+    for r in res:
+        assert r["A_ok"] and r["C_ok"] and r["again_ok"], r
+        assert r["redo"] == 0
+
+
+def test_failed_check_redoes_the_quantize():
+    """a speculative check that fails (forced at level 6, QVQ_KAHAN_FAIL_LEVEL) makes
+    the quantize run again with synchronous Kahan levels: kahan_redo == 1, the indices are still
+    the reference's, and a second quantize on the same context agrees."""
+    res = _env_worker({"QVQ_KAHAN_FAIL_LEVEL": "6"}, CORPUS["noise_seeds"][:1] + [
+        dict(kind="gen", seed=0x5EED, side=256, bw=2, bh=2, bits=8)])
+    for r in res:
+        assert r["A_ok"] and r["C_ok"] and r["again_ok"], r
+        assert r["redo"] == 1

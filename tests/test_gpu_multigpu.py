@@ -7,6 +7,7 @@ exchange runs here through a real one-rank RCCL communicator (qvq_comm_init(1, 0
 results must equal the communicator-free run bit for bit -- the property that makes the
 1/2/4/8-GPU codebooks identical (exact integer sums).  The reference loops
 being sharded are src/Quantizer.cpp:24-32 (assign) and :72-87 (centroids)."""
+import json
 import os
 import socket
 import subprocess
@@ -82,7 +83,7 @@ def test_c5_full_batch_properties():
         assert oracle.sha16(A4) == h_first
 
 
-def _run_ranks(world, case, tmp_path):
+def _run_ranks(world, case, tmp_path, env=None):
     """world rank processes (tests/helpers/rank_worker.py) sharing GPU 0 through the host
     communicator; returns each rank's results."""
     with socket.socket() as s:
@@ -90,7 +91,9 @@ def _run_ranks(world, case, tmp_path):
         port = str(s.getsockname()[1])
     worker = os.path.join(os.path.dirname(os.path.abspath(__file__)), "helpers", "rank_worker.py")
     outs = [str(tmp_path / ("rank%d.npz" % r)) for r in range(world)]
-    procs = [subprocess.Popen([sys.executable, worker, str(r), str(world), port, case, outs[r]]) for r in range(world)]
+    penv = dict(os.environ, **(env or {}))
+    procs = [subprocess.Popen([sys.executable, worker, str(r), str(world), port, case, outs[r]], env=penv)
+             for r in range(world)]
     try:
         codes = [p.wait(timeout=240) for p in procs]
     finally:
@@ -107,8 +110,7 @@ def test_sharded_ranks_bit_identical_c2(engine, tmp_path, world):
     """The N>1 schedule executed: C2's rows split over `world` processes (contiguous ranges,
     one shared GPU, the per-level exchange through gloo).  Every rank gets the 1-rank codebook
     and distortion bit for bit, the ranks' indices concatenate to the 1-rank indices, and all
-    equal the oracle (on one rank the reference's Kahan rule; with a communicator the engine
-    keeps the exact-sum rule, DESIGN.md 5 -- the two agree on this input)."""
+    equal the oracle's reference (Kahan) rule."""
     X, _ = oracle.tile(oracle.gen_image(512, 0x5EED), 512, 512, 2, 2)
     engine.set_vectors(X)
     C0, A0, d0 = engine.lbg(10)
@@ -137,8 +139,7 @@ def test_sharded_ranks_bit_identical_c5_slice(engine, tmp_path):
     X = np.concatenate([oracle.tile(im, 512, 512, 2, 2)[0] for im in imgs])
     C_x, A_x, _ = oracle.lbg(X, 10, sum_mode=1)
     _, A_k, _ = oracle.lbg(X, 10, sum_mode=0)
-    np.testing.assert_array_equal(A0, A_k)   # one rank: the reference rule
-    np.testing.assert_array_equal(A_k, A_x)  # (the ranks' exact-sum rule agrees here)
+    np.testing.assert_array_equal(A0, A_k)   # the reference rule
     np.testing.assert_array_equal(C0, C_x)
     res = _run_ranks(2, "c5", tmp_path)
     for r in res:
@@ -166,3 +167,71 @@ def test_failed_wait_poisons_the_context():
         eng.set_synthetic(512, 0x5EED, 1, 2, 2)
         C, A, d = eng.lbg(4)
         assert A.max() < 16
+
+
+CORPUS = json.load(open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "kahan_divergent.json")))
+CASES = CORPUS["noise_seeds"] + CORPUS["found"]
+
+
+def _corpus_expect(engine):
+    """Per corpus case: the tiled rows, the oracle's reference (Kahan) rule, and the one-rank
+    engine's results."""
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "helpers"))
+    from kahan_env_worker import make
+    out = []
+    for c in CASES:
+        X, _ = oracle.tile(make(c), c["side"], c["side"], c["bw"], c["bh"])
+        _, A_k, _ = oracle.lbg(X, c["bits"], sum_mode=0)
+        _, A_x, _ = oracle.lbg(X, c["bits"], sum_mode=1)
+        engine.set_vectors(X)
+        C0, A0, d0 = engine.lbg(c["bits"])
+        np.testing.assert_array_equal(A0, A_k)
+        out.append((X, A_k, A_x, C0, d0))
+    return out
+
+
+@pytest.fixture(scope="module")
+def corpus_expect(engine):
+    return _corpus_expect(engine)
+
+
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("world", [2, 3])
+def test_sharded_ranks_follow_the_kahan_rule_on_the_corpus(corpus_expect, tmp_path, world):
+    """with a communicator the indices follow the reference's rule.  Every
+    case of the divergent corpus (the exact-sum rule's indices differ from the reference's there)
+    with its rows split over `world` processes: the ranks' indices concatenate to the oracle's
+    Kahan-rule indices, every rank's codebook and distortion equal the one-rank run's bit for
+    bit, and qvq_update_kahan of the local indices returns the reference's centroids over all the
+    rows (cells' chains across ranks, src/Quantizer.cpp:59-70)."""
+    res = _run_ranks(world, "corpus", tmp_path)
+    relays = 0
+    for i, (X, A_k, A_x, C0, d0) in enumerate(corpus_expect):
+        assert not np.array_equal(A_k, A_x)
+        bits = CASES[i]["bits"]
+        np.testing.assert_array_equal(np.concatenate([r["A%d" % i] for r in res]), A_k, err_msg="case %d" % i)
+        K_ref = oracle.centroids(X, A_k, 1 << bits, sum_mode=0)
+        for r in res:
+            np.testing.assert_array_equal(r["C%d" % i], C0, err_msg="case %d" % i)
+            assert float(r["d%d" % i][0]) == d0
+            np.testing.assert_array_equal(r["K%d" % i].view(np.uint64), K_ref.view(np.uint64), err_msg="case %d" % i)
+        relays += int(res[0]["relays%d" % i][0])
+        assert len({int(r["redo%d" % i][0]) for r in res}) == 1   # every rank redoes, or none
+    assert relays > 0   # some levels needed cells summed across the ranks
+
+
+@pytest.mark.timeout(300)
+def test_one_rank_failure_redoes_every_rank(corpus_expect, tmp_path):
+    """A check failing on rank 0 only (QVQ_KAHAN_FAIL_LEVEL / _RANK) makes both ranks redo the
+    quantize with synchronous several-rank Kahan levels (the whole reference split summed across
+    the ranks on each tie level): same indices, kahan_redo 1 on both."""
+    res = _run_ranks(2, "corpus", tmp_path, env={"QVQ_KAHAN_FAIL_LEVEL": "4", "QVQ_KAHAN_FAIL_RANK": "0"})
+    redone = 0
+    for i, (X, A_k, A_x, C0, d0) in enumerate(corpus_expect):
+        np.testing.assert_array_equal(np.concatenate([r["A%d" % i] for r in res]), A_k, err_msg="case %d" % i)
+        for r in res:
+            np.testing.assert_array_equal(r["C%d" % i], C0, err_msg="case %d" % i)
+        rd = {int(r["redo%d" % i][0]) for r in res}
+        assert len(rd) == 1
+        redone += rd.pop()
+    assert redone >= len([c for c in CASES if c["bits"] >= 4])

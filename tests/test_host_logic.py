@@ -105,3 +105,12 @@ def test_bench_cie_blocks_follow_the_reference_tiling():
                     (p[:, 0] * 0.17697 + p[:, 1] * 0.81240 + p[:, 2] * 0.01063) / 0.17697,
                     (p[:, 0] * 0 + p[:, 1] * 0.01 + p[:, 2] * 0.99) / 0.17697], axis=1).reshape(-1, 12)
     np.testing.assert_array_equal(X, ref)
+
+
+def test_cert_pool_runs_each_slot_once():
+    """pool_run's helpers read a job's epoch, width and fn together, and a helper
+    spawned later starts from the current epoch -- no slot runs twice or is skipped while the
+    width grows and shrinks from job to job."""
+    import quant_amd
+    assert quant_amd.host_pool_stress(3000, 13) == 0
+    assert quant_amd.host_pool_stress(300, 64) == 0

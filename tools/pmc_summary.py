@@ -16,7 +16,7 @@ import sys
 
 def short(name):
     m = re.search(r"qvq(?:::|\d+)([A-Za-z_]+?)(?:_kernel)?(?:I|E|\(|$)", name)
-    m3 = re.search(r"assign_small_kernel(?:ILi(\d+)ELb([01])E|<(\d+), (true|false)>)", name)
+    m3 = re.search(r"assign_small_kernel(?:ILi(\d+)ELb([01])E|<(\d+), (true|false)[,>])", name)
     if m3:
         sk = m3.group(1) or m3.group(3)
         fused = m3.group(2) == "1" or m3.group(4) == "true"
