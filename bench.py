@@ -294,6 +294,7 @@ def main():
         update_ms.append(u_ms)
         flagged.append(f_rows)
     eng.set_timing(-2)
+    tm_last = eng.timings()   # the last quantize's Kahan-rule statistics
     torch.cuda.synchronize()
     barrier()
     if world > 1:
@@ -379,6 +380,11 @@ def main():
                            "achieved_GBps": round(upd_bytes / upd_secs / 1e9, 1), "peak_GBps": PEAK_HBM_GBS}
                           if upd_secs else "fused into the search (LDS u64 atomics of exact integer terms)"),
         "flagged_rows_per_step": flagged[-1],
+        # the indices' rule: the reference's (Kahan centroid bits decide the tie rows, on every
+        # rank count) unless QVQ_KAHAN=0 selects the exact-sum rule (A/B)
+        "index_rule": "exact-sum" if os.environ.get("QVQ_KAHAN") == "0" else "kahan (reference)",
+        "kahan_checks": {"redo": tm_last["kahan_redo"], "cross_rank_cell_sums": tm_last["kahan_relays"],
+                         "tie_export_overflow": tm_last["tie_overflow"]},
     }
     def timed(fn, steps, warmup):
         """Max-over-ranks wall of `steps` calls of fn after `warmup`, barrier + sync on both sides."""

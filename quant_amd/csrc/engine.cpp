@@ -177,6 +177,7 @@ struct qvq_ctx {
     uint8_t *h_tree[2] = {nullptr, nullptr}, *dh_tree[2] = {nullptr, nullptr};
     uint8_t *d_tree = nullptr;   // device copy of the level's tree image (one DMA per level)
     std::vector<double> cb_local;   // host copy of the published codebook for the tree build
+    std::vector<uint32_t> cnt_local;   // ... and of its parent cells' row counts (empty: not known)
     std::unique_ptr<RefKDTree> tree;   // the last level's tree over cb_local
     KdView tree_kd;                    // and its device image (depth 0: none)
     // deferred-tie levels build their tree on this worker, off the launch path (start_tree_job)
@@ -216,6 +217,7 @@ struct qvq_ctx {
         const uint32_t *A_prev = nullptr;
         std::unique_ptr<RefKDTree> tree;
         std::vector<double> cb;
+        std::vector<uint32_t> cnt;   // the parent cells' row counts (empty: not known)
         CertState cs;
         hipEvent_t ev = nullptr;
     } ver[3];   // level % 3
@@ -560,7 +562,7 @@ qvq_status ensure_levels(qvq_ctx *ctx, uint32_t Kmax) {
     HIPCHK(hipMemset(ctx->d_sums, 0, 2 * (2 * KD + Kmax) * 8));
     ctx->sums_bytes = 2 * (2 * KD + Kmax) * 8;
     const unsigned mflags = hipHostMallocMapped | hipHostMallocCoherent;
-    HIPCHK(hipHostMalloc(&ctx->h_cb, KD * 8, mflags));
+    HIPCHK(hipHostMalloc(&ctx->h_cb, KD * 8 + (uint64_t)Kmax * 4, mflags));   // split rows | parent counts
     HIPCHK(hipHostGetDevicePointer((void **)&ctx->dh_cb, ctx->h_cb, 0));
     ctx->tree_cap = tree_bytes(Kmax, ctx->D);
     for (int b = 0; b < 2; b++) {
@@ -753,7 +755,8 @@ qvq_status vote(qvq_ctx *ctx, uint64_t *vals, uint64_t n) {
 // 5; src/Quantizer.cpp:59-70 sums each cell's rows in ascending global order, so a chain runs
 // across the ranks).  A: this rank's rows' cells among K_in (nullptr: the mean, K_in = S = 1);
 // sel: the device slot map of launch_kahan_centroids (nullptr: every cell, S = K_in).  Every
-// rank calls it with the same cells and gets the same C_out [S][D] / split_out [2S][D] (device):
+// rank calls it with the same cells and gets the same centroids in d_kc_cent [S][D] and, with
+// want_split, their split in d_kc_split [2S][D] (device; ensure_kahan sizes both):
 //   1. each rank sorts its rows of the cells and sums each chain exactly (its totals and row
 //      counts into its slice of an all-gather, one collective): every chain's exact prefix at
 //      each rank's first row;
@@ -765,15 +768,16 @@ qvq_status vote(qvq_ctx *ctx, uint64_t *vals, uint64_t n) {
 // splits (qvq_update_kahan_split, tests): this context's rows as virtual ranks cut at the given
 // offsets, run one after another on the device (no collective).
 qvq_status kahan_chained(qvq_ctx *ctx, const uint32_t *A, uint32_t K_in, const uint32_t *sel, uint32_t S,
-                         double *C_out, double *split_out, const std::vector<uint64_t> *splits = nullptr) {
+                         bool want_split, const std::vector<uint64_t> *splits = nullptr) {
     const uint32_t D = ctx->D, Dp = ctx->Dp;
     const bool virt = splits != nullptr;
     const uint32_t R = virt ? (uint32_t)splits->size() - 1 : (uint32_t)ctx->nranks;
     const uint32_t rank = virt ? 0u : (uint32_t)ctx->rank;
     const uint32_t Ks = sel ? S : K_in;   // the sort's keys: slots, or cells
     if (!A && (K_in != 1 || S != 1 || sel)) return fail(ctx, QVQ_EINVAL, "kahan_chained: the mean is one cell");
-    qvq_status st = ensure_kahan(ctx, std::max(K_in, S));
+    qvq_status st = ensure_kahan(ctx, std::max(K_in, S));   // (may reallocate the outputs below)
     if (st != QVQ_OK) return st;
+    double *C_out = ctx->d_kc_cent, *split_out = want_split ? ctx->d_kc_split : nullptr;
     const uint64_t gcount = 2ull * R * S * D + (uint64_t)R * S, scount = 2ull * S * D;
     if (ctx->kc_chain_cap < gcount + scount) {
         dfree(ctx->d_kc_chain);
@@ -823,6 +827,12 @@ void build_tree_host(qvq_ctx *ctx, const double *hC, uint32_t K, int buf, KdView
     // the build reads the codebook many times; mapped memory the GPU just wrote is read
     // once, sequentially, into ordinary memory first
     ctx->cb_local.assign(hC, hC + (size_t)K * ctx->D);
+    if (hC == ctx->h_cb && K >= 2) {   // the finalize's split: the parent counts follow it
+        const uint32_t *cnt = reinterpret_cast<const uint32_t *>(hC + (size_t)K * ctx->D);
+        ctx->cnt_local.assign(cnt, cnt + K / 2);
+    } else {
+        ctx->cnt_local.clear();
+    }
     ctx->tree.reset(new RefKDTree(ctx->cb_local.data(), K, (int)ctx->D, cancel));
     const RefKDTree &tree = *ctx->tree;
     if (tree.cancelled()) return;
@@ -1313,8 +1323,9 @@ void pool_run(qvq_ctx *ctx, uint32_t n, const std::function<void(uint32_t)> &fn)
 // need in cs.sel (their candidates' and the blamed points'), and cert_finish completes them once
 // the ranks have summed those cells together (qvq_lbg).
 template <class Sync>
-qvq_status certify_rows(qvq_ctx *ctx, const RefKDTree &tree, const double *cb, uint32_t K, const uint32_t *A_prev,
-                        hipStream_t stream, Sync sync, CertState &cs, bool defer, uint32_t &open_rows) {
+qvq_status certify_rows(qvq_ctx *ctx, const RefKDTree &tree, const double *cb, const std::vector<uint32_t> &pcnt,
+                        uint32_t K, const uint32_t *A_prev, hipStream_t stream, Sync sync, CertState &cs, bool defer,
+                        uint32_t &open_rows) {
     const uint32_t D = ctx->D, Kc = K / 2, nu = cs.nu;
     const std::vector<double> &qs = cs.qs;
     std::vector<int64_t> &ans = cs.ans;
@@ -1325,11 +1336,15 @@ qvq_status certify_rows(qvq_ctx *ctx, const RefKDTree &tree, const double *cb, u
     std::vector<uint8_t> &known = cs.known;
     kp.assign(cb, cb + (size_t)K * D);
     known.resize((size_t)K * D);
+    // and every component of a cell of at most two rows (its Kahan sum, of one value or two, is
+    // the exact sum rounded once: the same centroid bits; pcnt, the finalize's parent counts)
+    const bool counts = pcnt.size() == Kc;
     for (uint32_t j = 0; j < K; j++) {
         const double u = j < Kc ? 1 + 0.2 : 1 - 0.2;
         const double *v = &kp[(size_t)j * D];
         uint8_t *k = &known[(size_t)j * D];
-        for (uint32_t d = 0; d < D; d++) k[d] = v[d] == 0 || std::fabs(v[d] - u) <= 1e-14;
+        const bool few = counts && pcnt[j % Kc] <= 2;
+        for (uint32_t d = 0; d < D; d++) k[d] = few || v[d] == 0 || std::fabs(v[d] - u) <= 1e-14;
     }
     ans.assign(nu, -1);
     cs.pend.clear();
@@ -1545,7 +1560,7 @@ qvq_status certify_kahan_ties(qvq_ctx *ctx, uint32_t K, unsigned nt, uint64_t *t
     CertState cs;
     cs.nu = distinct_rows(ctx, code.data(), Dp, nt, cs.qs, cs.of);
     uint32_t open = 0;
-    if ((st = certify_rows(ctx, *ctx->tree, ctx->cb_local.data(), K, K == 2 ? nullptr : ctx->d_A_alt, ctx->stream,
+    if ((st = certify_rows(ctx, *ctx->tree, ctx->cb_local.data(), ctx->cnt_local, K, K == 2 ? nullptr : ctx->d_A_alt, ctx->stream,
                            [ctx] { return wait_stream(ctx); }, cs, false, open)) != QVQ_OK)
         return st;
     if (open) {
@@ -1626,7 +1641,7 @@ void verify_level(qvq_ctx *ctx, qvq_ctx::Verify &v) {
     };
     const bool defer = ctx->nranks > 1;
     // (A_prev is complete: the GPU wrote the flag seen above after the levels that made it)
-    if (certify_rows(ctx, *v.tree, v.cb.data(), v.K, v.A_prev, ctx->vstream, sync, cs, defer, open) != QVQ_OK ||
+    if (certify_rows(ctx, *v.tree, v.cb.data(), v.cnt, v.K, v.A_prev, ctx->vstream, sync, cs, defer, open) != QVQ_OK ||
         (open && !defer))
         return;
     if (cert_mismatch(cs, v.K)) return;
@@ -1766,7 +1781,7 @@ qvq_status resolve_kahan_ties_multi(qvq_ctx *ctx, uint32_t K, int slot, unsigned
     const uint32_t D = ctx->D, Kc = K / 2;
     qvq_status st;
     uint64_t *target = ctx->d_sums + sums_cap_stride(ctx);
-    if ((st = kahan_chained(ctx, K == 2 ? nullptr : ctx->d_A_alt, Kc, nullptr, Kc, ctx->d_kc_cent, ctx->d_kc_split)) !=
+    if ((st = kahan_chained(ctx, K == 2 ? nullptr : ctx->d_A_alt, Kc, nullptr, Kc, true)) !=
         QVQ_OK)
         return st;
     ctx->h_kc_split.resize((size_t)K * D);
@@ -1829,9 +1844,9 @@ qvq_status resolve_deferred(qvq_ctx *ctx, uint32_t bits, const std::vector<uint3
             for (uint32_t c = 0; c < Kc; c++) ctx->h_kc_sel[c] = 0;
             for (uint32_t t = 0; t < S; t++) ctx->h_kc_sel[cell_of[t]] = t + 1;
             HIPCHK(hipMemcpyAsync(ctx->d_kc_sel, ctx->h_kc_sel, (size_t)Kc * 4, hipMemcpyHostToDevice, ctx->stream));
-            st = kahan_chained(ctx, alev[L - 1], Kc, ctx->d_kc_sel, S, ctx->d_kc_cent, ctx->d_kc_split);
+            st = kahan_chained(ctx, alev[L - 1], Kc, ctx->d_kc_sel, S, true);
         } else {
-            st = kahan_chained(ctx, nullptr, 1, nullptr, 1, ctx->d_kc_cent, ctx->d_kc_split);
+            st = kahan_chained(ctx, nullptr, 1, nullptr, 1, true);
         }
         if (st != QVQ_OK) return st;
         split.resize(2ull * S * D);
@@ -2355,8 +2370,10 @@ QVQ_API qvq_status qvq_lbg(qvq_ctx *ctx, uint32_t bits, double eps, double *code
     // the split a finalize writes: with deferred ties the level's own split must survive its
     // (speculative) finalize, so the next one goes to the other buffer and the two swap
     double *split_out = ctx->d_C64_split;
+    // clear1: the finalize also clears sums copy 1 after adding it (no fused search of a later
+    // level clears it: a communicator, or the synchronous Kahan levels' moves)
     auto finalize = [&](uint32_t K, bool split, uint32_t copies = 1, const unsigned *gate = nullptr,
-                        const TieExport &tx = TieExport()) {
+                        const TieExport &tx = TieExport(), bool clear1 = false) {
         if (split || tx.out) ctx->seq++;
         const bool prune = split && use_prune(ctx, 2 * K);   // the next search's tile order
         ctx->perm_k = prune ? 2 * K : 0;
@@ -2366,7 +2383,7 @@ QVQ_API qvq_status qvq_lbg(qvq_ctx *ctx, uint32_t bits, double eps, double *code
                                     ctx->d_C32, ctx->d_rows, ctx->d_E32, split ? ctx->dh_cb : nullptr, d_dist + 8,
                                     dist_done,
                                     split ? nullptr : d_dist + 2, (split || tx.out) ? ctx->dh_ready : nullptr,
-                                    ctx->seq, K == 1, K == 1 ? MEAN_COPIES : copies,
+                                    ctx->seq, K == 1 || (clear1 && copies > 1), K == 1 ? MEAN_COPIES : copies,
                                     prune ? ctx->d_perm : nullptr, prune ? ctx->d_tint : nullptr, K == 1 ? 0 : 1,
                                     copies > 1 ? sums_cap_stride(ctx) : 0,
                                     gate, tx);
@@ -2457,7 +2474,9 @@ QVQ_API qvq_status qvq_lbg(qvq_ctx *ctx, uint32_t bits, double eps, double *code
                 v.A_prev = lvl >= 2 ? ctx->d_A_alt : nullptr;
                 v.tree = std::move(ctx->tree);
                 v.cb = std::move(ctx->cb_local);
+                v.cnt = std::move(ctx->cnt_local);
                 ctx->cb_local.clear();
+                ctx->cnt_local.clear();
                 qvq_ctx::Verify *vp = &v;
                 post_job(ctx, [ctx, vp] {
                     verify_level(ctx, *vp);
@@ -2475,11 +2494,13 @@ QVQ_API qvq_status qvq_lbg(qvq_ctx *ctx, uint32_t bits, double eps, double *code
                     if (multi) {   // every rank's moves in copy 1, all-reduced, added by the finalize
                         ctx->sums1_dirty = true;
                         if ((st = resolve_kahan_ties_multi(ctx, K, slot, nt)) != QVQ_OK) return st;
-                        HIPCHK(finalize(K, split, 2, nullptr));
+                        HIPCHK(finalize(K, split, 2, nullptr, TieExport(), true));
                     } else {
                         if (fused) ctx->sums1_dirty = true;
                         if ((st = resolve_kahan_ties(ctx, K, slot, nt, fused)) != QVQ_OK) return st;
-                        HIPCHK(finalize(K, split, fused ? 2 : 1, fused ? tcnt : nullptr));
+                        // (without kd_reduce no fused search clears copy 1 before its next use)
+                        HIPCHK(finalize(K, split, fused ? 2 : 1, fused ? tcnt : nullptr, TieExport(),
+                                        fused && !kd_merge(ctx)));
                     }
                     ctx->sums1_dirty = false;
                 }
@@ -2651,7 +2672,7 @@ QVQ_API qvq_status qvq_update_kahan(qvq_ctx *ctx, const uint32_t *assign, uint32
     if ((st = ensure_kahan(ctx, K)) != QVQ_OK) return st;
     HIPCHK(hipMemcpy(ctx->d_A, assign, ctx->N * 4, hipMemcpyHostToDevice));
     if (ctx->nranks > 1) {   // every rank's rows: the chains pass from rank to rank (kahan_chained)
-        if ((st = kahan_chained(ctx, K == 1 ? nullptr : ctx->d_A, K, nullptr, K, ctx->d_kc_cent, nullptr)) != QVQ_OK)
+        if ((st = kahan_chained(ctx, K == 1 ? nullptr : ctx->d_A, K, nullptr, K, false)) != QVQ_OK)
             return st;
     } else {
         HIPCHK(launch_kahan_centroids(ctx->stream, ctx->kw, ctx->d_codes, ctx->Dp, ctx->D, ctx->N,
@@ -2692,7 +2713,7 @@ QVQ_API qvq_status qvq_update_kahan_split(qvq_ctx *ctx, const uint32_t *assign, 
     if (st != QVQ_OK) return st;
     HIPCHK(hipMemcpy(ctx->d_A, assign, ctx->N * 4, hipMemcpyHostToDevice));
     const std::vector<uint64_t> cuts(splits, splits + nsplits + 1);
-    if ((st = kahan_chained(ctx, K == 1 ? nullptr : ctx->d_A, K, nullptr, K, ctx->d_kc_cent, nullptr, &cuts)) != QVQ_OK)
+    if ((st = kahan_chained(ctx, K == 1 ? nullptr : ctx->d_A, K, nullptr, K, false, &cuts)) != QVQ_OK)
         return st;
     const uint64_t cB = (uint64_t)K * ctx->D * 8;
     if ((st = ensure_pinned(ctx, ctx->h_stage, ctx->stage_bytes, cB)) != QVQ_OK) return st;

@@ -21,6 +21,22 @@
 
 #define QVQ_FOR_EACH_DP(X) X(4) X(8) X(12) X(16) X(20) X(24) X(28) X(32) X(36) X(40) X(44) X(48) X(52) X(56) X(60) X(64)
 
+// QVQ_KDEBUG builds (tools: a debug libqvq): bounds checks on the chains' global accesses, a
+// failed one printed and the access skipped
+#ifdef QVQ_KDEBUG
+#define KCHK(cond)                                                                                          \
+    do {                                                                                                    \
+        if (!(cond)) {                                                                                      \
+            printf("KCHK line %d: %s (block %u thread %u)\n", __LINE__, #cond, blockIdx.x, threadIdx.x);     \
+            return;                                                                                         \
+        }                                                                                                   \
+    } while (0)
+#else
+#define KCHK(cond) \
+    do {           \
+    } while (0)
+#endif
+
 namespace qvq {
 
 using kahan::ByteTab;
@@ -184,6 +200,7 @@ __global__ __launch_bounds__(64) void ks_scatter_kernel(const uint8_t *__restric
         for (int u = 0; u < W; u++) row[u] = __shfl(w[u], from, 64);
         if (key != NOKEY) {
             const uint32_t dst = cur[key] + (lane - rs);
+            KCHK(key < K && dst < PL && (uint64_t)(D - 1) * PL + dst < (uint64_t)PL * D + 64);
 #pragma unroll
             for (int d = 0; d < DP; d++)
                 if ((uint32_t)d < D) planes[(uint64_t)d * PL + dst] = (uint8_t)(row[d >> 2] >> (8 * (d & 3)));
@@ -229,6 +246,7 @@ struct Geo {
     kahan::SegFn *sfn;                        // [D][segoff[K]]: the segment functions (estimates 0)
     Fn *bfn8;                                 // [D][blkoff[K]][8]: 8-segment sub-block functions
     unsigned *stats;                          // [4]: blocks not composable, block misses, segment replays, chains
+    uint64_t plane_bytes, seg_cap, blk_cap;   // capacities (QVQ_KDEBUG checks)
 };
 
 __device__ inline void stage_tab(const ByteTab *__restrict__ g, ByteTab *t) {
@@ -278,6 +296,8 @@ __global__ __launch_bounds__(64 * WPB) void ks_meta_kernel(Geo g, const ByteTab 
     const uint32_t k = find_cell(g.blkoff, g.K, bb), b = bb - g.blkoff[k];
     const uint32_t n = g.koff[k + 1] - g.koff[k];
     const uint32_t s0 = b * SPB, first = s0 * L, nb = min(BLK_STEPS, n - first);
+    KCHK(TB <= g.blk_cap && g.segoff[g.K] <= g.seg_cap && first < n && k < g.K);
+    KCHK((uint64_t)d * g.PL + g.koff[k] + first + nb + 8 <= g.plane_bytes);
     stage_bytes(g.planes + (uint64_t)d * g.PL + g.koff[k] + first, nb, bytes[w]);
     wave_sync();
     const uint32_t s = s0 + lane, nseg = (n + L - 1) / L;
@@ -306,6 +326,7 @@ __global__ __launch_bounds__(256) void ks_totals_kernel(Geo g, uint64_t *__restr
     if (wv >= (uint64_t)g.K * g.D) return;
     const uint32_t k = (uint32_t)(wv / g.D), d = (uint32_t)(wv - (uint64_t)k * g.D);
     const uint32_t TB = g.blkoff[g.K];
+    KCHK(TB <= g.blk_cap && g.blkoff[k + 1] <= TB && g.blkoff[k] <= g.blkoff[k + 1]);
     const u128 *p = g.bsum + (uint64_t)d * TB;
     uint64_t lo = 0, hi = 0;
     for (uint32_t i = g.blkoff[k] + lane; i < g.blkoff[k + 1]; i += 64) {
@@ -506,6 +527,9 @@ __global__ __launch_bounds__(64 * EPB) void ks_eval_kernel(Geo g, const ByteTab 
     const u128 *bpre = g.bsum + (uint64_t)d * TB + g.blkoff[k];
     const uint64_t mbase = (uint64_t)d * g.segoff[g.K] + g.segoff[k];
     const uint64_t t_out = (uint64_t)k * g.D + d;
+    KCHK(TB <= g.blk_cap && g.segoff[g.K] <= g.seg_cap && g.blkoff[k + 1] <= TB && g.koff[k + 1] <= g.koff[g.K]);
+    KCHK((uint64_t)d * g.PL + g.koff[g.K] + 64 <= g.plane_bytes);
+    KCHK(g.segoff[k] + nseg <= g.segoff[g.K] && g.blkoff[k] + (nseg + SPB - 1) / SPB <= g.blkoff[k + 1]);
     // the state entering this rank's rows, and their exact prefix (one rank: the chain's start)
     double sum = 0, c = 0;
     u128 P0 = 0;
@@ -743,6 +767,9 @@ Geo make_geo(const KahanWork &w, uint64_t N, uint32_t K, uint32_t D) {
     g.sfn = reinterpret_cast<kahan::SegFn *>(w.sfn);
     g.bfn8 = reinterpret_cast<Fn *>(w.bfn8);
     g.stats = w.stats;
+    g.plane_bytes = (uint64_t)w.d_cap * KahanWork::plane_len(w.n_cap);
+    g.seg_cap = w.seg_cap;
+    g.blk_cap = w.blk_cap;
     return g;
 }
 

@@ -946,7 +946,7 @@ hipError_t launch_copy_out(hipStream_t s, const void *src0, void *dst0, uint64_t
 // level's search tables.  Block = 256/L rows x L component lanes.  With split, row j < 2K is
 // split code vector j (cluster j mod K, factor 1.2 for j < K, 0.8 above) and rows
 // 2K..Kpad_next-1 are padding; the split codebook also goes to host_cb (mapped pinned
-// memory, for the host's kd-tree build).  L = 16, 32 or 64 lanes per row (>= Dp).  Without split (last level) row k < K writes
+// memory, for the host's kd-tree build; then the K cells' row counts, u32).  L = 16, 32 or 64 lanes per row (>= Dp).  Without split (last level) row k < K writes
 // centroid k and its distortion term sum_d (2 c S - n c^2).  The last block to finish sums
 // the per-block distortion terms in block order and then publishes *ready = seq (system
 // scope), which tells the host that host_cb holds the codebook.
@@ -993,6 +993,10 @@ __device__ inline void finalize_split_item(const FinArgs &a, uint32_t j, uint32_
             a.C64n[(uint64_t)j * D + d] = v;
             if (a.host_cb) a.host_cb[(uint64_t)j * D + d] = v;
         }
+        // after the split rows: the K cells' row counts (the tie check: a cell of <= 2 rows has
+        // the reference's bits, a Kahan sum of one or two values being the rounded exact sum)
+        if (a.host_cb && j < K && d == 0)
+            reinterpret_cast<uint32_t *>(a.host_cb + 2ull * K * D)[k] = cnt > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)cnt;
         if (d < Dp) a.C32[(uint64_t)j * Dp + d] = (float)v;
         if (a.rows) {   // MFMA row (common.hpp): hi / lo at their slots, norm at 2 LO
             const uint32_t RF = cb_row_f16(D, Dp), LO = cb_lo_off(D, Dp);
