@@ -95,6 +95,7 @@ struct CertState {
     std::vector<uint32_t> pend;       // distinct rows still open
     std::vector<uint8_t> sel;         // [K/2] the parent cells those rows need
     uint32_t cells = 0, rounds = 0;
+    bool prepared = false;            // kp / known set and the tree's replay state built (cert_init)
 };
 }  // namespace qvq
 
@@ -188,7 +189,7 @@ struct qvq_ctx {
         std::deque<std::function<void()>> q;
         bool stop = false;
         std::atomic<int> pending{0};
-    } worker;
+    } worker, prep;   // prep: each level's tie certificate prepared while the GPU runs the level
     // helpers of the worker for the certificate's replays (persistent: their per-thread replay
     // caches stay warm); pool_run forks fn over them and the calling thread
     struct Pool {
@@ -212,6 +213,7 @@ struct qvq_ctx {
         std::atomic<bool> done{true}, cancel{false};
         int status = 0;   // 0: the reference's indices are the speculative ones; 1: not shown; 2: deferred
         uint32_t K = 0, level = 0;
+        std::atomic<bool> prep_done{true};   // cs prepared (cert_init on the prep worker)
         uint64_t seq = 0;
         int par = 0;
         const uint32_t *A_prev = nullptr;
@@ -891,8 +893,8 @@ void build_tree(qvq_ctx *ctx, const double *hC, uint32_t K, int buf, KdView &kd)
 // host learns after the search: the worker awaits the codebook's publication and builds the
 // tree while this thread enqueues the rest of the level; join_tree_job waits for it (ties)
 // or cancels it (none).
-void post_job(qvq_ctx *ctx, std::function<void()> job) {
-    qvq_ctx::Worker &w = ctx->worker;
+void post_job(qvq_ctx *ctx, std::function<void()> job, qvq_ctx::Worker *wk = nullptr) {
+    qvq_ctx::Worker &w = wk ? *wk : ctx->worker;
     if (!w.th.joinable())
         w.th = std::thread([&w] {
             std::unique_lock<std::mutex> lk(w.m);
@@ -1314,6 +1316,31 @@ void pool_run(qvq_ctx *ctx, uint32_t n, const std::function<void(uint32_t)> &fn)
     while (P.busy.load(std::memory_order_acquire)) std::this_thread::yield();
 }
 
+// The certificate's known split: coordinates whose reference bits are the exact sums' without
+// computing them -- a cell's exact mean is 0 or 1 only when all its values are (SCALED values lie
+// in [0, 1], at least 1/(255 n) from 1 otherwise; Kahan sums of 0s and 1s are exact), split by 1.2
+// or 0.8, and every component of a cell of at most two rows (its Kahan sum, of one value or two,
+// is the exact sum rounded once: the same centroid bits; pcnt, the finalize's parent counts).
+// The tree's replay caches are reset for it; with prepare also built (the aggregates and every
+// node's replayed split: the last level's check does this before its tie rows arrive).
+void cert_init(const RefKDTree &tree, CertState &cs, const double *cb, const std::vector<uint32_t> &pcnt, uint32_t K,
+               uint32_t D, bool prepare) {
+    const uint32_t Kc = K / 2;
+    cs.kp.assign(cb, cb + (size_t)K * D);
+    cs.known.resize((size_t)K * D);
+    const bool counts = pcnt.size() == Kc;
+    for (uint32_t j = 0; j < K; j++) {
+        const double u = j < Kc ? 1 + 0.2 : 1 - 0.2;
+        const double *v = &cs.kp[(size_t)j * D];
+        uint8_t *k = &cs.known[(size_t)j * D];
+        const bool few = counts && pcnt[j % Kc] <= 2;
+        for (uint32_t d = 0; d < D; d++) k[d] = few || v[d] == 0 || std::fabs(v[d] - u) <= 1e-14;
+    }
+    tree.cert_clear();   // kp / known: this level's (the vectors are reused)
+    if (prepare) tree.cert_prepare(KAHAN_DELTA, cs.kp.data(), cs.known.data());
+    cs.prepared = true;
+}
+
 // The certificate over cs.nu distinct rows cs.qs (nu x D values): cs.ans[u] the reference's
 // index, or -1 for a row it leaves open.  tree: the level's tree over the exact-sum split cb (K
 // code vectors); A_prev: the previous level's assignment (nullptr at K = 2: the parent cell is the
@@ -1329,23 +1356,9 @@ qvq_status certify_rows(qvq_ctx *ctx, const RefKDTree &tree, const double *cb, c
     const uint32_t D = ctx->D, Kc = K / 2, nu = cs.nu;
     const std::vector<double> &qs = cs.qs;
     std::vector<int64_t> &ans = cs.ans;
-    // coordinates whose reference bits are the exact sums' without computing them: a cell's
-    // exact mean is 0 or 1 only when all its values are (SCALED values lie in [0, 1], at least
-    // 1/(255 n) from 1 otherwise; Kahan sums of 0s and 1s are exact), split by 1.2 or 0.8
+    if (!cs.prepared) cert_init(tree, cs, cb, pcnt, K, D, false);
     std::vector<double> &kp = cs.kp;
     std::vector<uint8_t> &known = cs.known;
-    kp.assign(cb, cb + (size_t)K * D);
-    known.resize((size_t)K * D);
-    // and every component of a cell of at most two rows (its Kahan sum, of one value or two, is
-    // the exact sum rounded once: the same centroid bits; pcnt, the finalize's parent counts)
-    const bool counts = pcnt.size() == Kc;
-    for (uint32_t j = 0; j < K; j++) {
-        const double u = j < Kc ? 1 + 0.2 : 1 - 0.2;
-        const double *v = &kp[(size_t)j * D];
-        uint8_t *k = &known[(size_t)j * D];
-        const bool few = counts && pcnt[j % Kc] <= 2;
-        for (uint32_t d = 0; d < D; d++) k[d] = few || v[d] == 0 || std::fabs(v[d] - u) <= 1e-14;
-    }
     ans.assign(nu, -1);
     cs.pend.clear();
     cs.sel.assign(Kc, 0);
@@ -1363,7 +1376,6 @@ qvq_status certify_rows(qvq_ctx *ctx, const RefKDTree &tree, const double *cb, c
         });
     };
     std::vector<uint32_t> open, left;
-    tree.cert_clear();   // kp / known: this level's (the vectors are reused)
     auto replay = [&](const std::vector<uint32_t> &rows) {
         each(rows, [&](uint32_t u, uint32_t) {
             ans[u] = tree.certified_search(&qs[(size_t)u * D], KAHAN_DELTA, kp.data(), known.data());
@@ -1592,6 +1604,10 @@ qvq_status certify_kahan_ties(qvq_ctx *ctx, uint32_t K, unsigned nt, uint64_t *t
 void verify_level(qvq_ctx *ctx, qvq_ctx::Verify &v) {
     v.status = 1;
     (void)hipSetDevice(ctx->dev);
+    // the known split and the tree's replay state were built on the prep worker while the GPU
+    // ran the level (qvq_lbg, after the level's tree)
+    while (!v.prep_done.load(std::memory_order_acquire))
+        if (v.cancel.load(std::memory_order_relaxed)) return;
     volatile uint64_t *flag = ctx->h_ready;
     while (*flag < v.seq)   // the export is released with the codebook's ready number
         if (v.cancel.load(std::memory_order_relaxed)) return;
@@ -1969,14 +1985,16 @@ QVQ_API void qvq_destroy(qvq_ctx *ctx) {
     }
     ctx->pool.cv.notify_all();
     for (auto &t : ctx->pool.th) t.join();
-    if (ctx->worker.th.joinable()) {
-        {
-            std::lock_guard<std::mutex> g(ctx->worker.m);
-            ctx->worker.stop = true;
+    while (ctx->prep.pending.load(std::memory_order_acquire)) std::this_thread::yield();
+    for (qvq_ctx::Worker *w : {&ctx->worker, &ctx->prep})
+        if (w->th.joinable()) {
+            {
+                std::lock_guard<std::mutex> g(w->m);
+                w->stop = true;
+            }
+            w->cv.notify_one();
+            w->th.join();
         }
-        ctx->worker.cv.notify_one();
-        ctx->worker.th.join();
-    }
     (void)hipSetDevice(ctx->dev);
     if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
     if (ctx->comm) ncclCommDestroy(ctx->comm);
@@ -2331,6 +2349,18 @@ QVQ_API qvq_status qvq_lbg(qvq_ctx *ctx, uint32_t bits, double eps, double *code
         ctx->d_Aext.push_back(p);
     }
     ctx->deferred.clear();
+    struct JobGuard {   // no tree build, check or prep job outlives the call (an error return included)
+        qvq_ctx *c;
+        ~JobGuard() {
+            join_tree_job(c, true);
+            // a prep job still running holds a level's tree and certificate: it finishes first
+            while (c->prep.pending.load(std::memory_order_acquire)) std::this_thread::yield();
+            for (auto &v : c->ver) {
+                v.cancel.store(true);
+                join_verify(c, v);
+            }
+        }
+    } job_guard{ctx};
     // distortion inputs, per-level counters and the codebook go to mapped pinned memory in one
     // launch (the mapped split-codebook buffer is free once the last tree is built); the copy's
     // own flag ends the wait: polling it wakes the host at once (a stream synchronize costs tens
@@ -2427,6 +2457,29 @@ QVQ_API qvq_status qvq_lbg(qvq_ctx *ctx, uint32_t bits, double eps, double *code
         }
         alev[lvl] = ctx->d_A;
         if ((st = run_level(ctx, K, slot, true, ctx->h_cb, ctx->seq, sync_kahan)) != QVQ_OK) return st;
+        if (spec) {   // the level's check: its tree now, its certificate prepared on the prep worker
+            qvq_ctx::Verify &v = ctx->ver[lvl % 3];
+            v.K = K;
+            v.level = lvl;
+            v.tree = std::move(ctx->tree);
+            v.cb = std::move(ctx->cb_local);
+            v.cnt = std::move(ctx->cnt_local);
+            ctx->cb_local.clear();
+            ctx->cnt_local.clear();
+            v.cs = CertState();
+            v.prep_done.store(false);
+            static const bool prep_on = !env_is("QVQ_CERT_PREP", "0");   // A/B
+            if (prep_on && v.tree && !v.tree->cancelled() && K >= 2 && v.cb.size() == (size_t)K * ctx->D) {
+                qvq_ctx::Verify *vp = &v;
+                const uint32_t D = ctx->D;
+                post_job(ctx, [vp, K, D] {
+                    cert_init(*vp->tree, vp->cs, vp->cb.data(), vp->cnt, K, D, true);
+                    vp->prep_done.store(true, std::memory_order_release);
+                }, &ctx->prep);
+            } else {
+                v.prep_done.store(true);
+            }
+        }
         const bool split = lvl < bits;
         {
             const uint32_t copies = ctx->sums_copies;
@@ -2467,16 +2520,9 @@ QVQ_API qvq_status qvq_lbg(qvq_ctx *ctx, uint32_t bits, double eps, double *code
                 v.done.store(false);
                 v.cancel.store(false);
                 v.status = 1;
-                v.K = K;
-                v.level = lvl;
                 v.seq = ctx->seq;
                 v.par = (int)(lvl % 3);
                 v.A_prev = lvl >= 2 ? ctx->d_A_alt : nullptr;
-                v.tree = std::move(ctx->tree);
-                v.cb = std::move(ctx->cb_local);
-                v.cnt = std::move(ctx->cnt_local);
-                ctx->cb_local.clear();
-                ctx->cnt_local.clear();
                 qvq_ctx::Verify *vp = &v;
                 post_job(ctx, [ctx, vp] {
                     verify_level(ctx, *vp);
@@ -2525,6 +2571,7 @@ QVQ_API qvq_status qvq_lbg(qvq_ctx *ctx, uint32_t bits, double eps, double *code
     if (!spec_failed) break;
     // a check failed: every check joined, the stream drained, then the quantize again with
     // synchronous Kahan levels
+    while (ctx->prep.pending.load(std::memory_order_acquire)) std::this_thread::yield();
     for (auto &v : ctx->ver) {
         v.cancel.store(true);
         join_verify(ctx, v);

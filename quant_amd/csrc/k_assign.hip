@@ -499,19 +499,27 @@ __global__ __launch_bounds__(NW * 64) void assign_small_kernel(
         (const __attribute__((address_space(3))) uint8_t *)(uintptr_t)0;
     uint64_t *cps = reinterpret_cast<uint64_t *>(lds + 256);
     const int tid = threadIdx.x;
-    const int lane = tid & 63, wave = tid >> 6;
-    // The wave owns rows [wbase, wend); lane L takes rows wbase + L + 64 t, so every load and
-    // store instruction of the wave covers 64 consecutive rows (768 contiguous bytes).
+    const int lane = tid & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);   // uniform: its rows' bases in SGPRs
+    // The wave owns rows [wbase, wbase + nw); lane L takes rows wbase + L + 64 t, so every load
+    // and store instruction of the wave covers 64 consecutive rows (768 contiguous bytes).  The
+    // wave's base pointers are uniform (SGPRs) and a lane's rows 32-bit offsets from them (N <
+    // 2^32), so every access is one SGPR base + one VGPR offset: no 64-bit row or address per row
+    // in VGPRs (with them the kernel spilled 15 VGPRs from K = 4, ~20 MB of scratch traffic each
+    // way per launch).
     const uint64_t wbase = ((uint64_t)blockIdx.x * NW + wave) * 64 * rows_per_lane;
-    const uint64_t wend = min(wbase + 64 * rows_per_lane, N);
-    // four rows of this lane (base + 64 r), two iterations ahead; branch-free (rows past N
-    // read row N - 1 and are masked later), so the loads stay in flight across iterations
-    auto load4 = [&](uint64_t r0, uint32_t (&w)[4][3]) {
+    const uint32_t nw = (uint32_t)(wbase < N ? min(64 * rows_per_lane, N - wbase) : 0);   // the wave's rows
+    const uint32_t nclamp = nw ? nw - 1 : 0;
+    const uint8_t *codes_w = codes + (wbase < N ? wbase : 0) * MF_D;
+    uint32_t *A_w = A + (wbase < N ? wbase : 0);
+    const uint32_t row0 = (uint32_t)wbase;   // flags hold global rows (N < 2^32)
+    // four rows of this lane (off + 64 r), two iterations ahead; branch-free (rows past the
+    // wave's end read its last row and are masked later), so the loads stay in flight
+    auto load4 = [&](uint32_t off, uint32_t (&w)[4][3]) {
 #pragma unroll
         for (int r = 0; r < 4; r++) {
-            uint64_t row = r0 + 64 * r;
-            row = row < N ? row : N - 1;
-            const uint32_t *p = reinterpret_cast<const uint32_t *>(codes + row * MF_D);
+            const uint32_t o = min(off + 64 * r, nclamp);
+            const uint32_t *p = reinterpret_cast<const uint32_t *>(codes_w + o * MF_D);
             w[r][0] = p[0];
             w[r][1] = p[1];
             w[r][2] = p[2];
@@ -519,7 +527,7 @@ __global__ __launch_bounds__(NW * 64) void assign_small_kernel(
     };
     // the first group's loads go out before the LDS set-up, under its latency
     uint32_t wa[4][3], wb[4][3];
-    load4(wbase + lane, wa);
+    load4(lane, wa);
     if (FUSE) {
         for (uint32_t i = tid; i < copies * S; i += (NW * 64)) cps[i] = 0;
         if (tid < 256) lo8[tid] = (uint8_t)(g_plut[tid] & 0xFF);
@@ -562,7 +570,7 @@ __global__ __launch_bounds__(NW * 64) void assign_small_kernel(
     // the exact centred byte integers -- 12 FMAs per code vector instead of the direct form's
     // 24 VALU.  Error bound (engine.cpp mfma_setup, e0 / e1): per row from sum_d |w_d|, which
     // is at most 2 sum_d |u_d - 127| + D (v_sad_u8 of the u = b ^ 0x80 bytes against 127).
-    auto process = [&](const uint32_t (&w)[4][3], uint64_t r0) {
+    auto process = [&](const uint32_t (&w)[4][3], uint32_t r0) {
         // four rows at once: each code vector's terms are loaded once (scalar) for all four,
         // and the four score chains are independent.  From SK = 32 rows go in pairs through
         // v_pk_fma_f32 (two fp32 FMAs per lane and instruction, each rounded as fmaf: the
@@ -619,15 +627,15 @@ __global__ __launch_bounds__(NW * 64) void assign_small_kernel(
         }
 #pragma unroll
         for (int r = 0; r < 4; r++) {
-            const uint64_t row = r0 + 64 * r;
+            const uint32_t row = r0 + 64 * r;   // the wave's row
             const uint32_t rk = idx[r];
-            const bool valid = row < wend;
+            const bool valid = row < nw;
             uint32_t sad = 0;
 #pragma unroll
             for (int q = 0; q < 3; q++) sad = __builtin_amdgcn_sad_u8(w[r][q] ^ 0x80808080u, 0x7F7F7F7Fu, sad);
             const float thr = __fmaf_rn((float)(2 * sad + MF_D), th.e1, th.e0);
             const bool flagged = valid && !(r2[r] - r1[r] > thr);
-            if (flagged) flags[atomicAdd(flag_cnt, 1u)] = (uint32_t)row;
+            if (flagged) flags[atomicAdd(flag_cnt, 1u)] = row0 + row;
             if (FUSE && valid) {   // provisional index, as in assign_mfma_kernel
                 if (rk != cur || acc[MF_D] == 256) {   // 16-bit fields hold 256 rows
                     flush();
@@ -654,15 +662,15 @@ __global__ __launch_bounds__(NW * 64) void assign_small_kernel(
         }
 #pragma unroll
         for (int r = 0; r < 4; r++)
-            if (r0 + 64 * r < wend) A[r0 + 64 * r] = idx[r];
+            if (r0 + 64 * r < nw) A_w[r0 + 64 * r] = idx[r];
     };
     // Two row groups per trip, each group's words loaded one group ahead into the other
     // buffer (no register copies, so the loads stay in flight under the previous group).
-    // The trip count is wave-uniform; rows past wend are masked inside process.
-    for (uint64_t ru = wbase; ru < wend; ru += 512) {
+    // The trip count is wave-uniform; rows past nw are masked inside process.
+    for (uint32_t ru = 0; ru < nw; ru += 512) {
         load4(ru + 256 + lane, wb);
         process(wa, ru + lane);
-        if (ru + 256 >= wend) break;
+        if (ru + 256 >= nw) break;
         load4(ru + 512 + lane, wa);
         process(wb, ru + 256 + lane);
     }

@@ -13,6 +13,64 @@
 
 namespace qvq {
 
+namespace {
+// The pool behind Recycled<T>: at most 8 buffers per type, the smallest that fits is taken.
+template <class T>
+struct BufPool {
+    std::mutex m;
+    std::vector<std::pair<size_t, std::unique_ptr<T[]>>> free;
+    static BufPool &get() {
+        static BufPool *p = new BufPool;   // never destroyed: trees may die at exit
+        return *p;
+    }
+};
+}  // namespace
+
+template <class T>
+void Recycled<T>::resize(size_t n) {
+    n_ = n;
+    if (n <= cap_) return;
+    release();
+    n_ = n;
+    BufPool<T> &P = BufPool<T>::get();
+    {
+        std::lock_guard<std::mutex> g(P.m);
+        size_t best = P.free.size();
+        for (size_t i = 0; i < P.free.size(); i++)
+            if (P.free[i].first >= n && (best == P.free.size() || P.free[i].first < P.free[best].first)) best = i;
+        if (best < P.free.size()) {
+            cap_ = P.free[best].first;
+            p_ = std::move(P.free[best].second);
+            P.free.erase(P.free.begin() + (std::ptrdiff_t)best);
+            return;
+        }
+    }
+    p_.reset(new T[n]);
+    cap_ = n;
+}
+
+template <class T>
+void Recycled<T>::release() {
+    if (!p_) return;
+    BufPool<T> &P = BufPool<T>::get();
+    std::lock_guard<std::mutex> g(P.m);
+    if (P.free.size() >= 8) {   // drop the smallest
+        size_t s = 0;
+        for (size_t i = 1; i < P.free.size(); i++)
+            if (P.free[i].first < P.free[s].first) s = i;
+        if (P.free[s].first >= cap_) {
+            p_.reset();
+            cap_ = n_ = 0;
+            return;
+        }
+        P.free.erase(P.free.begin() + (std::ptrdiff_t)s);
+    }
+    P.free.emplace_back(cap_, std::move(p_));
+    cap_ = n_ = 0;
+}
+template class Recycled<double>;
+template class Recycled<RefKDTree::Iv>;
+
 
 double ref_l2(const double *a, const double *b, int dim) { return ref_l2_hd(a, b, dim); }
 
@@ -661,6 +719,42 @@ void RefKDTree::certify_blame(const double *q, double delta, const double *kpts,
 }
 
 void RefKDTree::cert_clear() const { cert_gen_.fetch_add(1, std::memory_order_acq_rel); }
+
+void RefKDTree::cert_prepare(double delta, const double *kpts, const uint8_t *known) const {
+    if (dim_ > 64 || nodes_.empty()) return;
+    CertScratch &S = cert_scratch();
+    std::vector<uint32_t> *keep = S.blame;
+    S.blame = nullptr;   // the strict replay's key
+    cert_reset(delta, kpts, known);
+    // parents before children (a node's cell box is its parent's split), with the node states'
+    // protocol of certified_search (0 -> 3 -> 1 / 2)
+    std::vector<int> stack = {0};
+    while (!stack.empty()) {
+        const int node = stack.back();
+        stack.pop_back();
+        const Node &n = nodes_[node];
+        if (n.leaf) continue;
+        int8_t st = cstate_[node].load(std::memory_order_acquire);
+        if (st == 0) {
+            int8_t z = 0;
+            if (cstate_[node].compare_exchange_strong(z, 3, std::memory_order_acq_rel)) {
+                st = cert_split(node) ? 1 : 2;
+                cstate_[node].store(st, std::memory_order_release);
+            } else {
+                st = z;
+            }
+        }
+        while (st == 3) {
+            std::this_thread::yield();
+            st = cstate_[node].load(std::memory_order_acquire);
+        }
+        if (st == 1) {
+            stack.push_back(n.child1);
+            stack.push_back(n.child2);
+        }
+    }
+    S.blame = keep;
+}
 
 void RefKDTree::cert_update(const uint32_t *pts, size_t n) const {
     std::lock_guard<std::mutex> g(agg_mu_);

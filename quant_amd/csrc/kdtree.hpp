@@ -24,6 +24,30 @@ double ref_l2(const double *a, const double *b, int dim);
 
 struct Box { double low, high; };
 
+// A per-tree buffer of a trivial type, uninitialised, whose storage returns to a small process
+// pool when the tree dies: a level's tree lives one level, and a fresh multi-MB buffer page-
+// faults on its first touch and is unmapped again on free (at K = 4096, D = 48 the certificate's
+// aggregates and cell boxes cost more in faults, zero-fill and unmap than in the work on them).
+template <class T>
+class Recycled {
+public:
+    Recycled() = default;
+    Recycled(const Recycled &) = delete;
+    Recycled &operator=(const Recycled &) = delete;
+    ~Recycled() { release(); }
+    void resize(size_t n);   // contents undefined
+    size_t size() const { return n_; }
+    T *data() { return p_.get(); }
+    const T *data() const { return p_.get(); }
+    T &operator[](size_t i) { return p_[i]; }
+    const T &operator[](size_t i) const { return p_[i]; }
+
+private:
+    void release();
+    std::unique_ptr<T[]> p_;
+    size_t cap_ = 0, n_ = 0;
+};
+
 class RefKDTree {
 public:
     // pts: K x dim, row-major, borrowed for the lifetime of the tree.  cancel (optional): the
@@ -65,6 +89,10 @@ public:
                        std::vector<uint32_t> &blame) const;
     // Forget the replays' caches, on every thread (kpts or known changed in place).
     void cert_clear() const;
+    // The replays' shared state for (delta, kpts, known) built ahead of any query: the per-node
+    // aggregates and every node's replayed split, top down (a later certified_search with the
+    // same key then only walks).  The caller keeps kpts / known unchanged until its replays.
+    void cert_prepare(double delta, const double *kpts, const uint8_t *known) const;
     // The same after kpts / known changed on the rows pts[0..n) only: the calling thread's
     // cache keeps its per-node values but those of these points' leaves and their ancestors.
     void cert_update(const uint32_t *pts, size_t n) const;
@@ -127,7 +155,7 @@ private:
     // divhigh set) or 2 (not shown)
     mutable std::unique_ptr<std::atomic<int8_t>[]> cstate_;
     mutable std::vector<CertNode> cnode_;   // dl, dh
-    mutable std::vector<Iv> cbox_;          // [node][dim][lo, hi]: the node's cell box
+    mutable Recycled<Iv> cbox_;             // [node][dim][lo, hi]: the node's cell box
     mutable std::atomic<uint64_t> ckey_gen_{~0ull};
     mutable double ckey_delta_ = -1;
     mutable const double *ckey_k_ = nullptr;
@@ -139,7 +167,7 @@ private:
     mutable std::atomic<uint64_t> agg_gen_{~0ull};
     mutable const double *agg_k_ = nullptr;
     mutable const uint8_t *agg_known_ = nullptr;
-    mutable std::vector<double> agg_;      // [node][min unknown | max unknown | min known | max known][dim]
+    mutable Recycled<double> agg_;         // [node][min unknown | max unknown | min known | max known][dim]
     mutable std::vector<int> parent_;
     mutable std::vector<int> leaf_of_;     // point -> its leaf
     void cert_ensure_agg(uint64_t gen, const double *kpts, const uint8_t *known) const;
