@@ -312,28 +312,21 @@ __device__ inline void stage_bytes(const uint8_t *__restrict__ src, uint32_t n, 
 // ---- 3. meta ---------------------------------------------------------------------------------
 constexpr int WPB = 4;   // waves per workgroup (meta, build)
 
-__global__ __launch_bounds__(64 * WPB) void ks_meta_kernel(Geo g, const ByteTab *__restrict__ gtab) {
-    __shared__ ByteTab tab;
-    __shared__ __attribute__((aligned(16))) uint8_t bytes[WPB][BLK_STEPS];
-    stage_tab(gtab, &tab);
-    __syncthreads();
-    const uint32_t w = threadIdx.x >> 6, lane = lane_id();
-    const uint32_t TB = g.blkoff[g.K];
-    const uint64_t fb = (uint64_t)blockIdx.x * WPB + w;
-    if (fb >= (uint64_t)TB * g.D) return;
+__device__ inline void meta_block(const Geo &g, const ByteTab &tab, uint8_t *bytes_w, uint32_t TB, uint64_t fb,
+                                  uint32_t lane) {
     const uint32_t d = (uint32_t)(fb / TB), bb = (uint32_t)(fb - (uint64_t)d * TB);
     const uint32_t k = find_cell(g.blkoff, g.K, bb), b = bb - g.blkoff[k];
     const uint32_t n = g.koff[k + 1] - g.koff[k];
     const uint32_t s0 = b * SPB, first = s0 * L, nb = min(BLK_STEPS, n - first);
     KCHK(TB <= g.blk_cap && g.segoff[g.K] <= g.seg_cap && first < n && k < g.K);
     KCHK((uint64_t)d * g.PL + g.koff[k] + first + nb + 8 <= g.plane_bytes);
-    stage_bytes(g.planes + (uint64_t)d * g.PL + g.koff[k] + first, nb, bytes[w]);
+    stage_bytes(g.planes + (uint64_t)d * g.PL + g.koff[k] + first, nb, bytes_w);
     wave_sync();
     const uint32_t s = s0 + lane, nseg = (n + L - 1) / L;
     u128 tot = 0;
     if (s < nseg) {
         const uint32_t len = min(L, n - s * L);
-        const SegMeta m = kahan::seg_meta(tab, bytes[w] + lane * L, len);
+        const SegMeta m = kahan::seg_meta(tab, bytes_w + lane * L, len);
         g.meta[(uint64_t)d * g.segoff[g.K] + g.segoff[k] + s] = m;
         tot = kahan::meta_sum(m);
     }
@@ -345,6 +338,22 @@ __global__ __launch_bounds__(64 * WPB) void ks_meta_kernel(Geo g, const ByteTab 
         lo = t;
     }
     if (lane == 0) g.bsum[(uint64_t)d * TB + bb] = ((u128)hi << 64) | lo;
+}
+
+// Grid-stride over the (component, block) pairs: the grid is sized by the capacity (the host
+// does not know the block count), and a workgroup without a pair leaves before staging the
+// 6.5 KB byte table (28k empty workgroups staged it at C4: ~180 MB of L2 reads per launch).
+__global__ __launch_bounds__(64 * WPB) void ks_meta_kernel(Geo g, const ByteTab *__restrict__ gtab) {
+    __shared__ ByteTab tab;
+    __shared__ __attribute__((aligned(16))) uint8_t bytes[WPB][BLK_STEPS];
+    const uint32_t TB = g.blkoff[g.K];
+    const uint64_t total = (uint64_t)TB * g.D;
+    if ((uint64_t)blockIdx.x * WPB >= total) return;
+    stage_tab(gtab, &tab);
+    __syncthreads();
+    const uint32_t w = threadIdx.x >> 6, lane = lane_id();
+    for (uint64_t fb = (uint64_t)blockIdx.x * WPB + w; fb < total; fb += (uint64_t)gridDim.x * WPB)
+        meta_block(g, tab, bytes[w], TB, fb, lane);
 }
 
 // ---- 3b. chained: this rank's chain totals and row counts into its slice of gather ----------
@@ -474,54 +483,60 @@ __device__ inline u128 build_block_fns(const Geo &g, const ByteTab &tab, const u
 }
 
 // ---- 5. build: block functions ------------------------------------------------------------------
-__global__ __launch_bounds__(64 * WPB) void ks_build_kernel(Geo g, const ByteTab *__restrict__ gtab) {
-    __shared__ ByteTab tab;
-    __shared__ __attribute__((aligned(16))) uint8_t bytes[WPB][BLK_STEPS];
-    __shared__ Fn fns[WPB][SPB];
-    __shared__ uint8_t ok[WPB][SPB];
-    stage_tab(gtab, &tab);
-    __syncthreads();
-    const uint32_t w = threadIdx.x >> 6, lane = lane_id();
-    const uint32_t TB = g.blkoff[g.K];
-    const uint64_t fb = (uint64_t)blockIdx.x * WPB + w;
-    if (fb >= (uint64_t)TB * g.D) return;
+__device__ inline void build_block(const Geo &g, const ByteTab &tab, uint8_t *bytes_w, Fn *fns_w, uint8_t *ok_w,
+                                   uint32_t TB, uint64_t fb, uint32_t lane) {
     const uint32_t d = (uint32_t)(fb / TB), bb = (uint32_t)(fb - (uint64_t)d * TB);
     const uint32_t k = find_cell(g.blkoff, g.K, bb), b = bb - g.blkoff[k];
     const uint32_t n = g.koff[k + 1] - g.koff[k];
     const uint32_t first = b * BLK_STEPS;
-    stage_bytes(g.planes + (uint64_t)d * g.PL + g.koff[k] + first, min(BLK_STEPS, n - first), bytes[w]);
+    stage_bytes(g.planes + (uint64_t)d * g.PL + g.koff[k] + first, min(BLK_STEPS, n - first), bytes_w);
     wave_sync();
-    build_block_fns(g, tab, bytes[w], k, d, b, 0, fns[w]);
+    build_block_fns(g, tab, bytes_w, k, d, b, 0, fns_w);
     const uint32_t nseg = (n + L - 1) / L, cnt = min(SPB, nseg - b * SPB);
     if (lane < cnt) {   // for the evaluation's re-walks of blocks that do not answer
         kahan::SegFn sf;
-        kahan::pack_seg(fns[w][lane], sf);
+        kahan::pack_seg(fns_w[lane], sf);
         g.sfn[(uint64_t)d * g.segoff[g.K] + g.segoff[k] + b * SPB + lane] = sf;
     }
-    ok[w][lane] = kahan::fkind(fns[w][lane]) != kahan::FK_RAW;
+    ok_w[lane] = kahan::fkind(fns_w[lane]) != kahan::FK_RAW;
     wave_sync();
     for (uint32_t st = 1; st < SPB; st <<= 1) {   // tree: fns[i] <- fns[i] then fns[i + st]
         if ((lane & (2 * st - 1)) == 0 && lane + st < cnt) {
             Fn h;
-            const bool c = ok[w][lane] && ok[w][lane + st] && kahan::compose(fns[w][lane], fns[w][lane + st], h);
-            ok[w][lane] = c;
-            if (c) fns[w][lane] = h;
+            const bool c = ok_w[lane] && ok_w[lane + st] && kahan::compose(fns_w[lane], fns_w[lane + st], h);
+            ok_w[lane] = c;
+            if (c) fns_w[lane] = h;
         }
         wave_sync();
         if (st == 4 && (lane & 7) == 0 && lane < cnt) {   // the 8-segment sub-blocks, for the evaluation
-            Fn r = fns[w][lane];
-            if (!ok[w][lane]) kahan::set_raw(r);
+            Fn r = fns_w[lane];
+            if (!ok_w[lane]) kahan::set_raw(r);
             g.bfn8[((uint64_t)d * TB + bb) * 8 + lane / 8] = r;
         }
     }
     if (lane == 0) {
-        Fn r = fns[w][0];
-        if (!ok[w][0]) {
+        Fn r = fns_w[0];
+        if (!ok_w[0]) {
             kahan::set_raw(r);
             if (g.stats) atomicAdd(&g.stats[0], 1u);
         }
         g.bfn[(uint64_t)d * TB + bb] = r;
     }
+}
+
+__global__ __launch_bounds__(64 * WPB) void ks_build_kernel(Geo g, const ByteTab *__restrict__ gtab) {
+    __shared__ ByteTab tab;
+    __shared__ __attribute__((aligned(16))) uint8_t bytes[WPB][BLK_STEPS];
+    __shared__ Fn fns[WPB][SPB];
+    __shared__ uint8_t ok[WPB][SPB];
+    const uint32_t TB = g.blkoff[g.K];
+    const uint64_t total = (uint64_t)TB * g.D;
+    if ((uint64_t)blockIdx.x * WPB >= total) return;   // (ks_meta_kernel's note)
+    stage_tab(gtab, &tab);
+    __syncthreads();
+    const uint32_t w = threadIdx.x >> 6, lane = lane_id();
+    for (uint64_t fb = (uint64_t)blockIdx.x * WPB + w; fb < total; fb += (uint64_t)gridDim.x * WPB)
+        build_block(g, tab, bytes[w], fns[w], ok[w], TB, fb, lane);
 }
 
 // ---- 6. eval ----------------------------------------------------------------------------------
@@ -803,7 +818,10 @@ Geo make_geo(const KahanWork &w, uint64_t N, uint32_t K, uint32_t D) {
 }
 
 // grids sized by the capacities; waves past the actual block count return at once
-uint32_t blk_grid(const KahanWork &w, uint32_t D) { return (uint32_t)(((uint64_t)w.blk_cap * D + WPB - 1) / WPB); }
+// (grid-stride kernels: at most 8 workgroups per CU)
+uint32_t blk_grid(const KahanWork &w, uint32_t D) {
+    return (uint32_t)std::min<uint64_t>(((uint64_t)w.blk_cap * D + WPB - 1) / WPB, 2048);
+}
 uint32_t chain_grid(uint32_t K, uint32_t D) { return (uint32_t)(((uint64_t)K * D * 64 + 255) / 256); }
 
 }  // namespace
