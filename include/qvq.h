@@ -200,9 +200,9 @@ QVQ_API qvq_status qvq_comm_info(const qvq_ctx *ctx, int *nranks, int *rank, int
  * the call returned, and every later call but qvq_destroy returns QVQ_ESTATE. */
 QVQ_API qvq_status qvq_set_timeout(qvq_ctx *ctx, double seconds);
 
-/* Which levels get HIP events around their search kernel (each event record costs a few
- * microseconds of GPU idle): -1 every level (default), -2 none, n >= 0 level n+1 only.
- * Unmeasured levels report 0 in qvq_get_timings. */
+/* Which levels get HIP events around their search kernel (each event record idles the GPU
+ * ~6 us: every level costs ~10 % of a C3 quantize): -1 every level, -2 none (default), n >= 0
+ * level n+1 only.  Unmeasured levels report 0 in qvq_get_timings. */
 QVQ_API qvq_status qvq_set_timing(qvq_ctx *ctx, int level);
 QVQ_API qvq_status qvq_get_timings(const qvq_ctx *ctx, qvq_timings *out);
 

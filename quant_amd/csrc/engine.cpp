@@ -253,7 +253,7 @@ struct qvq_ctx {
     bool sums1_dirty = false;  // copy 1 of d_sums may hold moves (a quantize that stopped early)
     uint64_t sums_bytes = 0;
     uint32_t nsub = 0;     // ... of which the last nsub are subtracted
-    int timing_level = -1;   // qvq_set_timing: -1 all levels, -2 none, else that level only
+    int timing_level = -2;   // qvq_set_timing: -1 all levels, -2 none (default), else that level only
     bool upd[32] = {};
     hipEvent_t ev_end = nullptr;
     hipEvent_t ev_sync = nullptr;   // wait_stream
@@ -2468,8 +2468,12 @@ QVQ_API qvq_status qvq_lbg(qvq_ctx *ctx, uint32_t bits, double eps, double *code
             ctx->cnt_local.clear();
             v.cs = CertState();
             v.prep_done.store(false);
+            // (not the last level: its check follows at once, and replays that build the node
+            // splits they visit, spread over the helper threads, beat one thread building all;
+            // C4 8.0 ms with every level prepared on the worker, 7.3 with none: profiles/r05h)
             static const bool prep_on = !env_is("QVQ_CERT_PREP", "0");   // A/B
-            if (prep_on && v.tree && !v.tree->cancelled() && K >= 2 && v.cb.size() == (size_t)K * ctx->D) {
+            if (prep_on && lvl < bits && v.tree && !v.tree->cancelled() && K >= 2 &&
+                v.cb.size() == (size_t)K * ctx->D) {
                 qvq_ctx::Verify *vp = &v;
                 const uint32_t D = ctx->D;
                 post_job(ctx, [vp, K, D] {

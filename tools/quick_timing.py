@@ -10,6 +10,7 @@ cases = [(512, 2, 10), (4096, 2, 10), (4096, 4, 12)]
 if len(sys.argv) > 1:
     cases = [tuple(int(v) for v in c.split(',')) for c in sys.argv[1:]]
 eng = quant_amd.Engine(0)
+eng.set_timing(-1)   # per-level events (off by default: each record idles the GPU ~6 us)
 for (S, bw, bits) in cases:
     eng.set_synthetic(S, 0x5EED, 1, bw, bw)
     for rep in range(3):
