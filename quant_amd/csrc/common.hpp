@@ -416,9 +416,13 @@ struct KahanWork {
 // sel (n_sel entries, device; nullptr: every cell): the selected cells only, compacted: sel[a] =
 // slot + 1 for a selected cell a, 0 otherwise; K is then the number of slots, and C / split_out
 // rows are slots (split_out: slot | K + slot).  The sort skips the other rows' bytes.
+// max_rows: a bound on the rows of any cell summed (0: unknown); at most kahan_direct_max()
+// rows, each chain runs step by step on one lane (ks_direct_kernel) instead of through the
+// segment functions, whose set-up costs more than short chains.
 hipError_t launch_kahan_centroids(hipStream_t s, const KahanWork &w, const uint8_t *codes, uint32_t Dp, uint32_t D,
                                   uint64_t N, const uint32_t *A, uint32_t K, double *C, double *split_out,
-                                  const uint32_t *sel = nullptr, uint32_t n_sel = 0);
+                                  const uint32_t *sel = nullptr, uint32_t n_sel = 0, uint64_t max_rows = 0);
+uint64_t kahan_direct_max();   // QVQ_KAHAN_DIRECT_MAX (default 4096; 0: never)
 // The same centroids when a cell's rows are split over ranks (each rank holds a contiguous
 // range of the global rows, ranks in row order; engine.cpp kahan_chained).  gather: u64
 // [nranks][K * D][2] chain totals | [nranks][K] row counts, zeroed by the caller; each rank

@@ -172,7 +172,10 @@ struct qvq_ctx {
     uint64_t *h_decode_stat = nullptr;    // pinned host copy
     // mapped pinned host memory (coherent): the split codebook finalize writes for the
     // host's tree build, its ready sequence number, and two flattened kd-tree images
+    // the split codebooks the finalizes publish for the host, two halves of cb_half doubles
+    // (host_cb_of): level L's codebook in half L & 1
     double *h_cb = nullptr, *dh_cb = nullptr;
+    uint64_t cb_half = 0;
     uint64_t *h_ready = nullptr, *dh_ready = nullptr;
     uint64_t seq = 0;
     uint8_t *h_tree[2] = {nullptr, nullptr}, *dh_tree[2] = {nullptr, nullptr};
@@ -564,7 +567,9 @@ qvq_status ensure_levels(qvq_ctx *ctx, uint32_t Kmax) {
     HIPCHK(hipMemset(ctx->d_sums, 0, 2 * (2 * KD + Kmax) * 8));
     ctx->sums_bytes = 2 * (2 * KD + Kmax) * 8;
     const unsigned mflags = hipHostMallocMapped | hipHostMallocCoherent;
-    HIPCHK(hipHostMalloc(&ctx->h_cb, KD * 8 + (uint64_t)Kmax * 4, mflags));   // split rows | parent counts
+    // two halves, each split rows | parent counts (host_cb_of)
+    ctx->cb_half = (KD + (uint64_t)Kmax / 2 + 1 + 7) / 8 * 8;
+    HIPCHK(hipHostMalloc(&ctx->h_cb, 2 * ctx->cb_half * 8, mflags));
     HIPCHK(hipHostGetDevicePointer((void **)&ctx->dh_cb, ctx->h_cb, 0));
     ctx->tree_cap = tree_bytes(Kmax, ctx->D);
     for (int b = 0; b < 2; b++) {
@@ -820,6 +825,14 @@ bool join_tree_job(qvq_ctx *ctx, bool cancel);
 // Build the reference kd-tree over the host copy hC of the K code vectors being searched
 // into tree image buffer buf (pinned host memory, DMA-copied to d_tree for kd_resolve_kernel).  An empty
 // view means host resolution (tree too deep/large for the kernel's LDS, or QVQ_KDTREE=host).
+// Level L's split codebook as the finalize of level L - 1 publishes it (host / device view).
+// Double-buffered by level parity: the synchronous Kahan levels build a level's tree on the
+// worker from this copy while the level's own finalize already publishes the next level's
+// codebook (one buffer: a worker late by more than the level's search read a mix of the two,
+// the r05i-r05m intermittent mismatches on palette images).
+double *host_cb_of(const qvq_ctx *ctx, uint32_t level) { return ctx->h_cb + (uint64_t)(level & 1) * ctx->cb_half; }
+double *dev_cb_of(const qvq_ctx *ctx, uint32_t level) { return ctx->dh_cb + (uint64_t)(level & 1) * ctx->cb_half; }
+
 // The host part: the tree (ctx->tree over ctx->cb_local) and its flattened image in h_tree[buf];
 // v.bytes = 0 when there is no device image (too large, or too deep for the kernel's LDS).
 // No HIP call: the tree worker runs it.
@@ -829,7 +842,7 @@ void build_tree_host(qvq_ctx *ctx, const double *hC, uint32_t K, int buf, KdView
     // the build reads the codebook many times; mapped memory the GPU just wrote is read
     // once, sequentially, into ordinary memory first
     ctx->cb_local.assign(hC, hC + (size_t)K * ctx->D);
-    if (hC == ctx->h_cb && K >= 2) {   // the finalize's split: the parent counts follow it
+    if ((hC == host_cb_of(ctx, 0) || hC == host_cb_of(ctx, 1)) && K >= 2) {   // a finalize's split: the parent counts follow it
         const uint32_t *cnt = reinterpret_cast<const uint32_t *>(hC + (size_t)K * ctx->D);
         ctx->cnt_local.assign(cnt, cnt + K / 2);
     } else {
@@ -1440,12 +1453,16 @@ qvq_status certify_rows(qvq_ctx *ctx, const RefKDTree &tree, const double *cb, c
             if (pick[c]) cell_of.push_back(c);
         }
         if (A_prev) {
+            // the longest chain (the finalize's parent counts): short ones run step by step
+            uint64_t max_rows = pcnt.size() == Kc ? 1 : 0;
+            for (uint32_t c : cell_of) max_rows = max_rows ? std::max<uint64_t>(max_rows, pcnt[c]) : 0;
             HIPCHK(hipMemcpyAsync(ctx->d_kc_sel, ctx->h_kc_sel, (size_t)Kc * 4, hipMemcpyHostToDevice, stream));
             HIPCHK(launch_kahan_centroids(stream, ctx->kw, ctx->d_codes, ctx->Dp, D, ctx->N, A_prev,
-                                          (uint32_t)cell_of.size(), ctx->d_kc_cent, ctx->dh_kc_out, ctx->d_kc_sel, Kc));
+                                          (uint32_t)cell_of.size(), ctx->d_kc_cent, ctx->dh_kc_out, ctx->d_kc_sel, Kc,
+                                          max_rows));
         } else {   // K = 2: the one parent cell is the mean of every row
             HIPCHK(launch_kahan_centroids(stream, ctx->kw, ctx->d_codes, ctx->Dp, D, ctx->N, nullptr, 1,
-                                          ctx->d_kc_cent, ctx->dh_kc_out));
+                                          ctx->d_kc_cent, ctx->dh_kc_out, nullptr, 0, ctx->N));
         }
         cert_trace.mark("launched");
         return QVQ_OK;
@@ -1926,6 +1943,7 @@ QVQ_API qvq_status qvq_create(int hip_device, qvq_ctx **out) {
     if (hip_device < 0 || hip_device >= n) return fail(nullptr, QVQ_EINVAL, "bad device index");
     qvq_ctx *ctx = new qvq_ctx();
     ctx->dev = hip_device;
+    if (const char *t = std::getenv("QVQ_TIMING")) ctx->timing_level = std::atoi(t);   // A/B: the default per-level events
     std::memset(&ctx->tm, 0, sizeof(ctx->tm));
     auto bail = [&](hipError_t e, const char *what) {
         g_static_err = std::string(what) + ": " + hipGetErrorString(e);
@@ -2410,7 +2428,8 @@ QVQ_API qvq_status qvq_lbg(qvq_ctx *ctx, uint32_t bits, double eps, double *code
         return launch_finalize_prep(ctx->stream, K == 1 ? ctx->d_mean : ctx->d_sums, K, ctx->D, ctx->Dp, T.R, T.bias,
                                     T.scale,
                                     ctx->d_C64_cent, split, split_out, pad32(2 * K), T.mu, T.sx, ctx->mf_t,
-                                    ctx->d_C32, ctx->d_rows, ctx->d_E32, split ? ctx->dh_cb : nullptr, d_dist + 8,
+                                    ctx->d_C32, ctx->d_rows, ctx->d_E32,
+                                    split ? dev_cb_of(ctx, (uint32_t)__builtin_ctz(K) + 1) : nullptr, d_dist + 8,
                                     dist_done,
                                     split ? nullptr : d_dist + 2, (split || tx.out) ? ctx->dh_ready : nullptr,
                                     ctx->seq, K == 1 || (clear1 && copies > 1), K == 1 ? MEAN_COPIES : copies,
@@ -2456,7 +2475,7 @@ QVQ_API qvq_status qvq_lbg(qvq_ctx *ctx, uint32_t bits, double eps, double *code
             std::swap(ctx->d_A, ctx->d_A_alt);   // d_A_alt: the previous level's assignment
         }
         alev[lvl] = ctx->d_A;
-        if ((st = run_level(ctx, K, slot, true, ctx->h_cb, ctx->seq, sync_kahan)) != QVQ_OK) return st;
+        if ((st = run_level(ctx, K, slot, true, host_cb_of(ctx, lvl), ctx->seq, sync_kahan)) != QVQ_OK) return st;
         if (spec) {   // the level's check: its tree now, its certificate prepared on the prep worker
             qvq_ctx::Verify &v = ctx->ver[lvl % 3];
             v.K = K;
@@ -2726,8 +2745,14 @@ QVQ_API qvq_status qvq_update_kahan(qvq_ctx *ctx, const uint32_t *assign, uint32
         if ((st = kahan_chained(ctx, K == 1 ? nullptr : ctx->d_A, K, nullptr, K, false)) != QVQ_OK)
             return st;
     } else {
+        uint64_t max_rows = ctx->N;   // the longest chain (short ones run step by step)
+        if (K > 1) {
+            std::vector<uint64_t> n(K, 0);
+            for (uint64_t i = 0; i < ctx->N; i++) n[assign[i]]++;   // (checked < K above)
+            max_rows = std::max<uint64_t>(1, *std::max_element(n.begin(), n.end()));
+        }
         HIPCHK(launch_kahan_centroids(ctx->stream, ctx->kw, ctx->d_codes, ctx->Dp, ctx->D, ctx->N,
-                                      K == 1 ? nullptr : ctx->d_A, K, ctx->d_kc_cent, nullptr));
+                                      K == 1 ? nullptr : ctx->d_A, K, ctx->d_kc_cent, nullptr, nullptr, 0, max_rows));
     }
     const uint64_t cB = (uint64_t)K * ctx->D * 8;
     if ((st = ensure_pinned(ctx, ctx->h_stage, ctx->stage_bytes, cB)) != QVQ_OK) return st;

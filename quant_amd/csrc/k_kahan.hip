@@ -743,6 +743,41 @@ __global__ __launch_bounds__(256) void ks_finish_kernel(uint32_t K, uint32_t D, 
 
 __global__ void ks_set_u32_kernel(uint32_t *p, uint32_t v) { *p = v; }
 
+// Short chains: the reference's chain (src/Quantizer.cpp:59-70) step by step, one lane per
+// (cell, component), bytes from the sorted planes, values from the byte table; then fl(1/n) and
+// the split as ks_eval_kernel.  For cells of a few thousand rows this beats the segment
+// functions' meta / scan / build / eval (~200 us for C4's 20 checked cells, profiles/r05h: the
+// build of 64 functions per wave is the pole) at ~25 ns per step.
+__global__ __launch_bounds__(256) void ks_direct_kernel(const uint8_t *__restrict__ planes, uint64_t PL,
+                                                       const uint32_t *__restrict__ koff, uint32_t K, uint32_t D,
+                                                       const ByteTab *__restrict__ gtab, double *__restrict__ C,
+                                                       double *__restrict__ split_out) {
+    __shared__ double xv[256];
+    xv[threadIdx.x] = ldexp((double)gtab->X[threadIdx.x], -60);   // the byte's value, exactly
+    __syncthreads();
+    const uint64_t t = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (t >= (uint64_t)K * D) return;
+    const uint32_t k = (uint32_t)(t / D), d = (uint32_t)(t - (uint64_t)k * D);
+    const uint32_t n = koff[k + 1] - koff[k];
+    const uint8_t *src = planes + (uint64_t)d * PL + koff[k];
+    double sum = 0, c = 0;
+    uint32_t i = 0;
+    for (; i + 16 <= n; i += 16) {   // the loads of 16 steps issued together
+        uint8_t b[16];
+#pragma unroll
+        for (int j = 0; j < 16; j++) b[j] = src[i + j];
+#pragma unroll
+        for (int j = 0; j < 16; j++) kahan::fstep(sum, c, xv[b[j]]);
+    }
+    for (; i < n; i++) kahan::fstep(sum, c, xv[src[i]]);
+    const double result = n ? __dmul_rn(sum, 1.0 / (double)n) : 0.0;
+    C[t] = result;
+    if (split_out) {   // src/Quantizer.cpp:134-138
+        split_out[t] = __dmul_rn(result, (double)(1 + 0.2));
+        split_out[(uint64_t)K * D + t] = __dmul_rn(result, (double)(1 - 0.2));
+    }
+}
+
 }  // namespace
 
 // ---- host side -------------------------------------------------------------------------------
@@ -826,13 +861,24 @@ uint32_t chain_grid(uint32_t K, uint32_t D) { return (uint32_t)(((uint64_t)K * D
 
 }  // namespace
 
+uint64_t kahan_direct_max() {
+    static const uint64_t v = std::getenv("QVQ_KAHAN_DIRECT_MAX") ? std::strtoull(std::getenv("QVQ_KAHAN_DIRECT_MAX"), nullptr, 10)
+                                                                   : 4096;
+    return v;
+}
+
 hipError_t launch_kahan_centroids(hipStream_t s, const KahanWork &w, const uint8_t *codes, uint32_t Dp, uint32_t D,
                                   uint64_t N, const uint32_t *A, uint32_t K, double *C, double *split_out,
-                                  const uint32_t *sel, uint32_t n_sel) {
+                                  const uint32_t *sel, uint32_t n_sel, uint64_t max_rows) {
     hipError_t e = kahan_sort(s, w, codes, Dp, D, N, A, K, sel, n_sel);
     if (e != hipSuccess) return e;
     const Geo g = make_geo(w, N, K, D);
     const ByteTab *tab = reinterpret_cast<const ByteTab *>(w.tab);
+    if (max_rows && max_rows <= kahan_direct_max()) {
+        hipLaunchKernelGGL(ks_direct_kernel, dim3((uint32_t)(((uint64_t)K * D + 255) / 256)), dim3(256), 0, s,
+                           w.planes, KahanWork::plane_len(N), w.koff, K, D, tab, C, split_out);
+        return hipGetLastError();
+    }
     hipLaunchKernelGGL(ks_meta_kernel, dim3(blk_grid(w, D)), dim3(64 * WPB), 0, s, g, tab);
     hipLaunchKernelGGL(ks_bscan_kernel, dim3(chain_grid(K, D)), dim3(256), 0, s, g, (const uint64_t *)nullptr, 0u);
     hipLaunchKernelGGL(ks_build_kernel, dim3(blk_grid(w, D)), dim3(64 * WPB), 0, s, g, tab);

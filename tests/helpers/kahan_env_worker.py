@@ -1,5 +1,6 @@
 """Runs corpus cases through one engine in a process whose environment selects a Kahan schedule
-(tests/test_gpu_kahan.py: QVQ_SPECULATE=0, QVQ_KAHAN_FAIL_LEVEL; the engine reads these once),
+(tests/test_gpu_kahan.py: QVQ_SPECULATE=0, QVQ_KAHAN_FAIL_LEVEL, QVQ_KAHAN_DIRECT_MAX; the engine
+ reads these once),
 printing one JSON line per case: indices and codebook against the oracle's Kahan rule (the
 reference's, src/Quantizer.cpp:59-87), a second quantize on the same context, kahan_redo.
 

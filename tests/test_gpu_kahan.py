@@ -210,3 +210,14 @@ def test_failed_check_redoes_the_quantize():
     for r in res:
         assert r["A_ok"] and r["C_ok"] and r["again_ok"], r
         assert r["redo"] == 1
+
+
+def test_certificate_cells_through_segment_functions():
+    """The certificate's cell sums with the step-by-step chains off (QVQ_KAHAN_DIRECT_MAX=0:
+    every chain through the segment functions, as for long cells), on corpus cases whose
+    checks sum cells: the same indices and codebooks (the default run takes ks_direct_kernel
+    for their short cells)."""
+    res = _env_worker({"QVQ_KAHAN_DIRECT_MAX": "0"}, CORPUS["noise_seeds"][:2] + CORPUS["found"][:6])
+    assert len(res) == 8
+    for r in res:
+        assert r["A_ok"] and r["C_ok"] and r["again_ok"], r
