@@ -2487,10 +2487,12 @@ QVQ_API qvq_status qvq_lbg(qvq_ctx *ctx, uint32_t bits, double eps, double *code
             ctx->cnt_local.clear();
             v.cs = CertState();
             v.prep_done.store(false);
-            // (not the last level: its check follows at once, and replays that build the node
-            // splits they visit, spread over the helper threads, beat one thread building all;
-            // C4 8.0 ms with every level prepared on the worker, 7.3 with none: profiles/r05h)
-            static const bool prep_on = !env_is("QVQ_CERT_PREP", "0");   // A/B
+            // Off by default (QVQ_CERT_PREP=1: on, A/B): replays that build the node splits they
+            // visit beat one thread building them all, and the prep competes for the host's cores
+            // with the tree builds on the critical path.  C4 with every level prepared 8.0 ms,
+            // none 7.3 (profiles/r05h); with all but the last 8.08, none 7.41; C3 1.2536 / 1.2293
+            // (profiles/r05i).  Never the last level: its check follows at once.
+            static const bool prep_on = env_is("QVQ_CERT_PREP", "1");
             if (prep_on && lvl < bits && v.tree && !v.tree->cancelled() && K >= 2 &&
                 v.cb.size() == (size_t)K * ctx->D) {
                 qvq_ctx::Verify *vp = &v;
