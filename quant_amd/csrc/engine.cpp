@@ -1625,6 +1625,17 @@ void verify_level(qvq_ctx *ctx, qvq_ctx::Verify &v) {
     // ran the level (qvq_lbg, after the level's tree)
     while (!v.prep_done.load(std::memory_order_acquire))
         if (v.cancel.load(std::memory_order_relaxed)) return;
+    // the check usually starts while the GPU still runs its level (the last level's check is
+    // then all that is left of the call): the known split and the tree's aggregates before the
+    // export arrives, and for short searches (D = 12: a few hundred nodes) every node's split
+    // replay too (C3: the last level's 2 tie rows took ~95 us after the export, r05i)
+    static const bool early = !env_is("QVQ_CERT_EARLY", "0");   // A/B
+    if (early && !v.cs.prepared && v.tree && !v.tree->cancelled() && v.K >= 2 &&
+        v.cb.size() == (size_t)v.K * ctx->D) {
+        const bool full = (uint64_t)v.K * ctx->D < 65536;
+        cert_init(*v.tree, v.cs, v.cb.data(), v.cnt, v.K, ctx->D, full);
+        if (!full) v.tree->cert_warm(KAHAN_DELTA, v.cs.kp.data(), v.cs.known.data());
+    }
     volatile uint64_t *flag = ctx->h_ready;
     while (*flag < v.seq)   // the export is released with the codebook's ready number
         if (v.cancel.load(std::memory_order_relaxed)) return;

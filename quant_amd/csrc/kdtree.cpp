@@ -720,6 +720,15 @@ void RefKDTree::certify_blame(const double *q, double delta, const double *kpts,
 
 void RefKDTree::cert_clear() const { cert_gen_.fetch_add(1, std::memory_order_acq_rel); }
 
+void RefKDTree::cert_warm(double delta, const double *kpts, const uint8_t *known) const {
+    if (dim_ > 64 || nodes_.empty()) return;
+    CertScratch &S = cert_scratch();
+    std::vector<uint32_t> *keep = S.blame;
+    S.blame = nullptr;   // the strict replay's key
+    cert_reset(delta, kpts, known);
+    S.blame = keep;
+}
+
 void RefKDTree::cert_prepare(double delta, const double *kpts, const uint8_t *known) const {
     if (dim_ > 64 || nodes_.empty()) return;
     CertScratch &S = cert_scratch();

@@ -93,6 +93,9 @@ public:
     // aggregates and every node's replayed split, top down (a later certified_search with the
     // same key then only walks).  The caller keeps kpts / known unchanged until its replays.
     void cert_prepare(double delta, const double *kpts, const uint8_t *known) const;
+    // Only the shared state's cheap part for (delta, kpts, known): the per-node aggregates and
+    // the reset node states (every node's split is then replayed by the first search reaching it).
+    void cert_warm(double delta, const double *kpts, const uint8_t *known) const;
     // The same after kpts / known changed on the rows pts[0..n) only: the calling thread's
     // cache keeps its per-node values but those of these points' leaves and their ancestors.
     void cert_update(const uint32_t *pts, size_t n) const;
