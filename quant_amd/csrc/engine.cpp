@@ -1417,7 +1417,10 @@ qvq_status certify_rows(qvq_ctx *ctx, const RefKDTree &tree, const double *cb, c
         return true;
     };
     std::vector<uint32_t> ready, &pend = cs.pend;
-    const bool near_first = long_search || nu <= 16;   // few rows: skip replays doomed by unknown candidates
+    // long searches (48-D) list candidates first and skip the replays their unknown candidates
+    // doom; short ones replay first and list candidates for the rows left open only (C3's last
+    // level: 2 rows, near sets 36 us of a 53 us check after the export, profiles/r05p)
+    const bool near_first = long_search;
     if (near_first) {
         near(all);
         for (uint32_t u = 0; u < nu; u++) {

@@ -59,7 +59,7 @@ int main(int argc, char **argv) {
                 if (!known[(size_t)j * D + d]) return false;
             return true;
         };
-        const bool long_search = (uint64_t)K * D >= 65536 || n <= 16;   // (near_set first)
+        const bool long_search = (uint64_t)K * D >= 65536;   // (near_set first)
         for (uint32_t r = 0; r < n; r++) {
             bool k = true;
             if (long_search) {
