@@ -942,8 +942,10 @@ void start_tree_job(qvq_ctx *ctx, const double *hC, uint32_t K, int buf, uint64_
     post_job(ctx, [ctx, hC, K, buf, wait_seq, slot] {
         const auto t0 = std::chrono::steady_clock::now();
         volatile uint64_t *flag = ctx->h_ready;
-        while (wait_seq && *flag < wait_seq)   // the codebook's publication (bounded by cancel)
+        while (wait_seq && *flag < wait_seq) {   // the codebook's publication (bounded by cancel)
             if (ctx->tree_cancel.load(std::memory_order_relaxed)) return;
+            cpu_relax();
+        }
         std::atomic_thread_fence(std::memory_order_acquire);
         const auto t1 = std::chrono::steady_clock::now();
         build_tree_host(ctx, hC, K, buf, ctx->job_kd, &ctx->tree_cancel);
@@ -1549,6 +1551,8 @@ uint32_t cert_threads() {
     static const uint32_t n = [] {
         const char *e = std::getenv("QVQ_CERT_THREADS");
         if (e) return (uint32_t)std::max(1, std::atoi(e));
+        // (C4 at 1 / 2 / 4 / 8 helpers is within the boxes' run-to-run spread, 6.8-7.6 ms:
+        // profiles/r05s, r05u)
         return std::max<uint32_t>(1, std::min<uint32_t>(8, std::thread::hardware_concurrency() / 2));
     }();
     return n;
@@ -1626,8 +1630,10 @@ void verify_level(qvq_ctx *ctx, qvq_ctx::Verify &v) {
     (void)hipSetDevice(ctx->dev);
     // the known split and the tree's replay state were built on the prep worker while the GPU
     // ran the level (qvq_lbg, after the level's tree)
-    while (!v.prep_done.load(std::memory_order_acquire))
+    while (!v.prep_done.load(std::memory_order_acquire)) {
         if (v.cancel.load(std::memory_order_relaxed)) return;
+        cpu_relax();
+    }
     // the check usually starts while the GPU still runs its level (the last level's check is
     // then all that is left of the call): the known split and the tree's aggregates before the
     // export arrives, and for short searches (D = 12: a few hundred nodes) every node's split
@@ -1640,8 +1646,10 @@ void verify_level(qvq_ctx *ctx, qvq_ctx::Verify &v) {
         if (!full) v.tree->cert_warm(KAHAN_DELTA, v.cs.kp.data(), v.cs.known.data());
     }
     volatile uint64_t *flag = ctx->h_ready;
-    while (*flag < v.seq)   // the export is released with the codebook's ready number
+    while (*flag < v.seq) {   // the export is released with the codebook's ready number
         if (v.cancel.load(std::memory_order_relaxed)) return;
+        cpu_relax();
+    }
     std::atomic_thread_fence(std::memory_order_acquire);
     static const int fail_level = std::getenv("QVQ_KAHAN_FAIL_LEVEL") ? std::atoi(std::getenv("QVQ_KAHAN_FAIL_LEVEL")) : 0;
     static const int fail_rank = std::getenv("QVQ_KAHAN_FAIL_RANK") ? std::atoi(std::getenv("QVQ_KAHAN_FAIL_RANK")) : -1;

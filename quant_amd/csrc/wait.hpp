@@ -15,6 +15,14 @@
 
 namespace qvq {
 
+// One step of a host spin-wait: the x86 pause hint, so a polling thread leaves its core's
+// other hardware thread (often the one building the level's kd-tree) its issue slots.
+inline void cpu_relax() {
+#if defined(__x86_64__) || defined(__i386__)
+    __builtin_ia32_pause();
+#endif
+}
+
 enum class StreamState { Running, Drained, Failed };
 enum class CommState { None, Healthy, Failed };
 
@@ -32,6 +40,7 @@ qvq_status wait_until(Done done, Stream stream, Comm comm, double timeout_s, std
     // communicator only every ~20 ms of waiting
     auto next_check = t0 + std::chrono::milliseconds(20);
     while (!done()) {
+        cpu_relax();
         const auto now = clock::now();
         if (now < next_check) continue;
         std::string msg;
