@@ -825,6 +825,23 @@ bool join_tree_job(qvq_ctx *ctx, bool cancel);
 // Build the reference kd-tree over the host copy hC of the K code vectors being searched
 // into tree image buffer buf (pinned host memory, DMA-copied to d_tree for kd_resolve_kernel).  An empty
 // view means host resolution (tree too deep/large for the kernel's LDS, or QVQ_KDTREE=host).
+// QVQ_HOST_TRACE=1: a host timeline of each qvq_lbg (us since its start, per thread),
+// printed to stderr at its end: the main thread's tree builds and enqueues, the checks' start,
+// export and end (diagnostics for where a quantize waits).
+struct HostTrace {
+    bool on = false;
+    std::chrono::steady_clock::time_point t0;
+    std::mutex m;
+    std::vector<std::pair<double, std::string>> ev;
+    void mark(const std::string &what) {
+        if (!on) return;
+        const double t = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
+        std::lock_guard<std::mutex> g(m);
+        ev.emplace_back(t, what);
+    }
+};
+HostTrace g_htrace;
+
 // Level L's split codebook as the finalize of level L - 1 publishes it (host / device view).
 // Double-buffered by level parity: the synchronous Kahan levels build a level's tree on the
 // worker from this copy while the level's own finalize already publishes the next level's
@@ -1207,8 +1224,10 @@ qvq_status run_level(qvq_ctx *ctx, uint32_t K, int slot, bool sums_out, const do
     const auto tw0 = std::chrono::steady_clock::now();
     if (wait_seq && (st = wait_codebook(ctx, wait_seq)) != QVQ_OK) return st;
     const auto tw1 = std::chrono::steady_clock::now();
+    g_htrace.mark("K" + std::to_string(K) + " codebook seen, tree build");
     KdView kd;
     build_tree(ctx, hC, K, slot & 1, kd);
+    g_htrace.mark("K" + std::to_string(K) + " tree built");
     ctx->tm.wait_ms[slot] = std::chrono::duration<double, std::milli>(tw1 - tw0).count();
     ctx->tm.tree_ms[slot] = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tw1).count();
     if (abl_skip() & 2) {
@@ -1246,6 +1265,7 @@ constexpr double KAHAN_DELTA = 0x1p-49;
 // cells of the points a collecting replay blames, and once more.  done = false, nothing
 // changed, when a row stays open: the caller then computes the whole split and its tree.
 uint32_t cert_threads();
+
 
 // QVQ_CERT_TRACE=1: the certificate's phases, us since the check saw its level's export
 struct CertTrace {
@@ -1338,19 +1358,29 @@ void pool_run(qvq_ctx *ctx, uint32_t n, const std::function<void(uint32_t)> &fn)
 // is the exact sum rounded once: the same centroid bits; pcnt, the finalize's parent counts).
 // The tree's replay caches are reset for it; with prepare also built (the aggregates and every
 // node's replayed split: the last level's check does this before its tie rows arrive).
+// par (optional): the rows and the aggregates over the certificate's helper threads (the last
+// level's check sets up a K = 4096, D = 48 certificate after its tree: ~0.5 ms on one thread)
 void cert_init(const RefKDTree &tree, CertState &cs, const double *cb, const std::vector<uint32_t> &pcnt, uint32_t K,
-               uint32_t D, bool prepare) {
+               uint32_t D, bool prepare, qvq_ctx *par = nullptr) {
     const uint32_t Kc = K / 2;
-    cs.kp.assign(cb, cb + (size_t)K * D);
+    cs.kp.resize((size_t)K * D);
     cs.known.resize((size_t)K * D);
     const bool counts = pcnt.size() == Kc;
-    for (uint32_t j = 0; j < K; j++) {
-        const double u = j < Kc ? 1 + 0.2 : 1 - 0.2;
-        const double *v = &cs.kp[(size_t)j * D];
-        uint8_t *k = &cs.known[(size_t)j * D];
-        const bool few = counts && pcnt[j % Kc] <= 2;
-        for (uint32_t d = 0; d < D; d++) k[d] = few || v[d] == 0 || std::fabs(v[d] - u) <= 1e-14;
-    }
+    auto rows = [&](uint32_t j0, uint32_t j1) {
+        std::memcpy(&cs.kp[(size_t)j0 * D], cb + (size_t)j0 * D, (size_t)(j1 - j0) * D * 8);
+        for (uint32_t j = j0; j < j1; j++) {
+            const double u = j < Kc ? 1 + 0.2 : 1 - 0.2;
+            const double *v = &cs.kp[(size_t)j * D];
+            uint8_t *k = &cs.known[(size_t)j * D];
+            const bool few = counts && pcnt[j % Kc] <= 2;
+            for (uint32_t d = 0; d < D; d++) k[d] = few || v[d] == 0 || std::fabs(v[d] - u) <= 1e-14;
+        }
+    };
+    const uint32_t nt = par && (uint64_t)K * D >= 65536 ? std::min<uint32_t>(cert_threads(), 8) : 1;
+    if (nt > 1)
+        pool_run(par, nt, [&](uint32_t t) { rows((uint32_t)((uint64_t)K * t / nt), (uint32_t)((uint64_t)K * (t + 1) / nt)); });
+    else
+        rows(0, K);
     tree.cert_clear();   // kp / known: this level's (the vectors are reused)
     if (prepare) tree.cert_prepare(KAHAN_DELTA, cs.kp.data(), cs.known.data());
     cs.prepared = true;
@@ -1627,6 +1657,11 @@ qvq_status certify_kahan_ties(qvq_ctx *ctx, uint32_t K, unsigned nt, uint64_t *t
 // every rank), exercising the redo.
 void verify_level(qvq_ctx *ctx, qvq_ctx::Verify &v) {
     v.status = 1;
+    g_htrace.mark("check K" + std::to_string(v.K) + " start");
+    struct End {
+        const qvq_ctx::Verify &v;
+        ~End() { g_htrace.mark("check K" + std::to_string(v.K) + " end, status " + std::to_string(v.status)); }
+    } end_mark{v};
     (void)hipSetDevice(ctx->dev);
     // the known split and the tree's replay state were built on the prep worker while the GPU
     // ran the level (qvq_lbg, after the level's tree)
@@ -1642,8 +1677,12 @@ void verify_level(qvq_ctx *ctx, qvq_ctx::Verify &v) {
     if (early && !v.cs.prepared && v.tree && !v.tree->cancelled() && v.K >= 2 &&
         v.cb.size() == (size_t)v.K * ctx->D) {
         const bool full = (uint64_t)v.K * ctx->D < 65536;
-        cert_init(*v.tree, v.cs, v.cb.data(), v.cnt, v.K, ctx->D, full);
-        if (!full) v.tree->cert_warm(KAHAN_DELTA, v.cs.kp.data(), v.cs.known.data());
+        cert_init(*v.tree, v.cs, v.cb.data(), v.cnt, v.K, ctx->D, full, ctx);
+        g_htrace.mark("check K" + std::to_string(v.K) + " known split set");
+        if (!full)
+            v.tree->cert_warm(KAHAN_DELTA, v.cs.kp.data(), v.cs.known.data(), cert_threads(),
+                              [ctx](unsigned n, const std::function<void(unsigned)> &fn) { pool_run(ctx, n, fn); });
+        g_htrace.mark("check K" + std::to_string(v.K) + " aggregates set");
     }
     volatile uint64_t *flag = ctx->h_ready;
     while (*flag < v.seq) {   // the export is released with the codebook's ready number
@@ -1651,6 +1690,7 @@ void verify_level(qvq_ctx *ctx, qvq_ctx::Verify &v) {
         cpu_relax();
     }
     std::atomic_thread_fence(std::memory_order_acquire);
+    g_htrace.mark("check K" + std::to_string(v.K) + " export seen");
     static const int fail_level = std::getenv("QVQ_KAHAN_FAIL_LEVEL") ? std::atoi(std::getenv("QVQ_KAHAN_FAIL_LEVEL")) : 0;
     static const int fail_rank = std::getenv("QVQ_KAHAN_FAIL_RANK") ? std::atoi(std::getenv("QVQ_KAHAN_FAIL_RANK")) : -1;
     if (fail_level && (int)v.level == fail_level && (fail_rank < 0 || fail_rank == ctx->rank)) return;
@@ -2346,6 +2386,13 @@ QVQ_API qvq_status qvq_lbg(qvq_ctx *ctx, uint32_t bits, double eps, double *code
     HIPCHK(hipSetDevice(ctx->dev));
     if (ctx->exact) return lbg_exact(ctx, bits, codebook, assign, distortion);
     const auto t0 = std::chrono::steady_clock::now();
+    static const bool htrace = env_is("QVQ_HOST_TRACE", "1");
+    if (htrace) {
+        std::lock_guard<std::mutex> g(g_htrace.m);
+        g_htrace.on = true;
+        g_htrace.t0 = t0;
+        g_htrace.ev.clear();
+    }
     const uint32_t Kmax = 1u << bits;
     qvq_status st = ensure_levels(ctx, std::max<uint32_t>(Kmax, 2));
     if (st != QVQ_OK) return st;
@@ -2479,7 +2526,9 @@ QVQ_API qvq_status qvq_lbg(qvq_ctx *ctx, uint32_t bits, double eps, double *code
         if (spec) {
             if (lvl >= 4) {
                 bool ok;
+                g_htrace.mark("L" + std::to_string(lvl) + " joins check K" + std::to_string(ctx->ver[lvl % 3].K));
                 if ((st = join_verify_bounded(ctx, ctx->ver[lvl % 3], ok)) != QVQ_OK) return st;
+                g_htrace.mark("L" + std::to_string(lvl) + " joined");
                 if (!ok && !multi) {
                     spec_failed = true;
                     break;
@@ -2575,6 +2624,7 @@ QVQ_API qvq_status qvq_lbg(qvq_ctx *ctx, uint32_t bits, double eps, double *code
                     verify_level(ctx, *vp);
                     vp->done.store(true, std::memory_order_release);
                 });
+                g_htrace.mark("L" + std::to_string(lvl) + " finalize enqueued, check posted");
             }
             if (sync_kahan) {   // the level's ties (published after its recheck)
                 if ((st = wait_flag(ctx, ctx->h_ready + 1, ctx->pub_seq)) != QVQ_OK) return st;
@@ -2606,11 +2656,13 @@ QVQ_API qvq_status qvq_lbg(qvq_ctx *ctx, uint32_t bits, double eps, double *code
     }
     if (spec && !spec_failed) {   // the results' copy overlaps the last checks
         if ((st = enqueue_out()) != QVQ_OK) return st;
+        g_htrace.mark("results' copy enqueued");
         for (uint32_t l = bits >= 3 ? bits - 2 : 1; l <= bits; l++) {
             bool ok;
             if ((st = join_verify_bounded(ctx, ctx->ver[l % 3], ok)) != QVQ_OK) return st;
             local_fail = local_fail || !ok;
         }
+        g_htrace.mark("last checks joined");
         spec_failed = local_fail;
         if (multi && (st = resolve_deferred(ctx, bits, alev, spec_failed)) != QVQ_OK) return st;
     }
@@ -2645,6 +2697,7 @@ QVQ_API qvq_status qvq_lbg(qvq_ctx *ctx, uint32_t bits, double eps, double *code
         const uint64_t cb_bytes = codebook ? (uint64_t)Kmax * ctx->D * 8 : 0;
         qvq_status ws = wait_flag(ctx, reinterpret_cast<volatile uint64_t *>(h_small + (1024 - 64 - 8)), out_seq);
         if (ws != QVQ_OK) return ws;
+        g_htrace.mark("results copied");
         if (assign)   // every collective of this call is complete: a plain copy
             HIPCHK(host_copy(ctx, assign, ctx->d_A, ctx->N * 4, hipMemcpyDeviceToHost));
         std::memcpy(dres, h_small, sizeof(dres));
@@ -2678,6 +2731,14 @@ QVQ_API qvq_status qvq_lbg(qvq_ctx *ctx, uint32_t bits, double eps, double *code
     }
     (void)hipGetLastError();
     ctx->tm.total_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    if (htrace) {
+        g_htrace.mark("return");
+        std::lock_guard<std::mutex> g(g_htrace.m);
+        std::string out = "qvq host trace:";
+        for (const auto &e : g_htrace.ev) out += "\n  " + std::to_string((int)e.first) + " " + e.second;
+        std::fprintf(stderr, "%s\n", out.c_str());
+        g_htrace.on = false;
+    }
     return QVQ_OK;
 }
 

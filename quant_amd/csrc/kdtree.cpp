@@ -7,6 +7,8 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstring>
+#include <immintrin.h>
 #include <limits>
 #include <memory>
 #include <thread>
@@ -27,6 +29,12 @@ struct BufPool {
 }  // namespace
 
 template <class T>
+void Recycled<T>::align() {   // (threads that share a buffer write whole cache lines)
+    const uintptr_t a = reinterpret_cast<uintptr_t>(p_.get());
+    base_ = reinterpret_cast<T *>((a + 63) & ~(uintptr_t)63);
+}
+
+template <class T>
 void Recycled<T>::resize(size_t n) {
     n_ = n;
     if (n <= cap_) return;
@@ -42,11 +50,14 @@ void Recycled<T>::resize(size_t n) {
             cap_ = P.free[best].first;
             p_ = std::move(P.free[best].second);
             P.free.erase(P.free.begin() + (std::ptrdiff_t)best);
+            align();
             return;
         }
     }
-    p_.reset(new T[n]);
+    // cap_ usable elements after the 64-byte alignment of the base
+    p_.reset(new T[n + 64 / sizeof(T) + 1]);
     cap_ = n;
+    align();
 }
 
 template <class T>
@@ -60,12 +71,14 @@ void Recycled<T>::release() {
             if (P.free[i].first < P.free[s].first) s = i;
         if (P.free[s].first >= cap_) {
             p_.reset();
+            base_ = nullptr;
             cap_ = n_ = 0;
             return;
         }
         P.free.erase(P.free.begin() + (std::ptrdiff_t)s);
     }
     P.free.emplace_back(cap_, std::move(p_));
+    base_ = nullptr;
     cap_ = n_ = 0;
 }
 template class Recycled<double>;
@@ -596,6 +609,15 @@ void RefKDTree::cert_ensure_agg(uint64_t gen, const double *kpts, const uint8_t 
     if (agg_gen_.load(std::memory_order_acquire) == gen && agg_k_ == kpts && agg_known_ == known) return;
     std::lock_guard<std::mutex> g(agg_mu_);
     if (agg_gen_.load(std::memory_order_acquire) == gen && agg_k_ == kpts && agg_known_ == known) return;
+    agg_prepare(kpts, known);
+    // per node and dimension: min / max over its points whose bits are not known (exact-sum
+    // values) and over those known (the reference's values), children before parents
+    for (size_t i = nodes_.size(); i-- > 0;) cert_agg_node(i);
+    agg_gen_.store(gen, std::memory_order_release);
+}
+
+// (under agg_mu_) the parent / leaf maps and the aggregates' storage for (kpts, known)
+void RefKDTree::agg_prepare(const double *kpts, const uint8_t *known) const {
     const size_t nn = nodes_.size();
     if (parent_.size() != nn) {
         parent_.assign(nn, -1);
@@ -610,10 +632,6 @@ void RefKDTree::cert_ensure_agg(uint64_t gen, const double *kpts, const uint8_t 
     agg_k_ = kpts;
     agg_known_ = known;
     agg_.resize(nn * dim_ * 4);
-    // per node and dimension: min / max over its points whose bits are not known (exact-sum
-    // values) and over those known (the reference's values), children before parents
-    for (size_t i = nn; i-- > 0;) cert_agg_node(i);
-    agg_gen_.store(gen, std::memory_order_release);
 }
 
 void RefKDTree::cert_reset(double delta, const double *kpts, const uint8_t *known) const {
@@ -659,33 +677,71 @@ void RefKDTree::cert_reset(double delta, const double *kpts, const uint8_t *know
 // points, stored [min unknown | max unknown | min known | max known][dim] so that the loops
 // below are plain element-wise min / max (vectorised; a branch per value mispredicted on the
 // irregular known pattern).
-void RefKDTree::cert_agg_node(size_t i) const {
+namespace {
+bool has_avx2() {
+    static const bool v = __builtin_cpu_supports("avx2");
+    return v;
+}
+// One leaf point's row into a node's aggregates, four dimensions at a time (blends on the
+// known mask, then min / max; the values are finite, so min_pd / max_pd are exact): returns the
+// first dimension left to the scalar loop.
+__attribute__((target("avx2"))) int agg_row_avx2(const double *x, const double *kv, const uint8_t *k, int D,
+                                                 double *mnu, double *mxu, double *mnk, double *mxk) {
+    const __m256d inf = _mm256_set1_pd(std::numeric_limits<double>::infinity()), ninf = _mm256_sub_pd(_mm256_setzero_pd(), inf);
+    int d = 0;
+    for (; d + 4 <= D; d += 4) {
+        int32_t kb;
+        std::memcpy(&kb, k + d, 4);
+        const __m256i k64 = _mm256_cvtepu8_epi64(_mm_cvtsi32_si128(kb));
+        const __m256d m = _mm256_castsi256_pd(_mm256_cmpgt_epi64(k64, _mm256_setzero_si256()));   // known
+        const __m256d xv = _mm256_loadu_pd(x + d), kk = _mm256_loadu_pd(kv + d);
+        _mm256_storeu_pd(mnu + d, _mm256_min_pd(_mm256_loadu_pd(mnu + d), _mm256_blendv_pd(xv, inf, m)));
+        _mm256_storeu_pd(mxu + d, _mm256_max_pd(_mm256_loadu_pd(mxu + d), _mm256_blendv_pd(xv, ninf, m)));
+        _mm256_storeu_pd(mnk + d, _mm256_min_pd(_mm256_loadu_pd(mnk + d), _mm256_blendv_pd(inf, kk, m)));
+        _mm256_storeu_pd(mxk + d, _mm256_max_pd(_mm256_loadu_pd(mxk + d), _mm256_blendv_pd(ninf, kk, m)));
+    }
+    return d;
+}
+}  // namespace
+
+void RefKDTree::cert_agg_node(size_t i) const { cert_agg_dims(i, 0, dim_); }
+
+// cert_agg_node over dimensions [d0, d1) only (the parallel warm-up splits the dimensions).
+void RefKDTree::cert_agg_dims(size_t i, int d0, int d1) const {
     constexpr double INF = std::numeric_limits<double>::infinity();
     const int D = dim_;
     double *__restrict mnu = &agg_[i * D * 4], *__restrict mxu = mnu + D, *__restrict mnk = mxu + D,
                        *__restrict mxk = mnk + D;
     const Node &n = nodes_[i];
     if (n.leaf) {
-        for (int d = 0; d < D; d++) mnu[d] = mnk[d] = INF, mxu[d] = mxk[d] = -INF;
+        for (int d = d0; d < d1; d++) mnu[d] = mnk[d] = INF, mxu[d] = mxk[d] = -INF;
         for (size_t j = n.left; j < n.right; j++) {
-            const size_t r = vind_[j] * (size_t)D;
+            const size_t r = vind_[j] * (size_t)D + d0;
             const double *__restrict x = pts_ + r, *__restrict kv = agg_k_ + r;
             const uint8_t *__restrict k = agg_known_ + r;
-            for (int d = 0; d < D; d++) {
-                const bool kk = k[d] != 0;
-                mnu[d] = std::min(mnu[d], kk ? INF : x[d]);
-                mxu[d] = std::max(mxu[d], kk ? -INF : x[d]);
-                mnk[d] = std::min(mnk[d], kk ? kv[d] : INF);
-                mxk[d] = std::max(mxk[d], kk ? kv[d] : -INF);
+            const int w = d1 - d0;
+            int e = 0;
+            if (has_avx2()) e = agg_row_avx2(x, kv, k, w, mnu + d0, mxu + d0, mnk + d0, mxk + d0);
+            // (the compiler keeps this loop scalar: its selects on a loaded byte are control flow)
+            for (; e < w; e++) {
+                const int d = d0 + e;
+                const bool kk = k[e] != 0;
+                const double xu_lo = kk ? INF : x[e], xu_hi = kk ? -INF : x[e];
+                const double xk_lo = kk ? kv[e] : INF, xk_hi = kk ? kv[e] : -INF;
+                mnu[d] = xu_lo < mnu[d] ? xu_lo : mnu[d];
+                mxu[d] = xu_hi > mxu[d] ? xu_hi : mxu[d];
+                mnk[d] = xk_lo < mnk[d] ? xk_lo : mnk[d];
+                mxk[d] = xk_hi > mxk[d] ? xk_hi : mxk[d];
             }
         }
         return;
     }
     const double *__restrict b = &agg_[(size_t)n.child1 * D * 4], *__restrict c = &agg_[(size_t)n.child2 * D * 4];
-    for (int d = 0; d < D; d++) mnu[d] = std::min(b[d], c[d]);
-    for (int d = D; d < 2 * D; d++) mxu[d - D] = std::max(b[d], c[d]);
-    for (int d = 2 * D; d < 3 * D; d++) mnk[d - 2 * D] = std::min(b[d], c[d]);
-    for (int d = 3 * D; d < 4 * D; d++) mxk[d - 3 * D] = std::max(b[d], c[d]);
+    for (int q = 0; q < 4; q++)   // [min unknown | max unknown | min known | max known]
+        for (int d = d0; d < d1; d++) {
+            const double u = b[q * D + d], v = c[q * D + d];
+            mnu[q * D + d] = (q & 1) ? (v > u ? v : u) : (v < u ? v : u);
+        }
 }
 
 // The least (greatest) value of dimension d over node's points, over every allowed codebook.
@@ -720,11 +776,30 @@ void RefKDTree::certify_blame(const double *q, double delta, const double *kpts,
 
 void RefKDTree::cert_clear() const { cert_gen_.fetch_add(1, std::memory_order_acq_rel); }
 
-void RefKDTree::cert_warm(double delta, const double *kpts, const uint8_t *known) const {
+void RefKDTree::cert_warm(double delta, const double *kpts, const uint8_t *known, unsigned nthr,
+                          const std::function<void(unsigned, const std::function<void(unsigned)> &)> &run) const {
     if (dim_ > 64 || nodes_.empty()) return;
+    {   // the aggregates, the dimensions split over nthr threads (memory-bound: ~4.6 MB at
+        // K = 4096, D = 48; whole 64-byte lines per thread and node)
+        const uint64_t gen = cert_gen_.load(std::memory_order_acquire);
+        std::lock_guard<std::mutex> g(agg_mu_);
+        if (!(agg_gen_.load(std::memory_order_acquire) == gen && agg_k_ == kpts && agg_known_ == known)) {
+            agg_prepare(kpts, known);
+            const size_t nn = nodes_.size();
+            const int D = dim_;
+            const unsigned nt = run && nthr > 1 ? std::min<unsigned>(nthr, (unsigned)(D + 7) / 8) : 1;
+            auto part = [&](unsigned t) {
+                const int d0 = (int)((D * (uint64_t)t / nt) & ~7ull), d1 = t + 1 == nt ? D : (int)((D * (uint64_t)(t + 1) / nt) & ~7ull);
+                for (size_t i = nn; i-- > 0;) cert_agg_dims(i, d0, d1);
+            };
+            if (nt > 1) run(nt, part);
+            else part(0);
+            agg_gen_.store(gen, std::memory_order_release);
+        }
+    }
     CertScratch &S = cert_scratch();
     std::vector<uint32_t> *keep = S.blame;
-    S.blame = nullptr;   // the strict replay's key
+    S.blame = nullptr;   // the strict replay's key (the node states reset, the root's box)
     cert_reset(delta, kpts, known);
     S.blame = keep;
 }

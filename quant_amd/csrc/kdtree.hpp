@@ -13,6 +13,7 @@
 #include <memory>
 #include <mutex>
 #include <cstdint>
+#include <functional>
 #include <vector>
 
 #include "kdtree_dev.hpp"
@@ -35,16 +36,18 @@ public:
     Recycled(const Recycled &) = delete;
     Recycled &operator=(const Recycled &) = delete;
     ~Recycled() { release(); }
-    void resize(size_t n);   // contents undefined
+    void resize(size_t n);   // contents undefined; data() 64-byte aligned
     size_t size() const { return n_; }
-    T *data() { return p_.get(); }
-    const T *data() const { return p_.get(); }
-    T &operator[](size_t i) { return p_[i]; }
-    const T &operator[](size_t i) const { return p_[i]; }
+    T *data() { return base_; }
+    const T *data() const { return base_; }
+    T &operator[](size_t i) { return base_[i]; }
+    const T &operator[](size_t i) const { return base_[i]; }
 
 private:
     void release();
+    void align();
     std::unique_ptr<T[]> p_;
+    T *base_ = nullptr;
     size_t cap_ = 0, n_ = 0;
 };
 
@@ -95,7 +98,9 @@ public:
     void cert_prepare(double delta, const double *kpts, const uint8_t *known) const;
     // Only the shared state's cheap part for (delta, kpts, known): the per-node aggregates and
     // the reset node states (every node's split is then replayed by the first search reaching it).
-    void cert_warm(double delta, const double *kpts, const uint8_t *known) const;
+    // run(n, fn): fn(t) for t < n on n threads (nullptr / nthr 1: this thread only).
+    void cert_warm(double delta, const double *kpts, const uint8_t *known, unsigned nthr = 1,
+                   const std::function<void(unsigned, const std::function<void(unsigned)> &)> &run = nullptr) const;
     // The same after kpts / known changed on the rows pts[0..n) only: the calling thread's
     // cache keeps its per-node values but those of these points' leaves and their ancestors.
     void cert_update(const uint32_t *pts, size_t n) const;
@@ -185,6 +190,8 @@ private:
     void cert_reset(double delta, const double *kpts, const uint8_t *known) const;
     void blame_extremes(int node, int d) const;
     void cert_agg_node(size_t i) const;
+    void cert_agg_dims(size_t i, int d0, int d1) const;
+    void agg_prepare(const double *kpts, const uint8_t *known) const;
     Iv iv_min(int node, int d) const;
     Iv iv_max(int node, int d) const;
 
