@@ -243,6 +243,9 @@ struct qvq_ctx {
     uint64_t *d_kc_chain = nullptr;   // chained Kahan sums: gather | state (k_kahan.hip)
     uint64_t kc_chain_cap = 0;
     std::atomic<bool> tree_cancel{false};
+    // the main thread is building a level's kd-tree (on the critical path: the GPU waits for it);
+    // the checks then replay on their own thread only (cert_helpers)
+    std::atomic<bool> tree_building{false};
     bool tree_job = false, job_ok = false;
     int job_buf = 0;
     KdView job_kd;
@@ -1226,7 +1229,9 @@ qvq_status run_level(qvq_ctx *ctx, uint32_t K, int slot, bool sums_out, const do
     const auto tw1 = std::chrono::steady_clock::now();
     g_htrace.mark("K" + std::to_string(K) + " codebook seen, tree build");
     KdView kd;
+    ctx->tree_building.store(true, std::memory_order_relaxed);
     build_tree(ctx, hC, K, slot & 1, kd);
+    ctx->tree_building.store(false, std::memory_order_relaxed);
     g_htrace.mark("K" + std::to_string(K) + " tree built");
     ctx->tm.wait_ms[slot] = std::chrono::duration<double, std::milli>(tw1 - tw0).count();
     ctx->tm.tree_ms[slot] = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tw1).count();
@@ -1265,6 +1270,10 @@ constexpr double KAHAN_DELTA = 0x1p-49;
 // cells of the points a collecting replay blames, and once more.  done = false, nothing
 // changed, when a row stays open: the caller then computes the whole split and its tree.
 uint32_t cert_threads();
+// The threads a check may use now: cert_threads(), or 1 while the main thread builds a kd-tree
+// (a check of level L runs beside the build of level L + 1's tree, which 8 helpers slowed from
+// 1.7-1.8 to 2.2-2.5 ms at C4's level 12, profiles/r05t-r05y; QVQ_CHECK_YIELD=0: A/B).
+uint32_t cert_helpers(const qvq_ctx *ctx);
 
 
 // QVQ_CERT_TRACE=1: the certificate's phases, us since the check saw its level's export
@@ -1376,7 +1385,7 @@ void cert_init(const RefKDTree &tree, CertState &cs, const double *cb, const std
             for (uint32_t d = 0; d < D; d++) k[d] = few || v[d] == 0 || std::fabs(v[d] - u) <= 1e-14;
         }
     };
-    const uint32_t nt = par && (uint64_t)K * D >= 65536 ? std::min<uint32_t>(cert_threads(), 8) : 1;
+    const uint32_t nt = par && (uint64_t)K * D >= 65536 ? std::min<uint32_t>(cert_helpers(par), 8) : 1;
     if (nt > 1)
         pool_run(par, nt, [&](uint32_t t) { rows((uint32_t)((uint64_t)K * t / nt), (uint32_t)((uint64_t)K * (t + 1) / nt)); });
     else
@@ -1409,8 +1418,10 @@ qvq_status certify_rows(qvq_ctx *ctx, const RefKDTree &tree, const double *cb, c
     cs.sel.assign(Kc, 0);
     // rows over host threads when the replays are long (48-D: the search visits most leaves)
     const bool long_search = (uint64_t)K * D >= 65536;   // 48-D: a search visits most leaves
-    const uint32_t nthr = long_search ? std::min<uint32_t>(nu, cert_threads()) : 1;
+    const uint32_t nthr = long_search ? std::min<uint32_t>(nu, cert_threads()) : 1;   // (the most)
     auto each = [&](const std::vector<uint32_t> &rows, auto &&fn) {   // fn(u, thread slot)
+        // (per phase: one thread while the main thread builds a tree, cert_helpers)
+        const uint32_t nthr = long_search ? std::min<uint32_t>(nu, cert_helpers(ctx)) : 1;
         if (nthr <= 1 || rows.size() < 2) {
             for (uint32_t u : rows) fn(u, 0u);
             return;
@@ -1576,6 +1587,11 @@ bool cert_mismatch(const CertState &cs, uint32_t K) {
     return false;
 }
 
+uint32_t cert_helpers(const qvq_ctx *ctx) {
+    static const bool yield = !env_is("QVQ_CHECK_YIELD", "0");
+    return yield && ctx->tree_building.load(std::memory_order_relaxed) ? 1u : cert_threads();
+}
+
 // Host threads for the certificate's replays (at most 8, half the machine's).
 uint32_t cert_threads() {
     static const uint32_t n = [] {
@@ -1680,7 +1696,7 @@ void verify_level(qvq_ctx *ctx, qvq_ctx::Verify &v) {
         cert_init(*v.tree, v.cs, v.cb.data(), v.cnt, v.K, ctx->D, full, ctx);
         g_htrace.mark("check K" + std::to_string(v.K) + " known split set");
         if (!full)
-            v.tree->cert_warm(KAHAN_DELTA, v.cs.kp.data(), v.cs.known.data(), cert_threads(),
+            v.tree->cert_warm(KAHAN_DELTA, v.cs.kp.data(), v.cs.known.data(), cert_helpers(ctx),
                               [ctx](unsigned n, const std::function<void(unsigned)> &fn) { pool_run(ctx, n, fn); });
         g_htrace.mark("check K" + std::to_string(v.K) + " aggregates set");
     }

@@ -20,6 +20,10 @@
 #include "quant_amd/RGBImage.hpp"
 #include "wait.hpp"
 
+#include <cmath>
+#include <functional>
+#include <thread>
+
 extern "C" void orc_kdtree_nn(const double *C, size_t K, int D, const double *Q, size_t nq, uint32_t *out);
 
 static int failures = 0;
@@ -55,6 +59,60 @@ static void test_kdtree() {
             t.flatten(nodes.data(), vind.data(), lo.data(), hi.data());
             std::vector<int> seen(K, 0);
             for (uint32_t v : vind) CHECK(v < K && !seen[v]++);
+        }
+    }
+}
+
+// The tie certificate's host state (kdtree.cpp: recycled 64-byte aligned scratch, the
+// aggregates built on one thread or split over threads by dimension, node-split replays,
+// collecting replays, cert_update): the same answers either way, for trees built one after
+// another (buffers passed from tree to tree), under the sanitizers.
+static void test_certificate() {
+    std::mt19937_64 rng(11);
+    const double delta = std::ldexp(1.0, -49);
+    auto threads = [](unsigned n, const std::function<void(unsigned)> &fn) {
+        std::vector<std::thread> th;
+        for (unsigned t = 1; t < n; t++) th.emplace_back(fn, t);
+        fn(0);
+        for (auto &x : th) x.join();
+    };
+    for (int D : {12, 48}) {
+        for (size_t K : {64, 512, 2048}) {
+            std::vector<double> C(K * D);
+            std::uniform_int_distribution<int> q8(0, 7);
+            for (size_t i = 0; i < K; i++)
+                for (int d = 0; d < D; d++) C[i * D + d] = (i % 5 == 4) ? 0.0 : q8(rng) * 0.1 + 0.05;
+            std::vector<uint8_t> known0(K * D);
+            for (size_t i = 0; i < K * D; i++) known0[i] = C[i] == 0.0 || (rng() % 4 == 0);
+            std::vector<double> Q;
+            for (int i = 0; i < 24; i++)
+                for (int d = 0; d < D; d++) Q.push_back(q8(rng) * 0.1);
+            int64_t first[24];
+            for (int pass = 0; pass < 2; pass++) {
+                std::vector<uint8_t> known(known0);   // (each pass from the same known split)
+                qvq::RefKDTree t(C.data(), K, D);
+                t.cert_clear();
+                if (pass == 0) t.cert_warm(delta, C.data(), known.data());
+                else t.cert_warm(delta, C.data(), known.data(), 3, threads);
+                if (K <= 512) t.cert_prepare(delta, C.data(), known.data());
+                std::vector<uint32_t> blame;
+                for (int i = 0; i < 24; i++) {
+                    const int64_t a = t.certified_search(Q.data() + (size_t)i * D, delta, C.data(), known.data());
+                    CHECK(a >= -1 && a < (int64_t)K);
+                    if (pass == 0) first[i] = a;
+                    else CHECK(a == first[i]);
+                    if (a < 0) t.certify_blame(Q.data() + (size_t)i * D, delta, C.data(), known.data(), blame);
+                }
+                for (uint32_t p : blame) {
+                    CHECK(p < K);
+                    std::fill(known.begin() + (size_t)p * D, known.begin() + (size_t)(p + 1) * D, 1);
+                }
+                t.cert_update(blame.data(), blame.size());
+                for (int i = 0; i < 24; i++) {
+                    const int64_t a = t.certified_search(Q.data() + (size_t)i * D, delta, C.data(), known.data());
+                    CHECK(a >= -1 && a < (int64_t)K);
+                }
+            }
         }
     }
 }
@@ -149,6 +207,7 @@ static void test_codec(const std::string &tmp) {
 int main(int argc, char **argv) {
     const std::string tmp = argc > 1 ? argv[1] : ".";
     test_kdtree();
+    test_certificate();
     test_wait();
     test_codec(tmp);
     std::printf("host sanitize test: %s (%d failures)\n", failures ? "FAILED" : "ok", failures);
