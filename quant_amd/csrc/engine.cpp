@@ -1270,9 +1270,10 @@ constexpr double KAHAN_DELTA = 0x1p-49;
 // cells of the points a collecting replay blames, and once more.  done = false, nothing
 // changed, when a row stays open: the caller then computes the whole split and its tree.
 uint32_t cert_threads();
-// The threads a check may use now: cert_threads(), or 1 while the main thread builds a kd-tree
-// (a check of level L runs beside the build of level L + 1's tree, which 8 helpers slowed from
-// 1.7-1.8 to 2.2-2.5 ms at C4's level 12, profiles/r05t-r05y; QVQ_CHECK_YIELD=0: A/B).
+// The threads a check may use now: cert_threads(); with QVQ_CHECK_YIELD=1 (A/B) 1 while the
+// main thread builds a kd-tree (a check of level L runs beside the build of level L + 1's tree,
+// which its helpers slow: 1.7-1.8 vs 2.2-2.5 ms at C4's level 12, profiles/r05t-r05y; yet the
+// check then finishes later, and C4 took 6.88 ms yielding vs 6.52 not, profiles/r05z).
 uint32_t cert_helpers(const qvq_ctx *ctx);
 
 
@@ -1588,7 +1589,7 @@ bool cert_mismatch(const CertState &cs, uint32_t K) {
 }
 
 uint32_t cert_helpers(const qvq_ctx *ctx) {
-    static const bool yield = !env_is("QVQ_CHECK_YIELD", "0");
+    static const bool yield = env_is("QVQ_CHECK_YIELD", "1");
     return yield && ctx->tree_building.load(std::memory_order_relaxed) ? 1u : cert_threads();
 }
 
