@@ -130,6 +130,16 @@ struct qvq_ctx {
     // the reference-bit (Kahan) centroids a level with kd-tree ties needs
     uint32_t *d_A_alt = nullptr;
     KahanWork kw;
+    // the whole reference-bit split of a 48-D level, computed on the main stream while the host
+    // builds the level's tree (full_split_level): its own workspace (the checks' cells use kw on
+    // the side stream meanwhile), the split into mapped memory by level parity, h_ready[4] its
+    // ready number
+    KahanWork kw_full;
+    double *d_kf_cent = nullptr, *h_kf_out = nullptr, *dh_kf_out = nullptr;
+    uint32_t kf_kcap = 0;
+    uint64_t kf_seq = 0;
+    bool want_full = false;        // qvq_lbg: the level may take it (speculative, one rank)
+    uint64_t kf_level_seq = 0;     // run_level: this level's ready number (0: none)
     double *d_kc_cent = nullptr, *d_kc_split = nullptr;   // Kahan centroids [K/2][D], their split [K][D]
     uint32_t kc_kcap = 0;
     std::vector<double> h_kc_split;   // host copy of the split for the tree build
@@ -223,6 +233,7 @@ struct qvq_ctx {
         std::unique_ptr<RefKDTree> tree;
         std::vector<double> cb;
         std::vector<uint32_t> cnt;   // the parent cells' row counts (empty: not known)
+        uint64_t full_seq = 0;       // the whole reference-bit split (ready number; 0: none)
         CertState cs;
         hipEvent_t ev = nullptr;
     } ver[3];   // level % 3
@@ -381,6 +392,11 @@ void free_kahan_work(KahanWork &w) {
 
 void free_kahan(qvq_ctx *ctx) {
     free_kahan_work(ctx->kw);
+    free_kahan_work(ctx->kw_full);
+    dfree(ctx->d_kf_cent);
+    if (ctx->h_kf_out) (void)hipHostFree(ctx->h_kf_out);
+    ctx->h_kf_out = ctx->dh_kf_out = nullptr;
+    ctx->kf_kcap = 0;
     dfree(ctx->d_kc_chain);
     ctx->kc_chain_cap = 0;
     dfree(ctx->d_kc_cent);
@@ -684,9 +700,10 @@ bool kahan_mode(const qvq_ctx *ctx) {
 // The recheck's absolute tie band: only where a reference-bit step follows (kahan_mode)
 double tie_band(const qvq_ctx *ctx) { return kahan_mode(ctx) ? ctx->tie_abs : 0.0; }
 
+qvq_status alloc_kahan_work(qvq_ctx *ctx, KahanWork &w, uint32_t Kc);
+
 qvq_status ensure_kahan(qvq_ctx *ctx, uint32_t Kc) {
     KahanWork &w = ctx->kw;
-    const uint64_t N = ctx->N;
     const uint32_t D = ctx->D;
     if (ctx->kc_kcap < Kc) {
         dfree(ctx->d_kc_cent);
@@ -702,6 +719,13 @@ qvq_status ensure_kahan(qvq_ctx *ctx, uint32_t Kc) {
         HIPCHK(hipHostGetDevicePointer(reinterpret_cast<void **>(&ctx->dh_kc_out), ctx->h_kc_out, 0));
         ctx->kc_kcap = Kc;
     }
+    return alloc_kahan_work(ctx, w, Kc);
+}
+
+// A Kahan workspace for N rows, Kc cells and D components (kept while it fits).
+qvq_status alloc_kahan_work(qvq_ctx *ctx, KahanWork &w, uint32_t Kc) {
+    const uint64_t N = ctx->N;
+    const uint32_t D = ctx->D;
     if (w.n_cap == N && w.k_cap >= Kc && w.d_cap == D) return QVQ_OK;
     const uint32_t kcap = std::max(Kc, w.k_cap);
     free_kahan_work(w);
@@ -734,6 +758,21 @@ qvq_status ensure_kahan(qvq_ctx *ctx, uint32_t Kc) {
     w.k_cap = kcap;
     w.d_cap = D;
     return QVQ_OK;
+}
+
+qvq_status ensure_kahan_full(qvq_ctx *ctx, uint32_t Kc) {
+    if (ctx->kf_kcap < Kc) {
+        dfree(ctx->d_kf_cent);
+        if (ctx->h_kf_out) (void)hipHostFree(ctx->h_kf_out);
+        ctx->h_kf_out = ctx->dh_kf_out = nullptr;
+        ctx->kf_kcap = 0;
+        HIPCHK(hipMalloc(&ctx->d_kf_cent, (uint64_t)Kc * ctx->D * 8));
+        HIPCHK(hipHostMalloc(reinterpret_cast<void **>(&ctx->h_kf_out), 2 * 2ull * Kc * ctx->D * 8,
+                             hipHostMallocMapped | hipHostMallocCoherent));
+        HIPCHK(hipHostGetDevicePointer(reinterpret_cast<void **>(&ctx->dh_kf_out), ctx->h_kf_out, 0));
+        ctx->kf_kcap = Kc;
+    }
+    return alloc_kahan_work(ctx, ctx->kw_full, Kc);
 }
 
 // Sum over the ranks of n small u64 values (host, in place) on the context's stream, waiting for
@@ -1218,6 +1257,28 @@ qvq_status run_level(qvq_ctx *ctx, uint32_t K, int slot, bool sums_out, const do
         ctx->nslabs = 0;   // reduced already
         HIPCHK(hipEventRecord(ctx->ev[slot][3], ctx->stream));
     }
+    // A 48-D level of a speculative quantize: the whole reference-bit split (the previous
+    // level's cells summed as the reference sums them) right behind the level's search, on the
+    // stream, where it runs while the GPU would wait for the host's tree build; the level's
+    // check then knows every code vector's bits (no blamed cells, no second replay).  C4's levels
+    // 11 and 12 (QVQ_FULL_SPLIT=0: the certificate's cells as before, A/B).
+    ctx->kf_level_seq = 0;
+    static const bool full_on = !env_is("QVQ_FULL_SPLIT", "0");
+    if (full_on && !defer_ties && ctx->want_full && K >= 4 && (uint64_t)K * ctx->D >= 65536 && ctx->d_A_alt &&
+        hC && ctx->nranks <= 1) {
+        if (wait_seq && (st = wait_codebook(ctx, wait_seq)) != QVQ_OK) return st;   // (the parent counts)
+        const uint32_t Kc = K / 2;
+        const uint32_t *pc = reinterpret_cast<const uint32_t *>(hC + (size_t)K * ctx->D);
+        uint64_t max_rows = 1;
+        for (uint32_t c = 0; c < Kc; c++) max_rows = std::max<uint64_t>(max_rows, pc[c]);
+        if ((st = ensure_kahan_full(ctx, Kc)) != QVQ_OK) return st;
+        double *out = ctx->dh_kf_out + (uint64_t)(slot & 1) * 2ull * Kc * ctx->D;
+        HIPCHK(launch_kahan_centroids(ctx->stream, ctx->kw_full, ctx->d_codes, ctx->Dp, ctx->D, ctx->N, ctx->d_A_alt,
+                                      Kc, ctx->d_kf_cent, out, nullptr, 0, max_rows));
+        ctx->kf_level_seq = ++ctx->kf_seq;
+        HIPCHK(launch_copy_out(ctx->stream, nullptr, nullptr, 0, nullptr, nullptr, 0, nullptr, nullptr, 0,
+                               ctx->dh_ready + 4, ctx->kf_level_seq, ctx->d_counters + 2 * 33 + 1));
+    }
     if (defer_ties) {   // qvq_lbg answers the ties after the finalize, if there are any (tree on the worker)
         start_tree_job(ctx, hC, K, slot & 1, wait_seq);
         ctx->upd[slot] = false;
@@ -1691,6 +1752,25 @@ void verify_level(qvq_ctx *ctx, qvq_ctx::Verify &v) {
     // export arrives, and for short searches (D = 12: a few hundred nodes) every node's split
     // replay too (C3: the last level's 2 tie rows took ~95 us after the export, r05i)
     static const bool early = !env_is("QVQ_CERT_EARLY", "0");   // A/B
+    if (v.full_seq && !v.cs.prepared && v.tree && !v.tree->cancelled() && v.cb.size() == (size_t)v.K * ctx->D) {
+        // the whole reference-bit split (run_level): every code vector known
+        volatile uint64_t *ff = ctx->h_ready + 4;
+        while (*ff < v.full_seq) {
+            if (v.cancel.load(std::memory_order_relaxed)) return;
+            cpu_relax();
+        }
+        std::atomic_thread_fence(std::memory_order_acquire);
+        const size_t KD = (size_t)v.K * ctx->D;
+        const double *split = ctx->h_kf_out + (size_t)((v.level - 1) & 1) * KD;
+        v.cs.kp.assign(split, split + KD);
+        v.cs.known.assign(KD, 1);
+        v.tree->cert_clear();
+        v.cs.prepared = true;
+        g_htrace.mark("check K" + std::to_string(v.K) + " whole split in");
+        v.tree->cert_warm(KAHAN_DELTA, v.cs.kp.data(), v.cs.known.data(), cert_helpers(ctx),
+                          [ctx](unsigned n, const std::function<void(unsigned)> &fn) { pool_run(ctx, n, fn); });
+        g_htrace.mark("check K" + std::to_string(v.K) + " aggregates set");
+    }
     if (early && !v.cs.prepared && v.tree && !v.tree->cancelled() && v.K >= 2 &&
         v.cb.size() == (size_t)v.K * ctx->D) {
         const bool full = (uint64_t)v.K * ctx->D < 65536;
@@ -2563,6 +2643,7 @@ QVQ_API qvq_status qvq_lbg(qvq_ctx *ctx, uint32_t bits, double eps, double *code
             std::swap(ctx->d_A, ctx->d_A_alt);   // d_A_alt: the previous level's assignment
         }
         alev[lvl] = ctx->d_A;
+        ctx->want_full = spec && !multi && kahan;
         if ((st = run_level(ctx, K, slot, true, host_cb_of(ctx, lvl), ctx->seq, sync_kahan)) != QVQ_OK) return st;
         if (spec) {   // the level's check: its tree now, its certificate prepared on the prep worker
             qvq_ctx::Verify &v = ctx->ver[lvl % 3];
@@ -2573,6 +2654,7 @@ QVQ_API qvq_status qvq_lbg(qvq_ctx *ctx, uint32_t bits, double eps, double *code
             v.cnt = std::move(ctx->cnt_local);
             ctx->cb_local.clear();
             ctx->cnt_local.clear();
+            v.full_seq = ctx->kf_level_seq;
             v.cs = CertState();
             v.prep_done.store(false);
             // Off by default (QVQ_CERT_PREP=1: on, A/B): replays that build the node splits they
