@@ -1261,9 +1261,12 @@ qvq_status run_level(qvq_ctx *ctx, uint32_t K, int slot, bool sums_out, const do
     // level's cells summed as the reference sums them) right behind the level's search, on the
     // stream, where it runs while the GPU would wait for the host's tree build; the level's
     // check then knows every code vector's bits (no blamed cells, no second replay).  C4's levels
-    // 11 and 12 (QVQ_FULL_SPLIT=0: the certificate's cells as before, A/B).
+    // 11 and 12, off by default (QVQ_FULL_SPLIT=1: on, A/B): the whole split of 1,024 / 2,048
+    // cells over C4's 1M rows takes ~2.7 ms of device time, far longer than the tree build it was
+    // to hide behind, and the last check then waits for it (C4 11.5-11.9 ms vs 6.0-7.0 with the
+    // certificate's cells, profiles/r05ab).
     ctx->kf_level_seq = 0;
-    static const bool full_on = !env_is("QVQ_FULL_SPLIT", "0");
+    static const bool full_on = env_is("QVQ_FULL_SPLIT", "1");
     if (full_on && !defer_ties && ctx->want_full && K >= 4 && (uint64_t)K * ctx->D >= 65536 && ctx->d_A_alt &&
         hC && ctx->nranks <= 1) {
         if (wait_seq && (st = wait_codebook(ctx, wait_seq)) != QVQ_OK) return st;   // (the parent counts)

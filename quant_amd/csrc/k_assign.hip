@@ -679,12 +679,29 @@ __global__ __launch_bounds__(NW * 64) void assign_small_kernel(
         __syncthreads();
         uint64_t *pdst = part + (uint64_t)blockIdx.x * K * MF_D;   // slab layout [d][k]
         uint32_t *cdst = part_cnt + (uint64_t)blockIdx.x * K;
-        for (uint32_t i = tid; i < K * (MF_D + 1); i += (NW * 64)) {   // [d][k] of the slab
-            const uint32_t d = i / K, k = i - d * K;
+        // P threads per slab entry ([d][k]), each summing copies j, j + P, ...; the P partial
+        // sums meet by xor shuffles inside the wave.  One thread per entry summed all `copies`
+        // (64 at K <= 8) in a serial chain of LDS reads while the other waves idled.
+        const uint32_t E = K * (MF_D + 1);
+        uint32_t lp = 0;   // log2 P
+        while ((2u << lp) <= copies && (2u << lp) * E <= (uint32_t)(NW * 64) && lp < 6) lp++;
+        const uint32_t P = 1u << lp;
+        for (uint32_t b = 0; b < E * P; b += (NW * 64)) {   // uniform trips: every lane shuffles
+            const uint32_t i = b + tid, e = i >> lp, j = i & (P - 1);
             uint64_t v = 0;
-            for (uint32_t c = 0; c < copies; c++) v += cps[(size_t)c * S + d * SK + k];
-            if (d < MF_D) pdst[i] = v;
-            else cdst[k] = (uint32_t)v;
+            if (e < E) {
+                const uint32_t d = e / K, k = e - d * K;
+                for (uint32_t c = j; c < copies; c += P) v += cps[(size_t)c * S + d * SK + k];
+            }
+            for (uint32_t o = 1; o < P; o <<= 1) {
+                const uint32_t lo = (uint32_t)__shfl_xor((int)(uint32_t)v, (int)o);
+                const uint32_t hi = (uint32_t)__shfl_xor((int)(uint32_t)(v >> 32), (int)o);
+                v += ((uint64_t)hi << 32) | lo;
+            }
+            if (j == 0 && e < E) {
+                if (e < K * MF_D) pdst[e] = v;
+                else cdst[e - K * MF_D] = (uint32_t)v;
+            }
         }
     }
 }
