@@ -7,6 +7,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <immintrin.h>
 #include <limits>
@@ -702,6 +703,57 @@ __attribute__((target("avx2"))) int agg_row_avx2(const double *x, const double *
     }
     return d;
 }
+// A whole leaf into its aggregates, four dimensions at a time with the four running values in
+// registers over the leaf's points (one store per dimension block, no read-modify-write chain
+// through memory per point): returns the first dimension left to the scalar loop.
+__attribute__((target("avx2"))) int agg_leaf_avx2(const double *pts, const double *kpts, const uint8_t *known,
+                                                  const size_t *ind, size_t n, int D, int d0, int d1, double *mnu,
+                                                  double *mxu, double *mnk, double *mxk) {
+    const __m256d inf = _mm256_set1_pd(std::numeric_limits<double>::infinity()), ninf = _mm256_sub_pd(_mm256_setzero_pd(), inf);
+    for (size_t j = 0; j < n; j++) {   // every row of the leaf requested first (rows are scattered)
+        const size_t r = ind[j] * (size_t)D;
+        for (int o = d0; o < d1; o += 8) {
+            _mm_prefetch((const char *)(pts + r + o), _MM_HINT_T0);
+            _mm_prefetch((const char *)(kpts + r + o), _MM_HINT_T0);
+        }
+        _mm_prefetch((const char *)(known + r + d0), _MM_HINT_T0);
+    }
+    int d = d0;
+    for (; d + 4 <= d1; d += 4) {
+        __m256d a = inf, b = ninf, c = inf, e = ninf;
+        for (size_t j = 0; j < n; j++) {
+            const size_t r = ind[j] * (size_t)D + d;
+            int32_t kb;
+            std::memcpy(&kb, known + r, 4);
+            const __m256d m = _mm256_castsi256_pd(
+                _mm256_cmpgt_epi64(_mm256_cvtepu8_epi64(_mm_cvtsi32_si128(kb)), _mm256_setzero_si256()));
+            const __m256d xv = _mm256_loadu_pd(pts + r), kk = _mm256_loadu_pd(kpts + r);
+            a = _mm256_min_pd(a, _mm256_blendv_pd(xv, inf, m));
+            b = _mm256_max_pd(b, _mm256_blendv_pd(xv, ninf, m));
+            c = _mm256_min_pd(c, _mm256_blendv_pd(inf, kk, m));
+            e = _mm256_max_pd(e, _mm256_blendv_pd(ninf, kk, m));
+        }
+        _mm256_storeu_pd(mnu + d, a);
+        _mm256_storeu_pd(mxu + d, b);
+        _mm256_storeu_pd(mnk + d, c);
+        _mm256_storeu_pd(mxk + d, e);
+    }
+    return d;
+}
+// An inner node's aggregates from its children's (element-wise min / max of the two rows).
+__attribute__((target("avx2"))) void agg_inner_avx2(const double *b, const double *c, double *o, int D, int d0,
+                                                    int d1) {
+    for (int q = 0; q < 4; q++) {
+        const double *bq = b + q * D, *cq = c + q * D;
+        double *oq = o + q * D;
+        int d = d0;
+        for (; d + 4 <= d1; d += 4) {
+            const __m256d u = _mm256_loadu_pd(bq + d), v = _mm256_loadu_pd(cq + d);
+            _mm256_storeu_pd(oq + d, (q & 1) ? _mm256_max_pd(v, u) : _mm256_min_pd(v, u));
+        }
+        for (; d < d1; d++) oq[d] = (q & 1) ? (cq[d] > bq[d] ? cq[d] : bq[d]) : (cq[d] < bq[d] ? cq[d] : bq[d]);
+    }
+}
 }  // namespace
 
 void RefKDTree::cert_agg_node(size_t i) const { cert_agg_dims(i, 0, dim_); }
@@ -713,6 +765,27 @@ void RefKDTree::cert_agg_dims(size_t i, int d0, int d1) const {
     double *__restrict mnu = &agg_[i * D * 4], *__restrict mxu = mnu + D, *__restrict mnk = mxu + D,
                        *__restrict mxk = mnk + D;
     const Node &n = nodes_[i];
+    // (QVQ_AGG_ROWS=1: the leaf rows one at a time into the node's aggregates, A/B)
+    static const bool rows = std::getenv("QVQ_AGG_ROWS") && std::getenv("QVQ_AGG_ROWS")[0] == '1';
+    const bool avx2 = has_avx2() && !rows;
+    if (n.leaf && avx2) {
+        const int e = agg_leaf_avx2(pts_, agg_k_, agg_known_, vind_.data() + n.left, n.right - n.left, D, d0, d1, mnu,
+                                    mxu, mnk, mxk);
+        for (int d = e; d < d1; d++) {
+            mnu[d] = mnk[d] = INF, mxu[d] = mxk[d] = -INF;
+            for (size_t j = n.left; j < n.right; j++) {
+                const size_t r = vind_[j] * (size_t)D + d;
+                const bool kk = agg_known_[r] != 0;
+                const double x = pts_[r], kv = agg_k_[r];
+                const double xu_lo = kk ? INF : x, xu_hi = kk ? -INF : x, xk_lo = kk ? kv : INF, xk_hi = kk ? kv : -INF;
+                mnu[d] = mnu[d] < xu_lo ? mnu[d] : xu_lo;
+                mxu[d] = mxu[d] > xu_hi ? mxu[d] : xu_hi;
+                mnk[d] = mnk[d] < xk_lo ? mnk[d] : xk_lo;
+                mxk[d] = mxk[d] > xk_hi ? mxk[d] : xk_hi;
+            }
+        }
+        return;
+    }
     if (n.leaf) {
         for (int d = d0; d < d1; d++) mnu[d] = mnk[d] = INF, mxu[d] = mxk[d] = -INF;
         for (size_t j = n.left; j < n.right; j++) {
@@ -737,6 +810,10 @@ void RefKDTree::cert_agg_dims(size_t i, int d0, int d1) const {
         return;
     }
     const double *__restrict b = &agg_[(size_t)n.child1 * D * 4], *__restrict c = &agg_[(size_t)n.child2 * D * 4];
+    if (avx2) {
+        agg_inner_avx2(b, c, mnu, D, d0, d1);
+        return;
+    }
     for (int q = 0; q < 4; q++)   // [min unknown | max unknown | min known | max known]
         for (int d = d0; d < d1; d++) {
             const double u = b[q * D + d], v = c[q * D + d];
