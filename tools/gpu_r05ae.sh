@@ -1,0 +1,23 @@
+# Per-data-tile pruning windows (default) vs one window per chunk (QVQ_PRUNE_PER_TILE=0): the
+# GPU suite, C3 interleaved three times (20 steps, per-level search events), then the round's
+# record on the final tree (tools/gpu_bench.sh: bench.py default flags, kernel stats, PMC)
+set -o pipefail
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+O=$R/gpurun_out/r05ae
+mkdir -p $O
+cd $R
+timeout -k 10 600 python3 -u -m pytest tests -m gpu -x -v --timeout 200 --timeout-method thread > $O/gpu_tests.log 2>&1; rc=$?
+grep -E "passed|failed" $O/gpu_tests.log | tail -2
+[ $rc -ne 0 ] && exit $rc
+B="--steps 20 --warmup 3 --c4-steps 0 --c5-steps 0 --e2e-reps 0 --share-steps 0 --exact-reps 0 --no-cpu-baseline"
+run() {  # name env...
+  local n=$1; shift
+  env "$@" timeout -k 10 300 python3 bench.py $B > $O/$n.json 2> $O/$n.err || { tail -3 $O/$n.err; return 1; }
+  python3 -c "
+import json; d=json.loads(open('$O/$n.json').read().strip().splitlines()[-1]); p=d['roofline']['per_level']
+print('$n', 'C3', d['ms_per_step'], 'search us', [round(p[k]['avg_launch_ms']*1e3,1) for k in ['512','1024']])"
+}
+for i in 1 2 3; do
+run pertile_$i QVQ_X=0 && run chunk_$i QVQ_PRUNE_PER_TILE=0 || exit 1
+done
+bash tools/gpu_bench.sh r05ae_rec || exit $?
