@@ -1,0 +1,19 @@
+# C3 knob sweep on one box (env only): default vs pruning from K=256 with 8-code-vector units there
+# (QVQ_U4_MAXK=128 QVQ_PRUNE_MINK=256) vs the MFMA recheck from K=256 (QVQ_RECHECK_MF_MINK=256);
+# interleaved twice, 20 steps, per-level search events
+set -o pipefail
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+O=$R/gpurun_out/r05al
+mkdir -p $O
+cd $R
+B="--steps 20 --warmup 3 --c4-steps 0 --c5-steps 0 --e2e-reps 0 --share-steps 0 --exact-reps 0 --no-cpu-baseline"
+run() {  # name env...
+  local n=$1; shift
+  env "$@" timeout -k 10 300 python3 bench.py $B > $O/$n.json 2> $O/$n.err || { tail -3 $O/$n.err; return 1; }
+  python3 -c "
+import json; d=json.loads(open('$O/$n.json').read().strip().splitlines()[-1]); p=d['roofline']['per_level']
+print('$n', 'C3', d['ms_per_step'], 'search us', [round(p[k]['avg_launch_ms']*1e3,1) for k in ['128','256','512','1024']])"
+}
+for i in 1 2; do
+run def_$i QVQ_X=0 && run prune256_$i QVQ_U4_MAXK=128 QVQ_PRUNE_MINK=256 && run rc256_$i QVQ_RECHECK_MF_MINK=256 || exit 1
+done
