@@ -363,14 +363,14 @@ bool use_fused(const qvq_ctx *ctx, uint32_t K) {
     return use_mfma(ctx, K) && K <= mf_fuse_max_k() && !env_is("QVQ_FUSE", "0");
 }
 // Pruned MFMA search (k_mf32.hip PRUNE: tiles visited outward from a chunk's projection,
-// stopped by a provable bound) for D = 12 from K = QVQ_PRUNE_MINK (default 512; 0 = off) up to
+// stopped by a provable bound) for D = 12 from K = QVQ_PRUNE_MINK (default 256; 0 = off) up to
 // prune_order's capacity.  Its order is computed by the previous level's finalize.
 // Other D (assign_wide_kernel, streamed codebooks): from K = QVQ_WPRUNE_MINK (default 1024).
 // A codebook resident in LDS (small D) is searched unpruned unless QVQ_WPRUNE_MINK is set:
 // its per-wave windows measured no faster.
 // The D = 12 kernel keeps one tile envelope per lane: at most 64 tiles (K <= 2048).
 bool use_prune(const qvq_ctx *ctx, uint32_t K) {
-    static const uint32_t mink = std::getenv("QVQ_PRUNE_MINK") ? (uint32_t)std::atoi(std::getenv("QVQ_PRUNE_MINK")) : 512u;
+    static const uint32_t mink = std::getenv("QVQ_PRUNE_MINK") ? (uint32_t)std::atoi(std::getenv("QVQ_PRUNE_MINK")) : 256u;
     static const bool wset = std::getenv("QVQ_WPRUNE_MINK") != nullptr;
     static const uint32_t wmink = wset ? (uint32_t)std::atoi(std::getenv("QVQ_WPRUNE_MINK")) : 1024u;
     if (K > PRUNE_MAXK_HOST) return false;

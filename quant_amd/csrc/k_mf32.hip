@@ -743,9 +743,11 @@ hipError_t launch_assign_mf32(hipStream_t s, int grid, bool fuse, const uint8_t 
     if (fuse && K >= copies_mink && K <= copies_maxk)
         while (copies < 16 && m32_lds_layout(K, fuse, staged, copies * 2, prune).total <= M32_LDS_MAX) copies *= 2;
     const size_t lds = m32_lds_layout(K, fuse, staged, copies, prune).total;
-    // 4-code-vector units while the tile loop is short (the recompute dominates)
+    // 4-code-vector units while the tile loop is short (the recompute dominates); K = 256 takes
+    // 8-code-vector units, which the pruned search needs (QVQ_U4_MAXK=256 QVQ_PRUNE_MINK=512: the
+    // unpruned 4-unit search there, A/B: 129.2 / 123.4 vs 112.7 / 114.1 us, profiles/r05al)
     static const uint32_t u4_max =
-        std::getenv("QVQ_U4_MAXK") ? (uint32_t)std::atoi(std::getenv("QVQ_U4_MAXK")) : 256;
+        std::getenv("QVQ_U4_MAXK") ? (uint32_t)std::atoi(std::getenv("QVQ_U4_MAXK")) : 128;
     const bool u4 = K <= u4_max;
     // unit tags: ids t * NU + q < (Kp / 32) * NU per lane; QVQ_MF32_TAG=0 tracks them apart
     static const bool tag = !(std::getenv("QVQ_MF32_TAG") && std::getenv("QVQ_MF32_TAG")[0] == '0');
