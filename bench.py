@@ -44,6 +44,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 PEAK_F16_TFLOPS = 2500.0     # MI355X_MICROARCH.md: BF16/F16 MFMA ~2.5 PF dense (no sparsity)
+PEAK_F32_VALU_TFLOPS = 157.3  # MI355X_MICROARCH.md: FP32 vector peak (assign_small_kernel, K <= 32)
 PEAK_HBM_GBS = 8000.0
 PMC_SUMMARY = os.path.join(ROOT, "profiles", "pmc_hbm_latest.json")   # tools/pmc_summary.py output
 
@@ -319,28 +320,63 @@ def main():
     secs = sum(ms for _, ms in launches) * 1e-3
     achieved = flops / secs / 1e12
     avg_launch_s = secs / len(launches)
-    # per level (K): the largest K is the dominant launch of a quantize
+    # per level (K): the largest K is the dominant launch of a quantize.  Each level's search is
+    # priced against the peak of the unit it runs on: K <= 32 expanded fp32 scores on the VALU
+    # (assign_small_kernel), K >= 64 f16 MFMA tiles (assign_mf32_kernel); and against HBM with its
+    # algorithmic bytes (Dp bytes of codes in, a 4-byte index out per block)
+    Dp = (D + 3) & ~3
+    assign_bytes = n_local * (Dp + 4)
+    pmc = None
+    try:
+        pmc = json.load(open(PMC_SUMMARY))
+        if pmc.get("workload") != workload_key(args):
+            pmc = None
+    except (OSError, ValueError, KeyError):
+        pmc = None
+
+    def pmc_kernel(K):
+        """PMC HBM bytes per launch of level K's search kernel (tools/pmc_summary.py names)."""
+        if not pmc:
+            return None
+        if K <= 32:
+            name = "assign_small_kernel<%d,fused>" % K
+        elif K <= 128:
+            name = "assign_mf32_kernel<fused,staged,U4,tag>"
+        elif K <= 512:
+            name = "assign_mf32_kernel<fused,staged,U8,tag,prune>"
+        else:
+            name = "assign_mf32_kernel<fused,global,U8,tag,prune>"
+        v = pmc["kernels"].get(name)
+        return v["hbm_bytes"] if v else None
+
     by_k = {}
     for K, ms in launches:
         by_k.setdefault(K, []).append(ms)
-    per_level = {str(K): {"avg_launch_ms": round(sum(v) / len(v), 5),
-                          "TFLOPs": round(3.0 * K * D * n_local / (sum(v) / len(v) * 1e-3) / 1e12, 2),
-                          "frac": round(3.0 * K * D * n_local / (sum(v) / len(v) * 1e-3) / 1e12 / PEAK_F16_TFLOPS, 4)}
-                 for K, v in sorted(by_k.items())}
-    # its HBM view: codes in (Dp bytes per block) + index out (4 bytes per block)
-    assign_bytes = n_local * (((D + 3) & ~3) + 4)
-    traffic, traffic_src = None, None
-    try:
-        pmc = json.load(open(PMC_SUMMARY))
-        # every search launch (assign_mf32_kernel<...> and assign_small_kernel<...>, whatever
-        # the name's prefix), weighted by launches
-        ks = [v for k, v in pmc["kernels"].items() if "assign_" in k]
-        if ks and pmc.get("workload") == workload_key(args):
-            tot = sum(v["hbm_bytes"] * v["launches"] for v in ks)
-            traffic = round(tot / sum(v["launches"] for v in ks))
-            traffic_src = os.path.relpath(PMC_SUMMARY, ROOT)
-    except (OSError, ValueError, KeyError):
-        pass
+    per_level = {}
+    for K, v in sorted(by_k.items()):
+        t = sum(v) / len(v) * 1e-3
+        tf = 3.0 * K * D * n_local / t / 1e12
+        valu = K <= 32
+        peak = PEAK_F32_VALU_TFLOPS if valu else PEAK_F16_TFLOPS
+        gbs = assign_bytes / t / 1e9
+        per_level[str(K)] = {"avg_launch_ms": round(t * 1e3, 5), "TFLOPs": round(tf, 2),
+                             "unit_peak": "fp32 VALU %.1f TF" % peak if valu else "f16 MFMA dense %.0f TF" % peak,
+                             "frac": round(tf / peak, 4),
+                             "hbm_GBps": round(gbs, 1), "hbm_frac": round(gbs / PEAK_HBM_GBS, 4),
+                             "traffic": pmc_kernel(K)}
+    Kdom = max(by_k)
+    dom = per_level[str(Kdom)]
+    traffic = dom["traffic"]
+    traffic_src = os.path.relpath(PMC_SUMMARY, ROOT) if traffic is not None else None
+    # the mean (once per quantize, HBM-bound: Dp bytes per block) with events around it alone
+    mean_ms = []
+    eng.set_timing(-3)
+    for _ in range(5):
+        eng.lbg(args.bits, want_assign=False, out=out)
+        mean_ms.append(eng.timings()["mean_ms"])
+    eng.set_timing(-2)
+    mean_t = sum(mean_ms) / len(mean_ms) * 1e-3
+    mean_gbs = n_local * Dp / mean_t / 1e9
     upd_secs = sum(update_ms) * 1e-3
     upd_bytes = len(update_ms) * n_local * (((D + 3) & ~3) + 4)
     result = {
@@ -362,20 +398,22 @@ def main():
                                                                          args.block, D, 1 << args.bits, ipr),
                    "blocks_per_rank": n_local, "levels": levels, "parallelism": "dp%d" % world},
         "lbg_iters_per_s": round(levels * args.steps / elapsed, 3),
-        "roofline": {"bound": "mfma", "kernel": "search: qvq::assign_mf32_kernel (v_mfma_f32_32x32x16_f16, K >= 64) / "
-                                                 "qvq::assign_small_kernel (expanded fp32, K <= 32), fused sums",
-                     "achieved": round(achieved, 3), "peak": PEAK_F16_TFLOPS, "unit": "TFLOP/s",
-                     "frac": round(achieved / PEAK_F16_TFLOPS, 4), "traffic": traffic,
-                     "traffic_source": traffic_src, "avg_launch_ms": round(avg_launch_s * 1e3, 5),
-                     "launches": len(launches), "flop_per_block": "3*K*D",
-                     "timing": "HIP events around one level's search per quantize, levels in rotation, in quantizes after the timed steps",
+        # the dominant kernel: the largest level's search (K = 1024 at C3), one launch per quantize
+        "roofline": {"bound": "mfma", "kernel": "qvq::assign_mf32_kernel (v_mfma_f32_32x32x16_f16, pruned, fused "
+                                                 "exact sums), the K=%d level's search" % Kdom,
+                     "achieved": dom["TFLOPs"], "peak": PEAK_F16_TFLOPS, "unit": "TFLOP/s",
+                     "frac": dom["frac"], "traffic": traffic, "traffic_source": traffic_src,
+                     "algorithmic_bytes": assign_bytes, "avg_launch_ms": dom["avg_launch_ms"],
+                     "flop_per_block": "3*K*D", "flop_per_launch": 3 * Kdom * D * n_local,
+                     "timing": "HIP events around one level's search per quantize, levels in rotation, in quantizes "
+                               "after the timed steps",
                      "per_level": per_level,
-                     # the single dominant launch: the largest K's search (the headline frac above
-                     # averages every level's launches)
-                     "dominant": dict(K=max(by_k), **per_level[str(max(by_k))]),
-                     "hbm_view": {"algorithmic_bytes_per_launch": assign_bytes,
-                                  "achieved_GBps": round(assign_bytes / avg_launch_s / 1e9, 1),
-                                  "peak_GBps": PEAK_HBM_GBS}},
+                     # every level's search launches together (the mix a quantize runs)
+                     "all_levels": {"achieved": round(achieved, 3), "frac_of_f16_peak": round(achieved / PEAK_F16_TFLOPS, 4),
+                                    "avg_launch_ms": round(avg_launch_s * 1e3, 5), "launches": len(launches)},
+                     "mean_kernel": {"avg_launch_ms": round(mean_t * 1e3, 5), "algorithmic_bytes": n_local * Dp,
+                                     "hbm_GBps": round(mean_gbs, 1), "hbm_frac": round(mean_gbs / PEAK_HBM_GBS, 4)},
+                     "hbm_peak_GBps": PEAK_HBM_GBS},
         "update_kernel": ({"avg_launch_ms": round(upd_secs * 1e3 / max(1, len(update_ms)), 5),
                            "achieved_GBps": round(upd_bytes / upd_secs / 1e9, 1), "peak_GBps": PEAK_HBM_GBS}
                           if upd_secs else "fused into the search (LDS u64 atomics of exact integer terms)"),

@@ -68,6 +68,7 @@ typedef struct {
     int tie_overflow;           /* levels whose tie rows exceeded the check's export (each forces the redo) */
     int kahan_relays;           /* several ranks: levels whose tie rows needed cells summed over every
                                    rank's rows (the chained Kahan sums at the end of the call) */
+    double mean_ms;             /* device time of the mean kernel (qvq_set_timing(-3) only) */
 } qvq_timings;
 
 /* Context: one per GPU per host thread.  Owns device memory and one HIP stream. */
@@ -201,8 +202,9 @@ QVQ_API qvq_status qvq_comm_info(const qvq_ctx *ctx, int *nranks, int *rank, int
 QVQ_API qvq_status qvq_set_timeout(qvq_ctx *ctx, double seconds);
 
 /* Which levels get HIP events around their search kernel (each event record idles the GPU
- * ~6 us: every level costs ~10 % of a C3 quantize): -1 every level, -2 none (default), n >= 0
- * level n+1 only.  Unmeasured levels report 0 in qvq_get_timings. */
+ * ~6 us: every level costs ~10 % of a C3 quantize): -1 every level, -2 none (default), -3 the
+ * mean kernel only (mean_ms), n >= 0 level n+1 only.  Unmeasured levels report 0 in
+ * qvq_get_timings. */
 QVQ_API qvq_status qvq_set_timing(qvq_ctx *ctx, int level);
 QVQ_API qvq_status qvq_get_timings(const qvq_ctx *ctx, qvq_timings *out);
 

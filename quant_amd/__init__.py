@@ -34,7 +34,7 @@ class _Timings(ctypes.Structure):
                 ("other_ms", ctypes.c_double * 32), ("flagged", ctypes.c_uint64 * 32),
                 ("host_ties", ctypes.c_uint64 * 32), ("wait_ms", ctypes.c_double * 32),
                 ("tree_ms", ctypes.c_double * 32), ("kahan_redo", ctypes.c_int), ("tie_overflow", ctypes.c_int),
-                ("kahan_relays", ctypes.c_int)]
+                ("kahan_relays", ctypes.c_int), ("mean_ms", ctypes.c_double)]
 
 
 _lib = None
@@ -254,7 +254,8 @@ class Engine:
                 "other_ms": list(t.other_ms[:max(L, 1)]),
                 "flagged": list(t.flagged[:max(L, 1)]), "host_ties": list(t.host_ties[:max(L, 1)]),
                 "wait_ms": list(t.wait_ms[:max(L, 1)]), "tree_ms": list(t.tree_ms[:max(L, 1)]),
-                "kahan_redo": t.kahan_redo, "tie_overflow": t.tie_overflow, "kahan_relays": t.kahan_relays}
+                "kahan_redo": t.kahan_redo, "tie_overflow": t.tie_overflow, "kahan_relays": t.kahan_relays,
+                "mean_ms": t.mean_ms}
 
     # -- multi-GPU -----------------------------------------------------------------------
     def decode(self, cb_bytes, A, xSize, ySize, bw, bh):

@@ -87,6 +87,22 @@ size_t floor_log2(size_t n) {   // smallestPow2, src/Compressor.cpp:167-172
 
 bool engine_sums_exactly(ColorSpaces cs) { return cs == ColorSpaces::NORMAL || cs == ColorSpaces::SCALED; }
 
+// The SCALED byte of one centroid component (ScaledColor::colorSpaceToRGB, src/ColorSpace.cpp:23-28).
+int scaled_byte(double c) { return (int)std::round((c - 128.0) * 255); }
+
+// True when some component c has another byte within FLIP_ULPS ulps: the exact-sum and Kahan
+// centroids of a cell differ by at most a few ulps (both sums of nonnegative values: the exact
+// one is rounded once, Kahan's error is <= 2u of the sum plus O(n u^2) of it), so outside that
+// window both give the same byte.
+bool codebook_near_byte_flip(const std::vector<double> &C) {
+    constexpr double FLIP_ULPS = 16;
+    for (double c : C) {
+        const double w = FLIP_ULPS * (std::nextafter(std::fabs(c), INFINITY) - std::fabs(c));
+        if (scaled_byte(c - w) != scaled_byte(c + w)) return true;
+    }
+    return false;
+}
+
 // The image's blocks trained on the engine straight from the raster (device tiling).
 std::tuple<std::vector<Vector>, std::vector<size_t>, VectorType> quantize_raster(const RGBImage &image,
                                                                                  ColorSpaces cs, int bw, int bh,
@@ -101,6 +117,14 @@ std::tuple<std::vector<Vector>, std::vector<size_t>, VectorType> quantize_raster
     std::vector<uint32_t> A(N);
     double distortion = 0;
     EngineHandle::check(qvq_lbg(ctx, (uint32_t)n, eps, C.data(), A.data(), &distortion), "qvq_lbg");
+    // qvq_lbg returns exact-sum centroids; the reference's are Kahan sums (src/Quantizer.cpp:59-87),
+    // at most a few ulps away.  Only a component within a few ulps of a point where
+    // round((c - 128) * 255) changes can turn into another byte (src/ColorSpace.cpp:23-28), so the
+    // reference's bits are fetched when any component sits that close (SCALED only: NORMAL values
+    // are integers, whose Kahan sums are exact).
+    if (cs == ColorSpaces::SCALED && codebook_near_byte_flip(C)) {
+        EngineHandle::check(qvq_update_kahan(ctx, A.data(), (uint32_t)K, C.data()), "qvq_update_kahan");
+    }
     std::vector<Vector> codebook(K, Vector(D));
     for (size_t k = 0; k < K; k++) std::copy(C.begin() + k * D, C.begin() + (k + 1) * D, codebook[k].begin());
     return std::make_tuple(std::move(codebook), std::vector<size_t>(A.begin(), A.end()), distortion);

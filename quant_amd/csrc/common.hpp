@@ -211,7 +211,6 @@ struct MfThresholds {
     float mfma, alpha, beta, gamma;
     float inv_scale;   // 2^-t
     float mu, sx;      // x = mu + w * sx
-    uint32_t runs_max_k;   // fused sums: wave run reduction up to this K, plain LDS atomics above
     // small-K scan (expanded fp32 scores): flag when second - best <= e0 + e1 * sum_d |w_d|
     float e0, e1;
     // the mfma bound for one row (k_mf32.hip): m0 + m1 * sum_d |w_d| <= mfma

@@ -99,6 +99,36 @@ struct CertState {
 };
 }  // namespace qvq
 
+// QVQ_HOST_TRACE=1: a host timeline of each qvq_lbg (us since its start, per thread), printed
+// to stderr at its end: the main thread's tree builds and enqueues, the checks' start, export
+// and end (diagnostics for where a quantize waits).  One per context: the checks of a context
+// mark it from its worker thread while the calling thread does.
+struct HostTrace {
+    std::atomic<bool> on{false};
+    std::chrono::steady_clock::time_point t0;
+    std::mutex m;
+    std::vector<std::pair<double, std::string>> ev;
+    void start(std::chrono::steady_clock::time_point t) {
+        std::lock_guard<std::mutex> g(m);
+        t0 = t;
+        ev.clear();
+        on.store(true, std::memory_order_release);
+    }
+    void mark(const std::string &what) {
+        if (!on.load(std::memory_order_acquire)) return;
+        std::lock_guard<std::mutex> g(m);
+        const double t = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
+        ev.emplace_back(t, what);
+    }
+    std::string finish() {
+        std::lock_guard<std::mutex> g(m);
+        on.store(false, std::memory_order_release);
+        std::string out = "qvq host trace:";
+        for (const auto &e : ev) out += "\n  " + std::to_string((int)e.first) + " " + e.second;
+        return out;
+    }
+};
+
 struct qvq_ctx {
     int dev = 0;
     int num_cu = 256;
@@ -130,16 +160,6 @@ struct qvq_ctx {
     // the reference-bit (Kahan) centroids a level with kd-tree ties needs
     uint32_t *d_A_alt = nullptr;
     KahanWork kw;
-    // the whole reference-bit split of a 48-D level, computed on the main stream while the host
-    // builds the level's tree (full_split_level): its own workspace (the checks' cells use kw on
-    // the side stream meanwhile), the split into mapped memory by level parity, h_ready[4] its
-    // ready number
-    KahanWork kw_full;
-    double *d_kf_cent = nullptr, *h_kf_out = nullptr, *dh_kf_out = nullptr;
-    uint32_t kf_kcap = 0;
-    uint64_t kf_seq = 0;
-    bool want_full = false;        // qvq_lbg: the level may take it (speculative, one rank)
-    uint64_t kf_level_seq = 0;     // run_level: this level's ready number (0: none)
     double *d_kc_cent = nullptr, *d_kc_split = nullptr;   // Kahan centroids [K/2][D], their split [K][D]
     uint32_t kc_kcap = 0;
     std::vector<double> h_kc_split;   // host copy of the split for the tree build
@@ -202,7 +222,7 @@ struct qvq_ctx {
         std::deque<std::function<void()>> q;
         bool stop = false;
         std::atomic<int> pending{0};
-    } worker, prep;   // prep: each level's tie certificate prepared while the GPU runs the level
+    } worker;
     // helpers of the worker for the certificate's replays (persistent: their per-thread replay
     // caches stay warm); pool_run forks fn over them and the calling thread
     struct Pool {
@@ -226,14 +246,12 @@ struct qvq_ctx {
         std::atomic<bool> done{true}, cancel{false};
         int status = 0;   // 0: the reference's indices are the speculative ones; 1: not shown; 2: deferred
         uint32_t K = 0, level = 0;
-        std::atomic<bool> prep_done{true};   // cs prepared (cert_init on the prep worker)
         uint64_t seq = 0;
         int par = 0;
         const uint32_t *A_prev = nullptr;
         std::unique_ptr<RefKDTree> tree;
         std::vector<double> cb;
         std::vector<uint32_t> cnt;   // the parent cells' row counts (empty: not known)
-        uint64_t full_seq = 0;       // the whole reference-bit split (ready number; 0: none)
         CertState cs;
         hipEvent_t ev = nullptr;
     } ver[3];   // level % 3
@@ -254,9 +272,6 @@ struct qvq_ctx {
     uint64_t *d_kc_chain = nullptr;   // chained Kahan sums: gather | state (k_kahan.hip)
     uint64_t kc_chain_cap = 0;
     std::atomic<bool> tree_cancel{false};
-    // the main thread is building a level's kd-tree (on the critical path: the GPU waits for it);
-    // the checks then replay on their own thread only (cert_helpers)
-    std::atomic<bool> tree_building{false};
     bool tree_job = false, job_ok = false;
     int job_buf = 0;
     KdView job_kd;
@@ -291,6 +306,7 @@ struct qvq_ctx {
     uint64_t stage_bytes = 0;
 
     qvq_timings tm;
+    HostTrace htrace;
     hipEvent_t ev[32][4];
     bool ev_ready = false;
 };
@@ -336,48 +352,37 @@ void dfree(T *&p) {
 uint32_t pad32(uint32_t K) { return (K + 31) & ~31u; }   // MFMA tile pairs
 bool kahan_mode(const qvq_ctx *ctx);
 double tie_band(const qvq_ctx *ctx);
-// QVQ_SEARCH=valu, QVQ_FUSE=0 and QVQ_KDTREE=host select paths for ablations and tests.
+// The path knobs a test exercises: QVQ_SEARCH=valu (the VALU search at every K) and
+// QVQ_KDTREE=host (ties answered on the host); QVQ_KAHAN=0 / QVQ_SPECULATE=0 (index rule and
+// schedule); QVQ_KAHAN_FAIL_LEVEL / _RANK (forced check failures).
 bool env_is(const char *name, const char *val) {
     const char *v = std::getenv(name);
     return v && std::strcmp(v, val) == 0;
 }
-// Timing ablation only (results are wrong with it): QVQ_ABL_SKIP bit 1 drops the recheck,
-// bit 2 the kd-tree launch, bit 4 the reduce -- the marginal cost of each per-level launch.
-uint32_t abl_skip() {
-    static const uint32_t v = std::getenv("QVQ_ABL_SKIP") ? (uint32_t)std::atoi(std::getenv("QVQ_ABL_SKIP")) : 0u;
-    return v;
-}
 bool use_mfma(const qvq_ctx *ctx, uint32_t K) {
     return ctx->D == MF_D && mf_can_search(K) && !env_is("QVQ_SEARCH", "valu");
 }
-// MFMA search for D != 12 from K = QVQ_WIDE_MIN_K (default 128) code vectors up: below it the
-// VALU search wins (C4, D = 48: 82 vs 182 us at K = 32, 154 vs 187 at K = 64; tools/c4_ab.sh).
+// MFMA search for D != 12 from K = 128 code vectors up: below it the VALU search wins (C4,
+// D = 48: 82 vs 182 us at K = 32, 154 vs 187 at K = 64; from K = 64 or 32 the C4 levels ran
+// slower, profiles/r05ak).
+constexpr uint32_t WIDE_MIN_K = 128;
 bool use_wide(const qvq_ctx *ctx, uint32_t K) {
-    static const uint32_t min_k = [] {
-        const char *e = std::getenv("QVQ_WIDE_MIN_K");
-        return e ? (uint32_t)std::max(1, std::atoi(e)) : 128u;
-    }();
-    return ctx->D != MF_D && wide_can_search(ctx->Dp) && K >= min_k && !env_is("QVQ_SEARCH", "valu");
+    return ctx->D != MF_D && wide_can_search(ctx->Dp) && K >= WIDE_MIN_K && !env_is("QVQ_SEARCH", "valu");
 }
-bool use_fused(const qvq_ctx *ctx, uint32_t K) {
-    return use_mfma(ctx, K) && K <= mf_fuse_max_k() && !env_is("QVQ_FUSE", "0");
-}
-// Pruned MFMA search (k_mf32.hip PRUNE: tiles visited outward from a chunk's projection,
-// stopped by a provable bound) for D = 12 from K = QVQ_PRUNE_MINK (default 256; 0 = off) up to
-// prune_order's capacity.  Its order is computed by the previous level's finalize.
-// Other D (assign_wide_kernel, streamed codebooks): from K = QVQ_WPRUNE_MINK (default 1024).
-// A codebook resident in LDS (small D) is searched unpruned unless QVQ_WPRUNE_MINK is set:
-// its per-wave windows measured no faster.
+bool use_fused(const qvq_ctx *ctx, uint32_t K) { return use_mfma(ctx, K) && K <= mf_fuse_max_k(); }
+// Pruned MFMA search (k_mf32.hip PRUNE: tiles outside a chunk's provable window skipped) for
+// D = 12 from K = 256 (from K = 128 it measured slower, profiles/r05ao) up to prune_order's
+// capacity.  Its order is computed by the previous level's finalize.  Other D
+// (assign_wide_kernel, streamed codebooks): from K = 1024; a codebook resident in LDS (small D)
+// is searched unpruned: its per-wave windows measured no faster.
 // The D = 12 kernel keeps one tile envelope per lane: at most 64 tiles (K <= 2048).
+constexpr uint32_t PRUNE_MIN_K = 256, WPRUNE_MIN_K = 1024;
 bool use_prune(const qvq_ctx *ctx, uint32_t K) {
-    static const uint32_t mink = std::getenv("QVQ_PRUNE_MINK") ? (uint32_t)std::atoi(std::getenv("QVQ_PRUNE_MINK")) : 256u;
-    static const bool wset = std::getenv("QVQ_WPRUNE_MINK") != nullptr;
-    static const uint32_t wmink = wset ? (uint32_t)std::atoi(std::getenv("QVQ_WPRUNE_MINK")) : 1024u;
     if (K > PRUNE_MAXK_HOST) return false;
     if (ctx->D == MF_D)
-        return mink && K >= mink && K <= 2048 && use_mfma(ctx, K) && mf32_prune_fits(K, use_fused(ctx, K));
-    if (!wset && wide_codebook_resident(ctx->Dp, K)) return false;
-    return wmink && K >= wmink && use_wide(ctx, K) && wide_prune_fits(ctx->Dp, K);
+        return K >= PRUNE_MIN_K && K <= 2048 && use_mfma(ctx, K) && mf32_prune_fits(K, use_fused(ctx, K));
+    if (wide_codebook_resident(ctx->Dp, K)) return false;
+    return K >= WPRUNE_MIN_K && use_wide(ctx, K) && wide_prune_fits(ctx->Dp, K);
 }
 
 void free_kahan_work(KahanWork &w) {
@@ -392,11 +397,6 @@ void free_kahan_work(KahanWork &w) {
 
 void free_kahan(qvq_ctx *ctx) {
     free_kahan_work(ctx->kw);
-    free_kahan_work(ctx->kw_full);
-    dfree(ctx->d_kf_cent);
-    if (ctx->h_kf_out) (void)hipHostFree(ctx->h_kf_out);
-    ctx->h_kf_out = ctx->dh_kf_out = nullptr;
-    ctx->kf_kcap = 0;
     dfree(ctx->d_kc_chain);
     ctx->kc_chain_cap = 0;
     dfree(ctx->d_kc_cent);
@@ -523,10 +523,6 @@ void mfma_setup(qvq_ctx *ctx) {
     ctx->mf_th.e1 = (float)(ks * c2_max * sc * 1.0001);
     ctx->mf_th.mu = (float)t.mu;
     ctx->mf_th.sx = (float)t.sx;
-    {
-        const char *e = std::getenv("QVQ_RUNS_MAXK");   // ablation
-        ctx->mf_th.runs_max_k = e ? (uint32_t)std::atoi(e) : 1u << 30;
-    }
 }
 
 // Allocate the per-row buffers and upload the colour-space tables.
@@ -657,12 +653,9 @@ qvq_status all_reduce_sums(qvq_ctx *ctx, uint32_t K, uint64_t *sums = nullptr, u
 }
 
 // Sums of a final assignment through the counting sort (k_misc.hip) from K * D = 1536 (C4 from
-// K = 32: 5.52 -> 5.23 ms against 16384; QVQ_SORTED_MIN_KD, QVQ_SORTED_SUMS=0: A/B).
+// K = 32: 5.52 -> 5.23 ms against 16384).
 bool use_sorted_sums(const qvq_ctx *ctx, uint32_t K) {
-    static const bool on = !env_is("QVQ_SORTED_SUMS", "0");
-    static const uint64_t min_kd =
-        std::getenv("QVQ_SORTED_MIN_KD") ? (uint64_t)std::atoll(std::getenv("QVQ_SORTED_MIN_KD")) : 1536;
-    return on && (uint64_t)K * ctx->D >= min_kd && sorted_sums_fits(K) && ctx->N <= 0xFFFFFFFFull;
+    return (uint64_t)K * ctx->D >= 1536 && sorted_sums_fits(K) && ctx->N <= 0xFFFFFFFFull;
 }
 
 // Centroid sums under assignment d_A: slabs in d_part (ctx->nslabs of them, for the reduce),
@@ -760,20 +753,6 @@ qvq_status alloc_kahan_work(qvq_ctx *ctx, KahanWork &w, uint32_t Kc) {
     return QVQ_OK;
 }
 
-qvq_status ensure_kahan_full(qvq_ctx *ctx, uint32_t Kc) {
-    if (ctx->kf_kcap < Kc) {
-        dfree(ctx->d_kf_cent);
-        if (ctx->h_kf_out) (void)hipHostFree(ctx->h_kf_out);
-        ctx->h_kf_out = ctx->dh_kf_out = nullptr;
-        ctx->kf_kcap = 0;
-        HIPCHK(hipMalloc(&ctx->d_kf_cent, (uint64_t)Kc * ctx->D * 8));
-        HIPCHK(hipHostMalloc(reinterpret_cast<void **>(&ctx->h_kf_out), 2 * 2ull * Kc * ctx->D * 8,
-                             hipHostMallocMapped | hipHostMallocCoherent));
-        HIPCHK(hipHostGetDevicePointer(reinterpret_cast<void **>(&ctx->dh_kf_out), ctx->h_kf_out, 0));
-        ctx->kf_kcap = Kc;
-    }
-    return alloc_kahan_work(ctx, ctx->kw_full, Kc);
-}
 
 // Sum over the ranks of n small u64 values (host, in place) on the context's stream, waiting for
 // the result: the ranks' decisions at the end of qvq_lbg, so that every rank takes the same
@@ -867,30 +846,20 @@ bool join_tree_job(qvq_ctx *ctx, bool cancel);
 // Build the reference kd-tree over the host copy hC of the K code vectors being searched
 // into tree image buffer buf (pinned host memory, DMA-copied to d_tree for kd_resolve_kernel).  An empty
 // view means host resolution (tree too deep/large for the kernel's LDS, or QVQ_KDTREE=host).
-// QVQ_HOST_TRACE=1: a host timeline of each qvq_lbg (us since its start, per thread),
-// printed to stderr at its end: the main thread's tree builds and enqueues, the checks' start,
-// export and end (diagnostics for where a quantize waits).
-struct HostTrace {
-    bool on = false;
-    std::chrono::steady_clock::time_point t0;
-    std::mutex m;
-    std::vector<std::pair<double, std::string>> ev;
-    void mark(const std::string &what) {
-        if (!on) return;
-        const double t = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
-        std::lock_guard<std::mutex> g(m);
-        ev.emplace_back(t, what);
-    }
-};
-HostTrace g_htrace;
 
 // Level L's split codebook as the finalize of level L - 1 publishes it (host / device view).
 // Double-buffered by level parity: the synchronous Kahan levels build a level's tree on the
 // worker from this copy while the level's own finalize already publishes the next level's
 // codebook (one buffer: a worker late by more than the level's search read a mix of the two,
 // the r05i-r05m intermittent mismatches on palette images).
-double *host_cb_of(const qvq_ctx *ctx, uint32_t level) { return ctx->h_cb + (uint64_t)(level & 1) * ctx->cb_half; }
-double *dev_cb_of(const qvq_ctx *ctx, uint32_t level) { return ctx->dh_cb + (uint64_t)(level & 1) * ctx->cb_half; }
+// QVQ_CB_SINGLE=1 (tests only): the one buffer of before the fix, which with
+// QVQ_TREE_JOB_DELAY_MS makes the race deterministic (tests/test_gpu_kahan.py).
+uint32_t cb_half_of(uint32_t level) {
+    static const bool single = env_is("QVQ_CB_SINGLE", "1");
+    return single ? 0u : (level & 1);
+}
+double *host_cb_of(const qvq_ctx *ctx, uint32_t level) { return ctx->h_cb + (uint64_t)cb_half_of(level) * ctx->cb_half; }
+double *dev_cb_of(const qvq_ctx *ctx, uint32_t level) { return ctx->dh_cb + (uint64_t)cb_half_of(level) * ctx->cb_half; }
 
 // The host part: the tree (ctx->tree over ctx->cb_local) and its flattened image in h_tree[buf];
 // v.bytes = 0 when there is no device image (too large, or too deep for the kernel's LDS).
@@ -937,8 +906,7 @@ void tree_view(qvq_ctx *ctx, int buf, KdView &v) {
     }
     const uint32_t D = ctx->D;
     const double *dlo = reinterpret_cast<const double *>(ctx->dh_tree[buf]);
-    static const uint64_t dma_min = std::getenv("QVQ_TREE_DMA_MIN") ? std::atoll(std::getenv("QVQ_TREE_DMA_MIN"))
-                                                                      : 32768;   // ablation
+    constexpr uint64_t dma_min = 32768;
     if (v.bytes > dma_min) {
         if (hipMemcpyAsync(ctx->d_tree, ctx->h_tree[buf], v.bytes, hipMemcpyHostToDevice, ctx->stream) != hipSuccess) {
             v = KdView{};
@@ -1006,6 +974,10 @@ void start_tree_job(qvq_ctx *ctx, const double *hC, uint32_t K, int buf, uint64_
             cpu_relax();
         }
         std::atomic_thread_fence(std::memory_order_acquire);
+        // QVQ_TREE_JOB_DELAY_MS (tests only): a worker late past the level's own finalize, the
+        // interleaving of the r05m race (the finalize publishes the next level's codebook)
+        static const int delay_ms = std::getenv("QVQ_TREE_JOB_DELAY_MS") ? std::atoi(std::getenv("QVQ_TREE_JOB_DELAY_MS")) : 0;
+        if (delay_ms > 0) std::this_thread::sleep_for(std::chrono::milliseconds(delay_ms));
         const auto t1 = std::chrono::steady_clock::now();
         build_tree_host(ctx, hC, K, buf, ctx->job_kd, &ctx->tree_cancel);
         ctx->job_ok = !ctx->tree->cancelled();
@@ -1033,12 +1005,11 @@ bool join_tree_job(qvq_ctx *ctx, bool cancel) {
 // Copy between a caller's host buffer and device memory at DMA speed: the host range is pinned
 // in place for the copy (hipHostRegister; a pageable hipMemcpy goes through bounce buffers at a
 // fraction of PCIe bandwidth: the 50 MB C3 raster took ~3 ms), with a plain copy as the fallback
-// (already pinned memory, or registration refused).  QVQ_H2D=pageable: the plain copy (A/B).
+// (already pinned memory, or registration refused).
 // Synchronous on the context's stream.
 hipError_t host_copy(qvq_ctx *ctx, void *dst, const void *src, uint64_t bytes, hipMemcpyKind kind) {
-    static const bool pageable = env_is("QVQ_H2D", "pageable");
     void *host = const_cast<void *>(kind == hipMemcpyHostToDevice ? src : dst);
-    const bool reg = !pageable && bytes >= (1u << 20) && hipHostRegister(host, bytes, hipHostRegisterDefault) == hipSuccess;
+    const bool reg = bytes >= (1u << 20) && hipHostRegister(host, bytes, hipHostRegisterDefault) == hipSuccess;
     if (!reg) (void)hipGetLastError();
     hipError_t e = hipMemcpyAsync(dst, src, bytes, kind, ctx->stream);
     if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
@@ -1167,10 +1138,9 @@ qvq_status resolve_host_ties(qvq_ctx *ctx, const double *hC, uint32_t K, uint32_
 uint64_t sums_cap_stride(const qvq_ctx *ctx) { return 2 * (uint64_t)ctx->Kcap * ctx->D + ctx->Kcap; }
 
 // One rank, fused sums: the kd-tree ties go with the reduce (kd_reduce_kernel: one launch fewer
-// per level; QVQ_KD_REDUCE=0 keeps launch_kd_resolve + launch_reduce, A/B).
+// per level).
 bool kd_merge(const qvq_ctx *ctx) {
-    static const bool on = !env_is("QVQ_KD_REDUCE", "0");
-    return on && !ctx->comm && !ctx->host_ar && !(abl_skip() & 4);
+    return !ctx->comm && !ctx->host_ar;
 }
 
 qvq_status run_level(qvq_ctx *ctx, uint32_t K, int slot, bool sums_out, const double *hC, uint64_t wait_seq,
@@ -1215,15 +1185,9 @@ qvq_status run_level(qvq_ctx *ctx, uint32_t K, int slot, bool sums_out, const do
                                   ctx->d_lut32, alpha, beta, gamma, ctx->d_A, ctx->d_flags, &cnt[0]));
     }
     if (timing) HIPCHK(hipEventRecord(ctx->ev[slot][1], ctx->stream));
-    // the MFMA recheck from K = QVQ_RECHECK_MF_MINK (512; below it the fp32 pass over K code
-    // vectors is cheaper than staging the MFMA tables); QVQ_RECHECK=fp32 turns it off (A/B)
-    static const uint32_t rc_min_k = [] {
-        const char *v = std::getenv("QVQ_RECHECK_MF_MINK");
-        return v ? (uint32_t)std::atoi(v) : 512u;
-    }();
-    static const bool rc_mf32 = !env_is("QVQ_RECHECK", "fp32");
-    if (abl_skip() & 1) {
-    } else if (rc_mf32 && K >= rc_min_k && use_mfma(ctx, K) && recheck_mf32_fits(K)) {
+    // the MFMA recheck from K = 512 (below it the fp32 pass over K code vectors is cheaper than
+    // staging the MFMA tables, profiles/r02f)
+    if (K >= 512 && use_mfma(ctx, K) && recheck_mf32_fits(K)) {
         HIPCHK(launch_recheck_mf32(ctx->stream, ctx->num_cu, ctx->d_codes, ctx->d_flags, &cnt[0], ctx->d_rows,
                                    ctx->d_C64_split, K, ctx->d_lut64, ctx->mf_th, 1e-12, tie_band(ctx), ctx->d_A, ctx->d_ties,
                                    &cnt[1], xslab, xcnt, ctx->d_plut));
@@ -1257,31 +1221,6 @@ qvq_status run_level(qvq_ctx *ctx, uint32_t K, int slot, bool sums_out, const do
         ctx->nslabs = 0;   // reduced already
         HIPCHK(hipEventRecord(ctx->ev[slot][3], ctx->stream));
     }
-    // A 48-D level of a speculative quantize: the whole reference-bit split (the previous
-    // level's cells summed as the reference sums them) right behind the level's search, on the
-    // stream, where it runs while the GPU would wait for the host's tree build; the level's
-    // check then knows every code vector's bits (no blamed cells, no second replay).  C4's levels
-    // 11 and 12, off by default (QVQ_FULL_SPLIT=1: on, A/B): the whole split of 1,024 / 2,048
-    // cells over C4's 1M rows takes ~2.7 ms of device time, far longer than the tree build it was
-    // to hide behind, and the last check then waits for it (C4 11.5-11.9 ms vs 6.0-7.0 with the
-    // certificate's cells, profiles/r05ab).
-    ctx->kf_level_seq = 0;
-    static const bool full_on = env_is("QVQ_FULL_SPLIT", "1");
-    if (full_on && !defer_ties && ctx->want_full && K >= 4 && (uint64_t)K * ctx->D >= 65536 && ctx->d_A_alt &&
-        hC && ctx->nranks <= 1) {
-        if (wait_seq && (st = wait_codebook(ctx, wait_seq)) != QVQ_OK) return st;   // (the parent counts)
-        const uint32_t Kc = K / 2;
-        const uint32_t *pc = reinterpret_cast<const uint32_t *>(hC + (size_t)K * ctx->D);
-        uint64_t max_rows = 1;
-        for (uint32_t c = 0; c < Kc; c++) max_rows = std::max<uint64_t>(max_rows, pc[c]);
-        if ((st = ensure_kahan_full(ctx, Kc)) != QVQ_OK) return st;
-        double *out = ctx->dh_kf_out + (uint64_t)(slot & 1) * 2ull * Kc * ctx->D;
-        HIPCHK(launch_kahan_centroids(ctx->stream, ctx->kw_full, ctx->d_codes, ctx->Dp, ctx->D, ctx->N, ctx->d_A_alt,
-                                      Kc, ctx->d_kf_cent, out, nullptr, 0, max_rows));
-        ctx->kf_level_seq = ++ctx->kf_seq;
-        HIPCHK(launch_copy_out(ctx->stream, nullptr, nullptr, 0, nullptr, nullptr, 0, nullptr, nullptr, 0,
-                               ctx->dh_ready + 4, ctx->kf_level_seq, ctx->d_counters + 2 * 33 + 1));
-    }
     if (defer_ties) {   // qvq_lbg answers the ties after the finalize, if there are any (tree on the worker)
         start_tree_job(ctx, hC, K, slot & 1, wait_seq);
         ctx->upd[slot] = false;
@@ -1291,16 +1230,13 @@ qvq_status run_level(qvq_ctx *ctx, uint32_t K, int slot, bool sums_out, const do
     const auto tw0 = std::chrono::steady_clock::now();
     if (wait_seq && (st = wait_codebook(ctx, wait_seq)) != QVQ_OK) return st;
     const auto tw1 = std::chrono::steady_clock::now();
-    g_htrace.mark("K" + std::to_string(K) + " codebook seen, tree build");
+    ctx->htrace.mark("K" + std::to_string(K) + " codebook seen, tree build");
     KdView kd;
-    ctx->tree_building.store(true, std::memory_order_relaxed);
     build_tree(ctx, hC, K, slot & 1, kd);
-    ctx->tree_building.store(false, std::memory_order_relaxed);
-    g_htrace.mark("K" + std::to_string(K) + " tree built");
+    ctx->htrace.mark("K" + std::to_string(K) + " tree built");
     ctx->tm.wait_ms[slot] = std::chrono::duration<double, std::milli>(tw1 - tw0).count();
     ctx->tm.tree_ms[slot] = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tw1).count();
-    if (abl_skip() & 2) {
-    } else if (kd.depth > 0 && fused && kd_merge(ctx) && kd_reduce_fits(kd, K)) {
+    if (kd.depth > 0 && fused && kd_merge(ctx) && kd_reduce_fits(kd, K)) {
         ctx->kd_pend = true;   // with the reduce (qvq_lbg)
         ctx->pend_kd = kd;
         ctx->sums_copies = 2;
@@ -1334,11 +1270,9 @@ constexpr double KAHAN_DELTA = 0x1p-49;
 // cells of the points a collecting replay blames, and once more.  done = false, nothing
 // changed, when a row stays open: the caller then computes the whole split and its tree.
 uint32_t cert_threads();
-// The threads a check may use now: cert_threads(); with QVQ_CHECK_YIELD=1 (A/B) 1 while the
-// main thread builds a kd-tree (a check of level L runs beside the build of level L + 1's tree,
-// which its helpers slow: 1.7-1.8 vs 2.2-2.5 ms at C4's level 12, profiles/r05t-r05y; yet the
-// check then finishes later, and C4 took 6.88 ms yielding vs 6.52 not, profiles/r05z).
-uint32_t cert_helpers(const qvq_ctx *ctx);
+// The threads a check may use: cert_threads() (one while the main thread builds a kd-tree made
+// the builds faster but the checks later: C4 6.88 vs 6.52 ms, profiles/r05z).
+uint32_t cert_helpers(const qvq_ctx *) { return cert_threads(); }
 
 
 // QVQ_CERT_TRACE=1: the certificate's phases, us since the check saw its level's export
@@ -1652,16 +1586,9 @@ bool cert_mismatch(const CertState &cs, uint32_t K) {
     return false;
 }
 
-uint32_t cert_helpers(const qvq_ctx *ctx) {
-    static const bool yield = env_is("QVQ_CHECK_YIELD", "1");
-    return yield && ctx->tree_building.load(std::memory_order_relaxed) ? 1u : cert_threads();
-}
-
 // Host threads for the certificate's replays (at most 8, half the machine's).
 uint32_t cert_threads() {
     static const uint32_t n = [] {
-        const char *e = std::getenv("QVQ_CERT_THREADS");
-        if (e) return (uint32_t)std::max(1, std::atoi(e));
         // (C4 at 1 / 2 / 4 / 8 helpers is within the boxes' run-to-run spread, 6.8-7.6 ms:
         // profiles/r05s, r05u)
         return std::max<uint32_t>(1, std::min<uint32_t>(8, std::thread::hardware_concurrency() / 2));
@@ -1688,8 +1615,7 @@ uint32_t distinct_rows(const qvq_ctx *ctx, const uint8_t *code, size_t stride, u
 
 qvq_status certify_kahan_ties(qvq_ctx *ctx, uint32_t K, unsigned nt, uint64_t *target, bool &done) {
     done = false;
-    static const bool on = !env_is("QVQ_TIE_CERT", "0");
-    if (!on || !ctx->tree || ctx->cb_local.size() != (size_t)K * ctx->D || K < 2) return QVQ_OK;
+    if (!ctx->tree || ctx->cb_local.size() != (size_t)K * ctx->D || K < 2) return QVQ_OK;
     const uint32_t D = ctx->D, Dp = ctx->Dp;
     const uint64_t need = (uint64_t)nt * (4 + Dp);
     if (ctx->scatter_bytes < need) {
@@ -1738,51 +1664,27 @@ qvq_status certify_kahan_ties(qvq_ctx *ctx, uint32_t K, unsigned nt, uint64_t *t
 // every rank), exercising the redo.
 void verify_level(qvq_ctx *ctx, qvq_ctx::Verify &v) {
     v.status = 1;
-    g_htrace.mark("check K" + std::to_string(v.K) + " start");
+    ctx->htrace.mark("check K" + std::to_string(v.K) + " start");
     struct End {
+        qvq_ctx *c;
         const qvq_ctx::Verify &v;
-        ~End() { g_htrace.mark("check K" + std::to_string(v.K) + " end, status " + std::to_string(v.status)); }
-    } end_mark{v};
+        ~End() { c->htrace.mark("check K" + std::to_string(v.K) + " end, status " + std::to_string(v.status)); }
+    } end_mark{ctx, v};
     (void)hipSetDevice(ctx->dev);
-    // the known split and the tree's replay state were built on the prep worker while the GPU
-    // ran the level (qvq_lbg, after the level's tree)
-    while (!v.prep_done.load(std::memory_order_acquire)) {
-        if (v.cancel.load(std::memory_order_relaxed)) return;
-        cpu_relax();
-    }
     // the check usually starts while the GPU still runs its level (the last level's check is
     // then all that is left of the call): the known split and the tree's aggregates before the
     // export arrives, and for short searches (D = 12: a few hundred nodes) every node's split
     // replay too (C3: the last level's 2 tie rows took ~95 us after the export, r05i)
-    static const bool early = !env_is("QVQ_CERT_EARLY", "0");   // A/B
-    if (v.full_seq && !v.cs.prepared && v.tree && !v.tree->cancelled() && v.cb.size() == (size_t)v.K * ctx->D) {
-        // the whole reference-bit split (run_level): every code vector known
-        volatile uint64_t *ff = ctx->h_ready + 4;
-        while (*ff < v.full_seq) {
-            if (v.cancel.load(std::memory_order_relaxed)) return;
-            cpu_relax();
-        }
-        std::atomic_thread_fence(std::memory_order_acquire);
-        const size_t KD = (size_t)v.K * ctx->D;
-        const double *split = ctx->h_kf_out + (size_t)((v.level - 1) & 1) * KD;
-        v.cs.kp.assign(split, split + KD);
-        v.cs.known.assign(KD, 1);
-        v.tree->cert_clear();
-        v.cs.prepared = true;
-        g_htrace.mark("check K" + std::to_string(v.K) + " whole split in");
-        v.tree->cert_warm(KAHAN_DELTA, v.cs.kp.data(), v.cs.known.data(), cert_helpers(ctx),
-                          [ctx](unsigned n, const std::function<void(unsigned)> &fn) { pool_run(ctx, n, fn); });
-        g_htrace.mark("check K" + std::to_string(v.K) + " aggregates set");
-    }
-    if (early && !v.cs.prepared && v.tree && !v.tree->cancelled() && v.K >= 2 &&
+    // (C3 1.241 -> 1.197 ms, C4 7.51 -> 7.18, profiles/r05p)
+    if (!v.cs.prepared && v.tree && !v.tree->cancelled() && v.K >= 2 &&
         v.cb.size() == (size_t)v.K * ctx->D) {
         const bool full = (uint64_t)v.K * ctx->D < 65536;
         cert_init(*v.tree, v.cs, v.cb.data(), v.cnt, v.K, ctx->D, full, ctx);
-        g_htrace.mark("check K" + std::to_string(v.K) + " known split set");
+        ctx->htrace.mark("check K" + std::to_string(v.K) + " known split set");
         if (!full)
             v.tree->cert_warm(KAHAN_DELTA, v.cs.kp.data(), v.cs.known.data(), cert_helpers(ctx),
                               [ctx](unsigned n, const std::function<void(unsigned)> &fn) { pool_run(ctx, n, fn); });
-        g_htrace.mark("check K" + std::to_string(v.K) + " aggregates set");
+        ctx->htrace.mark("check K" + std::to_string(v.K) + " aggregates set");
     }
     volatile uint64_t *flag = ctx->h_ready;
     while (*flag < v.seq) {   // the export is released with the codebook's ready number
@@ -1790,7 +1692,7 @@ void verify_level(qvq_ctx *ctx, qvq_ctx::Verify &v) {
         cpu_relax();
     }
     std::atomic_thread_fence(std::memory_order_acquire);
-    g_htrace.mark("check K" + std::to_string(v.K) + " export seen");
+    ctx->htrace.mark("check K" + std::to_string(v.K) + " export seen");
     static const int fail_level = std::getenv("QVQ_KAHAN_FAIL_LEVEL") ? std::atoi(std::getenv("QVQ_KAHAN_FAIL_LEVEL")) : 0;
     static const int fail_rank = std::getenv("QVQ_KAHAN_FAIL_RANK") ? std::atoi(std::getenv("QVQ_KAHAN_FAIL_RANK")) : -1;
     if (fail_level && (int)v.level == fail_level && (fail_rank < 0 || fail_rank == ctx->rank)) return;
@@ -1839,6 +1741,22 @@ void verify_level(qvq_ctx *ctx, qvq_ctx::Verify &v) {
     if (certify_rows(ctx, *v.tree, v.cb.data(), v.cnt, v.K, v.A_prev, ctx->vstream, sync, cs, defer, open) != QVQ_OK ||
         (open && !defer))
         return;
+    // QVQ_KAHAN_OPEN_LEVEL=L (tests; -1: every level): a row of level L left open with no cell
+    // wanted, on rank QVQ_KAHAN_FAIL_RANK (default every rank) -- the state that no later sum can
+    // settle, which must end in the redo
+    static const int open_level = std::getenv("QVQ_KAHAN_OPEN_LEVEL") ? std::atoi(std::getenv("QVQ_KAHAN_OPEN_LEVEL")) : 0;
+    if (open_level && (open_level < 0 || (int)v.level == open_level) && (fail_rank < 0 || fail_rank == ctx->rank) &&
+        cs.nu > 0) {
+        if (cs.pend.empty()) cs.pend.push_back(0);
+        open = (uint32_t)cs.pend.size();
+        cs.sel.assign(v.K / 2, 0);
+        cs.cells = 0;
+    }
+    // open rows that want no cell (their candidates all known, yet a decision left open): no
+    // cell summed over the ranks can settle them, so the level fails here (several ranks: a
+    // deferred entry without cells would be skipped by resolve_deferred, keeping unconfirmed
+    // speculative indices)
+    if (open && cs.cells == 0) return;
     if (cert_mismatch(cs, v.K)) return;
     cert_trace.mark("done");
     if (env_is("QVQ_KAHAN_DEBUG", "1") || trace)
@@ -1908,8 +1826,7 @@ qvq_status ensure_speculation(qvq_ctx *ctx, uint32_t Kmax) {
     }
     if (!ctx->vstream) {   // high priority: the check's few short kernels go ahead of the next search's queued blocks
         int lo = 0, hi = 0;
-        static const bool prio = !env_is("QVQ_VSTREAM_PRIO", "0");   // A/B
-        if (prio && hipDeviceGetStreamPriorityRange(&lo, &hi) == hipSuccess && hi != lo)
+        if (hipDeviceGetStreamPriorityRange(&lo, &hi) == hipSuccess && hi != lo)
             HIPCHK(hipStreamCreateWithPriority(&ctx->vstream, hipStreamNonBlocking, hi));
         else
             HIPCHK(hipStreamCreateWithFlags(&ctx->vstream, hipStreamNonBlocking));
@@ -1951,8 +1868,7 @@ qvq_status resolve_kahan_ties(qvq_ctx *ctx, uint32_t K, int slot, unsigned nt, b
     KdView kd;
     // the level's tree (over the exact-sum split, built during the search) is the reference's
     // tree too when no differing coordinate can move a box, cut or partition (kdtree.cpp)
-    static const bool reuse = !env_is("QVQ_KAHAN_TREE", "rebuild");
-    if (reuse && ctx->tree && ctx->tree_kd.depth > 0 && ctx->cb_local.size() == (size_t)K * D &&
+    if (ctx->tree && ctx->tree_kd.depth > 0 && ctx->cb_local.size() == (size_t)K * D &&
         ctx->tree->unchanged_under(ctx->h_kc_split.data())) {
         kd = ctx->tree_kd;
         if (env_is("QVQ_KAHAN_DEBUG", "1")) std::fprintf(stderr, "qvq kahan: K %u the level's tree reused\n", K);
@@ -1984,8 +1900,7 @@ qvq_status resolve_kahan_ties_multi(qvq_ctx *ctx, uint32_t K, int slot, unsigned
     if ((st = wait_stream(ctx)) != QVQ_OK) return st;
     if (nt) {
         KdView kd;
-        static const bool reuse = !env_is("QVQ_KAHAN_TREE", "rebuild");
-        if (reuse && ctx->tree && ctx->tree_kd.depth > 0 && ctx->cb_local.size() == (size_t)K * D &&
+        if (ctx->tree && ctx->tree_kd.depth > 0 && ctx->cb_local.size() == (size_t)K * D &&
             ctx->tree->unchanged_under(ctx->h_kc_split.data()))
             kd = ctx->tree_kd;
         else
@@ -2031,7 +1946,11 @@ qvq_status resolve_deferred(qvq_ctx *ctx, uint32_t bits, const std::vector<uint3
         cell_of.clear();
         for (uint32_t c = 0; c < Kc; c++)
             if ((v[off[L] + c / 4] >> (16 * (c % 4))) & 0xFFFF) cell_of.push_back(c);
-        if (cell_of.empty()) continue;
+        if (cell_of.empty()) {   // no rank wants a cell here: rows still open stay open (a redo)
+            for (const auto &d : ctx->deferred)
+                if (d.level == L && !d.cs.pend.empty()) local_fail = true;
+            continue;
+        }
         ctx->tm.kahan_relays++;
         const uint32_t S = (uint32_t)cell_of.size();
         if ((st = ensure_kahan(ctx, Kc)) != QVQ_OK) return st;
@@ -2165,8 +2084,8 @@ QVQ_API void qvq_destroy(qvq_ctx *ctx) {
     }
     ctx->pool.cv.notify_all();
     for (auto &t : ctx->pool.th) t.join();
-    while (ctx->prep.pending.load(std::memory_order_acquire)) std::this_thread::yield();
-    for (qvq_ctx::Worker *w : {&ctx->worker, &ctx->prep})
+    {
+        qvq_ctx::Worker *w = &ctx->worker;
         if (w->th.joinable()) {
             {
                 std::lock_guard<std::mutex> g(w->m);
@@ -2175,6 +2094,7 @@ QVQ_API void qvq_destroy(qvq_ctx *ctx) {
             w->cv.notify_one();
             w->th.join();
         }
+    }
     (void)hipSetDevice(ctx->dev);
     if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
     if (ctx->comm) ncclCommDestroy(ctx->comm);
@@ -2488,10 +2408,7 @@ QVQ_API qvq_status qvq_lbg(qvq_ctx *ctx, uint32_t bits, double eps, double *code
     const auto t0 = std::chrono::steady_clock::now();
     static const bool htrace = env_is("QVQ_HOST_TRACE", "1");
     if (htrace) {
-        std::lock_guard<std::mutex> g(g_htrace.m);
-        g_htrace.on = true;
-        g_htrace.t0 = t0;
-        g_htrace.ev.clear();
+        ctx->htrace.start(t0);
     }
     const uint32_t Kmax = 1u << bits;
     qvq_status st = ensure_levels(ctx, std::max<uint32_t>(Kmax, 2));
@@ -2536,12 +2453,10 @@ QVQ_API qvq_status qvq_lbg(qvq_ctx *ctx, uint32_t bits, double eps, double *code
         ctx->d_Aext.push_back(p);
     }
     ctx->deferred.clear();
-    struct JobGuard {   // no tree build, check or prep job outlives the call (an error return included)
+    struct JobGuard {   // no tree build or check outlives the call (an error return included)
         qvq_ctx *c;
         ~JobGuard() {
             join_tree_job(c, true);
-            // a prep job still running holds a level's tree and certificate: it finishes first
-            while (c->prep.pending.load(std::memory_order_acquire)) std::this_thread::yield();
             for (auto &v : c->ver) {
                 v.cancel.store(true);
                 join_verify(c, v);
@@ -2570,8 +2485,11 @@ QVQ_API qvq_status qvq_lbg(qvq_ctx *ctx, uint32_t bits, double eps, double *code
     };
     for (;;) {   // once, or twice when a speculative check fails
     out_enqueued = false;
+    const bool tmean = ctx->timing_level == -3;   // events around the mean kernel (qvq_set_timing)
+    if (tmean) HIPCHK(hipEventRecord(ctx->ev[31][0], ctx->stream));
     HIPCHK(launch_mean_sums(ctx->stream, ctx->Dp, ctx->d_codes, ctx->N, ctx->D, ctx->d_plut, ctx->d_mean,
                             ctx->d_counters, N_COUNTERS, d_dist, hist, ctx->d_lut64));
+    if (tmean) HIPCHK(hipEventRecord(ctx->ev[31][1], ctx->stream));
     if ((st = all_reduce_sums(ctx, 1, ctx->d_mean, MEAN_COPIES)) != QVQ_OK) {
         (void)hipMemsetAsync(ctx->d_mean, 0, MEAN_COPIES * (2 * 64 + 1) * 8, ctx->stream);   // keep it clear for the next call
         return st;
@@ -2626,9 +2544,9 @@ QVQ_API qvq_status qvq_lbg(qvq_ctx *ctx, uint32_t bits, double eps, double *code
         if (spec) {
             if (lvl >= 4) {
                 bool ok;
-                g_htrace.mark("L" + std::to_string(lvl) + " joins check K" + std::to_string(ctx->ver[lvl % 3].K));
+                ctx->htrace.mark("L" + std::to_string(lvl) + " joins check K" + std::to_string(ctx->ver[lvl % 3].K));
                 if ((st = join_verify_bounded(ctx, ctx->ver[lvl % 3], ok)) != QVQ_OK) return st;
-                g_htrace.mark("L" + std::to_string(lvl) + " joined");
+                ctx->htrace.mark("L" + std::to_string(lvl) + " joined");
                 if (!ok && !multi) {
                     spec_failed = true;
                     break;
@@ -2646,9 +2564,8 @@ QVQ_API qvq_status qvq_lbg(qvq_ctx *ctx, uint32_t bits, double eps, double *code
             std::swap(ctx->d_A, ctx->d_A_alt);   // d_A_alt: the previous level's assignment
         }
         alev[lvl] = ctx->d_A;
-        ctx->want_full = spec && !multi && kahan;
         if ((st = run_level(ctx, K, slot, true, host_cb_of(ctx, lvl), ctx->seq, sync_kahan)) != QVQ_OK) return st;
-        if (spec) {   // the level's check: its tree now, its certificate prepared on the prep worker
+        if (spec) {   // the level's check: its tree now
             qvq_ctx::Verify &v = ctx->ver[lvl % 3];
             v.K = K;
             v.level = lvl;
@@ -2657,26 +2574,7 @@ QVQ_API qvq_status qvq_lbg(qvq_ctx *ctx, uint32_t bits, double eps, double *code
             v.cnt = std::move(ctx->cnt_local);
             ctx->cb_local.clear();
             ctx->cnt_local.clear();
-            v.full_seq = ctx->kf_level_seq;
             v.cs = CertState();
-            v.prep_done.store(false);
-            // Off by default (QVQ_CERT_PREP=1: on, A/B): replays that build the node splits they
-            // visit beat one thread building them all, and the prep competes for the host's cores
-            // with the tree builds on the critical path.  C4 with every level prepared 8.0 ms,
-            // none 7.3 (profiles/r05h); with all but the last 8.08, none 7.41; C3 1.2536 / 1.2293
-            // (profiles/r05i).  Never the last level: its check follows at once.
-            static const bool prep_on = env_is("QVQ_CERT_PREP", "1");
-            if (prep_on && lvl < bits && v.tree && !v.tree->cancelled() && K >= 2 &&
-                v.cb.size() == (size_t)K * ctx->D) {
-                qvq_ctx::Verify *vp = &v;
-                const uint32_t D = ctx->D;
-                post_job(ctx, [vp, K, D] {
-                    cert_init(*vp->tree, vp->cs, vp->cb.data(), vp->cnt, K, D, true);
-                    vp->prep_done.store(true, std::memory_order_release);
-                }, &ctx->prep);
-            } else {
-                v.prep_done.store(true);
-            }
         }
         const bool split = lvl < bits;
         {
@@ -2689,12 +2587,12 @@ QVQ_API qvq_status qvq_lbg(qvq_ctx *ctx, uint32_t bits, double eps, double *code
                                         ctx->d_part, ctx->d_part_cnt, ctx->nslabs, ctx->nsub, ctx->d_sums,
                                         ctx->d_sums + sums_cap_stride(ctx)));
                 ctx->kd_pend = false;
-            } else if (!(abl_skip() & 4) && ctx->nslabs) {   // nslabs 0: the sorted sums are in d_sums already
+            } else if (ctx->nslabs) {   // nslabs 0: the sorted sums are in d_sums already
                 HIPCHK(launch_reduce(ctx->stream, ctx->d_part, ctx->d_part_cnt, ctx->nslabs, ctx->nsub, K, ctx->D,
                                      ctx->d_sums, ctx->pub));
             }
             if (ctx->pub.flag) {   // run_level left the tie count to the reduce, which did not run
-                if (!ctx->nslabs || (abl_skip() & 4) || ctx->kd_pend)
+                if (!ctx->nslabs || ctx->kd_pend)
                     HIPCHK(launch_copy_out(ctx->stream, ctx->pub.cnt, ctx->pub.dst, 4, nullptr, nullptr, 0, nullptr,
                                            nullptr, 0, ctx->pub.flag, ctx->pub.seq, ctx->d_counters + 2 * 33 + 1));
                 ctx->pub = PubArgs();
@@ -2726,7 +2624,7 @@ QVQ_API qvq_status qvq_lbg(qvq_ctx *ctx, uint32_t bits, double eps, double *code
                     verify_level(ctx, *vp);
                     vp->done.store(true, std::memory_order_release);
                 });
-                g_htrace.mark("L" + std::to_string(lvl) + " finalize enqueued, check posted");
+                ctx->htrace.mark("L" + std::to_string(lvl) + " finalize enqueued, check posted");
             }
             if (sync_kahan) {   // the level's ties (published after its recheck)
                 if ((st = wait_flag(ctx, ctx->h_ready + 1, ctx->pub_seq)) != QVQ_OK) return st;
@@ -2758,13 +2656,13 @@ QVQ_API qvq_status qvq_lbg(qvq_ctx *ctx, uint32_t bits, double eps, double *code
     }
     if (spec && !spec_failed) {   // the results' copy overlaps the last checks
         if ((st = enqueue_out()) != QVQ_OK) return st;
-        g_htrace.mark("results' copy enqueued");
+        ctx->htrace.mark("results' copy enqueued");
         for (uint32_t l = bits >= 3 ? bits - 2 : 1; l <= bits; l++) {
             bool ok;
             if ((st = join_verify_bounded(ctx, ctx->ver[l % 3], ok)) != QVQ_OK) return st;
             local_fail = local_fail || !ok;
         }
-        g_htrace.mark("last checks joined");
+        ctx->htrace.mark("last checks joined");
         spec_failed = local_fail;
         if (multi && (st = resolve_deferred(ctx, bits, alev, spec_failed)) != QVQ_OK) return st;
     }
@@ -2772,7 +2670,6 @@ QVQ_API qvq_status qvq_lbg(qvq_ctx *ctx, uint32_t bits, double eps, double *code
     if (!spec_failed) break;
     // a check failed: every check joined, the stream drained, then the quantize again with
     // synchronous Kahan levels
-    while (ctx->prep.pending.load(std::memory_order_acquire)) std::this_thread::yield();
     for (auto &v : ctx->ver) {
         v.cancel.store(true);
         join_verify(ctx, v);
@@ -2799,7 +2696,7 @@ QVQ_API qvq_status qvq_lbg(qvq_ctx *ctx, uint32_t bits, double eps, double *code
         const uint64_t cb_bytes = codebook ? (uint64_t)Kmax * ctx->D * 8 : 0;
         qvq_status ws = wait_flag(ctx, reinterpret_cast<volatile uint64_t *>(h_small + (1024 - 64 - 8)), out_seq);
         if (ws != QVQ_OK) return ws;
-        g_htrace.mark("results copied");
+        ctx->htrace.mark("results copied");
         if (assign)   // every collective of this call is complete: a plain copy
             HIPCHK(host_copy(ctx, assign, ctx->d_A, ctx->N * 4, hipMemcpyDeviceToHost));
         std::memcpy(dres, h_small, sizeof(dres));
@@ -2831,15 +2728,17 @@ QVQ_API qvq_status qvq_lbg(qvq_ctx *ctx, uint32_t bits, double eps, double *code
         ctx->tm.flagged[lvl - 1] = stats[2 * (lvl - 1)];
         ctx->tm.host_ties[lvl - 1] = stats[2 * (lvl - 1) + 1];
     }
+    if (ctx->timing_level == -3) {
+        float m = 0;
+        (void)hipEventSynchronize(ctx->ev[31][1]);
+        (void)hipEventElapsedTime(&m, ctx->ev[31][0], ctx->ev[31][1]);
+        ctx->tm.mean_ms = m;
+    }
     (void)hipGetLastError();
     ctx->tm.total_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     if (htrace) {
-        g_htrace.mark("return");
-        std::lock_guard<std::mutex> g(g_htrace.m);
-        std::string out = "qvq host trace:";
-        for (const auto &e : g_htrace.ev) out += "\n  " + std::to_string((int)e.first) + " " + e.second;
-        std::fprintf(stderr, "%s\n", out.c_str());
-        g_htrace.on = false;
+        ctx->htrace.mark("return");
+        std::fprintf(stderr, "%s\n", ctx->htrace.finish().c_str());
     }
     return QVQ_OK;
 }
@@ -3137,7 +3036,7 @@ QVQ_API qvq_status qvq_set_timeout(qvq_ctx *ctx, double seconds) {
 }
 
 QVQ_API qvq_status qvq_set_timing(qvq_ctx *ctx, int level) {
-    if (!ctx || level < -2 || level > 31) return QVQ_EINVAL;
+    if (!ctx || level < -3 || level > 31) return QVQ_EINVAL;
     ctx->timing_level = level;
     return QVQ_OK;
 }

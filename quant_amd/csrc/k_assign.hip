@@ -1,15 +1,8 @@
 // k_assign.hip -- nearest-code-vector search (src/Quantizer.cpp:24-32 semantics).
 //
-//  assign_mfma_kernel  D = 12.  Scores 2^t(||x-c||^2 - ||x-mu||^2) for 16 code vectors x
-//                      16 rows per v_mfma_f32_16x16x32_f16: A = code-vector tile
-//                      [f16 hi(12) | f16 lo(12) | n_hi n_lo | 0], B = data tile
-//                      [w(12) | w(12) | 1 1 | 0] with w the exact centred byte integer.
-//                      Epilogue per lane and tile: min of its 4 values, running best tile
-//                      and second-best tile minimum.  At the end each lane recomputes its
-//                      best tile's 4 scores, lanes of a row combine, and rows whose best
-//                      two scores are inside the error bound are flagged for the fp64
-//                      recheck.  Optionally the exact centroid sums of the unflagged rows
-//                      are accumulated in LDS ([d][k] layout, u64 (hi<<32|lo) terms).
+//  assign_small_kernel D = 12, K <= 32: expanded fp32 scores per code vector; exact centroid
+//                      sums in per-lane register runs (LDS copies).  K >= 64 runs the
+//                      32x32x16 MFMA search of k_mf32.hip (launch_assign_mfma dispatches).
 //  assign_valu_kernel  any Dp <= 64, fp32 direct form (x-c)^2 with an fp32 error bound.
 //  recheck_kernel      fp64 distances of flagged rows in the reference build's order.
 #include <cstdlib>
@@ -24,16 +17,6 @@ namespace qvq {
 // =======================================================================================
 // MFMA search
 // =======================================================================================
-#ifndef QVQ_MF_LOOP
-#define QVQ_MF_LOOP 2
-#endif
-#ifndef QVQ_MF_THREADS
-#define QVQ_MF_THREADS 1024
-#endif
-constexpr int MF_THREADS = QVQ_MF_THREADS;       // 16 waves (4 per SIMD), one workgroup per CU
-constexpr int MF_WAVES = MF_THREADS / 64;
-constexpr int MF_TILES = 4;                      // 16-row data tiles per wave and chunk
-constexpr int MF_ROWS = 16 * MF_TILES;           // rows per wave and chunk
 constexpr int MF_LDS_MAX = 160 * 1024;
 
 struct MfLds {
@@ -64,397 +47,9 @@ uint32_t mf_fuse_max_k() {
 bool mf_can_search(uint32_t K) { return mf_lds_layout(K, false, false).total <= MF_LDS_MAX; }
 
 
-typedef uint64_t u64x2 __attribute__((ext_vector_type(2)));
-typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 
-// Per-run sums over consecutive lanes with equal key (lanes hold consecutive rows): plain
-// prefix sums, then each run's last lane takes prefix[last] - prefix[first - 1].  The
-// packed 16-bit fields of v never carry within 64 rows, so the subtraction is per field, and
-// prefix[first - 1] comes from one bpermute (a DPP max-scan form of it measured slower: the
-// search is VALU-issue bound, not LDS bound).  Returns true on the last lane of each run,
-// which then holds the run's sums.
-__device__ inline bool wave_runs_reduce(uint32_t key, uint32_t (&v)[MF_D + 1], int lane) {
-    const uint32_t prev = wave_prev_u32(key);
-    const uint32_t next = wave_next_u32(key);
-    const bool head = lane == 0 || prev != key;
-    const uint32_t h = wave_scan_max(head ? (uint32_t)lane : 0u);
-    const int src = h == 0 ? 0 : (int)h - 1;
-#pragma unroll
-    for (int i = 0; i <= MF_D; i++) {
-        const uint32_t pre = wave_scan_add(v[i]);
-        const uint32_t before = __shfl(pre, src);
-        v[i] = pre - (h == 0 ? 0u : before);
-    }
-    return lane == 63 || next != key;
-}
-
-
 constexpr int MF_SMALL_K = 32;
-
-// SK > 0 (K <= SK <= MF_SMALL_K, SK a power of two): no MFMA at all -- each lane scans SK
-// code vectors of its row (rows K..SK-1 are zero padding and masked) in the direct fp32 form
-// (the recompute below), cheaper than the MFMA pass's per-chunk fixed work at this size.
-template <bool FUSE, bool STAGED, int SK, bool U4>
-__global__ __launch_bounds__(MF_THREADS) void assign_mfma_kernel(
-    const uint8_t *__restrict__ codes, uint64_t N, const _Float16 *__restrict__ g_rows, uint32_t K,
-    const float *__restrict__ g_C32, const uint64_t *__restrict__ g_plut, MfThresholds th, uint32_t *__restrict__ A,
-    uint32_t *__restrict__ flags, unsigned *__restrict__ flag_cnt, uint64_t *__restrict__ part,
-    uint32_t *__restrict__ part_cnt) {
-    extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
-    constexpr bool SMALLK = SK > 0;
-    const uint32_t Kp = (K + 31) & ~31u;
-    const MfLds L = mf_lds_layout(K, FUSE, STAGED);
-    unsigned char *rows = lds;   // Kp x 56 B code-vector rows, then 16 B zero pad
-    float *c32s = reinterpret_cast<float *>(lds + L.c32);
-    uint64_t *sums = reinterpret_cast<uint64_t *>(lds + L.sums);   // [d][k]
-    uint32_t *cnt = reinterpret_cast<uint32_t *>(lds + L.cnt);
-    uint8_t *lo8 = lds + L.plut;   // low part of each byte's exact term (high part: b ^ 0x80)
-    const int tid = threadIdx.x;
-    if (!SMALLK) {
-        const uint64_t *src = reinterpret_cast<const uint64_t *>(g_rows);
-        uint64_t *dst = reinterpret_cast<uint64_t *>(rows);
-        for (uint32_t i = tid; i < Kp * (MF_ROW_BYTES / 8) + 2; i += MF_THREADS)
-            dst[i] = i < Kp * (MF_ROW_BYTES / 8) ? src[i] : 0ull;
-    }
-    if (STAGED) {
-        const float4 *src = reinterpret_cast<const float4 *>(g_C32);
-        float4 *dst = reinterpret_cast<float4 *>(c32s);
-        for (uint32_t i = tid; i < Kp * (MF_D / 4); i += MF_THREADS) dst[i] = src[i];
-    }
-    if (FUSE) {
-        for (uint32_t i = tid; i < K * MF_D; i += MF_THREADS) sums[i] = 0;
-        for (uint32_t i = tid; i < K; i += MF_THREADS) cnt[i] = 0;
-        if (tid < 256) lo8[tid] = (uint8_t)(g_plut[tid] & 0xFF);
-        if (blockIdx.x == 0) {   // the correction slabs G (+) and G + 1 (-), after all G others
-            for (uint32_t i = tid; i < 2 * K * MF_D; i += MF_THREADS) part[(uint64_t)gridDim.x * K * MF_D + i] = 0;
-            for (uint32_t i = tid; i < 2 * K; i += MF_THREADS) part_cnt[(uint64_t)gridDim.x * K + i] = 0;
-        }
-    }
-    __syncthreads();
-    const float *C32 = STAGED ? c32s : g_C32;
-
-    const int lane = tid & 63, wave = tid >> 6;
-    const int g = lane >> 4, c = lane & 15;
-    const uint32_t npairs = Kp / 32;
-    const uint64_t nchunks = (N + MF_ROWS - 1) / MF_ROWS;
-    const f32x4 zero = {0.f, 0.f, 0.f, 0.f};
-    // B fragment of a data tile (row layout, common.hpp): lane group g < 3 meets components
-    // 4g..4g+3 twice, so it needs word g of the row only; g = 3 meets [n_hi, n_lo, 0 ...] and
-    // holds [1, 1, 0 ...].  gm masks g = 3 lanes.
-    const uint32_t gm = g < 3 ? ~0u : 0u;
-    const int gw = g < 3 ? g : 2;
-    // A fragment of tile t: 16 B of code vector t*16 + c at byte 16g of its row (g = 3
-    // reads n_hi, n_lo, 0, 0 and 8 bytes of the next row, which meet zeros in B).
-    const unsigned char *a_base = rows + (size_t)c * MF_ROW_BYTES + 16 * g;
-    auto load_a = [&](uint32_t tile) -> half8 {
-        const uint64_t *p = reinterpret_cast<const uint64_t *>(a_base + (size_t)tile * 16 * MF_ROW_BYTES);
-        const u64x2 v = {p[0], p[1]};
-        return __builtin_bit_cast(half8, v);
-    };
-    // Branch-free: rows past N read row N - 1 (their results are never written).  A load
-    // under a branch gets an s_waitcnt vmcnt(0) at the join, which would void the prefetch.
-    // q[t] (t < MF_TILES): word gw of row t*16 + c of the chunk; q[MF_TILES..+2]: the lane's
-    // own row, base + lane.
-    constexpr int QW = MF_TILES + 3;
-    auto load_codes = [&](uint64_t chunk, uint32_t (&q)[QW]) {
-        if constexpr (!SMALLK) {
-#pragma unroll
-            for (int t = 0; t < MF_TILES; t++) {
-                uint64_t row = chunk * MF_ROWS + t * 16 + c;
-                row = row < N ? row : N - 1;
-                q[t] = reinterpret_cast<const uint32_t *>(codes + row * MF_D)[gw];
-            }
-        }
-        uint64_t row = chunk * MF_ROWS + lane;
-        row = row < N ? row : N - 1;
-        const uint32_t *p = reinterpret_cast<const uint32_t *>(codes + row * MF_D);
-        q[MF_TILES] = p[0];
-        q[MF_TILES + 1] = p[1];
-        q[MF_TILES + 2] = p[2];
-    };
-
-    uint64_t chunk = (uint64_t)blockIdx.x * MF_WAVES + wave;
-    const uint64_t stride = (uint64_t)gridDim.x * MF_WAVES;
-    uint32_t qn[QW];
-    load_codes(chunk, qn);
-    for (; chunk < nchunks; chunk += stride) {
-        const uint64_t base = chunk * MF_ROWS;
-        uint32_t q[QW];
-#pragma unroll
-        for (int i = 0; i < QW; i++) q[i] = qn[i];
-        load_codes(chunk + stride, qn);   // prefetch the next chunk under this one's search
-        const uint32_t own[3] = {q[MF_TILES], q[MF_TILES + 1], q[MF_TILES + 2]};
-        uint32_t unit = 0;       // 8-code-vector unit (pair*4 + g) the MFMA pass picked
-        float sec_m = INFINITY;  // best MFMA score among the other units
-        if constexpr (!SMALLK) {
-        // B fragments: lane (g, c) holds k-slots 8g..8g+7 of data row c of each tile:
-        // [w(4g..4g+3), w(4g..4g+3)] (byte_quad_w), or [1, 1, 0 ...] for g = 3, whose masked
-        // word (u = 128, w = 1) gives the two ones.
-        half8 b[MF_TILES];
-#pragma unroll
-        for (int t = 0; t < MF_TILES; t++) {
-            uint32_t w01, w23;
-            byte_quad_w(q[t] & gm, w01, w23);
-            const u32x4 v = {w01, w23 & gm, w01 & gm, w23 & gm};
-            b[t] = __builtin_bit_cast(half8, v);
-        }
-        float b1[MF_TILES], b2[MF_TILES];
-        uint32_t bp[MF_TILES];
-#pragma unroll
-        for (int t = 0; t < MF_TILES; t++) {
-            b1[t] = INFINITY;
-            b2[t] = INFINITY;
-            bp[t] = 0;
-        }
-#if QVQ_MF_LOOP == 2
-        // Tile pairs, ping-pong: the MFMAs of pair i overlap the epilogue of pair i-1, and
-        // the A fragments of pair i+1 are read from LDS under them.  Unrolled by two so the
-        // two accumulator sets alternate roles without register copies.
-        f32x4 pa0[MF_TILES], pa1[MF_TILES], qa0[MF_TILES], qa1[MF_TILES];
-        half8 a0 = load_a(0), a1 = load_a(1);
-        auto mfma_pair = [&](f32x4 (&r0)[MF_TILES], f32x4 (&r1)[MF_TILES]) {
-#pragma unroll
-            for (int t = 0; t < MF_TILES; t++) {
-                r0[t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a0, b[t], zero, 0, 0, 0);
-                r1[t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a1, b[t], zero, 0, 0, 0);
-            }
-        };
-        auto next_a = [&](uint32_t pr) {   // fragments of pair pr (clamped: the last is re-read)
-            const uint32_t p = pr < npairs ? pr : npairs - 1;
-            a0 = load_a(2 * p);
-            a1 = load_a(2 * p + 1);
-        };
-        mfma_pair(pa0, pa1);
-        next_a(1);
-        uint32_t pr = 1;
-        for (; pr + 1 < npairs; pr += 2) {
-            mfma_pair(qa0, qa1);
-            next_a(pr + 1);
-#pragma unroll
-            for (int t = 0; t < MF_TILES; t++) unit_update<U4>(pa0[t], pa1[t], pr - 1, b1[t], b2[t], bp[t]);
-            mfma_pair(pa0, pa1);
-            next_a(pr + 2);
-#pragma unroll
-            for (int t = 0; t < MF_TILES; t++) unit_update<U4>(qa0[t], qa1[t], pr, b1[t], b2[t], bp[t]);
-        }
-        if (pr < npairs) {   // npairs even: one pair left
-            mfma_pair(qa0, qa1);
-#pragma unroll
-            for (int t = 0; t < MF_TILES; t++) unit_update<U4>(pa0[t], pa1[t], pr - 1, b1[t], b2[t], bp[t]);
-#pragma unroll
-            for (int t = 0; t < MF_TILES; t++) unit_update<U4>(qa0[t], qa1[t], pr, b1[t], b2[t], bp[t]);
-        } else {
-#pragma unroll
-            for (int t = 0; t < MF_TILES; t++) unit_update<U4>(pa0[t], pa1[t], pr - 1, b1[t], b2[t], bp[t]);
-        }
-
-#elif QVQ_MF_LOOP == 1
-        // Tile pairs, ping-pong: the MFMAs of pair i overlap the epilogue of pair i-1, and
-        // the A fragments of pair i+1 are read from LDS under them.
-        f32x4 pa0[MF_TILES], pa1[MF_TILES];
-        half8 a0 = load_a(0), a1 = load_a(1);
-#pragma unroll
-        for (int t = 0; t < MF_TILES; t++) {
-            pa0[t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a0, b[t], zero, 0, 0, 0);
-            pa1[t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a1, b[t], zero, 0, 0, 0);
-        }
-        a0 = load_a(2);
-        a1 = load_a(3);
-        for (uint32_t pr = 1; pr < npairs; pr++) {
-            f32x4 qa0[MF_TILES], qa1[MF_TILES];
-#pragma unroll
-            for (int t = 0; t < MF_TILES; t++) {
-                qa0[t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a0, b[t], zero, 0, 0, 0);
-                qa1[t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a1, b[t], zero, 0, 0, 0);
-            }
-            // next pair's fragments (the last pair re-reads itself)
-            const uint32_t pn = pr + 1 < npairs ? pr + 1 : pr;
-            a0 = load_a(2 * pn);
-            a1 = load_a(2 * pn + 1);
-#pragma unroll
-            for (int t = 0; t < MF_TILES; t++) unit_update<U4>(pa0[t], pa1[t], pr - 1, b1[t], b2[t], bp[t]);
-#pragma unroll
-            for (int t = 0; t < MF_TILES; t++) {
-                pa0[t] = qa0[t];
-                pa1[t] = qa1[t];
-            }
-        }
-#pragma unroll
-        for (int t = 0; t < MF_TILES; t++) unit_update<U4>(pa0[t], pa1[t], npairs - 1, b1[t], b2[t], bp[t]);
-
-#else
-        // Tile pairs, ping-pong: the MFMAs of pair i overlap the epilogue of pair i-1.
-        f32x4 pa0[MF_TILES], pa1[MF_TILES];
-        {
-            const half8 a0 = load_a(0), a1 = load_a(1);
-#pragma unroll
-            for (int t = 0; t < MF_TILES; t++) {
-                pa0[t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a0, b[t], zero, 0, 0, 0);
-                pa1[t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a1, b[t], zero, 0, 0, 0);
-            }
-        }
-        for (uint32_t pr = 1; pr < npairs; pr++) {
-            const half8 a0 = load_a(2 * pr), a1 = load_a(2 * pr + 1);
-            f32x4 qa0[MF_TILES], qa1[MF_TILES];
-#pragma unroll
-            for (int t = 0; t < MF_TILES; t++) {
-                qa0[t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a0, b[t], zero, 0, 0, 0);
-                qa1[t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a1, b[t], zero, 0, 0, 0);
-            }
-#pragma unroll
-            for (int t = 0; t < MF_TILES; t++) unit_update<U4>(pa0[t], pa1[t], pr - 1, b1[t], b2[t], bp[t]);
-#pragma unroll
-            for (int t = 0; t < MF_TILES; t++) {
-                pa0[t] = qa0[t];
-                pa1[t] = qa1[t];
-            }
-        }
-#pragma unroll
-        for (int t = 0; t < MF_TILES; t++) unit_update<U4>(pa0[t], pa1[t], npairs - 1, b1[t], b2[t], bp[t]);
-
-#endif
-        // Combine the four lanes of each data row (groups g = 0..3 of every tile) on MFMA
-        // values: winning 8-code-vector unit (pair*4 + g, lowest on equal scores) and the
-        // second-best minimum among all other candidates.  A reduce-scatter on the VALU:
-        // v_permlane32_swap merges tiles t and t + 2 across lane ^ 32, v_permlane16_swap the
-        // two survivors across lane ^ 16, and lane (g, c) is left with tile g, row c -- its
-        // own row base + lane.  The merge is order-free: (best, unit) is the lexicographic
-        // minimum and the second the second-smallest of all candidates either way.
-        auto merge = [](float &m1, float &m2, uint32_t &mu, float o1, float o2, uint32_t ou) {
-            if (o1 < m1 || (o1 == m1 && ou < mu)) {
-                m2 = min2f(o2, m1);
-                m1 = o1;
-                mu = ou;
-            } else {
-                m2 = min2f(m2, o1);
-            }
-        };
-        float h1[2], h2[2];
-        uint32_t hu[2];
-#pragma unroll
-        for (int t = 0; t < 2; t++) {
-            // lanes < 32 end with tile t (g and g + 2 merged), lanes >= 32 with tile t + 2
-            const auto s1 = swap32_f32(b1[t], b1[t + 2]);
-            const auto s2 = swap32_f32(b2[t], b2[t + 2]);
-            const auto su = swap32_u32(bp[t] * 4 + g, bp[t + 2] * 4 + g);
-            h1[t] = s1.lo;
-            h2[t] = s2.lo;
-            hu[t] = su.lo;
-            merge(h1[t], h2[t], hu[t], s1.hi, s2.hi, su.hi);
-        }
-        {   // even rows keep h*[0] (tile 0 or 2), odd rows h*[1] (tile 1 or 3): tile g
-            const auto s1 = swap16_f32(h1[0], h1[1]);
-            const auto s2 = swap16_f32(h2[0], h2[1]);
-            const auto su = swap16_u32(hu[0], hu[1]);
-            float m1 = s1.lo;
-            sec_m = s2.lo;
-            unit = su.lo;
-            merge(m1, sec_m, unit, s1.hi, s2.hi, su.hi);
-        }
-        // Lane L owns row base + L (tile L/16, row L%16): recompute the 8 code vectors of
-        // its winning unit in the direct fp32 form (x - c)^2.
-        }   // !SMALLK
-        const uint64_t row = base + lane;
-        const bool valid = row < N;
-        uint32_t rk = 0;
-        bool flagged = false;
-        if (valid) {
-            float x[MF_D];
-            float xn = 0.f;   // ||x - mu||^2
-#pragma unroll
-            for (int d = 0; d < MF_D; d++) {
-                const float e = byte_w(own[d / 4], d % 4) * th.sx;
-                xn = __fmaf_rn(e, e, xn);
-                x[d] = e + th.mu;
-            }
-            float r1 = INFINITY, r2 = INFINITY;
-            const uint32_t pr = unit >> 2, gg = unit & 3;   // pair (tile with U4), lane group
-#ifdef QVQ_ABL_NORECOMP   // timing ablation only (wrong results): no recompute, no flags
-            constexpr bool skip = !SMALLK;
-            rk = (2 * pr) * 16 + 4 * gg;
-            r1 = 0.f;
-            r2 = 1e30f;
-#else
-            constexpr bool skip = false;
-#endif
-            // a unit is 4 code vectors of each tile of its pair; up to K = 16 the second
-            // tile is padding, and below 4 so is the rest of the first
-            // SMALLK: the unit is the whole codebook
-            // U4: a unit is 4 code vectors of one tile
-            const int jn = SMALLK ? SK : ((U4 || K <= 16) ? (K < 4 ? (int)K : 4) : 8);
-#pragma unroll
-            for (int j = 0; j < (SMALLK ? SK : (U4 ? 4 : 8)); j++) {
-                if (skip || (!SMALLK && j >= jn)) continue;   // uniform: K is
-                const uint32_t cv = SMALLK ? (uint32_t)j
-                                           : (U4 ? pr * 16 + 4 * gg + j : (2 * pr + (j >> 2)) * 16 + 4 * gg + (j & 3));
-                const float4 *c4 = reinterpret_cast<const float4 *>(C32 + (size_t)cv * MF_D);
-                float dist = 0.f;
-#pragma unroll
-                for (int qq = 0; qq < 3; qq++) {
-                    const float4 cq = c4[qq];
-                    float e;
-                    e = x[4 * qq + 0] - cq.x; dist = __fmaf_rn(e, e, dist);
-                    e = x[4 * qq + 1] - cq.y; dist = __fmaf_rn(e, e, dist);
-                    e = x[4 * qq + 2] - cq.z; dist = __fmaf_rn(e, e, dist);
-                    e = x[4 * qq + 3] - cq.w; dist = __fmaf_rn(e, e, dist);
-                }
-                dist = cv < K ? dist : INFINITY;   // padding code vectors never win
-                r2 = med3f(r1, r2, dist);
-                rk = dist < r1 ? cv : rk;
-                r1 = min2f(r1, dist);
-            }
-            const float sec = SMALLK ? r2 : min2f(__fmaf_rn(sec_m, th.inv_scale, xn), r2);
-            // sec from an MFMA score can be slightly negative (a row on a code vector): the
-            // row is flagged then anyway (r1 >= 0), and no NaN reaches the -fno-honor-nans compare
-            const float sp = fmaxf(sec, 0.f);
-            const float thr = (SMALLK ? 0.f : th.mfma) + 2.f * (th.alpha * sqrtf(sp) + th.beta * sp) + th.gamma;
-            A[row] = rk;
-            flagged = !(sec - r1 > thr);
-            if (flagged) flags[atomicAdd(flag_cnt, 1u)] = (uint32_t)row;
-        }
-        if (FUSE) {
-            // every row at its provisional index; the recheck / kd-tree moves re-assigned ones
-            const bool take = valid;
-            if (K <= th.runs_max_k) {
-                // runs of equal codes along consecutive rows (adjacent blocks): fold each run
-                // in registers first, one lane per run adds to LDS (fewer LDS atomics, and
-                // no same-address ones within a run).
-                uint32_t v[MF_D + 1];
-#pragma unroll
-                for (int d = 0; d < MF_D; d++) {
-                    const uint32_t b = (own[d / 4] >> (8 * (d % 4))) & 0xFF;
-                    v[d] = take ? ((b ^ 0x80u) << 16 | lo8[b]) : 0u;   // <= 64 rows: no carry
-                }
-                v[MF_D] = take ? 1u : 0u;
-                const bool tail = wave_runs_reduce(take ? rk : 0xFFFFFFFFu, v, lane);
-                if (tail && take) {
-#pragma unroll
-                    for (int d = 0; d < MF_D; d++)
-                        atomicAdd((unsigned long long *)&sums[(uint32_t)d * K + rk],
-                                  (unsigned long long)((((uint64_t)(v[d] >> 16)) << 32) | (v[d] & 0xFFFF)));
-                    atomicAdd(&cnt[rk], v[MF_D]);
-                }
-            } else if (take) {
-#pragma unroll
-                for (int d = 0; d < MF_D; d++)
-                {
-                    const uint32_t b = (own[d / 4] >> (8 * (d % 4))) & 0xFF;
-                    atomicAdd((unsigned long long *)&sums[(uint32_t)d * K + rk],
-                              (unsigned long long)((uint64_t)(b ^ 0x80u) << 32 | lo8[b]));
-                }
-                atomicAdd(&cnt[rk], 1u);
-            }
-        }
-    }
-    if (FUSE) {
-        __syncthreads();
-        uint64_t *pdst = part + (uint64_t)blockIdx.x * K * MF_D;   // slab layout [d][k]
-        for (uint32_t i = tid; i < K * MF_D; i += MF_THREADS) pdst[i] = sums[i];
-        uint32_t *cdst = part_cnt + (uint64_t)blockIdx.x * K;
-        for (uint32_t i = tid; i < K; i += MF_THREADS) cdst[i] = cnt[i];
-    }
-}
 
 // ---------------------------------------------------------------------------------------
 // Small codebooks (K <= MF_SMALL_K): direct fp32 scan of all SK code vectors per row, rows in
@@ -462,7 +57,7 @@ __global__ __launch_bounds__(MF_THREADS) void assign_mfma_kernel(
 // it (coalesced loads and stores), four rows per iteration.  At small K a lane's consecutive
 // rows (64 blocks apart in the image) mostly share their code vector: their exact terms
 // (u << 16 | lo per component, no carry within 256 rows) are added in registers and go to the
-// LDS sums only when the index changes.  Flag rule and sums as in assign_mfma_kernel.
+// LDS sums only when the index changes.  Flag rule and sums as in assign_mf32_kernel.
 // ---------------------------------------------------------------------------------------
 __host__ __device__ constexpr uint32_t small_copy_stride(uint32_t SK) { return SK * (MF_D + 1) + 1; }
 // Copies of the small kernel's sums: up to 64 (one per lane) while they fit ~112 KB of LDS.
@@ -636,7 +231,7 @@ __global__ __launch_bounds__(NW * 64) void assign_small_kernel(
             const float thr = __fmaf_rn((float)(2 * sad + MF_D), th.e1, th.e0);
             const bool flagged = valid && !(r2[r] - r1[r] > thr);
             if (flagged) flags[atomicAdd(flag_cnt, 1u)] = row0 + row;
-            if (FUSE && valid) {   // provisional index, as in assign_mfma_kernel
+            if (FUSE && valid) {   // provisional index, as in assign_mf32_kernel
                 if (rk != cur || acc[MF_D] == 256) {   // 16-bit fields hold 256 rows
                     flush();
                     cur = rk;
@@ -706,21 +301,6 @@ __global__ __launch_bounds__(NW * 64) void assign_small_kernel(
     }
 }
 
-template <bool F, bool S, int SK, bool U4>
-static void launch_mfma_variant(hipStream_t s, int grid, size_t lds, const uint8_t *codes, uint64_t N,
-                                const _Float16 *cb_rows, uint32_t K, const float *C32, const uint64_t *plut,
-                                const MfThresholds &th, uint32_t *A, uint32_t *flags, unsigned *flag_cnt,
-                                uint64_t *part, uint32_t *part_cnt) {
-    auto kern = assign_mfma_kernel<F, S, SK, U4>;
-    hipLaunchKernelGGL(kern, dim3(grid), dim3(MF_THREADS), lds, s, codes, N, cb_rows, K, C32, plut, th, A, flags,
-                       flag_cnt, part, part_cnt);
-}
-
-uint32_t mf_small_k() {
-    const char *e = std::getenv("QVQ_SMALLK");   // ablation: QVQ_SMALLK=0 keeps the MFMA pass
-    return e ? (uint32_t)std::min(std::atoi(e), MF_SMALL_K) : (uint32_t)MF_SMALL_K;
-}
-
 hipError_t launch_assign_mfma(hipStream_t s, int grid, bool fuse, const uint8_t *codes, uint64_t N,
                               const _Float16 *cb_rows, const float *E32, uint32_t K, const float *C32,
                               const uint64_t *plut,
@@ -728,32 +308,19 @@ hipError_t launch_assign_mfma(hipStream_t s, int grid, bool fuse, const uint8_t 
                               uint64_t *part, uint32_t *part_cnt, const uint32_t *perm, const int32_t *tint,
                               uint64_t *z1, uint32_t nz1) {
     if (!fuse) z1 = nullptr, nz1 = 0;   // (cleared by the fused kernels' set-up only)
-    static const bool no_stage = std::getenv("QVQ_NOSTAGE") != nullptr;   // ablation
-    const bool staged = mf_lds_layout(K, fuse, true).total <= MF_LDS_MAX && (!no_stage || K <= mf_small_k());
-    const size_t lds = mf_lds_layout(K, fuse, staged).total;
-    using Fn = void (*)(hipStream_t, int, size_t, const uint8_t *, uint64_t, const _Float16 *, uint32_t, const float *,
-                        const uint64_t *, const MfThresholds &, uint32_t *, uint32_t *, unsigned *, uint64_t *,
-                        uint32_t *);
-    Fn fn;
-    if (K <= mf_small_k() && E32) {   // E32 is padded up to 32 rows (n = 1e30)
+    if (K <= MF_SMALL_K && E32) {   // E32 is padded up to 32 rows (n = 1e30)
         const uint32_t sk = K <= 2 ? 2 : K <= 4 ? 4 : K <= 8 ? 8 : K <= 16 ? 16 : 32;
         // rows per lane: a multiple of 4 covering N over grid x waves x 64 lanes
         const uint32_t copies = fuse ? small_copies(sk) : 1;
         const size_t slds = fuse ? small_lds(sk, copies) : 256;
-        // packed run registers (QVQ_SMALL_PACK=0: one register per component, A/B).  Blocks of 16
-        // waves (4 per SIMD, 13 VGPRs spilled from K = 4): 12-wave blocks without spills (168 VGPRs)
+        // packed run registers with fused sums.  Blocks of 16 waves (4 per SIMD): 12-wave blocks
         // measured 1-10 % slower, also with three row groups in flight (profiles/r03d/ab_small.txt)
-        static const bool pack = !(std::getenv("QVQ_SMALL_PACK") && std::getenv("QVQ_SMALL_PACK")[0] == '0');
         const uint64_t lanes = (uint64_t)grid * 16 * 64;
         const uint64_t rpl = ((N + lanes - 1) / lanes + 3) / 4 * 4;
 #define QVQ_SMALL(V)                                                                                              \
     do {                                                                                                          \
-        if (fuse && pack)                                                                                         \
+        if (fuse)                                                                                                 \
             hipLaunchKernelGGL((assign_small_kernel<V, true, true, 16>), dim3(grid), dim3(16 * 64), slds, s,      \
-                               codes, N, K, E32, plut, th, rpl, copies, A, flags, flag_cnt, part, part_cnt, z1,  \
-                               nz1);                                                                      \
-        else if (fuse)                                                                                            \
-            hipLaunchKernelGGL((assign_small_kernel<V, true, false, 16>), dim3(grid), dim3(16 * 64), slds, s,     \
                                codes, N, K, E32, plut, th, rpl, copies, A, flags, flag_cnt, part, part_cnt, z1,  \
                                nz1);                                                                      \
         else                                                                                                      \
@@ -771,28 +338,9 @@ hipError_t launch_assign_mfma(hipStream_t s, int grid, bool fuse, const uint8_t 
 #undef QVQ_SMALL
         return hipGetLastError();
     }
-    // the 32x32x16 form (k_mf32.hip) unless QVQ_MF32=0 (A/B: this file's 16x16x32 form)
-    static const bool mf32 = !(std::getenv("QVQ_MF32") && std::getenv("QVQ_MF32")[0] == '0');
-    if (mf32 && mf32_fits(K, fuse))
-        return launch_assign_mf32(s, grid, fuse, codes, N, cb_rows, K, C32, plut, th, A, flags, flag_cnt, part,
-                                  part_cnt, perm, tint, z1, nz1);
-    if (nz1) {   // the 16x16x32 form (ablation) does not clear copy 1 itself
-        const hipError_t e = hipMemsetAsync(z1, 0, (size_t)nz1 * 8, s);
-        if (e != hipSuccess) return e;
-    }
-    // 4-code-vector units while the pair loop is short (the recompute dominates): up to
-    // K = QVQ_U4_MAXK (default 256)
-    static const uint32_t u4_max = std::getenv("QVQ_U4_MAXK") ? (uint32_t)std::atoi(std::getenv("QVQ_U4_MAXK")) : 256;
-    const bool u4 = K <= u4_max;
-    if (fuse) {
-        if (u4) fn = staged ? launch_mfma_variant<true, true, 0, true> : launch_mfma_variant<true, false, 0, true>;
-        else fn = staged ? launch_mfma_variant<true, true, 0, false> : launch_mfma_variant<true, false, 0, false>;
-    } else {
-        if (u4) fn = staged ? launch_mfma_variant<false, true, 0, true> : launch_mfma_variant<false, false, 0, true>;
-        else fn = staged ? launch_mfma_variant<false, true, 0, false> : launch_mfma_variant<false, false, 0, false>;
-    }
-    fn(s, grid, lds, codes, N, cb_rows, K, C32, plut, th, A, flags, flag_cnt, part, part_cnt);
-    return hipGetLastError();
+    // the 32x32x16 form (k_mf32.hip)
+    return launch_assign_mf32(s, grid, fuse, codes, N, cb_rows, K, C32, plut, th, A, flags, flag_cnt, part, part_cnt,
+                              perm, tint, z1, nz1);
 }
 
 // =======================================================================================
@@ -1290,9 +838,8 @@ hipError_t launch_recheck(hipStream_t s, int num_cu, const uint8_t *codes, uint3
     const size_t cb = (size_t)K * recheck_c32_stride(Dp) * 4;
     const bool staged = base + cb <= RECHECK_LDS;
     const size_t lds = base + (staged ? cb : 0);
-    // too big for LDS: the chunked sweep for the widths it is built for (QVQ_RECHECK_CHUNKED=0: A/B)
-    static const bool chunked = !(std::getenv("QVQ_RECHECK_CHUNKED") && std::getenv("QVQ_RECHECK_CHUNKED")[0] == '0');
-    if (!staged && chunked && (Dp == 12 || Dp == 48)) {
+    // too big for LDS: the chunked sweep for the widths it is built for
+    if (!staged && (Dp == 12 || Dp == 48)) {
         const size_t clds = base + (size_t)RC_CHUNK * recheck_c32_stride(Dp) * 4;
         if (Dp == 12)
             hipLaunchKernelGGL(recheck_chunked_kernel<12>, dim3(num_cu), dim3(RECHECK_THREADS), clds, s, codes, Dp, D,
@@ -1335,15 +882,12 @@ hipError_t launch_kd_resolve(hipStream_t s, const uint8_t *codes, uint32_t Dp, u
     int W = kd.depth > 0 ? kd_waves(kd, K) : 0;
     if (W == 0) return hipErrorInvalidValue;
     // big K * D (C3 level 10, C4 from K = 256): a block per tie, its 16 waves on the point
-    // distances (QVQ_KDR_WHOLE=0: a wave per tie throughout, A/B)
-    static const bool whole_ok = !(std::getenv("QVQ_KDR_WHOLE") && std::getenv("QVQ_KDR_WHOLE")[0] == '0');
-    const bool whole = whole_ok && (size_t)K * D >= 8192;
+    // distances
+    const bool whole = (size_t)K * D >= 8192;
     if (whole) W = 1;
     const size_t lds = kd_tree_bytes(kd) + (size_t)W * kd_wave_bytes(kd, K);
     const KdArgs a{codes, Dp, D, ties, C64, K, lut64, kd, A, xslab, xcnt, plut, xsums};
-    static const int blocks = std::getenv("QVQ_KDR_BLOCKS") ? std::max(1, std::atoi(std::getenv("QVQ_KDR_BLOCKS")))
-                                                             : KDR_BLOCKS;   // ablation
-    hipLaunchKernelGGL(kd_resolve_kernel, dim3(blocks), dim3(whole ? 64 * KDR_MAX_WAVES : 64 * W), lds, s, a, tie_cnt,
+    hipLaunchKernelGGL(kd_resolve_kernel, dim3(KDR_BLOCKS), dim3(whole ? 64 * KDR_MAX_WAVES : 64 * W), lds, s, a, tie_cnt,
                        W, whole ? 1 : 0);
     return hipGetLastError();
 }
@@ -1374,8 +918,7 @@ hipError_t launch_kd_reduce(hipStream_t s, const uint8_t *codes, uint32_t Dp, ui
                             const uint32_t *part_cnt, uint32_t G, uint32_t nsub, uint64_t *sums, uint64_t *sums1) {
     int W = kd.depth > 0 ? kd_waves(kd, K) : 0;
     if (W == 0 || nsub > G) return hipErrorInvalidValue;
-    static const bool whole_ok = !(std::getenv("QVQ_KDR_WHOLE") && std::getenv("QVQ_KDR_WHOLE")[0] == '0');
-    const bool whole = whole_ok && (size_t)K * D >= 8192;
+    const bool whole = (size_t)K * D >= 8192;
     if (whole) W = 1;
     const size_t lds = std::max(kd_tree_bytes(kd) + (size_t)W * kd_wave_bytes(kd, K), (size_t)2 * 16 * 64 * 8);
     // sums1 (the finalize's copy 1) takes the ties' moves

@@ -343,10 +343,8 @@ size_t exact_sort_temp_bytes(uint64_t N) {
 hipError_t launch_exact_centroids(hipStream_t s, const double *X, uint64_t N, uint32_t D, const uint32_t *A, uint32_t K,
                                   uint32_t *keys_out, uint32_t *iota, uint32_t *order, uint32_t *koff, void *temp,
                                   size_t temp_bytes, double *C, uint64_t *cnt) {
-    static const bool thread_chains = std::getenv("QVQ_EXACT_CHAINS") && !std::strcmp(std::getenv("QVQ_EXACT_CHAINS"), "thread");   // A/B
-    static const uint32_t lds_max_k = std::getenv("QVQ_EXACT_LDS_MAXK") ? (uint32_t)std::atoi(std::getenv("QVQ_EXACT_LDS_MAXK"))
-                                                                        : KC_MAX_K;   // A/B
-    const bool lds_chains = !thread_chains && D <= 64 && (!A || K <= lds_max_k);
+    // LDS-staged chains (a thread per chain only beyond their limits: D > 64 or K > KC_MAX_K)
+    const bool lds_chains = D <= 64 && (!A || K <= KC_MAX_K);
     const size_t lds_bytes = lds_chains ? 2 * (size_t)(KC_TILE_BYTES / 8 / D) * D * 8 : 0;
     if (!A) {   // the mean: every row, in order
         if (lds_chains)

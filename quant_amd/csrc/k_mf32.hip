@@ -453,7 +453,7 @@ __global__ __launch_bounds__(M32_THREADS) void assign_mf32_kernel(
                     }
                     atomicAdd(&cnt[cp * m32_cnt_stride(K, copies) + rk], 1u);
                 }
-            } else if (K <= th.runs_max_k) {
+            } else {
                 uint32_t v[MF_D + 1];
 #pragma unroll
                 for (int d = 0; d < MF_D; d++) {
@@ -469,14 +469,6 @@ __global__ __launch_bounds__(M32_THREADS) void assign_mf32_kernel(
                                   (unsigned long long)((((uint64_t)(v[d] >> 16)) << 32) | (v[d] & 0xFFFF)));
                     atomicAdd(&cnt[rk], v[MF_D]);
                 }
-            } else if (valid) {
-#pragma unroll
-                for (int d = 0; d < MF_D; d++) {
-                    const uint32_t b = (own[d / 4] >> (8 * (d % 4))) & 0xFF;
-                    atomicAdd((unsigned long long *)&sums[(uint32_t)d * m32_kstride(K) + rk],
-                              (unsigned long long)((uint64_t)(b ^ 0x80u) << 32 | lo8_at0[b]));
-                }
-                atomicAdd(&cnt[rk], 1u);
             }
         }
     }
@@ -732,25 +724,19 @@ hipError_t launch_assign_mf32(hipStream_t s, int grid, bool fuse, const uint8_t 
     const bool prune = perm && tint;
     if (prune && !mf32_prune_fits(K, fuse)) return hipErrorInvalidValue;
     const bool staged = m32_lds_layout(K, fuse, true, 1, prune).total <= M32_LDS_MAX;
-    // sums copies (fused, 64 <= K <= 512 by default: QVQ_SUM_COPIES_MINK / _MAXK): the most, up
-    // to 16, that fit.  With the padded copy strides, C3: K = 64 / 128 / 256 / 512 -6 / -22 /
-    // -19 / -16 us against the wave run reduction; K = 1024 has no room for a second copy.
-    static const uint32_t copies_mink =
-        std::getenv("QVQ_SUM_COPIES_MINK") ? (uint32_t)std::atoi(std::getenv("QVQ_SUM_COPIES_MINK")) : 64;
-    static const uint32_t copies_maxk =
-        std::getenv("QVQ_SUM_COPIES_MAXK") ? (uint32_t)std::atoi(std::getenv("QVQ_SUM_COPIES_MAXK")) : 512;
+    // sums copies (fused, 64 <= K <= 512): the most, up to 16, that fit.  With the padded copy
+    // strides, C3: K = 64 / 128 / 256 / 512 -6 / -22 / -19 / -16 us against the wave run
+    // reduction; K = 1024 has no room for a second copy (the run reduction at the pruned K = 256:
+    // 123.3-123.9 vs 113.6-116.2 us, profiles/r05ap).
     uint32_t copies = 1;
-    if (fuse && K >= copies_mink && K <= copies_maxk)
+    if (fuse && K >= 64 && K <= 512)
         while (copies < 16 && m32_lds_layout(K, fuse, staged, copies * 2, prune).total <= M32_LDS_MAX) copies *= 2;
     const size_t lds = m32_lds_layout(K, fuse, staged, copies, prune).total;
     // 4-code-vector units while the tile loop is short (the recompute dominates); K = 256 takes
-    // 8-code-vector units, which the pruned search needs (QVQ_U4_MAXK=256 QVQ_PRUNE_MINK=512: the
-    // unpruned 4-unit search there, A/B: 129.2 / 123.4 vs 112.7 / 114.1 us, profiles/r05al)
-    static const uint32_t u4_max =
-        std::getenv("QVQ_U4_MAXK") ? (uint32_t)std::atoi(std::getenv("QVQ_U4_MAXK")) : 128;
-    const bool u4 = K <= u4_max;
-    // unit tags: ids t * NU + q < (Kp / 32) * NU per lane; QVQ_MF32_TAG=0 tracks them apart
-    static const bool tag = !(std::getenv("QVQ_MF32_TAG") && std::getenv("QVQ_MF32_TAG")[0] == '0');
+    // 8-code-vector units, which the pruned search needs (the unpruned 4-unit search there:
+    // 129.2 / 123.4 vs 112.7 / 114.1 us, profiles/r05al)
+    const bool u4 = K <= 128;
+    // unit tags: ids t * NU + q < (Kp / 32) * NU per lane fit the low mantissa bits up to 12 bits
     const uint32_t units = ((K + 31) / 32) * (u4 ? 4 : 2);
     uint32_t idbits = 0;
     while ((1u << idbits) < units) idbits++;
@@ -770,7 +756,7 @@ hipError_t launch_assign_mf32(hipStream_t s, int grid, bool fuse, const uint8_t 
     if (prune && !u4 && idbits <= 12) {   // pruned search: 8-code-vector units, tagged
         if (fuse) fn = staged ? launch_mf32_variant<true, true, 8, true, true> : launch_mf32_variant<true, false, 8, true, true>;
         else fn = staged ? launch_mf32_variant<false, true, 8, true, true> : launch_mf32_variant<false, false, 8, true, true>;
-    } else if (tag && idbits <= 12) {
+    } else if (idbits <= 12) {
         QVQ_MF32_PICK(true)
     } else {
         QVQ_MF32_PICK(false)

@@ -95,8 +95,7 @@ __global__ __launch_bounds__(256) void tile22_kernel(const uint32_t *__restrict_
 
 hipError_t launch_tile(hipStream_t s, const uint8_t *rgb, uint8_t *codes, uint32_t n_images, uint32_t xSize,
                        uint32_t ySize, uint32_t bw, uint32_t bh, uint32_t D, uint32_t Dp, uint8_t pad) {
-    static const bool generic = std::getenv("QVQ_TILE_GENERIC") != nullptr;   // A/B
-    if (!generic && bw == 2 && bh == 2 && xSize % 2 == 0 && ySize % 4 == 0 && ((uintptr_t)rgb & 3) == 0) {
+    if (bw == 2 && bh == 2 && xSize % 2 == 0 && ySize % 4 == 0 && ((uintptr_t)rgb & 3) == 0) {
         const uint32_t ppr = ySize / 4, wpr = ySize * 3 / 4;
         const uint64_t ppi = (uint64_t)(xSize / 2) * ppr, wpi = (uint64_t)xSize * wpr;
         const uint64_t total = ppi * n_images;
@@ -605,8 +604,7 @@ hipError_t launch_sorted_sums(hipStream_t s, uint32_t Dp, uint32_t G, const uint
     const uint64_t rpg = (N + G - 1) / G;
     hipLaunchKernelGGL(sort_hist_kernel, dim3(G), dim3(SRT_THREADS), K * 4, s, A, N, K, rpg, hist, sums,
                        2 * (uint64_t)K * D + K);
-    static const bool cs4 = !(std::getenv("QVQ_COLSCAN4") && std::getenv("QVQ_COLSCAN4")[0] == '0');   // A/B
-    if (cs4 && G <= 4 * CS_QG)
+    if (G <= 4 * CS_QG)
         hipLaunchKernelGGL(sort_colscan4_kernel, dim3((K + 63) / 64), dim3(256), 0, s, hist, G, K, tot);
     else
         hipLaunchKernelGGL(sort_colscan_kernel, dim3((K + 255) / 256), dim3(256), 0, s, hist, G, K, tot);
@@ -870,7 +868,7 @@ hipError_t launch_mean_sums(hipStream_t s, uint32_t Dp, const uint8_t *codes, ui
     if (n_zero > MEAN_THREADS) return hipErrorInvalidValue;
     // one block per CU (few same-address atomics at the end), more only where a thread would
     // otherwise take over MEAN_ROWS_PER_THREAD rows (u32 fields)
-    static const uint64_t grid_cap = std::getenv("QVQ_MEAN_GRID") ? std::atoll(std::getenv("QVQ_MEAN_GRID")) : 256;
+    constexpr uint64_t grid_cap = 256;
     const uint64_t per_block = MEAN_THREADS * MEAN_ROWS_PER_THREAD;
     const uint64_t grid_min = (N + per_block - 1) / per_block;
     const uint64_t grid = std::max<uint64_t>(std::max<uint64_t>(grid_min, 1),
@@ -1780,12 +1778,12 @@ hipError_t launch_decode(hipStream_t s, const uint8_t *cb, uint32_t K, uint32_t 
         const bool lds = cbB <= 48 * 1024;
         // with the codebook staged in LDS, a block loops over several 256-item rounds (C3: 8192
         // one-round blocks staged 100 MB of codebook copies for 67 MB of output)
-        static const uint64_t cap = std::getenv("QVQ_DECODE_GRID") ? std::atoll(std::getenv("QVQ_DECODE_GRID")) : 2048;
+        constexpr uint64_t cap = 2048;
         const int grid = (int)std::max<uint64_t>(1, std::min<uint64_t>((items + 255) / 256, lds ? cap : 1u << 16));
         const size_t ldsB = lds ? (cbB + 15) & ~(size_t)15 : 0;
-        if (a.overhang == 0 && (h == 1 || h == 2 || h == 4 || h == 8) && !std::getenv("QVQ_DECODE_GENERIC")) {
+        if (a.overhang == 0 && (h == 1 || h == 2 || h == 4 || h == 8)) {
             // wave-contiguous output chunks need whole waves inside one raster row: 64 | ys / 8
-            const bool coal = (ys / 8) % 64 == 0 && !std::getenv("QVQ_DECODE_NOCOAL");
+            const bool coal = (ys / 8) % 64 == 0;
             const uint32_t soff = (uint32_t)ldsB;
             const size_t lb = ldsB + (coal ? 4 * 1536 : 0);
 #define QVQ_DEC_H(HV)                                                                                                  \

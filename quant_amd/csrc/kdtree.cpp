@@ -765,9 +765,7 @@ void RefKDTree::cert_agg_dims(size_t i, int d0, int d1) const {
     double *__restrict mnu = &agg_[i * D * 4], *__restrict mxu = mnu + D, *__restrict mnk = mxu + D,
                        *__restrict mxk = mnk + D;
     const Node &n = nodes_[i];
-    // (QVQ_AGG_ROWS=1: the leaf rows one at a time into the node's aggregates, A/B)
-    static const bool rows = std::getenv("QVQ_AGG_ROWS") && std::getenv("QVQ_AGG_ROWS")[0] == '1';
-    const bool avx2 = has_avx2() && !rows;
+    const bool avx2 = has_avx2();
     if (n.leaf && avx2) {
         const int e = agg_leaf_avx2(pts_, agg_k_, agg_known_, vind_.data() + n.left, n.right - n.left, D, d0, d1, mnu,
                                     mxu, mnk, mxk);

@@ -87,3 +87,39 @@ def test_quantizer_plugin_matches_oracle(test_api, tmp_path):
     np.testing.assert_array_equal(np.fromfile(af, np.uint32), A_x)
     np.testing.assert_array_equal(np.fromfile(cf, np.float64).reshape(C_x.shape), C_x)
     assert abs(float(r.stdout.split()[1]) - d_x) <= 1e-9 * abs(d_x)
+
+
+@pytest.mark.gpu
+def test_compress_near_byte_flip_takes_reference_bits(test_api, tmp_path):
+    """the .quant codebook bytes are round((c - 128) * 255) of the reference's
+    Kahan centroids (src/ColorSpace.cpp:23-28, src/Compressor.cpp:12-29).  The engine's exact-sum
+    centroids can differ by a few ulps, so compress fetches the reference's bits (qvq_update_kahan)
+    whenever a component lies within 16 ulps of a point where the byte changes.  Here one cell's
+    mean is exactly 117.5 / 255 in every channel (rows at u = 117 and 118, half each), the
+    neighbourhood of such a point: the file must hold the Kahan oracle's bytes."""
+    S = 64
+    rng = np.random.default_rng(117)
+    n = S * S
+    u = np.empty((n, 3), np.int64)
+    dark = np.zeros(n, bool)
+    dark[rng.permutation(n)[:n // 2]] = True
+    for ch in range(3):
+        v = np.array([117] * (n // 4) + [118] * (n // 4))
+        rng.shuffle(v)
+        u[dark, ch] = v
+        u[~dark, ch] = rng.integers(225, 250, n - n // 2)
+    rgb = ((u - 128) & 0xFF).astype(np.uint8).reshape(-1)
+    ppm, quant, dec = str(tmp_path / "in.ppm"), str(tmp_path / "out.quant"), str(tmp_path / "dec.ppm")
+    _write_ppm(ppm, rgb, S, S)
+    r = subprocess.run([test_api, "compress", ppm, quant, dec, "1", "1", "1", "1"], capture_output=True, text=True,
+                       timeout=300)
+    assert r.returncode == 0, r.stderr
+    X, _ = oracle.tile(rgb, S, S, 1, 1)
+    C_k, A_k, _ = oracle.lbg(X, 1, sum_mode=0)
+    C_x = oracle.centroids(X, A_k, 2, sum_mode=1)
+    # the dark cell sits next to a byte boundary: +/- 16 ulps of its exact-sum centroid straddle it
+    c = C_x[np.argmin(C_x[:, 0]), 0]
+    w = 16 * np.spacing(c)
+    assert oracle.codebook_bytes(np.array([[c - w]]))[0, 0] != oracle.codebook_bytes(np.array([[c + w]]))[0, 0]
+    expected = oracle.quant_file_bytes(oracle.codebook_bytes(C_k), A_k, 1, 1, S, S, 1, 1)
+    assert open(quant, "rb").read() == expected

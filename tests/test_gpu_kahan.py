@@ -221,3 +221,21 @@ def test_certificate_cells_through_segment_functions():
     assert len(res) == 8
     for r in res:
         assert r["A_ok"] and r["C_ok"] and r["again_ok"], r
+
+
+def test_late_tree_job_reads_its_own_codebook():
+    """the r05m race made deterministic.  A synchronous level's tree job
+    copies the codebook its level's search ran on from mapped memory, while the main thread has
+    already enqueued the level's own finalize, which publishes the next level's codebook.
+    QVQ_TREE_JOB_DELAY_MS=20 makes every job late past that finalize.  With the published codebooks
+    double-buffered by level parity (the fix, fc64269) the indices are the reference's; with the one
+    buffer of before (QVQ_CB_SINGLE=1, test only) the late jobs build their trees over the next
+    level's code vectors and some tie rows come out wrong."""
+    cases = CORPUS["noise_seeds"][:2] + CORPUS["found"][:6]
+    good = _env_worker({"QVQ_SPECULATE": "0", "QVQ_TREE_JOB_DELAY_MS": "20"}, cases)
+    assert len(good) == len(cases)
+    for r in good:
+        assert r["A_ok"] and r["C_ok"] and r["again_ok"], r
+    bad = _env_worker({"QVQ_SPECULATE": "0", "QVQ_TREE_JOB_DELAY_MS": "20", "QVQ_CB_SINGLE": "1"}, cases)
+    assert len(bad) == len(cases)
+    assert any(not (r["A_ok"] and r["again_ok"]) for r in bad), "the single buffer should show the race"

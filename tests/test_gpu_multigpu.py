@@ -235,3 +235,22 @@ def test_one_rank_failure_redoes_every_rank(corpus_expect, tmp_path):
         assert len(rd) == 1
         redone += rd.pop()
     assert redone >= len([c for c in CASES if c["bits"] >= 4])
+
+
+@pytest.mark.timeout(300)
+def test_open_row_without_cells_redoes_every_rank(corpus_expect, tmp_path):
+    """a deferred check whose open rows want no cell (nothing summed over the ranks can
+    settle them) must fail the level, not be skipped at the vote with its speculative indices kept.
+    QVQ_KAHAN_OPEN_LEVEL=-1 leaves a row of every tie level open with no cell wanted, on both
+    ranks: every corpus case (each has tie rows) redoes the quantize and still returns the
+    reference's indices."""
+    res = _run_ranks(2, "corpus", tmp_path, env={"QVQ_KAHAN_OPEN_LEVEL": "-1"})
+    redone = 0
+    for i, (X, A_k, A_x, C0, d0) in enumerate(corpus_expect):
+        np.testing.assert_array_equal(np.concatenate([r["A%d" % i] for r in res]), A_k, err_msg="case %d" % i)
+        for r in res:
+            np.testing.assert_array_equal(r["C%d" % i], C0, err_msg="case %d" % i)
+        rd = {int(r["redo%d" % i][0]) for r in res}
+        assert len(rd) == 1
+        redone += rd.pop()
+    assert redone == len(CASES)
