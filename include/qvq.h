@@ -208,6 +208,13 @@ QVQ_API qvq_status qvq_set_timeout(qvq_ctx *ctx, double seconds);
 QVQ_API qvq_status qvq_set_timing(qvq_ctx *ctx, int level);
 QVQ_API qvq_status qvq_get_timings(const qvq_ctx *ctx, qvq_timings *out);
 
+/* Test entry: the reference kd-tree of C (K x dim fp64) built on the device (the build qvq_lbg
+ * uses for its 48-D levels) against the host's RefKDTree, node for node; result 0 equal, 1
+ * different (qvq_last_error names the first difference), 2 the device build gave up.  build_ms
+ * (4 doubles): the launch, then its phases (big nodes, small subtrees, the images). */
+QVQ_API qvq_status qvq_kdtree_device_check(qvq_ctx *ctx, const double *C, uint32_t K, uint32_t dim, double *build_ms,
+                                           uint32_t *result);
+
 /* Host-only helpers (no GPU needed), exported for tests of the host logic. */
 /* The reference kd-tree's answer for nq queries (nanoflann semantics, see kdtree.hpp). */
 QVQ_API qvq_status qvq_host_kdtree_nn(const double *C, uint32_t K, uint32_t dim, const double *Q, uint64_t nq,

@@ -44,7 +44,7 @@ EXPORTED = ["qvq_create", "qvq_destroy", "qvq_last_error", "qvq_version", "qvq_s
             "qvq_comm_unique_id", "qvq_comm_init", "qvq_set_timing", "qvq_get_timings", "qvq_host_kdtree_nn",
             "qvq_host_finalize", "qvq_host_row_terms", "qvq_decode", "qvq_decode_mse", "qvq_decode_device",
             "qvq_set_timeout", "qvq_host_wait_probe", "qvq_comm_init_host", "qvq_comm_info", "qvq_set_vectors_exact",
-            "qvq_update_kahan_split", "qvq_host_pool_stress"]
+            "qvq_update_kahan_split", "qvq_host_pool_stress", "qvq_kdtree_device_check"]
 
 COMM_NONE, COMM_RCCL, COMM_HOST = 0, 1, 2
 # int fn(void *buf, uint64_t count, int dtype, void *user) (qvq.h, qvq_comm_init_host)
@@ -83,6 +83,7 @@ def lib():
             "qvq_set_timing": ([P, i], i),
             "qvq_get_timings": ([P, ctypes.POINTER(_Timings)], i),
             "qvq_host_kdtree_nn": ([P, u32, u32, P, u64, P], i),
+            "qvq_kdtree_device_check": ([P, P, u32, u32, P, P], i),
             "qvq_host_finalize": ([P, P, P, u32, u32, i, P], i),
             "qvq_host_row_terms": ([P, u32, i, P, P], i),
             "qvq_decode": ([P, P, u32, P, u64, u32, u32, u32, u32, P], i),
@@ -231,6 +232,17 @@ class Engine:
 
     def assign_device_ptr(self):
         return lib().qvq_assign_device(self._h)
+
+    def kdtree_device_check(self, C):
+        """The reference kd-tree of C (K x D) built on the device against the host's, node for node:
+        (result, [launch ms, phase-1 ms, phase-2 ms, images ms], first difference); result 0 equal,
+        1 different, 2 the build gave up."""
+        C = np.ascontiguousarray(C, np.float64)
+        ms = np.zeros(4, np.float64)
+        res = np.zeros(1, np.uint32)
+        _check(lib().qvq_kdtree_device_check(self._h, _p(C), C.shape[0], C.shape[1], _p(ms), _p(res)), self._h)
+        why = lib().qvq_last_error(self._h).decode() if res[0] == 1 else ""
+        return int(res[0]), [round(float(x), 4) for x in ms], why
 
     def set_timing(self, level=-1):
         """HIP events around the search of every level (-1), none (-2) or level+1 only."""

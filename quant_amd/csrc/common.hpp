@@ -282,6 +282,13 @@ hipError_t launch_recheck_mf32(hipStream_t s, int num_cu, const uint8_t *codes, 
 // distances fit the LDS.
 bool kd_resolve_fits(const KdView &kd, uint32_t K);
 // kd_reduce_kernel: launch_kd_resolve (ties into copy 1 of sums) + launch_reduce (into copy 0).
+// The reference kd-tree of P (K x D fp64, row-major) built on the device (k_kdbuild.hip), one
+// workgroup: vind / nodes / nbox / cbox are scratch of K, 2K, 2K x 2D, 2K x 2D entries; flat gets
+// kd_resolve's image (lo | hi | KdNodeDev[n] | vind, tree_bytes(K, D) at most), himg (mapped host
+// memory, kdb_host_layout) the whole tree, its header's seq set to seq last.
+bool kd_build_fits(uint32_t K, uint32_t D);
+hipError_t launch_kd_build(hipStream_t s, const double *P, uint32_t K, uint32_t D, uint32_t *vind, KdbNode *nodes,
+                           double *nbox, double *cbox, uint8_t *flat, uint8_t *himg, uint64_t seq);
 bool kd_reduce_fits(const KdView &kd, uint32_t K);
 hipError_t launch_kd_reduce(hipStream_t s, const uint8_t *codes, uint32_t Dp, uint32_t D, const uint32_t *ties,
                             const unsigned *tie_cnt, const double *C64, uint32_t K, const double *lut64,

@@ -79,6 +79,9 @@ bool make_terms(int cs, Terms &t) {
 using namespace qvq;
 
 constexpr uint32_t SCHED_COUNTERS = 2 * 33 + 2, N_COUNTERS = SCHED_COUNTERS + 2;
+// Levels whose kd-tree the device builds (k_kdbuild.hip, beside the search): K * D from this up
+// (C4's 48-D levels from K = 512; C3's 12-D trees take the host well under 0.1 ms).
+constexpr uint64_t KDB_MIN_KD = 16384;
 
 namespace qvq {
 // One level's tie certificate (engine.cpp certify_rows): the level's distinct tie
@@ -210,6 +213,16 @@ struct qvq_ctx {
     uint64_t seq = 0;
     uint8_t *h_tree[2] = {nullptr, nullptr}, *dh_tree[2] = {nullptr, nullptr};
     uint8_t *d_tree = nullptr;   // device copy of the level's tree image (one DMA per level)
+    // the level's kd-tree built on the device (k_kdbuild.hip) on kstream, beside the search:
+    // scratch (vind, nodes, boxes), the mapped host image of the whole tree, its launch number
+    hipStream_t kstream = nullptr;
+    hipEvent_t ev_kcb = nullptr, ev_kdb = nullptr;
+    uint32_t *d_kdb_vind = nullptr;
+    KdbNode *d_kdb_nodes = nullptr;
+    double *d_kdb_nbox = nullptr, *d_kdb_cbox = nullptr;
+    uint8_t *h_kdb = nullptr, *dh_kdb = nullptr;
+    uint32_t kdb_cap = 0;   // code vectors the scratch takes (0: none)
+    uint64_t kdb_seq = 0;
     std::vector<double> cb_local;   // host copy of the published codebook for the tree build
     std::vector<uint32_t> cnt_local;   // ... and of its parent cells' row counts (empty: not known)
     std::unique_ptr<RefKDTree> tree;   // the last level's tree over cb_local
@@ -457,9 +470,17 @@ void free_levels(qvq_ctx *ctx) {
     }
     dfree(ctx->d_tree);
     ctx->tree_cap = 0;
+    dfree(ctx->d_kdb_vind);
+    dfree(ctx->d_kdb_nodes);
+    dfree(ctx->d_kdb_nbox);
+    dfree(ctx->d_kdb_cbox);
+    if (ctx->h_kdb) (void)hipHostFree(ctx->h_kdb);
+    ctx->h_kdb = ctx->dh_kdb = nullptr;
+    ctx->kdb_cap = 0;
     ctx->Kcap = 0;
 }
 
+bool device_tree_on();
 // Flattened tree: root box lo[D], hi[D] | nodes[<= 2K] | vind[K].
 uint64_t tree_bytes(uint32_t K, uint32_t D) {
     return 16ull * D + (2ull * K + 1) * sizeof(KdNodeDev) + 4ull * K;
@@ -592,6 +613,22 @@ qvq_status ensure_levels(qvq_ctx *ctx, uint32_t Kmax) {
         HIPCHK(hipHostGetDevicePointer((void **)&ctx->dh_tree[b], ctx->h_tree[b], 0));
     }
     HIPCHK(hipMalloc(&ctx->d_tree, ctx->tree_cap));
+    {   // the device tree build's scratch (levels of up to KDB_MAXK code vectors)
+        const uint32_t Kb = std::min<uint32_t>(Kmax, KDB_MAXK);
+        if (device_tree_on() && kd_build_fits(Kb, ctx->D) && (uint64_t)Kmax * ctx->D >= KDB_MIN_KD) {
+            HIPCHK(hipMalloc(&ctx->d_kdb_vind, (uint64_t)Kb * 4));
+            HIPCHK(hipMalloc(&ctx->d_kdb_nodes, 2ull * Kb * sizeof(KdbNode)));
+            HIPCHK(hipMalloc(&ctx->d_kdb_nbox, 2ull * Kb * 2 * ctx->D * 8));
+            HIPCHK(hipMalloc(&ctx->d_kdb_cbox, 2ull * Kb * 2 * ctx->D * 8));
+            HIPCHK(hipHostMalloc(&ctx->h_kdb, kdb_host_layout(Kb, ctx->D).total, mflags));
+            HIPCHK(hipHostGetDevicePointer((void **)&ctx->dh_kdb, ctx->h_kdb, 0));
+            std::memset(ctx->h_kdb, 0, sizeof(KdbHeader));
+            ctx->kdb_cap = Kb;
+            if (!ctx->kstream) HIPCHK(hipStreamCreateWithFlags(&ctx->kstream, hipStreamNonBlocking));
+            if (!ctx->ev_kcb) HIPCHK(hipEventCreateWithFlags(&ctx->ev_kcb, hipEventDisableTiming));
+            if (!ctx->ev_kdb) HIPCHK(hipEventCreateWithFlags(&ctx->ev_kdb, hipEventDisableTiming));
+        }
+    }
     ctx->Kcap = Kmax;
     return QVQ_OK;
 }
@@ -929,6 +966,77 @@ void build_tree(qvq_ctx *ctx, const double *hC, uint32_t K, int buf, KdView &kd)
     ctx->tree_kd = kd;
 }
 
+CommState probe_comm(qvq_ctx *ctx, std::string &msg);
+qvq_status wait_failed(qvq_ctx *ctx, qvq_status st);
+
+// The device build of a level's tree (k_kdbuild.hip), 48-D levels from K = 512 up to KDB_MAXK:
+// opt-in (QVQ_KDTREE=device).  Bit-identical to the host build (tests/test_gpu_kdbuild.py), but
+// slower than it on the GPU box's host: K = 4096 3.7 ms vs 1.8 ms, K = 2048 2.2 vs 0.7 (a node
+// costs ~10-20 us of dependent device round trips and barriers, and C4's trees have ~300 big
+// nodes on one serial path), so the host build, overlapping the search, stays the default
+// (DESIGN.md 8).
+bool device_tree_on() {
+    static const bool on = env_is("QVQ_KDTREE", "device");
+    return on;
+}
+bool use_device_tree(const qvq_ctx *ctx, uint32_t K) {
+    return device_tree_on() && ctx->kdb_cap >= K && !ctx->exact && kd_build_fits(K, ctx->D) &&
+           (uint64_t)K * ctx->D >= KDB_MIN_KD;
+}
+
+// Enqueue the device build of the tree over the K code vectors in d_C64_split on kstream, after
+// the work already on the context's stream (the finalize that wrote them); the search then runs
+// beside it.
+qvq_status start_device_tree(qvq_ctx *ctx, uint32_t K) {
+    HIPCHK(hipEventRecord(ctx->ev_kcb, ctx->stream));
+    HIPCHK(hipStreamWaitEvent(ctx->kstream, ctx->ev_kcb, 0));
+    HIPCHK(launch_kd_build(ctx->kstream, ctx->d_C64_split, K, ctx->D, ctx->d_kdb_vind, ctx->d_kdb_nodes,
+                           ctx->d_kdb_nbox, ctx->d_kdb_cbox, ctx->d_tree, ctx->dh_kdb, ++ctx->kdb_seq));
+    HIPCHK(hipEventRecord(ctx->ev_kdb, ctx->kstream));
+    return QVQ_OK;
+}
+
+// The device build's tree for the level: waits (bounded) for its image, makes the context's
+// stream wait for the build (d_C64_split is rewritten by the level's finalize), and imports it as
+// ctx->tree over ctx->cb_local (which the caller filled) with its device view in kd.  false: the
+// build failed (the caller builds on the host).
+qvq_status finish_device_tree(qvq_ctx *ctx, uint32_t K, KdView &kd, bool &ok) {
+    ok = false;
+    kd = KdView{};
+    const KdbHeader *h = reinterpret_cast<const KdbHeader *>(ctx->h_kdb);
+    std::string err;
+    const qvq_status st = wait_until(
+        [&] { return *reinterpret_cast<const volatile uint64_t *>(&h->seq) >= ctx->kdb_seq; },
+        [&](std::string &m) {
+            const hipError_t q = hipStreamQuery(ctx->kstream);
+            if (q == hipSuccess) return StreamState::Drained;
+            if (q == hipErrorNotReady) return StreamState::Running;
+            m = hipGetErrorString(q);
+            return StreamState::Failed;
+        },
+        [&](std::string &m) { return probe_comm(ctx, m); }, ctx->timeout_s, err);
+    if (st != QVQ_OK) return wait_failed(ctx, fail(ctx, st, "device kd-tree build: " + err));
+    std::atomic_thread_fence(std::memory_order_acquire);
+    HIPCHK(hipStreamWaitEvent(ctx->stream, ctx->ev_kdb, 0));
+    if (h->status != 1) return QVQ_OK;
+    ctx->tree.reset(new RefKDTree(ctx->cb_local.data(), K, (int)ctx->D, ctx->h_kdb));
+    KdView t;
+    t.depth = (int)h->depth;
+    t.n_nodes = h->n_nodes;
+    const uint64_t bytes = 16ull * ctx->D + (uint64_t)h->n_nodes * sizeof(KdNodeDev) + 4ull * K;
+    ok = true;
+    if (bytes > ctx->tree_cap) return QVQ_OK;
+    t.bytes = (uint32_t)bytes;
+    if (!kd_resolve_fits(t, K)) return QVQ_OK;
+    const double *dlo = reinterpret_cast<const double *>(ctx->d_tree);
+    t.lo = dlo;
+    t.hi = dlo + ctx->D;
+    t.nodes = reinterpret_cast<const KdNodeDev *>(dlo + 2 * ctx->D);
+    t.vind = reinterpret_cast<const uint32_t *>(t.nodes + t.n_nodes);
+    kd = t;
+    return QVQ_OK;
+}
+
 // A deferred-tie level (qvq_lbg's Kahan path) needs its tree only when it has ties, which the
 // host learns after the search: the worker awaits the codebook's publication and builds the
 // tree while this thread enqueues the rest of the level; join_tree_job waits for it (ties)
@@ -1161,6 +1269,11 @@ qvq_status run_level(qvq_ctx *ctx, uint32_t K, int slot, bool sums_out, const do
     // HIP events around the search (each record costs a few us of GPU idle): every level,
     // one level, or none (qvq_set_timing)
     const bool timing = ctx->timing_level == -1 || ctx->timing_level == slot;
+    // the level's kd-tree on the device, beside the search (every CU holds a search workgroup
+    // and room for the build's)
+    const bool devtree = !defer_ties && use_device_tree(ctx, K);
+    qvq_status st;
+    if (devtree && (st = start_device_tree(ctx, K)) != QVQ_OK) return st;
     if (timing) HIPCHK(hipEventRecord(ctx->ev[slot][0], ctx->stream));
     if (use_mfma(ctx, K)) {
         const bool prune = ctx->perm_k == K;   // the order qvq_lbg's finalize left for this level
@@ -1201,7 +1314,6 @@ qvq_status run_level(qvq_ctx *ctx, uint32_t K, int slot, bool sums_out, const do
                               pruned ? ctx->d_tint : nullptr,
                               (float)((double)ctx->D / (ctx->terms.sx * ctx->terms.sx))));
     }
-    qvq_status st;
     if (defer_ties) {   // the level's tie count to the host, before the rest of the level runs
         ctx->pub_seq++;
         if (fused) {   // published by the slab reduce that follows (qvq_lbg): no launch of its own
@@ -1232,8 +1344,20 @@ qvq_status run_level(qvq_ctx *ctx, uint32_t K, int slot, bool sums_out, const do
     const auto tw1 = std::chrono::steady_clock::now();
     ctx->htrace.mark("K" + std::to_string(K) + " codebook seen, tree build");
     KdView kd;
-    build_tree(ctx, hC, K, slot & 1, kd);
-    ctx->htrace.mark("K" + std::to_string(K) + " tree built");
+    bool dev_ok = false;
+    if (devtree) {   // the host copies of the codebook and parent counts, then the device's tree
+        ctx->cb_local.assign(hC, hC + (size_t)K * ctx->D);
+        if ((hC == host_cb_of(ctx, 0) || hC == host_cb_of(ctx, 1)) && K >= 2) {
+            const uint32_t *pc = reinterpret_cast<const uint32_t *>(hC + (size_t)K * ctx->D);
+            ctx->cnt_local.assign(pc, pc + K / 2);
+        } else {
+            ctx->cnt_local.clear();
+        }
+        if ((st = finish_device_tree(ctx, K, kd, dev_ok)) != QVQ_OK) return st;
+        ctx->tree_kd = kd;
+    }
+    if (!dev_ok) build_tree(ctx, hC, K, slot & 1, kd);
+    ctx->htrace.mark("K" + std::to_string(K) + (dev_ok ? " device tree in" : " tree built"));
     ctx->tm.wait_ms[slot] = std::chrono::duration<double, std::milli>(tw1 - tw0).count();
     ctx->tm.tree_ms[slot] = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tw1).count();
     if (kd.depth > 0 && fused && kd_merge(ctx) && kd_reduce_fits(kd, K)) {
@@ -2097,6 +2221,12 @@ QVQ_API void qvq_destroy(qvq_ctx *ctx) {
     }
     (void)hipSetDevice(ctx->dev);
     if (ctx->stream) (void)hipStreamSynchronize(ctx->stream);
+    if (ctx->kstream) {
+        (void)hipStreamSynchronize(ctx->kstream);
+        (void)hipStreamDestroy(ctx->kstream);
+    }
+    if (ctx->ev_kcb) (void)hipEventDestroy(ctx->ev_kcb);
+    if (ctx->ev_kdb) (void)hipEventDestroy(ctx->ev_kdb);
     if (ctx->comm) ncclCommDestroy(ctx->comm);
     free_training(ctx);
     free_levels(ctx);
@@ -3052,6 +3182,85 @@ QVQ_API qvq_status qvq_host_kdtree_nn(const double *C, uint32_t K, uint32_t dim,
     if (!C || !Q || !out || K == 0 || dim == 0 || dim > 64) return QVQ_EINVAL;
     RefKDTree tree(C, K, (int)dim);
     for (uint64_t i = 0; i < nq; i++) out[i] = tree.nearest(Q + i * dim);
+    return QVQ_OK;
+}
+
+QVQ_API qvq_status qvq_kdtree_device_check(qvq_ctx *ctx, const double *C, uint32_t K, uint32_t dim, double *build_ms,
+                                           uint32_t *result) {
+    if (!ctx || !C || !result || K == 0 || dim == 0 || dim > 64) return QVQ_EINVAL;
+    GUARD(ctx);
+    if (!kd_build_fits(K, dim)) return fail(ctx, QVQ_EUNSUPPORTED, "device kd build: K or dim too large");
+    HIPCHK(hipSetDevice(ctx->dev));
+    const KdbHostLayout L = kdb_host_layout(K, dim);
+    double *dP = nullptr, *nbox = nullptr, *cbox = nullptr;
+    uint32_t *vind = nullptr;
+    KdbNode *nodes = nullptr;
+    uint8_t *flat = nullptr, *himg = nullptr, *dhimg = nullptr;
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    struct Free {
+        std::function<void()> f;
+        ~Free() { f(); }
+    } fr{[&] {
+        for (void *p : {(void *)dP, (void *)nbox, (void *)cbox, (void *)vind, (void *)nodes, (void *)flat})
+            if (p) (void)hipFree(p);
+        if (himg) (void)hipHostFree(himg);
+        if (e0) (void)hipEventDestroy(e0);
+        if (e1) (void)hipEventDestroy(e1);
+    }};
+    HIPCHK(hipMalloc(&dP, (uint64_t)K * dim * 8));
+    HIPCHK(hipMalloc(&nbox, 2ull * K * 2 * dim * 8));
+    HIPCHK(hipMalloc(&cbox, 2ull * K * 2 * dim * 8));
+    HIPCHK(hipMalloc(&vind, (uint64_t)K * 4));
+    HIPCHK(hipMalloc(&nodes, 2ull * K * sizeof(KdbNode)));
+    HIPCHK(hipMalloc(&flat, tree_bytes(K, dim)));
+    HIPCHK(hipHostMalloc(&himg, L.total, hipHostMallocMapped | hipHostMallocCoherent));
+    HIPCHK(hipHostGetDevicePointer((void **)&dhimg, himg, 0));
+    std::memset(himg, 0, sizeof(KdbHeader));
+    HIPCHK(hipEventCreate(&e0));
+    HIPCHK(hipEventCreate(&e1));
+    HIPCHK(hipMemcpy(dP, C, (uint64_t)K * dim * 8, hipMemcpyHostToDevice));
+    HIPCHK(hipEventRecord(e0, ctx->stream));
+    HIPCHK(launch_kd_build(ctx->stream, dP, K, dim, vind, nodes, nbox, cbox, flat, dhimg, 1));
+    HIPCHK(hipEventRecord(e1, ctx->stream));
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+    float ms = 0;
+    (void)hipEventElapsedTime(&ms, e0, e1);
+    const KdbHeader &h = *reinterpret_cast<const KdbHeader *>(himg);
+    if (build_ms) {   // the launch; phase 1, phase 2, the images (the kernel's 100 MHz stamps)
+        build_ms[0] = ms;
+        for (int i = 0; i < 3; i++) build_ms[1 + i] = (double)h.pad2[i] * 1e-5;
+    }
+    if (h.seq != 1 || h.status != 1) {
+        *result = 2;   // the build gave up (capacity): the engine builds on the host then
+        return QVQ_OK;
+    }
+    const RefKDTree dev(C, K, (int)dim, himg), host(C, K, (int)dim);
+    std::string why;
+    *result = host.same_as(dev, &why) ? 0u : 1u;
+    if (*result) ctx->err = "device kd-tree differs: " + why;
+    // the device image kd_resolve reads: the host flattening of the same tree, node ids aside
+    std::vector<uint8_t> fimg(16ull * dim + (uint64_t)h.n_nodes * sizeof(KdNodeDev) + 4ull * K);
+    HIPCHK(hipMemcpy(fimg.data(), flat, fimg.size(), hipMemcpyDeviceToHost));
+    const double *flo = reinterpret_cast<const double *>(fimg.data());
+    const KdNodeDev *fn = reinterpret_cast<const KdNodeDev *>(flo + 2 * dim);
+    const uint32_t *fv = reinterpret_cast<const uint32_t *>(fn + h.n_nodes);
+    const KdbNode *hn = reinterpret_cast<const KdbNode *>(himg + L.nodes);
+    const uint32_t *hv = reinterpret_cast<const uint32_t *>(himg + L.vind);
+    for (uint32_t i = 0; i < h.n_nodes && !*result; i++) {
+        const KdNodeDev &a = fn[i];
+        const KdbNode &b = hn[i];
+        const bool leaf = b.child1 < 0;
+        if (a.child1 != b.child1 || a.child2 != b.child2 || a.b != (int32_t)b.right ||
+            a.a != (int32_t)(leaf ? b.left : ((uint32_t)b.divfeat | b.left << 8)) || (!leaf && (a.lo != b.divlow || a.hi != b.divhigh))) {
+            *result = 1;
+            ctx->err = "device kd_resolve image differs at node " + std::to_string(i);
+        }
+    }
+    for (uint32_t i = 0; i < K && !*result; i++)
+        if (fv[i] != hv[i]) {
+            *result = 1;
+            ctx->err = "device kd_resolve image vind differs";
+        }
     return QVQ_OK;
 }
 

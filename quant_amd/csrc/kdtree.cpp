@@ -184,6 +184,92 @@ RefKDTree::RefKDTree(const double *pts, size_t K, int dim, const std::atomic<boo
     cols_ = nullptr;
 }
 
+RefKDTree::RefKDTree(const double *pts, size_t K, int dim, const uint8_t *img) : pts_(pts), dim_(dim), K_(K) {
+    static std::atomic<uint64_t> next_id{1};
+    id_ = next_id.fetch_add(1);
+    const KdbHeader &h = *reinterpret_cast<const KdbHeader *>(img);
+    const KdbHostLayout L = kdb_host_layout((uint32_t)K, (uint32_t)dim);
+    const KdbNode *dn = reinterpret_cast<const KdbNode *>(img + L.nodes);
+    const double *db = reinterpret_cast<const double *>(img + L.boxes);
+    const uint32_t *dv = reinterpret_cast<const uint32_t *>(img + L.vind);
+    const uint32_t nn = h.n_nodes;
+    // depth-first order, child 1 first: the host build's node numbering
+    std::vector<uint32_t> order, pre(nn, 0);
+    order.reserve(nn);
+    std::vector<uint32_t> st(1, 0);
+    while (!st.empty()) {
+        const uint32_t d = st.back();
+        st.pop_back();
+        pre[d] = (uint32_t)order.size();
+        order.push_back(d);
+        if (dn[d].child1 >= 0) {
+            st.push_back((uint32_t)dn[d].child2);
+            st.push_back((uint32_t)dn[d].child1);
+        }
+    }
+    nodes_.resize(order.size());
+    node_box_.resize(order.size() * (size_t)dim);
+    for (size_t i = 0; i < order.size(); i++) {
+        const KdbNode &d = dn[order[i]];
+        Node &n = nodes_[i];
+        n = Node();
+        n.leaf = d.child1 < 0;
+        n.left = d.left;
+        n.right = d.right;
+        if (n.leaf) {
+            n.child1 = n.child2 = -1;
+        } else {
+            n.divfeat = d.divfeat;
+            n.divlow = d.divlow;
+            n.divhigh = d.divhigh;
+            n.cutval = d.cutval;
+            n.split_val = d.split_val;
+            n.spread_gap = d.spread_gap;
+            n.cand = d.cand;
+            n.child1 = (int)pre[(uint32_t)d.child1];
+            n.child2 = (int)pre[(uint32_t)d.child2];
+        }
+        const double *b = db + (size_t)order[i] * 2 * dim;
+        for (int e = 0; e < dim; e++) node_box_[i * (size_t)dim + e] = Box{b[e], b[dim + e]};
+    }
+    vind_.assign(dv, dv + K);
+    root_bbox_.assign(node_box_.begin(), node_box_.begin() + dim);
+    depth_ = (int)h.depth;
+    flat_nodes_.resize(nodes_.size());
+    flat_vind_.resize(K);
+    flat_box_.resize(2 * (size_t)dim);
+    flatten(flat_nodes_.data(), flat_vind_.data(), flat_box_.data(), flat_box_.data() + dim);
+}
+
+bool RefKDTree::same_as(const RefKDTree &o, std::string *why) const {
+    auto fail = [&](const std::string &w) {
+        if (why) *why = w;
+        return false;
+    };
+    if (K_ != o.K_ || dim_ != o.dim_) return fail("shape");
+    if (nodes_.size() != o.nodes_.size()) return fail("node count " + std::to_string(nodes_.size()) + " vs " +
+                                                      std::to_string(o.nodes_.size()));
+    if (depth_ != o.depth_) return fail("depth " + std::to_string(depth_) + " vs " + std::to_string(o.depth_));
+    for (size_t i = 0; i < K_; i++)
+        if (vind_[i] != o.vind_[i]) return fail("vind at " + std::to_string(i));
+    for (size_t i = 0; i < nodes_.size(); i++) {
+        const Node &a = nodes_[i], &b = o.nodes_[i];
+        const std::string at = " at node " + std::to_string(i);
+        if (a.leaf != b.leaf || a.left != b.left || a.right != b.right) return fail("structure" + at);
+        if (!a.leaf && (a.divfeat != b.divfeat || a.child1 != b.child1 || a.child2 != b.child2 ||
+                        a.divlow != b.divlow || a.divhigh != b.divhigh || a.cutval != b.cutval ||
+                        a.split_val != b.split_val || a.spread_gap != b.spread_gap || a.cand != b.cand))
+            return fail("split" + at);
+        for (int d = 0; d < dim_; d++) {
+            const Box &x = node_box_[i * (size_t)dim_ + d], &y = o.node_box_[i * (size_t)dim_ + d];
+            if (x.low != y.low || x.high != y.high) return fail("point box" + at + " dim " + std::to_string(d));
+        }
+    }
+    for (int d = 0; d < dim_; d++)
+        if (root_bbox_[d].low != o.root_bbox_[d].low || root_bbox_[d].high != o.root_bbox_[d].high) return fail("root box");
+    return true;
+}
+
 // Branch-free minima and maxima: the comparisons are data-dependent, and mispredicted
 // branches dominated the build (min / max are exact, so any form gives the same values).
 void RefKDTree::min_max(const size_t *ind, size_t count, int e, double &mn, double &mx) const {

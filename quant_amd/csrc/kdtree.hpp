@@ -14,6 +14,7 @@
 #include <mutex>
 #include <cstdint>
 #include <functional>
+#include <string>
 #include <vector>
 
 #include "kdtree_dev.hpp"
@@ -56,7 +57,13 @@ public:
     // pts: K x dim, row-major, borrowed for the lifetime of the tree.  cancel (optional): the
     // build stops early once it reads true, leaving a tree to be discarded (cancelled()).
     RefKDTree(const double *pts, size_t K, int dim, const std::atomic<bool> *cancel = nullptr);
+    // The tree the device built over pts (k_kdbuild.hip; image in kdb_host_layout): its nodes
+    // renumbered depth first, child 1 first, as this class builds them; the same tree.
+    RefKDTree(const double *pts, size_t K, int dim, const uint8_t *device_image);
     bool cancelled() const { return cancelled_; }
+    // Node for node the same tree as o (structure, vind, cut dimensions and values, divlow /
+    // divhigh, the build's split records, point boxes, root box, depth); why: the first difference.
+    bool same_as(const RefKDTree &o, std::string *why = nullptr) const;
     // Index the reference's kd-tree search returns for query q (dim values).
     uint32_t nearest(const double *q) const;
     // Flattened copy for the device search (kdtree_dev.hpp); depth = longest root-to-leaf

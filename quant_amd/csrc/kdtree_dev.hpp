@@ -51,6 +51,36 @@ struct KdView {
     uint32_t bytes = 0;   // contiguous image lo[D] | hi[D] | nodes | vind from lo
 };
 
+// ---- the device build (k_kdbuild.hip) -------------------------------------------------------
+// One node as the device builds it (ids in creation order, root 0; child1 < 0: leaf).  The host
+// import (RefKDTree's image constructor) renumbers depth first.
+constexpr uint32_t KDB_MAXK = 4096;   // code vectors the device build takes (its LDS arrays)
+struct KdbNode {
+    int32_t child1, child2;
+    uint32_t left, right;   // vind[left, right)
+    int32_t divfeat;
+    uint32_t depth;         // the root is 1
+    double divlow, divhigh, cutval, split_val, spread_gap;
+    uint64_t cand;          // candidate dimensions (bit d)
+};
+struct KdbHeader {
+    uint32_t n_nodes, depth, status, pad;   // status 1: built, 2: failed (the host builds instead)
+    uint64_t seq;                           // written last: the launch's sequence number
+    uint64_t pad2[5];
+};
+// The mapped host image: header | nodes[2K] | point boxes [2K][lo row D | hi row D] | vind[K].
+struct KdbHostLayout {
+    uint64_t nodes, boxes, vind, total;
+};
+QVQ_HD inline KdbHostLayout kdb_host_layout(uint32_t K, uint32_t D) {
+    KdbHostLayout L;
+    L.nodes = sizeof(KdbHeader);
+    L.boxes = L.nodes + (uint64_t)2 * K * sizeof(KdbNode);
+    L.vind = L.boxes + (uint64_t)2 * K * 2 * D * sizeof(double);
+    L.total = L.vind + (uint64_t)K * 4;
+    return L;
+}
+
 // Device stack frames are 12 bytes: one double (the cell bound mindistsq, replaced by the
 // saved dists[f] once the first child is done) and node << 2 | phase.
 constexpr int KD_FRAME_BYTES = 12;
