@@ -516,9 +516,9 @@ __host__ __device__ inline RcLds rc_lds_layout(uint32_t K) {
     L.lut = o;
     o += 256 * 8;
     L.cand = o;
-    o += M32_WAVES * 32 * RC_CAP * 4;
+    o += M32_WAVES * 64 * RC_CAP * 4;   // [wave][half][row][RC_CAP]: a list per lane
     L.ncand = o;
-    o += M32_WAVES * 32 * 4;
+    o += M32_WAVES * 64 * 4;
     L.total = o;
     return L;
 }
@@ -544,9 +544,10 @@ __global__ __launch_bounds__(M32_THREADS) void recheck_mf32_kernel(
     for (uint32_t i = tid; i < 256; i += M32_THREADS) lut[i] = g_lut64[i];
     const int lane = tid & 63, wave = tid >> 6;
     const int r32 = lane & 31, h = lane >> 5;
-    uint32_t *cand = reinterpret_cast<uint32_t *>(lds + L.cand) + wave * 32 * RC_CAP;
-    uint32_t *ncand = reinterpret_cast<uint32_t *>(lds + L.ncand) + wave * 32;
-    if (h == 0) ncand[r32] = 0;
+    // each lane lists its own half's candidates of its row (no shared counter, no atomics)
+    uint32_t *cand = reinterpret_cast<uint32_t *>(lds + L.cand) + wave * 64 * RC_CAP;
+    uint32_t *ncand = reinterpret_cast<uint32_t *>(lds + L.ncand) + wave * 64;
+    uint32_t *mine = cand + lane * RC_CAP;
     __syncthreads();
     const uint32_t ntiles = Kp / 32;
     const unsigned char *pa = lds + r32 * 32 + 16 * (h ^ ((r32 >> 3) & 1));
@@ -607,16 +608,19 @@ __global__ __launch_bounds__(M32_THREADS) void recheck_mf32_kernel(
             m = min3f(m, min16(c), min16(d));
         }
         m = min2f(m, xor32_f32(m));
-        const float band = m + band_add * (1.0f + 1e-6f) + fabsf(m) * 1e-6f;
-        // pass 2: list the code vectors inside the band
+        const float band = valid ? m + band_add * (1.0f + 1e-6f) + fabsf(m) * 1e-6f : -INFINITY;
+        // pass 2: list the code vectors inside the band, each lane into its own list (one
+        // shared counter per row made every listing a returning LDS atomic, and the 16
+        // listing branches of a tile ran whenever any of the wave's 32 rows had a candidate
+        // there: pass 2 took 3-4x pass 1)
+        uint32_t nmine = 0;
         auto list = [&](const f32x16 &c, uint32_t t) {
-            if (valid && min16(c) <= band) {   // rare
+            if (__ballot(min16(c) <= band)) {   // some row of the wave has a candidate here
 #pragma unroll
                 for (int v = 0; v < 16; v++) {
                     if (c[v] <= band) {
-                        const uint32_t cv = t * 32 + (v & 3) + 8 * (v >> 2) + 4 * h;
-                        const uint32_t slot = atomicAdd(&ncand[r32], 1u);
-                        if (slot < RC_CAP) cand[r32 * RC_CAP + slot] = cv;
+                        if (nmine < RC_CAP) mine[nmine] = t * 32 + (v & 3) + 8 * (v >> 2) + 4 * h;
+                        nmine++;
                     }
                 }
             }
@@ -627,6 +631,7 @@ __global__ __launch_bounds__(M32_THREADS) void recheck_mf32_kernel(
             list(c, t);
             if (t + 1 < ntiles) list(d, t + 1);
         }
+        ncand[lane] = nmine;
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -635,9 +640,11 @@ __global__ __launch_bounds__(M32_THREADS) void recheck_mf32_kernel(
             double x[MF_D];
 #pragma unroll
             for (int d = 0; d < MF_D; d++) x[d] = lut[((d < 4 ? w0 : d < 8 ? w1 : w2) >> (8 * (d % 4))) & 0xFF];
-            const uint32_t nc = ncand[r32];
-            const bool all = nc > RC_CAP;
-            const uint32_t n = all ? K : nc;
+            const uint32_t n0 = nmine, n1 = ncand[lane + 32];   // this half's, the other half's
+            const uint32_t *other = mine + 32 * RC_CAP;
+            const bool all = n0 > RC_CAP || n1 > RC_CAP;
+            const uint32_t n = all ? K : n0 + n1;
+            auto cand_at = [&](uint32_t i) { return i < n0 ? mine[i] : other[i - n0]; };
             double d1 = INFINITY, d2 = INFINITY;
             uint32_t k1 = 0xFFFFFFFFu;
             auto take = [&](uint32_t k, double d) {
@@ -653,9 +660,9 @@ __global__ __launch_bounds__(M32_THREADS) void recheck_mf32_kernel(
             // two candidates per trip, both rows' loads in flight together (one round trip each
             // through L2 was the chain of a row with several candidates)
             for (uint32_t i = 0; i < n; i += 2) {
-                const uint32_t ka = all ? i : cand[r32 * RC_CAP + i];
+                const uint32_t ka = all ? i : cand_at(i);
                 const bool two = i + 1 < n;
-                const uint32_t kb = two ? (all ? i + 1 : cand[r32 * RC_CAP + i + 1]) : ka;
+                const uint32_t kb = two ? (all ? i + 1 : cand_at(i + 1)) : ka;
                 const RowN<MF_D> ra = load_row<MF_D>(C64 + (uint64_t)min(ka, K - 1) * MF_D);
                 const RowN<MF_D> rb = load_row<MF_D>(C64 + (uint64_t)min(kb, K - 1) * MF_D);
                 take(ka, ref_l2_n<MF_D>(x, ra));
@@ -679,7 +686,6 @@ __global__ __launch_bounds__(M32_THREADS) void recheck_mf32_kernel(
                     A[row] = k1;
                 }
             }
-            ncand[r32] = 0;
         }
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();

@@ -716,12 +716,16 @@ __global__ __launch_bounds__(MEAN_THREADS) void mean_sums_kernel(const uint8_t *
     constexpr int Q3 = DP / 4;   // component quads (words per row)
     __shared__ uint8_t lo8[256];
     __shared__ uint32_t red[MEAN_THREADS / 64][DP][2];
-    if (threadIdx.x < 256) lo8[threadIdx.x] = (uint8_t)(plut[threadIdx.x] & 0xFF);
-    if (blockIdx.x == 0) {
+    // the last block only initialises (the count, the distortion's moments, the zeroed words):
+    // in block 0 of the summing grid that serial work held one CU's loads back by ~2 us
+    const uint32_t nblk = gridDim.x - 1;
+    if (blockIdx.x == nblk) {
         if (threadIdx.x == 0) sums[2 * D] = N;   // cnt[0]
         if (threadIdx.x < 64) hist_moments(init.hist, init.v64, D, init.dist);
         if (threadIdx.x < init.n_zero) init.zero[threadIdx.x] = 0;
+        return;
     }
+    if (threadIdx.x < 256) lo8[threadIdx.x] = (uint8_t)(plut[threadIdx.x] & 0xFF);
     __syncthreads();
     // low parts two components per register too: lo2[2q] = (4q, 4q+1), lo2[2q+1] = (4q+2, 4q+3)
     uint32_t ue[Q3], uo[Q3], lo2[DP / 2];
@@ -746,7 +750,7 @@ __global__ __launch_bounds__(MEAN_THREADS) void mean_sums_kernel(const uint8_t *
         // lane's slots are rotated by 4 l mod Q at the end.  MEAN_U chunks per trip in flight.
         const uint64_t chunks = groups / 64;
         const uint64_t wave_id = (uint64_t)blockIdx.x * (MEAN_THREADS / 64) + (threadIdx.x >> 6);
-        const uint64_t nwaves = (uint64_t)gridDim.x * (MEAN_THREADS / 64);
+        const uint64_t nwaves = (uint64_t)nblk * (MEAN_THREADS / 64);
         const int lane = threadIdx.x & 63;
         for (uint64_t c = wave_id; c < chunks; c += MEAN_U * nwaves) {
             uint4 v[MEAN_U][Q];
@@ -796,7 +800,7 @@ __global__ __launch_bounds__(MEAN_THREADS) void mean_sums_kernel(const uint8_t *
     // groups past the wave chunks (every group for wide rows): one group per thread, MEAN_U
     // groups per trip with all their loads issued first
     constexpr int U = DP <= 16 ? MEAN_U : (DP <= 32 ? 2 : 1);   // (wide rows: fewer, by registers)
-    const uint64_t stride = (uint64_t)gridDim.x * MEAN_THREADS;
+    const uint64_t stride = (uint64_t)nblk * MEAN_THREADS;
     for (uint64_t g = g_begin + (uint64_t)blockIdx.x * MEAN_THREADS + threadIdx.x; g < groups; g += U * stride) {
         if constexpr (DP > 32) {   // wide rows: the group's 16-byte loads one by one (registers)
             const uint4 *p = reinterpret_cast<const uint4 *>(codes + g * 4 * DP);
@@ -878,7 +882,7 @@ hipError_t launch_mean_sums(hipStream_t s, uint32_t Dp, const uint8_t *codes, ui
     switch (Dp) {
 #define X(DPV)                                                                                              \
     case DPV:                                                                                               \
-        hipLaunchKernelGGL(mean_sums_kernel<DPV>, dim3((unsigned)grid), dim3(MEAN_THREADS), 0, s, codes, N, D, plut, \
+        hipLaunchKernelGGL(mean_sums_kernel<DPV>, dim3((unsigned)grid + 1), dim3(MEAN_THREADS), 0, s, codes, N, D, plut, \
                            sums, init);                                                                     \
         return hipGetLastError();
         QVQ_FOR_EACH_DP(X)
@@ -1186,6 +1190,9 @@ __device__ void finalize_block_done(const FinArgs &a, double term, double *red, 
                                     unsigned *__restrict__ done, double *__restrict__ dist_out,
                                     volatile uint64_t *ready, uint64_t seq) {
     __shared__ bool last;
+    // one block (small codebooks): no count and no agent fence, only the system fence before the
+    // ready number (two fences of ~2-3.5 us each were most of a small level's finalize)
+    const bool one = gridDim.x == 1;
     if (red) red[threadIdx.x] = term;
     // host_cb: every wave's mapped stores complete before the barrier, and thread 0's
     // system-scope fence below releases them with the block's count (MI355X guide's
@@ -1198,15 +1205,23 @@ __device__ void finalize_block_done(const FinArgs &a, double term, double *red, 
             __syncthreads();
         }
     if (threadIdx.x == 0) {
-        if (red) dist_part[blockIdx.x] = red[0];
-        if (a.host_cb || a.ties.out) __threadfence_system();
-        else __threadfence();
-        last = atomicAdd(done, 1u) == gridDim.x - 1;
+        if (one) {
+            last = true;
+        } else {
+            if (red) dist_part[blockIdx.x] = red[0];
+            if (a.host_cb || a.ties.out) __threadfence_system();
+            else __threadfence();
+            last = atomicAdd(done, 1u) == gridDim.x - 1;
+        }
     }
     __syncthreads();
     if (!last) return;
-    __threadfence();
-    if (dist_out) {   // the block partials, loaded in parallel, then added in block order
+    if (one) {
+        if (dist_out && threadIdx.x == 0) dist_out[0] = red[0];
+    } else {
+        __threadfence();
+    }
+    if (dist_out && !one) {   // the block partials, loaded in parallel, then added in block order
         __shared__ double parts[512];
         for (uint32_t b = threadIdx.x; b < gridDim.x; b += blockDim.x) parts[b] = __builtin_nontemporal_load(&dist_part[b]);
         __syncthreads();
@@ -1294,6 +1309,7 @@ static FinArgs fin_args(const uint64_t *sums, uint32_t K, uint32_t D, uint32_t D
     return a;
 }
 
+constexpr uint32_t FIN_ONE_BLOCK_ROWS = 64;   // split rows: K <= 32
 hipError_t launch_finalize_prep(hipStream_t s, const uint64_t *sums, uint32_t K, uint32_t D, uint32_t Dp, int64_t R,
                                 int64_t bias, int scale, double *C_cent, bool split, double *C64n, uint32_t Kpad_next,
                                 double mu, double sx, int t, float *C32, _Float16 *cb_rows, float *E32,
@@ -1307,7 +1323,9 @@ hipError_t launch_finalize_prep(hipStream_t s, const uint64_t *sums, uint32_t K,
     if (zero_sums && !done) return hipErrorInvalidValue;   // the clearing is the last block's
     const uint32_t L = D <= 16 ? 16 : (D <= 32 ? 32 : 64);
     const uint32_t n = split ? std::max(2 * K, Kpad_next) : K;
-    const uint32_t grid = std::min<uint32_t>((n + 256 / L - 1) / (256 / L), 512);   // <= dist_part capacity
+    // <= dist_part capacity; small codebooks in one block (the grid-stride loop takes several rows
+    // per thread), which needs no cross-block count or fence (finalize_block_done)
+    const uint32_t grid = n <= FIN_ONE_BLOCK_ROWS ? 1u : std::min<uint32_t>((n + 256 / L - 1) / (256 / L), 512);
     FinArgs a = fin_args(sums, K, D, Dp, R, bias, scale, C_cent, split, C64n, Kpad_next, mu, sx, t, C32, cb_rows,
                          E32, host_cb, dist_out != nullptr);
     a.ncopy = ncopy ? ncopy : 1;

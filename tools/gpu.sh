@@ -7,7 +7,7 @@
 #   record              bench.py defaults + kernel stats of the same command + FETCH/WRITE PMC passes
 #   bench[:ARGS]        bench.py with ARGS (commas for spaces), JSON to bench_N.json
 #   ab:N:SPEC;SPEC...   N interleaved C3 runs per SPEC "name=VAR=v,VAR2=v" (20 steps, per-level events)
-#   timeline:CASE       kernel trace of tools/quick_timing.py CASE (e.g. 4096,4,12) -> levels_CASE.txt
+#   timeline:CASE       kernel trace of tools/quick_timing.py CASE (e.g. 4096,4,12), no timing events -> levels_CASE.txt
 #   host:CASE           QVQ_HOST_TRACE=1 host timeline of CASE -> host_CASE.log
 #   sq:CASE:KIND        SQ counters of CASE's searches (tools/gpu_pmc_sq.sh)
 #   py:SCRIPT[:ARGS]    python3 SCRIPT ARGS (commas for spaces), log to py_N.log
@@ -48,7 +48,7 @@ print('${name}_$i', 'C3', d['ms_per_step'], 'search us', {k: round(p[k]['avg_lau
     done ;;
   timeline)
     c=${arg//,/_}
-    (cd /tmp && timeout -k 10 200 rocprofv3 --kernel-trace --output-format csv -d $O/t_$c -o t -- python3 $R/tools/quick_timing.py $arg > $O/t_$c.log 2>&1) || exit $?
+    (cd /tmp && QT_EVENTS=0 timeout -k 10 200 rocprofv3 --kernel-trace --output-format csv -d $O/t_$c -o t -- python3 $R/tools/quick_timing.py $arg > $O/t_$c.log 2>&1) || exit $?
     (cd $R && python3 tools/level_view.py $O/t_$c/t_kernel_trace.csv --names > $O/levels_$c.txt 2>&1) || exit $?
     tail -25 $O/levels_$c.txt ;;
   host)

@@ -10,7 +10,10 @@ cases = [(512, 2, 10), (4096, 2, 10), (4096, 4, 12)]
 if len(sys.argv) > 1:
     cases = [tuple(int(v) for v in c.split(',')) for c in sys.argv[1:]]
 eng = quant_amd.Engine(0)
-eng.set_timing(-1)   # per-level events (off by default: each record idles the GPU ~6 us)
+# per-level events (off by default: each record idles the GPU ~6 us, so a kernel trace taken with
+# them shows ~6 us gaps around every search); QT_EVENTS=0 leaves them off (the schedule as bench.py
+# runs it; the per-level times then read 0)
+eng.set_timing(-2 if __import__('os').environ.get("QT_EVENTS") == "0" else -1)
 for (S, bw, bits) in cases:
     eng.set_synthetic(S, 0x5EED, 1, bw, bw)
     for rep in range(3):
