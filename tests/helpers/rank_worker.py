@@ -4,7 +4,7 @@ GPU 0, exchange the per-level sums through the engine's test-only host communica
 shard of the rows -- the sharded schedule of SURVEY.md 8(e) (reference loops
 src/Quantizer.cpp:27-31 assign, :80-86 fix), executed for real.
 
-    python rank_worker.py RANK WORLD PORT CASE OUT.npz
+    python rank_worker.py RANK WORLD RENDEZVOUS_FILE CASE OUT.npz
 CASE: c2 -- the C2 image (512^2, 2x2) split into contiguous row ranges (qvq_set_vectors);
       c5 -- the reduced C5 batch (4 x 512^2 images, 2x2), whole images per rank (qvq_set_synthetic);
       corpus -- every case of tests/golden/kahan_divergent.json (inputs where the reference's
@@ -26,12 +26,16 @@ def shard(n, world, rank):
 
 
 def main():
-    rank, world, port, case, out = int(sys.argv[1]), int(sys.argv[2]), sys.argv[3], sys.argv[4], sys.argv[5]
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=port)
+    rank, world, rdv, case, out = int(sys.argv[1]), int(sys.argv[2]), sys.argv[3], sys.argv[4], sys.argv[5]
+    import datetime
     import torch
     import torch.distributed as dist
     import quant_amd
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    # a file rendezvous (no TCP store port picked ahead by the parent, which another process could
+    # take first), and a bounded one: a rank that cannot join fails instead of waiting 30 minutes
+    os.environ.setdefault("GLOO_SOCKET_IFNAME", "lo")
+    dist.init_process_group("gloo", init_method="file://" + rdv, rank=rank, world_size=world,
+                            timeout=datetime.timedelta(seconds=60))
 
     def allreduce(arr):
         t = torch.from_numpy(arr.view(np.int64) if arr.dtype == np.uint64 else arr)   # shares arr's memory

@@ -9,8 +9,8 @@ results must equal the communicator-free run bit for bit -- the property that ma
 being sharded are src/Quantizer.cpp:24-32 (assign) and :72-87 (centroids)."""
 import json
 import os
-import socket
 import subprocess
+import time
 import sys
 
 import numpy as np
@@ -83,23 +83,28 @@ def test_c5_full_batch_properties():
         assert oracle.sha16(A4) == h_first
 
 
-def _run_ranks(world, case, tmp_path, env=None):
+def _run_ranks(world, case, tmp_path, env=None, limit=150):
     """world rank processes (tests/helpers/rank_worker.py) sharing GPU 0 through the host
-    communicator; returns each rank's results."""
-    with socket.socket() as s:
-        s.bind(("127.0.0.1", 0))
-        port = str(s.getsockname()[1])
+    communicator; returns each rank's results.  A rank that fails ends the others at once, and the
+    whole group is bounded by `limit` seconds."""
+    rdv = str(tmp_path / "rendezvous")
     worker = os.path.join(os.path.dirname(os.path.abspath(__file__)), "helpers", "rank_worker.py")
     outs = [str(tmp_path / ("rank%d.npz" % r)) for r in range(world)]
     penv = dict(os.environ, **(env or {}))
-    procs = [subprocess.Popen([sys.executable, worker, str(r), str(world), port, case, outs[r]], env=penv)
+    procs = [subprocess.Popen([sys.executable, worker, str(r), str(world), rdv, case, outs[r]], env=penv)
              for r in range(world)]
+    deadline = time.time() + limit
     try:
-        codes = [p.wait(timeout=240) for p in procs]
+        while any(p.poll() is None for p in procs):
+            if any(p.poll() not in (None, 0) for p in procs) or time.time() > deadline:
+                break
+            time.sleep(0.05)
     finally:
         for p in procs:
             if p.poll() is None:
                 p.kill()
+                p.wait()
+    codes = [p.returncode for p in procs]
     assert codes == [0] * world, codes
     return [dict(np.load(o)) for o in outs]
 
