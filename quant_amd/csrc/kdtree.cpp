@@ -270,6 +270,52 @@ bool RefKDTree::same_as(const RefKDTree &o, std::string *why) const {
     return true;
 }
 
+void RefKDTree::to_device_image(uint8_t *img) const {
+    const KdbHostLayout L = kdb_host_layout((uint32_t)K_, (uint32_t)dim_);
+    KdbHeader &h = *reinterpret_cast<KdbHeader *>(img);
+    KdbNode *dn = reinterpret_cast<KdbNode *>(img + L.nodes);
+    double *db = reinterpret_cast<double *>(img + L.boxes);
+    uint32_t *dv = reinterpret_cast<uint32_t *>(img + L.vind);
+    // breadth first from the root: node q of the queue gets id q, its children the next two ids
+    std::vector<int> queue(1, 0);
+    std::vector<uint32_t> depth(1, 1);
+    for (size_t q = 0; q < queue.size(); q++) {
+        const Node &n = nodes_[(size_t)queue[q]];
+        KdbNode o{};
+        o.left = (uint32_t)n.left;
+        o.right = (uint32_t)n.right;
+        o.depth = depth[q];
+        if (n.leaf) {
+            o.child1 = o.child2 = -1;
+        } else {
+            o.child1 = (int32_t)queue.size();
+            o.child2 = o.child1 + 1;
+            queue.push_back(n.child1);
+            queue.push_back(n.child2);
+            depth.push_back(depth[q] + 1);
+            depth.push_back(depth[q] + 1);
+            o.divfeat = n.divfeat;
+            o.divlow = n.divlow;
+            o.divhigh = n.divhigh;
+            o.cutval = n.cutval;
+            o.split_val = n.split_val;
+            o.spread_gap = n.spread_gap;
+            o.cand = n.cand;
+        }
+        dn[q] = o;
+        for (int e = 0; e < dim_; e++) {
+            const Box &bx = node_box_[(size_t)queue[q] * dim_ + e];
+            db[q * 2 * (size_t)dim_ + e] = bx.low;
+            db[q * 2 * (size_t)dim_ + dim_ + e] = bx.high;
+        }
+    }
+    for (size_t i = 0; i < K_; i++) dv[i] = (uint32_t)vind_[i];
+    h = KdbHeader{};
+    h.n_nodes = (uint32_t)queue.size();
+    h.depth = (uint32_t)depth_;
+    h.status = 1;
+}
+
 // Branch-free minima and maxima: the comparisons are data-dependent, and mispredicted
 // branches dominated the build (min / max are exact, so any form gives the same values).
 void RefKDTree::min_max(const size_t *ind, size_t count, int e, double &mn, double &mx) const {

@@ -64,6 +64,10 @@ public:
     // Node for node the same tree as o (structure, vind, cut dimensions and values, divlow /
     // divhigh, the build's split records, point boxes, root box, depth); why: the first difference.
     bool same_as(const RefKDTree &o, std::string *why = nullptr) const;
+    // This tree as the device build writes it (kdb_host_layout: nodes numbered breadth first, the
+    // two children of a node consecutive), for the import's CPU tests.  img: kdb_host_layout(K,
+    // dim).total bytes.
+    void to_device_image(uint8_t *img) const;
     // Index the reference's kd-tree search returns for query q (dim values).
     uint32_t nearest(const double *q) const;
     // Flattened copy for the device search (kdtree_dev.hpp); depth = longest root-to-leaf

@@ -59,6 +59,15 @@ static void test_kdtree() {
             t.flatten(nodes.data(), vind.data(), lo.data(), hi.data());
             std::vector<int> seen(K, 0);
             for (uint32_t v : vind) CHECK(v < K && !seen[v]++);
+            // the device build's image of this tree (breadth-first ids) imported back: node for
+            // node the same tree (RefKDTree's image constructor renumbers depth first)
+            std::vector<uint8_t> img(qvq::kdb_host_layout((uint32_t)K, (uint32_t)D).total);
+            t.to_device_image(img.data());
+            qvq::RefKDTree u(C.data(), K, D, img.data());
+            std::string why;
+            CHECK(t.same_as(u, &why));
+            if (!why.empty()) std::fprintf(stderr, "import K=%zu D=%d: %s\n", K, D, why.c_str());
+            for (size_t i = 0; i < nq; i += 7) CHECK(u.nearest(Q.data() + i * D) == want[i]);
         }
     }
 }
