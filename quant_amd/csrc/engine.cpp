@@ -913,7 +913,9 @@ void build_tree_host(qvq_ctx *ctx, const double *hC, uint32_t K, int buf, KdView
     } else {
         ctx->cnt_local.clear();
     }
+    ctx->htrace.mark("K" + std::to_string(K) + " codebook copied");
     ctx->tree.reset(new RefKDTree(ctx->cb_local.data(), K, (int)ctx->D, cancel));
+    ctx->htrace.mark("K" + std::to_string(K) + " tree structure");
     const RefKDTree &tree = *ctx->tree;
     if (tree.cancelled()) return;
     const uint32_t D = ctx->D;
@@ -2700,8 +2702,10 @@ QVQ_API qvq_status qvq_lbg(qvq_ctx *ctx, uint32_t bits, double eps, double *code
             v.K = K;
             v.level = lvl;
             v.tree = std::move(ctx->tree);
-            v.cb = std::move(ctx->cb_local);
-            v.cnt = std::move(ctx->cnt_local);
+            // (swapped, not moved: the joined check's buffers come back with their capacity, so
+            // the next level's codebook copy writes no fresh pages -- 1.5 MB at C4's level 12)
+            std::swap(v.cb, ctx->cb_local);
+            std::swap(v.cnt, ctx->cnt_local);
             ctx->cb_local.clear();
             ctx->cnt_local.clear();
             v.cs = CertState();

@@ -84,6 +84,8 @@ void Recycled<T>::release() {
 }
 template class Recycled<double>;
 template class Recycled<RefKDTree::Iv>;
+template class Recycled<RefKDTree::Node>;
+template class Recycled<Box>;
 
 
 double ref_l2(const double *a, const double *b, int dim) { return ref_l2_hd(a, b, dim); }
@@ -172,9 +174,10 @@ RefKDTree::RefKDTree(const double *pts, size_t K, int dim, const std::atomic<boo
             root_bbox_[d].high = hi;
         }
     }
-    nodes_.reserve(2 * (K / 5 + 1));
-    node_box_.clear();
-    node_box_.reserve(2 * (K / 5 + 1) * (size_t)dim);
+    // every node's record and box in one pooled buffer each (a tree of K points has fewer than
+    // 2K + 1 nodes unless empty leaves pile up; push_back grows then)
+    nodes_.reserve(2 * K + 1);
+    node_box_.reserve((2 * K + 1) * (size_t)dim);
     std::vector<Box> box(root_bbox_);
     divide(0, K, box.data(), 1, nodes_, depth_);
     flat_nodes_.resize(nodes_.size());
@@ -413,7 +416,7 @@ void RefKDTree::middle_split(size_t *ind, size_t count, size_t &index, int &cutf
 }
 
 // bbox is in/out: the caller's cell box on entry, the node's actual point box on exit.
-int RefKDTree::divide(size_t left, size_t right, Box *bbox, int level, std::vector<Node> &nodes, int &depth) {
+int RefKDTree::divide(size_t left, size_t right, Box *bbox, int level, RecycledVec<Node> &nodes, int &depth) {
     const int me = (int)nodes.size();
     depth = std::max(depth, level);
     nodes.push_back(Node());

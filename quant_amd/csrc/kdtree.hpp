@@ -13,6 +13,7 @@
 #include <memory>
 #include <mutex>
 #include <cstdint>
+#include <cstring>
 #include <functional>
 #include <string>
 #include <vector>
@@ -38,6 +39,12 @@ public:
     Recycled &operator=(const Recycled &) = delete;
     ~Recycled() { release(); }
     void resize(size_t n);   // contents undefined; data() 64-byte aligned
+    void swap(Recycled &o) {
+        std::swap(p_, o.p_);
+        std::swap(base_, o.base_);
+        std::swap(cap_, o.cap_);
+        std::swap(n_, o.n_);
+    }
     size_t size() const { return n_; }
     T *data() { return base_; }
     const T *data() const { return base_; }
@@ -50,6 +57,43 @@ private:
     std::unique_ptr<T[]> p_;
     T *base_ = nullptr;
     size_t cap_ = 0, n_ = 0;
+};
+
+// A growable array of a trivially copyable type on Recycled storage: a level's tree allocates
+// its node records and boxes (MBs at K = 4096, D = 48) from the pool instead of fresh pages
+// (first-touch faults cost ~0.45 ms of the 1.5 ms K = 4096 build on the GPU box's host).
+template <class T>
+class RecycledVec {
+public:
+    void reserve(size_t n) {
+        if (n > buf_.size()) grow(n);
+    }
+    void resize(size_t n) {
+        reserve(n);
+        n_ = n;
+    }
+    void push_back(const T &v) {
+        if (n_ == buf_.size()) grow(n_ < 16 ? 16 : 2 * n_);
+        buf_[n_++] = v;
+    }
+    size_t size() const { return n_; }
+    bool empty() const { return n_ == 0; }
+    T *begin() { return buf_.data(); }
+    const T *begin() const { return buf_.data(); }
+    T *data() { return buf_.data(); }
+    const T *data() const { return buf_.data(); }
+    T &operator[](size_t i) { return buf_[i]; }
+    const T &operator[](size_t i) const { return buf_[i]; }
+
+private:
+    void grow(size_t cap) {
+        Recycled<T> nb;
+        nb.resize(cap);
+        if (n_) std::memcpy(static_cast<void *>(nb.data()), buf_.data(), n_ * sizeof(T));
+        buf_.swap(nb);
+    }
+    Recycled<T> buf_;
+    size_t n_ = 0;
 };
 
 class RefKDTree {
@@ -132,7 +176,7 @@ private:
     double pt(size_t i, int d) const { return cols_[(size_t)d * K_ + i]; }
     double ptr(size_t i, int d) const { return pts_[i * (size_t)dim_ + d]; }   // row-major
     // bbox: the node's cell box (dim entries); children's boxes live in boxes_ at their level
-    int divide(size_t left, size_t right, Box *bbox, int level, std::vector<Node> &nodes, int &depth);
+    int divide(size_t left, size_t right, Box *bbox, int level, RecycledVec<Node> &nodes, int &depth);
     void middle_split(size_t *ind, size_t count, size_t &index, int &cutfeat, double &cutval, const Box *bbox,
                       Node *info);
     void plane_split(size_t *ind, size_t count, int cutfeat, double cutval, size_t &lim1, size_t &lim2);
@@ -144,9 +188,9 @@ private:
     bool cancelled_ = false;
     const double *cols_ = nullptr;   // [dim][K], thread-local scratch valid during the build
     std::vector<size_t> vind_;
-    std::vector<Node> nodes_;
+    RecycledVec<Node> nodes_;
     std::vector<Box> root_bbox_;
-    std::vector<Box> node_box_;   // [node][dim]: the node's actual point box (the build's in/out bbox)
+    RecycledVec<Box> node_box_;   // [node][dim]: the node's actual point box (the build's in/out bbox)
     int depth_ = 0;
     std::vector<KdNodeDev> flat_nodes_;
     std::vector<uint32_t> flat_vind_;
