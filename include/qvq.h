@@ -219,6 +219,12 @@ QVQ_API qvq_status qvq_kdtree_device_check(qvq_ctx *ctx, const double *C, uint32
 /* The reference kd-tree's answer for nq queries (nanoflann semantics, see kdtree.hpp). */
 QVQ_API qvq_status qvq_host_kdtree_nn(const double *C, uint32_t K, uint32_t dim, const double *Q, uint64_t nq,
                                       uint32_t *out);
+/* The host kd-tree build over C (K x dim), as the device build's image (kdtree_dev.hpp
+ * kdb_host_layout: header | nodes[2K], breadth first | point boxes [2K][lo D | hi D] | vind[K]);
+ * *need = the image's bytes, written when bytes >= *need (QVQ_EINVAL otherwise).  For tests of
+ * the build against a restatement, node for node. */
+QVQ_API qvq_status qvq_host_kdtree_image(const double *C, uint32_t K, uint32_t dim, void *img, uint64_t bytes,
+                                         uint64_t *need);
 /* Exact centroid finalisation from reduced sums, as the device does it:
  * C[k][d] = round(R*hi + lo - bias*cnt) * 2^-scale * fl(1/cnt).  For tests. */
 QVQ_API qvq_status qvq_host_finalize(const uint64_t *hi, const uint64_t *lo, const uint64_t *cnt, uint32_t K,

@@ -44,7 +44,8 @@ EXPORTED = ["qvq_create", "qvq_destroy", "qvq_last_error", "qvq_version", "qvq_s
             "qvq_comm_unique_id", "qvq_comm_init", "qvq_set_timing", "qvq_get_timings", "qvq_host_kdtree_nn",
             "qvq_host_finalize", "qvq_host_row_terms", "qvq_decode", "qvq_decode_mse", "qvq_decode_device",
             "qvq_set_timeout", "qvq_host_wait_probe", "qvq_comm_init_host", "qvq_comm_info", "qvq_set_vectors_exact",
-            "qvq_update_kahan_split", "qvq_host_pool_stress", "qvq_kdtree_device_check"]
+            "qvq_update_kahan_split", "qvq_host_pool_stress", "qvq_kdtree_device_check",
+            "qvq_host_kdtree_image"]
 
 COMM_NONE, COMM_RCCL, COMM_HOST = 0, 1, 2
 # int fn(void *buf, uint64_t count, int dtype, void *user) (qvq.h, qvq_comm_init_host)
@@ -83,6 +84,7 @@ def lib():
             "qvq_set_timing": ([P, i], i),
             "qvq_get_timings": ([P, ctypes.POINTER(_Timings)], i),
             "qvq_host_kdtree_nn": ([P, u32, u32, P, u64, P], i),
+            "qvq_host_kdtree_image": ([P, u32, u32, P, u64, P], i),
             "qvq_kdtree_device_check": ([P, P, u32, u32, P, P], i),
             "qvq_host_finalize": ([P, P, P, u32, u32, i, P], i),
             "qvq_host_row_terms": ([P, u32, i, P, P], i),
@@ -344,6 +346,32 @@ def host_kdtree_nn(C, Q):
     out = np.empty(Q.shape[0], np.uint32)
     _check(lib().qvq_host_kdtree_nn(_p(C), C.shape[0], C.shape[1], _p(Q), Q.shape[0], _p(out)))
     return out
+
+
+# KdbNode (kdtree_dev.hpp) and the image layout of qvq_host_kdtree_image
+KDB_NODE = np.dtype([("child1", "<i4"), ("child2", "<i4"), ("left", "<u4"), ("right", "<u4"), ("divfeat", "<i4"),
+                     ("depth", "<u4"), ("divlow", "<f8"), ("divhigh", "<f8"), ("cutval", "<f8"),
+                     ("split_val", "<f8"), ("spread_gap", "<f8"), ("cand", "<u8")])
+KDB_HEADER_BYTES = 64
+
+
+def host_kdtree_image(C):
+    """The host build of C's kd-tree (RefKDTree) as arrays: (nodes [n] KDB_NODE breadth first,
+    lo [n, D], hi [n, D] point boxes, vind [K], depth)."""
+    C = np.ascontiguousarray(C, np.float64)
+    K, D = C.shape
+    need = ctypes.c_uint64()
+    lib().qvq_host_kdtree_image(_p(C), K, D, None, 0, ctypes.byref(need))
+    img = np.zeros(need.value, np.uint8)
+    _check(lib().qvq_host_kdtree_image(_p(C), K, D, _p(img), img.size, ctypes.byref(need)))
+    n_nodes, depth = (int(x) for x in img[:8].view("<u4"))
+    off = KDB_HEADER_BYTES
+    nodes = img[off:off + 2 * K * KDB_NODE.itemsize].view(KDB_NODE)[:n_nodes]
+    off += 2 * K * KDB_NODE.itemsize
+    boxes = img[off:off + 2 * K * 2 * D * 8].view("<f8").reshape(2 * K, 2, D)[:n_nodes]
+    off += 2 * K * 2 * D * 8
+    vind = img[off:off + 4 * K].view("<u4")
+    return nodes, boxes[:, 0], boxes[:, 1], vind.copy(), depth
 
 
 def host_wait_probe(scenario, timeout_s):

@@ -3264,6 +3264,18 @@ QVQ_API qvq_status qvq_host_kdtree_nn(const double *C, uint32_t K, uint32_t dim,
     return QVQ_OK;
 }
 
+QVQ_API qvq_status qvq_host_kdtree_image(const double *C, uint32_t K, uint32_t dim, void *img, uint64_t bytes,
+                                         uint64_t *need) {
+    if (!C || !need || K == 0 || dim == 0 || dim > 64) return QVQ_EINVAL;
+    *need = kdb_host_layout(K, dim).total;
+    if (!img || bytes < *need) return QVQ_EINVAL;
+    RefKDTree tree(C, K, (int)dim);
+    if (tree.num_nodes() > 2ull * K) return QVQ_EINVAL;   // (the layout holds 2K nodes)
+    std::memset(img, 0, *need);
+    tree.to_device_image(static_cast<uint8_t *>(img));
+    return QVQ_OK;
+}
+
 QVQ_API qvq_status qvq_kdtree_device_check(qvq_ctx *ctx, const double *C, uint32_t K, uint32_t dim, double *build_ms,
                                            uint32_t *result) {
     if (!ctx || !C || !result || K == 0 || dim == 0 || dim > 64) return QVQ_EINVAL;

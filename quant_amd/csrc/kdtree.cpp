@@ -112,6 +112,7 @@ inline double ref_l2_cap(const double *a, const double *b, int dim, double cap) 
 
 namespace {
 constexpr int KD_MAX_DIM = 64;
+inline uint64_t all_dims(int dim) { return dim >= 64 ? ~0ull : (1ull << dim) - 1; }
 
 // children's boxes per tree level, [2][KD_MAX_DIM] each: allocated on first use and kept
 // (duplicated points make degenerate trees hundreds of levels deep)
@@ -156,22 +157,19 @@ RefKDTree::RefKDTree(const double *pts, size_t K, int dim, const std::atomic<boo
     vind_.resize(K);
     for (size_t i = 0; i < K; i++) vind_[i] = i;
     root_bbox_.resize(dim);
-    // column-major copy and root box, 64 points at a time (their rows stay in L1 while
-    // every column takes its 64 values)
-    for (int d = 0; d < dim; d++) root_bbox_[d].low = root_bbox_[d].high = pts[d];
+    // the root box from one vectorised row-major pass; the column-major copy 64 points at a
+    // time (their rows stay in L1 while every column takes its 64 values), plain copies (a
+    // min / max chain per column here cost a dependent compare per value)
+    if (K) {
+        double mn[64], mx[64];
+        rows_min_max(pts, vind_.data(), K, dim, mn, mx);
+        for (int d = 0; d < dim; d++) root_bbox_[d] = Box{mn[d], mx[d]};
+    }
     for (size_t k0 = 0; k0 < K; k0 += 64) {
         const size_t k1 = std::min(K, k0 + 64);
         for (int d = 0; d < dim; d++) {
             double *col = cbuf + (size_t)d * K;
-            double lo = root_bbox_[d].low, hi = root_bbox_[d].high;
-            for (size_t k = k0; k < k1; k++) {
-                const double v = pts[k * (size_t)dim + d];
-                col[k] = v;
-                lo = v < lo ? v : lo;
-                hi = v > hi ? v : hi;
-            }
-            root_bbox_[d].low = lo;
-            root_bbox_[d].high = hi;
+            for (size_t k = k0; k < k1; k++) col[k] = pts[k * (size_t)dim + d];
         }
     }
     // every node's record and box in one pooled buffer each (a tree of K points has fewer than
@@ -179,7 +177,10 @@ RefKDTree::RefKDTree(const double *pts, size_t K, int dim, const std::atomic<boo
     nodes_.reserve(2 * K + 1);
     node_box_.reserve((2 * K + 1) * (size_t)dim);
     std::vector<Box> box(root_bbox_);
-    divide(0, K, box.data(), 1, nodes_, depth_);
+    Known &rk = level_known(0)[0];   // the root's extremes: its box
+    std::copy(root_bbox_.begin(), root_bbox_.end(), rk.b);
+    rk.mask = K ? all_dims(dim) : 0;
+    divide(0, K, box.data(), rk, 1, nodes_, depth_);
     flat_nodes_.resize(nodes_.size());
     flat_vind_.resize(K);
     flat_box_.resize(2 * (size_t)dim);
@@ -320,16 +321,34 @@ void RefKDTree::to_device_image(uint8_t *img) const {
 }
 
 // Branch-free minima and maxima: the comparisons are data-dependent, and mispredicted
-// branches dominated the build (min / max are exact, so any form gives the same values).
+// branches dominated the build; four independent chains, since one chain waits on a dependent
+// compare per value (min / max are exact, so any order gives the same values).
 void RefKDTree::min_max(const size_t *ind, size_t count, int e, double &mn, double &mx) const {
-    double a = pt(ind[0], e), b = a;
-    for (size_t i = 1; i < count; i++) {
-        const double v = pt(ind[i], e);
-        a = v < a ? v : a;
-        b = v > b ? v : b;
+    const double *col = cols_ + (size_t)e * K_;
+    double a0 = col[ind[0]], b0 = a0, a1 = a0, b1 = a0, a2 = a0, b2 = a0, a3 = a0, b3 = a0;
+    size_t i = 1;
+    for (; i + 4 <= count; i += 4) {
+        const double v0 = col[ind[i]], v1 = col[ind[i + 1]], v2 = col[ind[i + 2]], v3 = col[ind[i + 3]];
+        a0 = v0 < a0 ? v0 : a0;
+        b0 = v0 > b0 ? v0 : b0;
+        a1 = v1 < a1 ? v1 : a1;
+        b1 = v1 > b1 ? v1 : b1;
+        a2 = v2 < a2 ? v2 : a2;
+        b2 = v2 > b2 ? v2 : b2;
+        a3 = v3 < a3 ? v3 : a3;
+        b3 = v3 > b3 ? v3 : b3;
     }
-    mn = a;
-    mx = b;
+    for (; i < count; i++) {
+        const double v = col[ind[i]];
+        a0 = v < a0 ? v : a0;
+        b0 = v > b0 ? v : b0;
+    }
+    a0 = a1 < a0 ? a1 : a0;
+    a2 = a3 < a2 ? a3 : a2;
+    b0 = b1 > b0 ? b1 : b0;
+    b2 = b3 > b2 ? b3 : b2;
+    mn = a2 < a0 ? a2 : a0;
+    mx = b2 > b0 ? b2 : b0;
 }
 
 void RefKDTree::plane_split(size_t *ind, size_t count, int cutfeat, double cutval, size_t &lim1,
@@ -359,29 +378,39 @@ void RefKDTree::plane_split(size_t *ind, size_t count, int cutfeat, double cutva
 }
 
 void RefKDTree::middle_split(size_t *ind, size_t count, size_t &index, int &cutfeat, double &cutval,
-                             const Box *bbox, Node *info) {
+                             const Box *bbox, Known &kn, Node *info) {
     const double EPS = 0.00001;
     double max_span = bbox[0].high - bbox[0].low;
     for (int i = 1; i < dim_; i++) max_span = std::max(max_span, bbox[i].high - bbox[i].low);
     // Candidate dimensions: span within EPS of the widest.  In real codebooks (empty cells at
     // 0, saturated colours) every dimension not yet cut along the path has the root's span,
-    // so upper nodes need the point min/max of most dimensions, from the column copy.
-    int q[64], nq = 0;
+    // so upper nodes need the point min/max of most dimensions.  Those the parent's extremes
+    // do not settle (child_known) are computed here.
+    int q[64], nq = 0, nu = 0;
     for (int i = 0; i < dim_; i++)
-        if (bbox[i].high - bbox[i].low > (1 - EPS) * max_span) q[nq++] = i;
-    double qmn[64], qmx[64];
-    if (nq * 4 >= dim_ && dim_ >= 8) {
-        // most dimensions are candidates (real codebooks: every dimension not yet cut on the
-        // path keeps the root's span): one row-major pass over the node's points gives all
-        // of them -- each point's contiguous row once, instead of nq column gathers
+        if (bbox[i].high - bbox[i].low > (1 - EPS) * max_span) {
+            nu += !(kn.mask >> i & 1);
+            q[nq++] = i;
+        }
+    if (nu * 4 >= dim_ && dim_ >= 8) {
+        // most dimensions wanted (real codebooks: every dimension not yet cut on the path
+        // keeps the root's span): one row-major pass over the node's points gives all of
+        // them -- each point's contiguous row once, instead of nu column gathers
         double mn[64], mx[64];
         rows_min_max(pts_, ind, count, dim_, mn, mx);
-        for (int j = 0; j < nq; j++) {
-            qmn[j] = mn[q[j]];
-            qmx[j] = mx[q[j]];
-        }
-    } else {
-        for (int j = 0; j < nq; j++) min_max(ind, count, q[j], qmn[j], qmx[j]);
+        for (int d = 0; d < dim_; d++) kn.b[d] = Box{mn[d], mx[d]};
+        kn.mask = all_dims(dim_);
+    } else if (nu) {
+        for (int j = 0; j < nq; j++)
+            if (!(kn.mask >> q[j] & 1)) {
+                min_max(ind, count, q[j], kn.b[q[j]].low, kn.b[q[j]].high);
+                kn.mask |= 1ull << q[j];
+            }
+    }
+    double qmn[64], qmx[64];
+    for (int j = 0; j < nq; j++) {
+        qmn[j] = kn.b[q[j]].low;
+        qmx[j] = kn.b[q[j]].high;
     }
     double max_spread = -1, mn = 0, mx = 0;
     cutfeat = 0;
@@ -394,7 +423,14 @@ void RefKDTree::middle_split(size_t *ind, size_t count, size_t &index, int &cutf
             mx = qmx[j];
             have = true;
         }
-    if (!have) min_max(ind, count, cutfeat, mn, mx);
+    if (!have) {
+        if (!(kn.mask >> cutfeat & 1)) {
+            min_max(ind, count, cutfeat, kn.b[cutfeat].low, kn.b[cutfeat].high);
+            kn.mask |= 1ull << cutfeat;
+        }
+        mn = kn.b[cutfeat].low;
+        mx = kn.b[cutfeat].high;
+    }
     const double split_val = (bbox[cutfeat].low + bbox[cutfeat].high) / 2;
     cutval = split_val < mn ? mn : (split_val > mx ? mx : split_val);
     {   // what a later change of one coordinate can move (unchanged_under)
@@ -415,8 +451,43 @@ void RefKDTree::middle_split(size_t *ind, size_t count, size_t &index, int &cutf
     else index = count / 2;
 }
 
+// The children's known extremes (ind[0, n1) and ind[n1, count)), when the node's are all
+// known: the smaller child's from its rows; the larger child keeps each parent extreme the
+// smaller child stays strictly inside of (the point attaining it is the larger child's).  A
+// degenerate chain (a node peeling a few points off the duplicated code vectors per level)
+// then skips most of its row passes.
+void RefKDTree::child_known(const size_t *ind, size_t n1, size_t count, const Known &kn, Known &k1,
+                            Known &k2) const {
+    k1.mask = k2.mask = 0;
+    if (kn.mask != all_dims(dim_)) return;
+    const bool first_small = n1 <= count - n1;
+    const size_t s = first_small ? n1 : count - n1;
+    Known &ks = first_small ? k1 : k2, &kb = first_small ? k2 : k1;
+    if (s == 0) {   // (an empty child is a leaf; it reads nothing)
+        kb = kn;
+        return;
+    }
+    double mn[64], mx[64];
+    rows_min_max(pts_, first_small ? ind : ind + n1, s, dim_, mn, mx);
+    uint64_t m = 0;
+    for (int d = 0; d < dim_; d++) {
+        ks.b[d] = Box{mn[d], mx[d]};
+        kb.b[d] = kn.b[d];
+        m |= (uint64_t)(mn[d] > kn.b[d].low && mx[d] < kn.b[d].high) << d;
+    }
+    ks.mask = all_dims(dim_);
+    kb.mask = m;
+}
+
+RefKDTree::Known *RefKDTree::level_known(int level) {
+    static thread_local std::vector<std::unique_ptr<Known[]>> levels;
+    while ((int)levels.size() <= level) levels.emplace_back(new Known[2]);
+    return levels[level].get();
+}
+
 // bbox is in/out: the caller's cell box on entry, the node's actual point box on exit.
-int RefKDTree::divide(size_t left, size_t right, Box *bbox, int level, RecycledVec<Node> &nodes, int &depth) {
+int RefKDTree::divide(size_t left, size_t right, Box *bbox, Known &kn, int level, RecycledVec<Node> &nodes,
+                      int &depth) {
     const int me = (int)nodes.size();
     depth = std::max(depth, level);
     nodes.push_back(Node());
@@ -429,11 +500,15 @@ int RefKDTree::divide(size_t left, size_t right, Box *bbox, int level, RecycledV
         n.right = right;
         n.child1 = n.child2 = -1;
         n.cutval = 0;
-        double mn[64], mx[64];
-        rows_min_max(pts_, vind_.data() + left, right - left, dim_, mn, mx);   // row-major: a point's coordinates are contiguous
-        for (int d = 0; d < dim_; d++) {
-            bbox[d].low = mn[d];
-            bbox[d].high = mx[d];
+        if (right > left && kn.mask == all_dims(dim_)) {
+            std::copy(kn.b, kn.b + dim_, bbox);
+        } else {   // (an empty leaf reads the point at 'left', as the reference's loop)
+            double mn[64], mx[64];
+            rows_min_max(pts_, vind_.data() + left, right - left, dim_, mn, mx);   // row-major: a point's coordinates are contiguous
+            for (int d = 0; d < dim_; d++) {
+                bbox[d].low = mn[d];
+                bbox[d].high = mx[d];
+            }
         }
         std::copy(bbox, bbox + dim_, node_box_.begin() + (size_t)me * dim_);
         return me;
@@ -442,15 +517,17 @@ int RefKDTree::divide(size_t left, size_t right, Box *bbox, int level, RecycledV
     int cutfeat;
     double cutval;
     Node info;
-    middle_split(vind_.data() + left, right - left, idx, cutfeat, cutval, bbox, &info);
+    middle_split(vind_.data() + left, right - left, idx, cutfeat, cutval, bbox, kn, &info);
     // children's boxes (a vector per node cost two heap allocations each)
     Box *lb = level_boxes(level), *rb = lb + dim_;
     std::copy(bbox, bbox + dim_, lb);
     std::copy(bbox, bbox + dim_, rb);
     lb[cutfeat].high = cutval;
     rb[cutfeat].low = cutval;
-    const int c1 = divide(left, left + idx, lb, level + 1, nodes, depth);
-    const int c2 = divide(left + idx, right, rb, level + 1, nodes, depth);
+    Known *kc = level_known(level);   // (level 0 holds the root's, and level >= 1 here)
+    child_known(vind_.data() + left, idx, right - left, kn, kc[0], kc[1]);
+    const int c1 = divide(left, left + idx, lb, kc[0], level + 1, nodes, depth);
+    const int c2 = divide(left + idx, right, rb, kc[1], level + 1, nodes, depth);
     Node &n = nodes[me];
     n.leaf = false;
     n.left = left;

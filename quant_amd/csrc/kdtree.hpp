@@ -175,10 +175,18 @@ private:
     // those reads in cache (row-major, every read of a 48-D codebook was a cache miss)
     double pt(size_t i, int d) const { return cols_[(size_t)d * K_ + i]; }
     double ptr(size_t i, int d) const { return pts_[i * (size_t)dim_ + d]; }   // row-major
-    // bbox: the node's cell box (dim entries); children's boxes live in boxes_ at their level
-    int divide(size_t left, size_t right, Box *bbox, int level, RecycledVec<Node> &nodes, int &depth);
+    // The exact point min / max of a node's points in the dimensions of mask (the rest unknown).
+    struct Known {
+        Box b[64];
+        uint64_t mask;
+    };
+    // bbox: the node's cell box (dim entries); children's boxes live in boxes_ at their level.
+    // kn: what is known of the node's point extremes (middle_split adds what it computes).
+    int divide(size_t left, size_t right, Box *bbox, Known &kn, int level, RecycledVec<Node> &nodes, int &depth);
     void middle_split(size_t *ind, size_t count, size_t &index, int &cutfeat, double &cutval, const Box *bbox,
-                      Node *info);
+                      Known &kn, Node *info);
+    void child_known(const size_t *ind, size_t n1, size_t count, const Known &kn, Known &k1, Known &k2) const;
+    static Known *level_known(int level);   // two per tree level
     void plane_split(size_t *ind, size_t count, int cutfeat, double cutval, size_t &lim1, size_t &lim2);
     void min_max(const size_t *ind, size_t count, int e, double &mn, double &mx) const;
     const double *pts_;

@@ -11,6 +11,8 @@
 #   host:CASE           QVQ_HOST_TRACE=1 host timeline of CASE -> host_CASE.log
 #   sq:CASE:KIND        SQ counters of CASE's searches (tools/gpu_pmc_sq.sh)
 #   py:SCRIPT[:ARGS]    python3 SCRIPT ARGS (commas for spaces), log to py_N.log
+#   libab:N             N interleaved bench runs (C3 20 steps, C4 10) of quant_amd/lib_base/libqvq.so
+#                       (the build before a change) and quant_amd/lib -> base_I.json / new_I.json
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 TAG=$1; shift
@@ -63,6 +65,18 @@ print('${name}_$i', 'C3', d['ms_per_step'], 'search us', {k: round(p[k]['avg_lau
     s=${arg%%:*}; a=${arg#*:}; [ "$a" = "$arg" ] && a=""
     (cd $R && timeout -k 10 400 python3 -u $s ${a//,/ } > $O/py_$n.log 2>&1) || { tail -20 $O/py_$n.log; exit 1; }
     tail -20 $O/py_$n.log ;;
+  libab)
+    B="--steps 20 --warmup 3 --c4-steps 10 --c5-steps 0 --e2e-reps 0 --share-steps 0 --exact-reps 0 --no-cpu-baseline"
+    for i in $(seq 1 ${arg:-4}); do
+      (cd $R && QVQ_LIB=$R/quant_amd/lib_base/libqvq.so timeout -k 10 300 python3 bench.py $B > $O/base_$i.json 2> $O/base_$i.err) || { tail -5 $O/base_$i.err; exit 1; }
+      (cd $R && timeout -k 10 300 python3 bench.py $B > $O/new_$i.json 2> $O/new_$i.err) || { tail -5 $O/new_$i.err; exit 1; }
+    done
+    (cd $R && python3 -c "
+import json, sys
+for k in ('base', 'new'):
+    r = [json.load(open('$O/%s_%d.json' % (k, i))) for i in range(1, ${arg:-4} + 1)]
+    print(k, 'C3 ms', ' / '.join('%.4f' % x['ms_per_step'] for x in r), '| C4 ms', ' / '.join('%.3f' % x['c4']['ms_per_step'] for x in r))
+" | tee $O/libab.txt) ;;
   *) echo "unknown step $step"; exit 2 ;;
   esac
 done
