@@ -12,7 +12,7 @@
 #   sq:CASE:KIND        SQ counters of CASE's searches (tools/gpu_pmc_sq.sh)
 #   py:SCRIPT[:ARGS]    python3 SCRIPT ARGS (commas for spaces), log to py_N.log
 #   libab:N             N interleaved bench runs (C3 20 steps, C4 10) of quant_amd/lib_base/libqvq.so
-#                       (the build before a change) and quant_amd/lib -> base_I.json / new_I.json
+#                       (the build before a change) and quant_amd/lib, in ABBA order -> base_I.json / new_I.json
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 TAG=$1; shift
@@ -67,9 +67,11 @@ print('${name}_$i', 'C3', d['ms_per_step'], 'search us', {k: round(p[k]['avg_lau
     tail -20 $O/py_$n.log ;;
   libab)
     B="--steps 20 --warmup 3 --c4-steps 10 --c5-steps 0 --e2e-reps 0 --share-steps 0 --exact-reps 0 --no-cpu-baseline"
-    for i in $(seq 1 ${arg:-4}); do
-      (cd $R && QVQ_LIB=$R/quant_amd/lib_base/libqvq.so timeout -k 10 300 python3 bench.py $B > $O/base_$i.json 2> $O/base_$i.err) || { tail -5 $O/base_$i.err; exit 1; }
-      (cd $R && timeout -k 10 300 python3 bench.py $B > $O/new_$i.json 2> $O/new_$i.err) || { tail -5 $O/new_$i.err; exit 1; }
+    for i in $(seq 1 ${arg:-4}); do   # (order alternating, ABBA: a drift over the call cancels)
+      for k in $( [ $((i % 2)) = 1 ] && echo "base new" || echo "new base" ); do
+        L=""; [ $k = base ] && L=$R/quant_amd/lib_base/libqvq.so
+        (cd $R && QVQ_LIB=$L timeout -k 10 300 python3 bench.py $B > $O/${k}_$i.json 2> $O/${k}_$i.err) || { tail -5 $O/${k}_$i.err; exit 1; }
+      done
     done
     (cd $R && python3 -c "
 import json, sys

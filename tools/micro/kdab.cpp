@@ -1,20 +1,22 @@
-// One kdtree.cpp build on the C4 level codebooks (data/b4_L12.f64, b4_L11.f64): median build
-// time warm (back to back, 31 builds) and cold (a 256 MB sweep before each, 15 builds).
+// One kdtree.cpp build on level codebooks (data/b4_L12.f64, b4_L11.f64: C4, D = 48;
+// b2_L10.f64: D = 12): median build time warm (back to back, 31 builds) and cold (a 256 MB
+// sweep before each, 15 builds).
 #include "kdtree.hpp"
 #include <algorithm>
 #include <chrono>
 #include <cstdio>
+#include <string>
 #include <vector>
 int main() {
     std::vector<char> sweep(256u << 20, 1);
-    for (const char *f : {"tools/micro/data/b4_L12.f64", "tools/micro/data/b4_L11.f64"}) {
+    for (const char *f : {"tools/micro/data/b4_L12.f64", "tools/micro/data/b4_L11.f64", "tools/micro/data/b2_L10.f64"}) {
         std::vector<double> p;
         FILE *i = std::fopen(f, "rb");
         if (!i) return 1;
         double v;
         while (std::fread(&v, 8, 1, i) == 1) p.push_back(v);
         std::fclose(i);
-        const int D = 48, K = (int)(p.size() / D);
+        const int D = std::string(f).find("b2_") != std::string::npos ? 12 : 48, K = (int)(p.size() / D);
         for (int cold = 0; cold < 2; cold++) {
             std::vector<double> t;
             for (int r = 0; r < (cold ? 15 : 31); r++) {
@@ -27,7 +29,7 @@ int main() {
                 t.push_back(std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
             }
             std::sort(t.begin(), t.end());
-            std::printf("K %d %s: median %.3f ms min %.3f\n", K, cold ? "cold" : "warm", t[t.size() / 2], t[0]);
+            std::printf("D %d K %d %s: median %.3f ms min %.3f\n", D, K, cold ? "cold" : "warm", t[t.size() / 2], t[0]);
         }
     }
 }
