@@ -17,7 +17,8 @@
 namespace qvq {
 
 namespace {
-// The pool behind Recycled<T>: at most 8 buffers per type, the smallest that fits is taken.
+// The pool behind Recycled<T>: at most 8 buffers per type (the largest kept), the smallest that
+// fits and is at most 4x the request is taken.
 template <class T>
 struct BufPool {
     std::mutex m;
@@ -45,8 +46,12 @@ void Recycled<T>::resize(size_t n) {
     {
         std::lock_guard<std::mutex> g(P.m);
         size_t best = P.free.size();
+        // (not one of more than 4x the request: small trees took the big levels' buffers, and
+        // the big levels then wrote fresh pages every call -- C4 level 12 ~0.5 ms)
         for (size_t i = 0; i < P.free.size(); i++)
-            if (P.free[i].first >= n && (best == P.free.size() || P.free[i].first < P.free[best].first)) best = i;
+            if (P.free[i].first >= n && P.free[i].first <= 4 * n + 4096 &&
+                (best == P.free.size() || P.free[i].first < P.free[best].first))
+                best = i;
         if (best < P.free.size()) {
             cap_ = P.free[best].first;
             p_ = std::move(P.free[best].second);
