@@ -18,7 +18,7 @@ namespace qvq {
 
 namespace {
 // The pool behind Recycled<T>: at most 8 buffers per type (the largest kept), the smallest that
-// fits and is at most 4x the request is taken.
+// fits and is at most 1.5x the request is taken.
 template <class T>
 struct BufPool {
     std::mutex m;
@@ -46,10 +46,11 @@ void Recycled<T>::resize(size_t n) {
     {
         std::lock_guard<std::mutex> g(P.m);
         size_t best = P.free.size();
-        // (not one of more than 4x the request: small trees took the big levels' buffers, and
-        // the big levels then wrote fresh pages every call -- C4 level 12 ~0.5 ms)
+        // (not one of more than 1.5x the request: the levels' sizes double, and a level that
+        // took the next one's buffer left the largest level to write fresh pages -- C4 level
+        // 12 ~0.5 ms a call)
         for (size_t i = 0; i < P.free.size(); i++)
-            if (P.free[i].first >= n && P.free[i].first <= 4 * n + 4096 &&
+            if (P.free[i].first >= n && P.free[i].first <= n + n / 2 + 1024 &&
                 (best == P.free.size() || P.free[i].first < P.free[best].first))
                 best = i;
         if (best < P.free.size()) {
