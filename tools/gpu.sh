@@ -11,6 +11,7 @@
 #   host:CASE           QVQ_HOST_TRACE=1 host timeline of CASE -> host_CASE.log
 #   sq:CASE:KIND        SQ counters of CASE's searches (tools/gpu_pmc_sq.sh)
 #   py:SCRIPT[:ARGS]    python3 SCRIPT ARGS (commas for spaces), log to py_N.log
+#   callab:N            N ABBA pairs of tools/c4_calls.py (40 C4 calls each) with lib_base and lib -> callab.txt
 #   libab:N             N interleaved bench runs (C3 20 steps, C4 10) of quant_amd/lib_base/libqvq.so
 #                       (the build before a change) and quant_amd/lib, in ABBA order -> base_I.json / new_I.json
 set -o pipefail
@@ -65,6 +66,15 @@ print('${name}_$i', 'C3', d['ms_per_step'], 'search us', {k: round(p[k]['avg_lau
     s=${arg%%:*}; a=${arg#*:}; [ "$a" = "$arg" ] && a=""
     (cd $R && timeout -k 10 400 python3 -u $s ${a//,/ } > $O/py_$n.log 2>&1) || { tail -20 $O/py_$n.log; exit 1; }
     tail -20 $O/py_$n.log ;;
+  callab)
+    for i in $(seq 1 ${arg:-3}); do
+      for k in $( [ $((i % 2)) = 1 ] && echo "base new new base" || echo "new base base new" ); do
+        L=""; [ $k = base ] && L=$R/quant_amd/lib_base/libqvq.so
+        echo -n "$k " >> $O/callab.txt
+        (cd $R && QVQ_LIB=$L timeout -k 10 200 python3 tools/c4_calls.py 4096,4,12 40 >> $O/callab.txt 2> $O/callab.err) || { tail -5 $O/callab.err; exit 1; }
+      done
+    done
+    cat $O/callab.txt ;;
   libab)
     B="--steps 20 --warmup 3 --c4-steps 10 --c5-steps 0 --e2e-reps 0 --share-steps 0 --exact-reps 0 --no-cpu-baseline"
     for i in $(seq 1 ${arg:-4}); do   # (order alternating, ABBA: a drift over the call cancels)
