@@ -152,6 +152,50 @@ __attribute__((target_clones("avx2", "default"))) void rows_min_max(const double
 }
 }  // namespace
 
+namespace {
+bool has_avx2() {
+    static const bool v = __builtin_cpu_supports("avx2");
+    return v;
+}
+// cols[d][k] = pts[k][d]: 4 x 4 blocks through registers (4 rows' loads, 4 columns' stores),
+// the points 64 at a time (their rows stay in L1 while every column takes its 64 values)
+__attribute__((target("avx2"))) void transpose_rows_avx2(const double *pts, size_t K, int dim, double *cols) {
+    const size_t K4 = K & ~(size_t)3;
+    const int d4 = dim & ~3;
+    for (size_t k0 = 0; k0 < K4; k0 += 64) {
+        const size_t k1 = std::min(K4, k0 + 64);
+        for (int d = 0; d < d4; d += 4)
+            for (size_t k = k0; k < k1; k += 4) {
+                const double *p = pts + k * (size_t)dim + d;
+                const __m256d r0 = _mm256_loadu_pd(p), r1 = _mm256_loadu_pd(p + dim), r2 = _mm256_loadu_pd(p + 2 * dim),
+                              r3 = _mm256_loadu_pd(p + 3 * dim);
+                const __m256d t0 = _mm256_unpacklo_pd(r0, r1), t1 = _mm256_unpackhi_pd(r0, r1),
+                              t2 = _mm256_unpacklo_pd(r2, r3), t3 = _mm256_unpackhi_pd(r2, r3);
+                double *c = cols + (size_t)d * K + k;
+                _mm256_storeu_pd(c, _mm256_permute2f128_pd(t0, t2, 0x20));
+                _mm256_storeu_pd(c + K, _mm256_permute2f128_pd(t1, t3, 0x20));
+                _mm256_storeu_pd(c + 2 * K, _mm256_permute2f128_pd(t0, t2, 0x31));
+                _mm256_storeu_pd(c + 3 * K, _mm256_permute2f128_pd(t1, t3, 0x31));
+            }
+    }
+    for (int d = 0; d < dim; d++)   // the ragged edges
+        for (size_t k = d < d4 ? K4 : 0; k < K; k++) cols[(size_t)d * K + k] = pts[k * (size_t)dim + d];
+}
+void transpose_rows(const double *pts, size_t K, int dim, double *cols) {
+    if (has_avx2()) {
+        transpose_rows_avx2(pts, K, dim, cols);
+        return;
+    }
+    for (size_t k0 = 0; k0 < K; k0 += 64) {
+        const size_t k1 = std::min(K, k0 + 64);
+        for (int d = 0; d < dim; d++) {
+            double *col = cols + (size_t)d * K;
+            for (size_t k = k0; k < k1; k++) col[k] = pts[k * (size_t)dim + d];
+        }
+    }
+}
+}  // namespace
+
 RefKDTree::RefKDTree(const double *pts, size_t K, int dim, const std::atomic<bool> *cancel)
     : pts_(pts), dim_(dim), K_(K), cancel_(cancel) {
     static std::atomic<uint64_t> next_id{1};
@@ -171,13 +215,7 @@ RefKDTree::RefKDTree(const double *pts, size_t K, int dim, const std::atomic<boo
         rows_min_max(pts, vind_.data(), K, dim, mn, mx);
         for (int d = 0; d < dim; d++) root_bbox_[d] = Box{mn[d], mx[d]};
     }
-    for (size_t k0 = 0; k0 < K; k0 += 64) {
-        const size_t k1 = std::min(K, k0 + 64);
-        for (int d = 0; d < dim; d++) {
-            double *col = cbuf + (size_t)d * K;
-            for (size_t k = k0; k < k1; k++) col[k] = pts[k * (size_t)dim + d];
-        }
-    }
+    transpose_rows(pts, K, dim, cbuf);
     // every node's record and box in one pooled buffer each (a tree of K points has fewer than
     // 2K + 1 nodes unless empty leaves pile up; push_back grows then)
     nodes_.reserve(2 * K + 1);
@@ -899,10 +937,6 @@ void RefKDTree::cert_reset(double delta, const double *kpts, const uint8_t *know
 // below are plain element-wise min / max (vectorised; a branch per value mispredicted on the
 // irregular known pattern).
 namespace {
-bool has_avx2() {
-    static const bool v = __builtin_cpu_supports("avx2");
-    return v;
-}
 // One leaf point's row into a node's aggregates, four dimensions at a time (blends on the
 // known mask, then min / max; the values are finite, so min_pd / max_pd are exact): returns the
 // first dimension left to the scalar loop.
