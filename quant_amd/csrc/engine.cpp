@@ -128,7 +128,9 @@ struct HostTrace {
     std::string finish() {
         std::lock_guard<std::mutex> g(m);
         on.store(false, std::memory_order_release);
-        std::string out = "qvq host trace:";
+        // (t0 in steady_clock ns -- CLOCK_MONOTONIC, the clock of rocprofv3's timestamps)
+        std::string out = "qvq host trace: t0_ns " +
+                          std::to_string(std::chrono::duration_cast<std::chrono::nanoseconds>(t0.time_since_epoch()).count());
         for (const auto &e : ev) out += "\n  " + std::to_string((int)e.first) + " " + e.second;
         return out;
     }
@@ -1055,7 +1057,7 @@ void post_job(qvq_ctx *ctx, std::function<void()> job, qvq_ctx::Worker *wk = nul
             std::unique_lock<std::mutex> lk(w.m);
             for (;;) {
                 w.cv.wait(lk, [&w] { return w.stop || !w.q.empty(); });
-                if (w.stop) return;
+                if (w.stop && w.q.empty()) return;   // (queued frees still run)
                 std::function<void()> job = std::move(w.q.front());
                 w.q.pop_front();
                 lk.unlock();
@@ -1902,7 +1904,11 @@ void verify_level(qvq_ctx *ctx, qvq_ctx::Verify &v) {
 
 // The check's verdict (status 0 / 1 / 2, -1: none posted); its tree and rows are released,
 // except a deferred check's (status 2, several ranks), which moves to ctx->deferred.
-int join_verify(qvq_ctx *ctx, qvq_ctx::Verify &v) {
+
+// free_on_worker: the check's tree and state are destroyed on the worker, not here (the last
+// level's at the end of a call: C4's K = 4096 tree and certificate free ~30 us of buffers, with
+// the munmaps' TLB shootdowns, while the caller waits)
+int join_verify(qvq_ctx *ctx, qvq_ctx::Verify &v, bool free_on_worker = false) {
     if (!v.posted) return -1;
     while (!v.done.load(std::memory_order_acquire)) std::this_thread::yield();
     v.posted = false;
@@ -1917,6 +1923,14 @@ int join_verify(qvq_ctx *ctx, qvq_ctx::Verify &v) {
         d.cs = std::move(v.cs);
         ctx->deferred.push_back(std::move(d));
     }
+    if (free_on_worker && v.tree) {
+        RefKDTree *t = v.tree.release();
+        CertState *c = new CertState(std::move(v.cs));
+        post_job(ctx, [t, c] {
+            delete t;
+            delete c;
+        }, nullptr);
+    }
     v.tree.reset();
     v.cs = CertState();
     return status;
@@ -1925,7 +1939,7 @@ int join_verify(qvq_ctx *ctx, qvq_ctx::Verify &v) {
 // join_verify within the context's wait bounds: a failed stream or communicator, or a timeout,
 // fails the call as any other wait does (wait_failed; a drained stream is no failure here: the
 // check's host replays may outlast the GPU's work).  ok = not failed (status 0, 2 or none).
-qvq_status join_verify_bounded(qvq_ctx *ctx, qvq_ctx::Verify &v, bool &ok) {
+qvq_status join_verify_bounded(qvq_ctx *ctx, qvq_ctx::Verify &v, bool &ok, bool free_on_worker = false) {
     ok = true;
     if (!v.posted) return QVQ_OK;
     std::string err;
@@ -1940,7 +1954,7 @@ qvq_status join_verify_bounded(qvq_ctx *ctx, qvq_ctx::Verify &v, bool &ok) {
         for (auto &u : ctx->ver) u.cancel.store(true);
         return wait_failed(ctx, fail(ctx, st, err));
     }
-    ok = join_verify(ctx, v) != 1;
+    ok = join_verify(ctx, v, free_on_worker) != 1;
     return QVQ_OK;
 }
 
@@ -2690,8 +2704,26 @@ QVQ_API qvq_status qvq_lbg(qvq_ctx *ctx, uint32_t bits, double eps, double *code
         out_enqueued = true;
         return QVQ_OK;
     };
+    // the published results out of the mapped buffers: distortion inputs, per-level counters,
+    // the codebook (C4: 1.5 MB, ~60 us)
+    double dres[3];
+    unsigned stats[2 * 33];
+    bool results_copied = false;
+    auto copy_results = [&]() -> qvq_status {
+        uint8_t *h_small = reinterpret_cast<uint8_t *>(ctx->h_ready) + 64;
+        const uint64_t cb_bytes = codebook ? (uint64_t)Kmax * ctx->D * 8 : 0;
+        qvq_status ws = wait_flag(ctx, reinterpret_cast<volatile uint64_t *>(h_small + (1024 - 64 - 8)), out_seq);
+        if (ws != QVQ_OK) return ws;
+        std::memcpy(dres, h_small, sizeof(dres));
+        std::memcpy(stats, h_small + sizeof(dres), sizeof(stats));
+        if (codebook) std::memcpy(codebook, ctx->h_cb, cb_bytes);
+        results_copied = true;
+        ctx->htrace.mark("results copied");
+        return QVQ_OK;
+    };
     for (;;) {   // once, or twice when a speculative check fails
     out_enqueued = false;
+    results_copied = false;
     const bool tmean = ctx->timing_level == -3;   // events around the mean kernel (qvq_set_timing)
     if (tmean) HIPCHK(hipEventRecord(ctx->ev[31][0], ctx->stream));
     HIPCHK(launch_mean_sums(ctx->stream, ctx->Dp, ctx->d_codes, ctx->N, ctx->D, ctx->d_plut, ctx->d_mean,
@@ -2867,8 +2899,11 @@ QVQ_API qvq_status qvq_lbg(qvq_ctx *ctx, uint32_t bits, double eps, double *code
         if ((st = enqueue_out()) != QVQ_OK) return st;
         ctx->htrace.mark("results' copy enqueued");
         for (uint32_t l = bits >= 3 ? bits - 2 : 1; l <= bits; l++) {
+            // one rank: the results leave the mapped buffers while the last check runs (a
+            // failed check redoes the quantize, and the copy with it)
+            if (l == bits && !multi && (st = copy_results()) != QVQ_OK) return st;
             bool ok;
-            if ((st = join_verify_bounded(ctx, ctx->ver[l % 3], ok)) != QVQ_OK) return st;
+            if ((st = join_verify_bounded(ctx, ctx->ver[l % 3], ok, true)) != QVQ_OK) return st;
             local_fail = local_fail || !ok;
         }
         ctx->htrace.mark("last checks joined");
@@ -2898,20 +2933,9 @@ QVQ_API qvq_status qvq_lbg(qvq_ctx *ctx, uint32_t bits, double eps, double *code
     // from the sums of the final assignment (finalize_prep_kernel without split).
     // (enqueue_out: before the last checks are joined when speculating)
     if (!out_enqueued && (st = enqueue_out()) != QVQ_OK) return st;
-    double dres[3];
-    unsigned stats[2 * 33];
-    {
-        uint8_t *h_small = reinterpret_cast<uint8_t *>(ctx->h_ready) + 64;
-        const uint64_t cb_bytes = codebook ? (uint64_t)Kmax * ctx->D * 8 : 0;
-        qvq_status ws = wait_flag(ctx, reinterpret_cast<volatile uint64_t *>(h_small + (1024 - 64 - 8)), out_seq);
-        if (ws != QVQ_OK) return ws;
-        ctx->htrace.mark("results copied");
-        if (assign)   // every collective of this call is complete: a plain copy
-            HIPCHK(host_copy(ctx, assign, ctx->d_A, ctx->N * 4, hipMemcpyDeviceToHost));
-        std::memcpy(dres, h_small, sizeof(dres));
-        std::memcpy(stats, h_small + sizeof(dres), sizeof(stats));
-        if (codebook) std::memcpy(codebook, ctx->h_cb, cb_bytes);
-    }
+    if (!results_copied && (st = copy_results()) != QVQ_OK) return st;
+    if (assign)   // every collective of this call is complete: a plain copy
+        HIPCHK(host_copy(ctx, assign, ctx->d_A, ctx->N * 4, hipMemcpyDeviceToHost));
     // closed form: sum ||x||^2 - sum_k (2 c_k.S_k - n_k ||c_k||^2) cancels to a few ulps of
     // sum ||x||^2 when the cells are (nearly) exact; a distortion is never negative
     if (distortion) *distortion = std::max(0.0, (dres[0] - dres[2]) / (dres[1] * (double)ctx->D));
