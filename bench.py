@@ -67,7 +67,7 @@ def parse():
     ap.add_argument("--cpu-reps", type=int, default=5)
     ap.add_argument("--c5-images", type=int, default=64)
     ap.add_argument("--c5-steps", type=int, default=3, help="0 disables the c5 sub-object")
-    ap.add_argument("--c4-steps", type=int, default=5, help="0 disables the c4 sub-object")
+    ap.add_argument("--c4-steps", type=int, default=20, help="0 disables the c4 sub-object")
     ap.add_argument("--share-steps", type=int, default=3,
                     help="0 disables the c5_rank_share sub-object (N=8 per-rank share through a 1-rank RCCL communicator)")
     ap.add_argument("--e2e-reps", type=int, default=7, help="0 disables the end_to_end sub-object (the first rep after a reconfiguration is not timed; the second still pays first-use costs, hence the median of 7)")
@@ -464,10 +464,11 @@ def main():
         eng.set_synthetic(args.size, 0x5EED, 1, 4, 4, quant_amd.SCALED)
         eng.set_timing(-2)
         out4 = (np.empty((1 << 12, eng.dim), np.float64), np.zeros(1, np.float64))
-        el = timed(lambda: eng.lbg(12, want_assign=False, out=out4), args.c4_steps, 1)
+        # (3 warmups: the first C4 call sizes the context's and the trees' pooled buffers)
+        el = timed(lambda: eng.lbg(12, want_assign=False, out=out4), args.c4_steps, 3)
         result["c4"] = {"workload": "C4: %dx%d synthetic, 4x4 blocks (D=48), 4096 code vectors" % (args.size, args.size),
                         "value": round(eng.n * 12 * args.c4_steps / el / 1e6, 3), "unit": "Mblocks/s",
-                        "ms_per_step": round(el * 1e3 / args.c4_steps, 3), "steps": args.c4_steps, "warmup": 1}
+                        "ms_per_step": round(el * 1e3 / args.c4_steps, 3), "steps": args.c4_steps, "warmup": 3}
     if world == 1 and args.share_steps > 0:
         # one rank's share of C5 at N=8, under the communicator schedule (a 1-rank RCCL
         # communicator: the all-reduce per level, kd ties and reduce as with N ranks) and under
